@@ -1,0 +1,266 @@
+"""Generate the committed golden fixtures by running the REFERENCE implementation.
+
+Run in the build container only (it reads /root/reference, which does not exist on the
+GPU box):
+
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py
+
+The reference `src.models` is imported read-only with the four stubs of SURVEY.md §8(c)
+(none of them touches the arithmetic except the torch_sparse SpMM/degree stand-in, which
+implements the scatter-add semantics `lightgcn.py:103` intends and the duplicate-summing
+SpMM of torch_sparse):
+
+1. pytorch_lightning.LightningModule = nn.Module + save_hyperparameters() + no-op log()
+2. torchmetrics.Metric = nn.Module with add_state()
+3. torch_sparse.sum / torch_sparse.SparseTensor (scatter-add degree, index_add SpMM)
+4. src.evaluation.RecommendationMetrics (missing in the snapshot) = a placeholder class
+
+Weights come from `hnm_recommendation_amd.synthetic` (numpy PCG64 recipes) and are loaded
+into the reference modules via load_state_dict; outputs are stored as small .npz files
+(inputs + expected outputs only -- no reference source travels).
+"""
+from __future__ import annotations
+
+import inspect
+import os
+import sys
+import types
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+REF = "/root/reference"
+sys.path.insert(0, REPO)
+
+from hnm_recommendation_amd import synthetic as syn  # noqa: E402
+
+
+def install_stubs():
+    pl = types.ModuleType("pytorch_lightning")
+
+    class LightningModule(nn.Module):
+        def save_hyperparameters(self):
+            frame = inspect.currentframe().f_back
+            args = inspect.getargvalues(frame)
+            self.hparams = {k: args.locals[k] for k in args.args if k != "self"}
+
+        def log(self, *a, **k):
+            pass
+
+    pl.LightningModule = LightningModule
+    sys.modules["pytorch_lightning"] = pl
+
+    tm = types.ModuleType("torchmetrics")
+
+    class Metric(nn.Module):
+        def add_state(self, name, default, dist_reduce_fx=None):
+            setattr(self, name, default)
+
+    tm.Metric = Metric
+    sys.modules["torchmetrics"] = tm
+
+    ts = types.ModuleType("torch_sparse")
+
+    def ts_sum(src, index, dim=0, dim_size=None):
+        return torch.zeros(dim_size, dtype=src.dtype).index_add_(0, index.cpu(), src.cpu())
+
+    class SparseTensor:
+        def __init__(self, row, col, value, sparse_sizes):
+            self.row, self.col, self.value = row.cpu(), col.cpu(), value.cpu()
+            self.n = sparse_sizes[0]
+
+        def __matmul__(self, x):
+            out = torch.zeros(self.n, x.shape[1], dtype=x.dtype)
+            return out.index_add_(0, self.row, x[self.col] * self.value[:, None])
+
+    ts.sum = ts_sum
+    ts.SparseTensor = SparseTensor
+    sys.modules["torch_sparse"] = ts
+
+    sys.path.insert(0, REF)
+    import src.evaluation as ev  # noqa: E402
+
+    class RecommendationMetrics:
+        def __init__(self, top_k=12):
+            self.top_k = top_k
+
+    ev.RecommendationMetrics = RecommendationMetrics
+    import src.models as models  # noqa: E402
+    return models
+
+
+def load(model, sd):
+    model.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in sd.items()})
+    model.eval()
+    return model
+
+
+def filter_csr(user_ids, fdict):
+    ptr = [0]
+    idx = []
+    for u in user_ids.tolist():
+        items = sorted(fdict.get(int(u), ()))
+        idx.extend(items)
+        ptr.append(len(idx))
+    return np.asarray(ptr, np.int64), np.asarray(idx, np.int64)
+
+
+def dict_to_arrays(fdict):
+    keys = np.asarray(sorted(fdict), np.int64)
+    ptr, idx = [0], []
+    for k in keys.tolist():
+        idx.extend(sorted(fdict[k]))
+        ptr.append(len(idx))
+    return keys, np.asarray(ptr, np.int64), np.asarray(idx, np.int64)
+
+
+def tagged_users(U, B, seed):
+    ids = syn.user_batch(U, B - 4, seed=seed)
+    # duplicates, id 0 and id U-1
+    return np.concatenate([ids, [0, U - 1, ids[0], ids[1]]]).astype(np.int64)
+
+
+def save(name, **arrs):
+    path = os.path.join(HERE, name)
+    np.savez_compressed(path, **arrs)
+    print(f"wrote {path} ({os.path.getsize(path) / 1024:.0f} KiB)")
+
+
+def with_prefix(prefix, sd):
+    return {prefix + k: np.asarray(v) for k, v in sd.items()}
+
+
+def gen_ncf(models):
+    U, I, B, K = 600, 400, 64, 12
+    sd = syn.ncf_state_dict(U, I, 64, (128, 64, 32), seed=0, bias_scale=0.05, emb_scale=20.0)
+    m = load(models.NeuralCF(num_users=U, num_items=I, mf_dim=64, mlp_dims=[128, 64, 32], top_k=K), sd)
+    users = tagged_users(U, B, seed=1)
+    fdict = syn.filter_dict(users, I, per_user=23, seed=3)
+    with torch.no_grad():
+        ut = torch.from_numpy(users)
+        dense = m.predict_all_items(ut).numpy()
+        rec = m.recommend(ut).numpy()
+        rec_f = m.recommend(ut, filter_items=fdict).numpy()
+        pu = torch.from_numpy(syn.user_batch(U, 50, seed=5))
+        pi = torch.from_numpy(syn.user_batch(I, 50, seed=6))
+        pair = m(pu, pi).numpy()
+    fk, fp, fi = dict_to_arrays(fdict)
+    save("ncf_small.npz", U=U, I=I, K=K, mf_dim=64, mlp_dims=np.array([128, 64, 32]),
+         user_ids=users, dense=dense, topk=rec, topk_filtered=rec_f,
+         filter_keys=fk, filter_ptr=fp, filter_idx=fi,
+         pair_users=pu.numpy(), pair_items=pi.numpy(), pair_scores=pair,
+         **with_prefix("sd/", sd))
+
+    # BASELINE.json configs[0]: NCF dim=64 on the 10k-user/5k-item subset (weights from the
+    # recipe, regenerated by the tests -- only the seed + expected outputs are stored).
+    U1, I1 = 10_000, 5_000
+    sd1 = syn.ncf_state_dict(U1, I1, 64, (128, 64, 32), seed=0)
+    m1 = load(models.NeuralCF(num_users=U1, num_items=I1), sd1)
+    users1 = syn.user_batch(U1, 256, seed=1)
+    with torch.no_grad():
+        d1 = m1.predict_all_items(torch.from_numpy(users1)).numpy()
+        r1 = m1.recommend(torch.from_numpy(users1)).numpy()
+    top_vals = np.take_along_axis(d1, r1, axis=1)
+    save("ncf_config1.npz", U=U1, I=I1, K=12, seed=0, user_ids=users1, topk=r1,
+         topk_scores=top_vals, row_sums=d1.astype(np.float64).sum(1),
+         kth_gap=np.sort(d1, 1)[:, -12] - np.sort(d1, 1)[:, -13])
+
+
+def gen_lightgcn(models):
+    U, I, E, K = 600, 400, 4000, 12
+    for d, alpha, weighted in ((64, None, False), (128, None, False), (64, 0.5, True)):
+        sd = syn.lightgcn_state_dict(U, I, d, seed=0, emb_scale=10.0)
+        m = load(models.LightGCN(num_users=U, num_items=I, embedding_dim=d, num_layers=3,
+                                 top_k=K, alpha=alpha), sd)
+        # E interactions with duplicate edges (Zipf items make repeats certain)
+        ei = syn.bipartite_edge_index(U, I, E, seed=2)
+        ew = None
+        if weighted:
+            ew = np.random.Generator(np.random.PCG64(7)).uniform(0.5, 2.0, ei.shape[1]).astype(np.float32)
+        m.set_graph(torch.from_numpy(ei), None if ew is None else torch.from_numpy(ew))
+        users = tagged_users(U, 64, seed=1)
+        fdict = syn.filter_dict(users, I, per_user=23, seed=3)
+        with torch.no_grad():
+            fu, fi = m.forward()
+            ut = torch.from_numpy(users)
+            dense = m.predict_all_items(ut).numpy()
+            rec = m.recommend(ut).numpy()
+            rec_f = m.recommend(ut, filter_items=fdict).numpy()
+        fk, fp, fx = dict_to_arrays(fdict)
+        extra = {} if ew is None else {"edge_weight": ew}
+        tag = f"d{d}" + ("_alpha" if alpha is not None else "")
+        save(f"lightgcn_{tag}.npz", U=U, I=I, K=K, d=d, L=3,
+             alpha=np.float64(-1.0 if alpha is None else alpha),
+             alphas=np.asarray(m.alpha, np.float64),
+             edge_index=ei, user_ids=users, F_U=fu.numpy(), F_I=fi.numpy(), dense=dense,
+             topk=rec, topk_filtered=rec_f, filter_keys=fk, filter_ptr=fp, filter_idx=fx,
+             **extra, **with_prefix("sd/", sd))
+
+
+def gen_widedeep(models):
+    U, I, K = 300, 200, 12
+    sd = syn.widedeep_state_dict(U, I, 64, (512, 256, 128), seed=0, bias_scale=0.05,
+                                 randomize_bn=True, emb_scale=10.0)
+    m = load(models.WideDeep(num_users=U, num_items=I, embedding_dim=64,
+                             deep_layers=[512, 256, 128], top_k=K), sd)
+    users = tagged_users(U, 32, seed=1)
+    fdict = syn.filter_dict(users, I, per_user=23, seed=3)
+    with torch.no_grad():
+        ut = torch.from_numpy(users)
+        dense = m.predict_all_items(ut).numpy()
+        rec = m.recommend(ut).numpy()
+        rec_f = m.recommend(ut, filter_items=fdict).numpy()
+        pu = torch.from_numpy(syn.user_batch(U, 40, seed=5))
+        pi = torch.from_numpy(syn.user_batch(I, 40, seed=6))
+        pair = m(pu, pi).numpy()
+    fk, fp, fx = dict_to_arrays(fdict)
+    save("widedeep_small.npz", U=U, I=I, K=K, d=64, deep_layers=np.array([512, 256, 128]),
+         user_ids=users, dense=dense, topk=rec, topk_filtered=rec_f,
+         filter_keys=fk, filter_ptr=fp, filter_idx=fx,
+         pair_users=pu.numpy(), pair_items=pi.numpy(), pair_scores=pair,
+         **with_prefix("sd/", sd))
+
+    # user side features (num_item_features must be 0 for predict_all_items: wide_deep.py:275)
+    F = 10
+    sdf = syn.widedeep_state_dict(U, I, 16, (64, 32), num_user_features=F, seed=4,
+                                  bias_scale=0.05, randomize_bn=True, emb_scale=10.0)
+    mf = load(models.WideDeep(num_users=U, num_items=I, num_user_features=F, embedding_dim=16,
+                              deep_layers=[64, 32], top_k=5), sdf)
+    users = syn.user_batch(U, 16, seed=8)
+    feats = np.random.Generator(np.random.PCG64(9)).standard_normal((16, F)).astype(np.float32)
+    with torch.no_grad():
+        dense = mf.predict_all_items(torch.from_numpy(users), torch.from_numpy(feats)).numpy()
+        rec = mf.recommend(torch.from_numpy(users), torch.from_numpy(feats)).numpy()
+    save("widedeep_feat.npz", U=U, I=I, K=5, d=16, F=F, deep_layers=np.array([64, 32]),
+         user_ids=users, user_features=feats, dense=dense, topk=rec, **with_prefix("sd/", sdf))
+
+
+def gen_mf(models):
+    U, I, K = 500, 300, 12
+    sd = syn.mf_state_dict(U, I, 64, seed=0, bias_scale=0.05)
+    m = load(models.MatrixFactorization(num_users=U, num_items=I, embedding_dim=64, top_k=K,
+                                        sparse=False), sd)
+    users = tagged_users(U, 48, seed=1)
+    fdict = syn.filter_dict(users, I, per_user=23, seed=3)
+    with torch.no_grad():
+        ut = torch.from_numpy(users)
+        dense = m.predict_all_items(ut).numpy()
+        rec = m.recommend(ut).numpy()
+        rec_f = m.recommend(ut, filter_items=fdict).numpy()
+    fk, fp, fx = dict_to_arrays(fdict)
+    save("mf_small.npz", U=U, I=I, K=K, d=64, user_ids=users, dense=dense, topk=rec,
+         topk_filtered=rec_f, filter_keys=fk, filter_ptr=fp, filter_idx=fx,
+         **with_prefix("sd/", sd))
+
+
+if __name__ == "__main__":
+    torch.manual_seed(0)
+    torch.set_num_threads(8)
+    models = install_stubs()
+    gen_ncf(models)
+    gen_lightgcn(models)
+    gen_widedeep(models)
+    gen_mf(models)
