@@ -1,0 +1,161 @@
+"""ctypes binding of libhnm_mi355x.so (the C ABI in include/hnm.h).
+
+This is the ONLY route to compute: there is no CPU or eager-PyTorch fallback.  If the
+library is missing, or a tensor is not on an AMD GPU, every entry point raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import threading
+
+import torch
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(PKG, "libhnm_mi355x.so")
+
+HNM_OK, HNM_EINVAL, HNM_EOOB, HNM_EHIP, HNM_ENOMEM, HNM_EUNSUPPORTED = 0, -1, -2, -3, -4, -5
+
+_p = C.c_void_p
+_i64 = C.c_int64
+_i32 = C.c_int32
+_f32 = C.c_float
+
+
+class NcfWeights(C.Structure):
+    """hnm_ncf_weights (include/hnm.h)."""
+    _fields_ = [("gmf_user", _p), ("gmf_item", _p), ("mlp_user", _p), ("mlp_item", _p),
+                ("w1", _p), ("b1", _p), ("w2", _p), ("b2", _p), ("wp", _p), ("bp", _p),
+                ("num_users", _i64), ("num_items", _i64), ("mf", _i32), ("h0", _i32),
+                ("h1", _i32), ("h2", _i32)]
+
+
+class WideDeepWeights(C.Structure):
+    """hnm_widedeep_weights (include/hnm.h)."""
+    _fields_ = [("deep_user", _p), ("deep_item", _p), ("wide_user", _p), ("wide_item", _p),
+                ("w1", _p), ("b1", _p), ("w2", _p), ("b2", _p), ("w3", _p), ("b3", _p),
+                ("wd", _p), ("bias", _p),
+                ("num_users", _i64), ("num_items", _i64), ("ld_user", _i64),
+                ("d", _i32), ("l1", _i32), ("l2", _i32), ("l3", _i32)]
+
+
+_SIGS = {
+    "hnm_abi_version": (C.c_int, []),
+    "hnm_last_error": (C.c_char_p, []),
+    "hnm_ctx_create": (_i32, [C.c_int, C.POINTER(_p)]),
+    "hnm_ctx_destroy": (_i32, [_p]),
+    "hnm_ctx_set_stream": (_i32, [_p, _p]),
+    "hnm_ctx_reserve": (_i32, [_p, C.c_size_t]),
+    "hnm_ctx_check": (_i32, [_p]),
+    "hnm_ctx_num_cus": (_i32, [_p, C.POINTER(C.c_int)]),
+    "hnm_gather_rows_f32": (_i32, [_p, _p, _i64, _i64, C.c_int, _p, _i64, _p, _i64]),
+    "hnm_linear_rows_f32": (_i32, [_p, _p, _i64, _p, _i64, _i64, C.c_int, _p, _i64, _p,
+                                   C.c_int, _p, _i64, C.c_int]),
+    "hnm_dot_topk_f32": (_i32, [_p, _p, _i64, _i64, _p, _i64, _p, _i64, _i64, C.c_int, _p, _p,
+                                _p, _p, _p, C.c_int, _p, _p]),
+    "hnm_dot_scores_f32": (_i32, [_p, _p, _i64, _i64, _p, _i64, _p, _i64, _i64, C.c_int, _p,
+                                  _p, _p, _p, _i64]),
+    "hnm_pair_dot_f32": (_i32, [_p, _p, _i64, _i64, _p, _i64, _i64, C.c_int, _p, _p, _i64, _p,
+                                _p, _p, _p]),
+    "hnm_ncf_topk_f32": (_i32, [_p, C.POINTER(NcfWeights), _p, _i64, _p, _p, C.c_int, _p, _p]),
+    "hnm_ncf_scores_f32": (_i32, [_p, C.POINTER(NcfWeights), _p, _i64, _p, _i64]),
+    "hnm_ncf_pair_scores_f32": (_i32, [_p, C.POINTER(NcfWeights), _p, _p, _i64, _p]),
+    "hnm_topk_merge_f32": (_i32, [_p, _p, _p, _i64, _i64, _i64, _i64, C.c_int, C.c_int, _p, _p]),
+    "hnm_topk_rows_f32": (_i32, [_p, _p, _i64, _i64, _i64, _p, _p, C.c_int, _p, _p]),
+    "hnm_csr_build_norm": (_i32, [_p, _p, _p, _i64, _i64, _p, _p, _p]),
+    "hnm_spmm_plan_create": (_i32, [_p, _i64, _p, C.POINTER(_p)]),
+    "hnm_spmm_plan_destroy": (_i32, [_p]),
+    "hnm_spmm_csr_f32": (_i32, [_p, _p, _i64, _p, _p, _p, _p, C.c_int, _p, _f32, _p, _p]),
+    "hnm_axpby_f32": (_i32, [_p, _i64, _f32, _p, _f32, _p, _p]),
+    "hnm_widedeep_topk_f32": (_i32, [_p, C.POINTER(WideDeepWeights), _p, _i64, _p, _p, _p,
+                                     C.c_int, _p, _p]),
+    "hnm_widedeep_scores_f32": (_i32, [_p, C.POINTER(WideDeepWeights), _p, _i64, _p, _p,
+                                       _i64]),
+    "hnm_widedeep_pair_scores_f32": (_i32, [_p, C.POINTER(WideDeepWeights), _p, _p, _p, _i64,
+                                            _p]),
+}
+
+_lib = None
+_lock = threading.Lock()
+_ctxs: dict = {}
+
+
+def declared_symbols():
+    return sorted(_SIGS)
+
+
+def load(path: str = LIB_PATH):
+    """Load libhnm_mi355x.so (raises if it was not built -- no fallback)."""
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(path):
+            raise RuntimeError(
+                f"{path} is missing: the MI355X HIP library was not built "
+                "(run `python -m hnm_recommendation_amd.build`). There is no CPU fallback.")
+        lib = C.CDLL(path)
+        for name, (res, args) in _SIGS.items():
+            fn = getattr(lib, name, None)
+            if fn is None:
+                continue
+            fn.restype = res
+            fn.argtypes = args
+        if lib.hnm_abi_version() != 1:
+            raise RuntimeError("libhnm_mi355x ABI version mismatch")
+        _lib = lib
+        return lib
+
+
+def fn(name):
+    lib = load()
+    f = getattr(lib, name, None)
+    if f is None:
+        raise RuntimeError(f"{name} is not exported by {LIB_PATH}")
+    return f
+
+
+def check(status: int, what: str = ""):
+    if status == HNM_OK:
+        return
+    msg = load().hnm_last_error().decode(errors="replace")
+    if status == HNM_EOOB:
+        raise IndexError(msg)
+    if status in (HNM_EINVAL, HNM_EUNSUPPORTED):
+        raise ValueError(f"{what}: {msg}")
+    raise RuntimeError(f"{what}: {msg} (status {status})")
+
+
+def require_gpu(*tensors):
+    for t in tensors:
+        if t is None:
+            continue
+        if not (isinstance(t, torch.Tensor) and t.is_cuda):
+            raise RuntimeError(
+                "hnm_recommendation_amd runs on an AMD Instinct GPU (MI355X) through its HIP "
+                "library; move the module and its inputs to a GPU device (model.to('cuda')). "
+                "There is no CPU path.")
+
+
+def ctx(device: torch.device):
+    """Per-device hnm_ctx bound to torch's current stream on that device."""
+    dev = torch.device(device)
+    idx = dev.index if dev.index is not None else torch.cuda.current_device()
+    c = _ctxs.get(idx)
+    if c is None:
+        h = _p()
+        check(fn("hnm_ctx_create")(idx, C.byref(h)), "hnm_ctx_create")
+        c = h
+        _ctxs[idx] = c
+    stream = torch.cuda.current_stream(idx).cuda_stream
+    check(fn("hnm_ctx_set_stream")(c, _p(stream)), "hnm_ctx_set_stream")
+    return c
+
+
+def sync_check(device):
+    """Synchronize the ctx stream and raise IndexError if a kernel saw an out-of-range id."""
+    check(fn("hnm_ctx_check")(ctx(device)), "hnm_ctx_check")
+
+
+def ptr(t):
+    return None if t is None else _p(t.data_ptr())

@@ -1,0 +1,374 @@
+// libhnm_mi355x: context, errors, workspace, and the small memory-bound kernels
+// (row gather, layer-1 projection, axpby, top-K merge).
+#include <stdlib.h>
+#include <string.h>
+
+#include "hnm_device.h"
+#include "hnm_internal.h"
+
+static thread_local char g_err[512] = "";
+
+void hnm_set_error(const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+}
+
+extern "C" int hnm_abi_version(void) { return HNM_ABI_VERSION; }
+extern "C" const char* hnm_last_error(void) { return g_err; }
+
+extern "C" hnm_status hnm_ctx_create(int device, hnm_ctx** out) {
+  HNM_REQUIRE(out, HNM_EINVAL, "hnm_ctx_create: out is NULL");
+  HNM_HIP_CHECK(hipSetDevice(device));
+  hnm_ctx* c = (hnm_ctx*)calloc(1, sizeof(hnm_ctx));
+  HNM_REQUIRE(c, HNM_ENOMEM, "hnm_ctx_create: out of host memory");
+  c->device = device;
+  c->stream = 0;
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) == hipSuccess) c->num_cus = prop.multiProcessorCount;
+  if (c->num_cus <= 0) c->num_cus = 256;
+  if (hipMalloc((void**)&c->err_dev, sizeof(unsigned)) != hipSuccess) {
+    free(c);
+    hnm_set_error("hnm_ctx_create: hipMalloc of the error word failed");
+    return HNM_ENOMEM;
+  }
+  HNM_HIP_CHECK(hipMemset(c->err_dev, 0, sizeof(unsigned)));
+  *out = c;
+  return HNM_OK;
+}
+
+extern "C" hnm_status hnm_ctx_destroy(hnm_ctx* ctx) {
+  if (!ctx) return HNM_OK;
+  (void)hipSetDevice(ctx->device);
+  (void)hipDeviceSynchronize();
+  if (ctx->ws) (void)hipFree(ctx->ws);
+  if (ctx->err_dev) (void)hipFree(ctx->err_dev);
+  free(ctx);
+  return HNM_OK;
+}
+
+extern "C" hnm_status hnm_ctx_set_stream(hnm_ctx* ctx, void* s) {
+  HNM_REQUIRE(ctx, HNM_EINVAL, "ctx is NULL");
+  ctx->stream = (hipStream_t)s;
+  return HNM_OK;
+}
+
+extern "C" hnm_status hnm_ctx_num_cus(hnm_ctx* ctx, int* out) {
+  HNM_REQUIRE(ctx && out, HNM_EINVAL, "ctx/out is NULL");
+  *out = ctx->num_cus;
+  return HNM_OK;
+}
+
+hnm_status hnm_workspace(hnm_ctx* ctx, size_t bytes, void** out) {
+  bytes = hnm_align(bytes);
+  if (bytes > ctx->ws_size) {
+    HNM_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    if (ctx->ws) HNM_HIP_CHECK(hipFree(ctx->ws));
+    ctx->ws = nullptr;
+    ctx->ws_size = 0;
+    size_t want = hnm_align(bytes + bytes / 4);
+    if (hipMalloc(&ctx->ws, want) != hipSuccess) {
+      hnm_set_error("workspace: hipMalloc(%zu) failed", want);
+      return HNM_ENOMEM;
+    }
+    ctx->ws_size = want;
+  }
+  *out = ctx->ws;
+  return HNM_OK;
+}
+
+extern "C" hnm_status hnm_ctx_reserve(hnm_ctx* ctx, size_t bytes) {
+  HNM_REQUIRE(ctx, HNM_EINVAL, "ctx is NULL");
+  void* p;
+  return hnm_workspace(ctx, bytes, &p);
+}
+
+extern "C" hnm_status hnm_ctx_check(hnm_ctx* ctx) {
+  HNM_REQUIRE(ctx, HNM_EINVAL, "ctx is NULL");
+  unsigned h = 0;
+  HNM_HIP_CHECK(hipMemcpyAsync(&h, ctx->err_dev, sizeof(unsigned), hipMemcpyDeviceToHost,
+                               ctx->stream));
+  HNM_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+  if (h) {
+    HNM_HIP_CHECK(hipMemsetAsync(ctx->err_dev, 0, sizeof(unsigned), ctx->stream));
+    if (h & HNM_ERR_OOB) {
+      hnm_set_error("index out of range in self (an id exceeded the embedding table)");
+      return HNM_EOOB;
+    }
+  }
+  return HNM_OK;
+}
+
+// ------------------------------------------------------------------ a1 gather
+// One wave per output row; float4 lanes when rows are 16-B aligned.
+__global__ __launch_bounds__(256) void gather_rows_kernel(const float* __restrict__ tab,
+                                                          int64_t rows, int64_t ld, int d,
+                                                          const int64_t* __restrict__ ids,
+                                                          int64_t n, float* __restrict__ out,
+                                                          int64_t ldo, unsigned* err,
+                                                          bool vec4) {
+  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= n) return;
+  const int lane = threadIdx.x & 63;
+  const int64_t id = ids[r];
+  float* o = out + r * ldo;
+  if (id < 0 || id >= rows) {
+    if (lane == 0) hnm_flag(err, HNM_ERR_OOB);
+    for (int c = lane; c < d; c += 64) o[c] = __builtin_nanf("");
+    return;
+  }
+  const float* src = tab + id * ld;
+  if (vec4) {
+    for (int c = lane * 4; c < d; c += 256)
+      *reinterpret_cast<float4*>(o + c) = *reinterpret_cast<const float4*>(src + c);
+  } else {
+    for (int c = lane; c < d; c += 64) o[c] = src[c];
+  }
+}
+
+extern "C" hnm_status hnm_gather_rows_f32(hnm_ctx* ctx, const float* table, int64_t rows,
+                                          int64_t ld, int d, const int64_t* ids, int64_t n,
+                                          float* out, int64_t ldo) {
+  HNM_REQUIRE(ctx && table && ids && out, HNM_EINVAL, "gather: NULL argument");
+  HNM_REQUIRE(d > 0 && ld >= d && ldo >= d && rows > 0, HNM_EINVAL, "gather: bad shape");
+  if (n <= 0) return HNM_OK;
+  const bool vec4 = (d % 4 == 0) && (ld % 4 == 0) && (ldo % 4 == 0) &&
+                    ((uintptr_t)table % 16 == 0) && ((uintptr_t)out % 16 == 0);
+  hipLaunchKernelGGL(gather_rows_kernel, dim3((unsigned)hnm_cdiv(n, 4)), dim3(256), 0,
+                     ctx->stream, table, rows, ld, d, ids, n, out, ldo, ctx->err_dev, vec4);
+  HNM_LAUNCH_CHECK();
+  return HNM_OK;
+}
+
+// ------------------------------------------------------------------ projection
+// Y[r, c(n)] = sum_k X[x(r), k] W[n, k] (+ b[n]).  64 rows x 64 outputs per block, K in
+// chunks of 32 staged through LDS; each thread owns a 4 x 4 output patch.  fp32 FMA
+// chain in k order (a per-item / per-user precompute: <1 % of any scoring kernel).
+#define LIN_TM 64
+#define LIN_TN 64
+#define LIN_TK 32
+__global__ __launch_bounds__(256) void linear_rows_kernel(
+    const float* __restrict__ X, int64_t ldx, const int64_t* __restrict__ ids, int64_t x_rows,
+    int64_t M, int K, const float* __restrict__ W, int64_t ldw, const float* __restrict__ bias,
+    int N, float* __restrict__ Y, int64_t ldy, int pair_permute, unsigned* err) {
+  __shared__ float xs[LIN_TK][LIN_TM + 1];
+  __shared__ float ws[LIN_TK][LIN_TN + 1];
+  const int t = threadIdx.x;
+  const int64_t m0 = (int64_t)blockIdx.x * LIN_TM;
+  const int n0 = blockIdx.y * LIN_TN;
+  const int tr = (t >> 4) * 4;  // rows tr..tr+3
+  const int tc = (t & 15) * 4;  // cols tc..tc+3
+  float acc[4][4] = {};
+  // each thread loads 8 X elements and 8 W elements per K chunk
+  for (int k0 = 0; k0 < K; k0 += LIN_TK) {
+    for (int e = t; e < LIN_TM * LIN_TK; e += 256) {
+      const int rr = e / LIN_TK, kk = e % LIN_TK;
+      const int64_t m = m0 + rr;
+      float v = 0.f;
+      if (m < M && k0 + kk < K) {
+        int64_t src = ids ? ids[m] : m;
+        if (src < 0 || src >= x_rows) {
+          if (kk == 0) hnm_flag(err, HNM_ERR_OOB);
+          v = __builtin_nanf("");
+        } else {
+          v = X[src * ldx + k0 + kk];
+        }
+      }
+      xs[kk][rr] = v;
+    }
+    for (int e = t; e < LIN_TN * LIN_TK; e += 256) {
+      const int nn = e / LIN_TK, kk = e % LIN_TK;
+      float v = 0.f;
+      if (n0 + nn < N && k0 + kk < K) v = W[(int64_t)(n0 + nn) * ldw + k0 + kk];
+      ws[kk][nn] = v;
+    }
+    __syncthreads();
+    const int kmax = min(LIN_TK, K - k0);
+    for (int kk = 0; kk < kmax; ++kk) {
+      float xv[4], wv[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) xv[i] = xs[kk][tr + i];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) wv[j] = ws[kk][tc + j];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = fmaf(xv[i], wv[j], acc[i][j]);
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int64_t m = m0 + tr + i;
+    if (m >= M) continue;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int n = n0 + tc + j;
+      if (n >= N) continue;
+      float v = acc[i][j];
+      if (bias) v += bias[n];
+      const int64_t c = pair_permute ? (int64_t)(n & 1) * (ldy / 2) + (n >> 1) : n;
+      Y[m * ldy + c] = v;
+    }
+  }
+}
+
+extern "C" hnm_status hnm_linear_rows_f32(hnm_ctx* ctx, const float* X, int64_t ldx,
+                                          const int64_t* ids, int64_t x_rows, int64_t M, int K,
+                                          const float* W, int64_t ldw, const float* bias, int N,
+                                          float* Y, int64_t ldy, int pair_permute) {
+  HNM_REQUIRE(ctx && X && W && Y, HNM_EINVAL, "linear_rows: NULL argument");
+  HNM_REQUIRE(K > 0 && N > 0 && ldx >= K && ldw >= K && ldy >= N, HNM_EINVAL,
+              "linear_rows: bad shape");
+  HNM_REQUIRE(!pair_permute || (ldy % 2 == 0 && N <= ldy), HNM_EINVAL,
+              "linear_rows: pair_permute needs an even ldy");
+  if (M <= 0) return HNM_OK;
+  dim3 grid((unsigned)hnm_cdiv(M, LIN_TM), (unsigned)hnm_cdiv(N, LIN_TN));
+  hipLaunchKernelGGL(linear_rows_kernel, grid, dim3(256), 0, ctx->stream, X, ldx, ids,
+                     ids ? x_rows : M, M, K, W, ldw, bias, N, Y, ldy, pair_permute,
+                     ctx->err_dev);
+  HNM_LAUNCH_CHECK();
+  return HNM_OK;
+}
+
+// ------------------------------------------------------------------ axpby
+__global__ __launch_bounds__(256) void axpby_kernel(int64_t n, float a, const float* __restrict__ x,
+                                                    float b, const float* __restrict__ y,
+                                                    float* __restrict__ out) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * 256) {
+    float v = a * x[i];
+    if (y) v += b * y[i];
+    out[i] = v;
+  }
+}
+
+extern "C" hnm_status hnm_axpby_f32(hnm_ctx* ctx, int64_t n, float alpha, const float* x,
+                                    float beta, const float* y, float* out) {
+  HNM_REQUIRE(ctx && x && out, HNM_EINVAL, "axpby: NULL argument");
+  if (n <= 0) return HNM_OK;
+  const unsigned grid = (unsigned)std::min<int64_t>(hnm_cdiv(n, 256), 8 * 2048);
+  hipLaunchKernelGGL(axpby_kernel, dim3(grid), dim3(256), 0, ctx->stream, n, alpha, x, beta,
+                     y, out);
+  HNM_LAUNCH_CHECK();
+  return HNM_OK;
+}
+
+// ------------------------------------------------------------------ top-K merge
+// One wave per row: candidates stream through the wave list 64 at a time.
+template <int NS, typename IdxT>
+__global__ __launch_bounds__(256) void topk_merge_kernel(const float* __restrict__ cv,
+                                                         const IdxT* __restrict__ ci, int64_t B,
+                                                         int64_t G, int64_t gstride,
+                                                         int64_t bstride, int kc, int k,
+                                                         float* __restrict__ ov,
+                                                         int64_t* __restrict__ oi) {
+  const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (b >= B) return;
+  const int lane = threadIdx.x & 63;
+  WaveTopK<NS> L;
+  L.init();
+  const int64_t n = G * (int64_t)kc;
+  for (int64_t base = 0; base < n; base += 64) {
+    const int64_t j = base + lane;
+    float v = -__builtin_inff();
+    int idx = HNM_SENTINEL_IDX;
+    bool ok = false;
+    if (j < n) {
+      const int64_t g = j / kc, q = j % kc;
+      const int64_t off = g * gstride + b * bstride + q;
+      const IdxT ii = ci[off];
+      if (ii >= 0) {
+        v = cv[off];
+        idx = (int)ii;
+        ok = true;
+      }
+    }
+    L.offer(v, idx, ok, k);
+  }
+  L.store(ov ? ov + b * k : nullptr, oi + b * k, k);
+}
+
+template <typename IdxT>
+hnm_status launch_merge(hnm_ctx* ctx, const float* cv, const IdxT* ci, int64_t B, int64_t G,
+                        int64_t gstride, int64_t bstride, int kc, int k, float* ov,
+                        int64_t* oi) {
+  dim3 grid((unsigned)hnm_cdiv(B, 4));
+  if (k <= 64)
+    hipLaunchKernelGGL((topk_merge_kernel<1, IdxT>), grid, dim3(256), 0, ctx->stream, cv, ci,
+                       B, G, gstride, bstride, kc, k, ov, oi);
+  else
+    hipLaunchKernelGGL((topk_merge_kernel<2, IdxT>), grid, dim3(256), 0, ctx->stream, cv, ci,
+                       B, G, gstride, bstride, kc, k, ov, oi);
+  HNM_LAUNCH_CHECK();
+  return HNM_OK;
+}
+
+hnm_status hnm_topk_merge_i32(hnm_ctx* ctx, const float* cv, const int32_t* ci, int64_t B,
+                              int64_t G, int64_t gstride, int64_t bstride, int kc, int k,
+                              float* ov, int64_t* oi) {
+  return launch_merge<int32_t>(ctx, cv, ci, B, G, gstride, bstride, kc, k, ov, oi);
+}
+
+extern "C" hnm_status hnm_topk_merge_f32(hnm_ctx* ctx, const float* cand_val,
+                                         const int64_t* cand_idx, int64_t B, int64_t G,
+                                         int64_t gstride, int64_t bstride, int kc, int k,
+                                         float* out_val, int64_t* out_idx) {
+  HNM_REQUIRE(ctx && cand_val && cand_idx && out_idx, HNM_EINVAL, "merge: NULL argument");
+  HNM_REQUIRE(k >= 1 && k <= 128 && kc >= 1 && G >= 1, HNM_EINVAL, "merge: bad k/kc/G");
+  if (B <= 0) return HNM_OK;
+  return launch_merge<int64_t>(ctx, cand_val, cand_idx, B, G, gstride, bstride, kc, k,
+                               out_val, out_idx);
+}
+
+// ------------------------------------------------------------------ pairwise dot
+// out[n] = U[u[n]] . V[i[n]] (+ ub[u[n]]) (+ ib[i[n]]) (+ cb[0]); one wave per pair.
+// LightGCN.predict (lightgcn.py:166-186), MatrixFactorization.forward (:80-106).
+__global__ __launch_bounds__(256) void pair_dot_kernel(const float* __restrict__ U, int64_t nu,
+                                                       int64_t ldu, const float* __restrict__ V,
+                                                       int64_t ni, int64_t ldv, int d,
+                                                       const int64_t* __restrict__ uid,
+                                                       const int64_t* __restrict__ iid, int64_t n,
+                                                       const float* ub, const float* ib,
+                                                       const float* cb, float* __restrict__ out,
+                                                       unsigned* err) {
+  const int64_t e = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (e >= n) return;
+  const int lane = threadIdx.x & 63;
+  const int64_t u = uid[e], i = iid[e];
+  if (u < 0 || u >= nu || i < 0 || i >= ni) {
+    if (lane == 0) {
+      hnm_flag(err, HNM_ERR_OOB);
+      out[e] = __builtin_nanf("");
+    }
+    return;
+  }
+  float acc = 0.f;
+  for (int c = lane; c < d; c += 64) acc = fmaf(U[u * ldu + c], V[i * ldv + c], acc);
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) acc += __shfl_xor(acc, o);
+  if (lane == 0) {
+    if (ub) acc += ub[u];
+    if (ib) acc += ib[i];
+    if (cb) acc += cb[0];
+    out[e] = acc;
+  }
+}
+
+extern "C" hnm_status hnm_pair_dot_f32(hnm_ctx* ctx, const float* user_tab, int64_t num_users,
+                                       int64_t ldu, const float* item_tab, int64_t num_items,
+                                       int64_t ldi, int d, const int64_t* user_ids,
+                                       const int64_t* item_ids, int64_t n,
+                                       const float* user_bias, const float* item_bias,
+                                       const float* const_bias, float* out) {
+  HNM_REQUIRE(ctx && user_tab && item_tab && user_ids && item_ids && out, HNM_EINVAL,
+              "pair_dot: NULL argument");
+  HNM_REQUIRE(d >= 1 && ldu >= d && ldi >= d, HNM_EINVAL, "pair_dot: bad shape");
+  if (n <= 0) return HNM_OK;
+  hipLaunchKernelGGL(pair_dot_kernel, dim3((unsigned)hnm_cdiv(n, 4)), dim3(256), 0, ctx->stream,
+                     user_tab, num_users, ldu, item_tab, num_items, ldi, d, user_ids, item_ids, n,
+                     user_bias, item_bias, const_bias, out, ctx->err_dev);
+  HNM_LAUNCH_CHECK();
+  return HNM_OK;
+}

@@ -1,0 +1,130 @@
+// Device-side building blocks shared by the gfx950 kernels of libhnm_mi355x.
+//
+// * Top-K order is (score desc, item asc): a TOTAL order, so a top-K computed over item
+//   partitions, shards or GPUs and then merged is unique and reproducible.  torch.topk
+//   (`neural_cf.py:324`, `lightgcn.py:356`, `serve.py:355`) leaves ties unspecified.
+// * A wave-resident top-K list keeps slot s in lane (s % 64) of register (s / 64): sorted
+//   insertion is one ballot + popcount + shfl_up, no LDS.  Candidates reach it through a
+//   wave-uniform threshold pre-filter, so after warm-up almost every tile costs one
+//   compare + ballot per score.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define HNM_WAVE 64
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+#define HNM_SENTINEL_IDX 0x7fffffff
+
+__device__ __forceinline__ bool hnm_better(float va, int ia, float vb, int ib) {
+  return va > vb || (va == vb && ia < ib);
+}
+
+__device__ __forceinline__ int hnm_lane() { return __lane_id(); }
+
+__device__ __forceinline__ float hnm_readlane_f(float v, int l) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+__device__ __forceinline__ int hnm_readlane_i(int v, int l) {
+  return __builtin_amdgcn_readlane(v, l);
+}
+
+// Wave-wide sorted list of NS*64 slots (K <= NS*64).
+template <int NS>
+struct WaveTopK {
+  float v[NS];
+  int i[NS];
+  float thr_v;  // wave-uniform copy of slot K-1
+  int thr_i;
+
+  __device__ __forceinline__ void init() {
+#pragma unroll
+    for (int r = 0; r < NS; ++r) {
+      v[r] = -__builtin_inff();
+      i[r] = HNM_SENTINEL_IDX;
+    }
+    thr_v = -__builtin_inff();
+    thr_i = HNM_SENTINEL_IDX;
+  }
+
+  __device__ __forceinline__ void refresh(int K) {
+    const int r = (K - 1) >> 6, l = (K - 1) & 63;
+#pragma unroll
+    for (int q = 0; q < NS; ++q)
+      if (q == r) {
+        thr_v = hnm_readlane_f(v[q], l);
+        thr_i = hnm_readlane_i(i[q], l);
+      }
+  }
+
+  // Insert one wave-uniform candidate (no-op if it does not beat slot K-1).
+  __device__ __forceinline__ void insert(float cv, int ci, int K) {
+    if (!hnm_better(cv, ci, thr_v, thr_i)) return;
+    const int lane = hnm_lane();
+    int pos = 0;
+#pragma unroll
+    for (int r = 0; r < NS; ++r) {
+      const bool b = (lane + 64 * r < K) && hnm_better(v[r], i[r], cv, ci);
+      pos += __popcll(__ballot(b));
+    }
+    float nv[NS];
+    int ni[NS];
+#pragma unroll
+    for (int r = 0; r < NS; ++r) {
+      float up = __shfl_up(v[r], 1);
+      int upi = __shfl_up(i[r], 1);
+      if (r > 0) {
+        const float cv2 = hnm_readlane_f(v[r - 1], 63);
+        const int ci2 = hnm_readlane_i(i[r - 1], 63);
+        if (lane == 0) { up = cv2; upi = ci2; }
+      }
+      const int slot = lane + 64 * r;
+      nv[r] = slot > pos ? up : (slot == pos ? cv : v[r]);
+      ni[r] = slot > pos ? upi : (slot == pos ? ci : i[r]);
+    }
+#pragma unroll
+    for (int r = 0; r < NS; ++r) { v[r] = nv[r]; i[r] = ni[r]; }
+    refresh(K);
+  }
+
+  // Offer one candidate per lane (only lanes with `valid`).  Serial over the lanes whose
+  // candidate passes the current threshold; the threshold only rises, so every later
+  // candidate is re-checked against the updated value inside insert().
+  __device__ __forceinline__ void offer(float sv, int si, bool valid, int K) {
+    uint64_t m = __ballot(valid && (sv > thr_v || (sv == thr_v && si < thr_i)));
+    while (m) {
+      const int l = __builtin_ctzll(m);
+      m &= m - 1;
+      insert(hnm_readlane_f(sv, l), hnm_readlane_i(si, l), K);
+    }
+  }
+
+  // Write slots [0, K) to out_v/out_i (int32 or int64 indices).
+  template <typename IdxT>
+  __device__ __forceinline__ void store(float* out_v, IdxT* out_i, int K) const {
+    const int lane = hnm_lane();
+#pragma unroll
+    for (int r = 0; r < NS; ++r) {
+      const int s = lane + 64 * r;
+      if (s < K) {
+        if (out_v) out_v[s] = v[r];
+        out_i[s] = (IdxT)(i[r] == HNM_SENTINEL_IDX ? -1 : i[r]);
+      }
+    }
+  }
+};
+
+// v_mfma_f32_32x32x2_f32: A[i=l&31][k=l>>5], B[k=l>>5][j=l&31], exact fp32 fma chain.
+// C/D: col j = lane&31, row i = (r&3) + 8*(r>>2) + 4*(lane>>5) for register r.
+__device__ __forceinline__ f32x16 mfma32x32x2(float a, float b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ int mfma32_row(int r, int half) { return (r & 3) + 8 * (r >> 2) + 4 * half; }
+
+// Error word in device memory (ctx-owned): bit 0 = an id out of range was seen.
+#define HNM_ERR_OOB 1u
+__device__ __forceinline__ void hnm_flag(unsigned* err, unsigned bit) {
+  if (err) atomicOr(err, bit);
+}

@@ -1,0 +1,55 @@
+// Host-side internals of libhnm_mi355x: the context object, error plumbing, workspace.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdarg.h>
+#include <stdint.h>
+#include <stdio.h>
+
+#include "../../include/hnm.h"
+
+struct hnm_ctx {
+  int device;
+  hipStream_t stream;   // borrowed from the caller (torch's current stream); 0 = null stream
+  void* ws;             // grow-only device workspace owned by the ctx
+  size_t ws_size;
+  unsigned* err_dev;    // device error word (HNM_ERR_* bits), read by hnm_ctx_check
+  int num_cus;
+};
+
+void hnm_set_error(const char* fmt, ...);
+
+#define HNM_HIP_CHECK(expr)                                                        \
+  do {                                                                             \
+    hipError_t _e = (expr);                                                        \
+    if (_e != hipSuccess) {                                                        \
+      hnm_set_error("%s failed: %s (%s:%d)", #expr, hipGetErrorString(_e), __FILE__, \
+                    __LINE__);                                                     \
+      return HNM_EHIP;                                                             \
+    }                                                                              \
+  } while (0)
+
+#define HNM_REQUIRE(cond, code, ...)  \
+  do {                                \
+    if (!(cond)) {                    \
+      hnm_set_error(__VA_ARGS__);     \
+      return (code);                  \
+    }                                 \
+  } while (0)
+
+#define HNM_LAUNCH_CHECK()                                                          \
+  do {                                                                              \
+    hipError_t _e = hipGetLastError();                                              \
+    if (_e != hipSuccess) {                                                         \
+      hnm_set_error("kernel launch failed: %s (%s:%d)", hipGetErrorString(_e),      \
+                    __FILE__, __LINE__);                                            \
+      return HNM_EHIP;                                                              \
+    }                                                                               \
+  } while (0)
+
+// Returns a device pointer to at least `bytes` of workspace (aligned to 256 B), growing
+// the ctx workspace if needed.  Growth synchronizes the stream (the old buffer may still
+// be read by queued kernels); call hnm_ctx_reserve() before graph capture.
+hnm_status hnm_workspace(hnm_ctx* ctx, size_t bytes, void** out);
+
+static inline size_t hnm_align(size_t x, size_t a = 256) { return (x + a - 1) / a * a; }
+__host__ __device__ static inline int64_t hnm_cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }

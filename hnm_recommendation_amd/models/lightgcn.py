@@ -1,0 +1,234 @@
+"""LightGCN drop-in (reference: `src/models/lightgcn.py`).
+
+* `set_graph(edge_index, edge_weight)` (`:81-134`): records the edges; the normalized CSR
+  (hnm_csr_build_norm) and the SpMM plan are built on the module's GPU on first use, so
+  the reference's serve order -- set_graph, then load_state_dict, then .to(device)
+  (`serve.py:243-252`) -- works unchanged.
+* `forward()` (`:136-164`): L x hnm_spmm_csr_f32 with the alpha-weighted layer sum fused
+  into the SpMM epilogue.  The reference re-propagates on every call; here the result is
+  cached and invalidated whenever the embedding weight (torch version counter / storage)
+  or the graph changes -- same outputs, without L SpMMs per recommend().
+* `predict_all_items` (`:188-204`) -> hnm_dot_scores_f32;  `recommend` (`:332-358`) ->
+  hnm_dot_topk_f32 (fused score GEMM + filter + top-K, user gather fused).
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Dict, Optional, Tuple
+
+import torch
+import torch.nn as nn
+
+from .. import _lib
+from ..evaluation import RecommendationMetrics
+from .base import RecModule, dense_topk, f32c, filter_csr
+
+
+class NormalizedGraph:
+    """D^-1/2 (A + I) D^-1/2 as device CSR (rowptr int64, col int32, val fp32) + SpMM plan."""
+
+    def __init__(self, edge_index: torch.Tensor, edge_weight: Optional[torch.Tensor],
+                 num_nodes: int, device: torch.device):
+        _lib.require_gpu(torch.empty(0, device=device))
+        ei = edge_index.to(device=device, dtype=torch.int64).contiguous()
+        if ei.dim() != 2 or ei.shape[0] != 2:
+            raise ValueError(f"edge_index must be [2, E], got {tuple(ei.shape)}")
+        E = ei.shape[1]
+        ew = None
+        if edge_weight is not None:
+            ew = edge_weight.to(device=device, dtype=torch.float32).contiguous()
+            if ew.numel() != E:
+                raise ValueError("edge_weight must have one entry per edge")
+        self.num_nodes = num_nodes
+        self.nnz = E + num_nodes
+        self.device = device
+        self.rowptr = torch.empty(num_nodes + 1, dtype=torch.int64, device=device)
+        self.col = torch.empty(self.nnz, dtype=torch.int32, device=device)
+        self.val = torch.empty(self.nnz, dtype=torch.float32, device=device)
+        c = _lib.ctx(device)
+        _lib.check(_lib.fn("hnm_csr_build_norm")(c, _lib.ptr(ei), _lib.ptr(ew), E, num_nodes,
+                                                 _lib.ptr(self.rowptr), _lib.ptr(self.col),
+                                                 _lib.ptr(self.val)), "hnm_csr_build_norm")
+        _lib.sync_check(device)
+        plan = C.c_void_p()
+        _lib.check(_lib.fn("hnm_spmm_plan_create")(c, num_nodes, _lib.ptr(self.rowptr),
+                                                   C.byref(plan)), "hnm_spmm_plan_create")
+        self.plan = plan
+
+    def spmm(self, X: torch.Tensor, Y: Optional[torch.Tensor], alpha: float,
+             acc: Optional[torch.Tensor]):
+        """Y = A X;  acc += alpha * Y (either output optional)."""
+        c = _lib.ctx(X.device)
+        _lib.check(_lib.fn("hnm_spmm_csr_f32")(c, self.plan, self.num_nodes,
+                                               _lib.ptr(self.rowptr), _lib.ptr(self.col),
+                                               _lib.ptr(self.val), _lib.ptr(X), X.shape[1],
+                                               _lib.ptr(Y), alpha, _lib.ptr(acc), _lib.ptr(acc)),
+                   "hnm_spmm_csr_f32")
+
+    def __del__(self):
+        plan = getattr(self, "plan", None)
+        if plan and _lib._lib is not None:
+            try:
+                torch.cuda.synchronize(self.device)
+                _lib.fn("hnm_spmm_plan_destroy")(plan)
+            except Exception:
+                pass
+
+
+class _GraphSpec:
+    """What set_graph received; the device CSR is built lazily per device."""
+
+    def __init__(self, edge_index, edge_weight):
+        self.edge_index = edge_index
+        self.edge_weight = edge_weight
+        self.built: Dict[torch.device, NormalizedGraph] = {}
+
+
+class LightGCN(RecModule):
+    def __init__(
+        self,
+        num_users: int,
+        num_items: int,
+        embedding_dim: int = 64,
+        num_layers: int = 3,
+        learning_rate: float = 0.001,
+        weight_decay: float = 1e-4,
+        top_k: int = 12,
+        alpha: Optional[float] = None,
+    ):
+        super().__init__()
+        self.save_hyperparameters()
+        self.num_users = num_users
+        self.num_items = num_items
+        self.num_nodes = num_users + num_items
+        self.embedding_dim = embedding_dim
+        self.num_layers = num_layers
+        self.learning_rate = learning_rate
+        self.weight_decay = weight_decay
+        self.top_k = top_k
+        if alpha is None:  # lightgcn.py:59-67
+            self.alpha = [1.0 / (num_layers + 1)] * (num_layers + 1)
+        else:
+            self.alpha = [alpha ** i for i in range(num_layers + 1)]
+            s = sum(self.alpha)
+            self.alpha = [a / s for a in self.alpha]
+        self.embeddings = nn.Embedding(self.num_nodes, embedding_dim)
+        nn.init.xavier_uniform_(self.embeddings.weight)
+        self.graph = None
+        self.edge_index = None
+        self.edge_weight = None
+        self.metrics = RecommendationMetrics(top_k=top_k)
+        self._cache_key = None
+        self._cache = None
+
+    # ------------------------------------------------------------------ graph
+    def set_graph(self, edge_index: torch.Tensor, edge_weight: Optional[torch.Tensor] = None):
+        """Record the interaction graph (`lightgcn.py:81-112`)."""
+        if edge_index.dim() != 2 or edge_index.shape[0] != 2:
+            raise ValueError(f"edge_index must be [2, E], got {tuple(edge_index.shape)}")
+        self.edge_index = edge_index
+        self.edge_weight = edge_weight
+        self.graph = _GraphSpec(edge_index, edge_weight)
+        self._cache_key = None
+        self._cache = None
+
+    def _device_graph(self) -> NormalizedGraph:
+        if self.graph is None:
+            raise RuntimeError("Graph not set. Call set_graph() first.")
+        dev = self.device
+        g = self.graph.built.get(dev)
+        if g is None:
+            g = NormalizedGraph(self.graph.edge_index, self.graph.edge_weight, self.num_nodes, dev)
+            self.graph.built[dev] = g
+        return g
+
+    # ------------------------------------------------------------------ propagation
+    def forward(self) -> Tuple[torch.Tensor, torch.Tensor]:
+        """(final user embeddings [U, d], final item embeddings [I, d]) (`lightgcn.py:136-164`)."""
+        g = self._device_graph()
+        w = self.embeddings.weight
+        key = (w.data_ptr(), w._version, id(g), w.device)
+        if self._cache_key != key:
+            self._cache = self.propagate(g)
+            self._cache_key = key
+        F = self._cache
+        return F[: self.num_users], F[self.num_users:]
+
+    def propagate(self, g: Optional[NormalizedGraph] = None) -> torch.Tensor:
+        """E_{l+1} = A E_l, F = sum_l alpha_l E_l on the HIP SpMM (no cache)."""
+        g = self._device_graph() if g is None else g
+        E0 = f32c(self.embeddings.weight)
+        _lib.require_gpu(E0)
+        c = _lib.ctx(E0.device)
+        acc = torch.empty_like(E0)
+        _lib.check(_lib.fn("hnm_axpby_f32")(c, E0.numel(), float(self.alpha[0]), _lib.ptr(E0),
+                                            0.0, None, _lib.ptr(acc)), "hnm_axpby_f32")
+        cur = E0
+        for layer in range(self.num_layers):
+            last = layer == self.num_layers - 1
+            nxt = None if last else torch.empty_like(E0)
+            g.spmm(cur, nxt, float(self.alpha[layer + 1]), acc)
+            cur = nxt
+        return acc
+
+    # ------------------------------------------------------------------ scoring
+    def predict(self, user_ids: torch.Tensor, item_ids: torch.Tensor) -> torch.Tensor:
+        """Pairwise dot of propagated embeddings (`lightgcn.py:166-186`)."""
+        fu, fi = self.forward()
+        u = self._ids(user_ids, self.num_users)
+        i = self._ids(item_ids, self.num_items, "item_ids")
+        out = torch.empty(u.numel(), dtype=torch.float32, device=u.device)
+        d = self.embedding_dim
+        c = _lib.ctx(u.device)
+        _lib.check(_lib.fn("hnm_pair_dot_f32")(c, _lib.ptr(fu), self.num_users, d, _lib.ptr(fi),
+                                               self.num_items, d, d, _lib.ptr(u), _lib.ptr(i),
+                                               u.numel(), None, None, None, _lib.ptr(out)),
+                   "hnm_pair_dot_f32")
+        _lib.sync_check(u.device)
+        return out
+
+    def predict_all_items(self, user_ids: torch.Tensor) -> torch.Tensor:
+        """Dense scores F_U[ids] @ F_I^T, [B, num_items] (`lightgcn.py:188-204`)."""
+        fu, fi = self.forward()
+        u = self._ids(user_ids, self.num_users)
+        out = torch.empty(u.numel(), self.num_items, dtype=torch.float32, device=u.device)
+        d = self.embedding_dim
+        c = _lib.ctx(u.device)
+        _lib.check(_lib.fn("hnm_dot_scores_f32")(c, _lib.ptr(fu), self.num_users, d, _lib.ptr(u),
+                                                 u.numel(), _lib.ptr(fi), self.num_items, d, d,
+                                                 None, None, None, _lib.ptr(out), out.stride(0)),
+                   "hnm_dot_scores_f32")
+        _lib.sync_check(u.device)
+        return out
+
+    def recommend_with_scores(self, user_ids: torch.Tensor,
+                              filter_items: Optional[Dict[int, set]] = None,
+                              k: Optional[int] = None):
+        """(scores [B, k], items [B, k]) sorted by score desc, item asc."""
+        k = self.top_k if k is None else k
+        fu, fi = self.forward()
+        u = self._ids(user_ids, self.num_users)
+        n_items = fi.shape[0]
+        mptr, midx = filter_csr(u, filter_items, self.num_items, u.device)
+        kk = min(k, n_items)
+        if kk > 64:
+            scores = self.predict_all_items(u)
+            return dense_topk(scores, kk, mptr, midx)
+        out_v = torch.empty(u.numel(), kk, dtype=torch.float32, device=u.device)
+        out_i = torch.empty(u.numel(), kk, dtype=torch.int64, device=u.device)
+        d = self.embedding_dim
+        c = _lib.ctx(u.device)
+        _lib.check(_lib.fn("hnm_dot_topk_f32")(c, _lib.ptr(fu), self.num_users, d, _lib.ptr(u),
+                                               u.numel(), _lib.ptr(fi), n_items, fi.stride(0), d,
+                                               None, None, None, _lib.ptr(mptr), _lib.ptr(midx),
+                                               kk, _lib.ptr(out_v), _lib.ptr(out_i)),
+                   "hnm_dot_topk_f32")
+        _lib.sync_check(u.device)
+        return out_v, out_i
+
+    def recommend(self, user_ids: torch.Tensor,
+                  filter_items: Optional[Dict[int, set]] = None) -> torch.Tensor:
+        """Top-`top_k` item ids per user (`lightgcn.py:332-358`)."""
+        self.eval()
+        with torch.no_grad():
+            return self.recommend_with_scores(user_ids, filter_items)[1]

@@ -1,0 +1,180 @@
+/* libhnm_mi355x — C ABI of the MI355X-native top-N scoring hot path.
+ *
+ * Drop-in boundary for hyunlord/hnm_recommendation @ 2025-07-25 (reference paths below are
+ * relative to that repo).  The reference has no FFI: its boundary is the PyTorch module
+ * surface `NeuralCF` / `LightGCN` / `WideDeep` / `MatrixFactorization` with `forward`,
+ * `predict_all_items`, `recommend` and `set_graph`.  Each entry point
+ * below replaces the ATen / torch_sparse work one of those methods does; the Python
+ * mirror in `hnm_recommendation_amd/models/` binds them with ctypes.
+ *
+ * Conventions
+ *  - Every pointer argument is a DEVICE pointer owned by the caller (the torch caching
+ *    allocator); the library never frees caller memory.  Shapes are row-major, fp32
+ *    tables with an explicit leading dimension, int64 ids.
+ *  - Calls are asynchronous and stream-ordered on the ctx stream (hnm_ctx_set_stream:
+ *    torch's current stream).  One ctx per device; a ctx is not re-entrant.
+ *  - Status: 0 on success, negative on error; hnm_last_error() holds a thread-local
+ *    message.  No C++ exception crosses the ABI.
+ *  - Out-of-range user/item ids never fault: the row is skipped (index -1 / NaN) and the
+ *    ctx error word records it; hnm_ctx_check() synchronizes and returns HNM_EOOB, which
+ *    the Python layer raises as IndexError (reference: nn.Embedding IndexError).
+ *  - Top-K order is (score desc, item index asc); -inf (filtered) items rank last and are
+ *    returned only when fewer than k finite scores exist (torch.topk semantics).
+ */
+#ifndef HNM_H_
+#define HNM_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define HNM_ABI_VERSION 1
+
+typedef int32_t hnm_status;
+enum {
+  HNM_OK = 0,
+  HNM_EINVAL = -1,       /* bad argument / shape */
+  HNM_EOOB = -2,         /* an id was out of range (reported by hnm_ctx_check) */
+  HNM_EHIP = -3,         /* HIP runtime error */
+  HNM_ENOMEM = -4,       /* workspace allocation failed */
+  HNM_EUNSUPPORTED = -5  /* shape outside what the kernels are built for */
+};
+
+typedef struct hnm_ctx hnm_ctx;
+typedef struct hnm_spmm_plan hnm_spmm_plan;
+
+int hnm_abi_version(void);
+const char* hnm_last_error(void);
+
+/* ---- context ------------------------------------------------------------------------ */
+hnm_status hnm_ctx_create(int device, hnm_ctx** out);
+hnm_status hnm_ctx_destroy(hnm_ctx* ctx);
+hnm_status hnm_ctx_set_stream(hnm_ctx* ctx, void* hip_stream);
+hnm_status hnm_ctx_reserve(hnm_ctx* ctx, size_t bytes);   /* pre-grow workspace */
+hnm_status hnm_ctx_check(hnm_ctx* ctx);                   /* sync; HNM_EOOB if flagged */
+hnm_status hnm_ctx_num_cus(hnm_ctx* ctx, int* out);
+
+/* ---- a1: embedding row gather ------------------------------------------------------
+ * out[b, :d] = table[ids[b], :d].  Replaces nn.Embedding.__call__ at
+ * neural_cf.py:155-156, lightgcn.py:199, wide_deep.py:207. */
+hnm_status hnm_gather_rows_f32(hnm_ctx* ctx, const float* table, int64_t rows, int64_t ld,
+                               int d, const int64_t* ids, int64_t n, float* out,
+                               int64_t ldo);
+
+/* ---- per-row projection used to decompose the first MLP layer --------------------
+ * Y[r, c(n)] = sum_k X[x(r), k] * W[n, k] (+ bias[n]),  n < N, k < K.
+ * x(r) = ids ? ids[r] : r (ids bounded by x_rows);  c(n) = n, or with pair_permute
+ * c(n) = (n & 1) * (ldy / 2) + (n >> 1) — the lane-half layout the MFMA kernels read.
+ * W has leading dimension ldw (a column slice of a Linear weight, e.g. the user or the
+ * item half of mlp_layers.0.weight, neural_cf.py:85-87 / wide_deep.py:128). */
+hnm_status hnm_linear_rows_f32(hnm_ctx* ctx, const float* X, int64_t ldx, const int64_t* ids,
+                               int64_t x_rows, int64_t M, int K, const float* W,
+                               int64_t ldw, const float* bias, int N, float* Y, int64_t ldy,
+                               int pair_permute);
+
+/* ---- a7 + a11 + a12: dot-product scoring fused with filter and top-K ---------------
+ * s[b, i] = user_tab[user_ids[b]] . item_tab[i] (+ user_bias[user_ids[b]]) (+ item_bias[i])
+ *           (+ const_bias[0]); masked (b, i) -> -inf; top-k per row.
+ * LightGCN.predict_all_items + recommend (lightgcn.py:188-204, 332-358) and
+ * MatrixFactorization (matrix_factorization.py:108-131, 220-246).
+ * mask: CSR over the batch rows (mask_ptr[B+1], mask_idx sorted ascending per row) or NULL.
+ * d <= 128, d % 4 == 0, 16-B aligned tables.  Fused path: k <= 64 (larger k: dense
+ * scores + hnm_topk_rows_f32). */
+hnm_status hnm_dot_topk_f32(hnm_ctx* ctx, const float* user_tab, int64_t num_users,
+                            int64_t ldu, const int64_t* user_ids, int64_t B,
+                            const float* item_tab, int64_t num_items, int64_t ldi, int d,
+                            const float* user_bias, const float* item_bias,
+                            const float* const_bias, const int64_t* mask_ptr,
+                            const int32_t* mask_idx, int k, float* out_val,
+                            int64_t* out_idx);
+/* Dense variant: out[b, i] (ldo >= num_items), the predict_all_items matrix. */
+hnm_status hnm_dot_scores_f32(hnm_ctx* ctx, const float* user_tab, int64_t num_users,
+                              int64_t ldu, const int64_t* user_ids, int64_t B,
+                              const float* item_tab, int64_t num_items, int64_t ldi, int d,
+                              const float* user_bias, const float* item_bias,
+                              const float* const_bias, float* out, int64_t ldo);
+
+/* Pairwise variant: out[n] = user_tab[user_ids[n]] . item_tab[item_ids[n]] + biases
+ * (LightGCN.predict lightgcn.py:166-186, MatrixFactorization.forward :80-106). */
+hnm_status hnm_pair_dot_f32(hnm_ctx* ctx, const float* user_tab, int64_t num_users,
+                            int64_t ldu, const float* item_tab, int64_t num_items, int64_t ldi,
+                            int d, const int64_t* user_ids, const int64_t* item_ids, int64_t n,
+                            const float* user_bias, const float* item_bias,
+                            const float* const_bias, float* out);
+
+/* ---- a3 + a4: NeuralCF --------------------------------------------------------------
+ * Reference layout (state_dict of neural_cf.py:56-67):  mlp_dims = [2*h0, h1, h2].
+ *   s = wp[:mf].(g_u * g_i) + wp[mf:].relu(W2 relu(W1 [m_u; m_i] + b1) + b2) + bp
+ * Requires mf <= 128, h1 <= 128, h2 <= 32 (the default 64 / [128,64,32] config). */
+typedef struct {
+  const float* gmf_user;   /* [num_users, mf] */
+  const float* gmf_item;   /* [num_items, mf] */
+  const float* mlp_user;   /* [num_users, h0] */
+  const float* mlp_item;   /* [num_items, h0] */
+  const float* w1;         /* [h1, 2*h0]  mlp_layers.0.weight */
+  const float* b1;         /* [h1] */
+  const float* w2;         /* [h2, h1]    mlp_layers.3.weight */
+  const float* b2;         /* [h2] */
+  const float* wp;         /* [mf + h2]   prediction_layer.weight */
+  const float* bp;         /* [1]         prediction_layer.bias */
+  int64_t num_users;
+  int64_t num_items;
+  int32_t mf;
+  int32_t h0;
+  int32_t h1;
+  int32_t h2;
+} hnm_ncf_weights;
+
+hnm_status hnm_ncf_topk_f32(hnm_ctx* ctx, const hnm_ncf_weights* w, const int64_t* user_ids,
+                            int64_t B, const int64_t* mask_ptr, const int32_t* mask_idx,
+                            int k, float* out_val, int64_t* out_idx);
+hnm_status hnm_ncf_scores_f32(hnm_ctx* ctx, const hnm_ncf_weights* w,
+                              const int64_t* user_ids, int64_t B, float* out, int64_t ldo);
+/* NeuralCF.forward(user_ids, item_ids) (neural_cf.py:112-141): out[n]. */
+hnm_status hnm_ncf_pair_scores_f32(hnm_ctx* ctx, const hnm_ncf_weights* w,
+                                   const int64_t* user_ids, const int64_t* item_ids,
+                                   int64_t n, float* out);
+
+/* ---- top-K merge (item partitions, item shards across GPUs) ------------------------
+ * Candidates of row b: for g < G: cand[g*gstride + b*bstride + j], j < kc (value, global
+ * item index; index < 0 = empty).  out: the best k of them per row, sorted. */
+hnm_status hnm_topk_merge_f32(hnm_ctx* ctx, const float* cand_val, const int64_t* cand_idx,
+                              int64_t B, int64_t G, int64_t gstride, int64_t bstride,
+                              int kc, int k, float* out_val, int64_t* out_idx);
+
+/* ---- torch.topk over a dense score matrix (serve.py:350-355, k up to 100) ----------
+ * Row top-k of scores[b, :I] (leading dim ld) with the optional CSR -inf mask. k <= 128. */
+hnm_status hnm_topk_rows_f32(hnm_ctx* ctx, const float* scores, int64_t ld, int64_t B,
+                             int64_t I, const int64_t* mask_ptr, const int32_t* mask_idx,
+                             int k, float* out_val, int64_t* out_idx);
+
+/* ---- a5: LightGCN.set_graph ----------------------------------------------------------
+ * A_hat = D^-1/2 (A + I) D^-1/2 (lightgcn.py:81-134) as CSR with E + N entries:
+ * self-loops appended, deg = row sums of the weights (edge_weight NULL -> 1), deg^-1/2
+ * with inf -> 0, val = dinv[row] * w * dinv[col]; duplicates kept (summed by the SpMM). */
+hnm_status hnm_csr_build_norm(hnm_ctx* ctx, const int64_t* edge_index, const float* edge_weight,
+                              int64_t E, int64_t N, int64_t* rowptr, int32_t* col, float* val);
+
+/* ---- a6: LightGCN.forward propagation -----------------------------------------------
+ * Y = A_hat X (graph @ all_embeddings, lightgcn.py:152), with the layer combine fused:
+ * acc_out = acc_in + alpha * Y (lightgcn.py:156-158).  Y and acc_out may be NULL.
+ * d in {4, 8, 16, 32, 64, 128, 256}.  The plan splits power-law rows (item rows with
+ * up to ~1e6 neighbours) into fixed segments summed in a fixed order (deterministic). */
+hnm_status hnm_spmm_plan_create(hnm_ctx* ctx, int64_t N, const int64_t* rowptr,
+                                hnm_spmm_plan** out);
+hnm_status hnm_spmm_plan_destroy(hnm_spmm_plan* plan);
+hnm_status hnm_spmm_csr_f32(hnm_ctx* ctx, const hnm_spmm_plan* plan, int64_t N,
+                            const int64_t* rowptr, const int32_t* col, const float* val,
+                            const float* X, int d, float* Y, float alpha,
+                            const float* acc_in, float* acc_out);
+/* out = alpha * x + beta * y (y may be NULL): the alpha_0 * E_0 term of the combine. */
+hnm_status hnm_axpby_f32(hnm_ctx* ctx, int64_t n, float alpha, const float* x, float beta,
+                         const float* y, float* out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* HNM_H_ */

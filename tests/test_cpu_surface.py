@@ -1,0 +1,99 @@
+"""CPU-side checks (no GPU): library exports, module surface vs the reference, host logic,
+error behaviour."""
+import os
+import re
+
+import numpy as np
+import pytest
+import torch
+
+from parity import load_golden
+from hnm_recommendation_amd import LightGCN, MatrixFactorization, NeuralCF, RecommendationMetrics
+from hnm_recommendation_amd import _lib
+from hnm_recommendation_amd.models.base import filter_csr
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_symbols():
+    src = open(os.path.join(REPO, "include", "hnm.h")).read()
+    return sorted(set(re.findall(r"^\s*(?:hnm_status|int|const char\*)\s+(hnm_\w+)\s*\(", src, re.M)))
+
+
+def test_library_exports_every_declared_symbol():
+    lib = _lib.load()
+    syms = header_symbols()
+    assert len(syms) >= 20
+    missing = [s for s in syms if not hasattr(lib, s)]
+    assert not missing, missing
+    assert lib.hnm_abi_version() == 1
+    # every header symbol has a ctypes signature
+    assert set(syms) <= set(_lib.declared_symbols()), set(syms) - set(_lib.declared_symbols())
+
+
+@pytest.mark.parametrize("cls,golden,kw", [
+    (NeuralCF, "ncf_small.npz", {}),
+    (LightGCN, "lightgcn_d64.npz", {}),
+    (LightGCN, "lightgcn_d128.npz", {"embedding_dim": 128}),
+    (MatrixFactorization, "mf_small.npz", {"sparse": False}),
+])
+def test_state_dict_keys_match_reference(cls, golden, kw):
+    g = load_golden(golden)
+    m = cls(int(g["U"]), int(g["I"]), **kw)
+    ours = {k: tuple(v.shape) for k, v in m.state_dict().items()}
+    ref = {k: tuple(np.asarray(v).shape) for k, v in g["sd"].items()}
+    assert ours == ref
+    m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in g["sd"].items()})
+
+
+def test_hparams_and_signature_mirror_reference():
+    m = NeuralCF(num_users=100, num_items=50, mf_dim=32, mlp_dims=[64, 32, 16], top_k=5)
+    assert m.hparams["mf_dim"] == 32 and m.hparams["top_k"] == 5
+    # reference tests/test_models.py:75 passes embedding_dim to NeuralCF -> TypeError there too
+    with pytest.raises(TypeError):
+        NeuralCF(num_users=100, num_items=50, embedding_dim=16, top_k=5)
+    lg = LightGCN(num_users=100, num_items=50, embedding_dim=16, num_layers=3, top_k=5)
+    assert len(lg.alpha) == 4 and abs(sum(lg.alpha) - 1) < 1e-6
+    lg2 = LightGCN(100, 50, alpha=0.5)
+    np.testing.assert_allclose(lg2.alpha, np.array([1, .5, .25, .125]) / 1.875)
+
+
+def test_lightgcn_errors_like_reference():
+    m = LightGCN(100, 50, embedding_dim=16)
+    with pytest.raises(RuntimeError, match="Graph not set"):
+        m.forward()
+    users = torch.randint(0, 100, (200,))
+    items = torch.randint(0, 50, (200,)) + 100
+    m.set_graph(torch.stack([torch.cat([users, items]), torch.cat([items, users])]))
+    assert m.graph is not None
+
+
+def test_no_cpu_fallback():
+    m = NeuralCF(100, 50)
+    with pytest.raises(RuntimeError, match="no CPU path|GPU"):
+        m.recommend(torch.tensor([0, 1]))
+    with pytest.raises(RuntimeError, match="no CPU path|GPU"):
+        m.predict_all_items(torch.tensor([0, 1]))
+
+
+def test_filter_csr_host_logic():
+    ids = torch.tensor([5, 7, 5, 9])
+    mptr, midx = filter_csr(ids, {5: {3, 1, 1}, 9: {-1}, 11: {2}}, 10, torch.device("cpu"))
+    assert mptr.tolist() == [0, 2, 2, 4, 5]
+    assert midx.tolist() == [1, 3, 1, 3, 9]
+    assert filter_csr(ids, None, 10, torch.device("cpu")) == (None, None)
+    assert filter_csr(ids, {}, 10, torch.device("cpu")) == (None, None)
+    with pytest.raises(IndexError):
+        filter_csr(ids, {7: {10}}, 10, torch.device("cpu"))
+
+
+def test_recommendation_metrics_formulas():
+    m = RecommendationMetrics(top_k=3)
+    m.update(torch.tensor([[1, 2, 3], [4, 5, 6]]), [[2, 9], [7]])
+    r = m.compute()
+    # user 0: hit at rank 2 -> AP = (1/2)/min(2,3) = 0.25; user 1: 0
+    assert abs(float(r["map_at_k"]) - 0.125) < 1e-6
+    assert abs(float(r["recall_at_k"]) - 0.25) < 1e-6
+    assert abs(float(r["precision_at_k"]) - (1 / 3) / 2) < 1e-6
+    idcg = 1 + 1 / np.log2(3)
+    assert abs(float(r["ndcg_at_k"]) - (1 / np.log2(3)) / idcg / 2) < 1e-6
