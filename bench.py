@@ -1,0 +1,237 @@
+"""Headline benchmark: recommendations/sec (batched users, K=12) on the reference's
+configs (BASELINE.json), MI355X-native HIP path.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload ncf|lightgcn|lightgcn128|widedeep|mf]
+
+Default workload = BASELINE.json configs[1]: NeuralCF mf 64, mlp [128,64,32], full H&M
+shape (1,371,980 users x 105,542 items), batch 4096 users per rank per step, K=12,
+synthetic PCG64 weights with the reference init distributions.  A step = one
+`recommend()` of the batch: per-user + per-item layer-1 projections, the fused
+pair-MLP + top-K kernel, the partition merge (and at N>1 the item-sharded exchange:
+all_gather of user ids + all_to_all of candidates + merge).  Inputs (user-id batches) are
+resident in HBM before timing.
+
+N>1 (torchrun, one rank per GPU): items are row-sharded across ranks; every rank brings
+4096 users and scores all N*4096 users against its I/N items (weak scaling).
+
+Also printed in the same JSON line:
+  roofline     -- dominant kernel (ncf_score_kernel) algorithmic FLOPs per launch / its
+                  average duration (HIP events on the ctx stream, measured live here),
+                  vs the fp32 MFMA peak; `traffic` from the committed rocprofv3 PMC
+                  summary (profiles/) when present for this workload.
+  cpu_baseline -- the CPU oracle (numpy restatement of the reference, op for op) on a
+                  bounded user sample, rank 0 at N=1 only.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+from hnm_recommendation_amd import LightGCN, MatrixFactorization, NeuralCF  # noqa: E402
+from hnm_recommendation_amd import _lib  # noqa: E402
+from hnm_recommendation_amd import sharding as S  # noqa: E402
+from hnm_recommendation_amd import synthetic as syn  # noqa: E402
+
+METRIC = "recommendations/sec (batched users, K=12) at 1/2/4/8 MI355X; % HBM roofline"
+FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: fp32 matrix (= vector) peak
+HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md: HBM3E spec peak
+K = 12
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def setup_dist(n_gpus):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    return rank, world, torch.device("cuda", local if world > 1 else 0)
+
+
+def load(m, sd, device):
+    m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in sd.items()})
+    return m.to(device).eval()
+
+
+def build_workload(name, rank, world, device, batch):
+    """Returns (step_fn(users) -> (vals, idx), flops_or_bytes_per_launch, bound, info)."""
+    U, I = syn.HM_USERS, syn.HM_ITEMS
+    lo, hi = S.shard_range(I, rank, world)
+    if name == "ncf":
+        sd = syn.ncf_state_dict(U, I, 64, (128, 64, 32), seed=0)
+        m = load(NeuralCF(U, I), sd, device)
+        local = S.ncf_shard_topk(m, lo, hi, K)
+        per_launch = 4352.0 * batch * world * (hi - lo)   # 4,352 FLOP / pair
+        info = {"model": "NeuralCF", "mf_dim": 64, "mlp_dims": [128, 64, 32]}
+        bound, kernel = "mfma", "ncf_score_kernel"
+        cpu = ("ncf", sd)
+    elif name in ("lightgcn", "lightgcn128"):
+        d = 64 if name == "lightgcn" else 128
+        sd = syn.lightgcn_state_dict(U, I, d, seed=0)
+        m = LightGCN(U, I, embedding_dim=d, num_layers=3)
+        m.set_graph(torch.from_numpy(syn.bipartite_edge_index(U, I, syn.HM_INTERACTIONS, seed=2)))
+        m = load(m, sd, device)
+        fu, fi = m.forward()
+        local = S.dot_shard_topk(fu, fi, lo, hi, K)
+        per_launch = 2.0 * d * batch * world * (hi - lo)
+        info = {"model": "LightGCN", "embedding_dim": d, "num_layers": 3,
+                "interactions": syn.HM_INTERACTIONS}
+        bound, kernel = "mfma", "dot_score_kernel"
+        cpu = None
+        info["_model"] = m
+    elif name == "mf":
+        sd = syn.mf_state_dict(U, I, 64, seed=0)
+        m = load(MatrixFactorization(U, I, sparse=False), sd, device)
+        local = S.dot_shard_topk(m.user_embeddings.weight.detach(), m.item_embeddings.weight.detach(),
+                                 lo, hi, K)
+        per_launch = 2.0 * 64 * batch * world * (hi - lo)
+        info = {"model": "MatrixFactorization", "embedding_dim": 64}
+        bound, kernel = "mfma", "dot_score_kernel"
+        cpu = None
+    else:
+        raise SystemExit(f"unknown workload {name}")
+    rec = S.ItemShardedRecommender(local, S.hip_merge, K, lo, rank, world)
+    return rec.recommend, per_launch, bound, kernel, info, cpu
+
+
+def cpu_baseline(cpu, seconds_budget=20.0):
+    """Time the CPU oracle (numpy restatement of the reference) on a bounded user sample."""
+    if cpu is None:
+        return None
+    from oracle import hnm_oracle as O  # baseline leg only
+    kind, sd = cpu
+    cores = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    torch.set_num_threads(cores)
+    users = syn.user_batch(syn.HM_USERS, 64, seed=7)
+    O.recommend(O.ncf_predict_all_items(sd, users[:8]), users[:8], K)  # warm-up
+    times = []
+    t_start = time.perf_counter()
+    while len(times) < 3 and time.perf_counter() - t_start < seconds_budget:
+        t0 = time.perf_counter()
+        O.recommend(O.ncf_predict_all_items(sd, users), users, K)
+        times.append(time.perf_counter() - t0)
+    med = float(np.median(times))
+    return {"value": round(len(users) / med, 3), "unit": "users/s", "cores": cores,
+            "kind": "port",
+            "sample": f"oracle.ncf_predict_all_items + topk(12), B={len(users)} users x "
+                      f"{syn.HM_ITEMS} items (1000-item chunks as neural_cf.py:167), "
+                      f"median of {len(times)} runs, numpy fp32 BLAS on {cores} threads"}
+
+
+def pmc_traffic(workload):
+    """HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC summary."""
+    p = os.path.join(REPO, "profiles", f"pmc_{workload}.json")
+    if not os.path.exists(p):
+        return None
+    try:
+        return json.load(open(p)).get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=4096)
+    ap.add_argument("--workload", default="ncf")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    rank, world, device = setup_dist(args.gpus)
+    B = args.batch
+    t_setup = time.perf_counter()
+    step, per_launch, bound, kernel, info, cpu = build_workload(args.workload, rank, world,
+                                                                device, B)
+    # resident user batches: rank-specific, distinct ids
+    nb = 4
+    batches = [torch.from_numpy(syn.user_batch(syn.HM_USERS, B, seed=100 + 17 * rank + j)).to(device)
+               for j in range(nb)]
+    torch.cuda.synchronize()
+    log(f"[rank {rank}] setup {time.perf_counter() - t_setup:.1f}s")
+
+    for j in range(args.warmup):
+        step(batches[j % nb])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    _lib.enable_timing(device, True)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for j in range(args.steps):
+        step(batches[j % nb])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    ktime_ms, launches = _lib.kernel_timing(device)
+    _lib.enable_timing(device, False)
+    if world > 1:
+        t = torch.tensor([elapsed, ktime_ms / max(launches, 1)], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, avg_kernel_ms = float(t[0]), float(t[1])
+    else:
+        avg_kernel_ms = ktime_ms / max(launches, 1)
+
+    users_total = B * world * args.steps
+    value = users_total / elapsed
+    achieved = per_launch / (avg_kernel_ms * 1e-3) / 1e12
+    peak = FP32_MFMA_PEAK_TFLOPS
+    line = {
+        "metric": METRIC,
+        "value": round(value, 2),
+        "unit": "users/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (PCG64 weights with reference init distributions; H&M shape)",
+        "config": {"workload": f"{args.workload}: BASELINE configs[1] NeuralCF dim=64, full H&M "
+                               f"shape, batch={B} users/rank, K=12" if args.workload == "ncf"
+                   else args.workload,
+                   "users": syn.HM_USERS, "items": syn.HM_ITEMS, "batch_per_rank": B, "k": K,
+                   "parallelism": f"item-shard{world}" if world > 1 else "single",
+                   **{k: v for k, v in info.items() if not k.startswith("_")}},
+        "roofline": {"bound": bound, "kernel": kernel,
+                     "achieved": round(achieved, 3), "peak": peak, "unit": "TFLOP/s",
+                     "frac": round(achieved / peak, 4),
+                     "avg_kernel_ms": round(avg_kernel_ms, 4), "launches": launches,
+                     "algorithmic_per_launch": per_launch,
+                     "traffic": pmc_traffic(args.workload)},
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        try:
+            line["cpu_baseline"] = cpu_baseline(cpu)
+        except Exception as e:  # baseline is reported, never fatal
+            log(f"cpu baseline failed: {e!r}")
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

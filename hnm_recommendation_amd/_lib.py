@@ -48,6 +48,8 @@ _SIGS = {
     "hnm_ctx_reserve": (_i32, [_p, C.c_size_t]),
     "hnm_ctx_check": (_i32, [_p]),
     "hnm_ctx_num_cus": (_i32, [_p, C.POINTER(C.c_int)]),
+    "hnm_ctx_enable_timing": (_i32, [_p, C.c_int]),
+    "hnm_ctx_timing": (_i32, [_p, C.POINTER(C.c_double), C.POINTER(_i64)]),
     "hnm_gather_rows_f32": (_i32, [_p, _p, _i64, _i64, C.c_int, _p, _i64, _p, _i64]),
     "hnm_linear_rows_f32": (_i32, [_p, _p, _i64, _p, _i64, _i64, C.c_int, _p, _i64, _p,
                                    C.c_int, _p, _i64, C.c_int]),
@@ -155,6 +157,18 @@ def ctx(device: torch.device):
 def sync_check(device):
     """Synchronize the ctx stream and raise IndexError if a kernel saw an out-of-range id."""
     check(fn("hnm_ctx_check")(ctx(device)), "hnm_ctx_check")
+
+
+def enable_timing(device, on=True):
+    check(fn("hnm_ctx_enable_timing")(ctx(device), int(on)), "hnm_ctx_enable_timing")
+
+
+def kernel_timing(device):
+    """(summed dominant-kernel ms, launches) since enable_timing; syncs the stream."""
+    t = C.c_double()
+    n = _i64()
+    check(fn("hnm_ctx_timing")(ctx(device), C.byref(t), C.byref(n)), "hnm_ctx_timing")
+    return t.value, n.value
 
 
 def ptr(t):

@@ -42,6 +42,12 @@ extern "C" hnm_status hnm_ctx_destroy(hnm_ctx* ctx) {
   if (!ctx) return HNM_OK;
   (void)hipSetDevice(ctx->device);
   (void)hipDeviceSynchronize();
+  for (int i = 0; i < ctx->cap; ++i) {
+    (void)hipEventDestroy(ctx->ev0[i]);
+    (void)hipEventDestroy(ctx->ev1[i]);
+  }
+  free(ctx->ev0);
+  free(ctx->ev1);
   if (ctx->ws) (void)hipFree(ctx->ws);
   if (ctx->err_dev) (void)hipFree(ctx->err_dev);
   free(ctx);
@@ -82,6 +88,53 @@ extern "C" hnm_status hnm_ctx_reserve(hnm_ctx* ctx, size_t bytes) {
   HNM_REQUIRE(ctx, HNM_EINVAL, "ctx is NULL");
   void* p;
   return hnm_workspace(ctx, bytes, &p);
+}
+
+// ------------------------------------------------------------------ kernel timer
+void hnm_timer_begin(hnm_ctx* ctx) {
+  if (!ctx->timing) return;
+  if (ctx->nev == ctx->cap) {
+    const int ncap = ctx->cap ? 2 * ctx->cap : 256;
+    hipEvent_t* a = (hipEvent_t*)realloc(ctx->ev0, ncap * sizeof(hipEvent_t));
+    hipEvent_t* b = (hipEvent_t*)realloc(ctx->ev1, ncap * sizeof(hipEvent_t));
+    if (!a || !b) { ctx->timing = 0; return; }
+    ctx->ev0 = a;
+    ctx->ev1 = b;
+    for (int i = ctx->cap; i < ncap; ++i) {
+      (void)hipEventCreate(&ctx->ev0[i]);
+      (void)hipEventCreate(&ctx->ev1[i]);
+    }
+    ctx->cap = ncap;
+  }
+  (void)hipEventRecord(ctx->ev0[ctx->nev], ctx->stream);
+}
+
+void hnm_timer_end(hnm_ctx* ctx) {
+  if (!ctx->timing || ctx->nev >= ctx->cap) return;
+  (void)hipEventRecord(ctx->ev1[ctx->nev], ctx->stream);
+  ++ctx->nev;
+}
+
+extern "C" hnm_status hnm_ctx_enable_timing(hnm_ctx* ctx, int on) {
+  HNM_REQUIRE(ctx, HNM_EINVAL, "ctx is NULL");
+  ctx->timing = on;
+  ctx->nev = 0;
+  return HNM_OK;
+}
+
+extern "C" hnm_status hnm_ctx_timing(hnm_ctx* ctx, double* total_ms, int64_t* launches) {
+  HNM_REQUIRE(ctx && total_ms && launches, HNM_EINVAL, "hnm_ctx_timing: NULL argument");
+  HNM_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+  double t = 0.0;
+  for (int i = 0; i < ctx->nev; ++i) {
+    float ms = 0.f;
+    HNM_HIP_CHECK(hipEventElapsedTime(&ms, ctx->ev0[i], ctx->ev1[i]));
+    t += ms;
+  }
+  *total_ms = t;
+  *launches = ctx->nev;
+  ctx->nev = 0;
+  return HNM_OK;
 }
 
 extern "C" hnm_status hnm_ctx_check(hnm_ctx* ctx) {

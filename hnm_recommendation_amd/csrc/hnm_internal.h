@@ -14,7 +14,17 @@ struct hnm_ctx {
   size_t ws_size;
   unsigned* err_dev;    // device error word (HNM_ERR_* bits), read by hnm_ctx_check
   int num_cus;
+  // dominant-kernel timer (hnm_ctx_enable_timing): HIP events recorded on the ctx stream
+  // immediately before/after the main kernel of each call
+  int timing;
+  int nev;
+  int cap;
+  hipEvent_t* ev0;
+  hipEvent_t* ev1;
 };
+
+void hnm_timer_begin(hnm_ctx* ctx);
+void hnm_timer_end(hnm_ctx* ctx);
 
 void hnm_set_error(const char* fmt, ...);
 

@@ -571,12 +571,14 @@ static hnm_status dot_common(hnm_ctx* ctx, const float* ut, int64_t U, int64_t l
   else                                                                                     \
     launch_dot<DPV, DENSE, false>(ctx, grid, ut, U, ldu, ids, B, it, I, ldi, d, ub, ib,    \
                                   cb, part.ipp, mptr, midx, K, cv, ci, part.np, dense, ldo);
+  hnm_timer_begin(ctx);
   if (d <= 64) {
     HNM_DOT(64)
   } else {
     HNM_DOT(128)
   }
 #undef HNM_DOT
+  hnm_timer_end(ctx);
   HNM_LAUNCH_CHECK();
   if (!DENSE) return hnm_topk_merge_i32(ctx, cv, ci, B, 1, 0, (int64_t)part.np * K,
                                         part.np * K, K, ov, oi);
@@ -762,12 +764,14 @@ static hnm_status ncf_common(hnm_ctx* ctx, const hnm_ncf_weights* w, const int64
   else                                                                                        \
     launch_ncf<WUV, 64, 32, DENSE>(ctx, grid, Pu, WGu, Qi, G, ldg, w, B, part.ipp, mptr, midx, \
                                    K, cv, ci, part.np, dense, ldo);
+  hnm_timer_begin(ctx);
   if (WU == 4) {
     HNM_NCF(4)
   } else {
     HNM_NCF(1)
   }
 #undef HNM_NCF
+  hnm_timer_end(ctx);
   HNM_LAUNCH_CHECK();
   if (!DENSE)
     return hnm_topk_merge_i32(ctx, cv, ci, B, 1, 0, (int64_t)part.np * K, part.np * K, K, ov, oi);

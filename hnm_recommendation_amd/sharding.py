@@ -1,0 +1,131 @@
+"""Item-row sharding across the GPUs of a node (north_star).
+
+The reference has no distributed code; this is the MI355X design:
+
+* rank g owns items [floor(g I / G), floor((g+1) I / G)) -- its slice of the item tables
+  and of the per-item precompute;
+* every rank brings its own batch of B users; one `all_gather` of the user ids (int64,
+  B*8 bytes per rank) gives every rank the G*B users of the step;
+* each rank runs the fused score + top-K kernel over its item shard for all G*B users
+  (per-GPU work is the single-GPU work: weak scaling);
+* one `all_to_all` returns to every rank the G candidate lists (k scores + global item
+  ids) of ITS users (B*k*(4+8) bytes per rank pair: latency-bound on xGMI, so one
+  collective, not a ring of per-layer exchanges);
+* the owner merges G*k candidates per user with the HIP merge kernel.  The order
+  (score desc, item asc) is total, so the result is exactly the single-GPU top-k.
+
+Collectives go through `torch.distributed` (backend "nccl" = RCCL over xGMI on ROCm; gloo
+for the CPU tests).  The local scorer and the merge are injected so the host logic above
+is tested with gloo on CPU (tests/test_sharding_gloo.py) while the product wires the HIP
+kernels (`ncf_shard_topk`, `dot_shard_topk`, `hip_merge`).
+"""
+from __future__ import annotations
+
+from typing import Callable, Optional, Tuple
+
+import torch
+import torch.distributed as dist
+
+from . import _lib
+
+LocalTopK = Callable[[torch.Tensor], Tuple[torch.Tensor, torch.Tensor]]
+Merge = Callable[[torch.Tensor, torch.Tensor, int], Tuple[torch.Tensor, torch.Tensor]]
+
+
+def shard_range(num_items: int, rank: int, world: int) -> Tuple[int, int]:
+    return num_items * rank // world, num_items * (rank + 1) // world
+
+
+class ItemShardedRecommender:
+    def __init__(self, local_topk: LocalTopK, merge: Merge, k: int, item_offset: int,
+                 rank: int = 0, world: int = 1, group=None):
+        self.local_topk = local_topk
+        self.merge = merge
+        self.k = k
+        self.item_offset = item_offset
+        self.rank = rank
+        self.world = world
+        self.group = group
+
+    def recommend(self, user_ids: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+        """Top-k (scores, global item ids) for this rank's users [B] (same B on all ranks)."""
+        G, k = self.world, self.k
+        B = user_ids.numel()
+        if G == 1:
+            v, i = self.local_topk(user_ids)
+            return v, torch.where(i >= 0, i + self.item_offset, i)
+        all_ids = torch.empty(G * B, dtype=user_ids.dtype, device=user_ids.device)
+        dist.all_gather_into_tensor(all_ids, user_ids.contiguous(), group=self.group)
+        v, i = self.local_topk(all_ids)  # [G*B, k], shard-local ids
+        i = torch.where(i >= 0, i + self.item_offset, i)
+        rv = torch.empty(G * B * k, dtype=v.dtype, device=v.device)
+        ri = torch.empty(G * B * k, dtype=i.dtype, device=i.device)
+        dist.all_to_all_single(rv, v.contiguous().reshape(-1), group=self.group)
+        dist.all_to_all_single(ri, i.contiguous().reshape(-1), group=self.group)
+        return self.merge(rv.view(G, B, k), ri.view(G, B, k), k)
+
+
+# ------------------------------------------------------------------ HIP wiring
+def _pad(v, i, k):
+    """Keep k candidate columns on every rank (equal all_to_all splits) for tiny shards."""
+    if v.shape[1] == k:
+        return v, i
+    pv = torch.full((v.shape[0], k), float("-inf"), dtype=v.dtype, device=v.device)
+    pi = torch.full((v.shape[0], k), -1, dtype=i.dtype, device=i.device)
+    pv[:, : v.shape[1]] = v
+    pi[:, : v.shape[1]] = i
+    return pv, pi
+
+
+def hip_merge(cand_v: torch.Tensor, cand_i: torch.Tensor, k: int):
+    """[G, B, kc] candidates -> [B, k] via hnm_topk_merge_f32."""
+    G, B, kc = cand_v.shape
+    out_v = torch.empty(B, k, dtype=torch.float32, device=cand_v.device)
+    out_i = torch.empty(B, k, dtype=torch.int64, device=cand_v.device)
+    c = _lib.ctx(cand_v.device)
+    _lib.check(_lib.fn("hnm_topk_merge_f32")(c, _lib.ptr(cand_v), _lib.ptr(cand_i), B, G, B * kc,
+                                             kc, kc, k, _lib.ptr(out_v), _lib.ptr(out_i)),
+               "hnm_topk_merge_f32")
+    return out_v, out_i
+
+
+def ncf_shard_topk(model, lo: int, hi: int, k: int) -> LocalTopK:
+    """Fused NCF score + top-K over item rows [lo, hi) of `model` (a NeuralCF on a GPU)."""
+    def run(user_ids: torch.Tensor):
+        w, keep = model._weights()
+        mf, h0 = model.mf_dim, model.mlp_dims[0] // 2
+        w.gmf_item = w.gmf_item + lo * mf * 4
+        w.mlp_item = w.mlp_item + lo * h0 * 4
+        w.num_items = hi - lo
+        u = user_ids.to(torch.int64).contiguous()
+        kk = min(k, hi - lo)
+        out_v = torch.empty(u.numel(), kk, dtype=torch.float32, device=u.device)
+        out_i = torch.empty(u.numel(), kk, dtype=torch.int64, device=u.device)
+        c = _lib.ctx(u.device)
+        _lib.check(_lib.fn("hnm_ncf_topk_f32")(c, w, _lib.ptr(u), u.numel(), None, None, kk,
+                                               _lib.ptr(out_v), _lib.ptr(out_i)),
+                   "hnm_ncf_topk_f32")
+        return _pad(out_v, out_i, k)
+    return run
+
+
+def dot_shard_topk(user_tab: torch.Tensor, item_tab: torch.Tensor, lo: int, hi: int,
+                   k: int) -> LocalTopK:
+    """Fused dot score + top-K (LightGCN / MF without biases) over item rows [lo, hi)."""
+    shard = item_tab[lo:hi]
+
+    def run(user_ids: torch.Tensor):
+        u = user_ids.to(torch.int64).contiguous()
+        d = user_tab.shape[1]
+        kk = min(k, hi - lo)
+        out_v = torch.empty(u.numel(), kk, dtype=torch.float32, device=u.device)
+        out_i = torch.empty(u.numel(), kk, dtype=torch.int64, device=u.device)
+        c = _lib.ctx(u.device)
+        _lib.check(_lib.fn("hnm_dot_topk_f32")(c, _lib.ptr(user_tab), user_tab.shape[0],
+                                               user_tab.stride(0), _lib.ptr(u), u.numel(),
+                                               _lib.ptr(shard), hi - lo, shard.stride(0), d,
+                                               None, None, None, None, None, kk,
+                                               _lib.ptr(out_v), _lib.ptr(out_i)),
+                   "hnm_dot_topk_f32")
+        return _pad(out_v, out_i, k)
+    return run

@@ -56,6 +56,11 @@ hnm_status hnm_ctx_set_stream(hnm_ctx* ctx, void* hip_stream);
 hnm_status hnm_ctx_reserve(hnm_ctx* ctx, size_t bytes);   /* pre-grow workspace */
 hnm_status hnm_ctx_check(hnm_ctx* ctx);                   /* sync; HNM_EOOB if flagged */
 hnm_status hnm_ctx_num_cus(hnm_ctx* ctx, int* out);
+/* Dominant-kernel timer: while on, every scoring / SpMM call records HIP events on the ctx
+ * stream around its main kernel; hnm_ctx_timing() syncs, returns the summed kernel time
+ * and the number of timed launches, and resets.  (bench.py's live roofline figures.) */
+hnm_status hnm_ctx_enable_timing(hnm_ctx* ctx, int on);
+hnm_status hnm_ctx_timing(hnm_ctx* ctx, double* total_ms, int64_t* launches);
 
 /* ---- a1: embedding row gather ------------------------------------------------------
  * out[b, :d] = table[ids[b], :d].  Replaces nn.Embedding.__call__ at
