@@ -287,6 +287,7 @@ __global__ __launch_bounds__(256, 2) void ncf_score_kernel(
   __shared__ __attribute__((aligned(16))) float gs[2][TILE * GRS];
   __shared__ __attribute__((aligned(16))) float ps[NU * H1P];
   __shared__ __attribute__((aligned(16))) float ws[NU * GW];
+  __shared__ __attribute__((aligned(16))) float2 bw[32];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -319,13 +320,8 @@ __global__ __launch_bounds__(256, 2) void ncf_score_kernel(
     const int k = 2 * s + h;
     a[s] = (j < h2 && k < h1) ? W2[j * h1 + k] : 0.f;
   }
-  float b2r[16], wmr[16];
-#pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const int i = mfma32_row(r, h);
-    b2r[r] = i < h2 ? b2[i] : 0.f;
-    wmr[r] = i < h2 ? wm[i] : 0.f;
-  }
+  // (b2, wm) per hidden unit, read by the epilogue from LDS (keeps 32 VGPRs free)
+  if (tid < 32) bw[tid] = tid < h2 ? make_float2(b2[tid], wm[tid]) : make_float2(0.f, 0.f);
   const float bpv = bp[0];
 
   WaveTopK<1> L[WU];
@@ -393,7 +389,7 @@ __global__ __launch_bounds__(256, 2) void ncf_score_kernel(
 
     // 64-wide hidden layer: this lane's Q values stay in registers across the WU users;
     // the 128-wide variant re-reads them from LDS per user (register budget).
-    constexpr bool QREG = H1P <= 64;
+    constexpr bool QREG = false;  // q re-read per user pair (shared by both chains)
     float q[QREG ? KS : 1];
     const float* qrow = &qs[buf][j * QRS + h * KS];
     const float* grow = &gs[buf][j * GRS + h * MFH];
@@ -408,51 +404,90 @@ __global__ __launch_bounds__(256, 2) void ncf_score_kernel(
     const bool ivalid = (lane < 32) && item < part_end;
     const int64_t tile_end = std::min<int64_t>(base + TILE, part_end);
 
+    // Users are processed in pairs: two independent accumulator chains interleaved so
+    // each MFMA's accumulator dependency is two issues back, with the LDS reads of the
+    // next 4-step group issued before the current group's MFMAs.
 #pragma unroll
-    for (int u = 0; u < WU; ++u) {
-      const int ur = wave * WU + u;
-      const int64_t b = ublk + ur;
-      if (b >= B) break;
-      f32x16 acc = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-      const float* prow = &ps[ur * H1P + h * KS];
+    for (int up = 0; up < WU; up += 2) {
+      constexpr int dummy = 0;
+      (void)dummy;
+      const bool pair = (up + 1 < WU);  // compile-time after unrolling
+      const int urA = wave * WU + up;
+      const int urB = pair ? urA + 1 : urA;
+      const int64_t bA = ublk + urA, bB = ublk + urB;
+      if (bA >= B) break;
+      f32x16 accA = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      f32x16 accB = accA;
+      const float* prA = &ps[urA * H1P + h * KS];
+      const float* prB = &ps[urB * H1P + h * KS];
+      float4 pa = *reinterpret_cast<const float4*>(prA);
+      float4 pb = *reinterpret_cast<const float4*>(prB);
 #pragma unroll
       for (int s4 = 0; s4 < KS / 4; ++s4) {
-        const float4 pv = *reinterpret_cast<const float4*>(prow + 4 * s4);
+        float4 na = pa, nb = pb;
+        if (s4 + 1 < KS / 4) {
+          na = *reinterpret_cast<const float4*>(prA + 4 * (s4 + 1));
+          if (pair) nb = *reinterpret_cast<const float4*>(prB + 4 * (s4 + 1));
+        }
         float4 qv;
         if (QREG) qv = make_float4(q[4 * s4], q[4 * s4 + 1], q[4 * s4 + 2], q[4 * s4 + 3]);
         else qv = *reinterpret_cast<const float4*>(qrow + 4 * s4);
-        acc = mfma32x32x2(a[4 * s4 + 0], fmaxf(pv.x + qv.x, 0.f), acc);
-        acc = mfma32x32x2(a[4 * s4 + 1], fmaxf(pv.y + qv.y, 0.f), acc);
-        acc = mfma32x32x2(a[4 * s4 + 2], fmaxf(pv.z + qv.z, 0.f), acc);
-        acc = mfma32x32x2(a[4 * s4 + 3], fmaxf(pv.w + qv.w, 0.f), acc);
+        accA = mfma32x32x2(a[4 * s4 + 0], fmaxf(pa.x + qv.x, 0.f), accA);
+        if (pair) accB = mfma32x32x2(a[4 * s4 + 0], fmaxf(pb.x + qv.x, 0.f), accB);
+        accA = mfma32x32x2(a[4 * s4 + 1], fmaxf(pa.y + qv.y, 0.f), accA);
+        if (pair) accB = mfma32x32x2(a[4 * s4 + 1], fmaxf(pb.y + qv.y, 0.f), accB);
+        accA = mfma32x32x2(a[4 * s4 + 2], fmaxf(pa.z + qv.z, 0.f), accA);
+        if (pair) accB = mfma32x32x2(a[4 * s4 + 2], fmaxf(pb.z + qv.z, 0.f), accB);
+        accA = mfma32x32x2(a[4 * s4 + 3], fmaxf(pa.w + qv.w, 0.f), accA);
+        if (pair) accB = mfma32x32x2(a[4 * s4 + 3], fmaxf(pb.w + qv.w, 0.f), accB);
+        pa = na;
+        pb = nb;
       }
-      float gmf = 0.f;
-      const float* wrow = &ws[ur * GW + h * MFH];
+      // GMF term for both users with one pass over this lane's g_i half
+      float gmfA = 0.f, gmfB = 0.f;
+      const float* wA = &ws[urA * GW + h * MFH];
+      const float* wB = &ws[urB * GW + h * MFH];
 #pragma unroll
       for (int t4 = 0; t4 < MFH / 4; ++t4) {
-        const float4 wv = *reinterpret_cast<const float4*>(wrow + 4 * t4);
         const float4 gv = *reinterpret_cast<const float4*>(grow + 4 * t4);
-        gmf = fmaf(wv.x, gv.x, gmf);
-        gmf = fmaf(wv.y, gv.y, gmf);
-        gmf = fmaf(wv.z, gv.z, gmf);
-        gmf = fmaf(wv.w, gv.w, gmf);
-      }
-      float mlp = 0.f;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) mlp = fmaf(fmaxf(acc[r] + b2r[r], 0.f), wmr[r], mlp);
-      float tot = gmf + mlp;
-      tot += __shfl_xor(tot, 32);
-      float score = tot + bpv;
-
-      if (DENSE) {
-        if (ivalid) dense[b * ldo + item] = score;
-      } else {
-        while (nm[u] < tile_end) {  // wave-uniform mask cursor
-          if (item == nm[u]) score = -__builtin_inff();
-          ++mpos[u];
-          nm[u] = mpos[u] < mend[u] ? midx[mpos[u]] : INT_BIG;
+        const float4 xa = *reinterpret_cast<const float4*>(wA + 4 * t4);
+        gmfA = fmaf(xa.x, gv.x, gmfA);
+        gmfA = fmaf(xa.y, gv.y, gmfA);
+        gmfA = fmaf(xa.z, gv.z, gmfA);
+        gmfA = fmaf(xa.w, gv.w, gmfA);
+        if (pair) {
+          const float4 xb = *reinterpret_cast<const float4*>(wB + 4 * t4);
+          gmfB = fmaf(xb.x, gv.x, gmfB);
+          gmfB = fmaf(xb.y, gv.y, gmfB);
+          gmfB = fmaf(xb.z, gv.z, gmfB);
+          gmfB = fmaf(xb.w, gv.w, gmfB);
         }
-        L[u].offer(score, (int)item, ivalid, K);
+      }
+#pragma unroll
+      for (int side = 0; side < (pair ? 2 : 1); ++side) {
+        const int u = up + side;
+        const int64_t b = side ? bB : bA;
+        if (b >= B) break;
+        const f32x16& acc = side ? accB : accA;
+        float mlp = 0.f;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float2 c = bw[mfma32_row(r, h)];
+          mlp = fmaf(fmaxf(acc[r] + c.x, 0.f), c.y, mlp);
+        }
+        float tot = (side ? gmfB : gmfA) + mlp;
+        tot += __shfl_xor(tot, 32);
+        float score = tot + bpv;
+        if (DENSE) {
+          if (ivalid) dense[b * ldo + item] = score;
+        } else {
+          while (nm[u] < tile_end) {  // wave-uniform mask cursor
+            if (item == nm[u]) score = -__builtin_inff();
+            ++mpos[u];
+            nm[u] = mpos[u] < mend[u] ? midx[mpos[u]] : INT_BIG;
+          }
+          L[u].offer(score, (int)item, ivalid, K);
+        }
       }
     }
 
