@@ -5,6 +5,6 @@ as hand-written gfx950 HIP kernels behind the C ABI in include/hnm.h (libhnm_mi3
 exposed through modules that mirror the reference's `src/models` surface.
 """
 from .evaluation import RecommendationMetrics
-from .models import LightGCN, MatrixFactorization, NeuralCF
+from .models import LightGCN, MatrixFactorization, NeuralCF, WideDeep
 
-__all__ = ["NeuralCF", "LightGCN", "MatrixFactorization", "RecommendationMetrics"]
+__all__ = ["NeuralCF", "LightGCN", "WideDeep", "MatrixFactorization", "RecommendationMetrics"]

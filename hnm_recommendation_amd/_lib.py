@@ -32,11 +32,14 @@ class NcfWeights(C.Structure):
 
 class WideDeepWeights(C.Structure):
     """hnm_widedeep_weights (include/hnm.h)."""
-    _fields_ = [("deep_user", _p), ("deep_item", _p), ("wide_user", _p), ("wide_item", _p),
-                ("w1", _p), ("b1", _p), ("w2", _p), ("b2", _p), ("w3", _p), ("b3", _p),
-                ("wd", _p), ("bias", _p),
-                ("num_users", _i64), ("num_items", _i64), ("ld_user", _i64),
-                ("d", _i32), ("l1", _i32), ("l2", _i32), ("l3", _i32)]
+    _fields_ = [(n, _p) for n in (
+        "deep_user", "deep_item", "w1", "b1", "bn1_w", "bn1_b", "bn1_mean", "bn1_var",
+        "w2", "b2", "bn2_w", "bn2_b", "bn2_mean", "bn2_var",
+        "w3", "b3", "bn3_w", "bn3_b", "bn3_mean", "bn3_var",
+        "final_w", "final_b", "duf_w", "duf_b", "wuf_w", "wuf_b")] + [
+        ("num_users", _i64), ("num_items", _i64), ("deep_offset", _i64),
+        ("d", _i32), ("l1_in", _i32), ("l1", _i32), ("l2", _i32), ("l3", _i32),
+        ("num_user_features", _i32), ("eps", _f32)]
 
 
 _SIGS = {
@@ -71,8 +74,7 @@ _SIGS = {
     "hnm_axpby_f32": (_i32, [_p, _i64, _f32, _p, _f32, _p, _p]),
     "hnm_widedeep_topk_f32": (_i32, [_p, C.POINTER(WideDeepWeights), _p, _i64, _p, _p, _p,
                                      C.c_int, _p, _p]),
-    "hnm_widedeep_scores_f32": (_i32, [_p, C.POINTER(WideDeepWeights), _p, _i64, _p, _p,
-                                       _i64]),
+    "hnm_widedeep_scores_f32": (_i32, [_p, C.POINTER(WideDeepWeights), _p, _i64, _p, _p, _i64]),
     "hnm_widedeep_pair_scores_f32": (_i32, [_p, C.POINTER(WideDeepWeights), _p, _p, _p, _i64,
                                             _p]),
 }

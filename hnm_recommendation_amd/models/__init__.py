@@ -2,5 +2,6 @@
 from .lightgcn import LightGCN
 from .matrix_factorization import MatrixFactorization
 from .neural_cf import NeuralCF
+from .wide_deep import WideDeep
 
-__all__ = ["NeuralCF", "LightGCN", "MatrixFactorization"]
+__all__ = ["NeuralCF", "LightGCN", "WideDeep", "MatrixFactorization"]

@@ -143,6 +143,65 @@ hnm_status hnm_ncf_pair_scores_f32(hnm_ctx* ctx, const hnm_ncf_weights* w,
                                    const int64_t* user_ids, const int64_t* item_ids,
                                    int64_t n, float* out);
 
+/* ---- a9 + a10: Wide&Deep ------------------------------------------------------------
+ * Reference layout (wide_deep.py:92-134): deep tower Linear -> ReLU -> BatchNorm1d (eval:
+ * running stats, eps) per layer; final_layer over [wide (one-hot u, one-hot i, wide user
+ * features) ; deep].  wide_user/item_embedding are unused by the reference forward.
+ *   s = final_w[u] + final_w[U + i] (+ wide_user_features(f_u) . final_w[U+I : U+I+F])
+ *       + final_w[deep_offset:] . deep(u, i) + final_b
+ * Towers of 2 (w3 == NULL, l3 == 0) or 3 layers, widths <= 512 / 256 / 128; deep input
+ * [e_u; e_i] (+ deep_user_features(f_u) when num_user_features > 0). */
+typedef struct {
+  const float* deep_user;  /* [num_users, d] */
+  const float* deep_item;  /* [num_items, d] */
+  const float* w1;         /* [l1, l1_in]  deep_network.0 */
+  const float* b1;
+  const float* bn1_w;      /* deep_network.2 weight / bias / running_mean / running_var */
+  const float* bn1_b;
+  const float* bn1_mean;
+  const float* bn1_var;
+  const float* w2;         /* [l2, l1]  deep_network.4 */
+  const float* b2;
+  const float* bn2_w;
+  const float* bn2_b;
+  const float* bn2_mean;
+  const float* bn2_var;
+  const float* w3;         /* [l3, l2]  deep_network.8 (NULL for a two-layer tower) */
+  const float* b3;
+  const float* bn3_w;
+  const float* bn3_b;
+  const float* bn3_mean;
+  const float* bn3_var;
+  const float* final_w;    /* [deep_offset + last width]  final_layer.weight[0] */
+  const float* final_b;    /* [1] */
+  const float* duf_w;      /* [d, F] deep_user_features or NULL */
+  const float* duf_b;
+  const float* wuf_w;      /* [F, F] wide_user_features or NULL */
+  const float* wuf_b;
+  int64_t num_users;
+  int64_t num_items;
+  int64_t deep_offset;     /* wide width: U + I (+ user/item feature widths) */
+  int32_t d;
+  int32_t l1_in;
+  int32_t l1;
+  int32_t l2;
+  int32_t l3;
+  int32_t num_user_features;
+  float eps;
+} hnm_widedeep_weights;
+
+hnm_status hnm_widedeep_topk_f32(hnm_ctx* ctx, const hnm_widedeep_weights* w,
+                                 const int64_t* user_ids, int64_t B, const float* user_features,
+                                 const int64_t* mask_ptr, const int32_t* mask_idx, int k,
+                                 float* out_val, int64_t* out_idx);
+hnm_status hnm_widedeep_scores_f32(hnm_ctx* ctx, const hnm_widedeep_weights* w,
+                                   const int64_t* user_ids, int64_t B, const float* user_features,
+                                   float* out, int64_t ldo);
+/* WideDeep.forward(user_ids, item_ids, user_features) (wide_deep.py:157-230): out[n]. */
+hnm_status hnm_widedeep_pair_scores_f32(hnm_ctx* ctx, const hnm_widedeep_weights* w,
+                                        const int64_t* user_ids, const int64_t* item_ids,
+                                        const float* user_features, int64_t n, float* out);
+
 /* ---- top-K merge (item partitions, item shards across GPUs) ------------------------
  * Candidates of row b: for g < G: cand[g*gstride + b*bstride + j], j < kc (value, global
  * item index; index < 0 = empty).  out: the best k of them per row, sorted. */

@@ -8,7 +8,8 @@ import pytest
 import torch
 
 from parity import load_golden
-from hnm_recommendation_amd import LightGCN, MatrixFactorization, NeuralCF, RecommendationMetrics
+from hnm_recommendation_amd import (LightGCN, MatrixFactorization, NeuralCF,
+                                    RecommendationMetrics, WideDeep)
 from hnm_recommendation_amd import _lib
 from hnm_recommendation_amd.models.base import filter_csr
 
@@ -36,6 +37,9 @@ def test_library_exports_every_declared_symbol():
     (LightGCN, "lightgcn_d64.npz", {}),
     (LightGCN, "lightgcn_d128.npz", {"embedding_dim": 128}),
     (MatrixFactorization, "mf_small.npz", {"sparse": False}),
+    (WideDeep, "widedeep_small.npz", {}),
+    (WideDeep, "widedeep_feat.npz", {"num_user_features": 10, "embedding_dim": 16,
+                                      "deep_layers": [64, 32]}),
 ])
 def test_state_dict_keys_match_reference(cls, golden, kw):
     g = load_golden(golden)

@@ -12,7 +12,7 @@ import torch
 from parity import (assert_scores_close, assert_topk_equivalent, filter_from_arrays,
                     load_golden, same_topk_sets)
 from oracle import hnm_oracle as O
-from hnm_recommendation_amd import LightGCN, MatrixFactorization, NeuralCF
+from hnm_recommendation_amd import LightGCN, MatrixFactorization, NeuralCF, WideDeep
 from hnm_recommendation_amd import synthetic as syn
 
 pytestmark = pytest.mark.gpu
@@ -224,3 +224,53 @@ def test_mf_golden():
     f = filter_from_arrays(g["filter_keys"], g["filter_ptr"], g["filter_idx"])
     masked = O.apply_filter(g["dense"], g["user_ids"], f)
     assert_topk_equivalent(m.recommend(users, filter_items=f).cpu().numpy(), masked, int(g["K"]))
+
+
+# ------------------------------------------------------------------ Wide&Deep
+def test_widedeep_golden():
+    g = load_golden("widedeep_small.npz")
+    m = to_module(WideDeep(int(g["U"]), int(g["I"]), embedding_dim=64, deep_layers=[512, 256, 128],
+                           top_k=int(g["K"])), g["sd"])
+    users = t(g["user_ids"])
+    assert_scores_close(m.predict_all_items(users).cpu().numpy(), g["dense"], "wd dense")
+    assert_topk_equivalent(m.recommend(users).cpu().numpy(), g["dense"], int(g["K"]))
+    f = filter_from_arrays(g["filter_keys"], g["filter_ptr"], g["filter_idx"])
+    masked = O.apply_filter(g["dense"], g["user_ids"], f)
+    assert_topk_equivalent(m.recommend(users, filter_items=f).cpu().numpy(), masked, int(g["K"]))
+    pair = m(t(g["pair_users"]), t(g["pair_items"])).cpu().numpy()
+    assert_scores_close(pair, g["pair_scores"], "wd pair")
+
+
+def test_widedeep_user_features_golden():
+    g = load_golden("widedeep_feat.npz")
+    m = to_module(WideDeep(int(g["U"]), int(g["I"]), num_user_features=int(g["F"]), embedding_dim=16,
+                           deep_layers=[64, 32], top_k=int(g["K"])), g["sd"])
+    users = t(g["user_ids"])
+    feats = t(g["user_features"])
+    assert_scores_close(m.predict_all_items(users, feats).cpu().numpy(), g["dense"], "wd feat dense")
+    assert_topk_equivalent(m.recommend(users, feats).cpu().numpy(), g["dense"], int(g["K"]))
+    pair = m(users[:8], t(np.arange(8)), feats[:8]).cpu().numpy()
+    assert_scores_close(pair, g["dense"][np.arange(8), np.arange(8)], "wd feat pair")
+
+
+@pytest.mark.parametrize("layers", [[512, 256, 128], [128, 64, 32], [64, 32]])
+def test_widedeep_vs_oracle(layers):
+    U, I = 500, 1111
+    sd = syn.widedeep_state_dict(U, I, 64, tuple(layers), seed=5, bias_scale=0.05,
+                                 randomize_bn=True, emb_scale=10.0)
+    m = to_module(WideDeep(U, I, embedding_dim=64, deep_layers=layers), sd)
+    users = syn.user_batch(U, 70, seed=6)
+    ref = O.widedeep_predict_all_items(sd, users)
+    assert_scores_close(m.predict_all_items(t(users)).cpu().numpy(), ref, f"wd {layers}")
+    assert_topk_equivalent(m.recommend(t(users)).cpu().numpy(), ref, 12)
+
+
+def test_widedeep_full_shape_rows():
+    """configs[3]: full H&M shape; a few users against the oracle (users x all items)."""
+    U, I = syn.HM_USERS, syn.HM_ITEMS
+    sd = syn.widedeep_state_dict(U, I, 64, (512, 256, 128), seed=0)
+    m = to_module(WideDeep(U, I), sd)
+    users = syn.user_batch(U, 8, seed=1)
+    vals, rec = m.recommend_with_scores(t(users))
+    ref = O.widedeep_predict_all_items(sd, users[:2])
+    assert_topk_equivalent(rec.cpu().numpy()[:2], ref, 12, what="wd full")

@@ -1,0 +1,90 @@
+"""World-size-2 gloo test (CPU) of the item-sharded recommend path's host logic:
+shard ranges, all_gather of user ids, global index offsets, all_to_all layout and the
+(score desc, item asc) merge.  The per-shard scorer and the merge are the oracle here
+(the product wires the HIP kernels, covered by the GPU tests); the result must equal the
+single-process top-k over all items exactly."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from oracle import hnm_oracle as O
+from hnm_recommendation_amd import sharding as S
+from hnm_recommendation_amd import synthetic as syn
+
+U, I, B, K = 300, 257, 16, 12
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _np_merge(cv, ci, k):
+    G, Bn, kc = cv.shape
+    v = cv.permute(1, 0, 2).reshape(Bn, G * kc).numpy().astype(np.float64)
+    i = ci.permute(1, 0, 2).reshape(Bn, G * kc).numpy()
+    out_v = np.empty((Bn, k), np.float32)
+    out_i = np.empty((Bn, k), np.int64)
+    for b in range(Bn):
+        order = sorted(range(G * kc), key=lambda q: (-v[b, q], i[b, q]))[:k]
+        out_v[b] = v[b, order]
+        out_i[b] = i[b, order]
+    return torch.from_numpy(out_v), torch.from_numpy(out_i)
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    sd = syn.ncf_state_dict(U, I, 64, (128, 64, 32), seed=0, bias_scale=0.05, emb_scale=20.0)
+    lo, hi = S.shard_range(I, rank, world)
+
+    def local_topk(all_ids):
+        ids = all_ids.numpy()
+        sub = dict(sd)
+        sub["gmf_item_embedding.weight"] = sd["gmf_item_embedding.weight"][lo:hi]
+        sub["mlp_item_embedding.weight"] = sd["mlp_item_embedding.weight"][lo:hi]
+        scores = O.ncf_predict_all_items(sub, ids)
+        v, i = O.topk(scores, K)
+        return torch.from_numpy(v.astype(np.float32)), torch.from_numpy(i)
+
+    rec = S.ItemShardedRecommender(local_topk, _np_merge, K, lo, rank, world)
+    users = torch.from_numpy(syn.user_batch(U, B, seed=10 + rank))
+    v, i = rec.recommend(users)
+    q.put((rank, users.numpy(), v.numpy(), i.numpy()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2])
+def test_item_sharded_recommend_matches_single_process(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = [q.get(timeout=300) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    sd = syn.ncf_state_dict(U, I, 64, (128, 64, 32), seed=0, bias_scale=0.05, emb_scale=20.0)
+    for rank, users, v, i in results:
+        full = O.ncf_predict_all_items(sd, users)
+        rv, ri = O.topk(full, K)
+        assert np.array_equal(i, ri), f"rank {rank}"
+        np.testing.assert_array_equal(v, rv.astype(np.float32))
+
+
+def test_shard_ranges_cover_items():
+    for G in (1, 2, 3, 8):
+        r = [S.shard_range(105542, g, G) for g in range(G)]
+        assert r[0][0] == 0 and r[-1][1] == 105542
+        assert all(a[1] == b[0] for a, b in zip(r, r[1:]))
