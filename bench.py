@@ -37,7 +37,7 @@ import torch.distributed as dist
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
-from hnm_recommendation_amd import LightGCN, MatrixFactorization, NeuralCF  # noqa: E402
+from hnm_recommendation_amd import LightGCN, MatrixFactorization, NeuralCF, WideDeep  # noqa: E402
 from hnm_recommendation_amd import _lib  # noqa: E402
 from hnm_recommendation_amd import sharding as S  # noqa: E402
 from hnm_recommendation_amd import synthetic as syn  # noqa: E402
@@ -79,7 +79,7 @@ def build_workload(name, rank, world, device, batch):
         local = S.ncf_shard_topk(m, lo, hi, K)
         per_launch = 4352.0 * batch * world * (hi - lo)   # 4,352 FLOP / pair
         info = {"model": "NeuralCF", "mf_dim": 64, "mlp_dims": [128, 64, 32]}
-        bound, kernel = "mfma", "ncf_score_kernel"
+        bound, kernel = "mfma", "ncf32_kernel"
         cpu = ("ncf", sd)
     elif name in ("lightgcn", "lightgcn128"):
         d = 64 if name == "lightgcn" else 128
@@ -95,6 +95,14 @@ def build_workload(name, rank, world, device, batch):
         bound, kernel = "mfma", "dot_score_kernel"
         cpu = None
         info["_model"] = m
+    elif name == "widedeep":
+        sd = syn.widedeep_state_dict(U, I, 64, (512, 256, 128), seed=0)
+        m = load(WideDeep(U, I), sd, device)
+        local = S.widedeep_shard_topk(m, lo, hi, K)
+        per_launch = 328450.0 * batch * world * (hi - lo)   # 328,450 FLOP / pair
+        info = {"model": "WideDeep", "embedding_dim": 64, "deep_layers": [512, 256, 128]}
+        bound, kernel = "mfma", "widedeep_score_kernel"
+        cpu = None
     elif name == "mf":
         sd = syn.mf_state_dict(U, I, 64, seed=0)
         m = load(MatrixFactorization(U, I, sparse=False), sd, device)

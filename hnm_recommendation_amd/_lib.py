@@ -36,8 +36,9 @@ class WideDeepWeights(C.Structure):
         "deep_user", "deep_item", "w1", "b1", "bn1_w", "bn1_b", "bn1_mean", "bn1_var",
         "w2", "b2", "bn2_w", "bn2_b", "bn2_mean", "bn2_var",
         "w3", "b3", "bn3_w", "bn3_b", "bn3_mean", "bn3_var",
-        "final_w", "final_b", "duf_w", "duf_b", "wuf_w", "wuf_b")] + [
-        ("num_users", _i64), ("num_items", _i64), ("deep_offset", _i64),
+        "wide_user", "wide_item", "wide_feat", "final_deep", "final_b",
+        "duf_w", "duf_b", "wuf_w", "wuf_b")] + [
+        ("num_users", _i64), ("num_items", _i64),
         ("d", _i32), ("l1_in", _i32), ("l1", _i32), ("l2", _i32), ("l3", _i32),
         ("num_user_features", _i32), ("eps", _f32)]
 

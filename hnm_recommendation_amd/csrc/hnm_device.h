@@ -123,6 +123,42 @@ __device__ __forceinline__ f32x16 mfma32x32x2(float a, float b, f32x16 c) {
 }
 __device__ __forceinline__ int mfma32_row(int r, int half) { return (r & 3) + 8 * (r >> 2) + 4 * half; }
 
+// x(lane) + x(lane ^ 32) without LDS: one v_permlane32_swap (VALU) instead of a
+// ds_bpermute round trip.
+__device__ __forceinline__ float hnm_sum_halves(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false,
+                                                  false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
+#define TILE 32
+#define INT_BIG 0x7fffffff
+
+// Insert (cv, ci) into a single-register wave list (slot s in lane s, K <= 64).
+__device__ __forceinline__ void list1_insert(float& lv, int& li, float cv, int ci, int K) {
+  const float tv = hnm_readlane_f(lv, K - 1);
+  const int ti = hnm_readlane_i(li, K - 1);
+  if (!hnm_better(cv, ci, tv, ti)) return;
+  const int lane = hnm_lane();
+  const bool b = (lane < K) && hnm_better(lv, li, cv, ci);
+  const int pos = __popcll(__ballot(b));
+  const float up = __shfl_up(lv, 1);
+  const int upi = __shfl_up(li, 1);
+  lv = lane > pos ? up : (lane == pos ? cv : lv);
+  li = lane > pos ? upi : (lane == pos ? ci : li);
+}
+
+// First masked item >= start in the sorted row [lo, hi) of midx.
+__device__ __forceinline__ int64_t mask_lower_bound(const int32_t* midx, int64_t lo, int64_t hi,
+                                                    int start) {
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (midx[mid] < start) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
+
 // Error word in device memory (ctx-owned): bit 0 = an id out of range was seen.
 #define HNM_ERR_OOB 1u
 __device__ __forceinline__ void hnm_flag(unsigned* err, unsigned bit) {

@@ -91,7 +91,7 @@ __global__ void wd_prep_bias(hnm_widedeep_weights w, WdPrep p) {
   const float* lb = p.OB > 0 ? w.bn3_b : w.bn2_b;
   const float* lm = p.OB > 0 ? w.bn3_mean : w.bn2_mean;
   const float* lv = p.OB > 0 ? w.bn3_var : w.bn2_var;
-  const float* wd = w.final_w + w.deep_offset;
+  const float* wd = w.final_deep;
   for (int o = t; o < p.RB2 * 32; o += gridDim.x * 256) {
     float v = 0.f;
     if (o < w.l2) {
@@ -132,9 +132,9 @@ __global__ void wd_user_const(hnm_widedeep_weights w, const int64_t* __restrict_
   if (b >= B) return;
   const int64_t u = ids[b];
   float v = bias[0];
-  if (u >= 0 && u < w.num_users) v += w.final_w[u];
+  if (u >= 0 && u < w.num_users) v += w.wide_user[u];
   if (wuf) {
-    const float* wf = w.final_w + w.num_users + w.num_items;
+    const float* wf = w.wide_feat;
     for (int f = 0; f < w.num_user_features; ++f) v = fmaf(wuf[b * w.num_user_features + f], wf[f], v);
   }
   cu[b] = v;
@@ -369,7 +369,7 @@ __global__ __launch_bounds__(256) void widedeep_pair_kernel(
     in = widths[l];
     __syncthreads();
   }
-  const float* wd = w.final_w + w.deep_offset;
+  const float* wd = w.final_deep;
   float s = 0.f;
   for (int o = t; o < in; o += 256) s = fmaf(wd[o], cur[o], s);
   red[t] = s;
@@ -379,7 +379,7 @@ __global__ __launch_bounds__(256) void widedeep_pair_kernel(
     __syncthreads();
   }
   if (t == 0) {
-    float v = red[0] + w.final_w[u] + w.final_w[w.num_users + i] + w.final_b[0];
+    float v = red[0] + w.wide_user[u] + w.wide_item[i] + w.final_b[0];
     if (wide_extra) v += wide_extra[e];
     out[e] = v;
   }
@@ -388,7 +388,8 @@ __global__ __launch_bounds__(256) void widedeep_pair_kernel(
 // ------------------------------------------------------------------ host side
 static hnm_status wd_check(const hnm_widedeep_weights* w) {
   HNM_REQUIRE(w && w->deep_user && w->deep_item && w->w1 && w->b1 && w->w2 && w->b2 &&
-                  w->final_w && w->final_b && w->bn1_w && w->bn2_w,
+                  w->wide_user && w->wide_item && w->final_deep && w->final_b && w->bn1_w &&
+                  w->bn2_w,
               HNM_EINVAL, "widedeep: NULL weight pointer");
   HNM_REQUIRE(w->num_users > 0 && w->num_items > 0 && w->num_items < WD_INT_BIG, HNM_EINVAL,
               "widedeep: bad table sizes");
@@ -515,7 +516,7 @@ static hnm_status wd_common(hnm_ctx* ctx, const hnm_widedeep_weights* w, const i
                              w->d, Xf, w->d, 0);
     if (st) return st;
     // wide user features Linear(F, F)
-    if (w->wuf_w) {
+    if (w->wuf_w && w->wide_feat) {
       st = hnm_linear_rows_f32(ctx, ufeat, w->num_user_features, nullptr, B, B,
                                w->num_user_features, w->wuf_w, w->num_user_features, w->wuf_b,
                                w->num_user_features, WFu, w->num_user_features, 0);
@@ -538,7 +539,7 @@ static hnm_status wd_common(hnm_ctx* ctx, const hnm_widedeep_weights* w, const i
 
   const size_t lds = (size_t)(WD_TILE * (K1P + 4) + 4 * K1P + (pr.RB2 + pr.OB + nlast) * 32) * 4;
   dim3 grid((unsigned)ublocks, (unsigned)np);
-  const float* wI = w->final_w + w->num_users;
+  const float* wI = w->wide_item;
   hnm_timer_begin(ctx);
 #define WD_CASE(R, O)                                                                     \
   if (pr.RB2 == R && pr.OB == O)                                                          \
@@ -604,13 +605,12 @@ extern "C" hnm_status hnm_widedeep_pair_scores_f32(hnm_ctx* ctx, const hnm_wided
     st = hnm_linear_rows_f32(ctx, user_features, F, nullptr, n, n, F, w->duf_w, F, w->duf_b,
                              w->d, xu, w->d, 0);
     if (st) return st;
-    if (w->wuf_w) {
+    if (w->wuf_w && w->wide_feat) {
       st = hnm_linear_rows_f32(ctx, user_features, F, nullptr, n, n, F, w->wuf_w, F, w->wuf_b, F,
                                wf, F, 0);
       if (st) return st;
       // wide feature term = wf . final_w[U + I : U + I + F]
-      st = hnm_linear_rows_f32(ctx, wf, F, nullptr, n, n, F,
-                               w->final_w + w->num_users + w->num_items, F, nullptr, 1, wide, 1, 0);
+      st = hnm_linear_rows_f32(ctx, wf, F, nullptr, n, n, F, w->wide_feat, F, nullptr, 1, wide, 1, 0);
       if (st) return st;
     } else {
       wide = nullptr;

@@ -131,6 +131,8 @@ class WideDeep(RecModule):
 
         has3 = len(lin) == 3
         none4 = [None] * 4
+        U, I = self.num_users, self.num_items
+        fw = t(self.final_layer.weight.reshape(-1))  # [wide_dim + last]
         duf = getattr(self, "deep_user_features", None)
         wuf = getattr(self, "wide_user_features", None) if self.use_wide_features else None
         ptrs = [t(self.deep_user_embedding.weight), t(self.deep_item_embedding.weight),
@@ -138,13 +140,13 @@ class WideDeep(RecModule):
                 t(lin[1].weight), t(lin[1].bias), *bn(bns[1]),
                 t(lin[2].weight) if has3 else None, t(lin[2].bias) if has3 else None,
                 *(bn(bns[2]) if has3 else none4),
-                t(self.final_layer.weight.reshape(-1)), t(self.final_layer.bias),
+                fw, fw + 4 * U, (fw + 4 * (U + I)) if wuf is not None else None,
+                fw + 4 * self._calculate_wide_dim(), t(self.final_layer.bias),
                 t(duf.weight) if duf is not None else None, t(duf.bias) if duf is not None else None,
                 t(wuf.weight) if wuf is not None else None, t(wuf.bias) if wuf is not None else None]
         _lib.require_gpu(*keep)
         d = self.embedding_dim
-        deep_offset = self._calculate_wide_dim()
-        w = _lib.WideDeepWeights(*ptrs, self.num_users, self.num_items, deep_offset, d,
+        w = _lib.WideDeepWeights(*ptrs, self.num_users, self.num_items, d,
                                  lin[0].in_features, lin[0].out_features, lin[1].out_features,
                                  lin[2].out_features if has3 else 0, self.num_user_features,
                                  float(bns[0].eps))

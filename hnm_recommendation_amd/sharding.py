@@ -129,3 +129,23 @@ def dot_shard_topk(user_tab: torch.Tensor, item_tab: torch.Tensor, lo: int, hi: 
                    "hnm_dot_topk_f32")
         return _pad(out_v, out_i, k)
     return run
+
+
+def widedeep_shard_topk(model, lo: int, hi: int, k: int) -> LocalTopK:
+    """Fused Wide&Deep score + top-K over item rows [lo, hi) of `model` (a WideDeep on a GPU)."""
+    def run(user_ids: torch.Tensor):
+        w, keep = model._weights()
+        d = model.embedding_dim
+        w.deep_item = w.deep_item + lo * d * 4
+        w.wide_item = w.wide_item + lo * 4
+        w.num_items = hi - lo
+        u = user_ids.to(torch.int64).contiguous()
+        kk = min(k, hi - lo)
+        out_v = torch.empty(u.numel(), kk, dtype=torch.float32, device=u.device)
+        out_i = torch.empty(u.numel(), kk, dtype=torch.int64, device=u.device)
+        c = _lib.ctx(u.device)
+        _lib.check(_lib.fn("hnm_widedeep_topk_f32")(c, w, _lib.ptr(u), u.numel(), None, None,
+                                                    None, kk, _lib.ptr(out_v), _lib.ptr(out_i)),
+                   "hnm_widedeep_topk_f32")
+        return _pad(out_v, out_i, k)
+    return run

@@ -147,8 +147,10 @@ hnm_status hnm_ncf_pair_scores_f32(hnm_ctx* ctx, const hnm_ncf_weights* w,
  * Reference layout (wide_deep.py:92-134): deep tower Linear -> ReLU -> BatchNorm1d (eval:
  * running stats, eps) per layer; final_layer over [wide (one-hot u, one-hot i, wide user
  * features) ; deep].  wide_user/item_embedding are unused by the reference forward.
- *   s = final_w[u] + final_w[U + i] (+ wide_user_features(f_u) . final_w[U+I : U+I+F])
- *       + final_w[deep_offset:] . deep(u, i) + final_b
+ *   s = wide_user[u] + wide_item[i] (+ wide_user_features(f_u) . wide_feat)
+ *       + final_deep . deep(u, i) + final_b
+ * where wide_user / wide_item / wide_feat / final_deep are the segments [0, U), [U, U+I),
+ * [U+I, U+I+F) and [wide_dim, ...) of final_layer.weight[0] (item rows may be a shard).
  * Towers of 2 (w3 == NULL, l3 == 0) or 3 layers, widths <= 512 / 256 / 128; deep input
  * [e_u; e_i] (+ deep_user_features(f_u) when num_user_features > 0). */
 typedef struct {
@@ -172,7 +174,10 @@ typedef struct {
   const float* bn3_b;
   const float* bn3_mean;
   const float* bn3_var;
-  const float* final_w;    /* [deep_offset + last width]  final_layer.weight[0] */
+  const float* wide_user;  /* final_layer.weight[0, 0:U] */
+  const float* wide_item;  /* final_layer.weight[0, U:U+I] */
+  const float* wide_feat;  /* final_layer.weight[0, U+I:U+I+F] or NULL */
+  const float* final_deep; /* final_layer.weight[0, wide_dim:] (last hidden width) */
   const float* final_b;    /* [1] */
   const float* duf_w;      /* [d, F] deep_user_features or NULL */
   const float* duf_b;
@@ -180,7 +185,6 @@ typedef struct {
   const float* wuf_b;
   int64_t num_users;
   int64_t num_items;
-  int64_t deep_offset;     /* wide width: U + I (+ user/item feature widths) */
   int32_t d;
   int32_t l1_in;
   int32_t l1;
