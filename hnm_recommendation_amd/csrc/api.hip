@@ -310,15 +310,19 @@ extern "C" hnm_status hnm_axpby_f32(hnm_ctx* ctx, int64_t n, float alpha, const 
 
 // ------------------------------------------------------------------ top-K merge
 // One wave per row: candidates stream through the wave list 64 at a time.
+// rows/nrows (optional): candidate row b is output row rows[b], for b < *nrows.
 template <int NS, typename IdxT>
 __global__ __launch_bounds__(256) void topk_merge_kernel(const float* __restrict__ cv,
                                                          const IdxT* __restrict__ ci, int64_t B,
                                                          int64_t G, int64_t gstride,
                                                          int64_t bstride, int kc, int k,
                                                          float* __restrict__ ov,
-                                                         int64_t* __restrict__ oi) {
+                                                         int64_t* __restrict__ oi,
+                                                         const int32_t* __restrict__ rows,
+                                                         const int32_t* __restrict__ nrows) {
   const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (b >= B) return;
+  if (b >= (nrows ? (int64_t)*nrows : B)) return;
+  const int64_t ob = rows ? (int64_t)rows[b] : b;
   const int lane = threadIdx.x & 63;
   WaveTopK<NS> L;
   L.init();
@@ -340,20 +344,21 @@ __global__ __launch_bounds__(256) void topk_merge_kernel(const float* __restrict
     }
     L.offer(v, idx, ok, k);
   }
-  L.store(ov ? ov + b * k : nullptr, oi + b * k, k);
+  L.store(ov ? ov + ob * k : nullptr, oi + ob * k, k);
 }
 
 template <typename IdxT>
 hnm_status launch_merge(hnm_ctx* ctx, const float* cv, const IdxT* ci, int64_t B, int64_t G,
                         int64_t gstride, int64_t bstride, int kc, int k, float* ov,
-                        int64_t* oi) {
+                        int64_t* oi, const int32_t* rows = nullptr,
+                        const int32_t* nrows = nullptr) {
   dim3 grid((unsigned)hnm_cdiv(B, 4));
   if (k <= 64)
     hipLaunchKernelGGL((topk_merge_kernel<1, IdxT>), grid, dim3(256), 0, ctx->stream, cv, ci,
-                       B, G, gstride, bstride, kc, k, ov, oi);
+                       B, G, gstride, bstride, kc, k, ov, oi, rows, nrows);
   else
     hipLaunchKernelGGL((topk_merge_kernel<2, IdxT>), grid, dim3(256), 0, ctx->stream, cv, ci,
-                       B, G, gstride, bstride, kc, k, ov, oi);
+                       B, G, gstride, bstride, kc, k, ov, oi, rows, nrows);
   HNM_LAUNCH_CHECK();
   return HNM_OK;
 }
@@ -362,6 +367,13 @@ hnm_status hnm_topk_merge_i32(hnm_ctx* ctx, const float* cv, const int32_t* ci, 
                               int64_t G, int64_t gstride, int64_t bstride, int kc, int k,
                               float* ov, int64_t* oi) {
   return launch_merge<int32_t>(ctx, cv, ci, B, G, gstride, bstride, kc, k, ov, oi);
+}
+
+hnm_status hnm_topk_merge_rows(hnm_ctx* ctx, const float* cv, const int32_t* ci, int64_t B,
+                               int64_t G, int64_t gstride, int64_t bstride, int kc, int k,
+                               float* ov, int64_t* oi, const int32_t* rows,
+                               const int32_t* nrows) {
+  return launch_merge<int32_t>(ctx, cv, ci, B, G, gstride, bstride, kc, k, ov, oi, rows, nrows);
 }
 
 extern "C" hnm_status hnm_topk_merge_f32(hnm_ctx* ctx, const float* cand_val,

@@ -7,12 +7,18 @@
 //   a1 gather is fused).  32-item tiles are staged in LDS (shared by the 4 waves),
 //   permuted into lane-half order so each lane reads its B operand with ds_read_b128.
 //   v_mfma_f32_32x32x2_f32 = exact fp32 fma chain (no bf16 shortcut).  C[user][item]
-//   rows stay in registers; a 32-list wave top-K (one list per user) with per-lane
-//   threshold registers pre-filters every score with one compare.
+//   rows stay in registers.
 //
-// The kernel covers one item PARTITION per blockIdx.y; partial top-K lists go to a
-// [B, NP, K] candidate buffer merged by topk_merge_kernel (total order: score desc,
-// item asc, so the merged result is unique).  The NeuralCF kernels live in ncf.hip.
+// Top-K (total order: score desc, item asc -- unique, so partitions/shards merge exactly):
+//   THRESH (large item sets): a LIST pass over a strided ~4k-item sample gives every user
+//     tau_u = its K-th best sample score, a lower bound of its true K-th best (same fp32
+//     arithmetic in both passes).  The main pass appends only scores >= tau_u to a per-user
+//     buffer (one compare per score; ~K*I/S appends per user); thresh_select takes the
+//     exact top-K of the buffer.  Users whose buffer overflows (degenerate / adversarial
+//     scores) are re-run on device through the LIST path -- results are always exact.
+//   LIST: per item partition, a 32-list wave top-K (one list per user) with per-lane
+//     threshold registers; partial lists are merged by topk_merge_kernel.
+// The NeuralCF kernels live in ncf.hip.
 #include <algorithm>
 
 #include "hnm_device.h"
@@ -24,15 +30,40 @@ hnm_status hnm_topk_merge_i32(hnm_ctx* ctx, const float* cv, const int32_t* ci, 
 
 
 // ------------------------------------------------------------------ dot kernel
-template <int DP, bool DENSE, bool BIAS>
-__global__ __launch_bounds__(256, 2) void dot_score_kernel(
-    const float* __restrict__ ut, int64_t num_users, int64_t ldu,
-    const int64_t* __restrict__ uids, int64_t B, const float* __restrict__ it, int64_t I,
-    int64_t ldi, int d, const float* __restrict__ ubias, const float* __restrict__ ibias,
-    const float* __restrict__ cbias, int64_t ipp, const int64_t* __restrict__ mptr,
-    const int32_t* __restrict__ midx, int K, float* __restrict__ cand_v,
-    int32_t* __restrict__ cand_i, int NP, float* __restrict__ dense, int64_t ldo,
-    unsigned* err) {
+enum { DOT_LIST = 0, DOT_DENSE = 1, DOT_THRESH = 2 };
+
+struct DotArgs {
+  const float* ut;         // user table [U, ldu]
+  int64_t num_users, ldu;
+  const int64_t* uids;     // [B] user ids of the request rows
+  int64_t B;
+  const float* it;         // item table; item i is row i * istride
+  int64_t I, ldi, istride;
+  int d;
+  const float *ubias, *ibias, *cbias;
+  int64_t ipp;             // items per partition (blockIdx.y)
+  const int64_t* mptr;     // CSR mask over request rows (real item ids)
+  const int32_t* midx;
+  int K;
+  float* cand_v;           // LIST: [launch rows, NP, K]
+  int32_t* cand_i;
+  int NP;
+  float* dense;            // DENSE: [B, ldo]
+  int64_t ldo;
+  const float* tau;        // THRESH: tau of request row r at tau[r * tau_ld]
+  int64_t tau_ld;
+  int* cnt;                // THRESH: [B] append counters
+  float* buf_v;            // THRESH: [B, cap]
+  int32_t* buf_i;
+  int cap;
+  const int32_t* rows;     // optional: launch row b serves request row rows[b] ...
+  const int32_t* nrows;    // ... for b < *nrows (device count)
+  unsigned* err;
+};
+
+template <int DP, int MODE, bool BIAS>
+__global__ __launch_bounds__(256, 2) void dot_score_kernel(DotArgs A) {
+  constexpr bool LIST = MODE == DOT_LIST, DENSE = MODE == DOT_DENSE, THRESH = MODE == DOT_THRESH;
   constexpr int KS = DP / 2;        // MFMA k-steps (K = 2 each)
   constexpr int RS = DP + 4;        // LDS row stride (floats): conflict-free b128 reads
   constexpr int F4_PER_ROW = DP / 4;
@@ -44,63 +75,67 @@ __global__ __launch_bounds__(256, 2) void dot_score_kernel(
   const int wave = tid >> 6;
   const int h = lane >> 5;
   const int j = lane & 31;
+  const int64_t Bl = A.nrows ? (int64_t)*A.nrows : A.B;  // rows of this launch
   const int64_t b0 = (int64_t)blockIdx.x * 128 + wave * 32;
+  if ((int64_t)blockIdx.x * 128 >= Bl) return;  // whole workgroup idle (fallback launches)
   const int p = blockIdx.y;
-  const int64_t part_start = (int64_t)p * ipp;
-  const int64_t part_end = std::min<int64_t>(I, part_start + ipp);
+  const int64_t part_start = (int64_t)p * A.ipp;
+  const int64_t part_end = std::min<int64_t>(A.I, part_start + A.ipp);
+  const int64_t K = A.K;
+  auto req = [&](int64_t b) -> int64_t { return A.rows ? (int64_t)A.rows[b] : b; };
 
   // ---- A operand: this lane's user (b0 + j), k = 2s + h
   float a[KS];
-  bool uvalid;
   {
     const int64_t b = b0 + j;
     int64_t uid = -1;
-    if (b < B) uid = uids[b];
-    uvalid = (b < B) && uid >= 0 && uid < num_users;
-    if (b < B && !uvalid && h == 0) hnm_flag(err, HNM_ERR_OOB);
-    const float* row = ut + (uvalid ? uid : 0) * ldu;
+    if (b < Bl) uid = A.uids[req(b)];
+    const bool uvalid = (b < Bl) && uid >= 0 && uid < A.num_users;
+    if (b < Bl && !uvalid && h == 0) hnm_flag(A.err, HNM_ERR_OOB);
+    const float* row = A.ut + (uvalid ? uid : 0) * A.ldu;
 #pragma unroll
     for (int m = 0; m < KS / 2; ++m) {
       const int k0 = 4 * m;
       float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (uvalid && k0 < d) v = *reinterpret_cast<const float4*>(row + k0);
+      if (uvalid && k0 < A.d) v = *reinterpret_cast<const float4*>(row + k0);
       a[2 * m] = h ? v.y : v.x;
       a[2 * m + 1] = h ? v.w : v.z;
     }
   }
-  // per-row user bias for the 16 C rows of this lane
-  float ub[16];
-  if (BIAS) {
+  // per C-row constants of this lane: user bias, threshold
+  float ub[BIAS ? 16 : 1];
+  float tv[16];
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int64_t b = b0 + mfma32_row(r, h);
+  for (int r = 0; r < 16; ++r) {
+    const int64_t b = b0 + mfma32_row(r, h);
+    tv[r] = -__builtin_inff();
+    if (THRESH) tv[r] = b < Bl ? A.tau[req(b) * A.tau_ld] : __builtin_inff();
+    if (BIAS) {
       float v = 0.f;
-      if (ubias && b < B) {
-        const int64_t uid = uids[b];
-        if (uid >= 0 && uid < num_users) v = ubias[uid];
+      if (A.ubias && b < Bl) {
+        const int64_t uid = A.uids[req(b)];
+        if (uid >= 0 && uid < A.num_users) v = A.ubias[uid];
       }
-      ub[r] = v + (cbias ? cbias[0] : 0.f);
+      ub[r] = v + (A.cbias ? A.cbias[0] : 0.f);
     }
   }
-
-  // ---- top-K state: list for user row i lives in (lv[i], li[i]); threshold per C reg
-  float lv[DENSE ? 1 : 32];
-  int li[DENSE ? 1 : 32];
-  float tv[16];
-  if (!DENSE) {
+  // LIST state: list for user row i lives in (lv[i], li[i])
+  float lv[LIST ? 32 : 1];
+  int li[LIST ? 32 : 1];
+  if (LIST) {
 #pragma unroll
     for (int i = 0; i < 32; ++i) { lv[i] = -__builtin_inff(); li[i] = HNM_SENTINEL_IDX; }
-#pragma unroll
-    for (int r = 0; r < 16; ++r) tv[r] = -__builtin_inff();
   }
-  // mask cursor of user (b0 + lane), lanes < 32
+  // mask cursor of user (b0 + lane), lanes < 32 (real item ids; item i is i * istride)
+  const int64_t S = A.istride;
   int nm = INT_BIG;
   int64_t mpos = 0, mend = 0;
-  if (!DENSE && mptr && lane < 32 && b0 + lane < B) {
-    const int64_t lo = mptr[b0 + lane], hi = mptr[b0 + lane + 1];
-    mpos = mask_lower_bound(midx, lo, hi, (int)part_start);
+  if (!DENSE && A.mptr && lane < 32 && b0 + lane < Bl) {
+    const int64_t r = req(b0 + lane);
+    const int64_t lo = A.mptr[r], hi = A.mptr[r + 1];
+    mpos = mask_lower_bound(A.midx, lo, hi, (int)(part_start * S));
     mend = hi;
-    nm = mpos < mend ? midx[mpos] : INT_BIG;
+    nm = mpos < mend ? A.midx[mpos] : INT_BIG;
   }
 
   // ---- item tile staging (pair-permuted: vs[row][h*KS + s] = V[row][2s+h])
@@ -112,7 +147,8 @@ __global__ __launch_bounds__(256, 2) void dot_score_kernel(
       const int row = f / F4_PER_ROW, c4 = f % F4_PER_ROW;
       const int64_t item = base + row;
       float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (item < part_end && 4 * c4 < d) v = *reinterpret_cast<const float4*>(it + item * ldi + 4 * c4);
+      if (item < part_end && 4 * c4 < A.d)
+        v = *reinterpret_cast<const float4*>(A.it + item * S * A.ldi + 4 * c4);
       stage[q] = v;
     }
   };
@@ -155,7 +191,7 @@ __global__ __launch_bounds__(256, 2) void dot_score_kernel(
     float sc[16];
     {
       float ib = 0.f;
-      if (BIAS && ibias && ivalid) ib = ibias[item];
+      if (BIAS && A.ibias && ivalid) ib = A.ibias[item * S];
 #pragma unroll
       for (int r = 0; r < 16; ++r) sc[r] = BIAS ? (acc[r] + ub[r]) + ib : acc[r];
     }
@@ -164,47 +200,66 @@ __global__ __launch_bounds__(256, 2) void dot_score_kernel(
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int64_t b = b0 + mfma32_row(r, h);
-        if (ivalid && b < B) dense[b * ldo + item] = sc[r];
+        if (ivalid && b < Bl) A.dense[req(b) * A.ldo + item] = sc[r];
       }
     } else {
       const int64_t tile_end = std::min<int64_t>(base + TILE, part_end);
+      const int64_t real_end = (tile_end - 1) * S + 1;  // real ids of this tile are < real_end
       // -inf for masked (user, item) pairs inside this tile (rare path)
-      uint64_t mm = __ballot(lane < 32 && nm < tile_end) & 0xffffffffull;
+      uint64_t mm = __ballot(lane < 32 && nm < real_end) & 0xffffffffull;
       while (mm) {
         const int u = __builtin_ctzll(mm);
         mm &= mm - 1;
         while (true) {
           const int tgt = hnm_readlane_i(nm, u);
-          if (tgt >= tile_end) break;
+          if (tgt >= real_end) break;
+          if (tgt % S == 0) {
+            const int64_t ti = tgt / S;
 #pragma unroll
-          for (int r = 0; r < 16; ++r)
-            if (mfma32_row(r, h) == u && item == tgt) sc[r] = -__builtin_inff();
+            for (int r = 0; r < 16; ++r)
+              if (mfma32_row(r, h) == u && item == ti) sc[r] = -__builtin_inff();
+          }
           if (lane == u) {
             ++mpos;
-            nm = mpos < mend ? midx[mpos] : INT_BIG;
+            nm = mpos < mend ? A.midx[mpos] : INT_BIG;
           }
         }
       }
-      // threshold pre-filter, then exact serial insertion per user list
+      if (THRESH) {
+        // append every score >= tau_u (rare after the sample pass)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const uint64_t m = __ballot(ivalid && sc[r] >= tv[r]);
-        if (m) {
-          uint64_t lo = m & 0xffffffffull, hi = m >> 32;
-          const int i0 = mfma32_row(r, 0), i1 = mfma32_row(r, 1);
-          while (lo) {
-            const int l = __builtin_ctzll(lo);
-            lo &= lo - 1;
-            list1_insert(lv[i0], li[i0], hnm_readlane_f(sc[r], l), (int)(base + l), K);
+        for (int r = 0; r < 16; ++r) {
+          if (ivalid && sc[r] >= tv[r]) {
+            const int64_t rq = req(b0 + mfma32_row(r, h));
+            const int slot = atomicAdd(&A.cnt[rq], 1);
+            if (slot < A.cap) {
+              A.buf_v[rq * A.cap + slot] = sc[r];
+              A.buf_i[rq * A.cap + slot] = (int)item;
+            }
           }
-          while (hi) {
-            const int l = __builtin_ctzll(hi);
-            hi &= hi - 1;
-            list1_insert(lv[i1], li[i1], hnm_readlane_f(sc[r], 32 + l), (int)(base + l), K);
+        }
+      } else {
+        // threshold pre-filter, then exact serial insertion per user list
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const uint64_t m = __ballot(ivalid && sc[r] >= tv[r]);
+          if (m) {
+            uint64_t lo = m & 0xffffffffull, hi = m >> 32;
+            const int i0 = mfma32_row(r, 0), i1 = mfma32_row(r, 1);
+            while (lo) {
+              const int l = __builtin_ctzll(lo);
+              lo &= lo - 1;
+              list1_insert(lv[i0], li[i0], hnm_readlane_f(sc[r], l), (int)(base + l), (int)K);
+            }
+            while (hi) {
+              const int l = __builtin_ctzll(hi);
+              hi &= hi - 1;
+              list1_insert(lv[i1], li[i1], hnm_readlane_f(sc[r], 32 + l), (int)(base + l), (int)K);
+            }
+            const float t0 = hnm_readlane_f(lv[i0], K - 1);
+            const float t1 = hnm_readlane_f(lv[i1], K - 1);
+            tv[r] = h ? t1 : t0;
           }
-          const float t0 = hnm_readlane_f(lv[i0], K - 1);
-          const float t1 = hnm_readlane_f(lv[i1], K - 1);
-          tv[r] = h ? t1 : t0;
         }
       }
     }
@@ -213,17 +268,47 @@ __global__ __launch_bounds__(256, 2) void dot_score_kernel(
     __syncthreads();
   }
 
-  if (!DENSE) {
+  if (LIST) {
 #pragma unroll
     for (int i = 0; i < 32; ++i) {
       const int64_t b = b0 + i;
-      if (b < B && lane < K) {
-        const int64_t o = (b * NP + p) * K + lane;
-        cand_v[o] = lv[i];
-        cand_i[o] = li[i] == HNM_SENTINEL_IDX ? -1 : li[i];
+      if (b < Bl && lane < K) {
+        const int64_t o = (b * A.NP + p) * K + lane;
+        A.cand_v[o] = lv[i];
+        A.cand_i[o] = li[i] == HNM_SENTINEL_IDX ? -1 : li[i];
       }
     }
   }
+}
+
+// ------------------------------------------------------------------ threshold select
+// Row b: exact top-K of its appended candidates.  A row with more than `cap` appends, or
+// fewer than K (NaN thresholds), is queued for the LIST fallback instead.
+__global__ __launch_bounds__(256) void thresh_select_kernel(const int* __restrict__ cnt,
+                                                            const float* __restrict__ bv,
+                                                            const int32_t* __restrict__ bi,
+                                                            int cap, int64_t B, int K,
+                                                            float* __restrict__ ov,
+                                                            int64_t* __restrict__ oi,
+                                                            int32_t* __restrict__ ovf_rows,
+                                                            int32_t* __restrict__ ovf_cnt) {
+  const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (b >= B) return;
+  const int lane = threadIdx.x & 63;
+  const int n = cnt[b];
+  if (n > cap || n < K) {
+    if (lane == 0) ovf_rows[atomicAdd(ovf_cnt, 1)] = (int32_t)b;
+    return;
+  }
+  WaveTopK<1> L;
+  L.init();
+  for (int base = 0; base < n; base += 64) {
+    const int q = base + lane;
+    const bool ok = q < n;
+    L.offer(ok ? bv[b * cap + q] : -__builtin_inff(), ok ? bi[b * cap + q] : HNM_SENTINEL_IDX,
+            ok, K);
+  }
+  L.store(ov ? ov + b * K : nullptr, oi + b * K, K);
 }
 
 // ------------------------------------------------------------------ row top-K (dense in)
@@ -265,23 +350,32 @@ __global__ __launch_bounds__(256) void rows_topk_kernel(const float* __restrict_
 }
 
 // ------------------------------------------------------------------ host side
-template <int DP, bool DENSE, bool BIAS>
-static void launch_dot(hnm_ctx* ctx, dim3 grid, const float* ut, int64_t U, int64_t ldu,
-                       const int64_t* ids, int64_t B, const float* it, int64_t I, int64_t ldi,
-                       int d, const float* ub, const float* ib, const float* cb, int64_t ipp,
-                       const int64_t* mptr, const int32_t* midx, int K, float* cv, int32_t* ci,
-                       int NP, float* dense, int64_t ldo) {
-  hipLaunchKernelGGL((dot_score_kernel<DP, DENSE, BIAS>), grid, dim3(256), 0, ctx->stream, ut,
-                     U, ldu, ids, B, it, I, ldi, d, ub, ib, cb, ipp, mptr, midx, K, cv, ci, NP,
-                     dense, ldo, ctx->err_dev);
+hnm_status hnm_topk_merge_rows(hnm_ctx* ctx, const float* cv, const int32_t* ci, int64_t B,
+                               int64_t G, int64_t gstride, int64_t bstride, int kc, int k,
+                               float* ov, int64_t* oi, const int32_t* rows,
+                               const int32_t* nrows);
+
+template <int MODE>
+static void launch_dot(hnm_ctx* ctx, dim3 grid, const DotArgs& a, bool bias) {
+#define HNM_DOT(DPV)                                                                     \
+  if (bias)                                                                              \
+    hipLaunchKernelGGL((dot_score_kernel<DPV, MODE, true>), grid, dim3(256), 0, ctx->stream, a); \
+  else                                                                                   \
+    hipLaunchKernelGGL((dot_score_kernel<DPV, MODE, false>), grid, dim3(256), 0, ctx->stream, a);
+  if (a.d <= 64) {
+    HNM_DOT(64)
+  } else {
+    HNM_DOT(128)
+  }
+#undef HNM_DOT
 }
 
-template <bool DENSE>
-static hnm_status dot_common(hnm_ctx* ctx, const float* ut, int64_t U, int64_t ldu,
-                             const int64_t* ids, int64_t B, const float* it, int64_t I,
-                             int64_t ldi, int d, const float* ub, const float* ib,
-                             const float* cb, const int64_t* mptr, const int32_t* midx, int K,
-                             float* ov, int64_t* oi, float* dense, int64_t ldo) {
+// Sample-threshold design parameters (see the header comment).
+#define THRESH_MIN_ITEMS 8192
+#define THRESH_SAMPLE 4096
+
+static hnm_status dot_validate(hnm_ctx* ctx, const float* ut, int64_t U, int64_t ldu,
+                               const int64_t* ids, const float* it, int64_t I, int64_t ldi, int d) {
   HNM_REQUIRE(ctx && ut && ids && it, HNM_EINVAL, "dot: NULL argument");
   HNM_REQUIRE(d >= 1 && d <= 128 && ldu >= d && ldi >= d && U > 0 && I > 0, HNM_EINVAL,
               "dot: bad shape (d=%d)", d);
@@ -289,42 +383,41 @@ static hnm_status dot_common(hnm_ctx* ctx, const float* ut, int64_t U, int64_t l
                   (uintptr_t)it % 16 == 0,
               HNM_EUNSUPPORTED, "dot: tables must be 16-B aligned with d %% 4 == 0");
   HNM_REQUIRE(I < INT_BIG, HNM_EUNSUPPORTED, "dot: too many items");
-  if (B <= 0) return HNM_OK;
-  const int64_t ublocks = hnm_cdiv(B, 128);
-  Partition part = choose_partition(I, ublocks, ctx->num_cus);
-  dim3 grid((unsigned)ublocks, (unsigned)part.np);
-  const bool bias = ub || ib || cb;
-  float* cv = nullptr;
-  int32_t* ci = nullptr;
-  if (!DENSE) {
-    HNM_REQUIRE(K >= 1 && K <= 64, HNM_EINVAL, "dot_topk: fused path needs 1 <= k <= 64");
-    HNM_REQUIRE(oi, HNM_EINVAL, "dot_topk: out_idx is NULL");
-    const size_t n = (size_t)B * part.np * K;
-    void* w;
-    hnm_status st = hnm_workspace(ctx, hnm_align(n * 4) * 2, &w);
-    if (st) return st;
-    cv = (float*)w;
-    ci = (int32_t*)((char*)w + hnm_align(n * 4));
-  }
-#define HNM_DOT(DPV)                                                                       \
-  if (bias)                                                                                \
-    launch_dot<DPV, DENSE, true>(ctx, grid, ut, U, ldu, ids, B, it, I, ldi, d, ub, ib, cb, \
-                                 part.ipp, mptr, midx, K, cv, ci, part.np, dense, ldo);    \
-  else                                                                                     \
-    launch_dot<DPV, DENSE, false>(ctx, grid, ut, U, ldu, ids, B, it, I, ldi, d, ub, ib,    \
-                                  cb, part.ipp, mptr, midx, K, cv, ci, part.np, dense, ldo);
-  hnm_timer_begin(ctx);
-  if (d <= 64) {
-    HNM_DOT(64)
-  } else {
-    HNM_DOT(128)
-  }
-#undef HNM_DOT
-  hnm_timer_end(ctx);
-  HNM_LAUNCH_CHECK();
-  if (!DENSE) return hnm_topk_merge_i32(ctx, cv, ci, B, 1, 0, (int64_t)part.np * K,
-                                        part.np * K, K, ov, oi);
   return HNM_OK;
+}
+
+static DotArgs dot_args(hnm_ctx* ctx, const float* ut, int64_t U, int64_t ldu, const int64_t* ids,
+                        int64_t B, const float* it, int64_t I, int64_t ldi, int d, const float* ub,
+                        const float* ib, const float* cb, const int64_t* mptr,
+                        const int32_t* midx, int K) {
+  DotArgs a = {};
+  a.ut = ut; a.num_users = U; a.ldu = ldu; a.uids = ids; a.B = B;
+  a.it = it; a.I = I; a.ldi = ldi; a.istride = 1; a.d = d;
+  a.ubias = ub; a.ibias = ib; a.cbias = cb;
+  a.mptr = mptr; a.midx = midx; a.K = K;
+  a.err = ctx->err_dev;
+  return a;
+}
+
+// LIST pass over `a` (items a.I with stride a.istride) -> merged top-K into ov/oi rows
+// (rows remapped through a.rows when set).
+static hnm_status dot_list_pass(hnm_ctx* ctx, DotArgs a, bool bias, float* cv, int32_t* ci,
+                                float* ov, int64_t* oi) {
+  const int64_t ublocks = hnm_cdiv(a.B, 128);
+  Partition part = choose_partition(a.I, ublocks, ctx->num_cus);
+  a.ipp = part.ipp;
+  a.NP = part.np;
+  a.cand_v = cv;
+  a.cand_i = ci;
+  launch_dot<DOT_LIST>(ctx, dim3((unsigned)ublocks, (unsigned)part.np), a, bias);
+  HNM_LAUNCH_CHECK();
+  return hnm_topk_merge_rows(ctx, cv, ci, a.B, 1, 0, (int64_t)part.np * a.K, part.np * a.K, a.K,
+                             ov, oi, a.rows, a.nrows);
+}
+
+static size_t list_cand_bytes(int64_t B, int64_t I, int K, int num_cus) {
+  Partition part = choose_partition(I, hnm_cdiv(B, 128), num_cus);
+  return hnm_align((size_t)B * part.np * K * 4);
 }
 
 extern "C" hnm_status hnm_dot_topk_f32(hnm_ctx* ctx, const float* user_tab, int64_t num_users,
@@ -334,9 +427,80 @@ extern "C" hnm_status hnm_dot_topk_f32(hnm_ctx* ctx, const float* user_tab, int6
                                        const float* const_bias, const int64_t* mask_ptr,
                                        const int32_t* mask_idx, int k, float* out_val,
                                        int64_t* out_idx) {
-  return dot_common<false>(ctx, user_tab, num_users, ldu, user_ids, B, item_tab, num_items, ldi,
-                           d, user_bias, item_bias, const_bias, mask_ptr, mask_idx, k, out_val,
-                           out_idx, nullptr, 0);
+  hnm_status st = dot_validate(ctx, user_tab, num_users, ldu, user_ids, item_tab, num_items, ldi, d);
+  if (st) return st;
+  HNM_REQUIRE(k >= 1 && k <= 64 && out_idx, HNM_EINVAL, "dot_topk: fused path needs 1 <= k <= 64");
+  if (B <= 0) return HNM_OK;
+  const int64_t I = num_items;
+  const bool bias = user_bias || item_bias || const_bias;
+  DotArgs a = dot_args(ctx, user_tab, num_users, ldu, user_ids, B, item_tab, I, ldi, d, user_bias,
+                       item_bias, const_bias, mask_ptr, mask_idx, k);
+  if (I < THRESH_MIN_ITEMS || I < 4 * (int64_t)k) {
+    const size_t sc = list_cand_bytes(B, I, k, ctx->num_cus);
+    void* w;
+    st = hnm_workspace(ctx, 2 * sc, &w);
+    if (st) return st;
+    hnm_timer_begin(ctx);
+    st = dot_list_pass(ctx, a, bias, (float*)w, (int32_t*)((char*)w + sc), out_val, out_idx);
+    hnm_timer_end(ctx);
+    return st;
+  }
+  // ---- threshold path
+  const int64_t stride = std::max<int64_t>(1, I / THRESH_SAMPLE);
+  const int64_t Ns = hnm_cdiv(I, stride);
+  const int cap = (int)std::min<int64_t>(8192, std::max<int64_t>(256, 8 * (int64_t)k * stride));
+  const size_t s_samp = list_cand_bytes(B, Ns, k, ctx->num_cus);
+  const size_t s_full = list_cand_bytes(B, I, k, ctx->num_cus);
+  const size_t s_tau = hnm_align((size_t)B * k * 4), s_taui = hnm_align((size_t)B * k * 8);
+  const size_t s_cnt = hnm_align((size_t)B * 4), s_buf = hnm_align((size_t)B * cap * 4);
+  const size_t s_rows = hnm_align((size_t)B * 4 + 256);
+  const size_t s_cand = std::max(s_samp, s_full);
+  void* w;
+  st = hnm_workspace(ctx, 2 * s_cand + s_tau + s_taui + s_cnt + 2 * s_buf + s_rows, &w);
+  if (st) return st;
+  char* q = (char*)w;
+  float* cv = (float*)q; q += s_cand;
+  int32_t* ci = (int32_t*)q; q += s_cand;
+  float* tau = (float*)q; q += s_tau;
+  int64_t* taui = (int64_t*)q; q += s_taui;
+  int* cnt = (int*)q; q += s_cnt;
+  float* bv = (float*)q; q += s_buf;
+  int32_t* bi = (int32_t*)q; q += s_buf;
+  int32_t* ovf_cnt = (int32_t*)q;
+  int32_t* ovf_rows = ovf_cnt + 64;
+  HNM_HIP_CHECK(hipMemsetAsync(cnt, 0, (size_t)B * 4, ctx->stream));
+  HNM_HIP_CHECK(hipMemsetAsync(ovf_cnt, 0, 4, ctx->stream));
+  // 1. sample pass: tau_u = K-th best score over items 0, stride, 2*stride, ...
+  DotArgs as = a;
+  as.istride = stride;
+  as.I = Ns;
+  st = dot_list_pass(ctx, as, bias, cv, ci, tau, taui);
+  if (st) return st;
+  // 2. main pass: append scores >= tau_u
+  DotArgs am = a;
+  const int64_t ublocks = hnm_cdiv(B, 128);
+  Partition part = choose_partition(I, ublocks, ctx->num_cus);
+  am.ipp = part.ipp;
+  am.NP = part.np;
+  am.tau = tau + (k - 1);
+  am.tau_ld = k;
+  am.cnt = cnt;
+  am.buf_v = bv;
+  am.buf_i = bi;
+  am.cap = cap;
+  hnm_timer_begin(ctx);
+  launch_dot<DOT_THRESH>(ctx, dim3((unsigned)ublocks, (unsigned)part.np), am, bias);
+  hnm_timer_end(ctx);
+  HNM_LAUNCH_CHECK();
+  // 3. exact top-K of the appended candidates; overflowing rows -> fallback list
+  hipLaunchKernelGGL(thresh_select_kernel, dim3((unsigned)hnm_cdiv(B, 4)), dim3(256), 0,
+                     ctx->stream, cnt, bv, bi, cap, B, k, out_val, out_idx, ovf_rows, ovf_cnt);
+  HNM_LAUNCH_CHECK();
+  // 4. fallback: exact LIST pass restricted (on device) to the queued rows
+  DotArgs af = a;
+  af.rows = ovf_rows;
+  af.nrows = ovf_cnt;
+  return dot_list_pass(ctx, af, bias, cv, ci, out_val, out_idx);
 }
 
 extern "C" hnm_status hnm_dot_scores_f32(hnm_ctx* ctx, const float* user_tab, int64_t num_users,
@@ -344,10 +508,24 @@ extern "C" hnm_status hnm_dot_scores_f32(hnm_ctx* ctx, const float* user_tab, in
                                          const float* item_tab, int64_t num_items, int64_t ldi,
                                          int d, const float* user_bias, const float* item_bias,
                                          const float* const_bias, float* out, int64_t ldo) {
+  hnm_status st = dot_validate(ctx, user_tab, num_users, ldu, user_ids, item_tab, num_items, ldi, d);
+  if (st) return st;
   HNM_REQUIRE(out && ldo >= num_items, HNM_EINVAL, "dot_scores: bad output");
-  return dot_common<true>(ctx, user_tab, num_users, ldu, user_ids, B, item_tab, num_items, ldi,
-                          d, user_bias, item_bias, const_bias, nullptr, nullptr, 1, nullptr,
-                          nullptr, out, ldo);
+  if (B <= 0) return HNM_OK;
+  DotArgs a = dot_args(ctx, user_tab, num_users, ldu, user_ids, B, item_tab, num_items, ldi, d,
+                       user_bias, item_bias, const_bias, nullptr, nullptr, 1);
+  const int64_t ublocks = hnm_cdiv(B, 128);
+  Partition part = choose_partition(num_items, ublocks, ctx->num_cus);
+  a.ipp = part.ipp;
+  a.NP = part.np;
+  a.dense = out;
+  a.ldo = ldo;
+  hnm_timer_begin(ctx);
+  launch_dot<DOT_DENSE>(ctx, dim3((unsigned)ublocks, (unsigned)part.np), a,
+                        user_bias || item_bias || const_bias);
+  hnm_timer_end(ctx);
+  HNM_LAUNCH_CHECK();
+  return HNM_OK;
 }
 
 extern "C" hnm_status hnm_topk_rows_f32(hnm_ctx* ctx, const float* scores, int64_t ld, int64_t B,

@@ -274,3 +274,40 @@ def test_widedeep_full_shape_rows():
     vals, rec = m.recommend_with_scores(t(users))
     ref = O.widedeep_predict_all_items(sd, users[:2])
     assert_topk_equivalent(rec.cpu().numpy()[:2], ref, 12, what="wd full")
+
+
+# ------------------------------------------------------------------ threshold top-K path
+@pytest.mark.parametrize("B", [1, 37, 300])
+def test_dot_threshold_path_vs_oracle(B):
+    """I >= 8192 takes the sample-threshold path (sample pass + append + select)."""
+    U, I = 5000, 20011
+    sd = syn.mf_state_dict(U, I, 64, seed=21, bias_scale=0.05)
+    m = to_module(MatrixFactorization(U, I, sparse=False), sd)
+    users = syn.user_batch(U, B, seed=22)
+    ref = O.mf_predict_all_items(sd, users)
+    f = syn.filter_dict(users, I, per_user=200, seed=23)
+    # mask the current top items of some users so the filter changes the answer
+    for b, u in enumerate(users[:5]):
+        f[int(u)] |= set(int(x) for x in np.argsort(-ref[b])[:5])
+    vals, rec = m.recommend_with_scores(t(users), filter_items=f)
+    masked = O.apply_filter(ref, users, f)
+    assert_topk_equivalent(rec.cpu().numpy(), masked, 12, what=f"mf thresh B={B}")
+    np.testing.assert_allclose(vals.cpu().numpy(), np.take_along_axis(masked, rec.cpu().numpy(), 1),
+                               rtol=1e-4, atol=1e-6)
+
+
+def test_dot_threshold_overflow_fallback_exact_ties():
+    """All scores tied: every item passes tau -> buffer overflow -> device LIST fallback.
+    The (score desc, item asc) order must then return items 0..k-1."""
+    U, I, d = 64, 30000, 64
+    sd = syn.mf_state_dict(U, I, d, seed=1)
+    sd["item_embeddings.weight"][:] = sd["item_embeddings.weight"][0]
+    sd["item_bias.weight"][:] = 0
+    m = to_module(MatrixFactorization(U, I, sparse=False), sd)
+    users = np.arange(10)
+    rec = m.recommend(t(users)).cpu().numpy()
+    assert (rec == np.arange(12)[None, :]).all()
+    f = {3: set(range(0, 20))}
+    rec = m.recommend(t(users), filter_items=f).cpu().numpy()
+    assert rec[3].tolist() == list(range(20, 32))
+    assert (rec[4] == np.arange(12)).all()
