@@ -40,7 +40,7 @@ struct hnm_spmm_plan {
 // ------------------------------------------------------------------ CSR build kernels
 __global__ void csr_prep_kernel(const int64_t* __restrict__ ei, int64_t E, int64_t N,
                                 int32_t* __restrict__ keys, int32_t* __restrict__ vals,
-                                int32_t* __restrict__ cnt, unsigned* err) {
+                                unsigned* err) {
   for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < E;
        e += (int64_t)gridDim.x * 256) {
     int64_t r = ei[e], c = ei[E + e];
@@ -50,15 +50,27 @@ __global__ void csr_prep_kernel(const int64_t* __restrict__ ei, int64_t E, int64
     }
     keys[e] = (int32_t)r;
     vals[e] = (int32_t)e;
-    atomicAdd(&cnt[r], 1);
   }
 }
 
-__global__ void csr_counts_kernel(const int32_t* __restrict__ cnt, int64_t N,
+// Row extents from the sorted keys (no atomics: power-law rows would serialize them):
+// first[r] / last[r] = first and one-past-last sorted position of row r (0 / 0 if empty).
+__global__ void csr_extent_kernel(const int32_t* __restrict__ skeys, int64_t E,
+                                  int32_t* __restrict__ first, int32_t* __restrict__ last) {
+  for (int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x; p < E;
+       p += (int64_t)gridDim.x * 256) {
+    const int32_t r = skeys[p];
+    if (p == 0 || skeys[p - 1] != r) first[r] = (int32_t)p;
+    if (p == E - 1 || skeys[p + 1] != r) last[r] = (int32_t)(p + 1);
+  }
+}
+
+__global__ void csr_counts_kernel(const int32_t* __restrict__ first,
+                                  const int32_t* __restrict__ last, int64_t N,
                                   int64_t* __restrict__ counts) {
   for (int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x; r <= N;
        r += (int64_t)gridDim.x * 256)
-    counts[r] = r < N ? (int64_t)cnt[r] + 1 : 0;
+    counts[r] = r < N ? (int64_t)(last[r] - first[r]) + 1 : 0;
 }
 
 __global__ void csr_place_kernel(const int64_t* __restrict__ ei, const float* __restrict__ w,
@@ -112,15 +124,24 @@ __global__ __launch_bounds__(256) void csr_degree_kernel(const int64_t* __restri
   }
 }
 
-__global__ void csr_norm_kernel(const int64_t* __restrict__ rowptr, const int32_t* __restrict__ col,
-                                const float* __restrict__ dinv, int64_t N,
+// val = (dinv[row] * w) * dinv[col]: one thread per entry (edges via the sorted keys,
+// then the self-loops), so power-law rows cost nothing extra.
+__global__ void csr_norm_kernel(const int32_t* __restrict__ skeys, int64_t E, int64_t N,
+                                const int64_t* __restrict__ rowptr,
+                                const int32_t* __restrict__ col, const float* __restrict__ dinv,
                                 float* __restrict__ val) {
-  // one wave per row: val = (dinv[row] * w) * dinv[col]
-  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (r >= N) return;
-  const int lane = threadIdx.x & 63;
-  const float dr = dinv[r];
-  for (int64_t p = rowptr[r] + lane; p < rowptr[r + 1]; p += 64) val[p] = (dr * val[p]) * dinv[col[p]];
+  for (int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x; p < E + N;
+       p += (int64_t)gridDim.x * 256) {
+    int64_t r, dst;
+    if (p < E) {
+      r = skeys[p];
+      dst = p + r;
+    } else {
+      r = p - E;
+      dst = rowptr[r + 1] - 1;
+    }
+    val[dst] = (dinv[r] * val[dst]) * dinv[col[dst]];
+  }
 }
 
 extern "C" hnm_status hnm_csr_build_norm(hnm_ctx* ctx, const int64_t* edge_index,
@@ -145,28 +166,32 @@ extern "C" hnm_status hnm_csr_build_norm(hnm_ctx* ctx, const int64_t* edge_index
   const size_t sd = hnm_align((size_t)N * 4);
   const size_t tmp = hnm_align(std::max(sort_tmp, scan_tmp));
   void* wsp;
-  hnm_status s = hnm_workspace(ctx, 4 * s4 + sc + sc8 + sd + tmp, &wsp);
+  hnm_status s = hnm_workspace(ctx, 4 * s4 + 2 * sc + sc8 + sd + tmp, &wsp);
   if (s) return s;
   char* p = (char*)wsp;
   int32_t* kin = (int32_t*)p; p += s4;
   int32_t* kout = (int32_t*)p; p += s4;
   int32_t* vin = (int32_t*)p; p += s4;
   int32_t* vout = (int32_t*)p; p += s4;
-  int32_t* cnt = (int32_t*)p; p += sc;
+  int32_t* first = (int32_t*)p; p += sc;
+  int32_t* last = (int32_t*)p; p += sc;
   int64_t* counts = (int64_t*)p; p += sc8;
   float* dinv = (float*)p; p += sd;
   void* t = p;
 
-  HNM_HIP_CHECK(hipMemsetAsync(cnt, 0, (size_t)(N + 1) * 4, st));
+  HNM_HIP_CHECK(hipMemsetAsync(first, 0, (size_t)(N + 1) * 4, st));
+  HNM_HIP_CHECK(hipMemsetAsync(last, 0, (size_t)(N + 1) * 4, st));
   const unsigned g = 8 * 1024;
   if (E > 0) {
-    hipLaunchKernelGGL(csr_prep_kernel, dim3(g), dim3(256), 0, st, edge_index, E, N, kin, vin, cnt,
+    hipLaunchKernelGGL(csr_prep_kernel, dim3(g), dim3(256), 0, st, edge_index, E, N, kin, vin,
                        ctx->err_dev);
     HNM_LAUNCH_CHECK();
     size_t tb = sort_tmp;
     HNM_HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(t, tb, kin, kout, vin, vout, (int)E, 0, bits, st));
+    hipLaunchKernelGGL(csr_extent_kernel, dim3(g), dim3(256), 0, st, kout, E, first, last);
+    HNM_LAUNCH_CHECK();
   }
-  hipLaunchKernelGGL(csr_counts_kernel, dim3(g), dim3(256), 0, st, cnt, N, counts);
+  hipLaunchKernelGGL(csr_counts_kernel, dim3(g), dim3(256), 0, st, first, last, N, counts);
   HNM_LAUNCH_CHECK();
   size_t tb = scan_tmp;
   HNM_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(t, tb, counts, rowptr, (int)(N + 1), st));
@@ -177,7 +202,8 @@ extern "C" hnm_status hnm_csr_build_norm(hnm_ctx* ctx, const int64_t* edge_index
   hipLaunchKernelGGL(csr_degree_kernel, rg, dim3(256), 0, st, rowptr, val, N,
                      edge_weight != nullptr, dinv);
   HNM_LAUNCH_CHECK();
-  hipLaunchKernelGGL(csr_norm_kernel, rg, dim3(256), 0, st, rowptr, col, dinv, N, val);
+  hipLaunchKernelGGL(csr_norm_kernel, dim3(g), dim3(256), 0, st, kout, E, N, rowptr, col, dinv,
+                     val);
   HNM_LAUNCH_CHECK();
   return HNM_OK;
 }

@@ -61,8 +61,9 @@ struct DotArgs {
   unsigned* err;
 };
 
+// LIST keeps 32 user lists in registers (2 workgroups/CU); the list-free modes run 4.
 template <int DP, int MODE, bool BIAS>
-__global__ __launch_bounds__(256, 2) void dot_score_kernel(DotArgs A) {
+__global__ __launch_bounds__(256, MODE == DOT_LIST ? 2 : 4) void dot_score_kernel(DotArgs A) {
   constexpr bool LIST = MODE == DOT_LIST, DENSE = MODE == DOT_DENSE, THRESH = MODE == DOT_THRESH;
   constexpr int KS = DP / 2;        // MFMA k-steps (K = 2 each)
   constexpr int RS = DP + 4;        // LDS row stride (floats): conflict-free b128 reads
@@ -226,7 +227,11 @@ __global__ __launch_bounds__(256, 2) void dot_score_kernel(DotArgs A) {
         }
       }
       if (THRESH) {
-        // append every score >= tau_u (rare after the sample pass)
+        // append every score >= tau_u (rare after the sample pass): one ballot per tile
+        bool any = false;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) any |= sc[r] >= tv[r];
+        if (__ballot(ivalid && any))
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           if (ivalid && sc[r] >= tv[r]) {
@@ -314,13 +319,15 @@ __global__ __launch_bounds__(256) void thresh_select_kernel(const int* __restric
 // ------------------------------------------------------------------ row top-K (dense in)
 // torch.topk(scores, k) replacement over a dense [B, I] matrix with an optional CSR mask
 // (serve.py:350-355).  One wave per row; K <= 128.
+// `istride`: column c holds real item c * istride (mask ids are real item ids).
 template <int NS>
 __global__ __launch_bounds__(256) void rows_topk_kernel(const float* __restrict__ s,
                                                         int64_t ld, int64_t B, int64_t I,
                                                         const int64_t* __restrict__ mptr,
                                                         const int32_t* __restrict__ midx,
                                                         int K, float* __restrict__ ov,
-                                                        int64_t* __restrict__ oi) {
+                                                        int64_t* __restrict__ oi,
+                                                        int64_t istride = 1) {
   const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (b >= B) return;
   const int lane = threadIdx.x & 63;
@@ -338,9 +345,9 @@ __global__ __launch_bounds__(256) void rows_topk_kernel(const float* __restrict_
     const int64_t item = base + lane;
     const bool valid = item < I;
     float v = valid ? row[item] : -__builtin_inff();
-    const int64_t end = std::min<int64_t>(base + 64, I);
+    const int64_t end = (std::min<int64_t>(base + 64, I) - 1) * istride + 1;  // real ids < end
     while (nm < end) {
-      if (item == nm) v = -__builtin_inff();
+      if (nm % istride == 0 && item == nm / istride) v = -__builtin_inff();
       ++mpos;
       nm = mpos < mend ? midx[mpos] : INT_BIG;
     }
@@ -455,8 +462,9 @@ extern "C" hnm_status hnm_dot_topk_f32(hnm_ctx* ctx, const float* user_tab, int6
   const size_t s_cnt = hnm_align((size_t)B * 4), s_buf = hnm_align((size_t)B * cap * 4);
   const size_t s_rows = hnm_align((size_t)B * 4 + 256);
   const size_t s_cand = std::max(s_samp, s_full);
+  const size_t s_sd = hnm_align((size_t)B * Ns * 4);
   void* w;
-  st = hnm_workspace(ctx, 2 * s_cand + s_tau + s_taui + s_cnt + 2 * s_buf + s_rows, &w);
+  st = hnm_workspace(ctx, 2 * s_cand + s_tau + s_taui + s_cnt + 2 * s_buf + s_rows + s_sd, &w);
   if (st) return st;
   char* q = (char*)w;
   float* cv = (float*)q; q += s_cand;
@@ -466,20 +474,34 @@ extern "C" hnm_status hnm_dot_topk_f32(hnm_ctx* ctx, const float* user_tab, int6
   int* cnt = (int*)q; q += s_cnt;
   float* bv = (float*)q; q += s_buf;
   int32_t* bi = (int32_t*)q; q += s_buf;
-  int32_t* ovf_cnt = (int32_t*)q;
+  int32_t* ovf_cnt = (int32_t*)q; q += s_rows;
   int32_t* ovf_rows = ovf_cnt + 64;
+  float* sdense = (float*)q;
   HNM_HIP_CHECK(hipMemsetAsync(cnt, 0, (size_t)B * 4, ctx->stream));
   HNM_HIP_CHECK(hipMemsetAsync(ovf_cnt, 0, 4, ctx->stream));
-  // 1. sample pass: tau_u = K-th best score over items 0, stride, 2*stride, ...
-  DotArgs as = a;
-  as.istride = stride;
-  as.I = Ns;
-  st = dot_list_pass(ctx, as, bias, cv, ci, tau, taui);
-  if (st) return st;
+  // 1. sample pass: dense scores of items 0, stride, 2*stride, ... (masks applied by the
+  //    row top-K), tau_u = K-th best of them
+  {
+    DotArgs as = a;
+    as.istride = stride;
+    as.I = Ns;
+    as.mptr = nullptr;
+    as.midx = nullptr;
+    Partition ps = choose_partition(Ns, hnm_cdiv(B, 128), 2 * ctx->num_cus);
+    as.ipp = ps.ipp;
+    as.NP = ps.np;
+    as.dense = sdense;
+    as.ldo = Ns;
+    launch_dot<DOT_DENSE>(ctx, dim3((unsigned)hnm_cdiv(B, 128), (unsigned)ps.np), as, bias);
+    HNM_LAUNCH_CHECK();
+    hipLaunchKernelGGL(rows_topk_kernel<1>, dim3((unsigned)hnm_cdiv(B, 4)), dim3(256), 0,
+                       ctx->stream, sdense, Ns, B, Ns, mask_ptr, mask_idx, k, tau, taui, stride);
+    HNM_LAUNCH_CHECK();
+  }
   // 2. main pass: append scores >= tau_u
   DotArgs am = a;
   const int64_t ublocks = hnm_cdiv(B, 128);
-  Partition part = choose_partition(I, ublocks, ctx->num_cus);
+  Partition part = choose_partition(I, ublocks, 2 * ctx->num_cus);
   am.ipp = part.ipp;
   am.NP = part.np;
   am.tau = tau + (k - 1);
@@ -515,7 +537,7 @@ extern "C" hnm_status hnm_dot_scores_f32(hnm_ctx* ctx, const float* user_tab, in
   DotArgs a = dot_args(ctx, user_tab, num_users, ldu, user_ids, B, item_tab, num_items, ldi, d,
                        user_bias, item_bias, const_bias, nullptr, nullptr, 1);
   const int64_t ublocks = hnm_cdiv(B, 128);
-  Partition part = choose_partition(num_items, ublocks, ctx->num_cus);
+  Partition part = choose_partition(num_items, ublocks, 2 * ctx->num_cus);
   a.ipp = part.ipp;
   a.NP = part.np;
   a.dense = out;
@@ -539,10 +561,10 @@ extern "C" hnm_status hnm_topk_rows_f32(hnm_ctx* ctx, const float* scores, int64
   dim3 grid((unsigned)hnm_cdiv(B, 4));
   if (k <= 64)
     hipLaunchKernelGGL(rows_topk_kernel<1>, grid, dim3(256), 0, ctx->stream, scores, ld, B, I,
-                       mask_ptr, mask_idx, k, out_val, out_idx);
+                       mask_ptr, mask_idx, k, out_val, out_idx, (int64_t)1);
   else
     hipLaunchKernelGGL(rows_topk_kernel<2>, grid, dim3(256), 0, ctx->stream, scores, ld, B, I,
-                       mask_ptr, mask_idx, k, out_val, out_idx);
+                       mask_ptr, mask_idx, k, out_val, out_idx, (int64_t)1);
   HNM_LAUNCH_CHECK();
   return HNM_OK;
 }
