@@ -15,10 +15,11 @@ N>1 (torchrun, one rank per GPU): items are row-sharded across ranks; every rank
 4096 users and scores all N*4096 users against its I/N items (weak scaling).
 
 Also printed in the same JSON line:
-  roofline     -- dominant kernel (ncf_score_kernel) algorithmic FLOPs per launch / its
+  roofline     -- dominant kernel (NCF: ncf16_scan_kernel, the certified f16 scan; with
+                  --exact the fp32 ncf32_kernel) algorithmic FLOPs per launch / its
                   average duration (HIP events on the ctx stream, measured live here),
-                  vs the fp32 MFMA peak; `traffic` from the committed rocprofv3 PMC
-                  summary (profiles/) when present for this workload.
+                  vs the MFMA peak of the kernel's dtype; `traffic` from the committed
+                  rocprofv3 PMC summary (profiles/) when present for this workload.
   cpu_baseline -- the CPU oracle (numpy restatement of the reference, op for op) on a
                   bounded user sample, rank 0 at N=1 only.
 """
@@ -44,6 +45,9 @@ from hnm_recommendation_amd import synthetic as syn  # noqa: E402
 
 METRIC = "recommendations/sec (batched users, K=12) at 1/2/4/8 MI355X; % HBM roofline"
 FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: fp32 matrix (= vector) peak
+# f16 dense MFMA: v_mfma_f32_32x32x16_f16 = 32 cycles/SIMD -> 1024 FLOP/clk/SIMD x 4 x 256 CUs
+# x 2.4 GHz (MI355X_MICROARCH.md "Peak BF16/FP16 MFMA ~2.5 PF dense")
+F16_MFMA_PEAK_TFLOPS = 2516.6
 HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md: HBM3E spec peak
 K = 12
 
@@ -69,7 +73,7 @@ def load(m, sd, device):
     return m.to(device).eval()
 
 
-def build_workload(name, rank, world, device, batch):
+def build_workload(name, rank, world, device, batch, exact=False):
     """Returns (step_fn(users) -> (vals, idx), flops_or_bytes_per_launch, bound, info)."""
     U, I = syn.HM_USERS, syn.HM_ITEMS
     lo, hi = S.shard_range(I, rank, world)
@@ -78,8 +82,10 @@ def build_workload(name, rank, world, device, batch):
         m = load(NeuralCF(U, I), sd, device)
         local = S.ncf_shard_topk(m, lo, hi, K)
         per_launch = 4352.0 * batch * world * (hi - lo)   # 4,352 FLOP / pair
-        info = {"model": "NeuralCF", "mf_dim": 64, "mlp_dims": [128, 64, 32]}
-        bound, kernel = "mfma", "ncf32_kernel"
+        info = {"model": "NeuralCF", "mf_dim": 64, "mlp_dims": [128, 64, 32],
+                "scan": "exact fp32" if exact else
+                        "certified f16 pre-filter + exact fp32 re-scoring (ncf_cert.hip)"}
+        bound, kernel = "mfma", ("ncf32_kernel" if exact else "ncf16_scan_kernel")
         cpu = ("ncf", sd)
     elif name in ("lightgcn", "lightgcn128"):
         d = 64 if name == "lightgcn" else 128
@@ -161,13 +167,17 @@ def main():
     ap.add_argument("--batch", type=int, default=4096)
     ap.add_argument("--workload", default="ncf")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--exact", action="store_true",
+                    help="NCF: exact fp32 scan of every item instead of the certified pre-filter")
     args = ap.parse_args()
 
     rank, world, device = setup_dist(args.gpus)
     B = args.batch
     t_setup = time.perf_counter()
+    if args.exact:
+        _lib.set_prefilter(device, False)
     step, per_launch, bound, kernel, info, cpu = build_workload(args.workload, rank, world,
-                                                                device, B)
+                                                                device, B, args.exact)
     # resident user batches: rank-specific, distinct ids
     nb = 4
     batches = [torch.from_numpy(syn.user_batch(syn.HM_USERS, B, seed=100 + 17 * rank + j)).to(device)
@@ -181,6 +191,7 @@ def main():
     if world > 1:
         dist.barrier()
     _lib.enable_timing(device, True)
+    _lib.prefilter_stats(device, reset=True)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for j in range(args.steps):
@@ -191,6 +202,7 @@ def main():
     elapsed = time.perf_counter() - t0
     ktime_ms, launches = _lib.kernel_timing(device)
     _lib.enable_timing(device, False)
+    pf_rows, pf_cands, pf_fallback = _lib.prefilter_stats(device, reset=True)
     if world > 1:
         t = torch.tensor([elapsed, ktime_ms / max(launches, 1)], dtype=torch.float64, device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -201,7 +213,7 @@ def main():
     users_total = B * world * args.steps
     value = users_total / elapsed
     achieved = per_launch / (avg_kernel_ms * 1e-3) / 1e12
-    peak = FP32_MFMA_PEAK_TFLOPS
+    peak = F16_MFMA_PEAK_TFLOPS if kernel == "ncf16_scan_kernel" else FP32_MFMA_PEAK_TFLOPS
     line = {
         "metric": METRIC,
         "value": round(value, 2),
@@ -213,7 +225,7 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "f32",
+        "dtype": "f16+f32" if kernel == "ncf16_scan_kernel" else "f32",
         "data": "synthetic (PCG64 weights with reference init distributions; H&M shape)",
         "config": {"workload": f"{args.workload}: BASELINE configs[1] NeuralCF dim=64, full H&M "
                                f"shape, batch={B} users/rank, K=12" if args.workload == "ncf"
@@ -229,6 +241,10 @@ def main():
                      "traffic": pmc_traffic(args.workload)},
         "cpu_baseline": None,
     }
+    if pf_rows:
+        line["prefilter"] = {"rows": pf_rows, "candidates_per_row": round(
+            pf_cands / max(pf_rows - pf_fallback, 1), 1), "fallback_rows": pf_fallback,
+            "outputs": "bit-identical to the exact fp32 scan (tests/test_gpu_prefilter.py)"}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
             line["cpu_baseline"] = cpu_baseline(cpu)

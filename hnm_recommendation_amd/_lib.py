@@ -54,6 +54,8 @@ _SIGS = {
     "hnm_ctx_num_cus": (_i32, [_p, C.POINTER(C.c_int)]),
     "hnm_ctx_enable_timing": (_i32, [_p, C.c_int]),
     "hnm_ctx_timing": (_i32, [_p, C.POINTER(C.c_double), C.POINTER(_i64)]),
+    "hnm_ctx_set_option": (_i32, [_p, C.c_int, _i64]),
+    "hnm_ctx_prefilter_stats": (_i32, [_p, C.POINTER(_i64), C.c_int]),
     "hnm_gather_rows_f32": (_i32, [_p, _p, _i64, _i64, C.c_int, _p, _i64, _p, _i64]),
     "hnm_linear_rows_f32": (_i32, [_p, _p, _i64, _p, _i64, _i64, C.c_int, _p, _i64, _p,
                                    C.c_int, _p, _i64, C.c_int]),
@@ -66,6 +68,7 @@ _SIGS = {
     "hnm_ncf_topk_f32": (_i32, [_p, C.POINTER(NcfWeights), _p, _i64, _p, _p, C.c_int, _p, _p]),
     "hnm_ncf_scores_f32": (_i32, [_p, C.POINTER(NcfWeights), _p, _i64, _p, _i64]),
     "hnm_ncf_pair_scores_f32": (_i32, [_p, C.POINTER(NcfWeights), _p, _p, _i64, _p]),
+    "hnm_ncf_prefilter_debug_f32": (_i32, [_p, C.POINTER(NcfWeights), _p, _i64, _p, _i64, _p]),
     "hnm_topk_merge_f32": (_i32, [_p, _p, _p, _i64, _i64, _i64, _i64, C.c_int, C.c_int, _p, _p]),
     "hnm_topk_rows_f32": (_i32, [_p, _p, _i64, _i64, _i64, _p, _p, C.c_int, _p, _p]),
     "hnm_csr_build_norm": (_i32, [_p, _p, _p, _i64, _i64, _p, _p, _p]),
@@ -172,6 +175,22 @@ def kernel_timing(device):
     n = _i64()
     check(fn("hnm_ctx_timing")(ctx(device), C.byref(t), C.byref(n)), "hnm_ctx_timing")
     return t.value, n.value
+
+
+HNM_OPT_PREFILTER = 1
+
+
+def set_prefilter(device, on=True):
+    """Certified f16 pre-filter for NCF top-K (default on); off = exact fp32 scan."""
+    check(fn("hnm_ctx_set_option")(ctx(device), HNM_OPT_PREFILTER, int(bool(on))),
+          "hnm_ctx_set_option")
+
+
+def prefilter_stats(device, reset=False):
+    """(rows scored, candidates re-scored in fp32, rows that took the exact fallback)."""
+    out = (_i64 * 3)()
+    check(fn("hnm_ctx_prefilter_stats")(ctx(device), out, int(reset)), "hnm_ctx_prefilter_stats")
+    return tuple(int(v) for v in out)
 
 
 def ptr(t):

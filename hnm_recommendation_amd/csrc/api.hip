@@ -28,12 +28,15 @@ extern "C" hnm_status hnm_ctx_create(int device, hnm_ctx** out) {
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) == hipSuccess) c->num_cus = prop.multiProcessorCount;
   if (c->num_cus <= 0) c->num_cus = 256;
-  if (hipMalloc((void**)&c->err_dev, sizeof(unsigned)) != hipSuccess) {
+  c->prefilter = 1;
+  if (hipMalloc((void**)&c->err_dev, 64) != hipSuccess) {
     free(c);
     hnm_set_error("hnm_ctx_create: hipMalloc of the error word failed");
     return HNM_ENOMEM;
   }
-  HNM_HIP_CHECK(hipMemset(c->err_dev, 0, sizeof(unsigned)));
+  HNM_HIP_CHECK(hipMemset(c->err_dev, 0, 64));
+  // counters of the certified pre-filter live in the same allocation (8-byte aligned)
+  c->stats_dev = reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(c->err_dev) + 8);
   *out = c;
   return HNM_OK;
 }
@@ -57,6 +60,28 @@ extern "C" hnm_status hnm_ctx_destroy(hnm_ctx* ctx) {
 extern "C" hnm_status hnm_ctx_set_stream(hnm_ctx* ctx, void* s) {
   HNM_REQUIRE(ctx, HNM_EINVAL, "ctx is NULL");
   ctx->stream = (hipStream_t)s;
+  return HNM_OK;
+}
+
+extern "C" hnm_status hnm_ctx_set_option(hnm_ctx* ctx, int option, int64_t value) {
+  HNM_REQUIRE(ctx, HNM_EINVAL, "ctx is NULL");
+  switch (option) {
+    case HNM_OPT_PREFILTER:
+      ctx->prefilter = value != 0;
+      return HNM_OK;
+    default:
+      hnm_set_error("hnm_ctx_set_option: unknown option %d", option);
+      return HNM_EINVAL;
+  }
+}
+
+extern "C" hnm_status hnm_ctx_prefilter_stats(hnm_ctx* ctx, int64_t* out, int reset) {
+  HNM_REQUIRE(ctx && out, HNM_EINVAL, "ctx/out is NULL");
+  HNM_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+  unsigned long long v[3];
+  HNM_HIP_CHECK(hipMemcpy(v, ctx->stats_dev, sizeof(v), hipMemcpyDeviceToHost));
+  for (int i = 0; i < 3; ++i) out[i] = (int64_t)v[i];
+  if (reset) HNM_HIP_CHECK(hipMemset(ctx->stats_dev, 0, sizeof(v)));
   return HNM_OK;
 }
 

@@ -23,6 +23,8 @@ struct hnm_ctx {
   int cap;
   hipEvent_t* ev0;
   hipEvent_t* ev1;
+  int prefilter;                   // HNM_OPT_PREFILTER (default 1)
+  unsigned long long* stats_dev;   // pre-filter counters: rows, candidates, fallback rows
 };
 
 void hnm_timer_begin(hnm_ctx* ctx);
@@ -81,3 +83,9 @@ static inline Partition choose_partition(int64_t I, int64_t ublocks, int num_cus
   np = hnm_cdiv(I, ipp);
   return {(int)np, ipp};
 }
+
+// torch.topk over a dense [B, I] score matrix whose column c is item c * istride, with the
+// optional CSR mask in real item ids (score.hip).  K <= 64.
+hnm_status hnm_topk_rows_strided(hnm_ctx* ctx, const float* s, int64_t ld, int64_t B, int64_t I,
+                                 const int64_t* mptr, const int32_t* midx, int K, float* ov,
+                                 int64_t* oi, int64_t istride);

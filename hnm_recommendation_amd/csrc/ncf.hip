@@ -21,11 +21,15 @@
 #include <algorithm>
 
 #include "hnm_device.h"
-#include "hnm_internal.h"
+#include "ncf_internal.h"
 
 hnm_status hnm_topk_merge_i32(hnm_ctx* ctx, const float* cv, const int32_t* ci, int64_t B,
                               int64_t G, int64_t gstride, int64_t bstride, int kc, int k,
                               float* ov, int64_t* oi);
+hnm_status hnm_topk_merge_rows(hnm_ctx* ctx, const float* cv, const int32_t* ci, int64_t B,
+                               int64_t G, int64_t gstride, int64_t bstride, int kc, int k,
+                               float* ov, int64_t* oi, const int32_t* rows,
+                               const int32_t* nrows);
 
 // ------------------------------------------------------------------ 32-user kernel
 // ABL: ablation bits for tools/ncf_ablation.hip only (0 in the library): 1 = no top-K,
@@ -40,7 +44,10 @@ __global__ __launch_bounds__(256, 2) void ncf32_kernel(
     const float* __restrict__ wm, const float* __restrict__ bp, int64_t B, int64_t I,
     int64_t ipp, const int64_t* __restrict__ mptr, const int32_t* __restrict__ midx, int K,
     float* __restrict__ cand_v, int32_t* __restrict__ cand_i, int NP,
-    float* __restrict__ dense, int64_t ldo) {
+    float* __restrict__ dense, int64_t ldo, const int32_t* __restrict__ rows,
+    const int32_t* __restrict__ nrows) {
+  // rows != nullptr: batch row b is request row rows[b], b < *nrows (device-side list of
+  // the rows the certified path queued); candidates stay at the compact index b.
   constexpr int KS = 32;          // MFMA k-steps of layer 2 (h1 <= 64) and of GMF (mf <= 64)
   constexpr int RS = 68;          // LDS row stride (floats): conflict-free b128 reads
   constexpr int NU = 128;         // users per workgroup
@@ -52,6 +59,9 @@ __global__ __launch_bounds__(256, 2) void ncf32_kernel(
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5, j = lane & 31;
   const int64_t ublk = (int64_t)blockIdx.x * NU;
+  if (rows) B = *nrows;
+  if (ublk >= B) return;  // whole workgroup: before any barrier
+  auto R = [&](int64_t b) -> int64_t { return rows ? (int64_t)rows[b] : b; };
   const int64_t u0 = ublk + wave * 32;  // first user of this wave
   const int nu = (int)std::max<int64_t>(0, std::min<int64_t>(32, B - u0));
   const int p = blockIdx.y;
@@ -63,7 +73,7 @@ __global__ __launch_bounds__(256, 2) void ncf32_kernel(
   for (int e = tid; e < NU * 16; e += 256) {
     const int r = e >> 4, c = e & 15;
     float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (ublk + r < B) v = *reinterpret_cast<const float4*>(Pu + (ublk + r) * 64 + 4 * c);
+    if (ublk + r < B) v = *reinterpret_cast<const float4*>(Pu + R(ublk + r) * 64 + 4 * c);
     *reinterpret_cast<float4*>(&ps[r * 64 + 4 * c]) = v;
   }
   // A operands: W2 rows (hidden unit j), and this wave's users' wp_gmf*g_u rows
@@ -75,7 +85,7 @@ __global__ __launch_bounds__(256, 2) void ncf32_kernel(
   }
   {
     const bool ok = j < nu;
-    const float* row = WGu + (u0 + (ok ? j : 0)) * 64 + h * KS;
+    const float* row = WGu + (ok ? R(u0 + j) : 0) * 64 + h * KS;
 #pragma unroll
     for (int s4 = 0; s4 < KS / 4; ++s4) {
       float4 v = ok ? *reinterpret_cast<const float4*>(row + 4 * s4) : make_float4(0.f, 0.f, 0.f, 0.f);
@@ -100,7 +110,8 @@ __global__ __launch_bounds__(256, 2) void ncf32_kernel(
   int nm = INT_BIG, mpos = 0, mend = 0;
   const bool masked = !DENSE && mptr != nullptr;
   if (masked && lane < nu) {
-    const int64_t lo = mptr[u0 + lane], hi = mptr[u0 + lane + 1];
+    const int64_t ur = R(u0 + lane);
+    const int64_t lo = mptr[ur], hi = mptr[ur + 1];
     mpos = (int)mask_lower_bound(midx, lo, hi, (int)part_start);
     mend = (int)hi;
     nm = mpos < mend ? midx[mpos] : INT_BIG;
@@ -566,57 +577,68 @@ static hnm_status ncf_check(const hnm_ncf_weights* w) {
 }
 
 template <bool DENSE>
-static void launch_ncf32(hnm_ctx* ctx, dim3 grid, const float* Pu, const float* WGu,
-                         const float* Qi, const float* Gi, int64_t ldg, const hnm_ncf_weights* w,
+static void launch_ncf32(hnm_ctx* ctx, dim3 grid, const NcfTabs& t, const hnm_ncf_weights* w,
                          int64_t B, int64_t ipp, const int64_t* mptr, const int32_t* midx, int K,
-                         float* cv, int32_t* ci, int NP, float* dense, int64_t ldo) {
+                         float* cv, int32_t* ci, int NP, float* dense, int64_t ldo,
+                         const int32_t* rows = nullptr, const int32_t* nrows = nullptr) {
   const size_t lds = DENSE ? 0 : (size_t)4 * 32 * K * 8;
-  hipLaunchKernelGGL((ncf32_kernel<DENSE>), grid, dim3(256), lds, ctx->stream, Pu, WGu, Qi, Gi,
-                     ldg, w->mf, w->w2, w->h1, w->h2, w->b2, w->wp + w->mf, w->bp, B, w->num_items,
-                     ipp, mptr, midx, K, cv, ci, NP, dense, ldo);
+  hipLaunchKernelGGL((ncf32_kernel<DENSE>), grid, dim3(256), lds, ctx->stream, t.Pu, t.WGu, t.Qi,
+                     t.G, t.ldg, w->mf, w->w2, w->h1, w->h2, w->b2, w->wp + w->mf, w->bp, B,
+                     w->num_items, ipp, mptr, midx, K, cv, ci, NP, dense, ldo, rows, nrows);
 }
 
 template <int WU, int H1P, int MFH, bool DENSE>
-static void launch_ncf(hnm_ctx* ctx, dim3 grid, const float* Pu, const float* WGu,
-                       const float* Qi, const float* Gi, int64_t ldg, const hnm_ncf_weights* w,
+static void launch_ncf(hnm_ctx* ctx, dim3 grid, const NcfTabs& t, const hnm_ncf_weights* w,
                        int64_t B, int64_t ipp, const int64_t* mptr, const int32_t* midx, int K,
                        float* cv, int32_t* ci, int NP, float* dense, int64_t ldo) {
   hipLaunchKernelGGL((ncf_generic_kernel<WU, H1P, MFH, DENSE>), grid, dim3(256), 0, ctx->stream,
-                     Pu, WGu, Qi, Gi, ldg, w->w2, w->h1, w->h2, w->b2, w->wp + w->mf, w->bp, B,
-                     w->num_items, ipp, mptr, midx, K, cv, ci, NP, dense, ldo);
+                     t.Pu, t.WGu, t.Qi, t.G, t.ldg, w->w2, w->h1, w->h2, w->b2, w->wp + w->mf,
+                     w->bp, B, w->num_items, ipp, mptr, midx, K, cv, ci, NP, dense, ldo);
 }
 
-template <bool DENSE>
-static hnm_status ncf_common(hnm_ctx* ctx, const hnm_ncf_weights* w, const int64_t* ids,
-                             int64_t B, const int64_t* mptr, const int32_t* midx, int K,
-                             float* ov, int64_t* oi, float* dense, int64_t ldo) {
-  hnm_status st = ncf_check(w);
-  if (st) return st;
-  HNM_REQUIRE(ctx && ids, HNM_EINVAL, "ncf: NULL argument");
-  if (B <= 0) return HNM_OK;
-  const bool big = w->h1 > 64 || w->mf > 64;  // generic kernel; else the 32-user kernel
-  const int H1P = big ? 128 : 64, MFH = big ? 64 : 32, GW = 2 * MFH;
+size_t ncf_list_bytes(int64_t B, int64_t I, int K, int num_cus) {
+  const Partition part = choose_partition(I, hnm_cdiv(B, 128), num_cus);
+  return hnm_align((size_t)B * part.np * K * 4);
+}
+
+hnm_status ncf_list_rows(hnm_ctx* ctx, const hnm_ncf_weights* w, const NcfTabs& t, int64_t B,
+                         const int64_t* mptr, const int32_t* midx, int K, const int32_t* rows,
+                         const int32_t* nrows, float* cv, int32_t* ci, float* ov, int64_t* oi) {
+  const int64_t ublocks = hnm_cdiv(B, 128);
+  const Partition part = choose_partition(w->num_items, ublocks, ctx->num_cus);
+  launch_ncf32<false>(ctx, dim3((unsigned)ublocks, (unsigned)part.np), t, w, B, part.ipp, mptr,
+                      midx, K, cv, ci, part.np, nullptr, 0, rows, nrows);
+  HNM_LAUNCH_CHECK();
+  return hnm_topk_merge_rows(ctx, cv, ci, B, 1, 0, (int64_t)part.np * K, part.np * K, K, ov, oi,
+                             rows, nrows);
+}
+
+// Per-call tables: P_u, wp*g_u (users), Q_i (items), the GMF item table (padded copy when
+// needed), then `extra` bytes of scratch for the caller.
+struct NcfCall {
+  NcfTabs t;
+  bool big;
+  void* extra;
+};
+
+static hnm_status ncf_tables(hnm_ctx* ctx, const hnm_ncf_weights* w, const int64_t* ids,
+                             int64_t B, size_t extra, NcfCall* out) {
+  const bool big = w->h1 > 64 || w->mf > 64;  // generic kernel; else the 32-user kernels
+  const int H1P = big ? 128 : 64, GW = big ? 128 : 64;
   const int64_t I = w->num_items;
-  const int WU = B >= 256 ? 4 : 1;
-  const int64_t ublocks = big ? hnm_cdiv(B, 4 * WU) : hnm_cdiv(B, 128);
-  Partition part = choose_partition(I, ublocks, ctx->num_cus);
-  // workspace: Pu [B,H1P], WGu [B,GW], Qi [I,H1P], G copy [I,GW] (if needed), candidates
   const bool gcopy = (big ? w->mf != GW : w->mf % 4 != 0) || ((uintptr_t)w->gmf_item % 16 != 0);
   const size_t szP = hnm_align((size_t)B * H1P * 4), szW = hnm_align((size_t)B * GW * 4);
   const size_t szQ = hnm_align((size_t)I * H1P * 4), szG = gcopy ? hnm_align((size_t)I * GW * 4) : 0;
-  const size_t ncand = DENSE ? 0 : (size_t)B * part.np * K;
-  const size_t szC = hnm_align(ncand * 4);
   void* wsp;
-  st = hnm_workspace(ctx, szP + szW + szQ + szG + 2 * szC, &wsp);
+  hnm_status st = hnm_workspace(ctx, szP + szW + szQ + szG + extra, &wsp);
   if (st) return st;
   char* base = (char*)wsp;
   float* Pu = (float*)base; base += szP;
   float* WGu = (float*)base; base += szW;
   float* Qi = (float*)base; base += szQ;
   float* Gc = (float*)base; base += szG;
-  float* cv = (float*)base; base += szC;
-  int32_t* ci = (int32_t*)base;
-
+  out->extra = base;
+  out->big = big;
   if (w->h1 < H1P) {
     HNM_HIP_CHECK(hipMemsetAsync(Pu, 0, szP, ctx->stream));
     HNM_HIP_CHECK(hipMemsetAsync(Qi, 0, szQ, ctx->stream));
@@ -641,19 +663,45 @@ static hnm_status ncf_common(hnm_ctx* ctx, const hnm_ncf_weights* w, const int64
     G = Gc;
     ldg = GW;
   }
+  out->t = {Pu, WGu, Qi, G, ldg};
+  return HNM_OK;
+}
+
+template <bool DENSE>
+static hnm_status ncf_common(hnm_ctx* ctx, const hnm_ncf_weights* w, const int64_t* ids,
+                             int64_t B, const int64_t* mptr, const int32_t* midx, int K,
+                             float* ov, int64_t* oi, float* dense, int64_t ldo) {
+  hnm_status st = ncf_check(w);
+  if (st) return st;
+  HNM_REQUIRE(ctx && ids, HNM_EINVAL, "ncf: NULL argument");
+  if (B <= 0) return HNM_OK;
+  const int64_t I = w->num_items;
+  const bool big = w->h1 > 64 || w->mf > 64;
+  const bool cert = !DENSE && !big && ctx->prefilter && ncf_cert_eligible(w, K);
+  const int WU = B >= 256 ? 4 : 1;
+  const int64_t ublocks = big ? hnm_cdiv(B, 4 * WU) : hnm_cdiv(B, 128);
+  const Partition part = choose_partition(I, ublocks, ctx->num_cus);
+  const size_t szC = DENSE ? 0 : hnm_align((size_t)B * part.np * K * 4);
+  const size_t extra = cert ? ncf_cert_bytes(B, I, K, ctx->num_cus) : 2 * szC;
+  NcfCall c;
+  st = ncf_tables(ctx, w, ids, B, extra, &c);
+  if (st) return st;
+  if (cert) return ncf_cert_topk(ctx, w, c.t, B, mptr, midx, K, c.extra, ov, oi);
+  float* cv = (float*)c.extra;
+  int32_t* ci = (int32_t*)((char*)c.extra + szC);
 
   dim3 grid((unsigned)ublocks, (unsigned)part.np);
 #define HNM_NCF(WUV)                                                                          \
   if (big)                                                                                    \
-    launch_ncf<WUV, 128, 64, DENSE>(ctx, grid, Pu, WGu, Qi, G, ldg, w, B, part.ipp, mptr,     \
-                                    midx, K, cv, ci, part.np, dense, ldo);                    \
+    launch_ncf<WUV, 128, 64, DENSE>(ctx, grid, c.t, w, B, part.ipp, mptr, midx, K, cv, ci,    \
+                                    part.np, dense, ldo);                                     \
   else                                                                                        \
-    launch_ncf<WUV, 64, 32, DENSE>(ctx, grid, Pu, WGu, Qi, G, ldg, w, B, part.ipp, mptr, midx, \
-                                   K, cv, ci, part.np, dense, ldo);
+    launch_ncf<WUV, 64, 32, DENSE>(ctx, grid, c.t, w, B, part.ipp, mptr, midx, K, cv, ci,     \
+                                   part.np, dense, ldo);
   hnm_timer_begin(ctx);
   if (!big) {
-    launch_ncf32<DENSE>(ctx, grid, Pu, WGu, Qi, G, ldg, w, B, part.ipp, mptr, midx, K, cv, ci,
-                        part.np, dense, ldo);
+    launch_ncf32<DENSE>(ctx, grid, c.t, w, B, part.ipp, mptr, midx, K, cv, ci, part.np, dense,
+                        ldo);
   } else if (WU == 4) {
     HNM_NCF(4)
   } else {
@@ -681,6 +729,22 @@ extern "C" hnm_status hnm_ncf_scores_f32(hnm_ctx* ctx, const hnm_ncf_weights* w,
                                          int64_t ldo) {
   HNM_REQUIRE(out && w && ldo >= w->num_items, HNM_EINVAL, "ncf_scores: bad output");
   return ncf_common<true>(ctx, w, user_ids, B, nullptr, nullptr, 1, nullptr, nullptr, out, ldo);
+}
+
+extern "C" hnm_status hnm_ncf_prefilter_debug_f32(hnm_ctx* ctx, const hnm_ncf_weights* w,
+                                                  const int64_t* user_ids, int64_t B,
+                                                  float* approx, int64_t lda, float* bound) {
+  hnm_status st = ncf_check(w);
+  if (st) return st;
+  HNM_REQUIRE(ctx && user_ids && approx && bound && lda >= w->num_items, HNM_EINVAL,
+              "ncf_prefilter_debug: bad argument");
+  HNM_REQUIRE(w->h1 <= 64 && w->mf <= 64, HNM_EUNSUPPORTED,
+              "ncf_prefilter_debug: the f16 pre-filter covers h1 <= 64, mf <= 64");
+  if (B <= 0) return HNM_OK;
+  NcfCall c;
+  st = ncf_tables(ctx, w, user_ids, B, ncf_cert_bytes(B, w->num_items, 1, ctx->num_cus), &c);
+  if (st) return st;
+  return ncf_cert_debug(ctx, w, c.t, B, c.extra, approx, lda, bound);
 }
 
 extern "C" hnm_status hnm_ncf_pair_scores_f32(hnm_ctx* ctx, const hnm_ncf_weights* w,

@@ -1,0 +1,860 @@
+// NeuralCF top-K with a CERTIFIED f16 pre-filter and exact fp32 re-scoring
+// (neural_cf.py:300-326 recommend over :143-208 predict_all_items).
+//
+// The fp32 MFMA rate is 1/16 of the f16 rate on gfx950, and the NCF pair MLP is MFMA-bound.
+// So the all-items scan runs in f16 (v_mfma_f32_32x32x16_f16, fp32 accumulate) and only
+// PRUNES; every returned score is recomputed in exact fp32 by the same arithmetic as the
+// fp32 kernel (ncf32_kernel), so outputs are bit-identical to the fp32 path.  Pruning is
+// safe because of a rigorous per-user error bound E_u:
+//
+//   |approx(u, i) - (exact(u, i) - bp)| <= E_u   for every item i            (*)
+//
+// Let T = the K-th best exact score of user u (bp excluded) and e(u, i) the bound of (*) for
+// pair (u, i).  A strided item sample scored by the f16 kernel gives L_u = K-th best of
+// (approx - e) over the sample <= T.  Every item of the exact top-K has approx + e >= exact
+// >= T >= L_u, so the main f16 pass appends every item with approx + e(u, i) >= L_u, and
+// the exact top-K of the appended candidates IS the exact top-K.  Rows whose candidate
+// segments overflow (or whose bound is not usable) are recomputed by the exact fp32 kernel
+// over all items (on-device fallback).  No atomics in the scan: a wave owns its 32 users
+// within its item partition, so per-(user, partition) counters live in registers.
+//
+// Bound (*).  Let z_k = |P_k| + |Q_k| (the fp32 layer-1 values both paths read), v_k =
+// sum_j |wm_j||W2_jk|, A_u = sum_k v_k |P_uk|, B_i = sum_k v_k |Q_ik|, c0 = sum_j |wm_j b2_j|,
+// C_u = ||wp_gmf * g_u||_2, D_i = ||g_i||_2.  With f16 unit roundoff u = 2^-11, RNE
+// conversions (denormals kept: tools/mfma_semantics_probe.hip) and products exact in the
+// fp32 accumulator: the layer-1 sum and its operands contribute <= 2.01u z_k, W2 rounding
+// u|W2|, so |dH_j| <= 3.02u sum_k |W2_jk| z_k; relu is 1-Lipschitz; rounding relu(H) and wm
+// adds 2u |wm_j| R_j with R_j = |b2_j| + sum_k |W2_jk| z_k; the GMF dot adds 2.01u C_u D_i;
+// fp32 accumulation of both paths (<= 110 * 2^-24 relative) and the final adds are far
+// below u.  Hence |err| <= 5.1u (c0 + A_u + B_i) + 2.1u C_u D_i + (subnormal terms) and
+// we use e(u, i) = 6u (c0 + A_u + B_i + C_u D_i) + abs_slack.
+// tests/test_gpu_prefilter.py checks (*) pair by pair on the full catalogue.
+//
+// Scaling: every f16 operand is scaled by a power of two so its magnitude is <= 1 (layer-1
+// inputs <= 0.5, which also makes the packed add's [0,1] CLAMP an exact ReLU:
+// v_pk_add_f16 ... clamp).  Scores are compared in the scaled unit s1*sw*sm.
+#include <algorithm>
+
+#include "hnm_device.h"
+#include "ncf_internal.h"
+
+typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+
+hnm_status hnm_topk_merge_rows(hnm_ctx* ctx, const float* cv, const int32_t* ci, int64_t B,
+                               int64_t G, int64_t gstride, int64_t bstride, int kc, int k,
+                               float* ov, int64_t* oi, const int32_t* rows,
+                               const int32_t* nrows);
+
+namespace {
+
+constexpr int64_t CERT_MIN_ITEMS = 8192;  // below this the exact LIST kernel is cheaper
+constexpr int64_t CERT_SAMPLE = 12288;    // sample items for the threshold pass
+constexpr float CERT_RHO = 0.0029296875f; // 6 u16 = 3 * 2^-10
+constexpr int CERT_MAX_NP = 64;           // item partitions (candidate segments per row)
+
+enum { CM_P, CM_Q, CM_WG, CM_G, CM_B, CM_D, CM_N };
+
+struct CertParams {
+  unsigned mx[CM_N];  // float bits of non-negative maxima (NaN-propagating atomicMax)
+  float s1, sw, sm, sgu, sgi;
+  float unit, cg;     // scaled score unit; GMF accumulator -> score unit
+  float c0, absb, Bmax, Dmax;
+  int bad;            // bound not usable: every row takes the exact fallback
+};
+
+__device__ __forceinline__ float nmax(float a, float b) { return (b > a || b != b) ? b : a; }
+
+__device__ __forceinline__ float wave_sum(float x) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) x += __shfl_xor(x, o);
+  return x;
+}
+__device__ __forceinline__ float wave_max(float x) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) x = nmax(x, __shfl_xor(x, o));
+  return x;
+}
+
+// layer-1 unit stored at pair-permuted position t (x[h*32+s] = x[2s+h])
+__device__ __forceinline__ int korig(int t) { return 2 * (t & 31) + (t >> 5); }
+
+// ------------------------------------------------------------------ bound statistics
+__global__ __launch_bounds__(256) void cert_stats_kernel(NcfTabs t, int64_t B, int64_t I, int mf,
+                                                         const float* __restrict__ W2, int h1,
+                                                         int h2, const float* __restrict__ wm,
+                                                         CertParams* prm, float* __restrict__ Au,
+                                                         float* __restrict__ Cu,
+                                                         float* __restrict__ Bi,
+                                                         float* __restrict__ Di, int item_blocks,
+                                                         int user_blocks) {
+  __shared__ float vs[64];
+  __shared__ float red[4][4];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (tid < 64) {
+    float v = 0.f;
+    const int k = korig(tid);
+    if (k < h1)
+      for (int j = 0; j < h2; ++j) v += fabsf(wm[j]) * fabsf(W2[j * h1 + k]);
+    vs[tid] = v;
+  }
+  __syncthreads();
+  const float vt = vs[lane];
+  float m0 = 0.f, m1 = 0.f, m2 = 0.f, m3 = 0.f;  // items: Q, G, B, D / users: P, WG
+  const bool items = (int)blockIdx.x < item_blocks;
+  if (items) {
+    for (int64_t i = (int64_t)blockIdx.x * 4 + wave; i < I; i += (int64_t)item_blocks * 4) {
+      const float aq = fabsf(t.Qi[i * 64 + lane]);
+      const float g = lane < mf ? t.G[i * t.ldg + lane] : 0.f;
+      m0 = nmax(m0, aq);
+      m1 = nmax(m1, fabsf(g));
+      const float bq = wave_sum(vt * aq), dq = sqrtf(wave_sum(g * g));
+      m2 = nmax(m2, bq);
+      m3 = nmax(m3, dq);
+      if (lane == 0) {
+        Bi[i] = bq;
+        Di[i] = dq;
+      }
+    }
+  } else {
+    const int ub = (int)blockIdx.x - item_blocks;
+    for (int64_t b = (int64_t)ub * 4 + wave; b < B; b += (int64_t)user_blocks * 4) {
+      const float ap = fabsf(t.Pu[b * 64 + lane]);
+      const float wg = t.WGu[b * 64 + lane];
+      m0 = nmax(m0, ap);
+      m1 = nmax(m1, fabsf(wg));
+      const float a = wave_sum(vt * ap), c2 = wave_sum(wg * wg);
+      if (lane == 0) {
+        Au[b] = a;
+        Cu[b] = sqrtf(c2);
+      }
+    }
+  }
+  m0 = wave_max(m0);
+  m1 = wave_max(m1);
+  m2 = wave_max(m2);
+  m3 = wave_max(m3);
+  if (lane == 0) {
+    red[wave][0] = m0;
+    red[wave][1] = m1;
+    red[wave][2] = m2;
+    red[wave][3] = m3;
+  }
+  __syncthreads();
+  if (tid < 4) {
+    float m = red[0][tid];
+    for (int w = 1; w < 4; ++w) m = nmax(m, red[w][tid]);
+    // non-negative floats (and NaN) order like their bit patterns
+    const int slot = items ? (tid == 0 ? CM_Q : tid == 1 ? CM_G : tid == 2 ? CM_B : CM_D)
+                           : (tid == 0 ? CM_P : tid == 1 ? CM_WG : -1);
+    if (slot >= 0) atomicMax(&prm->mx[slot], __float_as_uint(m));
+  }
+}
+
+__device__ __forceinline__ float pow2_below_inv(float m) {  // 2^-e with m < 2^e (m > 0)
+  int e;
+  (void)frexpf(m, &e);
+  return ldexpf(1.f, -e);
+}
+
+// One block: weight statistics, scales, slack.
+__global__ __launch_bounds__(256) void cert_scales_kernel(const float* __restrict__ W2, int h1,
+                                                          int h2, const float* __restrict__ b2,
+                                                          const float* __restrict__ wm,
+                                                          const float* __restrict__ bp,
+                                                          CertParams* prm) {
+  __shared__ float red[6][4];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  float mW = 0.f, vsum = 0.f, mwm = 0.f, mb2 = 0.f, c0 = 0.f, swm = 0.f;
+  for (int e = tid; e < h2 * h1; e += 256) {
+    const float w = fabsf(W2[e]);
+    mW = nmax(mW, w);
+    vsum += fabsf(wm[e / h1]) * w;
+  }
+  for (int j = tid; j < h2; j += 256) {
+    mwm = nmax(mwm, fabsf(wm[j]));
+    mb2 = nmax(mb2, fabsf(b2[j]));
+    c0 += fabsf(wm[j]) * fabsf(b2[j]);
+    swm += fabsf(wm[j]);
+  }
+  mW = wave_max(mW);
+  mwm = wave_max(mwm);
+  mb2 = wave_max(mb2);
+  vsum = wave_sum(vsum);
+  c0 = wave_sum(c0);
+  swm = wave_sum(swm);
+  if (lane == 0) {
+    red[0][wave] = mW;
+    red[1][wave] = mwm;
+    red[2][wave] = mb2;
+    red[3][wave] = vsum;
+    red[4][wave] = c0;
+    red[5][wave] = swm;
+  }
+  __syncthreads();
+  if (tid != 0) return;
+  for (int w = 1; w < 4; ++w) {
+    red[0][0] = nmax(red[0][0], red[0][w]);
+    red[1][0] = nmax(red[1][0], red[1][w]);
+    red[2][0] = nmax(red[2][0], red[2][w]);
+    red[3][0] += red[3][w];
+    red[4][0] += red[4][w];
+    red[5][0] += red[5][w];
+  }
+  mW = red[0][0];
+  mwm = red[1][0];
+  mb2 = red[2][0];
+  vsum = red[3][0];
+  c0 = red[4][0];
+  swm = red[5][0];
+  const float mP = __uint_as_float(prm->mx[CM_P]), mQ = __uint_as_float(prm->mx[CM_Q]);
+  const float mWG = __uint_as_float(prm->mx[CM_WG]), mG = __uint_as_float(prm->mx[CM_G]);
+  const float Bmax = __uint_as_float(prm->mx[CM_B]), Dmax = __uint_as_float(prm->mx[CM_D]);
+  const float lim = 1099511627776.f;  // 2^40
+  bool bad = false;
+  for (float m : {mP, mQ, mWG, mG, Bmax, Dmax, mW, mwm, mb2, vsum, c0, fabsf(bp[0])})
+    bad |= !(m <= lim);  // also catches NaN / inf
+  const float zmax = mP + mQ;
+  const float s1 = zmax > 0.f ? 0.5f * pow2_below_inv(zmax) : 1.f;  // s1 * z <= 0.5
+  const float sw = mW > 0.f ? pow2_below_inv(mW) : 1.f;
+  const float sm = mwm > 0.f ? pow2_below_inv(mwm) : 1.f;
+  const float sgu = mWG > 0.f ? pow2_below_inv(mWG) : 1.f;
+  const float sgi = mG > 0.f ? pow2_below_inv(mG) : 1.f;
+  const float unit = s1 * sw * sm;
+  const float cg = unit / (sgu * sgi);
+  // f16 range of the scaled layer-2 pre-activation: |H~| <= s1 sw |b2| + 0.5 * 64
+  bad |= !(s1 * sw * mb2 <= 30000.f);
+  bad |= !(unit >= 1e-30f && unit <= 1e30f && cg >= 1e-30f && cg <= 1e30f);
+  const float phi = 2.98023224e-08f;  // 2^-25: half the f16 subnormal spacing
+  const float rmax = mb2 + 64.f * mW * zmax;
+  const float absb = 16.f * phi *
+                         (3.f * vsum / s1 + 64.f * swm * zmax / sw + swm / (s1 * sw) +
+                          32.f * rmax / sm + 64.f * mG / sgu + 64.f * mWG / sgi) +
+                     2.4e-7f * fabsf(bp[0]);
+  prm->s1 = s1;
+  prm->sw = sw;
+  prm->sm = sm;
+  prm->sgu = sgu;
+  prm->sgi = sgi;
+  prm->unit = unit;
+  prm->cg = cg;
+  prm->c0 = c0;
+  prm->absb = absb;
+  prm->Bmax = Bmax;
+  prm->Dmax = Dmax;
+  prm->bad = bad || !(absb <= lim);
+}
+
+// f16 operand tables.  Q16/P16 keep the pair-permuted order (the layer-1 unit order is
+// free as long as W2h's columns follow it); G16/WG16 use the natural GMF order.
+__global__ __launch_bounds__(256) void cert_convert_kernel(
+    NcfTabs t, int64_t B, int64_t I, int mf, const CertParams* __restrict__ prm,
+    _Float16* __restrict__ P16, _Float16* __restrict__ WG16, _Float16* __restrict__ Q16,
+    _Float16* __restrict__ G16, const float* __restrict__ W2, int h1, int h2,
+    const float* __restrict__ b2, const float* __restrict__ wm, _Float16* __restrict__ W2h,
+    _Float16* __restrict__ wmh, float* __restrict__ b2s) {
+  const float s1 = prm->s1, sgu = prm->sgu, sgi = prm->sgi;
+  const int64_t nthreads = (int64_t)gridDim.x * 256;
+  const int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  // items: 16 chunks of 4 per row
+  for (int64_t e = g; e < I * 16; e += nthreads) {
+    const int64_t i = e >> 4;
+    const int c = (int)(e & 15);
+    const float4 q = *reinterpret_cast<const float4*>(t.Qi + i * 64 + 4 * c);
+    _Float16* qo = Q16 + i * 64 + 4 * c;
+    qo[0] = (_Float16)(q.x * s1);
+    qo[1] = (_Float16)(q.y * s1);
+    qo[2] = (_Float16)(q.z * s1);
+    qo[3] = (_Float16)(q.w * s1);
+    float4 gv = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (4 * c < mf) gv = *reinterpret_cast<const float4*>(t.G + i * t.ldg + 4 * c);
+    _Float16* go = G16 + i * 64 + 4 * c;
+    go[0] = (_Float16)(4 * c + 0 < mf ? gv.x * sgi : 0.f);
+    go[1] = (_Float16)(4 * c + 1 < mf ? gv.y * sgi : 0.f);
+    go[2] = (_Float16)(4 * c + 2 < mf ? gv.z * sgi : 0.f);
+    go[3] = (_Float16)(4 * c + 3 < mf ? gv.w * sgi : 0.f);
+  }
+  for (int64_t e = g; e < B * 64; e += nthreads) {
+    const int64_t b = e >> 6;
+    const int k = (int)(e & 63);
+    P16[e] = (_Float16)(t.Pu[e] * s1);
+    WG16[e] = (_Float16)(t.WGu[b * 64 + (k & 1) * 32 + (k >> 1)] * sgu);
+  }
+  if (blockIdx.x == 0) {
+    const float sw = prm->sw, sm = prm->sm;
+    for (int e = threadIdx.x; e < 32 * 64; e += 256) {
+      const int j = e >> 6, k = korig(e & 63);
+      W2h[e] = (_Float16)((j < h2 && k < h1) ? W2[j * h1 + k] * sw : 0.f);
+    }
+    if (threadIdx.x < 32) {
+      const int j = threadIdx.x;
+      wmh[j] = (_Float16)(j < h2 ? wm[j] * sm : 0.f);
+      b2s[j] = j < h2 ? b2[j] * s1 * sw : 0.f;
+    }
+  }
+}
+
+// ------------------------------------------------------------------ f16 scan kernel
+// SAMPLE: dense[b][n] = approx - e_i (scanned item n = n * istride), e_i = the per-item part
+//         of the bound, 6u unit (B_i + C_u D_i);
+// THRESH: append item n to segment (b, partition) when approx + e_i >= tau_b;
+// DEBUG:  dense[b][n] = approx, dense2[b][n] = Eu_b + e_i (the whole bound), scaled units.
+enum { SCAN_SAMPLE = 0, SCAN_THRESH = 1, SCAN_DEBUG = 2 };
+
+struct ScanArgs {
+  const _Float16* P16;   // [B, 64]
+  const _Float16* WG16;  // [B, 64]
+  const _Float16* Q16;   // [Itot, 64]
+  const _Float16* G16;   // [Itot, 64]
+  const _Float16* W2h;   // [32, 64]
+  const _Float16* wmh;   // [32]
+  const float* b2s;      // [32]
+  const float* Bi;       // [Itot] per-item bound terms
+  const float* Di;
+  const float* Cu;       // [B] per-user bound terms
+  const float* Eu;       // [B] user-constant part of the bound, scaled (DEBUG)
+  const CertParams* prm;
+  int64_t B;
+  int64_t I;        // scanned items (sample count for the sample pass)
+  int64_t istride;  // scanned item n is item n * istride
+  int64_t ipp;
+  int NP;
+  const int64_t* mptr;
+  const int32_t* midx;
+  const float* tau;  // [B] scaled thresholds (THRESH)
+  int* cnt;          // [B, NP] appended counts (THRESH)
+  int32_t* buf;      // [B, NP, capp] appended item ids (THRESH)
+  int capp;
+  float* dense;      // [B, ldo]
+  float* dense2;     // [B, ldo] (DEBUG)
+  int64_t ldo;
+};
+
+__device__ __forceinline__ f32x16 mfma16(h8 a, h8 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+}
+
+// A wave owns 32 users, a workgroup 128; 32-item tiles of Q16/G16 go through LDS.
+// Per (user, tile): 4 f16 MFMAs for layer 2 (B = clamp(P~ + Q~), built with 16 packed
+// adds), 2 f16 MFMAs for wm . relu(H) (the accumulator tile reused as the B operand),
+// GMF once per tile for all 32 users (4 MFMAs).  v_mfma_f32_32x32x16_f16 B operand:
+// lane (j, h) holds B[k = 8h + e][col j], e = 0..7.
+template <int MODE>
+__global__ __launch_bounds__(256, 2) void ncf16_scan_kernel(ScanArgs A) {
+  constexpr int RS = 72;   // LDS row stride in halfs (144 B): conflict-free b128 reads
+  constexpr int NU = 128;  // users per workgroup
+  __shared__ __attribute__((aligned(16))) _Float16 qs[TILE * RS];
+  __shared__ __attribute__((aligned(16))) _Float16 gs[TILE * RS];
+  __shared__ __attribute__((aligned(16))) _Float16 ps[NU * 64];
+  __shared__ float gsm[4][32][33];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5, j = lane & 31;
+  const int64_t ublk = (int64_t)blockIdx.x * NU;
+  const int64_t u0 = ublk + wave * 32;
+  const int nu = (int)std::max<int64_t>(0, std::min<int64_t>(32, A.B - u0));
+  const int p = blockIdx.y;
+  const int64_t part_start = (int64_t)p * A.ipp;
+  const int64_t part_end = std::min<int64_t>(A.I, part_start + A.ipp);
+
+  for (int e = tid; e < NU * 8; e += 256) {
+    const int r = e >> 3, c = e & 7;
+    h8 v = {};
+    if (ublk + r < A.B) v = *reinterpret_cast<const h8*>(A.P16 + (ublk + r) * 64 + 8 * c);
+    *reinterpret_cast<h8*>(&ps[r * 64 + 8 * c]) = v;
+  }
+  h8 aw[4], ag[4], awm[2];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    aw[s] = *reinterpret_cast<const h8*>(A.W2h + j * 64 + 16 * s + 8 * h);
+    h8 z = {};
+    ag[s] = j < nu ? *reinterpret_cast<const h8*>(A.WG16 + (u0 + j) * 64 + 16 * s + 8 * h) : z;
+  }
+#pragma unroll
+  for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) awm[s2][e] = A.wmh[mfma32_row(8 * s2 + e, h)];
+  f32x16 b2c;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) b2c[r] = A.b2s[mfma32_row(r, h)];
+  const float cg = A.prm->cg;
+  const float ru = CERT_RHO * A.prm->unit;
+  // per-user registers: lane u < nu follows user u0 + u
+  const float cu = lane < nu ? ru * A.Cu[u0 + lane] : 0.f;
+  float tv = __builtin_inff(), eu = 0.f;
+  if (MODE == SCAN_THRESH && lane < nu) tv = A.tau[u0 + lane];
+  if (MODE == SCAN_DEBUG && lane < nu) eu = A.Eu[u0 + lane];
+  int ccount = 0;  // THRESH: appended items of user u0 + lane in this partition
+  int nm = INT_BIG, mpos = 0, mend = 0;
+  const bool masked = MODE == SCAN_THRESH && A.mptr != nullptr;
+  if (masked && lane < nu) {
+    const int64_t lo = A.mptr[u0 + lane], hi = A.mptr[u0 + lane + 1];
+    mpos = (int)mask_lower_bound(A.midx, lo, hi, (int)part_start);
+    mend = (int)hi;
+    nm = mpos < mend ? A.midx[mpos] : INT_BIG;
+  }
+  int32_t* seg = MODE == SCAN_THRESH ? A.buf + ((u0 * A.NP) + p) * (int64_t)A.capp : nullptr;
+  const int64_t segstride = (int64_t)A.NP * A.capp;  // next user's segment
+
+  const int64_t ntiles = part_end > part_start ? hnm_cdiv(part_end - part_start, TILE) : 0;
+  for (int64_t t = 0; t < ntiles; ++t) {
+    const int64_t base = part_start + t * TILE;
+    __syncthreads();
+    {
+      const int row = tid >> 3, c = tid & 7;
+      const int64_t n = base + row;
+      h8 q = {}, g = {};
+      if (n < part_end) {
+        const int64_t it = n * A.istride;
+        q = *reinterpret_cast<const h8*>(A.Q16 + it * 64 + 8 * c);
+        g = *reinterpret_cast<const h8*>(A.G16 + it * 64 + 8 * c);
+      }
+      *reinterpret_cast<h8*>(&qs[row * RS + 8 * c]) = q;
+      *reinterpret_cast<h8*>(&gs[row * RS + 8 * c]) = g;
+    }
+    __syncthreads();
+    if (nu == 0) continue;
+
+    {  // GMF of the wave's 32 users x 32 items, in score units
+      f32x16 gacc = {};
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+        gacc = mfma16(ag[s], *reinterpret_cast<const h8*>(&gs[j * RS + 16 * s + 8 * h]), gacc);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) gsm[wave][mfma32_row(r, h)][j] = gacc[r] * cg;
+    }
+    h8 q[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) q[s] = *reinterpret_cast<const h8*>(&qs[j * RS + 16 * s + 8 * h]);
+    const int64_t n = base + j;
+    const bool ivalid = h == 0 && n < part_end;
+    const int64_t itm = (ivalid ? n : part_start) * A.istride;
+    const float bj = ru * A.Bi[itm], dj = A.Di[itm];  // per-item bound terms of lane j's item
+    const int64_t tile_end = std::min<int64_t>(base + TILE, part_end);
+    unsigned mbits = 0;
+    if (masked) {  // scanned items are real items here (istride 1 in the THRESH pass)
+      uint64_t pend = __ballot(lane < 32 && nm < tile_end) & 0xffffffffull;
+      while (pend) {
+        const int u = __builtin_ctzll(pend);
+        pend &= pend - 1;
+        while (true) {
+          const int tgt = hnm_readlane_i(nm, u);
+          if (tgt >= tile_end) break;
+          if (lane == u) {
+            mbits |= 1u << (tgt - (int)base);
+            ++mpos;
+            nm = mpos < mend ? A.midx[mpos] : INT_BIG;
+          }
+        }
+      }
+    }
+
+    for (int u = 0; u < nu; ++u) {
+      const _Float16* pr = &ps[(wave * 32 + u) * 64 + 8 * h];
+      f32x16 acc = b2c;
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        h8 x = *reinterpret_cast<const h8*>(pr + 16 * s) + q[s];
+        x = __builtin_elementwise_min(__builtin_elementwise_max(x, (h8){}), (h8)(_Float16)1.f);
+        acc = mfma16(aw[s], x, acc);
+      }
+      h8 y0, y1;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        y0[e] = (_Float16)acc[e];
+        y1[e] = (_Float16)acc[8 + e];
+      }
+      y0 = __builtin_elementwise_max(y0, (h8){});
+      y1 = __builtin_elementwise_max(y1, (h8){});
+      f32x16 d = {};
+      d = mfma16(awm[0], y0, d);
+      d = mfma16(awm[1], y1, d);
+      const float score = d[0] + gsm[wave][u][j];
+      const float ei = fmaf(hnm_readlane_f(cu, u), dj, bj);
+      if (MODE == SCAN_SAMPLE) {
+        if (ivalid) A.dense[(u0 + u) * A.ldo + n] = score - ei;
+      } else if (MODE == SCAN_DEBUG) {
+        if (ivalid) {
+          A.dense[(u0 + u) * A.ldo + n] = score;
+          A.dense2[(u0 + u) * A.ldo + n] = hnm_readlane_f(eu, u) + ei;
+        }
+      } else {
+        bool pass = ivalid && !(score + ei < hnm_readlane_f(tv, u));
+        if (masked) pass = pass && !((hnm_readlane_i((int)mbits, u) >> j) & 1);
+        const uint64_t m = __ballot(pass);
+        if (m) {
+          const int pos = hnm_readlane_i(ccount, u) + __popcll(m & ((1ull << lane) - 1));
+          if (pass && pos < A.capp) seg[u * segstride + pos] = (int32_t)n;
+          if (lane == u) ccount += __popcll(m);
+        }
+      }
+    }
+  }
+  if (MODE == SCAN_THRESH && lane < nu) A.cnt[(u0 + lane) * A.NP + p] = ccount;
+}
+
+// Per row: Eu = user-constant part of the bound (scaled): 6u unit (c0 + A_u) + unit abs.
+// With the sample's K-th best of (approx - e_i), tau_u = Kth - 2 Eu - guard, where the
+// guard covers the fp32 rounding of the test quantities (<= a few 2^-24 of the row's
+// absolute score scale).  Rows with an unusable bound get tau = +inf and flag = 1.
+__global__ __launch_bounds__(256) void cert_tau_kernel(const float* __restrict__ kth, int K,
+                                                       const float* __restrict__ Au,
+                                                       const float* __restrict__ Cu,
+                                                       const CertParams* __restrict__ prm,
+                                                       int64_t B, float* __restrict__ tau,
+                                                       int* __restrict__ flag,
+                                                       float* __restrict__ Eu) {
+  const int64_t b = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (b >= B) return;
+  const float unit = prm->unit;
+  const float e = unit * (CERT_RHO * (prm->c0 + Au[b]) + prm->absb);
+  if (Eu) Eu[b] = e;
+  if (!kth) return;
+  const float scale = unit * (prm->c0 + Au[b] + prm->Bmax + Cu[b] * prm->Dmax);
+  const float kv = kth[b * K + (K - 1)];
+  float tv = kv - 2.f * e - 3.814697265625e-06f * scale;  // 2^-18 of the score scale
+  tv -= fabsf(tv) * 9.5367431640625e-07f;                 // 2^-20
+  const bool ok = !prm->bad && __builtin_isfinite(tv) && __builtin_isfinite(scale);
+  tau[b] = ok ? tv : __builtin_inff();
+  flag[b] = ok ? 0 : 1;
+}
+
+// ------------------------------------------------------------------ exact re-scoring
+// One wave per user: the exact fp32 score of each appended candidate, computed with the
+// arithmetic of ncf32_kernel (same MFMA chain for layer 2, the GMF dot as the fma chain
+// the f32 MFMA is bitwise equal to: tools/mfma_semantics_probe.hip (a)), then the exact
+// (score desc, item asc) top-K.  Candidates sit in NP per-partition segments; a row with a
+// flagged bound, an overflowing segment or fewer than K candidates is queued for the
+// fallback.
+__global__ __launch_bounds__(256, 2) void ncf_rescore_kernel(
+    NcfTabs t, int mf, const float* __restrict__ W2, int h1, int h2, const float* __restrict__ b2,
+    const float* __restrict__ wm, const float* __restrict__ bp, int64_t B,
+    const int* __restrict__ flag, const int* __restrict__ cnt, const int32_t* __restrict__ buf,
+    int NP, int capp, int K, float* __restrict__ ov, int64_t* __restrict__ oi,
+    int32_t* __restrict__ ovf_rows, int32_t* __restrict__ ovf_cnt,
+    unsigned long long* __restrict__ stats) {
+  constexpr int KS = 32;
+  __shared__ __attribute__((aligned(16))) float wgs[4][64];
+  __shared__ int pref[4][CERT_MAX_NP + 1];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5, j = lane & 31;
+  const int64_t b = (int64_t)blockIdx.x * 4 + wave;
+  const bool live = b < B;
+  int c = 0;
+  if (live) {
+    wgs[wave][lane] = t.WGu[b * 64 + lane];  // pair-permuted wp*g_u
+    c = lane < NP ? cnt[b * NP + lane] : 0;
+  }
+  // inclusive scan of the segment counts over the lanes
+  int incl = c;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int v = __shfl_up(incl, o);
+    if (lane >= o) incl += v;
+  }
+  if (live) {
+    if (lane == 0) pref[wave][0] = 0;
+    if (lane < NP) pref[wave][lane + 1] = incl;
+  }
+  __syncthreads();
+  if (!live) return;
+  const int n = hnm_readlane_i(incl, 63);
+  const bool over = __ballot(c > capp) != 0;
+  if (flag[b] || over || n < K) {
+    if (lane == 0) {
+      ovf_rows[atomicAdd(ovf_cnt, 1)] = (int32_t)b;
+      if (stats) {
+        atomicAdd(&stats[2], 1ull);
+        if (b == 0) atomicAdd(&stats[0], (unsigned long long)B);
+      }
+    }
+    return;
+  }
+  if (stats && lane == 0) {
+    atomicAdd(&stats[1], (unsigned long long)n);
+    if (b == 0) atomicAdd(&stats[0], (unsigned long long)B);
+  }
+  float a[KS];
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    const int k = 2 * s + h;
+    a[s] = (j < h2 && k < h1) ? W2[j * h1 + k] : 0.f;
+  }
+  f32x16 b2acc;
+  float wmr[16];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int i = mfma32_row(r, h);
+    b2acc[r] = i < h2 ? b2[i] : 0.f;
+    wmr[r] = i < h2 ? wm[i] : 0.f;
+  }
+  float p[KS];
+#pragma unroll
+  for (int s4 = 0; s4 < KS / 4; ++s4) {
+    const float4 v = *reinterpret_cast<const float4*>(t.Pu + b * 64 + h * KS + 4 * s4);
+    p[4 * s4] = v.x; p[4 * s4 + 1] = v.y; p[4 * s4 + 2] = v.z; p[4 * s4 + 3] = v.w;
+  }
+  const float bpv = bp[0];
+  WaveTopK<1> L;
+  L.init();
+  const int32_t* rowbuf = buf + b * (int64_t)NP * capp;
+  for (int c0 = 0; c0 < n; c0 += 32) {
+    const int g = c0 + j;
+    const bool ok = g < n;
+    int item = 0;
+    if (ok) {  // segment of candidate g: last p with pref[p] <= g
+      int lo = 0, hi = NP;
+      while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (pref[wave][mid] <= g) lo = mid;
+        else hi = mid;
+      }
+      item = rowbuf[(int64_t)lo * capp + (g - pref[wave][lo])];
+    }
+    // GMF: fma chain in the f32 MFMA's order (k = 2s, then 2s + 1)
+    float gm = 0.f;
+    const float* grow = t.G + (int64_t)item * t.ldg;
+    for (int c4 = 0; c4 < (mf + 3) / 4; ++c4) {
+      const float4 gv = *reinterpret_cast<const float4*>(grow + 4 * c4);
+      // pair-permuted: wgs[2c4], wgs[2c4+1] = k 4c4, 4c4+2; wgs[32+2c4], [32+2c4+1] = 4c4+1, 4c4+3
+      const float2 wv = *reinterpret_cast<const float2*>(&wgs[wave][2 * c4]);
+      const float2 wv1 = *reinterpret_cast<const float2*>(&wgs[wave][KS + 2 * c4]);
+      gm = fmaf(wv1.x, gv.y, fmaf(wv.x, gv.x, gm));
+      gm = fmaf(wv1.y, gv.w, fmaf(wv.y, gv.z, gm));
+    }
+    float q[KS];
+    const float* qrow = t.Qi + (int64_t)item * 64 + h * KS;
+#pragma unroll
+    for (int s4 = 0; s4 < KS / 4; ++s4) {
+      const float4 v = *reinterpret_cast<const float4*>(qrow + 4 * s4);
+      q[4 * s4] = v.x; q[4 * s4 + 1] = v.y; q[4 * s4 + 2] = v.z; q[4 * s4 + 3] = v.w;
+    }
+    f32x16 acc = b2acc;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) acc = mfma32x32x2(a[s], fmaxf(p[s] + q[s], 0.f), acc);
+    float m4[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int r = 0; r < 16; ++r) m4[r & 3] = fmaf(fmaxf(acc[r], 0.f), wmr[r], m4[r & 3]);
+    const float mlp = (m4[0] + m4[1]) + (m4[2] + m4[3]);
+    const float tot = hnm_sum_halves(mlp + (h == 0 ? gm : 0.f));
+    const float score = tot + bpv;
+    L.offer(score, item, ok && h == 0, K);
+  }
+  L.store(ov ? ov + b * K : nullptr, oi + b * K, K);
+}
+
+// scaled -> real units, for the diagnostics entry point
+__global__ void cert_unscale_kernel(float* __restrict__ a, float* __restrict__ e, int64_t lda,
+                                    int64_t B, int64_t I, const CertParams* __restrict__ prm) {
+  const int64_t x = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (x >= B * I) return;
+  const int64_t o = (x / I) * lda + x % I;
+  a[o] /= prm->unit;
+  e[o] /= prm->unit;
+}
+
+struct CertWs {
+  CertParams* prm;
+  float *Au, *Cu, *Bi, *Di, *tau, *Eu, *b2s, *kthv, *sdense;
+  int64_t* kthi;
+  int *cnt, *flag;
+  int32_t *buf, *ovf_cnt, *ovf_rows;
+  _Float16 *P16, *WG16, *Q16, *G16, *W2h, *wmh;
+  float* cv;
+  int32_t* ci;
+};
+
+struct CertShape {
+  int64_t stride, Ns;
+  Partition part;  // of the main scan
+  int capp;        // candidate slots per (row, partition)
+};
+
+CertShape cert_shape(int64_t B, int64_t I, int K, int num_cus) {
+  CertShape sh;
+  sh.stride = std::max<int64_t>(1, I / CERT_SAMPLE);
+  sh.Ns = hnm_cdiv(I, sh.stride);
+  Partition part = choose_partition(I, hnm_cdiv(B, 128), num_cus);
+  if (part.np > CERT_MAX_NP) {
+    part.ipp = hnm_cdiv(hnm_cdiv(I, CERT_MAX_NP), TILE) * TILE;
+    part.np = (int)hnm_cdiv(I, part.ipp);
+  }
+  sh.part = part;
+  // expected candidates ~ K * stride (the sample's K-th) plus the bound's margin; each
+  // partition gets 4x its even share, >= 64 slots
+  const int64_t total = std::min<int64_t>(8192, std::max<int64_t>(512, 16 * (int64_t)K * sh.stride));
+  sh.capp = (int)std::max<int64_t>(64, std::min<int64_t>(total, hnm_cdiv(4 * total, part.np)));
+  return sh;
+}
+
+// carve (or size, when base == nullptr) the scratch region
+size_t cert_carve(char* base, int64_t B, int64_t I, int K, int num_cus, CertWs* w) {
+  const CertShape sh = cert_shape(B, I, K, num_cus);
+  size_t off = 0;
+  auto take = [&](size_t bytes) {
+    char* p = base ? base + off : nullptr;
+    off += hnm_align(bytes);
+    return p;
+  };
+  CertWs x;
+  x.prm = (CertParams*)take(sizeof(CertParams));
+  x.Au = (float*)take(B * 4);
+  x.Cu = (float*)take(B * 4);
+  x.Bi = (float*)take(I * 4);
+  x.Di = (float*)take(I * 4);
+  x.tau = (float*)take(B * 4);
+  x.Eu = (float*)take(B * 4);
+  x.b2s = (float*)take(32 * 4);
+  x.kthv = (float*)take((size_t)B * K * 4);
+  x.kthi = (int64_t*)take((size_t)B * K * 8);
+  x.cnt = (int*)take((size_t)B * sh.part.np * 4);
+  x.flag = (int*)take(B * 4);
+  x.ovf_cnt = (int32_t*)take(256);
+  x.ovf_rows = (int32_t*)take(B * 4);
+  x.buf = (int32_t*)take((size_t)B * sh.part.np * sh.capp * 4);
+  x.sdense = (float*)take((size_t)B * sh.Ns * 4);
+  x.P16 = (_Float16*)take((size_t)B * 64 * 2);
+  x.WG16 = (_Float16*)take((size_t)B * 64 * 2);
+  x.Q16 = (_Float16*)take((size_t)I * 64 * 2);
+  x.G16 = (_Float16*)take((size_t)I * 64 * 2);
+  x.W2h = (_Float16*)take(32 * 64 * 2);
+  x.wmh = (_Float16*)take(32 * 2);
+  const size_t lb = ncf_list_bytes(B, I, K, num_cus);
+  x.cv = (float*)take(lb);
+  x.ci = (int32_t*)take(lb);
+  if (w) *w = x;
+  return off;
+}
+
+hnm_status cert_prepare(hnm_ctx* ctx, const hnm_ncf_weights* w, const NcfTabs& t, int64_t B,
+                        const CertWs& x) {
+  const int64_t I = w->num_items;
+  HNM_HIP_CHECK(hipMemsetAsync(x.prm, 0, sizeof(CertParams), ctx->stream));
+  const int ib = (int)std::min<int64_t>(1024, hnm_cdiv(I, 4));
+  const int ub = (int)std::min<int64_t>(256, hnm_cdiv(B, 4));
+  hipLaunchKernelGGL(cert_stats_kernel, dim3(ib + ub), dim3(256), 0, ctx->stream, t, B, I, w->mf,
+                     w->w2, w->h1, w->h2, w->wp + w->mf, x.prm, x.Au, x.Cu, x.Bi, x.Di, ib, ub);
+  HNM_LAUNCH_CHECK();
+  hipLaunchKernelGGL(cert_scales_kernel, dim3(1), dim3(256), 0, ctx->stream, w->w2, w->h1, w->h2,
+                     w->b2, w->wp + w->mf, w->bp, x.prm);
+  HNM_LAUNCH_CHECK();
+  const int cb = (int)std::min<int64_t>(2048, std::max<int64_t>(1, hnm_cdiv(I * 16, 256)));
+  hipLaunchKernelGGL(cert_convert_kernel, dim3(cb), dim3(256), 0, ctx->stream, t, B, I, w->mf,
+                     x.prm, x.P16, x.WG16, x.Q16, x.G16, w->w2, w->h1, w->h2, w->b2,
+                     w->wp + w->mf, x.W2h, x.wmh, x.b2s);
+  HNM_LAUNCH_CHECK();
+  return HNM_OK;
+}
+
+ScanArgs scan_args(const CertWs& x, int64_t B) {
+  ScanArgs a{};
+  a.P16 = x.P16;
+  a.WG16 = x.WG16;
+  a.Q16 = x.Q16;
+  a.G16 = x.G16;
+  a.W2h = x.W2h;
+  a.wmh = x.wmh;
+  a.b2s = x.b2s;
+  a.Bi = x.Bi;
+  a.Di = x.Di;
+  a.Cu = x.Cu;
+  a.Eu = x.Eu;
+  a.prm = x.prm;
+  a.B = B;
+  a.istride = 1;
+  return a;
+}
+
+}  // namespace
+
+bool ncf_cert_eligible(const hnm_ncf_weights* w, int K) {
+  return w->h1 <= 64 && w->mf <= 64 && w->h2 <= 32 && K <= 64 &&
+         w->num_items >= CERT_MIN_ITEMS && w->num_items >= 64 * (int64_t)K;
+}
+
+size_t ncf_cert_bytes(int64_t B, int64_t I, int K, int num_cus) {
+  return cert_carve(nullptr, B, I, K, num_cus, nullptr);
+}
+
+hnm_status ncf_cert_topk(hnm_ctx* ctx, const hnm_ncf_weights* w, const NcfTabs& t, int64_t B,
+                         const int64_t* mptr, const int32_t* midx, int K, void* scratch,
+                         float* ov, int64_t* oi) {
+  const int64_t I = w->num_items;
+  const CertShape sh = cert_shape(B, I, K, ctx->num_cus);
+  CertWs x;
+  cert_carve((char*)scratch, B, I, K, ctx->num_cus, &x);
+  hnm_status st = cert_prepare(ctx, w, t, B, x);
+  if (st) return st;
+  HNM_HIP_CHECK(hipMemsetAsync(x.ovf_cnt, 0, 4, ctx->stream));
+  const int64_t ublocks = hnm_cdiv(B, 128);
+  // 1. sample pass: approx - e of items 0, stride, ... -> K-th best per row -> tau
+  {
+    ScanArgs a = scan_args(x, B);
+    a.I = sh.Ns;
+    a.istride = sh.stride;
+    a.dense = x.sdense;
+    a.ldo = sh.Ns;
+    Partition ps = choose_partition(sh.Ns, ublocks, ctx->num_cus);
+    a.ipp = ps.ipp;
+    a.NP = ps.np;
+    hipLaunchKernelGGL(ncf16_scan_kernel<SCAN_SAMPLE>, dim3((unsigned)ublocks, (unsigned)ps.np),
+                       dim3(256), 0, ctx->stream, a);
+    HNM_LAUNCH_CHECK();
+    st = hnm_topk_rows_strided(ctx, x.sdense, sh.Ns, B, sh.Ns, mptr, midx, K, x.kthv, x.kthi,
+                               sh.stride);
+    if (st) return st;
+    hipLaunchKernelGGL(cert_tau_kernel, dim3((unsigned)hnm_cdiv(B, 256)), dim3(256), 0,
+                       ctx->stream, x.kthv, K, x.Au, x.Cu, x.prm, B, x.tau, x.flag, x.Eu);
+    HNM_LAUNCH_CHECK();
+  }
+  // 2. main f16 scan: append items with approx + e >= tau_u to per-partition segments
+  {
+    ScanArgs a = scan_args(x, B);
+    a.I = I;
+    a.mptr = mptr;
+    a.midx = midx;
+    a.tau = x.tau;
+    a.cnt = x.cnt;
+    a.buf = x.buf;
+    a.capp = sh.capp;
+    a.ipp = sh.part.ipp;
+    a.NP = sh.part.np;
+    hnm_timer_begin(ctx);
+    hipLaunchKernelGGL(ncf16_scan_kernel<SCAN_THRESH>,
+                       dim3((unsigned)ublocks, (unsigned)sh.part.np), dim3(256), 0, ctx->stream, a);
+    hnm_timer_end(ctx);
+    HNM_LAUNCH_CHECK();
+  }
+  // 3. exact fp32 re-scoring + top-K of the candidates; unusable rows -> queue
+  hipLaunchKernelGGL(ncf_rescore_kernel, dim3((unsigned)hnm_cdiv(B, 4)), dim3(256), 0, ctx->stream,
+                     t, w->mf, w->w2, w->h1, w->h2, w->b2, w->wp + w->mf, w->bp, B, x.flag, x.cnt,
+                     x.buf, sh.part.np, sh.capp, K, ov, oi, x.ovf_rows, x.ovf_cnt, ctx->stats_dev);
+  HNM_LAUNCH_CHECK();
+  // 4. exact fp32 scan over all items for the queued rows (device-side row list)
+  return ncf_list_rows(ctx, w, t, B, mptr, midx, K, x.ovf_rows, x.ovf_cnt, x.cv, x.ci, ov, oi);
+}
+
+hnm_status ncf_cert_debug(hnm_ctx* ctx, const hnm_ncf_weights* w, const NcfTabs& t, int64_t B,
+                          void* scratch, float* approx, int64_t lda, float* bound) {
+  const int64_t I = w->num_items;
+  CertWs x;
+  cert_carve((char*)scratch, B, I, 1, ctx->num_cus, &x);
+  hnm_status st = cert_prepare(ctx, w, t, B, x);
+  if (st) return st;
+  hipLaunchKernelGGL(cert_tau_kernel, dim3((unsigned)hnm_cdiv(B, 256)), dim3(256), 0, ctx->stream,
+                     nullptr, 1, x.Au, x.Cu, x.prm, B, nullptr, nullptr, x.Eu);
+  HNM_LAUNCH_CHECK();
+  ScanArgs a = scan_args(x, B);
+  a.I = I;
+  a.dense = approx;
+  a.dense2 = bound;
+  a.ldo = lda;
+  const int64_t ublocks = hnm_cdiv(B, 128);
+  Partition part = choose_partition(I, ublocks, ctx->num_cus);
+  a.ipp = part.ipp;
+  a.NP = part.np;
+  hipLaunchKernelGGL(ncf16_scan_kernel<SCAN_DEBUG>, dim3((unsigned)ublocks, (unsigned)part.np),
+                     dim3(256), 0, ctx->stream, a);
+  HNM_LAUNCH_CHECK();
+  hipLaunchKernelGGL(cert_unscale_kernel, dim3((unsigned)hnm_cdiv(B * I, 256)), dim3(256), 0,
+                     ctx->stream, approx, bound, lda, B, I, x.prm);
+  HNM_LAUNCH_CHECK();
+  return HNM_OK;
+}

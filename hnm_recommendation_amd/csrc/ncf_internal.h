@@ -1,0 +1,33 @@
+// Shared between ncf.hip (exact fp32 kernels) and ncf_cert.hip (certified f16 pre-filter).
+#pragma once
+#include "hnm_internal.h"
+
+// Per-call device tables built by ncf_common (layer-1 projections and the GMF operands).
+struct NcfTabs {
+  const float* Pu;   // [B, 64]  pair-permuted  W1u m_u + b1
+  const float* WGu;  // [B, 64]  pair-permuted  wp_gmf * g_u
+  const float* Qi;   // [I, 64]  pair-permuted  W1i m_i
+  const float* G;    // [I, ldg] natural order, ldg % 4 == 0, 16-byte aligned, zero-padded
+  int64_t ldg;
+};
+
+// Exact fp32 top-K over all items (ncf32_kernel LIST mode + partition merge) for the
+// request rows rows[0 .. *nrows) (device pointers; rows == nullptr: rows 0 .. B).
+// cv/ci: candidate scratch of ncf_list_bytes(B, I, K, num_cus) bytes each.
+hnm_status ncf_list_rows(hnm_ctx* ctx, const hnm_ncf_weights* w, const NcfTabs& t, int64_t B,
+                         const int64_t* mptr, const int32_t* midx, int K, const int32_t* rows,
+                         const int32_t* nrows, float* cv, int32_t* ci, float* ov, int64_t* oi);
+size_t ncf_list_bytes(int64_t B, int64_t I, int K, int num_cus);
+
+// Certified pre-filter path (ncf_cert.hip): eligible when h1 <= 64, mf <= 64, K <= 64 and
+// the catalogue is large enough for the sample pass to pay.
+bool ncf_cert_eligible(const hnm_ncf_weights* w, int K);
+size_t ncf_cert_bytes(int64_t B, int64_t I, int K, int num_cus);
+hnm_status ncf_cert_topk(hnm_ctx* ctx, const hnm_ncf_weights* w, const NcfTabs& t, int64_t B,
+                         const int64_t* mptr, const int32_t* midx, int K, void* scratch,
+                         float* ov, int64_t* oi);
+// Diagnostics: the pre-filter's approximate scores (real units, bp excluded) for every
+// item and its per-user error bound E_u: |approx + bp - exact| <= E_u is what the path
+// relies on (tests check it on the full catalogue).
+hnm_status ncf_cert_debug(hnm_ctx* ctx, const hnm_ncf_weights* w, const NcfTabs& t, int64_t B,
+                          void* scratch, float* approx, int64_t lda, float* bound);

@@ -357,6 +357,16 @@ __global__ __launch_bounds__(256) void rows_topk_kernel(const float* __restrict_
 }
 
 // ------------------------------------------------------------------ host side
+hnm_status hnm_topk_rows_strided(hnm_ctx* ctx, const float* s, int64_t ld, int64_t B, int64_t I,
+                                 const int64_t* mptr, const int32_t* midx, int K, float* ov,
+                                 int64_t* oi, int64_t istride) {
+  HNM_REQUIRE(K >= 1 && K <= 64, HNM_EINVAL, "topk_rows_strided: 1 <= K <= 64");
+  hipLaunchKernelGGL(rows_topk_kernel<1>, dim3((unsigned)hnm_cdiv(B, 4)), dim3(256), 0,
+                     ctx->stream, s, ld, B, I, mptr, midx, K, ov, oi, istride);
+  HNM_LAUNCH_CHECK();
+  return HNM_OK;
+}
+
 hnm_status hnm_topk_merge_rows(hnm_ctx* ctx, const float* cv, const int32_t* ci, int64_t B,
                                int64_t G, int64_t gstride, int64_t bstride, int kc, int k,
                                float* ov, int64_t* oi, const int32_t* rows,

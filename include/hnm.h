@@ -56,6 +56,14 @@ hnm_status hnm_ctx_set_stream(hnm_ctx* ctx, void* hip_stream);
 hnm_status hnm_ctx_reserve(hnm_ctx* ctx, size_t bytes);   /* pre-grow workspace */
 hnm_status hnm_ctx_check(hnm_ctx* ctx);                   /* sync; HNM_EOOB if flagged */
 hnm_status hnm_ctx_num_cus(hnm_ctx* ctx, int* out);
+/* Options.  HNM_OPT_PREFILTER (default 1): NCF top-K scans the catalogue with the certified
+ * f16 pre-filter and re-scores the surviving candidates in exact fp32 (results identical
+ * to the fp32 scan); 0 = exact fp32 scan of every item. */
+enum { HNM_OPT_PREFILTER = 1 };
+hnm_status hnm_ctx_set_option(hnm_ctx* ctx, int option, int64_t value);
+/* Pre-filter counters since the last reset (syncs): out[0] rows scored, out[1] candidates
+ * re-scored in fp32, out[2] rows that took the exact fallback scan. */
+hnm_status hnm_ctx_prefilter_stats(hnm_ctx* ctx, int64_t* out, int reset);
 /* Dominant-kernel timer: while on, every scoring / SpMM call records HIP events on the ctx
  * stream around its main kernel; hnm_ctx_timing() syncs, returns the summed kernel time
  * and the number of timed launches, and resets.  (bench.py's live roofline figures.) */
@@ -138,6 +146,13 @@ hnm_status hnm_ncf_topk_f32(hnm_ctx* ctx, const hnm_ncf_weights* w, const int64_
                             int k, float* out_val, int64_t* out_idx);
 hnm_status hnm_ncf_scores_f32(hnm_ctx* ctx, const hnm_ncf_weights* w,
                               const int64_t* user_ids, int64_t B, float* out, int64_t ldo);
+/* Diagnostics of the certified pre-filter (no reference counterpart): approx[b, i] = the
+ * f16 scan's score of item i without the output bias bp, bound[b, i] = the pair's error
+ * bound (both [B, lda]); |approx + bp - exact| <= bound holds for every pair (tests check
+ * it on the full catalogue). */
+hnm_status hnm_ncf_prefilter_debug_f32(hnm_ctx* ctx, const hnm_ncf_weights* w,
+                                       const int64_t* user_ids, int64_t B, float* approx,
+                                       int64_t lda, float* bound);
 /* NeuralCF.forward(user_ids, item_ids) (neural_cf.py:112-141): out[n]. */
 hnm_status hnm_ncf_pair_scores_f32(hnm_ctx* ctx, const hnm_ncf_weights* w,
                                    const int64_t* user_ids, const int64_t* item_ids,

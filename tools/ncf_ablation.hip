@@ -15,7 +15,7 @@ float time_variant(dim3 grid, size_t lds, float* P, float* WG, float* Q, float* 
   for (int rep = 0; rep < 4; ++rep) {
     (void)hipEventRecord(e0);
     hipLaunchKernelGGL((ncf32_kernel<false, ABL>), grid, dim3(256), lds, 0, P, WG, Q, G, 64, 64, W2,
-                       64, 32, b2, wm, bp, B, I, ipp, nullptr, nullptr, K, cv, ci, NP, nullptr, 0);
+                       64, 32, b2, wm, bp, B, I, ipp, nullptr, nullptr, K, cv, ci, NP, nullptr, 0, nullptr, nullptr);
     (void)hipEventRecord(e1);
     (void)hipEventSynchronize(e1);
     hipError_t err = hipGetLastError();
