@@ -167,6 +167,7 @@ def main():
     ap.add_argument("--batch", type=int, default=4096)
     ap.add_argument("--workload", default="ncf")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--scan-users", type=int, default=0, help="tuning: users per f16 scan iteration")
     ap.add_argument("--exact", action="store_true",
                     help="NCF: exact fp32 scan of every item instead of the certified pre-filter")
     args = ap.parse_args()
@@ -176,6 +177,8 @@ def main():
     t_setup = time.perf_counter()
     if args.exact:
         _lib.set_prefilter(device, False)
+    if args.scan_users:
+        _lib.set_option(device, _lib.HNM_OPT_SCAN_USERS, args.scan_users)
     step, per_launch, bound, kernel, info, cpu = build_workload(args.workload, rank, world,
                                                                 device, B, args.exact)
     # resident user batches: rank-specific, distinct ids

@@ -178,6 +178,11 @@ def kernel_timing(device):
 
 
 HNM_OPT_PREFILTER = 1
+HNM_OPT_SCAN_USERS = 2
+
+
+def set_option(device, option, value):
+    check(fn("hnm_ctx_set_option")(ctx(device), int(option), int(value)), "hnm_ctx_set_option")
 
 
 def set_prefilter(device, on=True):

@@ -24,6 +24,7 @@ struct hnm_ctx {
   hipEvent_t* ev0;
   hipEvent_t* ev1;
   int prefilter;                   // HNM_OPT_PREFILTER (default 1)
+  int scan_users;                  // HNM_OPT_SCAN_USERS (tuning: users per scan iteration)
   unsigned long long* stats_dev;   // pre-filter counters: rows, candidates, fallback rows
 };
 
@@ -68,15 +69,17 @@ hnm_status hnm_workspace(hnm_ctx* ctx, size_t bytes, void** out);
 static inline size_t hnm_align(size_t x, size_t a = 256) { return (x + a - 1) / a * a; }
 __host__ __device__ static inline int64_t hnm_cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
-// Item partitions for the fused scoring kernels: ~2 workgroups per CU, >= 4 tiles of
-// `tile` items per partition.
+// Item partitions for the fused scoring kernels: ~`wg_per_cu` workgroups per CU (the
+// kernel's occupancy, so the whole grid is resident in one wave of workgroups), >= 4
+// tiles of `tile` items per partition.
 struct Partition {
   int np;
   int64_t ipp;
 };
 static inline Partition choose_partition(int64_t I, int64_t ublocks, int num_cus,
-                                         int64_t tile = 32) {
-  const int64_t want = std::max<int64_t>(1, hnm_cdiv(2 * (int64_t)num_cus, std::max<int64_t>(ublocks, 1)));
+                                         int64_t tile = 32, int wg_per_cu = 2) {
+  const int64_t want = std::max<int64_t>(
+      1, (int64_t)wg_per_cu * num_cus / std::max<int64_t>(ublocks, 1));
   const int64_t maxp = std::max<int64_t>(1, hnm_cdiv(I, 4 * tile));
   int64_t np = std::min(want, maxp);
   int64_t ipp = hnm_cdiv(hnm_cdiv(I, np), tile) * tile;

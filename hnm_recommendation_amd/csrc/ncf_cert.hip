@@ -39,6 +39,7 @@
 #include "ncf_internal.h"
 
 typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+typedef _Float16 h2 __attribute__((ext_vector_type(2)));
 
 hnm_status hnm_topk_merge_rows(hnm_ctx* ctx, const float* cv, const int32_t* ci, int64_t B,
                                int64_t G, int64_t gstride, int64_t bstride, int kc, int k,
@@ -51,6 +52,10 @@ constexpr int64_t CERT_MIN_ITEMS = 8192;  // below this the exact LIST kernel is
 constexpr int64_t CERT_SAMPLE = 12288;    // sample items for the threshold pass
 constexpr float CERT_RHO = 0.0029296875f; // 6 u16 = 3 * 2^-10
 constexpr int CERT_MAX_NP = 64;           // item partitions (candidate segments per row)
+#ifndef HNM_SCAN_OCC
+#define HNM_SCAN_OCC 3
+#endif
+constexpr int CERT_WG_PER_CU = HNM_SCAN_OCC;  // scan workgroups per CU (LDS 51.7 KB each)
 
 enum { CM_P, CM_Q, CM_WG, CM_G, CM_B, CM_D, CM_N };
 
@@ -162,7 +167,7 @@ __global__ __launch_bounds__(256) void cert_scales_kernel(const float* __restric
                                                           const float* __restrict__ wm,
                                                           const float* __restrict__ bp,
                                                           CertParams* prm) {
-  __shared__ float red[6][4];
+  __shared__ float red[7][4];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   float mW = 0.f, vsum = 0.f, mwm = 0.f, mb2 = 0.f, c0 = 0.f, swm = 0.f;
   for (int e = tid; e < h2 * h1; e += 256) {
@@ -170,13 +175,18 @@ __global__ __launch_bounds__(256) void cert_scales_kernel(const float* __restric
     mW = nmax(mW, w);
     vsum += fabsf(wm[e / h1]) * w;
   }
+  float mrow = 0.f;  // max_j sum_k |W2_jk|
   for (int j = tid; j < h2; j += 256) {
+    float rs = 0.f;
+    for (int k = 0; k < h1; ++k) rs += fabsf(W2[j * h1 + k]);
+    mrow = nmax(mrow, rs);
     mwm = nmax(mwm, fabsf(wm[j]));
     mb2 = nmax(mb2, fabsf(b2[j]));
     c0 += fabsf(wm[j]) * fabsf(b2[j]);
     swm += fabsf(wm[j]);
   }
   mW = wave_max(mW);
+  mrow = wave_max(mrow);
   mwm = wave_max(mwm);
   mb2 = wave_max(mb2);
   vsum = wave_sum(vsum);
@@ -189,6 +199,7 @@ __global__ __launch_bounds__(256) void cert_scales_kernel(const float* __restric
     red[3][wave] = vsum;
     red[4][wave] = c0;
     red[5][wave] = swm;
+    red[6][wave] = mrow;
   }
   __syncthreads();
   if (tid != 0) return;
@@ -199,6 +210,7 @@ __global__ __launch_bounds__(256) void cert_scales_kernel(const float* __restric
     red[3][0] += red[3][w];
     red[4][0] += red[4][w];
     red[5][0] += red[5][w];
+    red[6][0] = nmax(red[6][0], red[6][w]);
   }
   mW = red[0][0];
   mwm = red[1][0];
@@ -206,23 +218,25 @@ __global__ __launch_bounds__(256) void cert_scales_kernel(const float* __restric
   vsum = red[3][0];
   c0 = red[4][0];
   swm = red[5][0];
+  mrow = red[6][0];
   const float mP = __uint_as_float(prm->mx[CM_P]), mQ = __uint_as_float(prm->mx[CM_Q]);
   const float mWG = __uint_as_float(prm->mx[CM_WG]), mG = __uint_as_float(prm->mx[CM_G]);
   const float Bmax = __uint_as_float(prm->mx[CM_B]), Dmax = __uint_as_float(prm->mx[CM_D]);
   const float lim = 1099511627776.f;  // 2^40
   bool bad = false;
-  for (float m : {mP, mQ, mWG, mG, Bmax, Dmax, mW, mwm, mb2, vsum, c0, fabsf(bp[0])})
+  for (float m : {mP, mQ, mWG, mG, Bmax, Dmax, mW, mrow, mwm, mb2, vsum, c0, fabsf(bp[0])})
     bad |= !(m <= lim);  // also catches NaN / inf
   const float zmax = mP + mQ;
   const float s1 = zmax > 0.f ? 0.5f * pow2_below_inv(zmax) : 1.f;  // s1 * z <= 0.5
-  const float sw = mW > 0.f ? pow2_below_inv(mW) : 1.f;
+  // W2 / b2 scale: |H~| <= s1 sw |b2| + sw sum_k |W2_jk| x~_k (x~ <= 0.5 (1 + u)^2) stays
+  // below 1, so the [0, 1] clamp of the f32 -> f16 convert is an exact ReLU
+  const float hmax = (s1 * mb2 + 0.51f * mrow) * 1.01f;
+  const float sw = hmax > 0.f ? pow2_below_inv(hmax) : 1.f;
   const float sm = mwm > 0.f ? pow2_below_inv(mwm) : 1.f;
   const float sgu = mWG > 0.f ? pow2_below_inv(mWG) : 1.f;
   const float sgi = mG > 0.f ? pow2_below_inv(mG) : 1.f;
   const float unit = s1 * sw * sm;
   const float cg = unit / (sgu * sgi);
-  // f16 range of the scaled layer-2 pre-activation: |H~| <= s1 sw |b2| + 0.5 * 64
-  bad |= !(s1 * sw * mb2 <= 30000.f);
   bad |= !(unit >= 1e-30f && unit <= 1e30f && cg >= 1e-30f && cg <= 1e30f);
   const float phi = 2.98023224e-08f;  // 2^-25: half the f16 subnormal spacing
   const float rmax = mb2 + 64.f * mW * zmax;
@@ -338,12 +352,15 @@ __device__ __forceinline__ f32x16 mfma16(h8 a, h8 b, f32x16 c) {
 // adds), 2 f16 MFMAs for wm . relu(H) (the accumulator tile reused as the B operand),
 // GMF once per tile for all 32 users (4 MFMAs).  v_mfma_f32_32x32x16_f16 B operand:
 // lane (j, h) holds B[k = 8h + e][col j], e = 0..7.
-template <int MODE>
-__global__ __launch_bounds__(256, 2) void ncf16_scan_kernel(ScanArgs A) {
+// ABL: ablation bits for tools/scan_ablation.hip only (0 in the library): 1 = no threshold
+// test, 2 = no wm epilogue, 4 = no layer-2 MFMA, 8 = no P~ LDS reads, 16 = no GMF,
+// 32 = no tile staging / barriers.
+template <int MODE, int EPI, int ABL = 0>
+__global__ __launch_bounds__(256, HNM_SCAN_OCC) void ncf16_scan_kernel(ScanArgs A) {
   constexpr int RS = 72;   // LDS row stride in halfs (144 B): conflict-free b128 reads
   constexpr int NU = 128;  // users per workgroup
-  __shared__ __attribute__((aligned(16))) _Float16 qs[TILE * RS];
-  __shared__ __attribute__((aligned(16))) _Float16 gs[TILE * RS];
+  __shared__ __attribute__((aligned(16))) _Float16 qs[2][TILE * RS];  // double-buffered tiles
+  __shared__ __attribute__((aligned(16))) _Float16 gs[2][TILE * RS];
   __shared__ __attribute__((aligned(16))) _Float16 ps[NU * 64];
   __shared__ float gsm[4][32][33];
 
@@ -361,10 +378,12 @@ __global__ __launch_bounds__(256, 2) void ncf16_scan_kernel(ScanArgs A) {
     if (ublk + r < A.B) v = *reinterpret_cast<const h8*>(A.P16 + (ublk + r) * 64 + 8 * c);
     *reinterpret_cast<h8*>(&ps[r * 64 + 8 * c]) = v;
   }
-  h8 aw[4], ag[4], awm[2];
+  h8 aw[4], awm[2];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) aw[s] = *reinterpret_cast<const h8*>(A.W2h + j * 64 + 16 * s + 8 * h);
+  h8 ag[4];  // GMF A operand: this wave's users' wp*g_u rows
 #pragma unroll
   for (int s = 0; s < 4; ++s) {
-    aw[s] = *reinterpret_cast<const h8*>(A.W2h + j * 64 + 16 * s + 8 * h);
     h8 z = {};
     ag[s] = j < nu ? *reinterpret_cast<const h8*>(A.WG16 + (u0 + j) * 64 + 16 * s + 8 * h) : z;
   }
@@ -372,6 +391,10 @@ __global__ __launch_bounds__(256, 2) void ncf16_scan_kernel(ScanArgs A) {
   for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
     for (int e = 0; e < 8; ++e) awm[s2][e] = A.wmh[mfma32_row(8 * s2 + e, h)];
+  h2 wm2[8];  // EPI 1: wm of this lane's accumulator rows, in pairs
+#pragma unroll
+  for (int r = 0; r < 16; r += 2)
+    wm2[r >> 1] = (h2){A.wmh[mfma32_row(r, h)], A.wmh[mfma32_row(r + 1, h)]};
   f32x16 b2c;
 #pragma unroll
   for (int r = 0; r < 16; ++r) b2c[r] = A.b2s[mfma32_row(r, h)];
@@ -395,39 +418,56 @@ __global__ __launch_bounds__(256, 2) void ncf16_scan_kernel(ScanArgs A) {
   const int64_t segstride = (int64_t)A.NP * A.capp;  // next user's segment
 
   const int64_t ntiles = part_end > part_start ? hnm_cdiv(part_end - part_start, TILE) : 0;
+  // tile staging: thread (row, c) moves 16 B of Q~ and of G~; tile t + 1 is fetched into
+  // registers while tile t is scored, then stored to the other LDS buffer (one barrier
+  // per tile)
+  const int srow = tid >> 3, sc = tid & 7;
+  h8 nq = {}, ng = {};
+  float nb = 0.f, nd = 0.f;  // per-item bound terms of lane j's next item
+  auto fetch = [&](int64_t base) {
+    const int64_t n = base + srow;
+    nq = (h8){};
+    ng = (h8){};
+    if (n < part_end) {
+      const int64_t it = n * A.istride;
+      nq = *reinterpret_cast<const h8*>(A.Q16 + it * 64 + 8 * sc);
+      ng = *reinterpret_cast<const h8*>(A.G16 + it * 64 + 8 * sc);
+    }
+    const int64_t nj = std::min<int64_t>(base + j, part_end - 1) * A.istride;
+    nb = A.Bi[nj];
+    nd = A.Di[nj];
+  };
+  auto stash = [&](int buf) {
+    *reinterpret_cast<h8*>(&qs[buf][srow * RS + 8 * sc]) = nq;
+    *reinterpret_cast<h8*>(&gs[buf][srow * RS + 8 * sc]) = ng;
+  };
+  if (ntiles > 0 && !(ABL & 32)) {
+    fetch(part_start);
+    stash(0);
+  }
+  __syncthreads();
   for (int64_t t = 0; t < ntiles; ++t) {
     const int64_t base = part_start + t * TILE;
-    __syncthreads();
-    {
-      const int row = tid >> 3, c = tid & 7;
-      const int64_t n = base + row;
-      h8 q = {}, g = {};
-      if (n < part_end) {
-        const int64_t it = n * A.istride;
-        q = *reinterpret_cast<const h8*>(A.Q16 + it * 64 + 8 * c);
-        g = *reinterpret_cast<const h8*>(A.G16 + it * 64 + 8 * c);
-      }
-      *reinterpret_cast<h8*>(&qs[row * RS + 8 * c]) = q;
-      *reinterpret_cast<h8*>(&gs[row * RS + 8 * c]) = g;
-    }
-    __syncthreads();
-    if (nu == 0) continue;
+    const int cur = (int)(t & 1);
+    const float bj = ru * nb, dj = nd;  // bound terms of this tile's item j
+    // the prefetch is the only global load in the tile body (vmcnt waits are in order: any
+    // later load's wait would also wait for it)
+    if (t + 1 < ntiles && !(ABL & 32)) fetch(base + TILE);
 
-    {  // GMF of the wave's 32 users x 32 items, in score units
+    if (nu > 0) {
+    if (!(ABL & 16)) {  // GMF of the wave's 32 users x 32 items, in score units
       f32x16 gacc = {};
 #pragma unroll
       for (int s = 0; s < 4; ++s)
-        gacc = mfma16(ag[s], *reinterpret_cast<const h8*>(&gs[j * RS + 16 * s + 8 * h]), gacc);
+        gacc = mfma16(ag[s], *reinterpret_cast<const h8*>(&gs[cur][j * RS + 16 * s + 8 * h]), gacc);
 #pragma unroll
       for (int r = 0; r < 16; ++r) gsm[wave][mfma32_row(r, h)][j] = gacc[r] * cg;
     }
     h8 q[4];
 #pragma unroll
-    for (int s = 0; s < 4; ++s) q[s] = *reinterpret_cast<const h8*>(&qs[j * RS + 16 * s + 8 * h]);
+    for (int s = 0; s < 4; ++s) q[s] = *reinterpret_cast<const h8*>(&qs[cur][j * RS + 16 * s + 8 * h]);
     const int64_t n = base + j;
     const bool ivalid = h == 0 && n < part_end;
-    const int64_t itm = (ivalid ? n : part_start) * A.istride;
-    const float bj = ru * A.Bi[itm], dj = A.Di[itm];  // per-item bound terms of lane j's item
     const int64_t tile_end = std::min<int64_t>(base + TILE, part_end);
     unsigned mbits = 0;
     if (masked) {  // scanned items are real items here (istride 1 in the THRESH pass)
@@ -447,28 +487,54 @@ __global__ __launch_bounds__(256, 2) void ncf16_scan_kernel(ScanArgs A) {
       }
     }
 
+    // next user's GMF value is read one iteration ahead
+    float gn = (ABL & 16) ? 0.f : gsm[wave][0][j];
     for (int u = 0; u < nu; ++u) {
-      const _Float16* pr = &ps[(wave * 32 + u) * 64 + 8 * h];
+      h8 pc[4];
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+        pc[s] = (ABL & 8) ? q[s] : *reinterpret_cast<const h8*>(&ps[(wave * 32 + u) * 64 + 8 * h + 16 * s]);
+      const float gmu = gn;
+      const float cuu = hnm_readlane_f(cu, u), tvu = hnm_readlane_f(tv, u);
+      if (u + 1 < nu) gn = (ABL & 16) ? 0.f : gsm[wave][u + 1][j];
       f32x16 acc = b2c;
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
-        h8 x = *reinterpret_cast<const h8*>(pr + 16 * s) + q[s];
+        h8 x = pc[s] + q[s];
         x = __builtin_elementwise_min(__builtin_elementwise_max(x, (h8){}), (h8)(_Float16)1.f);
-        acc = mfma16(aw[s], x, acc);
+        if (ABL & 4) acc[s] += (float)x[0] + (float)x[7];
+        else acc = mfma16(aw[s], x, acc);
       }
-      h8 y0, y1;
+      float score;
+      if (ABL & 2) {
+        score = acc[0] + acc[15] + gmu;
+      } else if (EPI == 0) {
+        // relu(H~) as the [0, 1] clamp of the convert (|H~| < 1 by the choice of sw); the
+        // accumulator tile is the B operand of wm . relu(H~)
+        h8 y0, y1;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        y0[e] = (_Float16)acc[e];
-        y1[e] = (_Float16)acc[8 + e];
+        for (int e = 0; e < 8; ++e) {
+          y0[e] = (_Float16)acc[e];
+          y1[e] = (_Float16)acc[8 + e];
+        }
+        y0 = __builtin_elementwise_min(__builtin_elementwise_max(y0, (h8){}), (h8)(_Float16)1.f);
+        y1 = __builtin_elementwise_min(__builtin_elementwise_max(y1, (h8){}), (h8)(_Float16)1.f);
+        f32x16 d = {};
+        d = mfma16(awm[0], y0, d);
+        d = mfma16(awm[1], y1, d);
+        score = d[0] + gmu;
+      } else {
+        // wm . relu(H~) on the VALU: 8 packed f16 dots per half + one cross-half add
+        float m2[2] = {0.f, 0.f};
+#pragma unroll
+        for (int r = 0; r < 16; r += 2) {
+          h2 y = {(_Float16)acc[r], (_Float16)acc[r + 1]};
+          y = __builtin_elementwise_min(__builtin_elementwise_max(y, (h2){}), (h2)(_Float16)1.f);
+          m2[(r >> 1) & 1] = __builtin_amdgcn_fdot2(y, wm2[r >> 1], m2[(r >> 1) & 1], false);
+        }
+        score = hnm_sum_halves(m2[0] + m2[1]) + gmu;
       }
-      y0 = __builtin_elementwise_max(y0, (h8){});
-      y1 = __builtin_elementwise_max(y1, (h8){});
-      f32x16 d = {};
-      d = mfma16(awm[0], y0, d);
-      d = mfma16(awm[1], y1, d);
-      const float score = d[0] + gsm[wave][u][j];
-      const float ei = fmaf(hnm_readlane_f(cu, u), dj, bj);
+      const float ei = fmaf(cuu, dj, bj);
       if (MODE == SCAN_SAMPLE) {
         if (ivalid) A.dense[(u0 + u) * A.ldo + n] = score - ei;
       } else if (MODE == SCAN_DEBUG) {
@@ -476,8 +542,10 @@ __global__ __launch_bounds__(256, 2) void ncf16_scan_kernel(ScanArgs A) {
           A.dense[(u0 + u) * A.ldo + n] = score;
           A.dense2[(u0 + u) * A.ldo + n] = hnm_readlane_f(eu, u) + ei;
         }
+      } else if (ABL & 1) {
+        tv += score + ei;  // keep the score live, no test
       } else {
-        bool pass = ivalid && !(score + ei < hnm_readlane_f(tv, u));
+        bool pass = ivalid && !(score + ei < tvu);
         if (masked) pass = pass && !((hnm_readlane_i((int)mbits, u) >> j) & 1);
         const uint64_t m = __ballot(pass);
         if (m) {
@@ -487,8 +555,11 @@ __global__ __launch_bounds__(256, 2) void ncf16_scan_kernel(ScanArgs A) {
         }
       }
     }
+    }  // nu > 0
+    if (t + 1 < ntiles && !(ABL & 32)) stash(cur ^ 1);
+    __syncthreads();
   }
-  if (MODE == SCAN_THRESH && lane < nu) A.cnt[(u0 + lane) * A.NP + p] = ccount;
+  if (MODE == SCAN_THRESH && lane < nu) A.cnt[(u0 + lane) * A.NP + p] = ccount + ((ABL & 1) ? (int)tv : 0);
 }
 
 // Per row: Eu = user-constant part of the bound (scaled): 6u unit (c0 + A_u) + unit abs.
@@ -671,7 +742,7 @@ CertShape cert_shape(int64_t B, int64_t I, int K, int num_cus) {
   CertShape sh;
   sh.stride = std::max<int64_t>(1, I / CERT_SAMPLE);
   sh.Ns = hnm_cdiv(I, sh.stride);
-  Partition part = choose_partition(I, hnm_cdiv(B, 128), num_cus);
+  Partition part = choose_partition(I, hnm_cdiv(B, 128), num_cus, TILE, CERT_WG_PER_CU);
   if (part.np > CERT_MAX_NP) {
     part.ipp = hnm_cdiv(hnm_cdiv(I, CERT_MAX_NP), TILE) * TILE;
     part.np = (int)hnm_cdiv(I, part.ipp);
@@ -743,6 +814,14 @@ hnm_status cert_prepare(hnm_ctx* ctx, const hnm_ncf_weights* w, const NcfTabs& t
   return HNM_OK;
 }
 
+template <int MODE>
+void launch_scan(hnm_ctx* ctx, dim3 grid, const ScanArgs& a) {
+  if (ctx->scan_users == 2)  // tuning knob: epilogue variant (1 = packed dots, 2 = MFMA)
+    hipLaunchKernelGGL((ncf16_scan_kernel<MODE, 0>), grid, dim3(256), 0, ctx->stream, a);
+  else
+    hipLaunchKernelGGL((ncf16_scan_kernel<MODE, 1>), grid, dim3(256), 0, ctx->stream, a);
+}
+
 ScanArgs scan_args(const CertWs& x, int64_t B) {
   ScanArgs a{};
   a.P16 = x.P16;
@@ -791,11 +870,10 @@ hnm_status ncf_cert_topk(hnm_ctx* ctx, const hnm_ncf_weights* w, const NcfTabs& 
     a.istride = sh.stride;
     a.dense = x.sdense;
     a.ldo = sh.Ns;
-    Partition ps = choose_partition(sh.Ns, ublocks, ctx->num_cus);
+    Partition ps = choose_partition(sh.Ns, ublocks, ctx->num_cus, TILE, CERT_WG_PER_CU);
     a.ipp = ps.ipp;
     a.NP = ps.np;
-    hipLaunchKernelGGL(ncf16_scan_kernel<SCAN_SAMPLE>, dim3((unsigned)ublocks, (unsigned)ps.np),
-                       dim3(256), 0, ctx->stream, a);
+    launch_scan<SCAN_SAMPLE>(ctx, dim3((unsigned)ublocks, (unsigned)ps.np), a);
     HNM_LAUNCH_CHECK();
     st = hnm_topk_rows_strided(ctx, x.sdense, sh.Ns, B, sh.Ns, mptr, midx, K, x.kthv, x.kthi,
                                sh.stride);
@@ -817,8 +895,7 @@ hnm_status ncf_cert_topk(hnm_ctx* ctx, const hnm_ncf_weights* w, const NcfTabs& 
     a.ipp = sh.part.ipp;
     a.NP = sh.part.np;
     hnm_timer_begin(ctx);
-    hipLaunchKernelGGL(ncf16_scan_kernel<SCAN_THRESH>,
-                       dim3((unsigned)ublocks, (unsigned)sh.part.np), dim3(256), 0, ctx->stream, a);
+    launch_scan<SCAN_THRESH>(ctx, dim3((unsigned)ublocks, (unsigned)sh.part.np), a);
     hnm_timer_end(ctx);
     HNM_LAUNCH_CHECK();
   }
@@ -850,8 +927,7 @@ hnm_status ncf_cert_debug(hnm_ctx* ctx, const hnm_ncf_weights* w, const NcfTabs&
   Partition part = choose_partition(I, ublocks, ctx->num_cus);
   a.ipp = part.ipp;
   a.NP = part.np;
-  hipLaunchKernelGGL(ncf16_scan_kernel<SCAN_DEBUG>, dim3((unsigned)ublocks, (unsigned)part.np),
-                     dim3(256), 0, ctx->stream, a);
+  launch_scan<SCAN_DEBUG>(ctx, dim3((unsigned)ublocks, (unsigned)part.np), a);
   HNM_LAUNCH_CHECK();
   hipLaunchKernelGGL(cert_unscale_kernel, dim3((unsigned)hnm_cdiv(B * I, 256)), dim3(256), 0,
                      ctx->stream, approx, bound, lda, B, I, x.prm);

@@ -59,7 +59,8 @@ hnm_status hnm_ctx_num_cus(hnm_ctx* ctx, int* out);
 /* Options.  HNM_OPT_PREFILTER (default 1): NCF top-K scans the catalogue with the certified
  * f16 pre-filter and re-scores the surviving candidates in exact fp32 (results identical
  * to the fp32 scan); 0 = exact fp32 scan of every item. */
-enum { HNM_OPT_PREFILTER = 1 };
+enum { HNM_OPT_PREFILTER = 1,
+       HNM_OPT_SCAN_USERS = 2 /* tuning: users per iteration of the f16 scan (1 or 2) */ };
 hnm_status hnm_ctx_set_option(hnm_ctx* ctx, int option, int64_t value);
 /* Pre-filter counters since the last reset (syncs): out[0] rows scored, out[1] candidates
  * re-scored in fp32, out[2] rows that took the exact fallback scan. */
