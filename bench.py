@@ -98,7 +98,7 @@ def build_workload(name, rank, world, device, batch, exact=False):
         per_launch = 2.0 * d * batch * world * (hi - lo)
         info = {"model": "LightGCN", "embedding_dim": d, "num_layers": 3,
                 "interactions": syn.HM_INTERACTIONS}
-        bound, kernel = "mfma", "dot_score_kernel"
+        bound, kernel = "mfma", ("dot_score_kernel" if exact else "dot16_scan_kernel")
         cpu = None
         info["_model"] = m
     elif name == "widedeep":
@@ -116,7 +116,7 @@ def build_workload(name, rank, world, device, batch, exact=False):
                                  lo, hi, K)
         per_launch = 2.0 * 64 * batch * world * (hi - lo)
         info = {"model": "MatrixFactorization", "embedding_dim": 64}
-        bound, kernel = "mfma", "dot_score_kernel"
+        bound, kernel = "mfma", ("dot_score_kernel" if exact else "dot16_scan_kernel")
         cpu = None
     else:
         raise SystemExit(f"unknown workload {name}")
@@ -169,7 +169,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--scan-users", type=int, default=0, help="tuning: users per f16 scan iteration")
     ap.add_argument("--exact", action="store_true",
-                    help="NCF: exact fp32 scan of every item instead of the certified pre-filter")
+                    help="exact fp32 scan of every item instead of the certified f16 pre-filter")
     args = ap.parse_args()
 
     rank, world, device = setup_dist(args.gpus)
@@ -216,7 +216,8 @@ def main():
     users_total = B * world * args.steps
     value = users_total / elapsed
     achieved = per_launch / (avg_kernel_ms * 1e-3) / 1e12
-    peak = F16_MFMA_PEAK_TFLOPS if kernel == "ncf16_scan_kernel" else FP32_MFMA_PEAK_TFLOPS
+    f16 = kernel in ("ncf16_scan_kernel", "dot16_scan_kernel")
+    peak = F16_MFMA_PEAK_TFLOPS if f16 else FP32_MFMA_PEAK_TFLOPS
     line = {
         "metric": METRIC,
         "value": round(value, 2),
@@ -228,7 +229,7 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "f16+f32" if kernel == "ncf16_scan_kernel" else "f32",
+        "dtype": "f16+f32" if f16 else "f32",
         "data": "synthetic (PCG64 weights with reference init distributions; H&M shape)",
         "config": {"workload": f"{args.workload}: BASELINE configs[1] NeuralCF dim=64, full H&M "
                                f"shape, batch={B} users/rank, K=12" if args.workload == "ncf"

@@ -61,6 +61,8 @@ _SIGS = {
                                    C.c_int, _p, _i64, C.c_int]),
     "hnm_dot_topk_f32": (_i32, [_p, _p, _i64, _i64, _p, _i64, _p, _i64, _i64, C.c_int, _p, _p,
                                 _p, _p, _p, C.c_int, _p, _p]),
+    "hnm_dot_prefilter_debug_f32": (_i32, [_p, _p, _i64, _i64, _p, _i64, _p, _i64, _i64, C.c_int,
+                                           _p, _p, _p, _p, _i64, _p]),
     "hnm_dot_scores_f32": (_i32, [_p, _p, _i64, _i64, _p, _i64, _p, _i64, _i64, C.c_int, _p,
                                   _p, _p, _p, _i64]),
     "hnm_pair_dot_f32": (_i32, [_p, _p, _i64, _i64, _p, _i64, _i64, C.c_int, _p, _p, _i64, _p,

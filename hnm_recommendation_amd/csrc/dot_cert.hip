@@ -1,0 +1,671 @@
+// Dot-product top-K (LightGCN lightgcn.py:332-358 over :188-204, MatrixFactorization
+// matrix_factorization.py:220-246 over :108-131) with a CERTIFIED f16 pre-filter and
+// exact fp32 re-scoring -- the dot-model counterpart of ncf_cert.hip.
+//
+//   exact score (dot_score_kernel):  s(u, i) = (fma-chain_k u_k i_k + ub_u) + ib_i
+//
+// The all-items scan multiplies f16 copies of the user rows and item table on
+// v_mfma_f32_32x32x16_f16 (16x the fp32 MFMA rate) and only prunes; every returned score
+// is recomputed by the fp32 fma chain the fp32 MFMA is bitwise equal to
+// (tools/mfma_semantics_probe.hip (a)), so results are bit-identical to the fp32 scan.
+//
+// Bound: with u~ = rn16(u su), i~ = rn16(i si) (powers of two, |u su|, |i si| <= 1, f16
+// denormals kept), |u~ i~ - s u i| <= 2.01 u16 s |u_k||i_k| + subnormal terms, the f16
+// MFMA's fp32 accumulation and the exact path's fp32 chain add <= (DP + 18) 2^-24 of
+// sum |u_k i_k| <= ||u|| ||i|| (Cauchy-Schwarz), the bias adds 2^-23 of |ub| + |ib| + |dot|.
+// Per user:  E_u = 3 u16 ||u|| max_i ||i|| + 2^-22 (|ub_u| + max|ib|) + abs_slack,
+// |approx - exact| <= E_u for every item (tests/test_gpu_prefilter.py checks it).
+// Pruning as in ncf_cert.hip: tau_u = (K-th best approx over a strided sample) - 2 E_u;
+// the scan appends items with approx >= tau_u; exact re-scoring + top-K of the
+// candidates; rows that overflow / have < K candidates / an unusable bound take the
+// exact LIST scan (device-side row list).
+//
+// Grid: blockIdx.x = item partition (NP a multiple of 8), blockIdx.y = 128-user block,
+// so the hardware's round-robin workgroup -> XCD placement pins partition p to XCD p % 8:
+// each XCD's L2 holds only its partitions' item tiles (XCD-aware mapping).
+#include <algorithm>
+
+#include "dot_internal.h"
+#include "hnm_device.h"
+
+typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+
+namespace {
+
+constexpr int64_t DCERT_MIN_ITEMS = 8192;
+constexpr int64_t DCERT_SAMPLE = 12288;
+constexpr float DCERT_RHO = 0.00146484375f;  // 3 u16 = 3 * 2^-11
+constexpr int DCERT_MAX_NP = 64;
+// scan occupancy (workgroups per CU): the d=128 A operand needs 32 more VGPRs
+__host__ __device__ constexpr int dcert_wg_per_cu(int DP) { return DP > 64 ? 3 : 4; }
+
+enum { DM_U, DM_I, DM_NI, DM_IB, DM_N };
+
+struct DParams {
+  unsigned mx[DM_N];  // float bits of non-negative maxima (NaN-propagating atomicMax)
+  float su, si, s;    // f16 scales; s = su * si is the scan's score unit
+  float absb;         // subnormal slack, scaled units
+  int bad;
+};
+
+__device__ __forceinline__ float nmax(float a, float b) { return (b > a || b != b) ? b : a; }
+__device__ __forceinline__ float wave_sum(float x) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) x += __shfl_xor(x, o);
+  return x;
+}
+__device__ __forceinline__ float wave_max(float x) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) x = nmax(x, __shfl_xor(x, o));
+  return x;
+}
+__device__ __forceinline__ float pow2_below_inv(float m) {  // 2^-e with m < 2^e (m > 0)
+  int e;
+  (void)frexpf(m, &e);
+  return ldexpf(1.f, -e);
+}
+
+struct DotCertWs {
+  DParams* prm;
+  float *Nu, *Ni, *ubr, *ibs, *tau, *E, *kthv, *sdense;
+  int64_t* kthi;
+  int *cnt, *flag;
+  int32_t *buf, *ovf_cnt, *ovf_rows;
+  _Float16 *U16, *I16;
+  float* cv;
+  int32_t* ci;
+};
+
+struct DotCertShape {
+  int DP;
+  int64_t stride, Ns;
+  Partition part;
+  int capp;
+};
+
+Partition xcd_partition(int64_t I, int64_t ublocks, int num_cus, int DP) {
+  // ~dcert_wg_per_cu workgroups per CU, NP a multiple of 8 (XCD-aware), <= DCERT_MAX_NP
+  int64_t np = std::max<int64_t>(
+      1, (int64_t)dcert_wg_per_cu(DP) * num_cus / std::max<int64_t>(ublocks, 1));
+  np = std::min<int64_t>(np, std::max<int64_t>(1, hnm_cdiv(I, 4 * TILE)));
+  np = std::min<int64_t>(np, DCERT_MAX_NP);
+  if (np >= 8) np = np / 8 * 8;
+  int64_t ipp = hnm_cdiv(hnm_cdiv(I, np), TILE) * TILE;
+  return {(int)hnm_cdiv(I, ipp), ipp};
+}
+
+DotCertShape dcert_shape(int64_t B, int64_t I, int d, int K, int num_cus) {
+  DotCertShape sh;
+  sh.DP = d <= 64 ? 64 : 128;
+  sh.stride = std::max<int64_t>(1, I / DCERT_SAMPLE);
+  sh.Ns = hnm_cdiv(I, sh.stride);
+  sh.part = xcd_partition(I, hnm_cdiv(B, 128), num_cus, sh.DP);
+  const int64_t total = std::min<int64_t>(8192, std::max<int64_t>(256, 8 * (int64_t)K * sh.stride));
+  sh.capp = (int)std::max<int64_t>(32, std::min<int64_t>(total, hnm_cdiv(4 * total, sh.part.np)));
+  return sh;
+}
+
+size_t dcert_carve(char* base, int64_t B, int64_t I, int d, int K, int num_cus, DotCertWs* w) {
+  const DotCertShape sh = dcert_shape(B, I, d, K, num_cus);
+  size_t off = 0;
+  auto take = [&](size_t bytes) {
+    char* p = base ? base + off : nullptr;
+    off += hnm_align(bytes);
+    return p;
+  };
+  DotCertWs x;
+  x.prm = (DParams*)take(sizeof(DParams));
+  x.Nu = (float*)take(B * 4);
+  x.Ni = (float*)take(I * 4);
+  x.ubr = (float*)take(B * 4);
+  x.ibs = (float*)take(I * 4);
+  x.tau = (float*)take(B * 4);
+  x.E = (float*)take(B * 4);
+  x.kthv = (float*)take((size_t)B * K * 4);
+  x.kthi = (int64_t*)take((size_t)B * K * 8);
+  x.cnt = (int*)take((size_t)B * sh.part.np * 4);
+  x.flag = (int*)take(B * 4);
+  x.ovf_cnt = (int32_t*)take(256);
+  x.ovf_rows = (int32_t*)take(B * 4);
+  x.buf = (int32_t*)take((size_t)B * sh.part.np * sh.capp * 4);
+  x.sdense = (float*)take((size_t)B * sh.Ns * 4);
+  x.U16 = (_Float16*)take((size_t)B * sh.DP * 2);
+  x.I16 = (_Float16*)take((size_t)I * sh.DP * 2);
+  const size_t lb = list_cand_bytes(B, I, K, num_cus);
+  x.cv = (float*)take(lb);
+  x.ci = (int32_t*)take(lb);
+  if (w) *w = x;
+  return off;
+}
+
+// ------------------------------------------------------------------ statistics + f16 copies
+// Users: wave per request row (the a1 gather fused), ||u||, user bias (+ global bias).
+// Items: wave per item, ||i||.  Maxima -> prm (atomicMax on float bits).
+__global__ __launch_bounds__(256) void dcert_stats_kernel(DotArgs a, DParams* prm,
+                                                          float* __restrict__ Nu,
+                                                          float* __restrict__ Ni,
+                                                          float* __restrict__ ubr, int item_blocks,
+                                                          int user_blocks) {
+  __shared__ float red[4][4];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  float m0 = 0.f, m1 = 0.f, m2 = 0.f;
+  const bool items = (int)blockIdx.x < item_blocks;
+  if (items) {  // m0 = max|i_k|, m1 = max ||i||, m2 = max |ib|
+    for (int64_t i = (int64_t)blockIdx.x * 4 + wave; i < a.I; i += (int64_t)item_blocks * 4) {
+      const float* row = a.it + i * a.ldi;
+      const float v0 = lane < a.d ? row[lane] : 0.f;
+      const float v1 = lane + 64 < a.d ? row[lane + 64] : 0.f;
+      m0 = nmax(m0, nmax(fabsf(v0), fabsf(v1)));
+      const float n = sqrtf(wave_sum(v0 * v0 + v1 * v1));
+      m1 = nmax(m1, n);
+      if (lane == 0) {
+        Ni[i] = n;
+        if (a.ibias) m2 = nmax(m2, fabsf(a.ibias[i]));
+      }
+    }
+  } else {  // m0 = max|u_k|
+    const int ub = (int)blockIdx.x - item_blocks;
+    for (int64_t b = (int64_t)ub * 4 + wave; b < a.B; b += (int64_t)user_blocks * 4) {
+      const int64_t uid = a.uids[b];
+      const bool ok = uid >= 0 && uid < a.num_users;
+      if (!ok && lane == 0) hnm_flag(a.err, HNM_ERR_OOB);
+      const float* row = a.ut + (ok ? uid : 0) * a.ldu;
+      const float v0 = lane < a.d ? row[lane] : 0.f;
+      const float v1 = lane + 64 < a.d ? row[lane + 64] : 0.f;
+      m0 = nmax(m0, nmax(fabsf(v0), fabsf(v1)));
+      const float n = sqrtf(wave_sum(v0 * v0 + v1 * v1));
+      if (lane == 0) {
+        Nu[b] = n;
+        const float v = (a.ubias && ok) ? a.ubias[uid] : 0.f;
+        ubr[b] = v + (a.cbias ? a.cbias[0] : 0.f);  // the exact kernel's ub[r]
+      }
+    }
+  }
+  m0 = wave_max(m0);
+  m1 = wave_max(m1);
+  m2 = wave_max(m2);
+  if (lane == 0) {
+    red[wave][0] = m0;
+    red[wave][1] = m1;
+    red[wave][2] = m2;
+  }
+  __syncthreads();
+  if (tid < 3) {
+    float m = red[0][tid];
+    for (int w = 1; w < 4; ++w) m = nmax(m, red[w][tid]);
+    const int slot = items ? (tid == 0 ? DM_I : tid == 1 ? DM_NI : DM_IB) : (tid == 0 ? DM_U : -1);
+    if (slot >= 0) atomicMax(&prm->mx[slot], __float_as_uint(m));
+  }
+}
+
+__global__ void dcert_scales_kernel(DParams* prm, int DP) {
+  if (threadIdx.x != 0) return;
+  const float mU = __uint_as_float(prm->mx[DM_U]), mI = __uint_as_float(prm->mx[DM_I]);
+  const float mN = __uint_as_float(prm->mx[DM_NI]), mB = __uint_as_float(prm->mx[DM_IB]);
+  const float lim = 1099511627776.f;  // 2^40
+  bool bad = false;
+  for (float m : {mU, mI, mN, mB}) bad |= !(m <= lim);
+  const float su = mU > 0.f ? pow2_below_inv(mU) : 1.f;
+  const float si = mI > 0.f ? pow2_below_inv(mI) : 1.f;
+  const float s = su * si;
+  bad |= !(s >= 1e-30f && s <= 1e30f);
+  prm->su = su;
+  prm->si = si;
+  prm->s = s;
+  // subnormal terms: sum_k phi (|u~_k| + |i~_k|) <= 2 DP phi, phi = 2^-25; x4 slack
+  prm->absb = 8.f * DP * 2.98023224e-08f;
+  prm->bad = bad;
+}
+
+__global__ __launch_bounds__(256) void dcert_convert_kernel(DotArgs a, int DP,
+                                                            const DParams* __restrict__ prm,
+                                                            _Float16* __restrict__ U16,
+                                                            _Float16* __restrict__ I16,
+                                                            float* __restrict__ ibs) {
+  const float su = prm->su, si = prm->si, s = prm->s;
+  const int64_t nthreads = (int64_t)gridDim.x * 256;
+  const int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int c4n = DP / 4;
+  for (int64_t e = g; e < a.I * c4n; e += nthreads) {
+    const int64_t i = e / c4n;
+    const int c = (int)(e % c4n);
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (4 * c < a.d) v = *reinterpret_cast<const float4*>(a.it + i * a.ldi + 4 * c);
+    _Float16* o = I16 + i * DP + 4 * c;
+    o[0] = (_Float16)(v.x * si);
+    o[1] = (_Float16)(v.y * si);
+    o[2] = (_Float16)(v.z * si);
+    o[3] = (_Float16)(v.w * si);
+    if (c == 0 && a.ibias) ibs[i] = a.ibias[i] * s;
+  }
+  for (int64_t e = g; e < a.B * c4n; e += nthreads) {
+    const int64_t b = e / c4n;
+    const int c = (int)(e % c4n);
+    const int64_t uid = a.uids[b];
+    const bool ok = uid >= 0 && uid < a.num_users;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (ok && 4 * c < a.d) v = *reinterpret_cast<const float4*>(a.ut + uid * a.ldu + 4 * c);
+    _Float16* o = U16 + b * DP + 4 * c;
+    o[0] = (_Float16)(v.x * su);
+    o[1] = (_Float16)(v.y * su);
+    o[2] = (_Float16)(v.z * su);
+    o[3] = (_Float16)(v.w * su);
+  }
+}
+
+// ------------------------------------------------------------------ f16 scan
+enum { DSCAN_SAMPLE = 0, DSCAN_THRESH = 1 };
+
+struct DScanArgs {
+  const _Float16* U16;  // [B, DP]
+  const _Float16* I16;  // [Itot, DP]
+  const float* ibs;     // [Itot] item bias, scaled (BIAS)
+  int64_t B, I, istride, ipp;
+  int NP;
+  const int64_t* mptr;
+  const int32_t* midx;
+  const float* tau;     // [B] scaled thresholds (THRESH)
+  int* cnt;             // [B, NP]
+  int32_t* buf;         // [B, NP, capp]
+  int capp;
+  float* dense;         // [B, ldo] scaled approx (SAMPLE)
+  int64_t ldo;
+};
+
+__device__ __forceinline__ f32x16 mfma16(h8 a, h8 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+}
+
+// A wave holds 32 users' f16 rows as the MFMA A operand; 32-item tiles of I16 stream
+// through LDS (double-buffered, one barrier per tile).  acc[r] = approx dot of user row
+// mfma32_row(r, h) with item lane j.
+template <int DP, int MODE, bool BIAS>
+__global__ __launch_bounds__(256, dcert_wg_per_cu(DP)) void dot16_scan_kernel(DScanArgs A) {
+  constexpr int KS = DP / 16;     // f16 MFMA k-steps
+  constexpr int RS = DP + 8;      // LDS row stride (halfs): conflict-free b128 reads
+  constexpr int CH = DP / 8;      // 16-B chunks per item row
+  constexpr int LD = TILE * CH / 256;  // chunks per thread per tile (1 or 2)
+  __shared__ __attribute__((aligned(16))) _Float16 vs[2][TILE * RS];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5, j = lane & 31;
+  const int p = blockIdx.x;
+  const int64_t b0 = (int64_t)blockIdx.y * 128 + wave * 32;
+  const int nu = (int)std::max<int64_t>(0, std::min<int64_t>(32, A.B - b0));
+  const int64_t part_start = (int64_t)p * A.ipp;
+  const int64_t part_end = std::min<int64_t>(A.I, part_start + A.ipp);
+  const int64_t S = A.istride;
+
+  h8 a[KS];
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    h8 z = {};
+    a[s] = j < nu ? *reinterpret_cast<const h8*>(A.U16 + (b0 + j) * DP + 16 * s + 8 * h) : z;
+  }
+  float tv[16];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int64_t b = b0 + mfma32_row(r, h);
+    tv[r] = (MODE == DSCAN_THRESH && b < A.B) ? A.tau[b] : __builtin_inff();
+  }
+  int ccount = 0;  // THRESH: appends of user row (lane) in this partition
+  int nm = INT_BIG;
+  int64_t mpos = 0, mend = 0;
+  const bool masked = MODE == DSCAN_THRESH && A.mptr != nullptr;
+  if (masked && lane < nu) {
+    const int64_t lo = A.mptr[b0 + lane], hi = A.mptr[b0 + lane + 1];
+    mpos = mask_lower_bound(A.midx, lo, hi, (int)part_start);
+    mend = hi;
+    nm = mpos < mend ? A.midx[mpos] : INT_BIG;
+  }
+  int32_t* seg = MODE == DSCAN_THRESH ? A.buf + (b0 * A.NP + p) * (int64_t)A.capp : nullptr;
+  const int64_t segstride = (int64_t)A.NP * A.capp;
+
+  const int64_t ntiles = part_end > part_start ? hnm_cdiv(part_end - part_start, TILE) : 0;
+  h8 st[LD];
+  float nib = 0.f;
+  auto fetch = [&](int64_t base) {
+#pragma unroll
+    for (int q = 0; q < LD; ++q) {
+      const int f = tid + 256 * q, row = f / CH, c = f % CH;
+      const int64_t n = base + row;
+      h8 z = {};
+      st[q] = n < part_end ? *reinterpret_cast<const h8*>(A.I16 + n * S * DP + 8 * c) : z;
+    }
+    if (BIAS) nib = A.ibs[std::min<int64_t>(base + j, part_end - 1) * S];
+  };
+  auto stash = [&](int bf) {
+#pragma unroll
+    for (int q = 0; q < LD; ++q) {
+      const int f = tid + 256 * q, row = f / CH, c = f % CH;
+      *reinterpret_cast<h8*>(&vs[bf][row * RS + 8 * c]) = st[q];
+    }
+  };
+  if (ntiles > 0) {
+    fetch(part_start);
+    stash(0);
+  }
+  __syncthreads();
+  for (int64_t t = 0; t < ntiles; ++t) {
+    const int64_t base = part_start + t * TILE;
+    const int cur = (int)(t & 1);
+    const float ib = nib;
+    if (t + 1 < ntiles) fetch(base + TILE);
+    if (nu > 0) {
+      f32x16 acc = {};
+#pragma unroll
+      for (int s = 0; s < KS; ++s)
+        acc = mfma16(a[s], *reinterpret_cast<const h8*>(&vs[cur][j * RS + 16 * s + 8 * h]), acc);
+      const int64_t n = base + j;
+      const bool ivalid = n < part_end;
+      float sc[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) sc[r] = BIAS ? acc[r] + ib : acc[r];
+      if (MODE == DSCAN_SAMPLE) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int64_t b = b0 + mfma32_row(r, h);
+          if (ivalid && b < A.B) A.dense[b * A.ldo + n] = sc[r];
+        }
+      } else {
+        const int64_t tile_end = std::min<int64_t>(base + TILE, part_end);
+        if (masked) {  // -inf for filtered (user, item) pairs of this tile (rare path)
+          uint64_t mm = __ballot(lane < 32 && nm < tile_end) & 0xffffffffull;
+          while (mm) {
+            const int u = __builtin_ctzll(mm);
+            mm &= mm - 1;
+            while (true) {
+              const int tgt = hnm_readlane_i(nm, u);
+              if (tgt >= tile_end) break;
+#pragma unroll
+              for (int r = 0; r < 16; ++r)
+                if (mfma32_row(r, h) == u && n == tgt) sc[r] = -__builtin_inff();
+              if (lane == u) {
+                ++mpos;
+                nm = mpos < mend ? A.midx[mpos] : INT_BIG;
+              }
+            }
+          }
+        }
+        unsigned pass = 0;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) pass |= (ivalid && !(sc[r] < tv[r])) ? (1u << r) : 0u;
+        if (__ballot(pass != 0)) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const uint64_t m = __ballot((pass >> r) & 1);
+            if (!m) continue;
+            const unsigned lo = (unsigned)m, hi = (unsigned)(m >> 32);
+            const int i0 = mfma32_row(r, 0), i1 = mfma32_row(r, 1);
+            const int c0 = hnm_readlane_i(ccount, i0), c1 = hnm_readlane_i(ccount, i1);
+            const unsigned mine = h ? hi : lo;
+            const int pos = (h ? c1 : c0) + __popc(mine & ((1u << j) - 1));
+            if (((pass >> r) & 1) && pos < A.capp) seg[(h ? i1 : i0) * segstride + pos] = (int32_t)n;
+            if (lane == i0) ccount += __popc(lo);
+            if (lane == i1) ccount += __popc(hi);
+          }
+        }
+      }
+    }
+    if (t + 1 < ntiles) stash(cur ^ 1);
+    __syncthreads();
+  }
+  if (MODE == DSCAN_THRESH && lane < nu) A.cnt[(b0 + lane) * A.NP + p] = ccount;
+}
+
+// E_u (scaled) and tau_u = (K-th best scaled approx of the sample) - 2 E_u - guard.
+__global__ __launch_bounds__(256) void dcert_tau_kernel(const float* __restrict__ kth, int K,
+                                                        const float* __restrict__ Nu,
+                                                        const float* __restrict__ ubr,
+                                                        const DParams* __restrict__ prm,
+                                                        int64_t B, float* __restrict__ tau,
+                                                        int* __restrict__ flag,
+                                                        float* __restrict__ Eout) {
+  const int64_t b = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (b >= B) return;
+  const float s = prm->s;
+  const float nimax = __uint_as_float(prm->mx[DM_NI]), ibmax = __uint_as_float(prm->mx[DM_IB]);
+  const float scale = s * (Nu[b] * nimax + fabsf(ubr[b]) + ibmax);
+  const float E = s * (DCERT_RHO * Nu[b] * nimax + 2.4e-7f * (fabsf(ubr[b]) + ibmax)) + prm->absb;
+  if (Eout) Eout[b] = E / s;
+  if (!kth) return;
+  const float kv = kth[b * K + (K - 1)];
+  float tv = kv - 2.f * E - 3.814697265625e-06f * scale;  // 2^-18 of the row's score scale
+  tv -= fabsf(tv) * 9.5367431640625e-07f;                 // 2^-20
+  const bool ok = !prm->bad && __builtin_isfinite(tv) && __builtin_isfinite(scale);
+  tau[b] = ok ? tv : __builtin_inff();
+  flag[b] = ok ? 0 : 1;
+}
+
+// ------------------------------------------------------------------ exact re-scoring
+// One wave per user; each lane re-scores one candidate with the sequential fp32 fma chain
+// (k = 0 .. DP-1, zero padding included) the f32 MFMA computes, then (acc + ub) + ib as
+// dot_score_kernel does; exact (score desc, item asc) top-K.
+template <int DP, bool BIAS>
+__global__ __launch_bounds__(256) void dcert_rescore_kernel(
+    DotArgs a, const float* __restrict__ ubr, const int* __restrict__ flag,
+    const int* __restrict__ cnt, const int32_t* __restrict__ buf, int NP, int capp, int K,
+    float* __restrict__ ov, int64_t* __restrict__ oi, int32_t* __restrict__ ovf_rows,
+    int32_t* __restrict__ ovf_cnt, unsigned long long* __restrict__ stats) {
+  __shared__ __attribute__((aligned(16))) float urow[4][DP];
+  __shared__ int pref[4][DCERT_MAX_NP + 1];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int64_t b = (int64_t)blockIdx.x * 4 + wave;
+  const bool live = b < a.B;
+  int c = 0;
+  if (live) {
+    const int64_t uid = a.uids[b];
+    const bool ok = uid >= 0 && uid < a.num_users;
+    for (int k = lane; k < DP; k += 64) urow[wave][k] = (ok && k < a.d) ? a.ut[uid * a.ldu + k] : 0.f;
+    c = lane < NP ? cnt[b * NP + lane] : 0;
+  }
+  int incl = c;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int v = __shfl_up(incl, o);
+    if (lane >= o) incl += v;
+  }
+  if (live) {
+    if (lane == 0) pref[wave][0] = 0;
+    if (lane < NP) pref[wave][lane + 1] = incl;
+  }
+  __syncthreads();
+  if (!live) return;
+  const int n = hnm_readlane_i(incl, 63);
+  if (flag[b] || __ballot(c > capp) != 0 || n < K) {
+    if (lane == 0) {
+      ovf_rows[atomicAdd(ovf_cnt, 1)] = (int32_t)b;
+      if (stats) {
+        atomicAdd(&stats[2], 1ull);
+        if (b == 0) atomicAdd(&stats[0], (unsigned long long)a.B);
+      }
+    }
+    return;
+  }
+  if (stats && lane == 0) {
+    atomicAdd(&stats[1], (unsigned long long)n);
+    if (b == 0) atomicAdd(&stats[0], (unsigned long long)a.B);
+  }
+  const float ub = ubr[b];
+  const int32_t* rowbuf = buf + b * (int64_t)NP * capp;
+  WaveTopK<1> L;
+  L.init();
+  for (int c0 = 0; c0 < n; c0 += 64) {
+    const int g = c0 + lane;
+    const bool ok = g < n;
+    int item = 0;
+    if (ok) {
+      int lo = 0, hi = NP;
+      while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (pref[wave][mid] <= g) lo = mid;
+        else hi = mid;
+      }
+      item = rowbuf[(int64_t)lo * capp + (g - pref[wave][lo])];
+    }
+    const float* irow = a.it + (int64_t)item * a.ldi;
+    float acc = 0.f;
+#pragma unroll 4
+    for (int k4 = 0; k4 < DP / 4; ++k4) {
+      float4 iv = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (4 * k4 < a.d) iv = *reinterpret_cast<const float4*>(irow + 4 * k4);
+      const float4 uv = *reinterpret_cast<const float4*>(&urow[wave][4 * k4]);
+      acc = fmaf(uv.x, iv.x, acc);
+      acc = fmaf(uv.y, iv.y, acc);
+      acc = fmaf(uv.z, iv.z, acc);
+      acc = fmaf(uv.w, iv.w, acc);
+    }
+    float sc = acc;
+    if (BIAS) sc = (acc + ub) + (a.ibias ? a.ibias[item] : 0.f);
+    L.offer(sc, item, ok, K);
+  }
+  L.store(ov ? ov + b * K : nullptr, oi + b * K, K);
+}
+
+__global__ void dcert_debug_out_kernel(float* __restrict__ ap, int64_t lda, int64_t B, int64_t I,
+                                       const float* __restrict__ ubr,
+                                       const DParams* __restrict__ prm) {
+  const int64_t x = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (x >= B * I) return;
+  const int64_t b = x / I, o = b * lda + x % I;
+  ap[o] = ap[o] / prm->s + ubr[b];  // scaled approx (item bias included) -> score units
+}
+
+hnm_status dcert_prepare(hnm_ctx* ctx, const DotArgs& a, const DotCertShape& sh,
+                         const DotCertWs& x) {
+  HNM_HIP_CHECK(hipMemsetAsync(x.prm, 0, sizeof(DParams), ctx->stream));
+  const int ib = (int)std::min<int64_t>(1024, hnm_cdiv(a.I, 4));
+  const int ub = (int)std::min<int64_t>(256, hnm_cdiv(a.B, 4));
+  hipLaunchKernelGGL(dcert_stats_kernel, dim3(ib + ub), dim3(256), 0, ctx->stream, a, x.prm, x.Nu,
+                     x.Ni, x.ubr, ib, ub);
+  HNM_LAUNCH_CHECK();
+  hipLaunchKernelGGL(dcert_scales_kernel, dim3(1), dim3(64), 0, ctx->stream, x.prm, sh.DP);
+  HNM_LAUNCH_CHECK();
+  const int cb = (int)std::min<int64_t>(2048, std::max<int64_t>(1, hnm_cdiv(a.I * sh.DP / 4, 256)));
+  hipLaunchKernelGGL(dcert_convert_kernel, dim3(cb), dim3(256), 0, ctx->stream, a, sh.DP, x.prm,
+                     x.U16, x.I16, x.ibs);
+  HNM_LAUNCH_CHECK();
+  return HNM_OK;
+}
+
+template <int MODE>
+void launch_dscan(hnm_ctx* ctx, dim3 grid, const DScanArgs& s, int DP, bool bias) {
+#define HNM_DS(DPV)                                                                             \
+  if (bias)                                                                                     \
+    hipLaunchKernelGGL((dot16_scan_kernel<DPV, MODE, true>), grid, dim3(256), 0, ctx->stream, s); \
+  else                                                                                          \
+    hipLaunchKernelGGL((dot16_scan_kernel<DPV, MODE, false>), grid, dim3(256), 0, ctx->stream, s);
+  if (DP == 64) {
+    HNM_DS(64)
+  } else {
+    HNM_DS(128)
+  }
+#undef HNM_DS
+}
+
+DScanArgs dscan_args(const DotCertWs& x, const DotArgs& a) {
+  DScanArgs s{};
+  s.U16 = x.U16;
+  s.I16 = x.I16;
+  s.ibs = x.ibs;
+  s.B = a.B;
+  s.istride = 1;
+  return s;
+}
+
+}  // namespace
+
+bool dot_cert_eligible(int d, int64_t I, int K) {
+  return d <= 128 && K <= 64 && I >= DCERT_MIN_ITEMS && I >= 64 * (int64_t)K;
+}
+
+size_t dot_cert_bytes(int64_t B, int64_t I, int d, int K, int num_cus) {
+  return dcert_carve(nullptr, B, I, d, K, num_cus, nullptr);
+}
+
+hnm_status dot_cert_topk(hnm_ctx* ctx, const DotArgs& a, bool bias, void* scratch, float* ov,
+                         int64_t* oi) {
+  const DotCertShape sh = dcert_shape(a.B, a.I, a.d, a.K, ctx->num_cus);
+  DotCertWs x;
+  dcert_carve((char*)scratch, a.B, a.I, a.d, a.K, ctx->num_cus, &x);
+  hnm_status st = dcert_prepare(ctx, a, sh, x);
+  if (st) return st;
+  HNM_HIP_CHECK(hipMemsetAsync(x.ovf_cnt, 0, 4, ctx->stream));
+  const int64_t ublocks = hnm_cdiv(a.B, 128);
+  {  // 1. sample pass -> K-th best per row -> tau
+    DScanArgs s = dscan_args(x, a);
+    s.I = sh.Ns;
+    s.istride = sh.stride;
+    s.dense = x.sdense;
+    s.ldo = sh.Ns;
+    const Partition ps = xcd_partition(sh.Ns, ublocks, ctx->num_cus, sh.DP);
+    s.ipp = ps.ipp;
+    s.NP = ps.np;
+    launch_dscan<DSCAN_SAMPLE>(ctx, dim3((unsigned)ps.np, (unsigned)ublocks), s, sh.DP, bias);
+    HNM_LAUNCH_CHECK();
+    st = hnm_topk_rows_strided(ctx, x.sdense, sh.Ns, a.B, sh.Ns, a.mptr, a.midx, a.K, x.kthv,
+                               x.kthi, sh.stride);
+    if (st) return st;
+    hipLaunchKernelGGL(dcert_tau_kernel, dim3((unsigned)hnm_cdiv(a.B, 256)), dim3(256), 0,
+                       ctx->stream, x.kthv, a.K, x.Nu, x.ubr, x.prm, a.B, x.tau, x.flag, x.E);
+    HNM_LAUNCH_CHECK();
+  }
+  {  // 2. main f16 scan: append approx >= tau_u
+    DScanArgs s = dscan_args(x, a);
+    s.I = a.I;
+    s.mptr = a.mptr;
+    s.midx = a.midx;
+    s.tau = x.tau;
+    s.cnt = x.cnt;
+    s.buf = x.buf;
+    s.capp = sh.capp;
+    s.ipp = sh.part.ipp;
+    s.NP = sh.part.np;
+    hnm_timer_begin(ctx);
+    launch_dscan<DSCAN_THRESH>(ctx, dim3((unsigned)sh.part.np, (unsigned)ublocks), s, sh.DP, bias);
+    hnm_timer_end(ctx);
+    HNM_LAUNCH_CHECK();
+  }
+  // 3. exact re-scoring + top-K; unusable rows queued
+#define HNM_RS(DPV, BV)                                                                         \
+  hipLaunchKernelGGL((dcert_rescore_kernel<DPV, BV>), dim3((unsigned)hnm_cdiv(a.B, 4)), dim3(256), \
+                     0, ctx->stream, a, x.ubr, x.flag, x.cnt, x.buf, sh.part.np, sh.capp, a.K, ov, \
+                     oi, x.ovf_rows, x.ovf_cnt, ctx->stats_dev);
+  if (sh.DP == 64) {
+    if (bias) { HNM_RS(64, true) } else { HNM_RS(64, false) }
+  } else {
+    if (bias) { HNM_RS(128, true) } else { HNM_RS(128, false) }
+  }
+#undef HNM_RS
+  HNM_LAUNCH_CHECK();
+  // 4. exact LIST scan for the queued rows
+  DotArgs af = a;
+  af.rows = x.ovf_rows;
+  af.nrows = x.ovf_cnt;
+  return dot_list_pass(ctx, af, bias, x.cv, x.ci, ov, oi);
+}
+
+hnm_status dot_cert_debug(hnm_ctx* ctx, const DotArgs& a, bool bias, void* scratch,
+                          float* approx, int64_t lda, float* bound) {
+  const DotCertShape sh = dcert_shape(a.B, a.I, a.d, 1, ctx->num_cus);
+  DotCertWs x;
+  dcert_carve((char*)scratch, a.B, a.I, a.d, 1, ctx->num_cus, &x);
+  hnm_status st = dcert_prepare(ctx, a, sh, x);
+  if (st) return st;
+  DScanArgs s = dscan_args(x, a);
+  s.I = a.I;
+  s.dense = approx;
+  s.ldo = lda;
+  const Partition ps = xcd_partition(a.I, hnm_cdiv(a.B, 128), ctx->num_cus, sh.DP);
+  s.ipp = ps.ipp;
+  s.NP = ps.np;
+  launch_dscan<DSCAN_SAMPLE>(ctx, dim3((unsigned)ps.np, (unsigned)hnm_cdiv(a.B, 128)), s, sh.DP,
+                             bias);
+  HNM_LAUNCH_CHECK();
+  hipLaunchKernelGGL(dcert_debug_out_kernel, dim3((unsigned)hnm_cdiv(a.B * a.I, 256)), dim3(256),
+                     0, ctx->stream, approx, lda, a.B, a.I, x.ubr, x.prm);
+  HNM_LAUNCH_CHECK();
+  hipLaunchKernelGGL(dcert_tau_kernel, dim3((unsigned)hnm_cdiv(a.B, 256)), dim3(256), 0,
+                     ctx->stream, nullptr, 1, x.Nu, x.ubr, x.prm, a.B, nullptr, nullptr, bound);
+  HNM_LAUNCH_CHECK();
+  return HNM_OK;
+}

@@ -22,7 +22,7 @@
 #include <algorithm>
 
 #include "hnm_device.h"
-#include "hnm_internal.h"
+#include "dot_internal.h"
 
 hnm_status hnm_topk_merge_i32(hnm_ctx* ctx, const float* cv, const int32_t* ci, int64_t B,
                               int64_t G, int64_t gstride, int64_t bstride, int kc, int k,
@@ -30,37 +30,6 @@ hnm_status hnm_topk_merge_i32(hnm_ctx* ctx, const float* cv, const int32_t* ci, 
 
 
 // ------------------------------------------------------------------ dot kernel
-enum { DOT_LIST = 0, DOT_DENSE = 1, DOT_THRESH = 2 };
-
-struct DotArgs {
-  const float* ut;         // user table [U, ldu]
-  int64_t num_users, ldu;
-  const int64_t* uids;     // [B] user ids of the request rows
-  int64_t B;
-  const float* it;         // item table; item i is row i * istride
-  int64_t I, ldi, istride;
-  int d;
-  const float *ubias, *ibias, *cbias;
-  int64_t ipp;             // items per partition (blockIdx.y)
-  const int64_t* mptr;     // CSR mask over request rows (real item ids)
-  const int32_t* midx;
-  int K;
-  float* cand_v;           // LIST: [launch rows, NP, K]
-  int32_t* cand_i;
-  int NP;
-  float* dense;            // DENSE: [B, ldo]
-  int64_t ldo;
-  const float* tau;        // THRESH: tau of request row r at tau[r * tau_ld]
-  int64_t tau_ld;
-  int* cnt;                // THRESH: [B] append counters
-  float* buf_v;            // THRESH: [B, cap]
-  int32_t* buf_i;
-  int cap;
-  const int32_t* rows;     // optional: launch row b serves request row rows[b] ...
-  const int32_t* nrows;    // ... for b < *nrows (device count)
-  unsigned* err;
-};
-
 // LIST keeps 32 user lists in registers (2 workgroups/CU); the list-free d<=64 modes run 4 (measured faster than 3 despite a small spill).
 template <int DP, int MODE, bool BIAS>
 __global__ __launch_bounds__(256, (MODE == DOT_LIST || DP > 64) ? 2 : 4) void dot_score_kernel(DotArgs A) {
@@ -403,7 +372,7 @@ static hnm_status dot_validate(hnm_ctx* ctx, const float* ut, int64_t U, int64_t
   return HNM_OK;
 }
 
-static DotArgs dot_args(hnm_ctx* ctx, const float* ut, int64_t U, int64_t ldu, const int64_t* ids,
+DotArgs dot_args(hnm_ctx* ctx, const float* ut, int64_t U, int64_t ldu, const int64_t* ids,
                         int64_t B, const float* it, int64_t I, int64_t ldi, int d, const float* ub,
                         const float* ib, const float* cb, const int64_t* mptr,
                         const int32_t* midx, int K) {
@@ -418,7 +387,7 @@ static DotArgs dot_args(hnm_ctx* ctx, const float* ut, int64_t U, int64_t ldu, c
 
 // LIST pass over `a` (items a.I with stride a.istride) -> merged top-K into ov/oi rows
 // (rows remapped through a.rows when set).
-static hnm_status dot_list_pass(hnm_ctx* ctx, DotArgs a, bool bias, float* cv, int32_t* ci,
+hnm_status dot_list_pass(hnm_ctx* ctx, DotArgs a, bool bias, float* cv, int32_t* ci,
                                 float* ov, int64_t* oi) {
   const int64_t ublocks = hnm_cdiv(a.B, 128);
   Partition part = choose_partition(a.I, ublocks, ctx->num_cus);
@@ -432,7 +401,7 @@ static hnm_status dot_list_pass(hnm_ctx* ctx, DotArgs a, bool bias, float* cv, i
                              ov, oi, a.rows, a.nrows);
 }
 
-static size_t list_cand_bytes(int64_t B, int64_t I, int K, int num_cus) {
+size_t list_cand_bytes(int64_t B, int64_t I, int K, int num_cus) {
   Partition part = choose_partition(I, hnm_cdiv(B, 128), num_cus);
   return hnm_align((size_t)B * part.np * K * 4);
 }
@@ -452,6 +421,12 @@ extern "C" hnm_status hnm_dot_topk_f32(hnm_ctx* ctx, const float* user_tab, int6
   const bool bias = user_bias || item_bias || const_bias;
   DotArgs a = dot_args(ctx, user_tab, num_users, ldu, user_ids, B, item_tab, I, ldi, d, user_bias,
                        item_bias, const_bias, mask_ptr, mask_idx, k);
+  if (ctx->prefilter && dot_cert_eligible(d, I, k)) {  // certified f16 scan (dot_cert.hip)
+    void* w;
+    st = hnm_workspace(ctx, dot_cert_bytes(B, I, d, k, ctx->num_cus), &w);
+    if (st) return st;
+    return dot_cert_topk(ctx, a, bias, w, out_val, out_idx);
+  }
   if (I < THRESH_MIN_ITEMS || I < 4 * (int64_t)k) {
     const size_t sc = list_cand_bytes(B, I, k, ctx->num_cus);
     void* w;
@@ -579,3 +554,23 @@ extern "C" hnm_status hnm_topk_rows_f32(hnm_ctx* ctx, const float* scores, int64
   return HNM_OK;
 }
 
+
+extern "C" hnm_status hnm_dot_prefilter_debug_f32(hnm_ctx* ctx, const float* user_tab,
+                                                  int64_t num_users, int64_t ldu,
+                                                  const int64_t* user_ids, int64_t B,
+                                                  const float* item_tab, int64_t num_items,
+                                                  int64_t ldi, int d, const float* user_bias,
+                                                  const float* item_bias, const float* const_bias,
+                                                  float* approx, int64_t lda, float* bound) {
+  hnm_status st = dot_validate(ctx, user_tab, num_users, ldu, user_ids, item_tab, num_items, ldi, d);
+  if (st) return st;
+  HNM_REQUIRE(approx && bound && lda >= num_items, HNM_EINVAL, "dot_prefilter_debug: bad output");
+  if (B <= 0) return HNM_OK;
+  const bool bias = user_bias || item_bias || const_bias;
+  DotArgs a = dot_args(ctx, user_tab, num_users, ldu, user_ids, B, item_tab, num_items, ldi, d,
+                       user_bias, item_bias, const_bias, nullptr, nullptr, 1);
+  void* w;
+  st = hnm_workspace(ctx, dot_cert_bytes(B, num_items, d, 1, ctx->num_cus), &w);
+  if (st) return st;
+  return dot_cert_debug(ctx, a, bias, w, approx, lda, bound);
+}

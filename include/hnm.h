@@ -56,9 +56,9 @@ hnm_status hnm_ctx_set_stream(hnm_ctx* ctx, void* hip_stream);
 hnm_status hnm_ctx_reserve(hnm_ctx* ctx, size_t bytes);   /* pre-grow workspace */
 hnm_status hnm_ctx_check(hnm_ctx* ctx);                   /* sync; HNM_EOOB if flagged */
 hnm_status hnm_ctx_num_cus(hnm_ctx* ctx, int* out);
-/* Options.  HNM_OPT_PREFILTER (default 1): NCF top-K scans the catalogue with the certified
- * f16 pre-filter and re-scores the surviving candidates in exact fp32 (results identical
- * to the fp32 scan); 0 = exact fp32 scan of every item. */
+/* Options.  HNM_OPT_PREFILTER (default 1): NCF and dot-product top-K scan the catalogue
+ * with the certified f16 pre-filter and re-score the surviving candidates in exact fp32
+ * (results identical to the fp32 scan); 0 = exact fp32 scan of every item. */
 enum { HNM_OPT_PREFILTER = 1,
        HNM_OPT_SCAN_USERS = 2 /* tuning: users per iteration of the f16 scan (1 or 2) */ };
 hnm_status hnm_ctx_set_option(hnm_ctx* ctx, int option, int64_t value);
@@ -104,6 +104,15 @@ hnm_status hnm_dot_topk_f32(hnm_ctx* ctx, const float* user_tab, int64_t num_use
                             const float* const_bias, const int64_t* mask_ptr,
                             const int32_t* mask_idx, int k, float* out_val,
                             int64_t* out_idx);
+/* Diagnostics of the certified f16 pre-filter of hnm_dot_topk_f32 (no reference
+ * counterpart): approx[b, i] = the f16 scan's score (biases included), bound[b] = the
+ * row's error bound; |approx - exact| <= bound for every item (tests check it). */
+hnm_status hnm_dot_prefilter_debug_f32(hnm_ctx* ctx, const float* user_tab, int64_t num_users,
+                                       int64_t ldu, const int64_t* user_ids, int64_t B,
+                                       const float* item_tab, int64_t num_items, int64_t ldi,
+                                       int d, const float* user_bias, const float* item_bias,
+                                       const float* const_bias, float* approx, int64_t lda,
+                                       float* bound);
 /* Dense variant: out[b, i] (ldo >= num_items), the predict_all_items matrix. */
 hnm_status hnm_dot_scores_f32(hnm_ctx* ctx, const float* user_tab, int64_t num_users,
                               int64_t ldu, const int64_t* user_ids, int64_t B,

@@ -133,3 +133,95 @@ def test_unusable_bound_falls_back():
     assert np.array_equal(ei, pi)
     assert np.array_equal(ev.view(np.uint32), pv.view(np.uint32))
     assert stats[2] == 300
+
+
+# ------------------------------------------------------------------ dot models (LightGCN / MF)
+def dot_topk(ut, ids, it, k, ub=None, ib=None, cb=None, mptr=None, midx=None):
+    B = ids.numel()
+    ov = torch.empty(B, k, device=DEV)
+    oi = torch.empty(B, k, dtype=torch.int64, device=DEV)
+    _lib.check(_lib.fn("hnm_dot_topk_f32")(
+        _lib.ctx(ids.device), _lib.ptr(ut), ut.shape[0], ut.stride(0), _lib.ptr(ids), B,
+        _lib.ptr(it), it.shape[0], it.stride(0), ut.shape[1], _lib.ptr(ub), _lib.ptr(ib),
+        _lib.ptr(cb), _lib.ptr(mptr), _lib.ptr(midx), k, _lib.ptr(ov), _lib.ptr(oi)), "dot_topk")
+    _lib.sync_check(ids.device)
+    return ov.cpu().numpy(), oi.cpu().numpy()
+
+
+def dot_both(*args, **kw):
+    dev = args[1].device
+    _lib.set_prefilter(dev, False)
+    try:
+        ex = dot_topk(*args, **kw)
+    finally:
+        _lib.set_prefilter(dev, True)
+    _lib.prefilter_stats(dev, reset=True)
+    pf = dot_topk(*args, **kw)
+    return ex, pf, _lib.prefilter_stats(dev, reset=True)
+
+
+def dot_tables(d, U=50000, I=syn.HM_ITEMS, seed=0, bias=False):
+    g = torch.Generator().manual_seed(seed)
+    ut = (torch.randn(U, d, generator=g) * 0.1).to(DEV)
+    it = (torch.randn(I, d, generator=g) * 0.1 * (1 + torch.rand(I, 1, generator=g))).to(DEV)
+    b = None
+    if bias:
+        b = ((torch.randn(U, generator=g) * 0.05).to(DEV), (torch.randn(I, generator=g) * 0.05).to(DEV),
+             torch.tensor([0.3], device=DEV))
+    return ut, it, b
+
+
+@pytest.mark.parametrize("d,bias", [(64, False), (128, False), (64, True), (32, True)])
+def test_dot_bound_holds(d, bias):
+    ut, it, b = dot_tables(d, bias=bias)
+    ids = torch.from_numpy(syn.user_batch(ut.shape[0], 40, seed=3)).to(DEV)
+    ub, ib, cb = b if b else (None, None, None)
+    I = it.shape[0]
+    approx = torch.empty(40, I, device=DEV)
+    bound = torch.empty(40, device=DEV)
+    _lib.check(_lib.fn("hnm_dot_prefilter_debug_f32")(
+        _lib.ctx(ids.device), _lib.ptr(ut), ut.shape[0], ut.stride(0), _lib.ptr(ids), 40,
+        _lib.ptr(it), I, it.stride(0), d, _lib.ptr(ub), _lib.ptr(ib), _lib.ptr(cb),
+        _lib.ptr(approx), I, _lib.ptr(bound)), "dot_prefilter_debug")
+    _lib.sync_check(ids.device)
+    exact = ut[ids] @ it.T
+    if b:
+        exact = exact + ub[ids][:, None] + cb + ib[None, :]
+    ratio = ((approx - exact).abs().amax(1) / bound).max().item()
+    print(f"d={d} bias={bias}: max err / bound = {ratio:.4f}, bound / std = "
+          f"{(bound / exact.std(1)).mean().item():.2e}")
+    assert ratio <= 1.0
+
+
+@pytest.mark.parametrize("d,bias,B", [(64, False, 4096), (128, False, 1000), (64, True, 777),
+                                      (32, True, 5)])
+def test_dot_prefilter_identical(d, bias, B):
+    ut, it, b = dot_tables(d, bias=bias, seed=d + B)
+    ids = torch.from_numpy(syn.user_batch(ut.shape[0], B, seed=B)).to(DEV)
+    kw = dict(zip(("ub", "ib", "cb"), b)) if b else {}
+    (ev, ei), (pv, pi), stats = dot_both(ut, ids, it, 12, **kw)
+    assert np.array_equal(ei, pi)
+    assert np.array_equal(ev.view(np.uint32), pv.view(np.uint32))
+    rows, cands, fallback = stats
+    print(f"d={d} B={B}: candidates/row {cands / max(rows - fallback, 1):.1f}, fallback {fallback}")
+    assert rows == B and fallback == 0
+
+
+def test_dot_prefilter_masks_ties_fallback():
+    d, I = 64, 30000
+    ut, it, _ = dot_tables(d, U=2000, I=I, seed=5)
+    it[100:200] = it[100]  # 100 exact ties
+    ids = torch.arange(0, 300, device=DEV)
+    rng = np.random.default_rng(1)
+    f = {u: set(rng.integers(0, I, 40).tolist()) | set(range(100, 150)) for u in range(0, 300, 3)}
+    f[7] = set(range(I)) - {5, 17}  # < K unfiltered items -> fallback row
+    from hnm_recommendation_amd.models.base import filter_csr
+    mptr, midx = filter_csr(ids, f, I, ids.device)
+    (ev, ei), (pv, pi), stats = dot_both(ut, ids, it, 12, mptr=mptr, midx=midx)
+    assert np.array_equal(ei, pi) and np.array_equal(ev.view(np.uint32), pv.view(np.uint32))
+    assert sorted(pi[7, :2].tolist()) == [5, 17] and np.isneginf(pv[7, 2:]).all()
+    assert stats[2] >= 1
+    # degenerate user (zero row): every item ties -> overflow -> exact fallback
+    ut[11] = 0
+    (ev, ei), (pv, pi), stats = dot_both(ut, ids, it, 12)
+    assert np.array_equal(ei, pi) and pi[11].tolist() == list(range(12))
