@@ -42,7 +42,7 @@ __host__ __device__ constexpr int dcert_wg_per_cu(int DP) { return DP > 64 ? 3 :
 enum { DM_U, DM_I, DM_NI, DM_IB, DM_N };
 
 struct DParams {
-  unsigned mx[DM_N];  // float bits of non-negative maxima (NaN-propagating atomicMax)
+  unsigned mx[DM_N];  // float bits of non-negative maxima (reduced from per-block partials)
   float su, si, s;    // f16 scales; s = su * si is the scan's score unit
   float absb;         // subnormal slack, scaled units
   int bad;
@@ -67,7 +67,7 @@ __device__ __forceinline__ float pow2_below_inv(float m) {  // 2^-e with m < 2^e
 
 struct DotCertWs {
   DParams* prm;
-  float *Nu, *Ni, *ubr, *ibs, *tau, *E, *kthv, *sdense;
+  float *Nu, *Ni, *ubr, *ibs, *tau, *E, *kthv, *sdense, *part;
   int64_t* kthi;
   int *cnt, *flag;
   int32_t *buf, *ovf_cnt, *ovf_rows;
@@ -79,7 +79,8 @@ struct DotCertWs {
 struct DotCertShape {
   int DP;
   int64_t stride, Ns;
-  Partition part;
+  Partition spart;  // of the sample pass
+  Partition part;   // of the main scan
   int capp;
 };
 
@@ -100,6 +101,7 @@ DotCertShape dcert_shape(int64_t B, int64_t I, int d, int K, int num_cus) {
   sh.stride = std::max<int64_t>(1, I / DCERT_SAMPLE);
   sh.Ns = hnm_cdiv(I, sh.stride);
   sh.part = xcd_partition(I, hnm_cdiv(B, 128), num_cus, sh.DP);
+  sh.spart = xcd_partition(sh.Ns, hnm_cdiv(B, 128), num_cus, sh.DP);
   const int64_t total = std::min<int64_t>(8192, std::max<int64_t>(256, 8 * (int64_t)K * sh.stride));
   sh.capp = (int)std::max<int64_t>(32, std::min<int64_t>(total, hnm_cdiv(4 * total, sh.part.np)));
   return sh;
@@ -116,6 +118,7 @@ size_t dcert_carve(char* base, int64_t B, int64_t I, int d, int K, int num_cus, 
   DotCertWs x;
   x.prm = (DParams*)take(sizeof(DParams));
   x.Nu = (float*)take(B * 4);
+  x.part = (float*)take(4 * 4 * (2048 + 512));
   x.Ni = (float*)take(I * 4);
   x.ubr = (float*)take(B * 4);
   x.ibs = (float*)take(I * 4);
@@ -128,7 +131,7 @@ size_t dcert_carve(char* base, int64_t B, int64_t I, int d, int K, int num_cus, 
   x.ovf_cnt = (int32_t*)take(256);
   x.ovf_rows = (int32_t*)take(B * 4);
   x.buf = (int32_t*)take((size_t)B * sh.part.np * sh.capp * 4);
-  x.sdense = (float*)take((size_t)B * sh.Ns * 4);
+  x.sdense = (float*)take((size_t)B * sh.spart.np * 32 * 4);
   x.U16 = (_Float16*)take((size_t)B * sh.DP * 2);
   x.I16 = (_Float16*)take((size_t)I * sh.DP * 2);
   const size_t lb = list_cand_bytes(B, I, K, num_cus);
@@ -140,8 +143,8 @@ size_t dcert_carve(char* base, int64_t B, int64_t I, int d, int K, int num_cus, 
 
 // ------------------------------------------------------------------ statistics + f16 copies
 // Users: wave per request row (the a1 gather fused), ||u||, user bias (+ global bias).
-// Items: wave per item, ||i||.  Maxima -> prm (atomicMax on float bits).
-__global__ __launch_bounds__(256) void dcert_stats_kernel(DotArgs a, DParams* prm,
+// Items: ||i|| with LPI lanes per row.  Per-block partial maxima -> part[block][4].
+__global__ __launch_bounds__(256) void dcert_stats_kernel(DotArgs a, float* __restrict__ part,
                                                           float* __restrict__ Nu,
                                                           float* __restrict__ Ni,
                                                           float* __restrict__ ubr, int item_blocks,
@@ -151,16 +154,24 @@ __global__ __launch_bounds__(256) void dcert_stats_kernel(DotArgs a, DParams* pr
   float m0 = 0.f, m1 = 0.f, m2 = 0.f;
   const bool items = (int)blockIdx.x < item_blocks;
   if (items) {  // m0 = max|i_k|, m1 = max ||i||, m2 = max |ib|
-    for (int64_t i = (int64_t)blockIdx.x * 4 + wave; i < a.I; i += (int64_t)item_blocks * 4) {
-      const float* row = a.it + i * a.ldi;
-      const float v0 = lane < a.d ? row[lane] : 0.f;
-      const float v1 = lane + 64 < a.d ? row[lane + 64] : 0.f;
-      m0 = nmax(m0, nmax(fabsf(v0), fabsf(v1)));
-      const float n = sqrtf(wave_sum(v0 * v0 + v1 * v1));
-      m1 = nmax(m1, n);
-      if (lane == 0) {
-        Ni[i] = n;
-        if (a.ibias) m2 = nmax(m2, fabsf(a.ibias[i]));
+    // LPI lanes x float4 per item row (d <= 4 LPI), 64 / LPI items per wave step
+    const int LPI = a.d <= 64 ? 16 : 32, ipw = 64 / LPI;
+    const int sub = lane / LPI, l = lane % LPI;
+    for (int64_t i0 = ((int64_t)blockIdx.x * 4 + wave) * ipw; i0 < a.I;
+         i0 += (int64_t)item_blocks * 4 * ipw) {
+      const int64_t i = i0 + sub;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (i < a.I && 4 * l < a.d) v = *reinterpret_cast<const float4*>(a.it + i * a.ldi + 4 * l);
+      m0 = nmax(m0, nmax(nmax(fabsf(v.x), fabsf(v.y)), nmax(fabsf(v.z), fabsf(v.w))));
+      float q = v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+      for (int o = LPI / 2; o >= 1; o >>= 1) q += __shfl_xor(q, o);
+      const float n = sqrtf(q);
+      if (i < a.I) {
+        m1 = nmax(m1, n);
+        if (l == 0) {
+          Ni[i] = n;
+          if (a.ibias) m2 = nmax(m2, fabsf(a.ibias[i]));
+        }
       }
     }
   } else {  // m0 = max|u_k|
@@ -193,13 +204,36 @@ __global__ __launch_bounds__(256) void dcert_stats_kernel(DotArgs a, DParams* pr
   if (tid < 3) {
     float m = red[0][tid];
     for (int w = 1; w < 4; ++w) m = nmax(m, red[w][tid]);
-    const int slot = items ? (tid == 0 ? DM_I : tid == 1 ? DM_NI : DM_IB) : (tid == 0 ? DM_U : -1);
-    if (slot >= 0) atomicMax(&prm->mx[slot], __float_as_uint(m));
+    part[blockIdx.x * 4 + tid] = m;  // per-block partials, reduced by dcert_scales_kernel
   }
 }
 
-__global__ void dcert_scales_kernel(DParams* prm, int DP) {
-  if (threadIdx.x != 0) return;
+__global__ __launch_bounds__(256) void dcert_scales_kernel(DParams* prm, int DP,
+                                                           const float* __restrict__ part,
+                                                           int item_blocks, int user_blocks,
+                                                           int* __restrict__ ovf_cnt) {
+  __shared__ float pm[4][4];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  float mi = 0.f, mn = 0.f, mb = 0.f, mu = 0.f;  // items: max|i|, max||i||, max|ib|; users: max|u|
+  for (int blk = tid; blk < item_blocks + user_blocks; blk += 256) {
+    const float* v = part + blk * 4;
+    if (blk < item_blocks) {
+      mi = nmax(mi, v[0]); mn = nmax(mn, v[1]); mb = nmax(mb, v[2]);
+    } else {
+      mu = nmax(mu, v[0]);
+    }
+  }
+  mi = wave_max(mi); mn = wave_max(mn); mb = wave_max(mb); mu = wave_max(mu);
+  if (lane == 0) { pm[wave][0] = mi; pm[wave][1] = mn; pm[wave][2] = mb; pm[wave][3] = mu; }
+  __syncthreads();
+  if (tid != 0) return;
+  for (int w = 1; w < 4; ++w)
+    for (int q = 0; q < 4; ++q) pm[0][q] = nmax(pm[0][q], pm[w][q]);
+  prm->mx[DM_I] = __float_as_uint(pm[0][0]);
+  prm->mx[DM_NI] = __float_as_uint(pm[0][1]);
+  prm->mx[DM_IB] = __float_as_uint(pm[0][2]);
+  prm->mx[DM_U] = __float_as_uint(pm[0][3]);
+  if (ovf_cnt) *ovf_cnt = 0;
   const float mU = __uint_as_float(prm->mx[DM_U]), mI = __uint_as_float(prm->mx[DM_I]);
   const float mN = __uint_as_float(prm->mx[DM_NI]), mB = __uint_as_float(prm->mx[DM_IB]);
   const float lim = 1099511627776.f;  // 2^40
@@ -254,7 +288,11 @@ __global__ __launch_bounds__(256) void dcert_convert_kernel(DotArgs a, int DP,
 }
 
 // ------------------------------------------------------------------ f16 scan
-enum { DSCAN_SAMPLE = 0, DSCAN_THRESH = 1 };
+// DENSE: dense[b][n] = scaled approx (diagnostics).  SAMPLE: per (user, partition, item
+// lane) running max of the scaled approx over the strided sample (masked items excluded)
+// -> dense[b][p * 32 + j]; the K-th best of those maxima is a lower bound of the sample's
+// K-th best.  THRESH: append approx >= tau_b to the (user, partition) segment.
+enum { DSCAN_DENSE = 0, DSCAN_THRESH = 1, DSCAN_SAMPLE = 2 };
 
 struct DScanArgs {
   const _Float16* U16;  // [B, DP]
@@ -308,12 +346,15 @@ __global__ __launch_bounds__(256, dcert_wg_per_cu(DP)) void dot16_scan_kernel(DS
     tv[r] = (MODE == DSCAN_THRESH && b < A.B) ? A.tau[b] : __builtin_inff();
   }
   int ccount = 0;  // THRESH: appends of user row (lane) in this partition
+  float rmax[MODE == DSCAN_SAMPLE ? 16 : 1];  // SAMPLE: running max per C row
+#pragma unroll
+  for (int r = 0; r < (MODE == DSCAN_SAMPLE ? 16 : 1); ++r) rmax[r] = -__builtin_inff();
   int nm = INT_BIG;
   int64_t mpos = 0, mend = 0;
-  const bool masked = MODE == DSCAN_THRESH && A.mptr != nullptr;
+  const bool masked = MODE != DSCAN_DENSE && A.mptr != nullptr;
   if (masked && lane < nu) {
     const int64_t lo = A.mptr[b0 + lane], hi = A.mptr[b0 + lane + 1];
-    mpos = mask_lower_bound(A.midx, lo, hi, (int)part_start);
+    mpos = mask_lower_bound(A.midx, lo, hi, (int)(part_start * S));
     mend = hi;
     nm = mpos < mend ? A.midx[mpos] : INT_BIG;
   }
@@ -360,7 +401,7 @@ __global__ __launch_bounds__(256, dcert_wg_per_cu(DP)) void dot16_scan_kernel(DS
       float sc[16];
 #pragma unroll
       for (int r = 0; r < 16; ++r) sc[r] = BIAS ? acc[r] + ib : acc[r];
-      if (MODE == DSCAN_SAMPLE) {
+      if (MODE == DSCAN_DENSE) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int64_t b = b0 + mfma32_row(r, h);
@@ -369,16 +410,19 @@ __global__ __launch_bounds__(256, dcert_wg_per_cu(DP)) void dot16_scan_kernel(DS
       } else {
         const int64_t tile_end = std::min<int64_t>(base + TILE, part_end);
         if (masked) {  // -inf for filtered (user, item) pairs of this tile (rare path)
-          uint64_t mm = __ballot(lane < 32 && nm < tile_end) & 0xffffffffull;
+          const int64_t real_end = (tile_end - 1) * S + 1;  // real ids of this tile are < real_end
+          uint64_t mm = __ballot(lane < 32 && nm < real_end) & 0xffffffffull;
           while (mm) {
             const int u = __builtin_ctzll(mm);
             mm &= mm - 1;
             while (true) {
               const int tgt = hnm_readlane_i(nm, u);
-              if (tgt >= tile_end) break;
+              if (tgt >= real_end) break;
+              if (tgt % S == 0) {
 #pragma unroll
-              for (int r = 0; r < 16; ++r)
-                if (mfma32_row(r, h) == u && n == tgt) sc[r] = -__builtin_inff();
+                for (int r = 0; r < 16; ++r)
+                  if (mfma32_row(r, h) == u && n == tgt / S) sc[r] = -__builtin_inff();
+              }
               if (lane == u) {
                 ++mpos;
                 nm = mpos < mend ? A.midx[mpos] : INT_BIG;
@@ -386,30 +430,47 @@ __global__ __launch_bounds__(256, dcert_wg_per_cu(DP)) void dot16_scan_kernel(DS
             }
           }
         }
-        unsigned pass = 0;
+        if (MODE == DSCAN_SAMPLE) {
 #pragma unroll
-        for (int r = 0; r < 16; ++r) pass |= (ivalid && !(sc[r] < tv[r])) ? (1u << r) : 0u;
-        if (__ballot(pass != 0)) {
+          for (int r = 0; r < 16; ++r)
+            if (ivalid) rmax[r] = (sc[r] > rmax[r] || sc[r] != sc[r]) ? sc[r] : rmax[r];  // NaN sticks
+        } else {
+        // any pass in this tile?  one compare per score (v_cmp + s_or); with ~100 candidates
+        // per user about one tile in two has an append, so the append path stays lean:
+        // per row a ballot (a v_cmp into SGPRs) and the store only where it fired
+        bool any = false;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) any |= !(sc[r] < tv[r]);
+        if (__ballot(ivalid && any)) {
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
-            const uint64_t m = __ballot((pass >> r) & 1);
+            const uint64_t m = __ballot(ivalid && !(sc[r] < tv[r]));
             if (!m) continue;
             const unsigned lo = (unsigned)m, hi = (unsigned)(m >> 32);
-            const int i0 = mfma32_row(r, 0), i1 = mfma32_row(r, 1);
+            const int i0 = mfma32_row(r, 0), i1 = mfma32_row(r, 1);  // compile-time rows
             const int c0 = hnm_readlane_i(ccount, i0), c1 = hnm_readlane_i(ccount, i1);
             const unsigned mine = h ? hi : lo;
             const int pos = (h ? c1 : c0) + __popc(mine & ((1u << j) - 1));
-            if (((pass >> r) & 1) && pos < A.capp) seg[(h ? i1 : i0) * segstride + pos] = (int32_t)n;
+            if (((mine >> j) & 1) && pos < A.capp)
+              seg[(h ? i1 : i0) * segstride + pos] = (int32_t)n;
             if (lane == i0) ccount += __popc(lo);
             if (lane == i1) ccount += __popc(hi);
           }
         }
+        }  // THRESH
       }
     }
     if (t + 1 < ntiles) stash(cur ^ 1);
     __syncthreads();
   }
   if (MODE == DSCAN_THRESH && lane < nu) A.cnt[(b0 + lane) * A.NP + p] = ccount;
+  if (MODE == DSCAN_SAMPLE) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int64_t b = b0 + mfma32_row(r, h);
+      if (b < A.B) A.dense[b * A.ldo + p * 32 + j] = rmax[r];
+    }
+  }
 }
 
 // E_u (scaled) and tau_u = (K-th best scaled approx of the sample) - 2 E_u - guard.
@@ -487,38 +548,58 @@ __global__ __launch_bounds__(256) void dcert_rescore_kernel(
   }
   const float ub = ubr[b];
   const int32_t* rowbuf = buf + b * (int64_t)NP * capp;
-  WaveTopK<1> L;
-  L.init();
-  for (int c0 = 0; c0 < n; c0 += 64) {
-    const int g = c0 + lane;
-    const bool ok = g < n;
-    int item = 0;
-    if (ok) {
-      int lo = 0, hi = NP;
-      while (hi - lo > 1) {
-        const int mid = (lo + hi) >> 1;
-        if (pref[wave][mid] <= g) lo = mid;
-        else hi = mid;
-      }
-      item = rowbuf[(int64_t)lo * capp + (g - pref[wave][lo])];
+  auto cand = [&](int g) -> int {  // segment of candidate g: last p with pref[p] <= g
+    int lo = 0, hi = NP;
+    while (hi - lo > 1) {
+      const int mid = (lo + hi) >> 1;
+      if (pref[wave][mid] <= g) lo = mid;
+      else hi = mid;
     }
-    const float* irow = a.it + (int64_t)item * a.ldi;
+    return rowbuf[(int64_t)lo * capp + (g - pref[wave][lo])];
+  };
+  // Rounds of 128 slots: slots 0..K-1 carry the running top-K, slots K..127 take the next
+  // candidates; one bitonic sort per round (no serial list inserts).
+  auto score = [&](int it) -> float {
+    const float* r0 = a.it + (int64_t)it * a.ldi;
     float acc = 0.f;
 #pragma unroll 4
     for (int k4 = 0; k4 < DP / 4; ++k4) {
-      float4 iv = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (4 * k4 < a.d) iv = *reinterpret_cast<const float4*>(irow + 4 * k4);
+      float4 v0 = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (4 * k4 < a.d) v0 = *reinterpret_cast<const float4*>(r0 + 4 * k4);
       const float4 uv = *reinterpret_cast<const float4*>(&urow[wave][4 * k4]);
-      acc = fmaf(uv.x, iv.x, acc);
-      acc = fmaf(uv.y, iv.y, acc);
-      acc = fmaf(uv.z, iv.z, acc);
-      acc = fmaf(uv.w, iv.w, acc);
+      acc = fmaf(uv.x, v0.x, acc);
+      acc = fmaf(uv.y, v0.y, acc);
+      acc = fmaf(uv.z, v0.z, acc);
+      acc = fmaf(uv.w, v0.w, acc);
     }
-    float sc = acc;
-    if (BIAS) sc = (acc + ub) + (a.ibias ? a.ibias[item] : 0.f);
-    L.offer(sc, item, ok, K);
+    return BIAS ? (acc + ub) + (a.ibias ? a.ibias[it] : 0.f) : acc;
+  };
+  float v0 = -__builtin_inff(), v1 = -__builtin_inff();
+  int i0 = HNM_SENTINEL_IDX, i1 = HNM_SENTINEL_IDX;
+  bool nan = false;
+  for (int c0 = 0; c0 < n; c0 += 128 - K) {
+    const int g0 = c0 + lane - K, g1 = c0 + 64 + lane - K;  // candidate of slot lane / lane+64
+    if (lane >= K) {
+      const bool ok = g0 < n;
+      i0 = ok ? cand(g0) : HNM_SENTINEL_IDX;
+      v0 = ok ? score(i0) : -__builtin_inff();
+    }
+    {
+      const bool ok = g1 < n;
+      i1 = ok ? cand(g1) : HNM_SENTINEL_IDX;
+      v1 = ok ? score(i1) : -__builtin_inff();
+    }
+    nan |= (v0 != v0) || (v1 != v1);
+    hnm_sort128(v0, i0, v1, i1);
   }
-  L.store(ov ? ov + b * K : nullptr, oi + b * K, K);
+  if (__ballot(nan)) {  // NaN scores: exact LIST semantics via the fallback
+    if (lane == 0) ovf_rows[atomicAdd(ovf_cnt, 1)] = (int32_t)b;
+    return;
+  }
+  if (lane < K) {
+    if (ov) ov[b * K + lane] = v0;
+    oi[b * K + lane] = i0 == HNM_SENTINEL_IDX ? -1 : i0;
+  }
 }
 
 __global__ void dcert_debug_out_kernel(float* __restrict__ ap, int64_t lda, int64_t B, int64_t I,
@@ -532,13 +613,13 @@ __global__ void dcert_debug_out_kernel(float* __restrict__ ap, int64_t lda, int6
 
 hnm_status dcert_prepare(hnm_ctx* ctx, const DotArgs& a, const DotCertShape& sh,
                          const DotCertWs& x) {
-  HNM_HIP_CHECK(hipMemsetAsync(x.prm, 0, sizeof(DParams), ctx->stream));
-  const int ib = (int)std::min<int64_t>(1024, hnm_cdiv(a.I, 4));
-  const int ub = (int)std::min<int64_t>(256, hnm_cdiv(a.B, 4));
-  hipLaunchKernelGGL(dcert_stats_kernel, dim3(ib + ub), dim3(256), 0, ctx->stream, a, x.prm, x.Nu,
-                     x.Ni, x.ubr, ib, ub);
+  const int ib = (int)std::min<int64_t>(2048, hnm_cdiv(a.I, 16));
+  const int ub = (int)std::min<int64_t>(512, hnm_cdiv(a.B, 4));
+  hipLaunchKernelGGL(dcert_stats_kernel, dim3(ib + ub), dim3(256), 0, ctx->stream, a, x.part,
+                     x.Nu, x.Ni, x.ubr, ib, ub);
   HNM_LAUNCH_CHECK();
-  hipLaunchKernelGGL(dcert_scales_kernel, dim3(1), dim3(64), 0, ctx->stream, x.prm, sh.DP);
+  hipLaunchKernelGGL(dcert_scales_kernel, dim3(1), dim3(256), 0, ctx->stream, x.prm, sh.DP, x.part,
+                     ib, ub, x.ovf_cnt);
   HNM_LAUNCH_CHECK();
   const int cb = (int)std::min<int64_t>(2048, std::max<int64_t>(1, hnm_cdiv(a.I * sh.DP / 4, 256)));
   hipLaunchKernelGGL(dcert_convert_kernel, dim3(cb), dim3(256), 0, ctx->stream, a, sh.DP, x.prm,
@@ -589,21 +670,21 @@ hnm_status dot_cert_topk(hnm_ctx* ctx, const DotArgs& a, bool bias, void* scratc
   dcert_carve((char*)scratch, a.B, a.I, a.d, a.K, ctx->num_cus, &x);
   hnm_status st = dcert_prepare(ctx, a, sh, x);
   if (st) return st;
-  HNM_HIP_CHECK(hipMemsetAsync(x.ovf_cnt, 0, 4, ctx->stream));
   const int64_t ublocks = hnm_cdiv(a.B, 128);
   {  // 1. sample pass -> K-th best per row -> tau
     DScanArgs s = dscan_args(x, a);
     s.I = sh.Ns;
     s.istride = sh.stride;
+    s.mptr = a.mptr;
+    s.midx = a.midx;
     s.dense = x.sdense;
-    s.ldo = sh.Ns;
-    const Partition ps = xcd_partition(sh.Ns, ublocks, ctx->num_cus, sh.DP);
-    s.ipp = ps.ipp;
-    s.NP = ps.np;
-    launch_dscan<DSCAN_SAMPLE>(ctx, dim3((unsigned)ps.np, (unsigned)ublocks), s, sh.DP, bias);
+    s.ldo = sh.spart.np * 32;
+    s.ipp = sh.spart.ipp;
+    s.NP = sh.spart.np;
+    launch_dscan<DSCAN_SAMPLE>(ctx, dim3((unsigned)sh.spart.np, (unsigned)ublocks), s, sh.DP, bias);
     HNM_LAUNCH_CHECK();
-    st = hnm_topk_rows_strided(ctx, x.sdense, sh.Ns, a.B, sh.Ns, a.mptr, a.midx, a.K, x.kthv,
-                               x.kthi, sh.stride);
+    const int64_t nmax_cols = (int64_t)sh.spart.np * 32;
+    st = hnm_sample_kth(ctx, x.sdense, nmax_cols, a.B, nmax_cols, nullptr, nullptr, a.K, 1, x.kthv);
     if (st) return st;
     hipLaunchKernelGGL(dcert_tau_kernel, dim3((unsigned)hnm_cdiv(a.B, 256)), dim3(256), 0,
                        ctx->stream, x.kthv, a.K, x.Nu, x.ubr, x.prm, a.B, x.tau, x.flag, x.E);
@@ -658,8 +739,8 @@ hnm_status dot_cert_debug(hnm_ctx* ctx, const DotArgs& a, bool bias, void* scrat
   const Partition ps = xcd_partition(a.I, hnm_cdiv(a.B, 128), ctx->num_cus, sh.DP);
   s.ipp = ps.ipp;
   s.NP = ps.np;
-  launch_dscan<DSCAN_SAMPLE>(ctx, dim3((unsigned)ps.np, (unsigned)hnm_cdiv(a.B, 128)), s, sh.DP,
-                             bias);
+  launch_dscan<DSCAN_DENSE>(ctx, dim3((unsigned)ps.np, (unsigned)hnm_cdiv(a.B, 128)), s, sh.DP,
+                            bias);
   HNM_LAUNCH_CHECK();
   hipLaunchKernelGGL(dcert_debug_out_kernel, dim3((unsigned)hnm_cdiv(a.B * a.I, 256)), dim3(256),
                      0, ctx->stream, approx, lda, a.B, a.I, x.ubr, x.prm);

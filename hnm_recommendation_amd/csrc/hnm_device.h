@@ -116,6 +116,41 @@ struct WaveTopK {
   }
 };
 
+// Wave-wide bitonic sort of 128 (value, index) pairs, two per lane (slot e = lane + 64 r:
+// (v0, i0) is slot lane, (v1, i1) slot lane + 64), into (value desc, index asc) order --
+// slot 0 = best.  28 compare-exchange steps of one shfl_xor each; no serial inserts.  The
+// order must be total on the inputs: distinct indices, no NaN (callers check).
+__device__ __forceinline__ void hnm_sort128(float& v0, int& i0, float& v1, int& i1) {
+  const int lane = hnm_lane();
+#pragma unroll
+  for (int k = 2; k <= 128; k <<= 1) {
+#pragma unroll
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      if (j == 64) {  // k == 128: partner is the other register of this lane; slot lane first
+        if (hnm_better(v1, i1, v0, i0)) {
+          const float tv = v0; v0 = v1; v1 = tv;
+          const int ti = i0; i0 = i1; i1 = ti;
+        }
+        continue;
+      }
+      const bool lower = (lane & j) == 0;
+#pragma unroll
+      for (int r = 0; r < 2; ++r) {
+        float& v = r ? v1 : v0;
+        int& ix = r ? i1 : i0;
+        const int e = lane + 64 * r;
+        const bool up = (e & k) == 0;       // this block is ordered best-first
+        const float pv = __shfl_xor(v, j);
+        const int pi = __shfl_xor(ix, j);
+        const bool pb = hnm_better(pv, pi, v, ix);  // partner ranks before mine
+        const bool take = (lower == up) ? pb : !pb;  // lower slot of an up block keeps the better
+        v = take ? pv : v;
+        ix = take ? pi : ix;
+      }
+    }
+  }
+}
+
 // v_mfma_f32_32x32x2_f32: A[i=l&31][k=l>>5], B[k=l>>5][j=l&31], exact fp32 fma chain.
 // C/D: col j = lane&31, row i = (r&3) + 8*(r>>2) + 4*(lane>>5) for register r.
 __device__ __forceinline__ f32x16 mfma32x32x2(float a, float b, f32x16 c) {

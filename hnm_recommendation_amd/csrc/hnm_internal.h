@@ -92,3 +92,8 @@ static inline Partition choose_partition(int64_t I, int64_t ublocks, int num_cus
 hnm_status hnm_topk_rows_strided(hnm_ctx* ctx, const float* s, int64_t ld, int64_t B, int64_t I,
                                  const int64_t* mptr, const int32_t* midx, int K, float* ov,
                                  int64_t* oi, int64_t istride);
+// Lower bound of the K-th best value of each sample row (score.hip sample_kth_kernel),
+// written at out[b * K + K - 1].
+hnm_status hnm_sample_kth(hnm_ctx* ctx, const float* s, int64_t ld, int64_t B, int64_t Ns,
+                          const int64_t* mptr, const int32_t* midx, int K, int64_t istride,
+                          float* out);

@@ -60,7 +60,7 @@ constexpr int CERT_WG_PER_CU = HNM_SCAN_OCC;  // scan workgroups per CU (LDS 51.
 enum { CM_P, CM_Q, CM_WG, CM_G, CM_B, CM_D, CM_N };
 
 struct CertParams {
-  unsigned mx[CM_N];  // float bits of non-negative maxima (NaN-propagating atomicMax)
+  unsigned mx[CM_N];  // float bits of non-negative maxima (reduced from per-block partials)
   float s1, sw, sm, sgu, sgi;
   float unit, cg;     // scaled score unit; GMF accumulator -> score unit
   float c0, absb, Bmax, Dmax;
@@ -90,7 +90,8 @@ __global__ __launch_bounds__(256) void cert_stats_kernel(NcfTabs t, int64_t B, i
                                                          CertParams* prm, float* __restrict__ Au,
                                                          float* __restrict__ Cu,
                                                          float* __restrict__ Bi,
-                                                         float* __restrict__ Di, int item_blocks,
+                                                         float* __restrict__ Di,
+                                                         float* __restrict__ part, int item_blocks,
                                                          int user_blocks) {
   __shared__ float vs[64];
   __shared__ float red[4][4];
@@ -148,10 +149,8 @@ __global__ __launch_bounds__(256) void cert_stats_kernel(NcfTabs t, int64_t B, i
   if (tid < 4) {
     float m = red[0][tid];
     for (int w = 1; w < 4; ++w) m = nmax(m, red[w][tid]);
-    // non-negative floats (and NaN) order like their bit patterns
-    const int slot = items ? (tid == 0 ? CM_Q : tid == 1 ? CM_G : tid == 2 ? CM_B : CM_D)
-                           : (tid == 0 ? CM_P : tid == 1 ? CM_WG : -1);
-    if (slot >= 0) atomicMax(&prm->mx[slot], __float_as_uint(m));
+    // per-block partials (no same-address atomics); reduced by cert_scales_kernel
+    part[blockIdx.x * 4 + tid] = m;
   }
 }
 
@@ -166,9 +165,40 @@ __global__ __launch_bounds__(256) void cert_scales_kernel(const float* __restric
                                                           int h2, const float* __restrict__ b2,
                                                           const float* __restrict__ wm,
                                                           const float* __restrict__ bp,
-                                                          CertParams* prm) {
+                                                          CertParams* prm,
+                                                          const float* __restrict__ part,
+                                                          int item_blocks, int user_blocks,
+                                                          int* __restrict__ ovf_cnt) {
   __shared__ float red[7][4];
+  __shared__ float pm[4][6];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  {  // per-block partial maxima of cert_stats_kernel: items Q G B D, users P WG
+    float q = 0.f, g = 0.f, bb = 0.f, dd = 0.f, pp = 0.f, wg = 0.f;
+    for (int blk = tid; blk < item_blocks + user_blocks; blk += 256) {
+      const float* v = part + blk * 4;
+      if (blk < item_blocks) {
+        q = nmax(q, v[0]); g = nmax(g, v[1]); bb = nmax(bb, v[2]); dd = nmax(dd, v[3]);
+      } else {
+        pp = nmax(pp, v[0]); wg = nmax(wg, v[1]);
+      }
+    }
+    q = wave_max(q); g = wave_max(g); bb = wave_max(bb); dd = wave_max(dd);
+    pp = wave_max(pp); wg = wave_max(wg);
+    if (lane == 0) {
+      pm[wave][0] = q; pm[wave][1] = g; pm[wave][2] = bb; pm[wave][3] = dd;
+      pm[wave][4] = pp; pm[wave][5] = wg;
+    }
+    __syncthreads();
+    if (tid < 6) {
+      float m = pm[0][tid];
+      for (int w = 1; w < 4; ++w) m = nmax(m, pm[w][tid]);
+      const int slot = tid == 0 ? CM_Q : tid == 1 ? CM_G : tid == 2 ? CM_B : tid == 3 ? CM_D
+                     : tid == 4 ? CM_P : CM_WG;
+      prm->mx[slot] = __float_as_uint(m);
+    }
+    if (tid == 0 && ovf_cnt) *ovf_cnt = 0;
+    __syncthreads();
+  }
   float mW = 0.f, vsum = 0.f, mwm = 0.f, mb2 = 0.f, c0 = 0.f, swm = 0.f;
   for (int e = tid; e < h2 * h1; e += 256) {
     const float w = fabsf(W2[e]);
@@ -723,7 +753,7 @@ __global__ void cert_unscale_kernel(float* __restrict__ a, float* __restrict__ e
 
 struct CertWs {
   CertParams* prm;
-  float *Au, *Cu, *Bi, *Di, *tau, *Eu, *b2s, *kthv, *sdense;
+  float *Au, *Cu, *Bi, *Di, *tau, *Eu, *b2s, *kthv, *sdense, *part;
   int64_t* kthi;
   int *cnt, *flag;
   int32_t *buf, *ovf_cnt, *ovf_rows;
@@ -768,6 +798,7 @@ size_t cert_carve(char* base, int64_t B, int64_t I, int K, int num_cus, CertWs* 
   x.prm = (CertParams*)take(sizeof(CertParams));
   x.Au = (float*)take(B * 4);
   x.Cu = (float*)take(B * 4);
+  x.part = (float*)take(4 * 4 * (1024 + 256));
   x.Bi = (float*)take(I * 4);
   x.Di = (float*)take(I * 4);
   x.tau = (float*)take(B * 4);
@@ -797,14 +828,14 @@ size_t cert_carve(char* base, int64_t B, int64_t I, int K, int num_cus, CertWs* 
 hnm_status cert_prepare(hnm_ctx* ctx, const hnm_ncf_weights* w, const NcfTabs& t, int64_t B,
                         const CertWs& x) {
   const int64_t I = w->num_items;
-  HNM_HIP_CHECK(hipMemsetAsync(x.prm, 0, sizeof(CertParams), ctx->stream));
   const int ib = (int)std::min<int64_t>(1024, hnm_cdiv(I, 4));
   const int ub = (int)std::min<int64_t>(256, hnm_cdiv(B, 4));
   hipLaunchKernelGGL(cert_stats_kernel, dim3(ib + ub), dim3(256), 0, ctx->stream, t, B, I, w->mf,
-                     w->w2, w->h1, w->h2, w->wp + w->mf, x.prm, x.Au, x.Cu, x.Bi, x.Di, ib, ub);
+                     w->w2, w->h1, w->h2, w->wp + w->mf, x.prm, x.Au, x.Cu, x.Bi, x.Di, x.part,
+                     ib, ub);
   HNM_LAUNCH_CHECK();
   hipLaunchKernelGGL(cert_scales_kernel, dim3(1), dim3(256), 0, ctx->stream, w->w2, w->h1, w->h2,
-                     w->b2, w->wp + w->mf, w->bp, x.prm);
+                     w->b2, w->wp + w->mf, w->bp, x.prm, x.part, ib, ub, x.ovf_cnt);
   HNM_LAUNCH_CHECK();
   const int cb = (int)std::min<int64_t>(2048, std::max<int64_t>(1, hnm_cdiv(I * 16, 256)));
   hipLaunchKernelGGL(cert_convert_kernel, dim3(cb), dim3(256), 0, ctx->stream, t, B, I, w->mf,
@@ -861,7 +892,6 @@ hnm_status ncf_cert_topk(hnm_ctx* ctx, const hnm_ncf_weights* w, const NcfTabs& 
   cert_carve((char*)scratch, B, I, K, ctx->num_cus, &x);
   hnm_status st = cert_prepare(ctx, w, t, B, x);
   if (st) return st;
-  HNM_HIP_CHECK(hipMemsetAsync(x.ovf_cnt, 0, 4, ctx->stream));
   const int64_t ublocks = hnm_cdiv(B, 128);
   // 1. sample pass: approx - e of items 0, stride, ... -> K-th best per row -> tau
   {
@@ -875,8 +905,7 @@ hnm_status ncf_cert_topk(hnm_ctx* ctx, const hnm_ncf_weights* w, const NcfTabs& 
     a.NP = ps.np;
     launch_scan<SCAN_SAMPLE>(ctx, dim3((unsigned)ublocks, (unsigned)ps.np), a);
     HNM_LAUNCH_CHECK();
-    st = hnm_topk_rows_strided(ctx, x.sdense, sh.Ns, B, sh.Ns, mptr, midx, K, x.kthv, x.kthi,
-                               sh.stride);
+    st = hnm_sample_kth(ctx, x.sdense, sh.Ns, B, sh.Ns, mptr, midx, K, sh.stride, x.kthv);
     if (st) return st;
     hipLaunchKernelGGL(cert_tau_kernel, dim3((unsigned)hnm_cdiv(B, 256)), dim3(256), 0,
                        ctx->stream, x.kthv, K, x.Au, x.Cu, x.prm, B, x.tau, x.flag, x.Eu);

@@ -325,7 +325,82 @@ __global__ __launch_bounds__(256) void rows_topk_kernel(const float* __restrict_
   L.store(ov ? ov + b * K : nullptr, oi + b * K, K);
 }
 
+// ------------------------------------------------------------------ sample K-th (lower bound)
+// For the certified pre-filters: a LOWER BOUND of the K-th best value of each row of a
+// dense [B, Ns] sample (masked columns excluded; column c is item c * istride).  Each lane
+// keeps its own top-4; the K-th best of the 64 x 4 survivors is <= the row's K-th best
+// (dropping values can only lower it).  ~3 VALU per element, no serial inserts.  A NaN in
+// the row makes the result NaN (the caller then takes the exact fallback).
+__global__ __launch_bounds__(256) void sample_kth_kernel(const float* __restrict__ s, int64_t ld,
+                                                         int64_t B, int64_t Ns,
+                                                         const int64_t* __restrict__ mptr,
+                                                         const int32_t* __restrict__ midx, int K,
+                                                         int64_t istride,
+                                                         float* __restrict__ out) {
+  const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (b >= B) return;
+  const int lane = threadIdx.x & 63;
+  float t0 = -__builtin_inff(), t1 = t0, t2 = t0, t3 = t0;
+  bool nan = false;
+  int64_t mpos = 0, mend = 0;
+  int nm = INT_BIG;
+  if (mptr) {
+    mpos = mptr[b];
+    mend = mptr[b + 1];
+    nm = mpos < mend ? midx[mpos] : INT_BIG;
+  }
+  const float* row = s + b * ld;
+  for (int64_t base = 0; base < Ns; base += 256) {  // 4 loads per lane in flight
+    float v[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int64_t c = base + 64 * q + lane;
+      v[q] = c < Ns ? row[c] : -__builtin_inff();
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int64_t cb = base + 64 * q;
+      if (mptr && cb < Ns) {
+        const int64_t c = cb + lane;
+        const int64_t end = (std::min<int64_t>(cb + 64, Ns) - 1) * istride + 1;  // real ids < end
+        while (nm < end) {
+          if (nm % istride == 0 && c == nm / istride) v[q] = -__builtin_inff();
+          ++mpos;
+          nm = mpos < mend ? midx[mpos] : INT_BIG;
+        }
+      }
+      nan |= v[q] != v[q];
+      if (v[q] > t3) {  // insert into the lane's sorted top-4
+        const float a = fminf(v[q], t2), c2 = fmaxf(v[q], t2);
+        t3 = a;
+        t2 = fminf(c2, t1);
+        const float c1 = fmaxf(c2, t1);
+        t1 = fminf(c1, t0);
+        t0 = fmaxf(c1, t0);
+      }
+    }
+  }
+  WaveTopK<1> L;
+  L.init();
+  L.offer(t0, lane, true, K);
+  L.offer(t1, 64 + lane, true, K);
+  L.offer(t2, 128 + lane, true, K);
+  L.offer(t3, 192 + lane, true, K);
+  const float kv = hnm_readlane_f(L.v[0], K - 1);
+  if (lane == 0) out[b * K + (K - 1)] = __ballot(nan) ? __builtin_nanf("") : kv;
+}
+
 // ------------------------------------------------------------------ host side
+hnm_status hnm_sample_kth(hnm_ctx* ctx, const float* s, int64_t ld, int64_t B, int64_t Ns,
+                          const int64_t* mptr, const int32_t* midx, int K, int64_t istride,
+                          float* out) {
+  HNM_REQUIRE(K >= 1 && K <= 64, HNM_EINVAL, "sample_kth: 1 <= K <= 64");
+  hipLaunchKernelGGL(sample_kth_kernel, dim3((unsigned)hnm_cdiv(B, 4)), dim3(256), 0, ctx->stream,
+                     s, ld, B, Ns, mptr, midx, K, istride, out);
+  HNM_LAUNCH_CHECK();
+  return HNM_OK;
+}
+
 hnm_status hnm_topk_rows_strided(hnm_ctx* ctx, const float* s, int64_t ld, int64_t B, int64_t I,
                                  const int64_t* mptr, const int32_t* midx, int K, float* ov,
                                  int64_t* oi, int64_t istride) {
