@@ -181,6 +181,7 @@ def kernel_timing(device):
 
 HNM_OPT_PREFILTER = 1
 HNM_OPT_SCAN_USERS = 2
+HNM_OPT_STATS = 3
 
 
 def set_option(device, option, value):
@@ -194,7 +195,8 @@ def set_prefilter(device, on=True):
 
 
 def prefilter_stats(device, reset=False):
-    """(rows scored, candidates re-scored in fp32, rows that took the exact fallback)."""
+    """(rows scored, candidates re-scored in fp32, rows that took the exact fallback);
+    counted only while HNM_OPT_STATS is on (set_option(dev, HNM_OPT_STATS, 1))."""
     out = (_i64 * 3)()
     check(fn("hnm_ctx_prefilter_stats")(ctx(device), out, int(reset)), "hnm_ctx_prefilter_stats")
     return tuple(int(v) for v in out)

@@ -70,6 +70,9 @@ extern "C" hnm_status hnm_ctx_set_option(hnm_ctx* ctx, int option, int64_t value
     case HNM_OPT_PREFILTER:
       ctx->prefilter = value != 0;
       return HNM_OK;
+    case HNM_OPT_STATS:
+      ctx->stats_on = value != 0;
+      return HNM_OK;
     case HNM_OPT_SCAN_USERS:
       HNM_REQUIRE(value == 1 || value == 2, HNM_EINVAL, "HNM_OPT_SCAN_USERS: 1 or 2");
       ctx->scan_users = (int)value;

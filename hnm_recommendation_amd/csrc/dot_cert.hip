@@ -560,17 +560,28 @@ __global__ __launch_bounds__(256) void dcert_rescore_kernel(
   // Rounds of 128 slots: slots 0..K-1 carry the running top-K, slots K..127 take the next
   // candidates; one bitonic sort per round (no serial list inserts).
   auto score = [&](int it) -> float {
+    // 64 dims = 16 float4 loads issued together (addresses clamped in range, zero padding by
+    // select); groups of 64 run one after another
     const float* r0 = a.it + (int64_t)it * a.ldi;
     float acc = 0.f;
-#pragma unroll 4
-    for (int k4 = 0; k4 < DP / 4; ++k4) {
-      float4 v0 = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (4 * k4 < a.d) v0 = *reinterpret_cast<const float4*>(r0 + 4 * k4);
-      const float4 uv = *reinterpret_cast<const float4*>(&urow[wave][4 * k4]);
-      acc = fmaf(uv.x, v0.x, acc);
-      acc = fmaf(uv.y, v0.y, acc);
-      acc = fmaf(uv.z, v0.z, acc);
-      acc = fmaf(uv.w, v0.w, acc);
+#pragma unroll 1
+    for (int g = 0; g < DP / 64; ++g) {
+      float4 v[16];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int k = 64 * g + 4 * q;
+        v[q] = *reinterpret_cast<const float4*>(r0 + std::min(k, a.d - 4));
+      }
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int k = 64 * g + 4 * q;
+        const bool in = k < a.d;
+        const float4 uv = *reinterpret_cast<const float4*>(&urow[wave][k]);
+        acc = fmaf(uv.x, in ? v[q].x : 0.f, acc);
+        acc = fmaf(uv.y, in ? v[q].y : 0.f, acc);
+        acc = fmaf(uv.z, in ? v[q].z : 0.f, acc);
+        acc = fmaf(uv.w, in ? v[q].w : 0.f, acc);
+      }
     }
     return BIAS ? (acc + ub) + (a.ibias ? a.ibias[it] : 0.f) : acc;
   };
@@ -707,10 +718,11 @@ hnm_status dot_cert_topk(hnm_ctx* ctx, const DotArgs& a, bool bias, void* scratc
     HNM_LAUNCH_CHECK();
   }
   // 3. exact re-scoring + top-K; unusable rows queued
+  unsigned long long* stp = ctx->stats_on ? ctx->stats_dev : nullptr;
 #define HNM_RS(DPV, BV)                                                                         \
   hipLaunchKernelGGL((dcert_rescore_kernel<DPV, BV>), dim3((unsigned)hnm_cdiv(a.B, 4)), dim3(256), \
                      0, ctx->stream, a, x.ubr, x.flag, x.cnt, x.buf, sh.part.np, sh.capp, a.K, ov, \
-                     oi, x.ovf_rows, x.ovf_cnt, ctx->stats_dev);
+                     oi, x.ovf_rows, x.ovf_cnt, stp);
   if (sh.DP == 64) {
     if (bias) { HNM_RS(64, true) } else { HNM_RS(64, false) }
   } else {

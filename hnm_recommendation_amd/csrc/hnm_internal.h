@@ -26,6 +26,7 @@ struct hnm_ctx {
   int prefilter;                   // HNM_OPT_PREFILTER (default 1)
   int scan_users;                  // HNM_OPT_SCAN_USERS (tuning: users per scan iteration)
   unsigned long long* stats_dev;   // pre-filter counters: rows, candidates, fallback rows
+  int stats_on;                    // HNM_OPT_STATS (default 0: counting costs same-address atomics)
 };
 
 void hnm_timer_begin(hnm_ctx* ctx);

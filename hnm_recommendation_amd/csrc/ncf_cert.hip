@@ -931,7 +931,8 @@ hnm_status ncf_cert_topk(hnm_ctx* ctx, const hnm_ncf_weights* w, const NcfTabs& 
   // 3. exact fp32 re-scoring + top-K of the candidates; unusable rows -> queue
   hipLaunchKernelGGL(ncf_rescore_kernel, dim3((unsigned)hnm_cdiv(B, 4)), dim3(256), 0, ctx->stream,
                      t, w->mf, w->w2, w->h1, w->h2, w->b2, w->wp + w->mf, w->bp, B, x.flag, x.cnt,
-                     x.buf, sh.part.np, sh.capp, K, ov, oi, x.ovf_rows, x.ovf_cnt, ctx->stats_dev);
+                     x.buf, sh.part.np, sh.capp, K, ov, oi, x.ovf_rows, x.ovf_cnt,
+                     ctx->stats_on ? ctx->stats_dev : nullptr);
   HNM_LAUNCH_CHECK();
   // 4. exact fp32 scan over all items for the queued rows (device-side row list)
   return ncf_list_rows(ctx, w, t, B, mptr, midx, K, x.ovf_rows, x.ovf_cnt, x.cv, x.ci, ov, oi);

@@ -60,10 +60,12 @@ hnm_status hnm_ctx_num_cus(hnm_ctx* ctx, int* out);
  * with the certified f16 pre-filter and re-score the surviving candidates in exact fp32
  * (results identical to the fp32 scan); 0 = exact fp32 scan of every item. */
 enum { HNM_OPT_PREFILTER = 1,
-       HNM_OPT_SCAN_USERS = 2 /* tuning: users per iteration of the f16 scan (1 or 2) */ };
+       HNM_OPT_SCAN_USERS = 2, /* tuning: NCF scan epilogue variant (1 = packed dots, 2 = MFMA) */
+       HNM_OPT_STATS = 3       /* 1: count pre-filter candidates / fallback rows (diagnostics) */ };
 hnm_status hnm_ctx_set_option(hnm_ctx* ctx, int option, int64_t value);
-/* Pre-filter counters since the last reset (syncs): out[0] rows scored, out[1] candidates
- * re-scored in fp32, out[2] rows that took the exact fallback scan. */
+/* Pre-filter counters since the last reset (syncs; counted only while HNM_OPT_STATS is 1):
+ * out[0] rows scored, out[1] candidates re-scored in fp32, out[2] rows that took the exact
+ * fallback scan. */
 hnm_status hnm_ctx_prefilter_stats(hnm_ctx* ctx, int64_t* out, int reset);
 /* Dominant-kernel timer: while on, every scoring / SpMM call records HIP events on the ctx
  * stream around its main kernel; hnm_ctx_timing() syncs, returns the summed kernel time

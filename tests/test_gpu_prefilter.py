@@ -43,7 +43,9 @@ def topk_both(m, users, filter_items=None, k=12):
     finally:
         _lib.set_prefilter(users.device, True)
     _lib.prefilter_stats(users.device, reset=True)
+    _lib.set_option(users.device, _lib.HNM_OPT_STATS, 1)
     pv, pi = m.recommend_with_scores(users, filter_items=filter_items, k=k)
+    _lib.set_option(users.device, _lib.HNM_OPT_STATS, 0)
     stats = _lib.prefilter_stats(users.device, reset=True)
     return (ev.cpu().numpy(), ei.cpu().numpy()), (pv.cpu().numpy(), pi.cpu().numpy()), stats
 
@@ -156,7 +158,9 @@ def dot_both(*args, **kw):
     finally:
         _lib.set_prefilter(dev, True)
     _lib.prefilter_stats(dev, reset=True)
+    _lib.set_option(dev, _lib.HNM_OPT_STATS, 1)
     pf = dot_topk(*args, **kw)
+    _lib.set_option(dev, _lib.HNM_OPT_STATS, 0)
     return ex, pf, _lib.prefilter_stats(dev, reset=True)
 
 
