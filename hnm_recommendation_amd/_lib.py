@@ -167,7 +167,11 @@ def sync_check(device):
     check(fn("hnm_ctx_check")(ctx(device)), "hnm_ctx_check")
 
 
+TIME_SCORE, TIME_SPMM = 1, 2
+
+
 def enable_timing(device, on=True):
+    """on: False/0 off, True/1 scoring kernels, 2 SpMM layers, 3 both."""
     check(fn("hnm_ctx_enable_timing")(ctx(device), int(on)), "hnm_ctx_enable_timing")
 
 

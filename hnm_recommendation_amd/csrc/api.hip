@@ -74,7 +74,7 @@ extern "C" hnm_status hnm_ctx_set_option(hnm_ctx* ctx, int option, int64_t value
       ctx->stats_on = value != 0;
       return HNM_OK;
     case HNM_OPT_SCAN_USERS:
-      HNM_REQUIRE(value == 1 || value == 2, HNM_EINVAL, "HNM_OPT_SCAN_USERS: 1 or 2");
+      HNM_REQUIRE(value >= 1 && value <= 3, HNM_EINVAL, "HNM_OPT_SCAN_USERS: 1, 2 or 3");
       ctx->scan_users = (int)value;
       return HNM_OK;
     default:
@@ -124,8 +124,8 @@ extern "C" hnm_status hnm_ctx_reserve(hnm_ctx* ctx, size_t bytes) {
 }
 
 // ------------------------------------------------------------------ kernel timer
-void hnm_timer_begin(hnm_ctx* ctx) {
-  if (!ctx->timing) return;
+void hnm_timer_begin(hnm_ctx* ctx, int cls) {
+  if (!(ctx->timing & cls)) return;
   if (ctx->nev == ctx->cap) {
     const int ncap = ctx->cap ? 2 * ctx->cap : 256;
     hipEvent_t* a = (hipEvent_t*)realloc(ctx->ev0, ncap * sizeof(hipEvent_t));
@@ -142,8 +142,8 @@ void hnm_timer_begin(hnm_ctx* ctx) {
   (void)hipEventRecord(ctx->ev0[ctx->nev], ctx->stream);
 }
 
-void hnm_timer_end(hnm_ctx* ctx) {
-  if (!ctx->timing || ctx->nev >= ctx->cap) return;
+void hnm_timer_end(hnm_ctx* ctx, int cls) {
+  if (!(ctx->timing & cls) || ctx->nev >= ctx->cap) return;
   (void)hipEventRecord(ctx->ev1[ctx->nev], ctx->stream);
   ++ctx->nev;
 }

@@ -712,9 +712,9 @@ hnm_status dot_cert_topk(hnm_ctx* ctx, const DotArgs& a, bool bias, void* scratc
     s.capp = sh.capp;
     s.ipp = sh.part.ipp;
     s.NP = sh.part.np;
-    hnm_timer_begin(ctx);
+    hnm_timer_begin(ctx, HNM_TIME_SCORE);
     launch_dscan<DSCAN_THRESH>(ctx, dim3((unsigned)sh.part.np, (unsigned)ublocks), s, sh.DP, bias);
-    hnm_timer_end(ctx);
+    hnm_timer_end(ctx, HNM_TIME_SCORE);
     HNM_LAUNCH_CHECK();
   }
   // 3. exact re-scoring + top-K; unusable rows queued

@@ -390,7 +390,7 @@ static hnm_status spmm_launch(hnm_ctx* ctx, const hnm_spmm_plan* pl, int64_t N,
                               const float* X, int d, float* Y, float alpha, const float* acc_in,
                               float* acc_out) {
   const int64_t heavy = (pl && pl->n_heavy > 0) ? HEAVY : INT64_MAX;
-  hnm_timer_begin(ctx);
+  hnm_timer_begin(ctx, HNM_TIME_SPMM);
   hipLaunchKernelGGL(spmm_light_kernel<LPR>, dim3((unsigned)hnm_cdiv(N, 4)), dim3(256), 0,
                      ctx->stream, N, rowptr, col, val, X, d, Y, alpha, acc_in, acc_out, heavy);
   HNM_LAUNCH_CHECK();
@@ -408,7 +408,7 @@ static hnm_status spmm_launch(hnm_ctx* ctx, const hnm_spmm_plan* pl, int64_t N,
                        alpha, acc_in, acc_out);
     HNM_LAUNCH_CHECK();
   }
-  hnm_timer_end(ctx);
+  hnm_timer_end(ctx, HNM_TIME_SPMM);
   return HNM_OK;
 }
 

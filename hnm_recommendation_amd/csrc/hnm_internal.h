@@ -29,8 +29,11 @@ struct hnm_ctx {
   int stats_on;                    // HNM_OPT_STATS (default 0: counting costs same-address atomics)
 };
 
-void hnm_timer_begin(hnm_ctx* ctx);
-void hnm_timer_end(hnm_ctx* ctx);
+// dominant-kernel timer classes (hnm_ctx_enable_timing mask)
+#define HNM_TIME_SCORE 1  // the scoring / scan kernel of each top-K or dense call
+#define HNM_TIME_SPMM 2   // one LightGCN propagation layer (light + segment + finish kernels)
+void hnm_timer_begin(hnm_ctx* ctx, int cls);
+void hnm_timer_end(hnm_ctx* ctx, int cls);
 
 void hnm_set_error(const char* fmt, ...);
 

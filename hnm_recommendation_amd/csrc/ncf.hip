@@ -698,7 +698,7 @@ static hnm_status ncf_common(hnm_ctx* ctx, const hnm_ncf_weights* w, const int64
   else                                                                                        \
     launch_ncf<WUV, 64, 32, DENSE>(ctx, grid, c.t, w, B, part.ipp, mptr, midx, K, cv, ci,     \
                                    part.np, dense, ldo);
-  hnm_timer_begin(ctx);
+  hnm_timer_begin(ctx, HNM_TIME_SCORE);
   if (!big) {
     launch_ncf32<DENSE>(ctx, grid, c.t, w, B, part.ipp, mptr, midx, K, cv, ci, part.np, dense,
                         ldo);
@@ -708,7 +708,7 @@ static hnm_status ncf_common(hnm_ctx* ctx, const hnm_ncf_weights* w, const int64
     HNM_NCF(1)
   }
 #undef HNM_NCF
-  hnm_timer_end(ctx);
+  hnm_timer_end(ctx, HNM_TIME_SCORE);
   HNM_LAUNCH_CHECK();
   if (!DENSE)
     return hnm_topk_merge_i32(ctx, cv, ci, B, 1, 0, (int64_t)part.np * K, part.np * K, K, ov, oi);

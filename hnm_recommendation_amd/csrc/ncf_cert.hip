@@ -517,71 +517,83 @@ __global__ __launch_bounds__(256, HNM_SCAN_OCC) void ncf16_scan_kernel(ScanArgs 
       }
     }
 
-    // next user's GMF value is read one iteration ahead
-    float gn = (ABL & 16) ? 0.f : gsm[wave][0][j];
-    for (int u = 0; u < nu; ++u) {
-      h8 pc[4];
+    // EPI 0: MFMA epilogue; 1: packed-dot epilogue; 2: packed dots, two users' chains per
+    // iteration (independent MFMA chains the scheduler interleaves)
+    constexpr int UI = EPI == 2 ? 2 : 1;
+    for (int u = 0; u < nu; u += UI) {
+      int uu[UI];
+      float gmu[UI];
+      f32x16 acc[UI];
+#pragma unroll
+      for (int i = 0; i < UI; ++i) {
+        uu[i] = std::min(u + i, nu - 1);
+        gmu[i] = (ABL & 16) ? 0.f : gsm[wave][uu[i]][j];
+        acc[i] = b2c;
+      }
 #pragma unroll
       for (int s = 0; s < 4; ++s)
-        pc[s] = (ABL & 8) ? q[s] : *reinterpret_cast<const h8*>(&ps[(wave * 32 + u) * 64 + 8 * h + 16 * s]);
-      const float gmu = gn;
-      const float cuu = hnm_readlane_f(cu, u), tvu = hnm_readlane_f(tv, u);
-      if (u + 1 < nu) gn = (ABL & 16) ? 0.f : gsm[wave][u + 1][j];
-      f32x16 acc = b2c;
 #pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        h8 x = pc[s] + q[s];
-        x = __builtin_elementwise_min(__builtin_elementwise_max(x, (h8){}), (h8)(_Float16)1.f);
-        if (ABL & 4) acc[s] += (float)x[0] + (float)x[7];
-        else acc = mfma16(aw[s], x, acc);
-      }
-      float score;
-      if (ABL & 2) {
-        score = acc[0] + acc[15] + gmu;
-      } else if (EPI == 0) {
-        // relu(H~) as the [0, 1] clamp of the convert (|H~| < 1 by the choice of sw); the
-        // accumulator tile is the B operand of wm . relu(H~)
-        h8 y0, y1;
+        for (int i = 0; i < UI; ++i) {
+          // P~ fragment read right before its MFMA (fewer live registers than reading all 4)
+          const h8 pc = (ABL & 8) ? q[s]
+                                  : *reinterpret_cast<const h8*>(&ps[(wave * 32 + uu[i]) * 64 + 8 * h + 16 * s]);
+          h8 x = pc + q[s];
+          x = __builtin_elementwise_min(__builtin_elementwise_max(x, (h8){}), (h8)(_Float16)1.f);
+          if (ABL & 4) acc[i][s] += (float)x[0] + (float)x[7];
+          else acc[i] = mfma16(aw[s], x, acc[i]);
+        }
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          y0[e] = (_Float16)acc[e];
-          y1[e] = (_Float16)acc[8 + e];
-        }
-        y0 = __builtin_elementwise_min(__builtin_elementwise_max(y0, (h8){}), (h8)(_Float16)1.f);
-        y1 = __builtin_elementwise_min(__builtin_elementwise_max(y1, (h8){}), (h8)(_Float16)1.f);
-        f32x16 d = {};
-        d = mfma16(awm[0], y0, d);
-        d = mfma16(awm[1], y1, d);
-        score = d[0] + gmu;
-      } else {
-        // wm . relu(H~) on the VALU: 8 packed f16 dots per half + one cross-half add
-        float m2[2] = {0.f, 0.f};
+      for (int i = 0; i < UI; ++i) {
+        if (i > 0 && u + i >= nu) break;
+        const int ui = u + i;
+        float score;
+        if (ABL & 2) {
+          score = acc[i][0] + acc[i][15] + gmu[i];
+        } else if (EPI == 0) {
+          // relu(H~) as the [0, 1] clamp of the convert (|H~| < 1 by the choice of sw); the
+          // accumulator tile is the B operand of wm . relu(H~)
+          h8 y0, y1;
 #pragma unroll
-        for (int r = 0; r < 16; r += 2) {
-          h2 y = {(_Float16)acc[r], (_Float16)acc[r + 1]};
-          y = __builtin_elementwise_min(__builtin_elementwise_max(y, (h2){}), (h2)(_Float16)1.f);
-          m2[(r >> 1) & 1] = __builtin_amdgcn_fdot2(y, wm2[r >> 1], m2[(r >> 1) & 1], false);
+          for (int e = 0; e < 8; ++e) {
+            y0[e] = (_Float16)acc[i][e];
+            y1[e] = (_Float16)acc[i][8 + e];
+          }
+          y0 = __builtin_elementwise_min(__builtin_elementwise_max(y0, (h8){}), (h8)(_Float16)1.f);
+          y1 = __builtin_elementwise_min(__builtin_elementwise_max(y1, (h8){}), (h8)(_Float16)1.f);
+          f32x16 d = {};
+          d = mfma16(awm[0], y0, d);
+          d = mfma16(awm[1], y1, d);
+          score = d[0] + gmu[i];
+        } else {
+          // wm . relu(H~) on the VALU: 8 packed f16 dots per half + one cross-half add
+          float m2[2] = {0.f, 0.f};
+#pragma unroll
+          for (int r = 0; r < 16; r += 2) {
+            h2 y = {(_Float16)acc[i][r], (_Float16)acc[i][r + 1]};
+            y = __builtin_elementwise_min(__builtin_elementwise_max(y, (h2){}), (h2)(_Float16)1.f);
+            m2[(r >> 1) & 1] = __builtin_amdgcn_fdot2(y, wm2[r >> 1], m2[(r >> 1) & 1], false);
+          }
+          score = hnm_sum_halves(m2[0] + m2[1]) + gmu[i];
         }
-        score = hnm_sum_halves(m2[0] + m2[1]) + gmu;
-      }
-      const float ei = fmaf(cuu, dj, bj);
-      if (MODE == SCAN_SAMPLE) {
-        if (ivalid) A.dense[(u0 + u) * A.ldo + n] = score - ei;
-      } else if (MODE == SCAN_DEBUG) {
-        if (ivalid) {
-          A.dense[(u0 + u) * A.ldo + n] = score;
-          A.dense2[(u0 + u) * A.ldo + n] = hnm_readlane_f(eu, u) + ei;
-        }
-      } else if (ABL & 1) {
-        tv += score + ei;  // keep the score live, no test
-      } else {
-        bool pass = ivalid && !(score + ei < tvu);
-        if (masked) pass = pass && !((hnm_readlane_i((int)mbits, u) >> j) & 1);
-        const uint64_t m = __ballot(pass);
-        if (m) {
-          const int pos = hnm_readlane_i(ccount, u) + __popcll(m & ((1ull << lane) - 1));
-          if (pass && pos < A.capp) seg[u * segstride + pos] = (int32_t)n;
-          if (lane == u) ccount += __popcll(m);
+        const float ei = fmaf(hnm_readlane_f(cu, ui), dj, bj);
+        if (MODE == SCAN_SAMPLE) {
+          if (ivalid) A.dense[(u0 + ui) * A.ldo + n] = score - ei;
+        } else if (MODE == SCAN_DEBUG) {
+          if (ivalid) {
+            A.dense[(u0 + ui) * A.ldo + n] = score;
+            A.dense2[(u0 + ui) * A.ldo + n] = hnm_readlane_f(eu, ui) + ei;
+          }
+        } else if (ABL & 1) {
+          tv += score + ei;  // keep the score live, no test
+        } else {
+          bool pass = ivalid && !(score + ei < hnm_readlane_f(tv, ui));
+          if (masked) pass = pass && !((hnm_readlane_i((int)mbits, ui) >> j) & 1);
+          const uint64_t m = __ballot(pass);
+          if (m) {
+            const int pos = hnm_readlane_i(ccount, ui) + __popcll(m & ((1ull << lane) - 1));
+            if (pass && pos < A.capp) seg[ui * segstride + pos] = (int32_t)n;
+            if (lane == ui) ccount += __popcll(m);
+          }
         }
       }
     }
@@ -847,7 +859,11 @@ hnm_status cert_prepare(hnm_ctx* ctx, const hnm_ncf_weights* w, const NcfTabs& t
 
 template <int MODE>
 void launch_scan(hnm_ctx* ctx, dim3 grid, const ScanArgs& a) {
-  if (ctx->scan_users == 2)  // tuning knob: epilogue variant (1 = packed dots, 2 = MFMA)
+  // tuning knob HNM_OPT_SCAN_USERS: 1 = packed-dot epilogue (default), 2 = two users per
+  // iteration, 3 = MFMA epilogue
+  if (ctx->scan_users == 2)
+    hipLaunchKernelGGL((ncf16_scan_kernel<MODE, 2>), grid, dim3(256), 0, ctx->stream, a);
+  else if (ctx->scan_users == 3)
     hipLaunchKernelGGL((ncf16_scan_kernel<MODE, 0>), grid, dim3(256), 0, ctx->stream, a);
   else
     hipLaunchKernelGGL((ncf16_scan_kernel<MODE, 1>), grid, dim3(256), 0, ctx->stream, a);
@@ -923,9 +939,9 @@ hnm_status ncf_cert_topk(hnm_ctx* ctx, const hnm_ncf_weights* w, const NcfTabs& 
     a.capp = sh.capp;
     a.ipp = sh.part.ipp;
     a.NP = sh.part.np;
-    hnm_timer_begin(ctx);
+    hnm_timer_begin(ctx, HNM_TIME_SCORE);
     launch_scan<SCAN_THRESH>(ctx, dim3((unsigned)ublocks, (unsigned)sh.part.np), a);
-    hnm_timer_end(ctx);
+    hnm_timer_end(ctx, HNM_TIME_SCORE);
     HNM_LAUNCH_CHECK();
   }
   // 3. exact fp32 re-scoring + top-K of the candidates; unusable rows -> queue

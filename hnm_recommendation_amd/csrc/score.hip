@@ -507,9 +507,9 @@ extern "C" hnm_status hnm_dot_topk_f32(hnm_ctx* ctx, const float* user_tab, int6
     void* w;
     st = hnm_workspace(ctx, 2 * sc, &w);
     if (st) return st;
-    hnm_timer_begin(ctx);
+    hnm_timer_begin(ctx, HNM_TIME_SCORE);
     st = dot_list_pass(ctx, a, bias, (float*)w, (int32_t*)((char*)w + sc), out_val, out_idx);
-    hnm_timer_end(ctx);
+    hnm_timer_end(ctx, HNM_TIME_SCORE);
     return st;
   }
   // ---- threshold path
@@ -570,9 +570,9 @@ extern "C" hnm_status hnm_dot_topk_f32(hnm_ctx* ctx, const float* user_tab, int6
   am.buf_v = bv;
   am.buf_i = bi;
   am.cap = cap;
-  hnm_timer_begin(ctx);
+  hnm_timer_begin(ctx, HNM_TIME_SCORE);
   launch_dot<DOT_THRESH>(ctx, dim3((unsigned)ublocks, (unsigned)part.np), am, bias);
-  hnm_timer_end(ctx);
+  hnm_timer_end(ctx, HNM_TIME_SCORE);
   HNM_LAUNCH_CHECK();
   // 3. exact top-K of the appended candidates; overflowing rows -> fallback list
   hipLaunchKernelGGL(thresh_select_kernel, dim3((unsigned)hnm_cdiv(B, 4)), dim3(256), 0,
@@ -602,10 +602,10 @@ extern "C" hnm_status hnm_dot_scores_f32(hnm_ctx* ctx, const float* user_tab, in
   a.NP = part.np;
   a.dense = out;
   a.ldo = ldo;
-  hnm_timer_begin(ctx);
+  hnm_timer_begin(ctx, HNM_TIME_SCORE);
   launch_dot<DOT_DENSE>(ctx, dim3((unsigned)ublocks, (unsigned)part.np), a,
                         user_bias || item_bias || const_bias);
-  hnm_timer_end(ctx);
+  hnm_timer_end(ctx, HNM_TIME_SCORE);
   HNM_LAUNCH_CHECK();
   return HNM_OK;
 }

@@ -540,7 +540,7 @@ static hnm_status wd_common(hnm_ctx* ctx, const hnm_widedeep_weights* w, const i
   const size_t lds = (size_t)(WD_TILE * (K1P + 4) + 4 * K1P + (pr.RB2 + pr.OB + nlast) * 32) * 4;
   dim3 grid((unsigned)ublocks, (unsigned)np);
   const float* wI = w->wide_item;
-  hnm_timer_begin(ctx);
+  hnm_timer_begin(ctx, HNM_TIME_SCORE);
 #define WD_CASE(R, O)                                                                     \
   if (pr.RB2 == R && pr.OB == O)                                                          \
     launch_wd<R, O, DENSE>(ctx, grid, lds, Pu, Qi, K1P, pr, cu, wI, B, I, ipp, mptr, midx, K, \
@@ -556,7 +556,7 @@ static hnm_status wd_common(hnm_ctx* ctx, const hnm_widedeep_weights* w, const i
   WD_CASE(4, 4)
   WD_CASE(8, 2)
 #undef WD_CASE
-  hnm_timer_end(ctx);
+  hnm_timer_end(ctx, HNM_TIME_SCORE);
   HNM_LAUNCH_CHECK();
   if (!DENSE) return hnm_topk_merge_i32(ctx, cv, ci, B, 1, 0, np * K, (int)(np * K), K, ov, oi);
   return HNM_OK;

@@ -60,17 +60,20 @@ hnm_status hnm_ctx_num_cus(hnm_ctx* ctx, int* out);
  * with the certified f16 pre-filter and re-score the surviving candidates in exact fp32
  * (results identical to the fp32 scan); 0 = exact fp32 scan of every item. */
 enum { HNM_OPT_PREFILTER = 1,
-       HNM_OPT_SCAN_USERS = 2, /* tuning: NCF scan epilogue variant (1 = packed dots, 2 = MFMA) */
+       HNM_OPT_SCAN_USERS = 2, /* tuning: NCF scan variant (1 packed-dot epilogue, 2 two users
+                                  per iteration, 3 MFMA epilogue) */
        HNM_OPT_STATS = 3       /* 1: count pre-filter candidates / fallback rows (diagnostics) */ };
 hnm_status hnm_ctx_set_option(hnm_ctx* ctx, int option, int64_t value);
 /* Pre-filter counters since the last reset (syncs; counted only while HNM_OPT_STATS is 1):
  * out[0] rows scored, out[1] candidates re-scored in fp32, out[2] rows that took the exact
  * fallback scan. */
 hnm_status hnm_ctx_prefilter_stats(hnm_ctx* ctx, int64_t* out, int reset);
-/* Dominant-kernel timer: while on, every scoring / SpMM call records HIP events on the ctx
- * stream around its main kernel; hnm_ctx_timing() syncs, returns the summed kernel time
- * and the number of timed launches, and resets.  (bench.py's live roofline figures.) */
-hnm_status hnm_ctx_enable_timing(hnm_ctx* ctx, int on);
+/* Dominant-kernel timer: while on, calls record HIP events on the ctx stream around their
+ * main kernel; `mask` selects the class: 1 = the scoring / scan kernel of every top-K or
+ * dense call, 2 = each LightGCN propagation layer (SpMM), 3 = both.  hnm_ctx_timing()
+ * syncs, returns the summed kernel time and the number of timed launches, and resets.
+ * (bench.py's live roofline figures.) */
+hnm_status hnm_ctx_enable_timing(hnm_ctx* ctx, int mask);
 hnm_status hnm_ctx_timing(hnm_ctx* ctx, double* total_ms, int64_t* launches);
 
 /* ---- a1: embedding row gather ------------------------------------------------------

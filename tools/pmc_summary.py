@@ -1,6 +1,9 @@
 """Summarize rocprofv3 PMC passes (tools/pmc_profile.sh) into profiles/pmc_<workload>.json.
 
-    python tools/pmc_summary.py <pmc run dir> <workload> <kernel substring> [out.json]
+    python tools/pmc_summary.py <pmc run dir> <workload> <kernel substring[,substring...]> [out.json]
+
+Several comma-separated substrings: the per-launch figures are the SUM over those kernels
+(e.g. one LightGCN propagation layer = spmm_light + spmm_segment + spmm_finish).
 
 HBM traffic per launch of the dominant kernel, corrected as MI355X_MICROARCH.md's
 HBM/rocprofv3 section prescribes: FETCH_SIZE (kB) counts L2 -> fabric read requests and on
@@ -19,16 +22,25 @@ import sys
 def main():
     run, workload, ksub = sys.argv[1], sys.argv[2], sys.argv[3]
     out = sys.argv[4] if len(sys.argv) > 4 else os.path.join("profiles", f"pmc_{workload}.json")
-    vals = collections.defaultdict(list)
+    subs = ksub.split(",")
+    per = {sub: collections.defaultdict(list) for sub in subs}
     names = set()
     for f in sorted(glob.glob(os.path.join(run, "p*", "*counter_collection.csv"))):
         for r in csv.DictReader(open(f)):
-            if ksub in r["Kernel_Name"]:
-                names.add(r["Kernel_Name"])
-                vals[r["Counter_Name"]].append(float(r["Counter_Value"]))
-    if not vals:
+            for sub in subs:
+                if sub in r["Kernel_Name"]:
+                    names.add(r["Kernel_Name"])
+                    per[sub][r["Counter_Name"]].append(float(r["Counter_Value"]))
+                    break
+    if not any(per.values()):
         raise SystemExit(f"no dispatches of a kernel matching {ksub!r} under {run}")
-    avg = {k: sum(v) / len(v) for k, v in vals.items()}
+    avg = collections.defaultdict(float)  # per-launch sum over the listed kernels
+    vals = collections.defaultdict(list)
+    for sub, d in per.items():
+        for k, v in d.items():
+            avg[k] += sum(v) / len(v)
+            vals[k] += v
+    avg = dict(avg)
     fetch = 2.0 * avg.get("FETCH_SIZE", 0.0) * 1024.0   # kB -> B, x2 gfx950 correction
     write = avg.get("WRITE_SIZE", 0.0) * 1024.0
     clk = avg.get("GRBM_GUI_ACTIVE", 0.0) / 8.0        # summed over the 8 XCDs
