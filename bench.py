@@ -57,15 +57,23 @@ def log(*a):
 
 
 def setup_dist(n_gpus):
+    """One process per GPU; backend "nccl" (= RCCL over xGMI).  HNM_DIST_BACKEND=gloo
+    rehearses the sharded path on fewer GPUs than ranks (collectives staged through host)."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    else:
-        torch.cuda.set_device(0)
-    return rank, world, torch.device("cuda", local if world > 1 else 0)
+        backend = os.environ.get("HNM_DIST_BACKEND", "nccl")
+        ndev = torch.cuda.device_count()
+        dev = local if backend == "nccl" else local % max(ndev, 1)
+        torch.cuda.set_device(dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+        else:
+            dist.init_process_group(backend)
+        return rank, world, torch.device("cuda", dev)
+    torch.cuda.set_device(0)
+    return rank, world, torch.device("cuda", 0)
 
 
 def load(m, sd, device):
@@ -227,7 +235,9 @@ def main():
     _lib.set_option(device, _lib.HNM_OPT_STATS, 0)
     pf_rows, pf_cands, pf_fallback = _lib.prefilter_stats(device, reset=True)
     if world > 1:
-        t = torch.tensor([elapsed, ktime_ms / max(launches, 1)], dtype=torch.float64, device=device)
+        on_host = dist.get_backend() == "gloo"
+        t = torch.tensor([elapsed, ktime_ms / max(launches, 1)], dtype=torch.float64,
+                         device="cpu" if on_host else device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, avg_kernel_ms = float(t[0]), float(t[1])
     else:

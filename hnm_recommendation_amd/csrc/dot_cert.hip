@@ -98,7 +98,7 @@ Partition xcd_partition(int64_t I, int64_t ublocks, int num_cus, int DP) {
 DotCertShape dcert_shape(int64_t B, int64_t I, int d, int K, int num_cus) {
   DotCertShape sh;
   sh.DP = d <= 64 ? 64 : 128;
-  sh.stride = std::max<int64_t>(1, I / DCERT_SAMPLE);
+  sh.stride = std::max<int64_t>(8, I / DCERT_SAMPLE);  // sample <= 1/8 of the items (shards too)
   sh.Ns = hnm_cdiv(I, sh.stride);
   sh.part = xcd_partition(I, hnm_cdiv(B, 128), num_cus, sh.DP);
   sh.spart = xcd_partition(sh.Ns, hnm_cdiv(B, 128), num_cus, sh.DP);

@@ -782,7 +782,7 @@ struct CertShape {
 
 CertShape cert_shape(int64_t B, int64_t I, int K, int num_cus) {
   CertShape sh;
-  sh.stride = std::max<int64_t>(1, I / CERT_SAMPLE);
+  sh.stride = std::max<int64_t>(8, I / CERT_SAMPLE);  // sample <= 1/8 of the items (shards too)
   sh.Ns = hnm_cdiv(I, sh.stride);
   Partition part = choose_partition(I, hnm_cdiv(B, 128), num_cus, TILE, CERT_WG_PER_CU);
   if (part.np > CERT_MAX_NP) {

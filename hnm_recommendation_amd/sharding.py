@@ -54,15 +54,20 @@ class ItemShardedRecommender:
         if G == 1:
             v, i = self.local_topk(user_ids)
             return v, torch.where(i >= 0, i + self.item_offset, i)
-        all_ids = torch.empty(G * B, dtype=user_ids.dtype, device=user_ids.device)
-        dist.all_gather_into_tensor(all_ids, user_ids.contiguous(), group=self.group)
-        v, i = self.local_topk(all_ids)  # [G*B, k], shard-local ids
+        dev = user_ids.device
+        # gloo (CPU tests, single-GPU rehearsal) moves host tensors; RCCL moves device tensors
+        host = dist.get_backend(self.group) == "gloo"
+        stage = (lambda t: t.cpu()) if host else (lambda t: t)
+        ids = stage(user_ids.contiguous())
+        all_ids = torch.empty(G * B, dtype=ids.dtype, device=ids.device)
+        dist.all_gather_into_tensor(all_ids, ids, group=self.group)
+        v, i = self.local_topk(all_ids.to(dev))  # [G*B, k], shard-local ids
         i = torch.where(i >= 0, i + self.item_offset, i)
-        rv = torch.empty(G * B * k, dtype=v.dtype, device=v.device)
-        ri = torch.empty(G * B * k, dtype=i.dtype, device=i.device)
-        dist.all_to_all_single(rv, v.contiguous().reshape(-1), group=self.group)
-        dist.all_to_all_single(ri, i.contiguous().reshape(-1), group=self.group)
-        return self.merge(rv.view(G, B, k), ri.view(G, B, k), k)
+        v, i = stage(v.contiguous().reshape(-1)), stage(i.contiguous().reshape(-1))
+        rv, ri = torch.empty_like(v), torch.empty_like(i)
+        dist.all_to_all_single(rv, v, group=self.group)
+        dist.all_to_all_single(ri, i, group=self.group)
+        return self.merge(rv.to(dev).view(G, B, k), ri.to(dev).view(G, B, k), k)
 
 
 # ------------------------------------------------------------------ HIP wiring
