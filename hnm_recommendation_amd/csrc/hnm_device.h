@@ -166,6 +166,20 @@ __device__ __forceinline__ float hnm_sum_halves(float x) {
   return __uint_as_float(r[0]) + __uint_as_float(r[1]);
 }
 
+// c + a.lo * b.lo and c + a.hi * b.hi in fp32 from packed f16 operands (v_fma_mix_f32:
+// f16 x f16 products are exact in fp32).  Unlike v_dot2_f32_f16 it co-issues with MFMA.
+typedef _Float16 hnm_h2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ float hnm_fma_mix_lo(hnm_h2 a, hnm_h2 b, float c) {
+  float d;
+  asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel_hi:[1,1,0]" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+  return d;
+}
+__device__ __forceinline__ float hnm_fma_mix_hi(hnm_h2 a, hnm_h2 b, float c) {
+  float d;
+  asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[1,1,0]" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+  return d;
+}
+
 #define TILE 32
 #define INT_BIG 0x7fffffff
 

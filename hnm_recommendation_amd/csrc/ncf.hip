@@ -682,7 +682,7 @@ static hnm_status ncf_common(hnm_ctx* ctx, const hnm_ncf_weights* w, const int64
   const int64_t ublocks = big ? hnm_cdiv(B, 4 * WU) : hnm_cdiv(B, 128);
   const Partition part = choose_partition(I, ublocks, ctx->num_cus);
   const size_t szC = DENSE ? 0 : hnm_align((size_t)B * part.np * K * 4);
-  const size_t extra = cert ? ncf_cert_bytes(B, I, K, ctx->num_cus) : 2 * szC;
+  const size_t extra = cert ? ncf_cert_bytes(B, I, K, ctx->num_cus, ncf_cert_wg(ctx)) : 2 * szC;
   NcfCall c;
   st = ncf_tables(ctx, w, ids, B, extra, &c);
   if (st) return st;
@@ -742,7 +742,7 @@ extern "C" hnm_status hnm_ncf_prefilter_debug_f32(hnm_ctx* ctx, const hnm_ncf_we
               "ncf_prefilter_debug: the f16 pre-filter covers h1 <= 64, mf <= 64");
   if (B <= 0) return HNM_OK;
   NcfCall c;
-  st = ncf_tables(ctx, w, user_ids, B, ncf_cert_bytes(B, w->num_items, 1, ctx->num_cus), &c);
+  st = ncf_tables(ctx, w, user_ids, B, ncf_cert_bytes(B, w->num_items, 1, ctx->num_cus, ncf_cert_wg(ctx)), &c);
   if (st) return st;
   return ncf_cert_debug(ctx, w, c.t, B, c.extra, approx, lda, bound);
 }

@@ -384,21 +384,30 @@ __device__ __forceinline__ f32x16 mfma16(h8 a, h8 b, f32x16 c) {
 // lane (j, h) holds B[k = 8h + e][col j], e = 0..7.
 // ABL: ablation bits for tools/scan_ablation.hip only (0 in the library): 1 = no threshold
 // test, 2 = no wm epilogue, 4 = no layer-2 MFMA, 8 = no P~ LDS reads, 16 = no GMF,
-// 32 = no tile staging / barriers.
+// 32 = no tile staging / barriers, 64 = no cross-half swap (EPI 2), 128 = no tile loads (zeros
+// staged), 256 = tile loads but no LDS stores.
 template <int MODE, int EPI, int ABL = 0>
-__global__ __launch_bounds__(256, HNM_SCAN_OCC) void ncf16_scan_kernel(ScanArgs A) {
+__global__ __launch_bounds__(256, EPI == 4 ? 2 : HNM_SCAN_OCC) void ncf16_scan_kernel(ScanArgs A) {
   constexpr int RS = 72;   // LDS row stride in halfs (144 B): conflict-free b128 reads
   constexpr int NU = 128;  // users per workgroup
   __shared__ __attribute__((aligned(16))) _Float16 qs[2][TILE * RS];  // double-buffered tiles
   __shared__ __attribute__((aligned(16))) _Float16 gs[2][TILE * RS];
   __shared__ __attribute__((aligned(16))) _Float16 ps[NU * 64];
   __shared__ float gsm[4][32][33];
+  // EPI 2 (THRESH / SAMPLE): the per-user test terms are folded into the GMF table once per
+  // tile, gsm' = gmf + sgn * e_i - tau (sgn = +1 for the threshold test, -1 for the sample's
+  // lower bound); ut holds (tau or 0, cu) per user
+  constexpr bool FOLD = (EPI == 2 || EPI == 4) && (MODE == SCAN_THRESH || MODE == SCAN_SAMPLE);
+  __shared__ float2 ut[FOLD ? 4 : 1][32];
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5, j = lane & 31;
-  const int64_t ublk = (int64_t)blockIdx.x * NU;
+  const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, j = lane & 31;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // uniform: scalar loop state
+  // grid: x = item partition (NP a multiple of 8), y = user block -> the round-robin
+  // workgroup -> XCD placement keeps partition p on XCD p % 8 (its tiles stay in that L2)
+  const int64_t ublk = (int64_t)blockIdx.y * NU;
   const int64_t u0 = ublk + wave * 32;
   const int nu = (int)std::max<int64_t>(0, std::min<int64_t>(32, A.B - u0));
-  const int p = blockIdx.y;
+  const int p = blockIdx.x;
   const int64_t part_start = (int64_t)p * A.ipp;
   const int64_t part_end = std::min<int64_t>(A.I, part_start + A.ipp);
 
@@ -435,6 +444,8 @@ __global__ __launch_bounds__(256, HNM_SCAN_OCC) void ncf16_scan_kernel(ScanArgs 
   float tv = __builtin_inff(), eu = 0.f;
   if (MODE == SCAN_THRESH && lane < nu) tv = A.tau[u0 + lane];
   if (MODE == SCAN_DEBUG && lane < nu) eu = A.Eu[u0 + lane];
+  if (FOLD && lane < 32)
+    ut[wave][lane] = make_float2(MODE == SCAN_THRESH ? tv : 0.f, cu);  // lanes >= nu: (inf | 0, 0)
   int ccount = 0;  // THRESH: appended items of user u0 + lane in this partition
   int nm = INT_BIG, mpos = 0, mend = 0;
   const bool masked = MODE == SCAN_THRESH && A.mptr != nullptr;
@@ -458,7 +469,7 @@ __global__ __launch_bounds__(256, HNM_SCAN_OCC) void ncf16_scan_kernel(ScanArgs 
     const int64_t n = base + srow;
     nq = (h8){};
     ng = (h8){};
-    if (n < part_end) {
+    if (n < part_end && !(ABL & 128)) {
       const int64_t it = n * A.istride;
       nq = *reinterpret_cast<const h8*>(A.Q16 + it * 64 + 8 * sc);
       ng = *reinterpret_cast<const h8*>(A.G16 + it * 64 + 8 * sc);
@@ -468,6 +479,10 @@ __global__ __launch_bounds__(256, HNM_SCAN_OCC) void ncf16_scan_kernel(ScanArgs 
     nd = A.Di[nj];
   };
   auto stash = [&](int buf) {
+    if (ABL & 256) {
+      __builtin_amdgcn_s_waitcnt(0);  // keep the loads' wait, drop the stores
+      return;
+    }
     *reinterpret_cast<h8*>(&qs[buf][srow * RS + 8 * sc]) = nq;
     *reinterpret_cast<h8*>(&gs[buf][srow * RS + 8 * sc]) = ng;
   };
@@ -490,8 +505,18 @@ __global__ __launch_bounds__(256, HNM_SCAN_OCC) void ncf16_scan_kernel(ScanArgs 
 #pragma unroll
       for (int s = 0; s < 4; ++s)
         gacc = mfma16(ag[s], *reinterpret_cast<const h8*>(&gs[cur][j * RS + 16 * s + 8 * h]), gacc);
+      if constexpr (FOLD) {
+        constexpr float sgn = MODE == SCAN_THRESH ? 1.f : -1.f;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) gsm[wave][mfma32_row(r, h)][j] = gacc[r] * cg;
+        for (int r = 0; r < 16; ++r) {
+          const int row = mfma32_row(r, h);
+          const float2 tc = ut[wave][row];
+          gsm[wave][row][j] = (gacc[r] * cg + sgn * fmaf(tc.y, dj, bj)) - tc.x;
+        }
+      } else {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) gsm[wave][mfma32_row(r, h)][j] = gacc[r] * cg;
+      }
     }
     h8 q[4];
 #pragma unroll
@@ -517,63 +542,209 @@ __global__ __launch_bounds__(256, HNM_SCAN_OCC) void ncf16_scan_kernel(ScanArgs 
       }
     }
 
-    // EPI 0: MFMA epilogue; 1: packed-dot epilogue; 2: packed dots, two users' chains per
-    // iteration (independent MFMA chains the scheduler interleaves)
-    constexpr int UI = EPI == 2 ? 2 : 1;
-    for (int u = 0; u < nu; u += UI) {
-      int uu[UI];
-      float gmu[UI];
-      f32x16 acc[UI];
+    if constexpr (EPI == 2 || EPI == 4) {
+      // Two users per iteration: independent MFMA chains for users a and b, and ONE
+      // epilogue for both -- after the packed-dot partials, a single permlane32 swap of
+      // (a's partials, b's partials) and an add leave a's totals in lanes 0-31 and b's in
+      // lanes 32-63 (same fp32 operations and order as the one-user epilogue), so the GMF
+      // read, the bound, the test and the ballot are shared by the pair.  EPI 4 reads the
+      // next pair's P~ fragments and GMF term one iteration ahead.
+      constexpr bool PF = EPI == 4;
+      h8 pn[8];
+      float gn = 0.f;
+      auto pload = [&](int ua_, int ub_) {
 #pragma unroll
-      for (int i = 0; i < UI; ++i) {
-        uu[i] = std::min(u + i, nu - 1);
-        gmu[i] = (ABL & 16) ? 0.f : gsm[wave][uu[i]][j];
-        acc[i] = b2c;
-      }
-#pragma unroll
-      for (int s = 0; s < 4; ++s)
-#pragma unroll
-        for (int i = 0; i < UI; ++i) {
-          // P~ fragment read right before its MFMA (fewer live registers than reading all 4)
-          const h8 pc = (ABL & 8) ? q[s]
-                                  : *reinterpret_cast<const h8*>(&ps[(wave * 32 + uu[i]) * 64 + 8 * h + 16 * s]);
-          h8 x = pc + q[s];
-          x = __builtin_elementwise_min(__builtin_elementwise_max(x, (h8){}), (h8)(_Float16)1.f);
-          if (ABL & 4) acc[i][s] += (float)x[0] + (float)x[7];
-          else acc[i] = mfma16(aw[s], x, acc[i]);
+        for (int s = 0; s < 4; ++s) {
+          pn[s] = (ABL & 8) ? q[s] : *reinterpret_cast<const h8*>(&ps[(wave * 32 + ua_) * 64 + 8 * h + 16 * s]);
+          pn[4 + s] = (ABL & 8) ? q[(s + 1) & 3] : *reinterpret_cast<const h8*>(&ps[(wave * 32 + ub_) * 64 + 8 * h + 16 * s]);
         }
+        gn = (ABL & 16) ? 0.f : gsm[wave][h ? ub_ : ua_][j];
+      };
+      if (PF) pload(0, std::min(1, nu - 1));
+      for (int u = 0; u < nu; u += 2) {
+        const int ua = u, ub = std::min(u + 1, nu - 1);
+        const bool hasb = u + 1 < nu;
+        const int uh = h ? ub : ua;
+        if (!PF) pload(ua, ub);
+        const float gmu = gn;
+        h8 xa[4], xb[4];
 #pragma unroll
-      for (int i = 0; i < UI; ++i) {
-        if (i > 0 && u + i >= nu) break;
-        const int ui = u + i;
+        for (int s = 0; s < 4; ++s) {
+          xa[s] = pn[s] + q[s];
+          xa[s] = __builtin_elementwise_min(__builtin_elementwise_max(xa[s], (h8){}), (h8)(_Float16)1.f);
+          xb[s] = pn[4 + s] + q[s];
+          xb[s] = __builtin_elementwise_min(__builtin_elementwise_max(xb[s], (h8){}), (h8)(_Float16)1.f);
+        }
+        if (PF && u + 2 < nu) pload(u + 2, std::min(u + 3, nu - 1));
+        f32x16 acc0 = b2c, acc1 = b2c;
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          if (ABL & 4) {
+            acc0[s] += (float)xa[s][0] + (float)xa[s][7];
+            acc1[s] += (float)xb[s][0] + (float)xb[s][7];
+          } else {
+            acc0 = mfma16(aw[s], xa[s], acc0);
+            acc1 = mfma16(aw[s], xb[s], acc1);
+          }
+        }
+        if constexpr (FOLD) {
+          // wm . relu(H~) with fma-mix (f16 x f16 products, exact in fp32, fp32 sums), which
+          // co-issues with the MFMA pipe -- v_dot2_f32_f16 does not (tools/issue_probe.hip);
+          // two chains per user, the first seeded with the folded term of that user's half:
+          // after the swap, lanes 0-31 hold user a's test value, lanes 32-63 user b's
+          float ma0 = h ? 0.f : gmu, mb0 = h ? gmu : 0.f, ma1 = 0.f, mb1 = 0.f;
+          if (ABL & 2) {
+            ma1 = acc0[0] + acc0[15];
+            mb1 = acc1[0] + acc1[15];
+          } else
+#pragma unroll
+          for (int r = 0; r < 16; r += 2) {
+            h2 ya = {(_Float16)acc0[r], (_Float16)acc0[r + 1]};
+            ya = __builtin_elementwise_min(__builtin_elementwise_max(ya, (h2){}), (h2)(_Float16)1.f);
+            h2 yb = {(_Float16)acc1[r], (_Float16)acc1[r + 1]};
+            yb = __builtin_elementwise_min(__builtin_elementwise_max(yb, (h2){}), (h2)(_Float16)1.f);
+            const h2 wv = wm2[r >> 1];
+            ma0 = hnm_fma_mix_lo(ya, wv, ma0);
+            ma1 = hnm_fma_mix_hi(ya, wv, ma1);
+            mb0 = hnm_fma_mix_lo(yb, wv, mb0);
+            mb1 = hnm_fma_mix_hi(yb, wv, mb1);
+          }
+          const float ma = ma0 + ma1, mb = mb0 + mb1;
+          float val;
+          if (ABL & 64) {
+            val = h ? mb : ma;
+          } else {
+            const auto sw2 = __builtin_amdgcn_permlane32_swap(__float_as_uint(ma), __float_as_uint(mb),
+                                                              false, false);
+            val = __uint_as_float(sw2[0]) + __uint_as_float(sw2[1]);
+          }
+          const bool lvalid = n < part_end && (h == 0 || hasb);
+          if (MODE == SCAN_SAMPLE) {
+            if (lvalid) A.dense[(u0 + uh) * A.ldo + n] = val;  // score - e_i
+          } else if (ABL & 1) {
+            tv += val;  // keep the value live, no test
+          } else {
+            bool pass = lvalid && !(val < 0.f);                 // !(score + e_i < tau)
+            if (masked) {
+              const int mba = hnm_readlane_i((int)mbits, ua), mbb = hnm_readlane_i((int)mbits, ub);
+              pass = pass && !(((h ? mbb : mba) >> j) & 1);
+            }
+            const uint64_t m = __ballot(pass);
+            if (m) {
+              const unsigned mh = (unsigned)(m >> (32 * h));
+              const int ca = hnm_readlane_i(ccount, ua), cb = hnm_readlane_i(ccount, ub);
+              const int pos = (h ? cb : ca) + __builtin_popcount(mh & ((1u << j) - 1u));
+              if (pass && pos < A.capp) seg[uh * segstride + pos] = (int32_t)n;
+              if (lane == ua) ccount += __builtin_popcount((unsigned)m);
+              if (lane == ub && hasb) ccount += __builtin_popcount((unsigned)(m >> 32));
+            }
+          }
+          continue;
+        }
+        float ma[2] = {0.f, 0.f}, mb[2] = {0.f, 0.f};
+#pragma unroll
+        for (int r = 0; r < 16; r += 2) {
+          h2 ya = {(_Float16)acc0[r], (_Float16)acc0[r + 1]};
+          ya = __builtin_elementwise_min(__builtin_elementwise_max(ya, (h2){}), (h2)(_Float16)1.f);
+          ma[(r >> 1) & 1] = __builtin_amdgcn_fdot2(ya, wm2[r >> 1], ma[(r >> 1) & 1], false);
+          h2 yb = {(_Float16)acc1[r], (_Float16)acc1[r + 1]};
+          yb = __builtin_elementwise_min(__builtin_elementwise_max(yb, (h2){}), (h2)(_Float16)1.f);
+          mb[(r >> 1) & 1] = __builtin_amdgcn_fdot2(yb, wm2[r >> 1], mb[(r >> 1) & 1], false);
+        }
+        const auto sw2 = __builtin_amdgcn_permlane32_swap(__float_as_uint(ma[0] + ma[1]),
+                                                          __float_as_uint(mb[0] + mb[1]), false, false);
+        const float score = (__uint_as_float(sw2[0]) + __uint_as_float(sw2[1])) + gmu;
+        const float cua = hnm_readlane_f(cu, ua), cub = hnm_readlane_f(cu, ub);
+        const float cuh = h ? cub : cua;
+        const float ei = fmaf(cuh, dj, bj);
+        const bool lvalid = n < part_end && (h == 0 || hasb);
+        if (MODE == SCAN_SAMPLE) {
+          if (lvalid) A.dense[(u0 + uh) * A.ldo + n] = score - ei;
+        } else if (MODE == SCAN_DEBUG) {
+          const float eua = hnm_readlane_f(eu, ua), eub = hnm_readlane_f(eu, ub);
+          const float euh = h ? eub : eua;
+          if (lvalid) {
+            A.dense[(u0 + uh) * A.ldo + n] = score;
+            A.dense2[(u0 + uh) * A.ldo + n] = euh + ei;
+          }
+        } else if (ABL & 1) {
+          tv += score + ei;
+        } else {
+          const float tva = hnm_readlane_f(tv, ua), tvb = hnm_readlane_f(tv, ub);
+          const float tvh = h ? tvb : tva;
+          bool pass = lvalid && !(score + ei < tvh);
+          if (masked) {
+            const int mba = hnm_readlane_i((int)mbits, ua), mbb = hnm_readlane_i((int)mbits, ub);
+            const int mb_ = h ? mbb : mba;
+            pass = pass && !((mb_ >> j) & 1);
+          }
+          const uint64_t m = __ballot(pass);
+          if (m) {
+            const unsigned mh = (unsigned)(m >> (32 * h));
+            const int ca = hnm_readlane_i(ccount, ua), cb = hnm_readlane_i(ccount, ub);
+            const int base_c = h ? cb : ca;
+            const int pos = base_c + __builtin_popcount(mh & ((1u << j) - 1u));
+            if (pass && pos < A.capp) seg[uh * segstride + pos] = (int32_t)n;
+            if (lane == ua) ccount += __builtin_popcount((unsigned)m);
+            if (lane == ub && hasb) ccount += __builtin_popcount((unsigned)(m >> 32));
+          }
+        }
+      }
+    } else {
+      // EPI 0: MFMA epilogue; 1: packed-dot epilogue (one user per iteration; reading the
+      // next user's P~ one iteration ahead measured slower at occupancy 3)
+      h8 pc[4];
+      float gmn = 0.f;
+      auto pload = [&](int uu) {
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+          pc[s] = (ABL & 8) ? q[s] : *reinterpret_cast<const h8*>(&ps[(wave * 32 + uu) * 64 + 8 * h + 16 * s]);
+        gmn = (ABL & 16) ? 0.f : gsm[wave][uu][j];
+      };
+      for (int u = 0; u < nu; ++u) {
+        const int ui = u;
+        pload(u);
+        const float gmu = gmn;
+        h8 x[4];
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          x[s] = pc[s] + q[s];
+          x[s] = __builtin_elementwise_min(__builtin_elementwise_max(x[s], (h8){}), (h8)(_Float16)1.f);
+        }
+        f32x16 acc = b2c;
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          if (ABL & 4) acc[s] += (float)x[s][0] + (float)x[s][7];
+          else acc = mfma16(aw[s], x[s], acc);
+        }
         float score;
         if (ABL & 2) {
-          score = acc[i][0] + acc[i][15] + gmu[i];
+          score = acc[0] + acc[15] + gmu;
         } else if (EPI == 0) {
           // relu(H~) as the [0, 1] clamp of the convert (|H~| < 1 by the choice of sw); the
           // accumulator tile is the B operand of wm . relu(H~)
           h8 y0, y1;
 #pragma unroll
           for (int e = 0; e < 8; ++e) {
-            y0[e] = (_Float16)acc[i][e];
-            y1[e] = (_Float16)acc[i][8 + e];
+            y0[e] = (_Float16)acc[e];
+            y1[e] = (_Float16)acc[8 + e];
           }
           y0 = __builtin_elementwise_min(__builtin_elementwise_max(y0, (h8){}), (h8)(_Float16)1.f);
           y1 = __builtin_elementwise_min(__builtin_elementwise_max(y1, (h8){}), (h8)(_Float16)1.f);
           f32x16 d = {};
           d = mfma16(awm[0], y0, d);
           d = mfma16(awm[1], y1, d);
-          score = d[0] + gmu[i];
+          score = d[0] + gmu;
         } else {
           // wm . relu(H~) on the VALU: 8 packed f16 dots per half + one cross-half add
           float m2[2] = {0.f, 0.f};
 #pragma unroll
           for (int r = 0; r < 16; r += 2) {
-            h2 y = {(_Float16)acc[i][r], (_Float16)acc[i][r + 1]};
+            h2 y = {(_Float16)acc[r], (_Float16)acc[r + 1]};
             y = __builtin_elementwise_min(__builtin_elementwise_max(y, (h2){}), (h2)(_Float16)1.f);
             m2[(r >> 1) & 1] = __builtin_amdgcn_fdot2(y, wm2[r >> 1], m2[(r >> 1) & 1], false);
           }
-          score = hnm_sum_halves(m2[0] + m2[1]) + gmu[i];
+          score = hnm_sum_halves(m2[0] + m2[1]) + gmu;
         }
         const float ei = fmaf(hnm_readlane_f(cu, ui), dj, bj);
         if (MODE == SCAN_SAMPLE) {
@@ -596,7 +767,7 @@ __global__ __launch_bounds__(256, HNM_SCAN_OCC) void ncf16_scan_kernel(ScanArgs 
           }
         }
       }
-    }
+    }  // EPI
     }  // nu > 0
     if (t + 1 < ntiles && !(ABL & 32)) stash(cur ^ 1);
     __syncthreads();
@@ -721,16 +892,28 @@ __global__ __launch_bounds__(256, 2) void ncf_rescore_kernel(
       }
       item = rowbuf[(int64_t)lo * capp + (g - pref[wave][lo])];
     }
-    // GMF: fma chain in the f32 MFMA's order (k = 2s, then 2s + 1)
+    // GMF: fma chain in the f32 MFMA's order (k = 2s, then 2s + 1) over all 64 k (zero
+    // beyond mf, as the fp32 kernel's padded operands); loads in two batches of 8 float4
+    // issued together (a runtime-bounded loop would wait on each load)
     float gm = 0.f;
     const float* grow = t.G + (int64_t)item * t.ldg;
-    for (int c4 = 0; c4 < (mf + 3) / 4; ++c4) {
-      const float4 gv = *reinterpret_cast<const float4*>(grow + 4 * c4);
-      // pair-permuted: wgs[2c4], wgs[2c4+1] = k 4c4, 4c4+2; wgs[32+2c4], [32+2c4+1] = 4c4+1, 4c4+3
-      const float2 wv = *reinterpret_cast<const float2*>(&wgs[wave][2 * c4]);
-      const float2 wv1 = *reinterpret_cast<const float2*>(&wgs[wave][KS + 2 * c4]);
-      gm = fmaf(wv1.x, gv.y, fmaf(wv.x, gv.x, gm));
-      gm = fmaf(wv1.y, gv.w, fmaf(wv.y, gv.z, gm));
+    const int glast = (int)t.ldg - 4;
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+      float4 gv[8];
+#pragma unroll
+      for (int q4 = 0; q4 < 8; ++q4)
+        gv[q4] = *reinterpret_cast<const float4*>(grow + std::min(4 * (8 * half + q4), glast));
+#pragma unroll
+      for (int q4 = 0; q4 < 8; ++q4) {
+        const int c4 = 8 * half + q4;
+        const bool in = 4 * c4 < mf;
+        // pair-permuted: wgs[2c4], wgs[2c4+1] = k 4c4, 4c4+2; wgs[32+2c4], [32+2c4+1] = 4c4+1, 4c4+3
+        const float2 wv = *reinterpret_cast<const float2*>(&wgs[wave][2 * c4]);
+        const float2 wv1 = *reinterpret_cast<const float2*>(&wgs[wave][KS + 2 * c4]);
+        gm = fmaf(wv1.x, in ? gv[q4].y : 0.f, fmaf(wv.x, in ? gv[q4].x : 0.f, gm));
+        gm = fmaf(wv1.y, in ? gv[q4].w : 0.f, fmaf(wv.y, in ? gv[q4].z : 0.f, gm));
+      }
     }
     float q[KS];
     const float* qrow = t.Qi + (int64_t)item * 64 + h * KS;
@@ -774,32 +957,38 @@ struct CertWs {
   int32_t* ci;
 };
 
+// ~wg workgroups per CU (the scan variant's occupancy), NP a multiple of 8 (XCD-aware),
+// <= CERT_MAX_NP
+Partition scan_partition(int64_t I, int64_t ublocks, int num_cus, int wg) {
+  int64_t np = std::max<int64_t>(1, (int64_t)wg * num_cus / std::max<int64_t>(ublocks, 1));
+  np = std::min<int64_t>(np, std::max<int64_t>(1, hnm_cdiv(I, 4 * TILE)));
+  np = std::min<int64_t>(np, CERT_MAX_NP);
+  if (np >= 8) np = np / 8 * 8;
+  const int64_t ipp = hnm_cdiv(hnm_cdiv(I, np), TILE) * TILE;
+  return {(int)hnm_cdiv(I, ipp), ipp};
+}
+
 struct CertShape {
   int64_t stride, Ns;
   Partition part;  // of the main scan
   int capp;        // candidate slots per (row, partition)
 };
 
-CertShape cert_shape(int64_t B, int64_t I, int K, int num_cus) {
+CertShape cert_shape(int64_t B, int64_t I, int K, int num_cus, int wg) {
   CertShape sh;
   sh.stride = std::max<int64_t>(8, I / CERT_SAMPLE);  // sample <= 1/8 of the items (shards too)
   sh.Ns = hnm_cdiv(I, sh.stride);
-  Partition part = choose_partition(I, hnm_cdiv(B, 128), num_cus, TILE, CERT_WG_PER_CU);
-  if (part.np > CERT_MAX_NP) {
-    part.ipp = hnm_cdiv(hnm_cdiv(I, CERT_MAX_NP), TILE) * TILE;
-    part.np = (int)hnm_cdiv(I, part.ipp);
-  }
-  sh.part = part;
+  sh.part = scan_partition(I, hnm_cdiv(B, 128), num_cus, wg);
   // expected candidates ~ K * stride (the sample's K-th) plus the bound's margin; each
   // partition gets 4x its even share, >= 64 slots
   const int64_t total = std::min<int64_t>(8192, std::max<int64_t>(512, 16 * (int64_t)K * sh.stride));
-  sh.capp = (int)std::max<int64_t>(64, std::min<int64_t>(total, hnm_cdiv(4 * total, part.np)));
+  sh.capp = (int)std::max<int64_t>(64, std::min<int64_t>(total, hnm_cdiv(4 * total, sh.part.np)));
   return sh;
 }
 
 // carve (or size, when base == nullptr) the scratch region
-size_t cert_carve(char* base, int64_t B, int64_t I, int K, int num_cus, CertWs* w) {
-  const CertShape sh = cert_shape(B, I, K, num_cus);
+size_t cert_carve(char* base, int64_t B, int64_t I, int K, int num_cus, int wg, CertWs* w) {
+  const CertShape sh = cert_shape(B, I, K, num_cus, wg);
   size_t off = 0;
   auto take = [&](size_t bytes) {
     char* p = base ? base + off : nullptr;
@@ -859,9 +1048,12 @@ hnm_status cert_prepare(hnm_ctx* ctx, const hnm_ncf_weights* w, const NcfTabs& t
 
 template <int MODE>
 void launch_scan(hnm_ctx* ctx, dim3 grid, const ScanArgs& a) {
-  // tuning knob HNM_OPT_SCAN_USERS: 1 = packed-dot epilogue (default), 2 = two users per
-  // iteration, 3 = MFMA epilogue
-  if (ctx->scan_users == 2)
+  // tuning knob HNM_OPT_SCAN_USERS: 1 = packed-dot epilogue, 2 = two users per iteration
+  // with the folded test (default), 3 = MFMA epilogue, 4 = as 2 with the next pair's LDS
+  // operands prefetched, at 2 workgroups per CU
+  if (ctx->scan_users == 4)
+    hipLaunchKernelGGL((ncf16_scan_kernel<MODE, 4>), grid, dim3(256), 0, ctx->stream, a);
+  else if (ctx->scan_users == 2)
     hipLaunchKernelGGL((ncf16_scan_kernel<MODE, 2>), grid, dim3(256), 0, ctx->stream, a);
   else if (ctx->scan_users == 3)
     hipLaunchKernelGGL((ncf16_scan_kernel<MODE, 0>), grid, dim3(256), 0, ctx->stream, a);
@@ -895,17 +1087,20 @@ bool ncf_cert_eligible(const hnm_ncf_weights* w, int K) {
          w->num_items >= CERT_MIN_ITEMS && w->num_items >= 64 * (int64_t)K;
 }
 
-size_t ncf_cert_bytes(int64_t B, int64_t I, int K, int num_cus) {
-  return cert_carve(nullptr, B, I, K, num_cus, nullptr);
+int ncf_cert_wg(const hnm_ctx* ctx) { return ctx->scan_users == 4 ? 2 : CERT_WG_PER_CU; }
+
+size_t ncf_cert_bytes(int64_t B, int64_t I, int K, int num_cus, int wg) {
+  return cert_carve(nullptr, B, I, K, num_cus, wg, nullptr);
 }
 
 hnm_status ncf_cert_topk(hnm_ctx* ctx, const hnm_ncf_weights* w, const NcfTabs& t, int64_t B,
                          const int64_t* mptr, const int32_t* midx, int K, void* scratch,
                          float* ov, int64_t* oi) {
   const int64_t I = w->num_items;
-  const CertShape sh = cert_shape(B, I, K, ctx->num_cus);
+  const int wg = ncf_cert_wg(ctx);
+  const CertShape sh = cert_shape(B, I, K, ctx->num_cus, wg);
   CertWs x;
-  cert_carve((char*)scratch, B, I, K, ctx->num_cus, &x);
+  cert_carve((char*)scratch, B, I, K, ctx->num_cus, wg, &x);
   hnm_status st = cert_prepare(ctx, w, t, B, x);
   if (st) return st;
   const int64_t ublocks = hnm_cdiv(B, 128);
@@ -916,10 +1111,10 @@ hnm_status ncf_cert_topk(hnm_ctx* ctx, const hnm_ncf_weights* w, const NcfTabs& 
     a.istride = sh.stride;
     a.dense = x.sdense;
     a.ldo = sh.Ns;
-    Partition ps = choose_partition(sh.Ns, ublocks, ctx->num_cus, TILE, CERT_WG_PER_CU);
+    Partition ps = scan_partition(sh.Ns, ublocks, ctx->num_cus, wg);
     a.ipp = ps.ipp;
     a.NP = ps.np;
-    launch_scan<SCAN_SAMPLE>(ctx, dim3((unsigned)ublocks, (unsigned)ps.np), a);
+    launch_scan<SCAN_SAMPLE>(ctx, dim3((unsigned)ps.np, (unsigned)ublocks), a);
     HNM_LAUNCH_CHECK();
     st = hnm_sample_kth(ctx, x.sdense, sh.Ns, B, sh.Ns, mptr, midx, K, sh.stride, x.kthv);
     if (st) return st;
@@ -940,7 +1135,7 @@ hnm_status ncf_cert_topk(hnm_ctx* ctx, const hnm_ncf_weights* w, const NcfTabs& 
     a.ipp = sh.part.ipp;
     a.NP = sh.part.np;
     hnm_timer_begin(ctx, HNM_TIME_SCORE);
-    launch_scan<SCAN_THRESH>(ctx, dim3((unsigned)ublocks, (unsigned)sh.part.np), a);
+    launch_scan<SCAN_THRESH>(ctx, dim3((unsigned)sh.part.np, (unsigned)ublocks), a);
     hnm_timer_end(ctx, HNM_TIME_SCORE);
     HNM_LAUNCH_CHECK();
   }
@@ -958,7 +1153,7 @@ hnm_status ncf_cert_debug(hnm_ctx* ctx, const hnm_ncf_weights* w, const NcfTabs&
                           void* scratch, float* approx, int64_t lda, float* bound) {
   const int64_t I = w->num_items;
   CertWs x;
-  cert_carve((char*)scratch, B, I, 1, ctx->num_cus, &x);
+  cert_carve((char*)scratch, B, I, 1, ctx->num_cus, ncf_cert_wg(ctx), &x);
   hnm_status st = cert_prepare(ctx, w, t, B, x);
   if (st) return st;
   hipLaunchKernelGGL(cert_tau_kernel, dim3((unsigned)hnm_cdiv(B, 256)), dim3(256), 0, ctx->stream,
@@ -973,7 +1168,7 @@ hnm_status ncf_cert_debug(hnm_ctx* ctx, const hnm_ncf_weights* w, const NcfTabs&
   Partition part = choose_partition(I, ublocks, ctx->num_cus);
   a.ipp = part.ipp;
   a.NP = part.np;
-  launch_scan<SCAN_DEBUG>(ctx, dim3((unsigned)ublocks, (unsigned)part.np), a);
+  launch_scan<SCAN_DEBUG>(ctx, dim3((unsigned)part.np, (unsigned)ublocks), a);
   HNM_LAUNCH_CHECK();
   hipLaunchKernelGGL(cert_unscale_kernel, dim3((unsigned)hnm_cdiv(B * I, 256)), dim3(256), 0,
                      ctx->stream, approx, bound, lda, B, I, x.prm);

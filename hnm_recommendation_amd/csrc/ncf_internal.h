@@ -22,7 +22,8 @@ size_t ncf_list_bytes(int64_t B, int64_t I, int K, int num_cus);
 // Certified pre-filter path (ncf_cert.hip): eligible when h1 <= 64, mf <= 64, K <= 64 and
 // the catalogue is large enough for the sample pass to pay.
 bool ncf_cert_eligible(const hnm_ncf_weights* w, int K);
-size_t ncf_cert_bytes(int64_t B, int64_t I, int K, int num_cus);
+size_t ncf_cert_bytes(int64_t B, int64_t I, int K, int num_cus, int wg);
+int ncf_cert_wg(const hnm_ctx* ctx);  // scan workgroups per CU of the selected variant
 hnm_status ncf_cert_topk(hnm_ctx* ctx, const hnm_ncf_weights* w, const NcfTabs& t, int64_t B,
                          const int64_t* mptr, const int32_t* midx, int K, void* scratch,
                          float* ov, int64_t* oi);

@@ -70,26 +70,35 @@ def test_bound_holds_full_catalogue(kw):
     assert ratio <= 1.0, ratio
 
 
+@pytest.fixture(params=[1, 2, 3, 4], ids=["epi-dot", "epi-pair", "epi-mfma", "epi-pair-pf"])
+def scan_users(request):
+    """The scan kernel's epilogue variants (HNM_OPT_SCAN_USERS): all must be identical."""
+    dev = torch.device(DEV, 0)
+    _lib.set_option(dev, _lib.HNM_OPT_SCAN_USERS, request.param)
+    yield request.param
+    _lib.set_option(dev, _lib.HNM_OPT_SCAN_USERS, 2)
+
+
 @pytest.mark.parametrize("kw", [{}, {"bias_scale": 0.1, "emb_scale": 30.0}])
-def test_prefilter_identical_to_exact_scan(kw):
+def test_prefilter_identical_to_exact_scan(kw, scan_users):
     m = full_model(seed=3, **kw)
-    users_np = syn.user_batch(syn.HM_USERS, 1024, seed=9)
+    users_np = syn.user_batch(syn.HM_USERS, 1024 - 23, seed=9)  # odd users in the last wave
     users = torch.from_numpy(users_np).to(DEV)
     (ev, ei), (pv, pi), stats = topk_both(m, users)
     assert np.array_equal(ei, pi)
     assert np.array_equal(ev.view(np.uint32), pv.view(np.uint32))  # bit-identical scores
     rows, cands, fallback = stats
     print(f"candidates/row {cands / max(rows - fallback, 1):.1f}, fallback rows {fallback}")
-    assert rows == 1024 and fallback == 0
+    assert rows == users_np.size and fallback == 0
     # and against the CPU oracle on a few rows
     ref = O.ncf_predict_all_items(syn.ncf_state_dict(syn.HM_USERS, syn.HM_ITEMS, 64,
                                                      (128, 64, 32), seed=3, **kw), users_np[:3])
     assert_topk_equivalent(pi[:3], ref, 12, what="prefilter vs oracle")
 
 
-def test_prefilter_with_filters_and_k():
+def test_prefilter_with_filters_and_k(scan_users):
     m = full_model(seed=4)
-    users_np = syn.user_batch(syn.HM_USERS, 200, seed=2)
+    users_np = syn.user_batch(syn.HM_USERS, 201, seed=2)
     users = torch.from_numpy(users_np).to(DEV)
     # filter each user's exact top-30 partially, plus random history
     _lib.set_prefilter(users.device, False)

@@ -1,0 +1,62 @@
+// Random 256-B row-gather bandwidth vs table size on MI355X: does a table that fits the
+// 256 MB Infinity Cache gather faster than one that spills to HBM?  (Premise check for
+// user-range blocking of the LightGCN SpMM item rows.)
+// Build: hipcc --offload-arch=gfx950 -O3 tools/gather_probe.hip -o build/gather_probe
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+
+// wave per output row, 16 lanes x float4 per gathered row, 4 rows in flight per wave
+__global__ __launch_bounds__(256) void gather_sum(const float* __restrict__ X, int64_t rows,
+                                                  const int32_t* __restrict__ idx, int64_t nnz_per_out,
+                                                  int64_t nout, float* __restrict__ out) {
+  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= nout) return;
+  const int lane = threadIdx.x & 63, grp = lane >> 4, sub = lane & 15;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  const int32_t* ir = idx + r * nnz_per_out;
+  for (int64_t p = grp; p < nnz_per_out; p += 4) {
+    const float4 x = *reinterpret_cast<const float4*>(X + (int64_t)ir[p] * 64 + 4 * sub);
+    acc.x += x.x; acc.y += x.y; acc.z += x.z; acc.w += x.w;
+  }
+  if (lane < 16) *reinterpret_cast<float4*>(out + r * 64 + 4 * sub) = acc;
+}
+
+int main() {
+  const int64_t maxrows = 1400000;  // 358 MB at 64 floats
+  float* X;
+  (void)hipMalloc(&X, maxrows * 64 * 4);
+  (void)hipMemset(X, 0, maxrows * 64 * 4);
+  const int64_t nout = 200000, per = 64;  // 12.8M gathers = 3.3 GB per launch
+  int32_t* idx;
+  float* out;
+  (void)hipMalloc(&idx, nout * per * 4);
+  (void)hipMalloc(&out, nout * 64 * 4);
+  int32_t* h = (int32_t*)malloc(nout * per * 4);
+  hipEvent_t e0, e1;
+  (void)hipEventCreate(&e0);
+  (void)hipEventCreate(&e1);
+  for (int64_t rows : {16384L, 65536L, 262144L, 524288L, 786432L, 1048576L, 1400000L}) {
+    uint64_t s = 88172645463325252ull;
+    for (int64_t k = 0; k < nout * per; ++k) {
+      s ^= s << 13; s ^= s >> 7; s ^= s << 17;
+      h[k] = (int32_t)(s % (uint64_t)rows);
+    }
+    (void)hipMemcpy(idx, h, nout * per * 4, hipMemcpyHostToDevice);
+    float best = 1e30f;
+    for (int rep = 0; rep < 4; ++rep) {
+      (void)hipEventRecord(e0);
+      hipLaunchKernelGGL(gather_sum, dim3((unsigned)(nout / 4)), dim3(256), 0, 0, X, rows, idx, per,
+                         nout, out);
+      (void)hipEventRecord(e1);
+      (void)hipEventSynchronize(e1);
+      float ms;
+      (void)hipEventElapsedTime(&ms, e0, e1);
+      if (rep > 0 && ms < best) best = ms;
+    }
+    const double bytes = (double)nout * per * 256;
+    printf("table %7.1f MB: %.3f ms, gather %.2f TB/s\n", rows * 256.0 / 1e6, best,
+           bytes / (best * 1e-3) / 1e12);
+  }
+  return 0;
+}

@@ -42,7 +42,7 @@ static float time_variant(dim3 grid, const ScanArgs& a) {
 
 int main() {
   const int64_t B = 4096, I = 105542;
-  const CertShape sh = cert_shape(B, I, 12, 256);
+  const CertShape sh = cert_shape(B, I, 12, 256, CERT_WG_PER_CU);
   ScanArgs a{};
   a.P16 = dev_fill<_Float16>(B * 64, -0.25f, 0.25f, 1);
   a.WG16 = dev_fill<_Float16>(B * 64, -0.5f, 0.5f, 2);
@@ -70,7 +70,7 @@ int main() {
   a.capp = sh.capp;
   (void)hipMalloc(&a.cnt, B * sh.part.np * 4);
   (void)hipMalloc(&a.buf, (size_t)B * sh.part.np * sh.capp * 4);
-  dim3 grid((unsigned)hnm_cdiv(B, 128), (unsigned)sh.part.np);
+  dim3 grid((unsigned)sh.part.np, (unsigned)hnm_cdiv(B, 128));
   const double pairs = (double)B * I, useful = 4352.0 * pairs;
   printf("grid %u x %u, ipp %ld\n", grid.x, grid.y, (long)sh.part.ipp);
 #define V(ABL, EPI)                                                                          \
@@ -79,7 +79,6 @@ int main() {
     printf("EPI=%d ABL=%2d  %7.3f ms  %6.1f TF useful  %5.2f cyc/user-tile/SIMD @2.2GHz\n", EPI, \
            ABL, ms, useful / (ms * 1e-3) / 1e12, ms * 1e-3 * 2.2e9 / (pairs / 32 / 1024));   \
   }
-  V(0, 0) V(0, 1) V(1, 1) V(2, 1) V(4, 1) V(8, 1) V(16, 1) V(32, 1) V(1 | 16 | 32, 1)
-  V(1 | 2 | 16 | 32, 1) V(2 | 8 | 16 | 32, 1) V(4 | 8 | 16 | 32, 1)
+  V(0, 2) V(32, 2) V(128, 2) V(256, 2) V(0, 2)
   return 0;
 }
