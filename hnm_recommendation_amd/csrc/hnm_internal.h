@@ -99,5 +99,5 @@ hnm_status hnm_topk_rows_strided(hnm_ctx* ctx, const float* s, int64_t ld, int64
 // Lower bound of the K-th best value of each sample row (score.hip sample_kth_kernel),
 // written at out[b * K + K - 1].
 hnm_status hnm_sample_kth(hnm_ctx* ctx, const float* s, int64_t ld, int64_t B, int64_t Ns,
-                          const int64_t* mptr, const int32_t* midx, int K, int64_t istride,
-                          float* out);
+                          const int64_t* mptr, const int32_t* midx, int K, int64_t grp,
+                          int64_t period, float* out);

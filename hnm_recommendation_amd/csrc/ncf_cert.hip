@@ -338,7 +338,7 @@ __global__ __launch_bounds__(256) void cert_convert_kernel(
 }
 
 // ------------------------------------------------------------------ f16 scan kernel
-// SAMPLE: dense[b][n] = approx - e_i (scanned item n = n * istride), e_i = the per-item part
+// SAMPLE: dense[b][n] = approx - e_i (scanned item n = (n / 32) * tstride + n % 32), e_i = the per-item part
 //         of the bound, 6u unit (B_i + C_u D_i);
 // THRESH: append item n to segment (b, partition) when approx + e_i >= tau_b;
 // DEBUG:  dense[b][n] = approx, dense2[b][n] = Eu_b + e_i (the whole bound), scaled units.
@@ -359,14 +359,19 @@ struct ScanArgs {
   const CertParams* prm;
   int64_t B;
   int64_t I;        // scanned items (sample count for the sample pass)
-  int64_t istride;  // scanned item n is item n * istride
+  int64_t tstride;  // scanned item n is item (n >> gshift) * tstride + n % 2^gshift (gshift 5,
+                    // tstride 32: identity; the sample pass scans every (tstride / 32)-th tile)
+  int gshift;
+  int64_t skip;     // THRESH: tiles with (global tile index % skip) == 0 are the sample's
+                    // and are not scanned (0: scan every tile)
   int64_t ipp;
   int NP;
+  int nseg;         // candidate segments per row (NP, + 1 for the sample's candidates)
   const int64_t* mptr;
   const int32_t* midx;
   const float* tau;  // [B] scaled thresholds (THRESH)
-  int* cnt;          // [B, NP] appended counts (THRESH)
-  int32_t* buf;      // [B, NP, capp] appended item ids (THRESH)
+  int* cnt;          // [B, nseg] appended counts (THRESH)
+  int32_t* buf;      // [B, nseg, capp] appended item ids (THRESH)
   int capp;
   float* dense;      // [B, ldo]
   float* dense2;     // [B, ldo] (DEBUG)
@@ -384,8 +389,8 @@ __device__ __forceinline__ f32x16 mfma16(h8 a, h8 b, f32x16 c) {
 // lane (j, h) holds B[k = 8h + e][col j], e = 0..7.
 // ABL: ablation bits for tools/scan_ablation.hip only (0 in the library): 1 = no threshold
 // test, 2 = no wm epilogue, 4 = no layer-2 MFMA, 8 = no P~ LDS reads, 16 = no GMF,
-// 32 = no tile staging / barriers, 64 = no cross-half swap (EPI 2), 128 = no tile loads (zeros
-// staged), 256 = tile loads but no LDS stores.
+// 32 = no tile loads (zero tiles staged; skipping the LDS stores instead lets the compiler
+// delete the work on the undefined tiles), 64 = no cross-half swap (EPI 2).
 template <int MODE, int EPI, int ABL = 0>
 __global__ __launch_bounds__(256, EPI == 4 ? 2 : HNM_SCAN_OCC) void ncf16_scan_kernel(ScanArgs A) {
   constexpr int RS = 72;   // LDS row stride in halfs (144 B): conflict-free b128 reads
@@ -397,7 +402,7 @@ __global__ __launch_bounds__(256, EPI == 4 ? 2 : HNM_SCAN_OCC) void ncf16_scan_k
   // EPI 2 (THRESH / SAMPLE): the per-user test terms are folded into the GMF table once per
   // tile, gsm' = gmf + sgn * e_i - tau (sgn = +1 for the threshold test, -1 for the sample's
   // lower bound); ut holds (tau or 0, cu) per user
-  constexpr bool FOLD = (EPI == 2 || EPI == 4) && (MODE == SCAN_THRESH || MODE == SCAN_SAMPLE);
+  constexpr bool FOLD = (EPI == 2 || EPI == 4 || EPI == 5 || EPI == 6) && (MODE == SCAN_THRESH || MODE == SCAN_SAMPLE);
   __shared__ float2 ut[FOLD ? 4 : 1][32];
 
   const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, j = lane & 31;
@@ -430,6 +435,15 @@ __global__ __launch_bounds__(256, EPI == 4 ? 2 : HNM_SCAN_OCC) void ncf16_scan_k
   for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
     for (int e = 0; e < 8; ++e) awm[s2][e] = A.wmh[mfma32_row(8 * s2 + e, h)];
+  // EPI 5: the wm rows of the pair epilogue -- user a's MFMAs carry wm in A row 0, user b's
+  // in A row 4, so one accumulator ends with a's total at (row 0 -> lanes 0-31, r = 0) and
+  // b's at (row 4 -> lanes 32-63, r = 0)
+  h8 awa[2], awb[2];
+#pragma unroll
+  for (int s2 = 0; s2 < 2; ++s2) {
+    awa[s2] = j == 0 ? awm[s2] : (h8){};
+    awb[s2] = j == 4 ? awm[s2] : (h8){};
+  }
   h2 wm2[8];  // EPI 1: wm of this lane's accumulator rows, in pairs
 #pragma unroll
   for (int r = 0; r < 16; r += 2)
@@ -455,8 +469,8 @@ __global__ __launch_bounds__(256, EPI == 4 ? 2 : HNM_SCAN_OCC) void ncf16_scan_k
     mend = (int)hi;
     nm = mpos < mend ? A.midx[mpos] : INT_BIG;
   }
-  int32_t* seg = MODE == SCAN_THRESH ? A.buf + ((u0 * A.NP) + p) * (int64_t)A.capp : nullptr;
-  const int64_t segstride = (int64_t)A.NP * A.capp;  // next user's segment
+  int32_t* seg = MODE == SCAN_THRESH ? A.buf + ((u0 * A.nseg) + p) * (int64_t)A.capp : nullptr;
+  const int64_t segstride = (int64_t)A.nseg * A.capp;  // next user's segment
 
   const int64_t ntiles = part_end > part_start ? hnm_cdiv(part_end - part_start, TILE) : 0;
   // tile staging: thread (row, c) moves 16 B of Q~ and of G~; tile t + 1 is fetched into
@@ -469,35 +483,40 @@ __global__ __launch_bounds__(256, EPI == 4 ? 2 : HNM_SCAN_OCC) void ncf16_scan_k
     const int64_t n = base + srow;
     nq = (h8){};
     ng = (h8){};
-    if (n < part_end && !(ABL & 128)) {
-      const int64_t it = n * A.istride;
+    if (n < part_end && !(ABL & 32)) {
+      const int64_t it = (n >> A.gshift) * A.tstride + (n & ((1 << A.gshift) - 1));
       nq = *reinterpret_cast<const h8*>(A.Q16 + it * 64 + 8 * sc);
       ng = *reinterpret_cast<const h8*>(A.G16 + it * 64 + 8 * sc);
     }
-    const int64_t nj = std::min<int64_t>(base + j, part_end - 1) * A.istride;
+    const int64_t cj = std::min<int64_t>(base + j, part_end - 1);
+    const int64_t nj = (cj >> A.gshift) * A.tstride + (cj & ((1 << A.gshift) - 1));
     nb = A.Bi[nj];
     nd = A.Di[nj];
   };
   auto stash = [&](int buf) {
-    if (ABL & 256) {
-      __builtin_amdgcn_s_waitcnt(0);  // keep the loads' wait, drop the stores
-      return;
-    }
     *reinterpret_cast<h8*>(&qs[buf][srow * RS + 8 * sc]) = nq;
     *reinterpret_cast<h8*>(&gs[buf][srow * RS + 8 * sc]) = ng;
   };
-  if (ntiles > 0 && !(ABL & 32)) {
-    fetch(part_start);
+  // tiles of the partition in order, stepping over the sample's tiles (THRESH with skip)
+  const int64_t gt0 = part_start / TILE;  // partitions are tile-aligned
+  auto next_tile = [&](int64_t t) {
+    ++t;
+    if (MODE == SCAN_THRESH && A.skip && t < ntiles && (gt0 + t) % A.skip == 0) ++t;
+    return t;
+  };
+  int64_t t = next_tile(-1);
+  if (t < ntiles) {
+    fetch(part_start + t * TILE);
     stash(0);
   }
   __syncthreads();
-  for (int64_t t = 0; t < ntiles; ++t) {
+  for (int cur = 0; t < ntiles; cur ^= 1) {
     const int64_t base = part_start + t * TILE;
-    const int cur = (int)(t & 1);
+    const int64_t tn = next_tile(t);
     const float bj = ru * nb, dj = nd;  // bound terms of this tile's item j
     // the prefetch is the only global load in the tile body (vmcnt waits are in order: any
     // later load's wait would also wait for it)
-    if (t + 1 < ntiles && !(ABL & 32)) fetch(base + TILE);
+    if (tn < ntiles) fetch(part_start + tn * TILE);
 
     if (nu > 0) {
     if (!(ABL & 16)) {  // GMF of the wave's 32 users x 32 items, in score units
@@ -525,7 +544,7 @@ __global__ __launch_bounds__(256, EPI == 4 ? 2 : HNM_SCAN_OCC) void ncf16_scan_k
     const bool ivalid = h == 0 && n < part_end;
     const int64_t tile_end = std::min<int64_t>(base + TILE, part_end);
     unsigned mbits = 0;
-    if (masked) {  // scanned items are real items here (istride 1 in the THRESH pass)
+    if (masked) {  // scanned items are real items here (identity map in the THRESH pass)
       uint64_t pend = __ballot(lane < 32 && nm < tile_end) & 0xffffffffull;
       while (pend) {
         const int u = __builtin_ctzll(pend);
@@ -534,7 +553,7 @@ __global__ __launch_bounds__(256, EPI == 4 ? 2 : HNM_SCAN_OCC) void ncf16_scan_k
           const int tgt = hnm_readlane_i(nm, u);
           if (tgt >= tile_end) break;
           if (lane == u) {
-            mbits |= 1u << (tgt - (int)base);
+            if (tgt >= base) mbits |= 1u << (tgt - (int)base);  // (a skipped tile's: consumed)
             ++mpos;
             nm = mpos < mend ? A.midx[mpos] : INT_BIG;
           }
@@ -542,7 +561,7 @@ __global__ __launch_bounds__(256, EPI == 4 ? 2 : HNM_SCAN_OCC) void ncf16_scan_k
       }
     }
 
-    if constexpr (EPI == 2 || EPI == 4) {
+    if constexpr (EPI == 2 || EPI == 4 || EPI == 5 || EPI == 6) {
       // Two users per iteration: independent MFMA chains for users a and b, and ONE
       // epilogue for both -- after the packed-dot partials, a single permlane32 swap of
       // (a's partials, b's partials) and an add leave a's totals in lanes 0-31 and b's in
@@ -562,55 +581,94 @@ __global__ __launch_bounds__(256, EPI == 4 ? 2 : HNM_SCAN_OCC) void ncf16_scan_k
       };
       if (PF) pload(0, std::min(1, nu - 1));
       for (int u = 0; u < nu; u += 2) {
-        const int ua = u, ub = std::min(u + 1, nu - 1);
+        // FOLD: user b = u + 1 even past nu (zero P~ rows, folded term -inf / not stored)
+        const int ua = u, ub = FOLD ? u + 1 : std::min(u + 1, nu - 1);
         const bool hasb = u + 1 < nu;
         const int uh = h ? ub : ua;
-        if (!PF) pload(ua, ub);
+        if (!PF) gn = (ABL & 16) ? 0.f : gsm[wave][uh][j];
         const float gmu = gn;
-        h8 xa[4], xb[4];
+        h8 pc[8];  // EPI 4: this pair's prefetched fragments (the next pair's go to pn)
 #pragma unroll
-        for (int s = 0; s < 4; ++s) {
-          xa[s] = pn[s] + q[s];
-          xa[s] = __builtin_elementwise_min(__builtin_elementwise_max(xa[s], (h8){}), (h8)(_Float16)1.f);
-          xb[s] = pn[4 + s] + q[s];
-          xb[s] = __builtin_elementwise_min(__builtin_elementwise_max(xb[s], (h8){}), (h8)(_Float16)1.f);
-        }
+        for (int c = 0; c < 8; ++c) pc[c] = pn[c];
         if (PF && u + 2 < nu) pload(u + 2, std::min(u + 3, nu - 1));
         f32x16 acc0 = b2c, acc1 = b2c;
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
+          // without the prefetch each fragment is read right before its MFMA (fewer live
+          // registers than the 8-fragment prefetch)
+          const h8 pa = PF ? pc[s] : (ABL & 8) ? q[s] : *reinterpret_cast<const h8*>(&ps[(wave * 32 + ua) * 64 + 8 * h + 16 * s]);
+          const h8 pb = PF ? pc[4 + s] : (ABL & 8) ? q[(s + 1) & 3] : *reinterpret_cast<const h8*>(&ps[(wave * 32 + ub) * 64 + 8 * h + 16 * s]);
+          h8 x = pa + q[s];
+          x = __builtin_elementwise_min(__builtin_elementwise_max(x, (h8){}), (h8)(_Float16)1.f);
+          h8 y = pb + q[s];
+          y = __builtin_elementwise_min(__builtin_elementwise_max(y, (h8){}), (h8)(_Float16)1.f);
           if (ABL & 4) {
-            acc0[s] += (float)xa[s][0] + (float)xa[s][7];
-            acc1[s] += (float)xb[s][0] + (float)xb[s][7];
+            acc0[s] += (float)x[0] + (float)x[7];
+            acc1[s] += (float)y[0] + (float)y[7];
           } else {
-            acc0 = mfma16(aw[s], xa[s], acc0);
-            acc1 = mfma16(aw[s], xb[s], acc1);
+            acc0 = mfma16(aw[s], x, acc0);
+            acc1 = mfma16(aw[s], y, acc1);
           }
         }
         if constexpr (FOLD) {
-          // wm . relu(H~) with fma-mix (f16 x f16 products, exact in fp32, fp32 sums), which
-          // co-issues with the MFMA pipe -- v_dot2_f32_f16 does not (tools/issue_probe.hip);
-          // two chains per user, the first seeded with the folded term of that user's half:
-          // after the swap, lanes 0-31 hold user a's test value, lanes 32-63 user b's
+          // wm . relu(H~): the chains of user a / b are seeded with the folded term of that
+          // user's half; after the swap, lanes 0-31 hold user a's test value, lanes 32-63 b's
+          float val;
+          if constexpr (EPI == 5) {
+            // wm . relu(H~) of both users on the matrix pipe (4 MFMAs into one accumulator
+            // seeded with the folded term); relu by the [0, 1] clamp of the converts
+            h8 y[4];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              y[0][e] = (_Float16)acc0[e];
+              y[1][e] = (_Float16)acc0[8 + e];
+              y[2][e] = (_Float16)acc1[e];
+              y[3][e] = (_Float16)acc1[8 + e];
+            }
+#pragma unroll
+            for (int c = 0; c < 4; ++c)
+              y[c] = __builtin_elementwise_min(__builtin_elementwise_max(y[c], (h8){}), (h8)(_Float16)1.f);
+            f32x16 d = {};
+            d[0] = gmu;
+            d = mfma16(awa[0], y[0], d);
+            d = mfma16(awa[1], y[1], d);
+            d = mfma16(awb[0], y[2], d);
+            d = mfma16(awb[1], y[3], d);
+            val = d[0];
+          } else {
           float ma0 = h ? 0.f : gmu, mb0 = h ? gmu : 0.f, ma1 = 0.f, mb1 = 0.f;
           if (ABL & 2) {
             ma1 = acc0[0] + acc0[15];
             mb1 = acc1[0] + acc1[15];
-          } else
+          } else if (EPI == 6) {
+            // fma-mix reduction (co-issues with the MFMA pipe, twice the VALU count)
 #pragma unroll
-          for (int r = 0; r < 16; r += 2) {
-            h2 ya = {(_Float16)acc0[r], (_Float16)acc0[r + 1]};
-            ya = __builtin_elementwise_min(__builtin_elementwise_max(ya, (h2){}), (h2)(_Float16)1.f);
-            h2 yb = {(_Float16)acc1[r], (_Float16)acc1[r + 1]};
-            yb = __builtin_elementwise_min(__builtin_elementwise_max(yb, (h2){}), (h2)(_Float16)1.f);
-            const h2 wv = wm2[r >> 1];
-            ma0 = hnm_fma_mix_lo(ya, wv, ma0);
-            ma1 = hnm_fma_mix_hi(ya, wv, ma1);
-            mb0 = hnm_fma_mix_lo(yb, wv, mb0);
-            mb1 = hnm_fma_mix_hi(yb, wv, mb1);
+            for (int r = 0; r < 16; r += 2) {
+              h2 ya = {(_Float16)acc0[r], (_Float16)acc0[r + 1]};
+              ya = __builtin_elementwise_min(__builtin_elementwise_max(ya, (h2){}), (h2)(_Float16)1.f);
+              h2 yb = {(_Float16)acc1[r], (_Float16)acc1[r + 1]};
+              yb = __builtin_elementwise_min(__builtin_elementwise_max(yb, (h2){}), (h2)(_Float16)1.f);
+              const h2 wv = wm2[r >> 1];
+              ma0 = hnm_fma_mix_lo(ya, wv, ma0);
+              ma1 = hnm_fma_mix_hi(ya, wv, ma1);
+              mb0 = hnm_fma_mix_lo(yb, wv, mb0);
+              mb1 = hnm_fma_mix_hi(yb, wv, mb1);
+            }
+          } else {
+            // packed dots: half the VALU count of fma-mix; the dot unit shares the matrix pipe
+            // (tools/issue_probe.hip), which the layer-2 MFMAs leave ~60% idle
+#pragma unroll
+            for (int r = 0; r < 16; r += 2) {
+              h2 ya = {(_Float16)acc0[r], (_Float16)acc0[r + 1]};
+              ya = __builtin_elementwise_min(__builtin_elementwise_max(ya, (h2){}), (h2)(_Float16)1.f);
+              h2 yb = {(_Float16)acc1[r], (_Float16)acc1[r + 1]};
+              yb = __builtin_elementwise_min(__builtin_elementwise_max(yb, (h2){}), (h2)(_Float16)1.f);
+              ma0 = __builtin_amdgcn_fdot2(ya, wm2[r >> 1], ma0, false);
+              mb0 = __builtin_amdgcn_fdot2(yb, wm2[r >> 1], mb0, false);
+            }
           }
-          const float ma = ma0 + ma1, mb = mb0 + mb1;
-          float val;
+          const float ma = EPI == 6 || (ABL & 2) ? ma0 + ma1 : ma0;
+          const float mb = EPI == 6 || (ABL & 2) ? mb0 + mb1 : mb0;
           if (ABL & 64) {
             val = h ? mb : ma;
           } else {
@@ -618,6 +676,7 @@ __global__ __launch_bounds__(256, EPI == 4 ? 2 : HNM_SCAN_OCC) void ncf16_scan_k
                                                               false, false);
             val = __uint_as_float(sw2[0]) + __uint_as_float(sw2[1]);
           }
+          }  // EPI
           const bool lvalid = n < part_end && (h == 0 || hasb);
           if (MODE == SCAN_SAMPLE) {
             if (lvalid) A.dense[(u0 + uh) * A.ldo + n] = val;  // score - e_i
@@ -769,10 +828,11 @@ __global__ __launch_bounds__(256, EPI == 4 ? 2 : HNM_SCAN_OCC) void ncf16_scan_k
       }
     }  // EPI
     }  // nu > 0
-    if (t + 1 < ntiles && !(ABL & 32)) stash(cur ^ 1);
+    if (tn < ntiles) stash(cur ^ 1);
     __syncthreads();
+    t = tn;
   }
-  if (MODE == SCAN_THRESH && lane < nu) A.cnt[(u0 + lane) * A.NP + p] = ccount + ((ABL & 1) ? (int)tv : 0);
+  if (MODE == SCAN_THRESH && lane < nu) A.cnt[(u0 + lane) * A.nseg + p] = ccount + ((ABL & 1) ? (int)tv : 0);
 }
 
 // Per row: Eu = user-constant part of the bound (scaled): 6u unit (c0 + A_u) + unit abs.
@@ -799,6 +859,61 @@ __global__ __launch_bounds__(256) void cert_tau_kernel(const float* __restrict__
   const bool ok = !prm->bad && __builtin_isfinite(tv) && __builtin_isfinite(scale);
   tau[b] = ok ? tv : __builtin_inff();
   flag[b] = ok ? 0 : 1;
+}
+
+// The main scan skips the sample's tiles; their candidates come from the sample pass's
+// values v = approx - e_i instead: approx + e_i >= tau  <=>  v + 2 e_i >= tau (the same
+// quantities up to fp32 rounding, which tau's guard covers).  One wave per row, in item
+// order, into the row's last segment; flagged rows take the fallback and append nothing.
+__global__ __launch_bounds__(256) void cert_sample_append_kernel(
+    const float* __restrict__ sd, int64_t Ns, int64_t tstride, int64_t B,
+    const float* __restrict__ tau, const int* __restrict__ flag, const float* __restrict__ Cu,
+    const float* __restrict__ Bi, const float* __restrict__ Di, const CertParams* __restrict__ prm,
+    const int64_t* __restrict__ mptr, const int32_t* __restrict__ midx, int nseg, int capp,
+    int* __restrict__ cnt, int32_t* __restrict__ buf) {
+  const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (b >= B) return;
+  const int lane = threadIdx.x & 63;
+  int32_t* seg = buf + (b * nseg + nseg - 1) * (int64_t)capp;
+  int count = 0;
+  if (!flag[b]) {
+    const float tv = tau[b];
+    const float ru = CERT_RHO * prm->unit;
+    const float cu = ru * Cu[b];
+    int64_t mpos = 0, mend = 0;
+    int nm = INT_BIG;
+    if (mptr) {
+      mpos = mptr[b];
+      mend = mptr[b + 1];
+      nm = mpos < mend ? midx[mpos] : INT_BIG;
+    }
+    const float* row = sd + b * Ns;
+    for (int64_t c0 = 0; c0 < Ns; c0 += 64) {
+      const int64_t c = c0 + lane;
+      const int64_t item = (c >> 5) * tstride + (c & 31);
+      bool pass = false;
+      if (c < Ns) {
+        const float ei = fmaf(cu, Di[item], ru * Bi[item]);
+        pass = !(row[c] + 2.f * ei < tv);
+      }
+      if (mptr) {  // filtered items of this chunk (the cursor is wave-uniform)
+        const int64_t cl = std::min<int64_t>(c0 + 64, Ns) - 1;
+        const int64_t end = (cl >> 5) * tstride + (cl & 31) + 1;
+        while (nm < end) {
+          if (nm == item) pass = false;
+          ++mpos;
+          nm = mpos < mend ? midx[mpos] : INT_BIG;
+        }
+      }
+      const uint64_t m = __ballot(pass);
+      if (m) {
+        const int pos = count + __popcll(m & ((1ull << lane) - 1));
+        if (pass && pos < capp) seg[pos] = (int32_t)item;
+        count += __popcll(m);
+      }
+    }
+  }
+  if (lane == 0) cnt[b * nseg + nseg - 1] = count;
 }
 
 // ------------------------------------------------------------------ exact re-scoring
@@ -958,27 +1073,31 @@ struct CertWs {
 };
 
 // ~wg workgroups per CU (the scan variant's occupancy), NP a multiple of 8 (XCD-aware),
-// <= CERT_MAX_NP
+// <= CERT_MAX_NP - 8 (one more candidate segment per row holds the sample's candidates)
 Partition scan_partition(int64_t I, int64_t ublocks, int num_cus, int wg) {
   int64_t np = std::max<int64_t>(1, (int64_t)wg * num_cus / std::max<int64_t>(ublocks, 1));
   np = std::min<int64_t>(np, std::max<int64_t>(1, hnm_cdiv(I, 4 * TILE)));
-  np = std::min<int64_t>(np, CERT_MAX_NP);
+  np = std::min<int64_t>(np, CERT_MAX_NP - 8);
   if (np >= 8) np = np / 8 * 8;
   const int64_t ipp = hnm_cdiv(hnm_cdiv(I, np), TILE) * TILE;
   return {(int)hnm_cdiv(I, ipp), ipp};
 }
 
 struct CertShape {
-  int64_t stride, Ns;
-  Partition part;  // of the main scan
-  int capp;        // candidate slots per (row, partition)
+  int64_t stride;  // the sample is every stride-th tile of 32 items (tiles 0, stride, ...)
+  int64_t Ns;      // sample items
+  Partition part;  // of the main scan (which skips the sample's tiles)
+  int nseg;        // candidate segments per row: part.np + the sample's
+  int capp;        // candidate slots per (row, segment)
 };
 
 CertShape cert_shape(int64_t B, int64_t I, int K, int num_cus, int wg) {
   CertShape sh;
   sh.stride = std::max<int64_t>(8, I / CERT_SAMPLE);  // sample <= 1/8 of the items (shards too)
-  sh.Ns = hnm_cdiv(I, sh.stride);
+  const int64_t tiles = hnm_cdiv(I, TILE), stiles = hnm_cdiv(tiles, sh.stride);
+  sh.Ns = (stiles - 1) * TILE + std::min<int64_t>(TILE, I - (stiles - 1) * sh.stride * TILE);
   sh.part = scan_partition(I, hnm_cdiv(B, 128), num_cus, wg);
+  sh.nseg = sh.part.np + 1;
   // expected candidates ~ K * stride (the sample's K-th) plus the bound's margin; each
   // partition gets 4x its even share, >= 64 slots
   const int64_t total = std::min<int64_t>(8192, std::max<int64_t>(512, 16 * (int64_t)K * sh.stride));
@@ -1007,11 +1126,11 @@ size_t cert_carve(char* base, int64_t B, int64_t I, int K, int num_cus, int wg, 
   x.b2s = (float*)take(32 * 4);
   x.kthv = (float*)take((size_t)B * K * 4);
   x.kthi = (int64_t*)take((size_t)B * K * 8);
-  x.cnt = (int*)take((size_t)B * sh.part.np * 4);
+  x.cnt = (int*)take((size_t)B * sh.nseg * 4);
   x.flag = (int*)take(B * 4);
   x.ovf_cnt = (int32_t*)take(256);
   x.ovf_rows = (int32_t*)take(B * 4);
-  x.buf = (int32_t*)take((size_t)B * sh.part.np * sh.capp * 4);
+  x.buf = (int32_t*)take((size_t)B * sh.nseg * sh.capp * 4);
   x.sdense = (float*)take((size_t)B * sh.Ns * 4);
   x.P16 = (_Float16*)take((size_t)B * 64 * 2);
   x.WG16 = (_Float16*)take((size_t)B * 64 * 2);
@@ -1050,8 +1169,13 @@ template <int MODE>
 void launch_scan(hnm_ctx* ctx, dim3 grid, const ScanArgs& a) {
   // tuning knob HNM_OPT_SCAN_USERS: 1 = packed-dot epilogue, 2 = two users per iteration
   // with the folded test (default), 3 = MFMA epilogue, 4 = as 2 with the next pair's LDS
-  // operands prefetched, at 2 workgroups per CU
-  if (ctx->scan_users == 4)
+  // operands prefetched, at 2 workgroups per CU, 5 = as 2 with the wm reduction on the
+  // matrix pipe, 6 = as 2 with fma-mix reduction
+  if (ctx->scan_users == 6)
+    hipLaunchKernelGGL((ncf16_scan_kernel<MODE, 6>), grid, dim3(256), 0, ctx->stream, a);
+  else if (ctx->scan_users == 5)
+    hipLaunchKernelGGL((ncf16_scan_kernel<MODE, 5>), grid, dim3(256), 0, ctx->stream, a);
+  else if (ctx->scan_users == 4)
     hipLaunchKernelGGL((ncf16_scan_kernel<MODE, 4>), grid, dim3(256), 0, ctx->stream, a);
   else if (ctx->scan_users == 2)
     hipLaunchKernelGGL((ncf16_scan_kernel<MODE, 2>), grid, dim3(256), 0, ctx->stream, a);
@@ -1076,7 +1200,9 @@ ScanArgs scan_args(const CertWs& x, int64_t B) {
   a.Eu = x.Eu;
   a.prm = x.prm;
   a.B = B;
-  a.istride = 1;
+  a.tstride = TILE;
+  a.gshift = 5;
+  a.skip = 0;
   return a;
 }
 
@@ -1104,22 +1230,32 @@ hnm_status ncf_cert_topk(hnm_ctx* ctx, const hnm_ncf_weights* w, const NcfTabs& 
   hnm_status st = cert_prepare(ctx, w, t, B, x);
   if (st) return st;
   const int64_t ublocks = hnm_cdiv(B, 128);
-  // 1. sample pass: approx - e of items 0, stride, ... -> K-th best per row -> tau
+  // 1. sample pass: approx - e of the items of tiles 0, stride, ... -> K-th best per row ->
+  // tau; the sample's own candidates are appended from these values (segment nseg - 1)
+  const int64_t tstride = sh.stride * TILE;
+  const int64_t Ns = sh.Ns;
   {
     ScanArgs a = scan_args(x, B);
-    a.I = sh.Ns;
-    a.istride = sh.stride;
+    a.I = Ns;
+    a.tstride = tstride;
+    a.gshift = 5;
     a.dense = x.sdense;
-    a.ldo = sh.Ns;
-    Partition ps = scan_partition(sh.Ns, ublocks, ctx->num_cus, wg);
+    a.ldo = Ns;
+    Partition ps = scan_partition(Ns, ublocks, ctx->num_cus, wg);
     a.ipp = ps.ipp;
     a.NP = ps.np;
+    a.nseg = ps.np;
     launch_scan<SCAN_SAMPLE>(ctx, dim3((unsigned)ps.np, (unsigned)ublocks), a);
     HNM_LAUNCH_CHECK();
-    st = hnm_sample_kth(ctx, x.sdense, sh.Ns, B, sh.Ns, mptr, midx, K, sh.stride, x.kthv);
+    st = hnm_sample_kth(ctx, x.sdense, Ns, B, Ns, mptr, midx, K, TILE, tstride, x.kthv);
     if (st) return st;
     hipLaunchKernelGGL(cert_tau_kernel, dim3((unsigned)hnm_cdiv(B, 256)), dim3(256), 0,
                        ctx->stream, x.kthv, K, x.Au, x.Cu, x.prm, B, x.tau, x.flag, x.Eu);
+    HNM_LAUNCH_CHECK();
+    hipLaunchKernelGGL(cert_sample_append_kernel, dim3((unsigned)hnm_cdiv(B, 4)), dim3(256), 0,
+                       ctx->stream, x.sdense, Ns, tstride, B, x.tau,
+                       x.flag, x.Cu, x.Bi, x.Di,
+                       x.prm, mptr, midx, sh.nseg, sh.capp, x.cnt, x.buf);
     HNM_LAUNCH_CHECK();
   }
   // 2. main f16 scan: append items with approx + e >= tau_u to per-partition segments
@@ -1134,6 +1270,8 @@ hnm_status ncf_cert_topk(hnm_ctx* ctx, const hnm_ncf_weights* w, const NcfTabs& 
     a.capp = sh.capp;
     a.ipp = sh.part.ipp;
     a.NP = sh.part.np;
+    a.nseg = sh.nseg;
+    a.skip = sh.stride;
     hnm_timer_begin(ctx, HNM_TIME_SCORE);
     launch_scan<SCAN_THRESH>(ctx, dim3((unsigned)sh.part.np, (unsigned)ublocks), a);
     hnm_timer_end(ctx, HNM_TIME_SCORE);
@@ -1142,7 +1280,7 @@ hnm_status ncf_cert_topk(hnm_ctx* ctx, const hnm_ncf_weights* w, const NcfTabs& 
   // 3. exact fp32 re-scoring + top-K of the candidates; unusable rows -> queue
   hipLaunchKernelGGL(ncf_rescore_kernel, dim3((unsigned)hnm_cdiv(B, 4)), dim3(256), 0, ctx->stream,
                      t, w->mf, w->w2, w->h1, w->h2, w->b2, w->wp + w->mf, w->bp, B, x.flag, x.cnt,
-                     x.buf, sh.part.np, sh.capp, K, ov, oi, x.ovf_rows, x.ovf_cnt,
+                     x.buf, sh.nseg, sh.capp, K, ov, oi, x.ovf_rows, x.ovf_cnt,
                      ctx->stats_on ? ctx->stats_dev : nullptr);
   HNM_LAUNCH_CHECK();
   // 4. exact fp32 scan over all items for the queued rows (device-side row list)
@@ -1168,6 +1306,7 @@ hnm_status ncf_cert_debug(hnm_ctx* ctx, const hnm_ncf_weights* w, const NcfTabs&
   Partition part = choose_partition(I, ublocks, ctx->num_cus);
   a.ipp = part.ipp;
   a.NP = part.np;
+  a.nseg = part.np;
   launch_scan<SCAN_DEBUG>(ctx, dim3((unsigned)part.np, (unsigned)ublocks), a);
   HNM_LAUNCH_CHECK();
   hipLaunchKernelGGL(cert_unscale_kernel, dim3((unsigned)hnm_cdiv(B * I, 256)), dim3(256), 0,

@@ -327,7 +327,7 @@ __global__ __launch_bounds__(256) void rows_topk_kernel(const float* __restrict_
 
 // ------------------------------------------------------------------ sample K-th (lower bound)
 // For the certified pre-filters: a LOWER BOUND of the K-th best value of each row of a
-// dense [B, Ns] sample (masked columns excluded; column c is item c * istride).  Each lane
+// dense [B, Ns] sample (masked columns excluded; column c is item (c / grp) * period + c % grp).  Each lane
 // keeps its own top-4; the K-th best of the 64 x 4 survivors is <= the row's K-th best
 // (dropping values can only lower it).  ~3 VALU per element, no serial inserts.  A NaN in
 // the row makes the result NaN (the caller then takes the exact fallback).
@@ -335,7 +335,7 @@ __global__ __launch_bounds__(256) void sample_kth_kernel(const float* __restrict
                                                          int64_t B, int64_t Ns,
                                                          const int64_t* __restrict__ mptr,
                                                          const int32_t* __restrict__ midx, int K,
-                                                         int64_t istride,
+                                                         int64_t grp, int64_t period,
                                                          float* __restrict__ out) {
   const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (b >= B) return;
@@ -362,9 +362,11 @@ __global__ __launch_bounds__(256) void sample_kth_kernel(const float* __restrict
       const int64_t cb = base + 64 * q;
       if (mptr && cb < Ns) {
         const int64_t c = cb + lane;
-        const int64_t end = (std::min<int64_t>(cb + 64, Ns) - 1) * istride + 1;  // real ids < end
+        const int64_t cl = std::min<int64_t>(cb + 64, Ns) - 1;
+        const int64_t end = (cl / grp) * period + cl % grp + 1;  // real ids < end
         while (nm < end) {
-          if (nm % istride == 0 && c == nm / istride) v[q] = -__builtin_inff();
+          const int64_t r = nm % period;
+          if (r < grp && c == (nm / period) * grp + r) v[q] = -__builtin_inff();
           ++mpos;
           nm = mpos < mend ? midx[mpos] : INT_BIG;
         }
@@ -392,11 +394,12 @@ __global__ __launch_bounds__(256) void sample_kth_kernel(const float* __restrict
 
 // ------------------------------------------------------------------ host side
 hnm_status hnm_sample_kth(hnm_ctx* ctx, const float* s, int64_t ld, int64_t B, int64_t Ns,
-                          const int64_t* mptr, const int32_t* midx, int K, int64_t istride,
-                          float* out) {
+                          const int64_t* mptr, const int32_t* midx, int K, int64_t grp,
+                          int64_t period, float* out) {
   HNM_REQUIRE(K >= 1 && K <= 64, HNM_EINVAL, "sample_kth: 1 <= K <= 64");
+  HNM_REQUIRE(grp >= 1 && period >= grp, HNM_EINVAL, "sample_kth: 1 <= grp <= period");
   hipLaunchKernelGGL(sample_kth_kernel, dim3((unsigned)hnm_cdiv(B, 4)), dim3(256), 0, ctx->stream,
-                     s, ld, B, Ns, mptr, midx, K, istride, out);
+                     s, ld, B, Ns, mptr, midx, K, grp, period, out);
   HNM_LAUNCH_CHECK();
   return HNM_OK;
 }

@@ -70,7 +70,8 @@ def test_bound_holds_full_catalogue(kw):
     assert ratio <= 1.0, ratio
 
 
-@pytest.fixture(params=[1, 2, 3, 4], ids=["epi-dot", "epi-pair", "epi-mfma", "epi-pair-pf"])
+@pytest.fixture(params=[1, 2, 3, 4, 5, 6],
+                ids=["epi-dot", "epi-pair", "epi-mfma", "epi-pair-pf", "epi-pair-mfma", "epi-pair-mix"])
 def scan_users(request):
     """The scan kernel's epilogue variants (HNM_OPT_SCAN_USERS): all must be identical."""
     dev = torch.device(DEV, 0)

@@ -79,6 +79,6 @@ int main() {
     printf("EPI=%d ABL=%2d  %7.3f ms  %6.1f TF useful  %5.2f cyc/user-tile/SIMD @2.2GHz\n", EPI, \
            ABL, ms, useful / (ms * 1e-3) / 1e12, ms * 1e-3 * 2.2e9 / (pairs / 32 / 1024));   \
   }
-  V(0, 2) V(32, 2) V(128, 2) V(256, 2) V(0, 2)
+  V(0, 2) V(0, 5) V(0, 6) V(0, 2) V(0, 5) V(0, 6) V(0, 2) V(0, 5) V(0, 6) V(0, 1)
   return 0;
 }
