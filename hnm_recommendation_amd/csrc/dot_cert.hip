@@ -695,7 +695,7 @@ hnm_status dot_cert_topk(hnm_ctx* ctx, const DotArgs& a, bool bias, void* scratc
     launch_dscan<DSCAN_SAMPLE>(ctx, dim3((unsigned)sh.spart.np, (unsigned)ublocks), s, sh.DP, bias);
     HNM_LAUNCH_CHECK();
     const int64_t nmax_cols = (int64_t)sh.spart.np * 32;
-    st = hnm_sample_kth(ctx, x.sdense, nmax_cols, a.B, nmax_cols, nullptr, nullptr, a.K, 1, 1, x.kthv);
+    st = hnm_sample_kth(ctx, x.sdense, nmax_cols, a.B, nmax_cols, nullptr, nullptr, a.K, 1, 1, nullptr, x.kthv);
     if (st) return st;
     hipLaunchKernelGGL(dcert_tau_kernel, dim3((unsigned)hnm_cdiv(a.B, 256)), dim3(256), 0,
                        ctx->stream, x.kthv, a.K, x.Nu, x.ubr, x.prm, a.B, x.tau, x.flag, x.E);

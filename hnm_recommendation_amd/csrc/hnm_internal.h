@@ -100,4 +100,4 @@ hnm_status hnm_topk_rows_strided(hnm_ctx* ctx, const float* s, int64_t ld, int64
 // written at out[b * K + K - 1].
 hnm_status hnm_sample_kth(hnm_ctx* ctx, const float* s, int64_t ld, int64_t B, int64_t Ns,
                           const int64_t* mptr, const int32_t* midx, int K, int64_t grp,
-                          int64_t period, float* out);
+                          int64_t period, const int32_t* sidx, float* out);

@@ -49,9 +49,10 @@ hnm_status hnm_topk_merge_rows(hnm_ctx* ctx, const float* cv, const int32_t* ci,
 namespace {
 
 constexpr int64_t CERT_MIN_ITEMS = 8192;  // below this the exact LIST kernel is cheaper
-constexpr int64_t CERT_SAMPLE = 12288;    // sample items for the threshold pass
 constexpr float CERT_RHO = 0.0029296875f; // 6 u16 = 3 * 2^-10
 constexpr int CERT_MAX_NP = 64;           // item partitions (candidate segments per row)
+constexpr int CERT_PROXY_USERS = 8;       // batch rows that pick the champion sample
+constexpr int64_t CERT_CHAMPIONS = 2048;  // champion sample size (item groups)
 #ifndef HNM_SCAN_OCC
 #define HNM_SCAN_OCC 3
 #endif
@@ -338,7 +339,7 @@ __global__ __launch_bounds__(256) void cert_convert_kernel(
 }
 
 // ------------------------------------------------------------------ f16 scan kernel
-// SAMPLE: dense[b][n] = approx - e_i (scanned item n = (n / 32) * tstride + n % 32), e_i = the per-item part
+// SAMPLE: dense[b][n] = approx - e_i (scanned item n = sidx[n] if set), e_i = the per-item part
 //         of the bound, 6u unit (B_i + C_u D_i);
 // THRESH: append item n to segment (b, partition) when approx + e_i >= tau_b;
 // DEBUG:  dense[b][n] = approx, dense2[b][n] = Eu_b + e_i (the whole bound), scaled units.
@@ -359,19 +360,14 @@ struct ScanArgs {
   const CertParams* prm;
   int64_t B;
   int64_t I;        // scanned items (sample count for the sample pass)
-  int64_t tstride;  // scanned item n is item (n >> gshift) * tstride + n % 2^gshift (gshift 5,
-                    // tstride 32: identity; the sample pass scans every (tstride / 32)-th tile)
-  int gshift;
-  int64_t skip;     // THRESH: tiles with (global tile index % skip) == 0 are the sample's
-                    // and are not scanned (0: scan every tile)
+  const int32_t* sidx;  // SAMPLE: scanned item n is item sidx[n] (gather map), if set
   int64_t ipp;
   int NP;
-  int nseg;         // candidate segments per row (NP, + 1 for the sample's candidates)
   const int64_t* mptr;
   const int32_t* midx;
   const float* tau;  // [B] scaled thresholds (THRESH)
-  int* cnt;          // [B, nseg] appended counts (THRESH)
-  int32_t* buf;      // [B, nseg, capp] appended item ids (THRESH)
+  int* cnt;          // [B, NP] appended counts (THRESH)
+  int32_t* buf;      // [B, NP, capp] appended item ids (THRESH)
   int capp;
   float* dense;      // [B, ldo]
   float* dense2;     // [B, ldo] (DEBUG)
@@ -469,8 +465,8 @@ __global__ __launch_bounds__(256, EPI == 4 ? 2 : HNM_SCAN_OCC) void ncf16_scan_k
     mend = (int)hi;
     nm = mpos < mend ? A.midx[mpos] : INT_BIG;
   }
-  int32_t* seg = MODE == SCAN_THRESH ? A.buf + ((u0 * A.nseg) + p) * (int64_t)A.capp : nullptr;
-  const int64_t segstride = (int64_t)A.nseg * A.capp;  // next user's segment
+  int32_t* seg = MODE == SCAN_THRESH ? A.buf + ((u0 * A.NP) + p) * (int64_t)A.capp : nullptr;
+  const int64_t segstride = (int64_t)A.NP * A.capp;  // next user's segment
 
   const int64_t ntiles = part_end > part_start ? hnm_cdiv(part_end - part_start, TILE) : 0;
   // tile staging: thread (row, c) moves 16 B of Q~ and of G~; tile t + 1 is fetched into
@@ -484,12 +480,12 @@ __global__ __launch_bounds__(256, EPI == 4 ? 2 : HNM_SCAN_OCC) void ncf16_scan_k
     nq = (h8){};
     ng = (h8){};
     if (n < part_end && !(ABL & 32)) {
-      const int64_t it = (n >> A.gshift) * A.tstride + (n & ((1 << A.gshift) - 1));
+      const int64_t it = A.sidx ? (int64_t)A.sidx[n] : n;
       nq = *reinterpret_cast<const h8*>(A.Q16 + it * 64 + 8 * sc);
       ng = *reinterpret_cast<const h8*>(A.G16 + it * 64 + 8 * sc);
     }
     const int64_t cj = std::min<int64_t>(base + j, part_end - 1);
-    const int64_t nj = (cj >> A.gshift) * A.tstride + (cj & ((1 << A.gshift) - 1));
+    const int64_t nj = A.sidx ? (int64_t)A.sidx[cj] : cj;
     nb = A.Bi[nj];
     nd = A.Di[nj];
   };
@@ -497,14 +493,7 @@ __global__ __launch_bounds__(256, EPI == 4 ? 2 : HNM_SCAN_OCC) void ncf16_scan_k
     *reinterpret_cast<h8*>(&qs[buf][srow * RS + 8 * sc]) = nq;
     *reinterpret_cast<h8*>(&gs[buf][srow * RS + 8 * sc]) = ng;
   };
-  // tiles of the partition in order, stepping over the sample's tiles (THRESH with skip)
-  const int64_t gt0 = part_start / TILE;  // partitions are tile-aligned
-  auto next_tile = [&](int64_t t) {
-    ++t;
-    if (MODE == SCAN_THRESH && A.skip && t < ntiles && (gt0 + t) % A.skip == 0) ++t;
-    return t;
-  };
-  int64_t t = next_tile(-1);
+  int64_t t = 0;
   if (t < ntiles) {
     fetch(part_start + t * TILE);
     stash(0);
@@ -512,7 +501,7 @@ __global__ __launch_bounds__(256, EPI == 4 ? 2 : HNM_SCAN_OCC) void ncf16_scan_k
   __syncthreads();
   for (int cur = 0; t < ntiles; cur ^= 1) {
     const int64_t base = part_start + t * TILE;
-    const int64_t tn = next_tile(t);
+    const int64_t tn = t + 1;
     const float bj = ru * nb, dj = nd;  // bound terms of this tile's item j
     // the prefetch is the only global load in the tile body (vmcnt waits are in order: any
     // later load's wait would also wait for it)
@@ -553,7 +542,7 @@ __global__ __launch_bounds__(256, EPI == 4 ? 2 : HNM_SCAN_OCC) void ncf16_scan_k
           const int tgt = hnm_readlane_i(nm, u);
           if (tgt >= tile_end) break;
           if (lane == u) {
-            if (tgt >= base) mbits |= 1u << (tgt - (int)base);  // (a skipped tile's: consumed)
+            mbits |= 1u << (tgt - (int)base);
             ++mpos;
             nm = mpos < mend ? A.midx[mpos] : INT_BIG;
           }
@@ -832,7 +821,7 @@ __global__ __launch_bounds__(256, EPI == 4 ? 2 : HNM_SCAN_OCC) void ncf16_scan_k
     __syncthreads();
     t = tn;
   }
-  if (MODE == SCAN_THRESH && lane < nu) A.cnt[(u0 + lane) * A.nseg + p] = ccount + ((ABL & 1) ? (int)tv : 0);
+  if (MODE == SCAN_THRESH && lane < nu) A.cnt[(u0 + lane) * A.NP + p] = ccount + ((ABL & 1) ? (int)tv : 0);
 }
 
 // Per row: Eu = user-constant part of the bound (scaled): 6u unit (c0 + A_u) + unit abs.
@@ -861,59 +850,38 @@ __global__ __launch_bounds__(256) void cert_tau_kernel(const float* __restrict__
   flag[b] = ok ? 0 : 1;
 }
 
-// The main scan skips the sample's tiles; their candidates come from the sample pass's
-// values v = approx - e_i instead: approx + e_i >= tau  <=>  v + 2 e_i >= tau (the same
-// quantities up to fp32 rounding, which tau's guard covers).  One wave per row, in item
-// order, into the row's last segment; flagged rows take the fallback and append nothing.
-__global__ __launch_bounds__(256) void cert_sample_append_kernel(
-    const float* __restrict__ sd, int64_t Ns, int64_t tstride, int64_t B,
-    const float* __restrict__ tau, const int* __restrict__ flag, const float* __restrict__ Cu,
-    const float* __restrict__ Bi, const float* __restrict__ Di, const CertParams* __restrict__ prm,
-    const int64_t* __restrict__ mptr, const int32_t* __restrict__ midx, int nseg, int capp,
-    int* __restrict__ cnt, int32_t* __restrict__ buf) {
-  const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (b >= B) return;
+// Champion sample: items split into nch contiguous groups of gsz; each group's item with the
+// best mean (approx - e_i) over the proxy rows (the first users of the batch) -- a
+// popularity-like sample in increasing item order.  Any item subset gives a valid lower
+// bound of a row's K-th; this one tends to hold the rows' best items.  One wave per group.
+__global__ __launch_bounds__(256) void cert_champion_kernel(const float* __restrict__ pd,
+                                                            int64_t ld, int np_rows, int64_t I,
+                                                            int64_t gsz, int64_t nch,
+                                                            int32_t* __restrict__ sidx) {
+  const int64_t g = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (g >= nch) return;
   const int lane = threadIdx.x & 63;
-  int32_t* seg = buf + (b * nseg + nseg - 1) * (int64_t)capp;
-  int count = 0;
-  if (!flag[b]) {
-    const float tv = tau[b];
-    const float ru = CERT_RHO * prm->unit;
-    const float cu = ru * Cu[b];
-    int64_t mpos = 0, mend = 0;
-    int nm = INT_BIG;
-    if (mptr) {
-      mpos = mptr[b];
-      mend = mptr[b + 1];
-      nm = mpos < mend ? midx[mpos] : INT_BIG;
-    }
-    const float* row = sd + b * Ns;
-    for (int64_t c0 = 0; c0 < Ns; c0 += 64) {
-      const int64_t c = c0 + lane;
-      const int64_t item = (c >> 5) * tstride + (c & 31);
-      bool pass = false;
-      if (c < Ns) {
-        const float ei = fmaf(cu, Di[item], ru * Bi[item]);
-        pass = !(row[c] + 2.f * ei < tv);
-      }
-      if (mptr) {  // filtered items of this chunk (the cursor is wave-uniform)
-        const int64_t cl = std::min<int64_t>(c0 + 64, Ns) - 1;
-        const int64_t end = (cl >> 5) * tstride + (cl & 31) + 1;
-        while (nm < end) {
-          if (nm == item) pass = false;
-          ++mpos;
-          nm = mpos < mend ? midx[mpos] : INT_BIG;
-        }
-      }
-      const uint64_t m = __ballot(pass);
-      if (m) {
-        const int pos = count + __popcll(m & ((1ull << lane) - 1));
-        if (pass && pos < capp) seg[pos] = (int32_t)item;
-        count += __popcll(m);
-      }
+  const int64_t i0 = g * gsz, i1 = std::min<int64_t>(I, i0 + gsz);
+  float best = -__builtin_inff();
+  int64_t bi = i0;
+  for (int64_t i = i0 + lane; i < i1; i += 64) {
+    float m = 0.f;
+    for (int r = 0; r < np_rows; ++r) m += pd[r * ld + i];
+    if (m > best) {  // NaN never wins; the lane's items are visited in increasing order
+      best = m;
+      bi = i;
     }
   }
-  if (lane == 0) cnt[b * nseg + nseg - 1] = count;
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {  // wave argmax, ties -> smaller item
+    const float ob = __shfl_xor(best, o);
+    const int64_t oi = __shfl_xor(bi, o);
+    if (ob > best || (ob == best && oi < bi)) {
+      best = ob;
+      bi = oi;
+    }
+  }
+  if (lane == 0) sidx[g] = (int32_t)bi;
 }
 
 // ------------------------------------------------------------------ exact re-scoring
@@ -1063,7 +1031,8 @@ __global__ void cert_unscale_kernel(float* __restrict__ a, float* __restrict__ e
 
 struct CertWs {
   CertParams* prm;
-  float *Au, *Cu, *Bi, *Di, *tau, *Eu, *b2s, *kthv, *sdense, *part;
+  float *Au, *Cu, *Bi, *Di, *tau, *Eu, *b2s, *kthv, *pdense, *cdense, *part;
+  int32_t* sidx;  // champion items
   int64_t* kthi;
   int *cnt, *flag;
   int32_t *buf, *ovf_cnt, *ovf_rows;
@@ -1073,34 +1042,31 @@ struct CertWs {
 };
 
 // ~wg workgroups per CU (the scan variant's occupancy), NP a multiple of 8 (XCD-aware),
-// <= CERT_MAX_NP - 8 (one more candidate segment per row holds the sample's candidates)
+// <= CERT_MAX_NP
 Partition scan_partition(int64_t I, int64_t ublocks, int num_cus, int wg) {
   int64_t np = std::max<int64_t>(1, (int64_t)wg * num_cus / std::max<int64_t>(ublocks, 1));
   np = std::min<int64_t>(np, std::max<int64_t>(1, hnm_cdiv(I, 4 * TILE)));
-  np = std::min<int64_t>(np, CERT_MAX_NP - 8);
+  np = std::min<int64_t>(np, CERT_MAX_NP);
   if (np >= 8) np = np / 8 * 8;
   const int64_t ipp = hnm_cdiv(hnm_cdiv(I, np), TILE) * TILE;
   return {(int)hnm_cdiv(I, ipp), ipp};
 }
 
 struct CertShape {
-  int64_t stride;  // the sample is every stride-th tile of 32 items (tiles 0, stride, ...)
-  int64_t Ns;      // sample items
-  Partition part;  // of the main scan (which skips the sample's tiles)
-  int nseg;        // candidate segments per row: part.np + the sample's
-  int capp;        // candidate slots per (row, segment)
+  int64_t nch, gsz;  // champion sample: nch groups of gsz items
+  Partition part;    // of the main scan
+  int capp;          // candidate slots per (row, partition)
 };
 
 CertShape cert_shape(int64_t B, int64_t I, int K, int num_cus, int wg) {
   CertShape sh;
-  sh.stride = std::max<int64_t>(8, I / CERT_SAMPLE);  // sample <= 1/8 of the items (shards too)
-  const int64_t tiles = hnm_cdiv(I, TILE), stiles = hnm_cdiv(tiles, sh.stride);
-  sh.Ns = (stiles - 1) * TILE + std::min<int64_t>(TILE, I - (stiles - 1) * sh.stride * TILE);
+  sh.gsz = hnm_cdiv(I, std::min<int64_t>(CERT_CHAMPIONS, I));
+  sh.nch = hnm_cdiv(I, sh.gsz);
   sh.part = scan_partition(I, hnm_cdiv(B, 128), num_cus, wg);
-  sh.nseg = sh.part.np + 1;
-  // expected candidates ~ K * stride (the sample's K-th) plus the bound's margin; each
-  // partition gets 4x its even share, >= 64 slots
-  const int64_t total = std::min<int64_t>(8192, std::max<int64_t>(512, 16 * (int64_t)K * sh.stride));
+  // a row's candidates: items within the bound's margin of the champion sample's K-th --
+  // at worst (no shared best items) the K-th of a 1/gsz sample, ~K * gsz items; each
+  // partition gets 4x its even share of 2x that, >= 64 slots (overflow: fallback row)
+  const int64_t total = std::min<int64_t>(8192, std::max<int64_t>(512, 2 * (int64_t)K * sh.gsz));
   sh.capp = (int)std::max<int64_t>(64, std::min<int64_t>(total, hnm_cdiv(4 * total, sh.part.np)));
   return sh;
 }
@@ -1125,13 +1091,15 @@ size_t cert_carve(char* base, int64_t B, int64_t I, int K, int num_cus, int wg, 
   x.Eu = (float*)take(B * 4);
   x.b2s = (float*)take(32 * 4);
   x.kthv = (float*)take((size_t)B * K * 4);
+  x.pdense = (float*)take((size_t)CERT_PROXY_USERS * I * 4);
+  x.cdense = (float*)take((size_t)B * sh.nch * 4);
+  x.sidx = (int32_t*)take((size_t)sh.nch * 4);
   x.kthi = (int64_t*)take((size_t)B * K * 8);
-  x.cnt = (int*)take((size_t)B * sh.nseg * 4);
+  x.cnt = (int*)take((size_t)B * sh.part.np * 4);
   x.flag = (int*)take(B * 4);
   x.ovf_cnt = (int32_t*)take(256);
   x.ovf_rows = (int32_t*)take(B * 4);
-  x.buf = (int32_t*)take((size_t)B * sh.nseg * sh.capp * 4);
-  x.sdense = (float*)take((size_t)B * sh.Ns * 4);
+  x.buf = (int32_t*)take((size_t)B * sh.part.np * sh.capp * 4);
   x.P16 = (_Float16*)take((size_t)B * 64 * 2);
   x.WG16 = (_Float16*)take((size_t)B * 64 * 2);
   x.Q16 = (_Float16*)take((size_t)I * 64 * 2);
@@ -1200,9 +1168,7 @@ ScanArgs scan_args(const CertWs& x, int64_t B) {
   a.Eu = x.Eu;
   a.prm = x.prm;
   a.B = B;
-  a.tstride = TILE;
-  a.gshift = 5;
-  a.skip = 0;
+  a.sidx = nullptr;
   return a;
 }
 
@@ -1230,32 +1196,37 @@ hnm_status ncf_cert_topk(hnm_ctx* ctx, const hnm_ncf_weights* w, const NcfTabs& 
   hnm_status st = cert_prepare(ctx, w, t, B, x);
   if (st) return st;
   const int64_t ublocks = hnm_cdiv(B, 128);
-  // 1. sample pass: approx - e of the items of tiles 0, stride, ... -> K-th best per row ->
-  // tau; the sample's own candidates are appended from these values (segment nseg - 1)
-  const int64_t tstride = sh.stride * TILE;
-  const int64_t Ns = sh.Ns;
+  // 1. champion sample: the first rows' approx - e over all items -> the best item of each
+  // of nch groups -> every row's K-th best approx - e over those items -> tau (a lower bound
+  // of the exact K-th for any item subset; this one tends to hold the rows' best items)
   {
-    ScanArgs a = scan_args(x, B);
-    a.I = Ns;
-    a.tstride = tstride;
-    a.gshift = 5;
-    a.dense = x.sdense;
-    a.ldo = Ns;
-    Partition ps = scan_partition(Ns, ublocks, ctx->num_cus, wg);
-    a.ipp = ps.ipp;
-    a.NP = ps.np;
-    a.nseg = ps.np;
-    launch_scan<SCAN_SAMPLE>(ctx, dim3((unsigned)ps.np, (unsigned)ublocks), a);
+    const int64_t bp = std::min<int64_t>(CERT_PROXY_USERS, B);
+    ScanArgs a = scan_args(x, bp);
+    a.I = I;
+    a.dense = x.pdense;
+    a.ldo = I;
+    const int64_t np = std::min<int64_t>(3 * (int64_t)ctx->num_cus, hnm_cdiv(I, 4 * TILE));
+    a.ipp = hnm_cdiv(hnm_cdiv(I, np), TILE) * TILE;
+    a.NP = (int)hnm_cdiv(I, a.ipp);
+    launch_scan<SCAN_SAMPLE>(ctx, dim3((unsigned)a.NP, 1), a);
     HNM_LAUNCH_CHECK();
-    st = hnm_sample_kth(ctx, x.sdense, Ns, B, Ns, mptr, midx, K, TILE, tstride, x.kthv);
+    hipLaunchKernelGGL(cert_champion_kernel, dim3((unsigned)hnm_cdiv(sh.nch, 4)), dim3(256), 0,
+                       ctx->stream, x.pdense, I, (int)bp, I, sh.gsz, sh.nch, x.sidx);
+    HNM_LAUNCH_CHECK();
+    ScanArgs c = scan_args(x, B);
+    c.I = sh.nch;
+    c.sidx = x.sidx;
+    c.dense = x.cdense;
+    c.ldo = sh.nch;
+    const Partition pc = scan_partition(sh.nch, ublocks, ctx->num_cus, wg);
+    c.ipp = pc.ipp;
+    c.NP = pc.np;
+    launch_scan<SCAN_SAMPLE>(ctx, dim3((unsigned)pc.np, (unsigned)ublocks), c);
+    HNM_LAUNCH_CHECK();
+    st = hnm_sample_kth(ctx, x.cdense, sh.nch, B, sh.nch, mptr, midx, K, 1, 1, x.sidx, x.kthv);
     if (st) return st;
     hipLaunchKernelGGL(cert_tau_kernel, dim3((unsigned)hnm_cdiv(B, 256)), dim3(256), 0,
                        ctx->stream, x.kthv, K, x.Au, x.Cu, x.prm, B, x.tau, x.flag, x.Eu);
-    HNM_LAUNCH_CHECK();
-    hipLaunchKernelGGL(cert_sample_append_kernel, dim3((unsigned)hnm_cdiv(B, 4)), dim3(256), 0,
-                       ctx->stream, x.sdense, Ns, tstride, B, x.tau,
-                       x.flag, x.Cu, x.Bi, x.Di,
-                       x.prm, mptr, midx, sh.nseg, sh.capp, x.cnt, x.buf);
     HNM_LAUNCH_CHECK();
   }
   // 2. main f16 scan: append items with approx + e >= tau_u to per-partition segments
@@ -1270,8 +1241,6 @@ hnm_status ncf_cert_topk(hnm_ctx* ctx, const hnm_ncf_weights* w, const NcfTabs& 
     a.capp = sh.capp;
     a.ipp = sh.part.ipp;
     a.NP = sh.part.np;
-    a.nseg = sh.nseg;
-    a.skip = sh.stride;
     hnm_timer_begin(ctx, HNM_TIME_SCORE);
     launch_scan<SCAN_THRESH>(ctx, dim3((unsigned)sh.part.np, (unsigned)ublocks), a);
     hnm_timer_end(ctx, HNM_TIME_SCORE);
@@ -1280,7 +1249,7 @@ hnm_status ncf_cert_topk(hnm_ctx* ctx, const hnm_ncf_weights* w, const NcfTabs& 
   // 3. exact fp32 re-scoring + top-K of the candidates; unusable rows -> queue
   hipLaunchKernelGGL(ncf_rescore_kernel, dim3((unsigned)hnm_cdiv(B, 4)), dim3(256), 0, ctx->stream,
                      t, w->mf, w->w2, w->h1, w->h2, w->b2, w->wp + w->mf, w->bp, B, x.flag, x.cnt,
-                     x.buf, sh.nseg, sh.capp, K, ov, oi, x.ovf_rows, x.ovf_cnt,
+                     x.buf, sh.part.np, sh.capp, K, ov, oi, x.ovf_rows, x.ovf_cnt,
                      ctx->stats_on ? ctx->stats_dev : nullptr);
   HNM_LAUNCH_CHECK();
   // 4. exact fp32 scan over all items for the queued rows (device-side row list)
@@ -1306,7 +1275,6 @@ hnm_status ncf_cert_debug(hnm_ctx* ctx, const hnm_ncf_weights* w, const NcfTabs&
   Partition part = choose_partition(I, ublocks, ctx->num_cus);
   a.ipp = part.ipp;
   a.NP = part.np;
-  a.nseg = part.np;
   launch_scan<SCAN_DEBUG>(ctx, dim3((unsigned)part.np, (unsigned)ublocks), a);
   HNM_LAUNCH_CHECK();
   hipLaunchKernelGGL(cert_unscale_kernel, dim3((unsigned)hnm_cdiv(B * I, 256)), dim3(256), 0,

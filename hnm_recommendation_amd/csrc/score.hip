@@ -327,7 +327,8 @@ __global__ __launch_bounds__(256) void rows_topk_kernel(const float* __restrict_
 
 // ------------------------------------------------------------------ sample K-th (lower bound)
 // For the certified pre-filters: a LOWER BOUND of the K-th best value of each row of a
-// dense [B, Ns] sample (masked columns excluded; column c is item (c / grp) * period + c % grp).  Each lane
+// dense [B, Ns] sample (masked columns excluded; column c is item sidx[c], or
+// (c / grp) * period + c % grp -- increasing in c either way).  Each lane
 // keeps its own top-4; the K-th best of the 64 x 4 survivors is <= the row's K-th best
 // (dropping values can only lower it).  ~3 VALU per element, no serial inserts.  A NaN in
 // the row makes the result NaN (the caller then takes the exact fallback).
@@ -336,6 +337,7 @@ __global__ __launch_bounds__(256) void sample_kth_kernel(const float* __restrict
                                                          const int64_t* __restrict__ mptr,
                                                          const int32_t* __restrict__ midx, int K,
                                                          int64_t grp, int64_t period,
+                                                         const int32_t* __restrict__ sidx,
                                                          float* __restrict__ out) {
   const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (b >= B) return;
@@ -361,12 +363,13 @@ __global__ __launch_bounds__(256) void sample_kth_kernel(const float* __restrict
     for (int q = 0; q < 4; ++q) {
       const int64_t cb = base + 64 * q;
       if (mptr && cb < Ns) {
-        const int64_t c = cb + lane;
+        // column -> item (increasing in the column), matched against the row's sorted mask
+        auto item_of = [&](int64_t c) { return sidx ? (int64_t)sidx[c] : (c / grp) * period + c % grp; };
+        const int64_t c = std::min<int64_t>(cb + lane, Ns - 1);
         const int64_t cl = std::min<int64_t>(cb + 64, Ns) - 1;
-        const int64_t end = (cl / grp) * period + cl % grp + 1;  // real ids < end
+        const int64_t it = item_of(c), end = item_of(cl) + 1;  // real ids < end
         while (nm < end) {
-          const int64_t r = nm % period;
-          if (r < grp && c == (nm / period) * grp + r) v[q] = -__builtin_inff();
+          if (cb + lane < Ns && it == nm) v[q] = -__builtin_inff();
           ++mpos;
           nm = mpos < mend ? midx[mpos] : INT_BIG;
         }
@@ -395,11 +398,11 @@ __global__ __launch_bounds__(256) void sample_kth_kernel(const float* __restrict
 // ------------------------------------------------------------------ host side
 hnm_status hnm_sample_kth(hnm_ctx* ctx, const float* s, int64_t ld, int64_t B, int64_t Ns,
                           const int64_t* mptr, const int32_t* midx, int K, int64_t grp,
-                          int64_t period, float* out) {
+                          int64_t period, const int32_t* sidx, float* out) {
   HNM_REQUIRE(K >= 1 && K <= 64, HNM_EINVAL, "sample_kth: 1 <= K <= 64");
   HNM_REQUIRE(grp >= 1 && period >= grp, HNM_EINVAL, "sample_kth: 1 <= grp <= period");
   hipLaunchKernelGGL(sample_kth_kernel, dim3((unsigned)hnm_cdiv(B, 4)), dim3(256), 0, ctx->stream,
-                     s, ld, B, Ns, mptr, midx, K, grp, period, out);
+                     s, ld, B, Ns, mptr, midx, K, grp, period, sidx, out);
   HNM_LAUNCH_CHECK();
   return HNM_OK;
 }

@@ -64,7 +64,7 @@ int main() {
   a.prm = prm;
   a.B = B;
   a.I = I;
-  a.istride = 1;
+
   a.ipp = sh.part.ipp;
   a.NP = sh.part.np;
   a.capp = sh.capp;
