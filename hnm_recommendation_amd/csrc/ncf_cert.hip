@@ -558,6 +558,7 @@ __global__ __launch_bounds__(256, EPI == 4 ? 2 : HNM_SCAN_OCC) void ncf16_scan_k
       // read, the bound, the test and the ballot are shared by the pair.  EPI 4 reads the
       // next pair's P~ fragments and GMF term one iteration ahead.
       constexpr bool PF = EPI == 4;
+      const float* gsmh = &gsm[wave][h][j];
       h8 pn[8];
       float gn = 0.f;
       auto pload = [&](int ua_, int ub_) {
@@ -574,7 +575,8 @@ __global__ __launch_bounds__(256, EPI == 4 ? 2 : HNM_SCAN_OCC) void ncf16_scan_k
         const int ua = u, ub = FOLD ? u + 1 : std::min(u + 1, nu - 1);
         const bool hasb = u + 1 < nu;
         const int uh = h ? ub : ua;
-        if (!PF) gn = (ABL & 16) ? 0.f : gsm[wave][uh][j];
+        // FOLD: lane (j, h) reads its own user's row u + h (= uh) through a per-lane base
+        if (!PF) gn = (ABL & 16) ? 0.f : FOLD ? gsmh[u * 33] : gsm[wave][uh][j];
         const float gmu = gn;
         h8 pc[8];  // EPI 4: this pair's prefetched fragments (the next pair's go to pn)
 #pragma unroll
@@ -672,12 +674,12 @@ __global__ __launch_bounds__(256, EPI == 4 ? 2 : HNM_SCAN_OCC) void ncf16_scan_k
           } else if (ABL & 1) {
             tv += val;  // keep the value live, no test
           } else {
-            bool pass = lvalid && !(val < 0.f);                 // !(score + e_i < tau)
-            if (masked) {
+            uint64_t m = __ballot(lvalid && !(val < 0.f));      // !(score + e_i < tau)
+            if (masked) {  // uniform: filtered items of the two users
               const int mba = hnm_readlane_i((int)mbits, ua), mbb = hnm_readlane_i((int)mbits, ub);
-              pass = pass && !(((h ? mbb : mba) >> j) & 1);
+              m &= __ballot(!(((h ? mbb : mba) >> j) & 1));
             }
-            const uint64_t m = __ballot(pass);
+            const bool pass = (m >> lane) & 1;
             if (m) {
               const unsigned mh = (unsigned)(m >> (32 * h));
               const int ca = hnm_readlane_i(ccount, ua), cb = hnm_readlane_i(ccount, ub);
