@@ -68,6 +68,9 @@ _SIGS = {
     "hnm_pair_dot_f32": (_i32, [_p, _p, _i64, _i64, _p, _i64, _i64, C.c_int, _p, _p, _i64, _p,
                                 _p, _p, _p]),
     "hnm_ncf_topk_f32": (_i32, [_p, C.POINTER(NcfWeights), _p, _i64, _p, _p, C.c_int, _p, _p]),
+    "hnm_ncf_topk_begin_f32": (_i32, [_p, C.POINTER(NcfWeights), _p, _i64, _p, _p, C.c_int, _p]),
+    "hnm_ncf_topk_finish_f32": (_i32, [_p, C.POINTER(NcfWeights), _p, _i64, _p, _p, C.c_int, _p,
+                                       C.c_int, _p, _p]),
     "hnm_ncf_scores_f32": (_i32, [_p, C.POINTER(NcfWeights), _p, _i64, _p, _i64]),
     "hnm_ncf_pair_scores_f32": (_i32, [_p, C.POINTER(NcfWeights), _p, _p, _i64, _p]),
     "hnm_ncf_prefilter_debug_f32": (_i32, [_p, C.POINTER(NcfWeights), _p, _i64, _p, _i64, _p]),

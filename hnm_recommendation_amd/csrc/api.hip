@@ -100,6 +100,8 @@ extern "C" hnm_status hnm_ctx_num_cus(hnm_ctx* ctx, int* out) {
 }
 
 hnm_status hnm_workspace(hnm_ctx* ctx, size_t bytes, void** out) {
+  HNM_REQUIRE(!ctx->pend.kind, HNM_EINVAL,
+              "a two-phase top-K call is open on this ctx: call its _finish first");
   bytes = hnm_align(bytes);
   if (bytes > ctx->ws_size) {
     HNM_HIP_CHECK(hipStreamSynchronize(ctx->stream));
@@ -114,6 +116,19 @@ hnm_status hnm_workspace(hnm_ctx* ctx, size_t bytes, void** out) {
     ctx->ws_size = want;
   }
   *out = ctx->ws;
+  return HNM_OK;
+}
+
+__global__ void fill_f32_kernel(float* __restrict__ p, int64_t n, float v) {
+  const int64_t x = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (x < n) p[x] = v;
+}
+
+hnm_status hnm_fill_f32(hnm_ctx* ctx, float* p, int64_t n, float v) {
+  if (n <= 0) return HNM_OK;
+  hipLaunchKernelGGL(fill_f32_kernel, dim3((unsigned)hnm_cdiv(n, 256)), dim3(256), 0, ctx->stream,
+                     p, n, v);
+  HNM_LAUNCH_CHECK();
   return HNM_OK;
 }
 

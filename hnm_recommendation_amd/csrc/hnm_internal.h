@@ -27,7 +27,21 @@ struct hnm_ctx {
   int scan_users;                  // HNM_OPT_SCAN_USERS (tuning: users per scan iteration)
   unsigned long long* stats_dev;   // pre-filter counters: rows, candidates, fallback rows
   int stats_on;                    // HNM_OPT_STATS (default 0: counting costs same-address atomics)
+  // open two-phase top-K call (hnm_*_topk_begin_f32 ... hnm_*_topk_finish_f32): the
+  // workspace holds the begin phase's tables until the matching finish, so every other
+  // workspace user is refused meanwhile
+  struct {
+    int kind;               // 0 none; HNM_PEND_* below
+    int64_t B, I;
+    int K;
+    const void* ids;
+    const void* items;      // the item table the begin phase read
+  } pend;
 };
+#define HNM_PEND_NCF_CERT 1
+#define HNM_PEND_NCF_EXACT 2
+#define HNM_PEND_DOT_CERT 3
+#define HNM_PEND_DOT_EXACT 4
 
 // dominant-kernel timer classes (hnm_ctx_enable_timing mask)
 #define HNM_TIME_SCORE 1  // the scoring / scan kernel of each top-K or dense call
@@ -101,3 +115,6 @@ hnm_status hnm_topk_rows_strided(hnm_ctx* ctx, const float* s, int64_t ld, int64
 hnm_status hnm_sample_kth(hnm_ctx* ctx, const float* s, int64_t ld, int64_t B, int64_t Ns,
                           const int64_t* mptr, const int32_t* midx, int K, int64_t grp,
                           int64_t period, const int32_t* sidx, float* out);
+
+// p[0, n) = v on the ctx stream
+hnm_status hnm_fill_f32(hnm_ctx* ctx, float* p, int64_t n, float v);

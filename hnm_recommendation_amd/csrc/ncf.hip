@@ -621,17 +621,25 @@ struct NcfCall {
   void* extra;
 };
 
+// fill = false: only re-derive the pointers into the workspace the begin phase of a
+// two-phase call filled (hnm_ncf_topk_finish_f32).
 static hnm_status ncf_tables(hnm_ctx* ctx, const hnm_ncf_weights* w, const int64_t* ids,
-                             int64_t B, size_t extra, NcfCall* out) {
+                             int64_t B, size_t extra, NcfCall* out, bool fill = true) {
   const bool big = w->h1 > 64 || w->mf > 64;  // generic kernel; else the 32-user kernels
   const int H1P = big ? 128 : 64, GW = big ? 128 : 64;
   const int64_t I = w->num_items;
   const bool gcopy = (big ? w->mf != GW : w->mf % 4 != 0) || ((uintptr_t)w->gmf_item % 16 != 0);
   const size_t szP = hnm_align((size_t)B * H1P * 4), szW = hnm_align((size_t)B * GW * 4);
   const size_t szQ = hnm_align((size_t)I * H1P * 4), szG = gcopy ? hnm_align((size_t)I * GW * 4) : 0;
-  void* wsp;
-  hnm_status st = hnm_workspace(ctx, szP + szW + szQ + szG + extra, &wsp);
-  if (st) return st;
+  void* wsp = ctx->ws;
+  hnm_status st = HNM_OK;
+  if (fill) {
+    st = hnm_workspace(ctx, szP + szW + szQ + szG + extra, &wsp);
+    if (st) return st;
+  } else {
+    HNM_REQUIRE(ctx->ws && ctx->ws_size >= szP + szW + szQ + szG + extra, HNM_EINVAL,
+                "ncf: the begin phase's workspace is gone");
+  }
   char* base = (char*)wsp;
   float* Pu = (float*)base; base += szP;
   float* WGu = (float*)base; base += szW;
@@ -639,6 +647,14 @@ static hnm_status ncf_tables(hnm_ctx* ctx, const hnm_ncf_weights* w, const int64
   float* Gc = (float*)base; base += szG;
   out->extra = base;
   out->big = big;
+  const float* G = w->gmf_item;
+  int64_t ldg = w->mf;
+  if (gcopy) {
+    G = Gc;
+    ldg = GW;
+  }
+  out->t = {Pu, WGu, Qi, G, ldg};
+  if (!fill) return HNM_OK;
   if (w->h1 < H1P) {
     HNM_HIP_CHECK(hipMemsetAsync(Pu, 0, szP, ctx->stream));
     HNM_HIP_CHECK(hipMemsetAsync(Qi, 0, szQ, ctx->stream));
@@ -654,16 +670,11 @@ static hnm_status ncf_tables(hnm_ctx* ctx, const hnm_ncf_weights* w, const int64
                      ctx->stream, w->gmf_user, w->num_users, w->mf, w->mf, ids, B, w->wp, WGu,
                      GW, ctx->err_dev, big ? 0 : 1);
   HNM_LAUNCH_CHECK();
-  const float* G = w->gmf_item;
-  int64_t ldg = w->mf;
   if (gcopy) {
     HNM_HIP_CHECK(hipMemsetAsync(Gc, 0, szG, ctx->stream));
     HNM_HIP_CHECK(hipMemcpy2DAsync(Gc, GW * 4, w->gmf_item, w->mf * 4, w->mf * 4, I,
                                    hipMemcpyDeviceToDevice, ctx->stream));
-    G = Gc;
-    ldg = GW;
   }
-  out->t = {Pu, WGu, Qi, G, ldg};
   return HNM_OK;
 }
 
@@ -722,6 +733,67 @@ extern "C" hnm_status hnm_ncf_topk_f32(hnm_ctx* ctx, const hnm_ncf_weights* w,
   HNM_REQUIRE(k >= 1 && k <= 64 && out_idx, HNM_EINVAL, "ncf_topk: fused path needs 1 <= k <= 64");
   return ncf_common<false>(ctx, w, user_ids, B, mask_ptr, mask_idx, k, out_val, out_idx,
                            nullptr, 0);
+}
+
+// Two-phase fused top-K for item-sharded serving (sharding.py): begin computes the per-call
+// tables and each row's certified lower bound of its exact K-th best score over this
+// call's items (real units, -inf when unknown); the caller may replace the bounds by any
+// valid lower bounds -- the max over the item shards of a node (one all-reduce) -- and
+// finish scans with them.  Rows may then keep fewer than K entries (short_ok), padded with
+// (-inf, -1); the merge across shards completes them.  Exact mode (pre-filter off or not
+// eligible): begin writes -inf, finish runs the exact fused scan.
+extern "C" hnm_status hnm_ncf_topk_begin_f32(hnm_ctx* ctx, const hnm_ncf_weights* w,
+                                             const int64_t* user_ids, int64_t B,
+                                             const int64_t* mask_ptr, const int32_t* mask_idx,
+                                             int k, float* lower_bound) {
+  hnm_status st = ncf_check(w);
+  if (st) return st;
+  HNM_REQUIRE(ctx && user_ids && lower_bound && k >= 1 && k <= 64, HNM_EINVAL,
+              "ncf_topk_begin: bad argument");
+  HNM_REQUIRE(!ctx->pend.kind, HNM_EINVAL, "ncf_topk_begin: a two-phase call is already open");
+  if (B <= 0) return HNM_OK;
+  const bool big = w->h1 > 64 || w->mf > 64;
+  const bool cert = !big && ctx->prefilter && ncf_cert_eligible(w, k);
+  if (cert) {
+    NcfCall c;
+    st = ncf_tables(ctx, w, user_ids, B,
+                    ncf_cert_bytes(B, w->num_items, k, ctx->num_cus, ncf_cert_wg(ctx)), &c);
+    if (st) return st;
+    st = ncf_cert_begin(ctx, w, c.t, B, mask_ptr, mask_idx, k, c.extra, lower_bound);
+    if (st) return st;
+  } else {
+    st = hnm_fill_f32(ctx, lower_bound, B, -__builtin_inff());
+    if (st) return st;
+  }
+  ctx->pend = {cert ? HNM_PEND_NCF_CERT : HNM_PEND_NCF_EXACT, B, w->num_items, k, user_ids,
+               w->mlp_item};
+  return HNM_OK;
+}
+
+extern "C" hnm_status hnm_ncf_topk_finish_f32(hnm_ctx* ctx, const hnm_ncf_weights* w,
+                                              const int64_t* user_ids, int64_t B,
+                                              const int64_t* mask_ptr, const int32_t* mask_idx,
+                                              int k, const float* lower_bound, int short_ok,
+                                              float* out_val, int64_t* out_idx) {
+  HNM_REQUIRE(ctx && w && out_idx, HNM_EINVAL, "ncf_topk_finish: bad argument");
+  if (B <= 0) return HNM_OK;
+  const int kind = ctx->pend.kind;
+  HNM_REQUIRE((kind == HNM_PEND_NCF_CERT || kind == HNM_PEND_NCF_EXACT) && ctx->pend.B == B &&
+                  ctx->pend.K == k && ctx->pend.I == w->num_items && ctx->pend.ids == user_ids &&
+                  ctx->pend.items == w->mlp_item,
+              HNM_EINVAL, "ncf_topk_finish: no matching hnm_ncf_topk_begin_f32 on this ctx");
+  ctx->pend.kind = 0;
+  if (kind == HNM_PEND_NCF_EXACT)
+    return ncf_common<false>(ctx, w, user_ids, B, mask_ptr, mask_idx, k, out_val, out_idx,
+                             nullptr, 0);
+  HNM_REQUIRE(lower_bound, HNM_EINVAL, "ncf_topk_finish: lower_bound is NULL");
+  NcfCall c;
+  hnm_status st = ncf_tables(ctx, w, user_ids, B,
+                             ncf_cert_bytes(B, w->num_items, k, ctx->num_cus, ncf_cert_wg(ctx)),
+                             &c, false);
+  if (st) return st;
+  return ncf_cert_finish(ctx, w, c.t, B, mask_ptr, mask_idx, k, c.extra, lower_bound,
+                         short_ok, out_val, out_idx);
 }
 
 extern "C" hnm_status hnm_ncf_scores_f32(hnm_ctx* ctx, const hnm_ncf_weights* w,

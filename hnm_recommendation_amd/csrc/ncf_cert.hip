@@ -52,7 +52,8 @@ constexpr int64_t CERT_MIN_ITEMS = 8192;  // below this the exact LIST kernel is
 constexpr float CERT_RHO = 0.0029296875f; // 6 u16 = 3 * 2^-10
 constexpr int CERT_MAX_NP = 64;           // item partitions (candidate segments per row)
 constexpr int CERT_PROXY_USERS = 8;       // batch rows that pick the champion sample
-constexpr int64_t CERT_CHAMPIONS = 2048;  // champion sample size (item groups)
+constexpr int64_t CERT_CHAMPIONS = 2048;  // champion sample size (item groups), at most
+constexpr int64_t CERT_GROUP_MIN = 48;    // items per champion group, at least
 #ifndef HNM_SCAN_OCC
 #define HNM_SCAN_OCC 3
 #endif
@@ -827,26 +828,48 @@ __global__ __launch_bounds__(256, EPI == 4 ? 2 : HNM_SCAN_OCC) void ncf16_scan_k
 }
 
 // Per row: Eu = user-constant part of the bound (scaled): 6u unit (c0 + A_u) + unit abs.
-// With the sample's K-th best of (approx - e_i), tau_u = Kth - 2 Eu - guard, where the
-// guard covers the fp32 rounding of the test quantities (<= a few 2^-24 of the row's
-// absolute score scale).  Rows with an unusable bound get tau = +inf and flag = 1.
-__global__ __launch_bounds__(256) void cert_tau_kernel(const float* __restrict__ kth, int K,
-                                                       const float* __restrict__ Au,
-                                                       const float* __restrict__ Cu,
-                                                       const CertParams* __restrict__ prm,
-                                                       int64_t B, float* __restrict__ tau,
-                                                       int* __restrict__ flag,
-                                                       float* __restrict__ Eu) {
+// Exact scores and the scan's values satisfy |approx - (exact - bp) unit| <= Eu + e_i, so
+// the sample's K-th best of (approx - e_i), kv, certifies a lower bound of the row's exact
+// K-th best score in real units: L = (kv - Eu) / unit + bp (unit is a power of two; the
+// relative 2^-21 covers the fp32 rounding of the subtraction and of + bp).  Rows with an
+// unusable bound get L = -inf.  Any lower bound works downstream -- e.g. the max of the
+// item shards' L over the ranks of a node (hnm_ncf_topk_begin_f32 / _finish_f32).
+__global__ __launch_bounds__(256) void cert_bound_kernel(const float* __restrict__ kth, int K,
+                                                         const float* __restrict__ Au,
+                                                         const CertParams* __restrict__ prm,
+                                                         const float* __restrict__ bp, int64_t B,
+                                                         float* __restrict__ lb,
+                                                         float* __restrict__ Eu) {
   const int64_t b = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (b >= B) return;
   const float unit = prm->unit;
   const float e = unit * (CERT_RHO * (prm->c0 + Au[b]) + prm->absb);
   if (Eu) Eu[b] = e;
   if (!kth) return;
+  float l = (kth[b * K + (K - 1)] - e) / unit + bp[0];
+  l -= fabsf(l) * 4.76837158203125e-07f;  // 2^-21
+  lb[b] = (!prm->bad && __builtin_isfinite(l) && __builtin_isfinite(e)) ? l : -__builtin_inff();
+}
+
+// Per row: the scan threshold in this call's scaled units from a lower bound L of the exact
+// K-th (real units): an item can be in the top-K only if exact >= L, i.e. approx + e_i >=
+// (L - bp) unit - Eu; minus a guard for the fp32 rounding of the test quantities (2^-18 of
+// the row's absolute score scale, 2^-20 relative).  Unusable rows: tau = +inf, flag = 1
+// (the exact fallback scan).
+__global__ __launch_bounds__(256) void cert_tau_kernel(const float* __restrict__ lb,
+                                                       const float* __restrict__ Au,
+                                                       const float* __restrict__ Cu,
+                                                       const float* __restrict__ Eu,
+                                                       const CertParams* __restrict__ prm,
+                                                       const float* __restrict__ bp, int64_t B,
+                                                       float* __restrict__ tau,
+                                                       int* __restrict__ flag) {
+  const int64_t b = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (b >= B) return;
+  const float unit = prm->unit;
   const float scale = unit * (prm->c0 + Au[b] + prm->Bmax + Cu[b] * prm->Dmax);
-  const float kv = kth[b * K + (K - 1)];
-  float tv = kv - 2.f * e - 3.814697265625e-06f * scale;  // 2^-18 of the score scale
-  tv -= fabsf(tv) * 9.5367431640625e-07f;                 // 2^-20
+  float tv = (lb[b] - bp[0]) * unit - Eu[b] - 3.814697265625e-06f * scale;  // 2^-18
+  tv -= fabsf(tv) * 9.5367431640625e-07f;                                     // 2^-20
   const bool ok = !prm->bad && __builtin_isfinite(tv) && __builtin_isfinite(scale);
   tau[b] = ok ? tv : __builtin_inff();
   flag[b] = ok ? 0 : 1;
@@ -897,7 +920,7 @@ __global__ __launch_bounds__(256, 2) void ncf_rescore_kernel(
     NcfTabs t, int mf, const float* __restrict__ W2, int h1, int h2, const float* __restrict__ b2,
     const float* __restrict__ wm, const float* __restrict__ bp, int64_t B,
     const int* __restrict__ flag, const int* __restrict__ cnt, const int32_t* __restrict__ buf,
-    int NP, int capp, int K, float* __restrict__ ov, int64_t* __restrict__ oi,
+    int NP, int capp, int K, int short_ok, float* __restrict__ ov, int64_t* __restrict__ oi,
     int32_t* __restrict__ ovf_rows, int32_t* __restrict__ ovf_cnt,
     unsigned long long* __restrict__ stats) {
   constexpr int KS = 32;
@@ -926,7 +949,9 @@ __global__ __launch_bounds__(256, 2) void ncf_rescore_kernel(
   if (!live) return;
   const int n = hnm_readlane_i(incl, 63);
   const bool over = __ballot(c > capp) != 0;
-  if (flag[b] || over || n < K) {
+  // fewer than K candidates: the row's bound came from another item shard (short_ok: the
+  // merge across shards completes the list) or the threshold is unusable -> fallback
+  if (flag[b] || over || (n < K && !short_ok)) {
     if (lane == 0) {
       ovf_rows[atomicAdd(ovf_cnt, 1)] = (int32_t)b;
       if (stats) {
@@ -1033,7 +1058,7 @@ __global__ void cert_unscale_kernel(float* __restrict__ a, float* __restrict__ e
 
 struct CertWs {
   CertParams* prm;
-  float *Au, *Cu, *Bi, *Di, *tau, *Eu, *b2s, *kthv, *pdense, *cdense, *part;
+  float *Au, *Cu, *Bi, *Di, *tau, *Eu, *b2s, *kthv, *lb, *pdense, *cdense, *part;
   int32_t* sidx;  // champion items
   int64_t* kthi;
   int *cnt, *flag;
@@ -1062,7 +1087,7 @@ struct CertShape {
 
 CertShape cert_shape(int64_t B, int64_t I, int K, int num_cus, int wg) {
   CertShape sh;
-  sh.gsz = hnm_cdiv(I, std::min<int64_t>(CERT_CHAMPIONS, I));
+  sh.gsz = std::max<int64_t>(CERT_GROUP_MIN, hnm_cdiv(I, CERT_CHAMPIONS));
   sh.nch = hnm_cdiv(I, sh.gsz);
   sh.part = scan_partition(I, hnm_cdiv(B, 128), num_cus, wg);
   // a row's candidates: items within the bound's margin of the champion sample's K-th --
@@ -1093,6 +1118,7 @@ size_t cert_carve(char* base, int64_t B, int64_t I, int K, int num_cus, int wg, 
   x.Eu = (float*)take(B * 4);
   x.b2s = (float*)take(32 * 4);
   x.kthv = (float*)take((size_t)B * K * 4);
+  x.lb = (float*)take((size_t)B * 4);
   x.pdense = (float*)take((size_t)CERT_PROXY_USERS * I * 4);
   x.cdense = (float*)take((size_t)B * sh.nch * 4);
   x.sidx = (int32_t*)take((size_t)sh.nch * 4);
@@ -1187,9 +1213,11 @@ size_t ncf_cert_bytes(int64_t B, int64_t I, int K, int num_cus, int wg) {
   return cert_carve(nullptr, B, I, K, num_cus, wg, nullptr);
 }
 
-hnm_status ncf_cert_topk(hnm_ctx* ctx, const hnm_ncf_weights* w, const NcfTabs& t, int64_t B,
-                         const int64_t* mptr, const int32_t* midx, int K, void* scratch,
-                         float* ov, int64_t* oi) {
+// Phase 1: per-call bound statistics and f16 copies, the champion sample, and every row's
+// certified lower bound of the exact K-th best score (real units) into lb[B].
+hnm_status ncf_cert_begin(hnm_ctx* ctx, const hnm_ncf_weights* w, const NcfTabs& t, int64_t B,
+                          const int64_t* mptr, const int32_t* midx, int K, void* scratch,
+                          float* lb) {
   const int64_t I = w->num_items;
   const int wg = ncf_cert_wg(ctx);
   const CertShape sh = cert_shape(B, I, K, ctx->num_cus, wg);
@@ -1198,64 +1226,86 @@ hnm_status ncf_cert_topk(hnm_ctx* ctx, const hnm_ncf_weights* w, const NcfTabs& 
   hnm_status st = cert_prepare(ctx, w, t, B, x);
   if (st) return st;
   const int64_t ublocks = hnm_cdiv(B, 128);
-  // 1. champion sample: the first rows' approx - e over all items -> the best item of each
-  // of nch groups -> every row's K-th best approx - e over those items -> tau (a lower bound
-  // of the exact K-th for any item subset; this one tends to hold the rows' best items)
-  {
-    const int64_t bp = std::min<int64_t>(CERT_PROXY_USERS, B);
-    ScanArgs a = scan_args(x, bp);
-    a.I = I;
-    a.dense = x.pdense;
-    a.ldo = I;
-    const int64_t np = std::min<int64_t>(3 * (int64_t)ctx->num_cus, hnm_cdiv(I, 4 * TILE));
-    a.ipp = hnm_cdiv(hnm_cdiv(I, np), TILE) * TILE;
-    a.NP = (int)hnm_cdiv(I, a.ipp);
-    launch_scan<SCAN_SAMPLE>(ctx, dim3((unsigned)a.NP, 1), a);
-    HNM_LAUNCH_CHECK();
-    hipLaunchKernelGGL(cert_champion_kernel, dim3((unsigned)hnm_cdiv(sh.nch, 4)), dim3(256), 0,
-                       ctx->stream, x.pdense, I, (int)bp, I, sh.gsz, sh.nch, x.sidx);
-    HNM_LAUNCH_CHECK();
-    ScanArgs c = scan_args(x, B);
-    c.I = sh.nch;
-    c.sidx = x.sidx;
-    c.dense = x.cdense;
-    c.ldo = sh.nch;
-    const Partition pc = scan_partition(sh.nch, ublocks, ctx->num_cus, wg);
-    c.ipp = pc.ipp;
-    c.NP = pc.np;
-    launch_scan<SCAN_SAMPLE>(ctx, dim3((unsigned)pc.np, (unsigned)ublocks), c);
-    HNM_LAUNCH_CHECK();
-    st = hnm_sample_kth(ctx, x.cdense, sh.nch, B, sh.nch, mptr, midx, K, 1, 1, x.sidx, x.kthv);
-    if (st) return st;
-    hipLaunchKernelGGL(cert_tau_kernel, dim3((unsigned)hnm_cdiv(B, 256)), dim3(256), 0,
-                       ctx->stream, x.kthv, K, x.Au, x.Cu, x.prm, B, x.tau, x.flag, x.Eu);
-    HNM_LAUNCH_CHECK();
-  }
-  // 2. main f16 scan: append items with approx + e >= tau_u to per-partition segments
-  {
-    ScanArgs a = scan_args(x, B);
-    a.I = I;
-    a.mptr = mptr;
-    a.midx = midx;
-    a.tau = x.tau;
-    a.cnt = x.cnt;
-    a.buf = x.buf;
-    a.capp = sh.capp;
-    a.ipp = sh.part.ipp;
-    a.NP = sh.part.np;
-    hnm_timer_begin(ctx, HNM_TIME_SCORE);
-    launch_scan<SCAN_THRESH>(ctx, dim3((unsigned)sh.part.np, (unsigned)ublocks), a);
-    hnm_timer_end(ctx, HNM_TIME_SCORE);
-    HNM_LAUNCH_CHECK();
-  }
-  // 3. exact fp32 re-scoring + top-K of the candidates; unusable rows -> queue
+  // champion sample: the first rows' approx - e over all items -> the best item of each of
+  // nch groups -> every row's K-th best approx - e over those items -> L (a lower bound of
+  // the exact K-th for any item subset; this one tends to hold the rows' best items)
+  const int64_t bp = std::min<int64_t>(CERT_PROXY_USERS, B);
+  ScanArgs a = scan_args(x, bp);
+  a.I = I;
+  a.dense = x.pdense;
+  a.ldo = I;
+  const int64_t np = std::min<int64_t>(3 * (int64_t)ctx->num_cus, hnm_cdiv(I, 4 * TILE));
+  a.ipp = hnm_cdiv(hnm_cdiv(I, np), TILE) * TILE;
+  a.NP = (int)hnm_cdiv(I, a.ipp);
+  launch_scan<SCAN_SAMPLE>(ctx, dim3((unsigned)a.NP, 1), a);
+  HNM_LAUNCH_CHECK();
+  hipLaunchKernelGGL(cert_champion_kernel, dim3((unsigned)hnm_cdiv(sh.nch, 4)), dim3(256), 0,
+                     ctx->stream, x.pdense, I, (int)bp, I, sh.gsz, sh.nch, x.sidx);
+  HNM_LAUNCH_CHECK();
+  ScanArgs c = scan_args(x, B);
+  c.I = sh.nch;
+  c.sidx = x.sidx;
+  c.dense = x.cdense;
+  c.ldo = sh.nch;
+  const Partition pc = scan_partition(sh.nch, ublocks, ctx->num_cus, wg);
+  c.ipp = pc.ipp;
+  c.NP = pc.np;
+  launch_scan<SCAN_SAMPLE>(ctx, dim3((unsigned)pc.np, (unsigned)ublocks), c);
+  HNM_LAUNCH_CHECK();
+  st = hnm_sample_kth(ctx, x.cdense, sh.nch, B, sh.nch, mptr, midx, K, 1, 1, x.sidx, x.kthv);
+  if (st) return st;
+  hipLaunchKernelGGL(cert_bound_kernel, dim3((unsigned)hnm_cdiv(B, 256)), dim3(256), 0,
+                     ctx->stream, x.kthv, K, x.Au, x.prm, w->bp, B, lb ? lb : x.lb, x.Eu);
+  HNM_LAUNCH_CHECK();
+  return HNM_OK;
+}
+
+// Phase 2: thresholds from the lower bounds lb (this call's, or the max over item shards),
+// the main f16 scan, exact fp32 re-scoring + top-K, the exact fallback for unusable rows.
+// short_ok: a row may keep fewer than K candidates (its bound came from another shard).
+hnm_status ncf_cert_finish(hnm_ctx* ctx, const hnm_ncf_weights* w, const NcfTabs& t, int64_t B,
+                           const int64_t* mptr, const int32_t* midx, int K, void* scratch,
+                           const float* lb, int short_ok, float* ov, int64_t* oi) {
+  const int64_t I = w->num_items;
+  const int wg = ncf_cert_wg(ctx);
+  const CertShape sh = cert_shape(B, I, K, ctx->num_cus, wg);
+  CertWs x;
+  cert_carve((char*)scratch, B, I, K, ctx->num_cus, wg, &x);
+  const int64_t ublocks = hnm_cdiv(B, 128);
+  hipLaunchKernelGGL(cert_tau_kernel, dim3((unsigned)hnm_cdiv(B, 256)), dim3(256), 0,
+                     ctx->stream, lb ? lb : x.lb, x.Au, x.Cu, x.Eu, x.prm, w->bp, B, x.tau, x.flag);
+  HNM_LAUNCH_CHECK();
+  // main f16 scan: append items with approx + e >= tau_u to per-partition segments
+  ScanArgs a = scan_args(x, B);
+  a.I = I;
+  a.mptr = mptr;
+  a.midx = midx;
+  a.tau = x.tau;
+  a.cnt = x.cnt;
+  a.buf = x.buf;
+  a.capp = sh.capp;
+  a.ipp = sh.part.ipp;
+  a.NP = sh.part.np;
+  hnm_timer_begin(ctx, HNM_TIME_SCORE);
+  launch_scan<SCAN_THRESH>(ctx, dim3((unsigned)sh.part.np, (unsigned)ublocks), a);
+  hnm_timer_end(ctx, HNM_TIME_SCORE);
+  HNM_LAUNCH_CHECK();
+  // exact fp32 re-scoring + top-K of the candidates; unusable rows -> queue
   hipLaunchKernelGGL(ncf_rescore_kernel, dim3((unsigned)hnm_cdiv(B, 4)), dim3(256), 0, ctx->stream,
                      t, w->mf, w->w2, w->h1, w->h2, w->b2, w->wp + w->mf, w->bp, B, x.flag, x.cnt,
-                     x.buf, sh.part.np, sh.capp, K, ov, oi, x.ovf_rows, x.ovf_cnt,
+                     x.buf, sh.part.np, sh.capp, K, short_ok, ov, oi, x.ovf_rows, x.ovf_cnt,
                      ctx->stats_on ? ctx->stats_dev : nullptr);
   HNM_LAUNCH_CHECK();
-  // 4. exact fp32 scan over all items for the queued rows (device-side row list)
+  // exact fp32 scan over all items for the queued rows (device-side row list)
   return ncf_list_rows(ctx, w, t, B, mptr, midx, K, x.ovf_rows, x.ovf_cnt, x.cv, x.ci, ov, oi);
+}
+
+hnm_status ncf_cert_topk(hnm_ctx* ctx, const hnm_ncf_weights* w, const NcfTabs& t, int64_t B,
+                         const int64_t* mptr, const int32_t* midx, int K, void* scratch,
+                         float* ov, int64_t* oi) {
+  hnm_status st = ncf_cert_begin(ctx, w, t, B, mptr, midx, K, scratch, nullptr);
+  if (st) return st;
+  return ncf_cert_finish(ctx, w, t, B, mptr, midx, K, scratch, nullptr, 0, ov, oi);
 }
 
 hnm_status ncf_cert_debug(hnm_ctx* ctx, const hnm_ncf_weights* w, const NcfTabs& t, int64_t B,
@@ -1265,8 +1315,8 @@ hnm_status ncf_cert_debug(hnm_ctx* ctx, const hnm_ncf_weights* w, const NcfTabs&
   cert_carve((char*)scratch, B, I, 1, ctx->num_cus, ncf_cert_wg(ctx), &x);
   hnm_status st = cert_prepare(ctx, w, t, B, x);
   if (st) return st;
-  hipLaunchKernelGGL(cert_tau_kernel, dim3((unsigned)hnm_cdiv(B, 256)), dim3(256), 0, ctx->stream,
-                     nullptr, 1, x.Au, x.Cu, x.prm, B, nullptr, nullptr, x.Eu);
+  hipLaunchKernelGGL(cert_bound_kernel, dim3((unsigned)hnm_cdiv(B, 256)), dim3(256), 0, ctx->stream,
+                     nullptr, 1, x.Au, x.prm, w->bp, B, nullptr, x.Eu);
   HNM_LAUNCH_CHECK();
   ScanArgs a = scan_args(x, B);
   a.I = I;

@@ -27,6 +27,15 @@ int ncf_cert_wg(const hnm_ctx* ctx);  // scan workgroups per CU of the selected 
 hnm_status ncf_cert_topk(hnm_ctx* ctx, const hnm_ncf_weights* w, const NcfTabs& t, int64_t B,
                          const int64_t* mptr, const int32_t* midx, int K, void* scratch,
                          float* ov, int64_t* oi);
+// The two phases of ncf_cert_topk: begin writes each row's certified lower bound of the
+// exact K-th best score (real units) to lb (nullptr: kept in the scratch); finish takes any
+// lower bounds (e.g. the max over item shards) and completes the top-K.
+hnm_status ncf_cert_begin(hnm_ctx* ctx, const hnm_ncf_weights* w, const NcfTabs& t, int64_t B,
+                          const int64_t* mptr, const int32_t* midx, int K, void* scratch,
+                          float* lb);
+hnm_status ncf_cert_finish(hnm_ctx* ctx, const hnm_ncf_weights* w, const NcfTabs& t, int64_t B,
+                           const int64_t* mptr, const int32_t* midx, int K, void* scratch,
+                           const float* lb, int short_ok, float* ov, int64_t* oi);
 // Diagnostics: the pre-filter's approximate scores (real units, bp excluded) for every
 // item and its per-user error bound E_u: |approx + bp - exact| <= E_u is what the path
 // relies on (tests check it on the full catalogue).

@@ -7,7 +7,12 @@ The reference has no distributed code; this is the MI355X design:
 * every rank brings its own batch of B users; one `all_gather` of the user ids (int64,
   B*8 bytes per rank) gives every rank the G*B users of the step;
 * each rank runs the fused score + top-K kernel over its item shard for all G*B users
-  (per-GPU work is the single-GPU work: weak scaling);
+  (per-GPU work is the single-GPU work: weak scaling).  With the certified pre-filter the
+  local scorer runs in two phases: `begin` gives every user's certified lower bound of the
+  k-th best score over the rank's items -- a lower bound of the GLOBAL k-th too -- one
+  `all_reduce(MAX)` of those G*B floats gives every rank the best bound of all shards, and
+  `finish` keeps only items that can be in the global top-k (candidates per user stay
+  ~constant as G grows instead of G x; rows may come back short, padded with -inf / -1);
 * one `all_to_all` returns to every rank the G candidate lists (k scores + global item
   ids) of ITS users (B*k*(4+8) bytes per rank pair: latency-bound on xGMI, so one
   collective, not a ring of per-layer exchanges);
@@ -61,7 +66,14 @@ class ItemShardedRecommender:
         ids = stage(user_ids.contiguous())
         all_ids = torch.empty(G * B, dtype=ids.dtype, device=ids.device)
         dist.all_gather_into_tensor(all_ids, ids, group=self.group)
-        v, i = self.local_topk(all_ids.to(dev))  # [G*B, k], shard-local ids
+        all_ids = all_ids.to(dev)
+        if hasattr(self.local_topk, "begin"):
+            # two-phase local scorer: global lower bounds of each user's k-th best score
+            lb = stage(self.local_topk.begin(all_ids).contiguous())
+            dist.all_reduce(lb, op=dist.ReduceOp.MAX, group=self.group)
+            v, i = self.local_topk.finish(all_ids, lb.to(dev))  # [G*B, k], shard-local ids
+        else:
+            v, i = self.local_topk(all_ids)  # [G*B, k], shard-local ids
         i = torch.where(i >= 0, i + self.item_offset, i)
         v, i = stage(v.contiguous().reshape(-1)), stage(i.contiguous().reshape(-1))
         rv, ri = torch.empty_like(v), torch.empty_like(i)
@@ -94,24 +106,56 @@ def hip_merge(cand_v: torch.Tensor, cand_i: torch.Tensor, k: int):
     return out_v, out_i
 
 
-def ncf_shard_topk(model, lo: int, hi: int, k: int) -> LocalTopK:
-    """Fused NCF score + top-K over item rows [lo, hi) of `model` (a NeuralCF on a GPU)."""
-    def run(user_ids: torch.Tensor):
-        w, keep = model._weights()
-        mf, h0 = model.mf_dim, model.mlp_dims[0] // 2
-        w.gmf_item = w.gmf_item + lo * mf * 4
-        w.mlp_item = w.mlp_item + lo * h0 * 4
-        w.num_items = hi - lo
+class ncf_shard_topk:
+    """Fused NCF score + top-K over item rows [lo, hi) of `model` (a NeuralCF on a GPU).
+
+    Called directly: one hnm_ncf_topk_f32.  `begin` / `finish`: the two phases of
+    hnm_ncf_topk_begin_f32 / _finish_f32 around a cross-shard bound exchange."""
+
+    def __init__(self, model, lo: int, hi: int, k: int):
+        self.model, self.lo, self.hi, self.k = model, lo, hi, k
+        self._open = None
+
+    def _args(self, user_ids):
+        w, keep = self.model._weights()
+        mf, h0 = self.model.mf_dim, self.model.mlp_dims[0] // 2
+        w.gmf_item = w.gmf_item + self.lo * mf * 4
+        w.mlp_item = w.mlp_item + self.lo * h0 * 4
+        w.num_items = self.hi - self.lo
         u = user_ids.to(torch.int64).contiguous()
-        kk = min(k, hi - lo)
-        out_v = torch.empty(u.numel(), kk, dtype=torch.float32, device=u.device)
-        out_i = torch.empty(u.numel(), kk, dtype=torch.int64, device=u.device)
-        c = _lib.ctx(u.device)
-        _lib.check(_lib.fn("hnm_ncf_topk_f32")(c, w, _lib.ptr(u), u.numel(), None, None, kk,
-                                               _lib.ptr(out_v), _lib.ptr(out_i)),
+        return w, keep, u, min(self.k, self.hi - self.lo)
+
+    def _out(self, u, kk):
+        return (torch.empty(u.numel(), kk, dtype=torch.float32, device=u.device),
+                torch.empty(u.numel(), kk, dtype=torch.int64, device=u.device))
+
+    def __call__(self, user_ids: torch.Tensor):
+        w, keep, u, kk = self._args(user_ids)
+        out_v, out_i = self._out(u, kk)
+        _lib.check(_lib.fn("hnm_ncf_topk_f32")(_lib.ctx(u.device), w, _lib.ptr(u), u.numel(), None,
+                                               None, kk, _lib.ptr(out_v), _lib.ptr(out_i)),
                    "hnm_ncf_topk_f32")
-        return _pad(out_v, out_i, k)
-    return run
+        return _pad(out_v, out_i, self.k)
+
+    def begin(self, user_ids: torch.Tensor) -> torch.Tensor:
+        w, keep, u, kk = self._args(user_ids)
+        lb = torch.empty(u.numel(), dtype=torch.float32, device=u.device)
+        _lib.check(_lib.fn("hnm_ncf_topk_begin_f32")(_lib.ctx(u.device), w, _lib.ptr(u), u.numel(),
+                                                     None, None, kk, _lib.ptr(lb)),
+                   "hnm_ncf_topk_begin_f32")
+        self._open = (w, keep, u, kk)  # finish must pass the same ids / tables
+        return lb
+
+    def finish(self, user_ids: torch.Tensor, lb: torch.Tensor):
+        w, keep, u, kk = self._open
+        self._open = None
+        lb = lb.to(torch.float32).contiguous()
+        out_v, out_i = self._out(u, kk)
+        _lib.check(_lib.fn("hnm_ncf_topk_finish_f32")(_lib.ctx(u.device), w, _lib.ptr(u), u.numel(),
+                                                      None, None, kk, _lib.ptr(lb), 1,
+                                                      _lib.ptr(out_v), _lib.ptr(out_i)),
+                   "hnm_ncf_topk_finish_f32")
+        return _pad(out_v, out_i, self.k)
 
 
 def dot_shard_topk(user_tab: torch.Tensor, item_tab: torch.Tensor, lo: int, hi: int,

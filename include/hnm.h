@@ -162,6 +162,21 @@ typedef struct {
 hnm_status hnm_ncf_topk_f32(hnm_ctx* ctx, const hnm_ncf_weights* w, const int64_t* user_ids,
                             int64_t B, const int64_t* mask_ptr, const int32_t* mask_idx,
                             int k, float* out_val, int64_t* out_idx);
+/* Two-phase hnm_ncf_topk_f32 for item-sharded serving (no reference counterpart: the
+ * reference is single-device).  begin: per-call tables + each row's
+ * certified lower bound of its exact k-th best score over this call's items, lower_bound[B]
+ * (real score units; -inf when unknown, e.g. with the pre-filter off).  The caller may
+ * replace the bounds by any valid lower bounds -- the max over the item shards of a node --
+ * then finish completes the fused top-k with them; short_ok = 1 lets a row keep fewer than
+ * k entries (padded with -inf / -1: another shard holds its better items).  Nothing else may
+ * use the ctx between begin and finish (HNM_EINVAL otherwise). */
+hnm_status hnm_ncf_topk_begin_f32(hnm_ctx* ctx, const hnm_ncf_weights* w,
+                                  const int64_t* user_ids, int64_t B, const int64_t* mask_ptr,
+                                  const int32_t* mask_idx, int k, float* lower_bound);
+hnm_status hnm_ncf_topk_finish_f32(hnm_ctx* ctx, const hnm_ncf_weights* w,
+                                   const int64_t* user_ids, int64_t B, const int64_t* mask_ptr,
+                                   const int32_t* mask_idx, int k, const float* lower_bound,
+                                   int short_ok, float* out_val, int64_t* out_idx);
 hnm_status hnm_ncf_scores_f32(hnm_ctx* ctx, const hnm_ncf_weights* w,
                               const int64_t* user_ids, int64_t B, float* out, int64_t ldo);
 /* Diagnostics of the certified pre-filter (no reference counterpart): approx[b, i] = the

@@ -55,10 +55,30 @@ def _worker(rank, world, port, q):
         v, i = O.topk(scores, K)
         return torch.from_numpy(v.astype(np.float32)), torch.from_numpy(i)
 
-    rec = S.ItemShardedRecommender(local_topk, _np_merge, K, lo, rank, world)
+    class TwoPhase:
+        """The certified scorer's protocol: begin -> lower bounds of each user's k-th best
+        score (here: the shard's exact k-th), finish -> only items >= the all-reduced bound
+        (short rows padded with -inf / -1)."""
+        def __call__(self, all_ids):
+            return local_topk(all_ids)
+
+        def begin(self, all_ids):
+            v, _ = local_topk(all_ids)
+            return v[:, K - 1].clone()
+
+        def finish(self, all_ids, lb):
+            v, i = local_topk(all_ids)
+            keep = v >= lb[:, None]
+            return torch.where(keep, v, torch.tensor(-np.inf)), torch.where(keep, i, torch.tensor(-1))
+
     users = torch.from_numpy(syn.user_batch(U, B, seed=10 + rank))
-    v, i = rec.recommend(users)
-    q.put((rank, users.numpy(), v.numpy(), i.numpy()))
+    out = []
+    for scorer in (local_topk, TwoPhase()):
+        rec = S.ItemShardedRecommender(scorer, _np_merge, K, lo, rank, world)
+        v, i = rec.recommend(users)
+        out.append((v.numpy(), i.numpy()))
+    assert np.array_equal(out[0][1], out[1][1]) and np.array_equal(out[0][0], out[1][0])
+    q.put((rank, users.numpy(), out[1][0], out[1][1]))
     dist.barrier()
     dist.destroy_process_group()
 
