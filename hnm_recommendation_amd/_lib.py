@@ -61,6 +61,10 @@ _SIGS = {
                                    C.c_int, _p, _i64, C.c_int]),
     "hnm_dot_topk_f32": (_i32, [_p, _p, _i64, _i64, _p, _i64, _p, _i64, _i64, C.c_int, _p, _p,
                                 _p, _p, _p, C.c_int, _p, _p]),
+    "hnm_dot_topk_begin_f32": (_i32, [_p, _p, _i64, _i64, _p, _i64, _p, _i64, _i64, C.c_int, _p,
+                                      _p, _p, _p, _p, C.c_int, _p]),
+    "hnm_dot_topk_finish_f32": (_i32, [_p, _p, _i64, _i64, _p, _i64, _p, _i64, _i64, C.c_int, _p,
+                                       _p, _p, _p, _p, C.c_int, _p, C.c_int, _p, _p]),
     "hnm_dot_prefilter_debug_f32": (_i32, [_p, _p, _i64, _i64, _p, _i64, _p, _i64, _i64, C.c_int,
                                            _p, _p, _p, _p, _i64, _p]),
     "hnm_dot_scores_f32": (_i32, [_p, _p, _i64, _i64, _p, _i64, _p, _i64, _i64, C.c_int, _p,

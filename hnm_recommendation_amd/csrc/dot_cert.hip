@@ -67,7 +67,7 @@ __device__ __forceinline__ float pow2_below_inv(float m) {  // 2^-e with m < 2^e
 
 struct DotCertWs {
   DParams* prm;
-  float *Nu, *Ni, *ubr, *ibs, *tau, *E, *kthv, *sdense, *part;
+  float *Nu, *Ni, *ubr, *ibs, *tau, *E, *kthv, *lb, *sdense, *part;
   int64_t* kthi;
   int *cnt, *flag;
   int32_t *buf, *ovf_cnt, *ovf_rows;
@@ -125,6 +125,7 @@ size_t dcert_carve(char* base, int64_t B, int64_t I, int d, int K, int num_cus, 
   x.tau = (float*)take(B * 4);
   x.E = (float*)take(B * 4);
   x.kthv = (float*)take((size_t)B * K * 4);
+  x.lb = (float*)take((size_t)B * 4);
   x.kthi = (int64_t*)take((size_t)B * K * 8);
   x.cnt = (int*)take((size_t)B * sh.part.np * 4);
   x.flag = (int*)take(B * 4);
@@ -473,25 +474,46 @@ __global__ __launch_bounds__(256, dcert_wg_per_cu(DP)) void dot16_scan_kernel(DS
   }
 }
 
-// E_u (scaled) and tau_u = (K-th best scaled approx of the sample) - 2 E_u - guard.
-__global__ __launch_bounds__(256) void dcert_tau_kernel(const float* __restrict__ kth, int K,
+// Per row: E = the bound (scaled units; exact = approx / s + ubr up to E / s for every item).
+// The sample's K-th best approx kv certifies a lower bound of the row's exact K-th best
+// score in real units, L = (kv - E) / s + ubr (s a power of two; 2^-21 relative covers the
+// fp32 rounding); unusable rows get L = -inf.  Any lower bound works downstream -- e.g. the
+// max of the item shards' L over the ranks of a node (hnm_dot_topk_begin_f32 / _finish_f32).
+__global__ __launch_bounds__(256) void dcert_bound_kernel(const float* __restrict__ kth, int K,
+                                                          const float* __restrict__ Nu,
+                                                          const float* __restrict__ ubr,
+                                                          const DParams* __restrict__ prm,
+                                                          int64_t B, float* __restrict__ lb,
+                                                          float* __restrict__ Eout) {
+  const int64_t b = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (b >= B) return;
+  const float s = prm->s;
+  const float nimax = __uint_as_float(prm->mx[DM_NI]), ibmax = __uint_as_float(prm->mx[DM_IB]);
+  const float E = s * (DCERT_RHO * Nu[b] * nimax + 2.4e-7f * (fabsf(ubr[b]) + ibmax)) + prm->absb;
+  if (Eout) Eout[b] = E / s;
+  if (!kth) return;
+  float l = (kth[b * K + (K - 1)] - E) / s + ubr[b];
+  l -= fabsf(l) * 4.76837158203125e-07f;  // 2^-21
+  lb[b] = (!prm->bad && __builtin_isfinite(l) && __builtin_isfinite(E)) ? l : -__builtin_inff();
+}
+
+// Per row: the scan threshold (scaled units) from a lower bound L of the exact K-th: an item
+// can be in the top-K only if exact >= L, i.e. approx >= (L - ubr) s - E; minus the guard for
+// the fp32 rounding of the test quantities (2^-18 of the row's score scale, 2^-20 relative).
+__global__ __launch_bounds__(256) void dcert_tau_kernel(const float* __restrict__ lb,
                                                         const float* __restrict__ Nu,
                                                         const float* __restrict__ ubr,
                                                         const DParams* __restrict__ prm,
                                                         int64_t B, float* __restrict__ tau,
-                                                        int* __restrict__ flag,
-                                                        float* __restrict__ Eout) {
+                                                        int* __restrict__ flag) {
   const int64_t b = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (b >= B) return;
   const float s = prm->s;
   const float nimax = __uint_as_float(prm->mx[DM_NI]), ibmax = __uint_as_float(prm->mx[DM_IB]);
   const float scale = s * (Nu[b] * nimax + fabsf(ubr[b]) + ibmax);
   const float E = s * (DCERT_RHO * Nu[b] * nimax + 2.4e-7f * (fabsf(ubr[b]) + ibmax)) + prm->absb;
-  if (Eout) Eout[b] = E / s;
-  if (!kth) return;
-  const float kv = kth[b * K + (K - 1)];
-  float tv = kv - 2.f * E - 3.814697265625e-06f * scale;  // 2^-18 of the row's score scale
-  tv -= fabsf(tv) * 9.5367431640625e-07f;                 // 2^-20
+  float tv = (lb[b] - ubr[b]) * s - E - 3.814697265625e-06f * scale;  // 2^-18
+  tv -= fabsf(tv) * 9.5367431640625e-07f;                               // 2^-20
   const bool ok = !prm->bad && __builtin_isfinite(tv) && __builtin_isfinite(scale);
   tau[b] = ok ? tv : __builtin_inff();
   flag[b] = ok ? 0 : 1;
@@ -505,7 +527,7 @@ template <int DP, bool BIAS>
 __global__ __launch_bounds__(256) void dcert_rescore_kernel(
     DotArgs a, const float* __restrict__ ubr, const int* __restrict__ flag,
     const int* __restrict__ cnt, const int32_t* __restrict__ buf, int NP, int capp, int K,
-    float* __restrict__ ov, int64_t* __restrict__ oi, int32_t* __restrict__ ovf_rows,
+    int short_ok, float* __restrict__ ov, int64_t* __restrict__ oi, int32_t* __restrict__ ovf_rows,
     int32_t* __restrict__ ovf_cnt, unsigned long long* __restrict__ stats) {
   __shared__ __attribute__((aligned(16))) float urow[4][DP];
   __shared__ int pref[4][DCERT_MAX_NP + 1];
@@ -532,7 +554,9 @@ __global__ __launch_bounds__(256) void dcert_rescore_kernel(
   __syncthreads();
   if (!live) return;
   const int n = hnm_readlane_i(incl, 63);
-  if (flag[b] || __ballot(c > capp) != 0 || n < K) {
+  // fewer than K candidates: the bound came from another item shard (short_ok: the merge
+  // across shards completes the row) or the threshold is unusable -> fallback
+  if (flag[b] || __ballot(c > capp) != 0 || (n < K && !short_ok)) {
     if (lane == 0) {
       ovf_rows[atomicAdd(ovf_cnt, 1)] = (int32_t)b;
       if (stats) {
@@ -674,34 +698,48 @@ size_t dot_cert_bytes(int64_t B, int64_t I, int d, int K, int num_cus) {
   return dcert_carve(nullptr, B, I, d, K, num_cus, nullptr);
 }
 
-hnm_status dot_cert_topk(hnm_ctx* ctx, const DotArgs& a, bool bias, void* scratch, float* ov,
-                         int64_t* oi) {
+// Phase 1: bound statistics, f16 copies, the sample pass and every row's certified lower
+// bound of its exact K-th best score (real units) into lb (nullptr: kept in the scratch).
+hnm_status dot_cert_begin(hnm_ctx* ctx, const DotArgs& a, bool bias, void* scratch, float* lb) {
   const DotCertShape sh = dcert_shape(a.B, a.I, a.d, a.K, ctx->num_cus);
   DotCertWs x;
   dcert_carve((char*)scratch, a.B, a.I, a.d, a.K, ctx->num_cus, &x);
   hnm_status st = dcert_prepare(ctx, a, sh, x);
   if (st) return st;
   const int64_t ublocks = hnm_cdiv(a.B, 128);
-  {  // 1. sample pass -> K-th best per row -> tau
-    DScanArgs s = dscan_args(x, a);
-    s.I = sh.Ns;
-    s.istride = sh.stride;
-    s.mptr = a.mptr;
-    s.midx = a.midx;
-    s.dense = x.sdense;
-    s.ldo = sh.spart.np * 32;
-    s.ipp = sh.spart.ipp;
-    s.NP = sh.spart.np;
-    launch_dscan<DSCAN_SAMPLE>(ctx, dim3((unsigned)sh.spart.np, (unsigned)ublocks), s, sh.DP, bias);
-    HNM_LAUNCH_CHECK();
-    const int64_t nmax_cols = (int64_t)sh.spart.np * 32;
-    st = hnm_sample_kth(ctx, x.sdense, nmax_cols, a.B, nmax_cols, nullptr, nullptr, a.K, 1, 1, nullptr, x.kthv);
-    if (st) return st;
-    hipLaunchKernelGGL(dcert_tau_kernel, dim3((unsigned)hnm_cdiv(a.B, 256)), dim3(256), 0,
-                       ctx->stream, x.kthv, a.K, x.Nu, x.ubr, x.prm, a.B, x.tau, x.flag, x.E);
-    HNM_LAUNCH_CHECK();
-  }
-  {  // 2. main f16 scan: append approx >= tau_u
+  DScanArgs s = dscan_args(x, a);
+  s.I = sh.Ns;
+  s.istride = sh.stride;
+  s.mptr = a.mptr;
+  s.midx = a.midx;
+  s.dense = x.sdense;
+  s.ldo = sh.spart.np * 32;
+  s.ipp = sh.spart.ipp;
+  s.NP = sh.spart.np;
+  launch_dscan<DSCAN_SAMPLE>(ctx, dim3((unsigned)sh.spart.np, (unsigned)ublocks), s, sh.DP, bias);
+  HNM_LAUNCH_CHECK();
+  const int64_t nmax_cols = (int64_t)sh.spart.np * 32;
+  st = hnm_sample_kth(ctx, x.sdense, nmax_cols, a.B, nmax_cols, nullptr, nullptr, a.K, 1, 1,
+                      nullptr, x.kthv);
+  if (st) return st;
+  hipLaunchKernelGGL(dcert_bound_kernel, dim3((unsigned)hnm_cdiv(a.B, 256)), dim3(256), 0,
+                     ctx->stream, x.kthv, a.K, x.Nu, x.ubr, x.prm, a.B, lb ? lb : x.lb, x.E);
+  HNM_LAUNCH_CHECK();
+  return HNM_OK;
+}
+
+// Phase 2: thresholds from lower bounds lb (this call's, or the max over item shards), the
+// main f16 scan, exact re-scoring + top-K, the exact LIST scan for unusable rows.
+hnm_status dot_cert_finish(hnm_ctx* ctx, const DotArgs& a, bool bias, void* scratch,
+                           const float* lb, int short_ok, float* ov, int64_t* oi) {
+  const DotCertShape sh = dcert_shape(a.B, a.I, a.d, a.K, ctx->num_cus);
+  DotCertWs x;
+  dcert_carve((char*)scratch, a.B, a.I, a.d, a.K, ctx->num_cus, &x);
+  const int64_t ublocks = hnm_cdiv(a.B, 128);
+  hipLaunchKernelGGL(dcert_tau_kernel, dim3((unsigned)hnm_cdiv(a.B, 256)), dim3(256), 0,
+                     ctx->stream, lb ? lb : x.lb, x.Nu, x.ubr, x.prm, a.B, x.tau, x.flag);
+  HNM_LAUNCH_CHECK();
+  {  // main f16 scan: append approx >= tau_u
     DScanArgs s = dscan_args(x, a);
     s.I = a.I;
     s.mptr = a.mptr;
@@ -717,12 +755,12 @@ hnm_status dot_cert_topk(hnm_ctx* ctx, const DotArgs& a, bool bias, void* scratc
     hnm_timer_end(ctx, HNM_TIME_SCORE);
     HNM_LAUNCH_CHECK();
   }
-  // 3. exact re-scoring + top-K; unusable rows queued
+  // exact re-scoring + top-K; unusable rows queued
   unsigned long long* stp = ctx->stats_on ? ctx->stats_dev : nullptr;
 #define HNM_RS(DPV, BV)                                                                         \
   hipLaunchKernelGGL((dcert_rescore_kernel<DPV, BV>), dim3((unsigned)hnm_cdiv(a.B, 4)), dim3(256), \
-                     0, ctx->stream, a, x.ubr, x.flag, x.cnt, x.buf, sh.part.np, sh.capp, a.K, ov, \
-                     oi, x.ovf_rows, x.ovf_cnt, stp);
+                     0, ctx->stream, a, x.ubr, x.flag, x.cnt, x.buf, sh.part.np, sh.capp, a.K,   \
+                     short_ok, ov, oi, x.ovf_rows, x.ovf_cnt, stp);
   if (sh.DP == 64) {
     if (bias) { HNM_RS(64, true) } else { HNM_RS(64, false) }
   } else {
@@ -730,11 +768,18 @@ hnm_status dot_cert_topk(hnm_ctx* ctx, const DotArgs& a, bool bias, void* scratc
   }
 #undef HNM_RS
   HNM_LAUNCH_CHECK();
-  // 4. exact LIST scan for the queued rows
+  // exact LIST scan for the queued rows
   DotArgs af = a;
   af.rows = x.ovf_rows;
   af.nrows = x.ovf_cnt;
   return dot_list_pass(ctx, af, bias, x.cv, x.ci, ov, oi);
+}
+
+hnm_status dot_cert_topk(hnm_ctx* ctx, const DotArgs& a, bool bias, void* scratch, float* ov,
+                         int64_t* oi) {
+  hnm_status st = dot_cert_begin(ctx, a, bias, scratch, nullptr);
+  if (st) return st;
+  return dot_cert_finish(ctx, a, bias, scratch, nullptr, 0, ov, oi);
 }
 
 hnm_status dot_cert_debug(hnm_ctx* ctx, const DotArgs& a, bool bias, void* scratch,
@@ -757,8 +802,8 @@ hnm_status dot_cert_debug(hnm_ctx* ctx, const DotArgs& a, bool bias, void* scrat
   hipLaunchKernelGGL(dcert_debug_out_kernel, dim3((unsigned)hnm_cdiv(a.B * a.I, 256)), dim3(256),
                      0, ctx->stream, approx, lda, a.B, a.I, x.ubr, x.prm);
   HNM_LAUNCH_CHECK();
-  hipLaunchKernelGGL(dcert_tau_kernel, dim3((unsigned)hnm_cdiv(a.B, 256)), dim3(256), 0,
-                     ctx->stream, nullptr, 1, x.Nu, x.ubr, x.prm, a.B, nullptr, nullptr, bound);
+  hipLaunchKernelGGL(dcert_bound_kernel, dim3((unsigned)hnm_cdiv(a.B, 256)), dim3(256), 0,
+                     ctx->stream, nullptr, 1, x.Nu, x.ubr, x.prm, a.B, nullptr, bound);
   HNM_LAUNCH_CHECK();
   return HNM_OK;
 }

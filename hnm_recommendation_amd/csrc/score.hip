@@ -591,6 +591,70 @@ extern "C" hnm_status hnm_dot_topk_f32(hnm_ctx* ctx, const float* user_tab, int6
   return dot_list_pass(ctx, af, bias, cv, ci, out_val, out_idx);
 }
 
+// Two-phase hnm_dot_topk_f32 for item-sharded serving (see hnm_ncf_topk_begin_f32).
+extern "C" hnm_status hnm_dot_topk_begin_f32(hnm_ctx* ctx, const float* user_tab,
+                                             int64_t num_users, int64_t ldu,
+                                             const int64_t* user_ids, int64_t B,
+                                             const float* item_tab, int64_t num_items,
+                                             int64_t ldi, int d, const float* user_bias,
+                                             const float* item_bias, const float* const_bias,
+                                             const int64_t* mask_ptr, const int32_t* mask_idx,
+                                             int k, float* lower_bound) {
+  hnm_status st = dot_validate(ctx, user_tab, num_users, ldu, user_ids, item_tab, num_items, ldi, d);
+  if (st) return st;
+  HNM_REQUIRE(k >= 1 && k <= 64 && lower_bound, HNM_EINVAL, "dot_topk_begin: bad argument");
+  HNM_REQUIRE(!ctx->pend.kind, HNM_EINVAL, "dot_topk_begin: a two-phase call is already open");
+  if (B <= 0) return HNM_OK;
+  const bool cert = ctx->prefilter && dot_cert_eligible(d, num_items, k);
+  if (cert) {
+    const bool bias = user_bias || item_bias || const_bias;
+    DotArgs a = dot_args(ctx, user_tab, num_users, ldu, user_ids, B, item_tab, num_items, ldi, d,
+                         user_bias, item_bias, const_bias, mask_ptr, mask_idx, k);
+    void* w;
+    st = hnm_workspace(ctx, dot_cert_bytes(B, num_items, d, k, ctx->num_cus), &w);
+    if (st) return st;
+    st = dot_cert_begin(ctx, a, bias, w, lower_bound);
+    if (st) return st;
+  } else {
+    st = hnm_fill_f32(ctx, lower_bound, B, -__builtin_inff());
+    if (st) return st;
+  }
+  ctx->pend = {cert ? HNM_PEND_DOT_CERT : HNM_PEND_DOT_EXACT, B, num_items, k, user_ids, item_tab};
+  return HNM_OK;
+}
+
+extern "C" hnm_status hnm_dot_topk_finish_f32(hnm_ctx* ctx, const float* user_tab,
+                                              int64_t num_users, int64_t ldu,
+                                              const int64_t* user_ids, int64_t B,
+                                              const float* item_tab, int64_t num_items,
+                                              int64_t ldi, int d, const float* user_bias,
+                                              const float* item_bias, const float* const_bias,
+                                              const int64_t* mask_ptr, const int32_t* mask_idx,
+                                              int k, const float* lower_bound, int short_ok,
+                                              float* out_val, int64_t* out_idx) {
+  HNM_REQUIRE(ctx && out_idx, HNM_EINVAL, "dot_topk_finish: bad argument");
+  if (B <= 0) return HNM_OK;
+  const int kind = ctx->pend.kind;
+  HNM_REQUIRE((kind == HNM_PEND_DOT_CERT || kind == HNM_PEND_DOT_EXACT) && ctx->pend.B == B &&
+                  ctx->pend.K == k && ctx->pend.I == num_items && ctx->pend.ids == user_ids &&
+                  ctx->pend.items == item_tab,
+              HNM_EINVAL, "dot_topk_finish: no matching hnm_dot_topk_begin_f32 on this ctx");
+  ctx->pend.kind = 0;
+  if (kind == HNM_PEND_DOT_EXACT)
+    return hnm_dot_topk_f32(ctx, user_tab, num_users, ldu, user_ids, B, item_tab, num_items, ldi,
+                            d, user_bias, item_bias, const_bias, mask_ptr, mask_idx, k, out_val,
+                            out_idx);
+  HNM_REQUIRE(lower_bound, HNM_EINVAL, "dot_topk_finish: lower_bound is NULL");
+  hnm_status st = dot_validate(ctx, user_tab, num_users, ldu, user_ids, item_tab, num_items, ldi, d);
+  if (st) return st;
+  HNM_REQUIRE(ctx->ws && ctx->ws_size >= dot_cert_bytes(B, num_items, d, k, ctx->num_cus),
+              HNM_EINVAL, "dot_topk_finish: the begin phase's workspace is gone");
+  const bool bias = user_bias || item_bias || const_bias;
+  DotArgs a = dot_args(ctx, user_tab, num_users, ldu, user_ids, B, item_tab, num_items, ldi, d,
+                       user_bias, item_bias, const_bias, mask_ptr, mask_idx, k);
+  return dot_cert_finish(ctx, a, bias, ctx->ws, lower_bound, short_ok, out_val, out_idx);
+}
+
 extern "C" hnm_status hnm_dot_scores_f32(hnm_ctx* ctx, const float* user_tab, int64_t num_users,
                                          int64_t ldu, const int64_t* user_ids, int64_t B,
                                          const float* item_tab, int64_t num_items, int64_t ldi,

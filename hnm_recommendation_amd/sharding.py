@@ -158,26 +158,52 @@ class ncf_shard_topk:
         return _pad(out_v, out_i, self.k)
 
 
-def dot_shard_topk(user_tab: torch.Tensor, item_tab: torch.Tensor, lo: int, hi: int,
-                   k: int) -> LocalTopK:
-    """Fused dot score + top-K (LightGCN / MF without biases) over item rows [lo, hi)."""
-    shard = item_tab[lo:hi]
+class dot_shard_topk:
+    """Fused dot score + top-K (LightGCN / MF without biases) over item rows [lo, hi).
 
-    def run(user_ids: torch.Tensor):
+    Called directly: one hnm_dot_topk_f32.  `begin` / `finish`: the two phases of
+    hnm_dot_topk_begin_f32 / _finish_f32 around a cross-shard bound exchange."""
+
+    def __init__(self, user_tab: torch.Tensor, item_tab: torch.Tensor, lo: int, hi: int, k: int):
+        self.user_tab, self.shard, self.k = user_tab, item_tab[lo:hi], k
+        self.n = hi - lo
+        self._open = None
+
+    def _common(self, u):
+        ut, sh = self.user_tab, self.shard
+        return (_lib.ptr(ut), ut.shape[0], ut.stride(0), _lib.ptr(u), u.numel(), _lib.ptr(sh),
+                self.n, sh.stride(0), ut.shape[1], None, None, None, None, None)
+
+    def _out(self, u, kk):
+        return (torch.empty(u.numel(), kk, dtype=torch.float32, device=u.device),
+                torch.empty(u.numel(), kk, dtype=torch.int64, device=u.device))
+
+    def __call__(self, user_ids: torch.Tensor):
         u = user_ids.to(torch.int64).contiguous()
-        d = user_tab.shape[1]
-        kk = min(k, hi - lo)
-        out_v = torch.empty(u.numel(), kk, dtype=torch.float32, device=u.device)
-        out_i = torch.empty(u.numel(), kk, dtype=torch.int64, device=u.device)
-        c = _lib.ctx(u.device)
-        _lib.check(_lib.fn("hnm_dot_topk_f32")(c, _lib.ptr(user_tab), user_tab.shape[0],
-                                               user_tab.stride(0), _lib.ptr(u), u.numel(),
-                                               _lib.ptr(shard), hi - lo, shard.stride(0), d,
-                                               None, None, None, None, None, kk,
-                                               _lib.ptr(out_v), _lib.ptr(out_i)),
-                   "hnm_dot_topk_f32")
-        return _pad(out_v, out_i, k)
-    return run
+        kk = min(self.k, self.n)
+        out_v, out_i = self._out(u, kk)
+        _lib.check(_lib.fn("hnm_dot_topk_f32")(_lib.ctx(u.device), *self._common(u), kk,
+                                               _lib.ptr(out_v), _lib.ptr(out_i)), "hnm_dot_topk_f32")
+        return _pad(out_v, out_i, self.k)
+
+    def begin(self, user_ids: torch.Tensor) -> torch.Tensor:
+        u = user_ids.to(torch.int64).contiguous()
+        kk = min(self.k, self.n)
+        lb = torch.empty(u.numel(), dtype=torch.float32, device=u.device)
+        _lib.check(_lib.fn("hnm_dot_topk_begin_f32")(_lib.ctx(u.device), *self._common(u), kk,
+                                                     _lib.ptr(lb)), "hnm_dot_topk_begin_f32")
+        self._open = (u, kk)  # finish must pass the same ids
+        return lb
+
+    def finish(self, user_ids: torch.Tensor, lb: torch.Tensor):
+        u, kk = self._open
+        self._open = None
+        lb = lb.to(torch.float32).contiguous()
+        out_v, out_i = self._out(u, kk)
+        _lib.check(_lib.fn("hnm_dot_topk_finish_f32")(_lib.ctx(u.device), *self._common(u), kk,
+                                                      _lib.ptr(lb), 1, _lib.ptr(out_v),
+                                                      _lib.ptr(out_i)), "hnm_dot_topk_finish_f32")
+        return _pad(out_v, out_i, self.k)
 
 
 def widedeep_shard_topk(model, lo: int, hi: int, k: int) -> LocalTopK:

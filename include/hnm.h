@@ -112,6 +112,21 @@ hnm_status hnm_dot_topk_f32(hnm_ctx* ctx, const float* user_tab, int64_t num_use
                             const float* const_bias, const int64_t* mask_ptr,
                             const int32_t* mask_idx, int k, float* out_val,
                             int64_t* out_idx);
+/* Two-phase hnm_dot_topk_f32 for item-sharded serving: as hnm_ncf_topk_begin_f32 /
+ * _finish_f32 (lower bounds in real score units, biases included). */
+hnm_status hnm_dot_topk_begin_f32(hnm_ctx* ctx, const float* user_tab, int64_t num_users,
+                                  int64_t ldu, const int64_t* user_ids, int64_t B,
+                                  const float* item_tab, int64_t num_items, int64_t ldi, int d,
+                                  const float* user_bias, const float* item_bias,
+                                  const float* const_bias, const int64_t* mask_ptr,
+                                  const int32_t* mask_idx, int k, float* lower_bound);
+hnm_status hnm_dot_topk_finish_f32(hnm_ctx* ctx, const float* user_tab, int64_t num_users,
+                                   int64_t ldu, const int64_t* user_ids, int64_t B,
+                                   const float* item_tab, int64_t num_items, int64_t ldi, int d,
+                                   const float* user_bias, const float* item_bias,
+                                   const float* const_bias, const int64_t* mask_ptr,
+                                   const int32_t* mask_idx, int k, const float* lower_bound,
+                                   int short_ok, float* out_val, int64_t* out_idx);
 /* Diagnostics of the certified f16 pre-filter of hnm_dot_topk_f32 (no reference
  * counterpart): approx[b, i] = the f16 scan's score (biases included), bound[b] = the
  * row's error bound; |approx - exact| <= bound for every item (tests check it). */

@@ -69,3 +69,25 @@ def test_two_rank_item_sharding_matches_single_gpu(tmp_path):
         sv, si = S.dot_shard_topk(gu, gi, 0, I, K)(users)
         assert np.array_equal(z["di"], si.cpu().numpy())
         assert np.array_equal(z["dv"].view(np.uint32), sv.cpu().numpy().view(np.uint32))
+
+
+def test_two_phase_contract():
+    """begin/finish with the call's own bounds == the one-shot top-K (bitwise); the ctx
+    refuses other work while a pair is open; finish without a matching begin raises."""
+    m = _model()
+    users = torch.from_numpy(syn.user_batch(U, 777, seed=3)).cuda()
+    gu = m.gmf_user_embedding.weight.detach().contiguous()
+    gi = m.gmf_item_embedding.weight.detach().contiguous()
+    for scorer in (S.ncf_shard_topk(m, 0, I, K), S.dot_shard_topk(gu, gi, 0, I, K)):
+        v1, i1 = scorer(users)
+        lb = scorer.begin(users)
+        assert torch.isfinite(lb).all()
+        assert (v1[:, K - 1] >= lb).all()  # a lower bound of the exact k-th best score
+        with pytest.raises(ValueError):
+            scorer(users)  # the ctx's workspace is held by the open pair
+        v2, i2 = scorer.finish(users, lb)
+        assert torch.equal(i1, i2) and torch.equal(v1.view(torch.int32), v2.view(torch.int32))
+    sc = S.dot_shard_topk(gu, gi, 0, I, K)
+    sc._open = (users.to(torch.int64).contiguous(), K)  # no begin on the ctx
+    with pytest.raises(ValueError):
+        sc.finish(users, torch.zeros(users.numel(), device="cuda"))
