@@ -305,6 +305,25 @@ hnm_status hnm_spmm_csr_f32(hnm_ctx* ctx, const hnm_spmm_plan* plan, int64_t N,
 hnm_status hnm_axpby_f32(hnm_ctx* ctx, int64_t n, float alpha, const float* x, float beta,
                          const float* y, float* out);
 
+/* ---- (f)4: ranking metrics over top-K lists (src/evaluation/metrics.py) ---------------
+ * Per user r: predicted ids pred[r*ldp + j], j < min(pred_len ? pred_len[r] : ldp, k);
+ * truth ids either CSR (truth_ptr[B+1] non-NULL: truth_idx[truth_ptr[r] .. truth_ptr[r+1]))
+ * or dense rows truth_idx[r*ldt + j], j < ldt, kept where truth_mask == NULL ||
+ * truth_mask[r*ldt + j] != 0 (the torchmetrics classes' `target[i][mask[i]]`).
+ * n_true = the kept-entry count (pass unique ids for evaluate_recommendations' set
+ * semantics, metrics.py:212).  inv_log2[i] = 1.0 / np.log2(i + 2), i < k (device, float64).
+ * per_user[r*4 + 0..3] = AP@k, Recall@k, Precision@k, NDCG@k: the reference's float64
+ * formulas in its summation order (evaluate_recommendations :218-247, MeanAveragePrecision
+ * :49-62, RecallAtK :95-100, PrecisionAtK :133-137, NDCGAtK :176-186), zero denominators
+ * -> 0.0.  sums[0..3] = sum over all rows of each metric, sums[4..7] = the same over rows
+ * with n_true > 0, sums[8] = that row count (deterministic fixed-order reduction).
+ * per_user, n_true and sums may each be NULL (not all three).  k <= 128. */
+hnm_status hnm_rank_metrics_f64(hnm_ctx* ctx, const int64_t* pred, int64_t B, int64_t ldp,
+                                const int64_t* pred_len, int k, const int64_t* truth_ptr,
+                                const int64_t* truth_idx, int64_t ldt, const uint8_t* truth_mask,
+                                const double* inv_log2, double* per_user, int64_t* n_true,
+                                double* sums);
+
 #ifdef __cplusplus
 }
 #endif

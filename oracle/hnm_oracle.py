@@ -251,3 +251,89 @@ def widedeep_predict_all_items(sd, user_ids, user_features=None, item_batch_size
         ef = None if user_features is None else np.repeat(user_features, e - s, axis=0)
         out.append(widedeep_forward(sd, eu, ei, ef).reshape(B, e - s))
     return np.concatenate(out, axis=1)
+
+
+# --------------------------------------------------------------------------- metrics
+def inv_log2_table(k):
+    """[1.0 / np.log2(i + 2) for i < k] -- the per-position NDCG discount exactly as the
+    reference forms each term (`metrics.py:180`, `:243`), one scalar np.log2 at a time."""
+    return np.asarray([1.0 / np.log2(i + 2) for i in range(k)], np.float64)
+
+
+def user_metrics(pred_items, true_items, k):
+    """One user's (AP@k, Recall@k, Precision@k, NDCG@k) with the float64 arithmetic and
+    loop order of `evaluate_recommendations` (`metrics.py:218-247`).  `true_items` is
+    the already de-duplicated truth collection (a set there, `:212`); `pred_items` the
+    first k predictions (`:223`).  Zero denominators -> 0.0 (the reference's guards;
+    its AP division by min(0, k) would raise -- callers check that case)."""
+    pred = list(pred_items)[:k]
+    ap, nh = 0.0, 0.0
+    for i, it in enumerate(pred):
+        if it in true_items:
+            nh += 1.0
+            ap += nh / (i + 1.0)
+    lim = min(len(true_items), k)
+    hits = sum(1 for it in pred if it in true_items)
+    dcg = 0.0
+    for i, it in enumerate(pred):
+        if it in true_items:
+            dcg += 1.0 / np.log2(i + 2)
+    idcg = sum(1.0 / np.log2(i + 2) for i in range(lim))
+    return (ap / lim if lim else 0.0,
+            hits / len(true_items) if len(true_items) else 0.0,
+            hits / len(pred) if pred else 0.0,
+            dcg / idcg if idcg > 0 else 0.0)
+
+
+def evaluate_recommendations(predictions, ground_truth, k=12):
+    """`evaluate_recommendations` (`metrics.py:193-255`): mean over the ground-truth users;
+    users without predictions contribute zeros (`:214-220`)."""
+    rows = []
+    for u in ground_truth:
+        t = set(ground_truth[u])
+        if u not in predictions:
+            rows.append((0.0, 0.0, 0.0, 0.0))
+            continue
+        if not t:
+            raise ZeroDivisionError("float division by zero")  # `:229` with an empty set
+        rows.append(user_metrics(predictions[u], t, k))
+    a = np.asarray(rows, np.float64).reshape(-1, 4)
+    return {f"map@{k}": np.mean(a[:, 0]), f"recall@{k}": np.mean(a[:, 1]),
+            f"precision@{k}": np.mean(a[:, 2]), f"ndcg@{k}": np.mean(a[:, 3])}, a
+
+
+def metric_classes(scores, target, mask, k=12):
+    """The torchmetrics classes MeanAveragePrecision / RecallAtK / PrecisionAtK / NDCGAtK
+    (`metrics.py:10-190`) over one `update(preds, target, mask)`: 2-D preds are scores, so
+    each row's top-min(k, n_items) is taken first (`:33-35`; tie order (score desc, index
+    asc) here); truth = `target[i][mask[i]]` with duplicates counted in len() (tensor
+    semantics, `:41-44`).  MAP and Precision average over every row, Recall and NDCG over
+    rows with non-empty truth (`:97`, `:170`).  Returns (dict of means, per-row [B, 4])."""
+    scores = np.asarray(scores)
+    kk = min(k, scores.shape[1])
+    _, top = topk(scores, kk)
+    B = scores.shape[0]
+    per = np.zeros((B, 4))
+    has = np.zeros(B, bool)
+    for b in range(B):
+        t = np.asarray(target[b])
+        if mask is not None:
+            t = t[np.asarray(mask[b], bool)]
+        tset = set(t.tolist())
+        n = len(t)
+        has[b] = n > 0
+        pred = top[b].tolist()
+        hits = [p in tset for p in pred]
+        ap, nh, dcg = 0.0, 0.0, 0.0
+        for i, h in enumerate(hits):
+            if h:
+                nh += 1.0
+                ap += nh / (i + 1.0)
+                dcg += 1.0 / np.log2(i + 2)
+        idcg = sum(1.0 / np.log2(i + 2) for i in range(min(n, k)))
+        per[b] = (ap / min(n, k) if n else 0.0, nh / n if n else 0.0,
+                  nh / len(pred) if pred else 0.0, dcg / idcg if idcg > 0 else 0.0)
+    mean = lambda col, sel: float(per[sel, col].mean()) if sel.any() else 0.0  # noqa: E731
+    allr = np.ones(B, bool)
+    return {"map": mean(0, allr), "recall": mean(1, has), "precision": mean(2, allr),
+            "ndcg": mean(3, has)}, per

@@ -256,6 +256,65 @@ def gen_mf(models):
          **with_prefix("sd/", sd))
 
 
+def dict_lists_to_arrays(d):
+    """{user: list} -> keys, ptr, idx (list order and duplicates kept)."""
+    keys = np.asarray(sorted(d), np.int64)
+    ptr, idx = [0], []
+    for k in keys.tolist():
+        idx.extend(int(x) for x in d[k])
+        ptr.append(len(idx))
+    return keys, np.asarray(ptr, np.int64), np.asarray(idx, np.int64)
+
+
+def gen_metrics():
+    """src/evaluation/metrics.py on synthetic top-K lists."""
+    from src.evaluation import metrics as M  # noqa: E402  (reference, stubs installed)
+    rng = np.random.Generator(np.random.PCG64(11))
+    I, U, k = 60, 300, 12
+    truth, preds = {}, {}
+    for u in range(U):
+        n = int(rng.integers(1, 40))  # duplicates inside a truth list (set semantics)
+        truth[u] = [int(x) for x in rng.integers(0, I, n)]
+        r = rng.random()
+        if r < 0.1:
+            continue  # user without predictions -> zeros
+        ln = k if r < 0.7 else int(rng.integers(0, k + 5))  # short / long / empty lists
+        preds[u] = [int(x) for x in rng.choice(I, ln, replace=r < 0.8)]  # some repeats
+    preds[U + 5] = [1, 2, 3]  # predicted user without truth: ignored
+    agg = M.evaluate_recommendations(preds, truth, k=k)
+    per_user = np.zeros((U, 4))
+    for u in range(U):
+        one = M.evaluate_recommendations({u: preds[u]} if u in preds else {}, {u: truth[u]}, k=k)
+        per_user[u] = [one[f"map@{k}"], one[f"recall@{k}"], one[f"precision@{k}"], one[f"ndcg@{k}"]]
+    pk, pp, pi = dict_lists_to_arrays(preds)
+    tk, tp, ti = dict_lists_to_arrays(truth)
+    # torchmetrics classes: preds are scores [B, n_items] (topk inside), dense target + mask
+    B, T = 96, 30
+    scores = rng.standard_normal((B, I)).astype(np.float32)
+    target = rng.integers(0, I, (B, T)).astype(np.int64)
+    mask = rng.random((B, T)) < 0.5
+    mask[3] = False  # a row with no valid truth
+    cls = {"map": M.MeanAveragePrecision, "recall": M.RecallAtK, "precision": M.PrecisionAtK,
+           "ndcg": M.NDCGAtK}
+    out = {}
+    st, tt, mt = torch.from_numpy(scores), torch.from_numpy(target), torch.from_numpy(mask)
+    for name, C in cls.items():
+        m = C(k=k)
+        m.update(st, tt, mt)
+        out[f"cls_{name}"] = np.float64(m.compute())
+        rows = []
+        for b in range(B):
+            m1 = C(k=k)
+            m1.update(st[b:b + 1], tt[b:b + 1], mt[b:b + 1])
+            rows.append(float(m1.compute()))
+        out[f"cls_{name}_rows"] = np.asarray(rows, np.float64)
+    save("metrics_small.npz", k=k, I=I, U=U, pred_keys=pk, pred_ptr=pp, pred_idx=pi,
+         truth_keys=tk, truth_ptr=tp, truth_idx=ti, per_user=per_user,
+         agg=np.asarray([agg[f"map@{k}"], agg[f"recall@{k}"], agg[f"precision@{k}"],
+                         agg[f"ndcg@{k}"]]),
+         scores=scores, target=target, mask=mask, **out)
+
+
 if __name__ == "__main__":
     torch.manual_seed(0)
     torch.set_num_threads(8)
@@ -264,3 +323,4 @@ if __name__ == "__main__":
     gen_lightgcn(models)
     gen_widedeep(models)
     gen_mf(models)
+    gen_metrics()

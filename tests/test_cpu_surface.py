@@ -91,13 +91,54 @@ def test_filter_csr_host_logic():
         filter_csr(ids, {7: {10}}, 10, torch.device("cpu"))
 
 
-def test_recommendation_metrics_formulas():
-    m = RecommendationMetrics(top_k=3)
-    m.update(torch.tensor([[1, 2, 3], [4, 5, 6]]), [[2, 9], [7]])
-    r = m.compute()
-    # user 0: hit at rank 2 -> AP = (1/2)/min(2,3) = 0.25; user 1: 0
-    assert abs(float(r["map_at_k"]) - 0.125) < 1e-6
-    assert abs(float(r["recall_at_k"]) - 0.25) < 1e-6
-    assert abs(float(r["precision_at_k"]) - (1 / 3) / 2) < 1e-6
-    idcg = 1 + 1 / np.log2(3)
-    assert abs(float(r["ndcg_at_k"]) - (1 / np.log2(3)) / idcg / 2) < 1e-6
+# ------------------------------------------------------------------ serving / checkpoints
+def test_checkpoint_dispatch_on_cpu(tmp_path):
+    """serve.py:216-258: directory-name substring -> class, hparams override, state load
+    (module construction and state loading need no GPU; scoring does)."""
+    from hnm_recommendation_amd.serving import create_model_from_checkpoint, load_checkpoint
+    from hnm_recommendation_amd import synthetic as syn
+    U, I = 50, 40
+    cases = [("exp1/neural_cf", NeuralCF(U, I)), ("wide_deep_run", WideDeep(U, I)),
+             ("matrix_factorization", MatrixFactorization(U, I)),
+             ("lightgcn_best", LightGCN(U, I))]
+    graph = (torch.from_numpy(syn.bipartite_edge_index(U, I, 200, seed=2)), None)
+    for name, src in cases:
+        with torch.no_grad():
+            for p in src.parameters():
+                p.copy_(torch.randn_like(p))
+        path = tmp_path / (name.replace("/", "_") + ".ckpt")
+        hp = dict(src.hparams)
+        hp["num_users"], hp["num_items"] = 1, 1  # overridden by the server (serve.py:233-234)
+        torch.save({"state_dict": src.state_dict(), "hyper_parameters": hp}, path)
+        m = create_model_from_checkpoint(name, load_checkpoint(str(path)), U, I, "cpu", graph)
+        assert type(m) is type(src) and not m.training
+        for (ka, a), (kb, b) in zip(m.state_dict().items(), src.state_dict().items()):
+            assert ka == kb and torch.equal(a, b)
+    ck = {"state_dict": LightGCN(U, I).state_dict(), "hyper_parameters": {}}
+    assert create_model_from_checkpoint("lightgcn", ck, U, I, "cpu", None) is None  # no graph
+    assert create_model_from_checkpoint("popularity", ck, U, I, "cpu") is None
+    assert create_model_from_checkpoint("neural_cf", ck, U, I, "cpu") is None  # wrong keys
+
+
+def test_recommender_host_logic():
+    from hnm_recommendation_amd.serving import Recommender
+    srv = Recommender(100, 50, device="cpu", customer_index={"abc": 7})
+    assert srv.get_user_idx(5) == 5 and srv.get_user_idx(100) is None
+    assert srv.get_user_idx("abc") == 7 and srv.get_user_idx("zzz") is None
+    with pytest.raises(ValueError):
+        srv._get_best_model()
+    srv.add_model("neural_cf", NeuralCF(100, 50), {"test_map": 0.1})
+    srv.add_model("lightgcn", LightGCN(100, 50), {"test_map": 0.3})
+    srv.add_model("mf", MatrixFactorization(100, 50))
+    assert srv._get_best_model() == "lightgcn"
+    with pytest.raises(ValueError):
+        srv.get_recommendations(1, model_name="nope")
+    with pytest.raises(RuntimeError):  # scoring needs the GPU: no CPU path
+        srv.get_recommendations(1, model_name="mf")
+
+
+def test_metrics_need_gpu():
+    from hnm_recommendation_amd import evaluation as EV
+    with pytest.raises(RuntimeError):
+        EV.rank_metrics(torch.zeros(2, 12, dtype=torch.int64), 12,
+                        truth=torch.zeros(2, 3, dtype=torch.int64))

@@ -85,3 +85,27 @@ def test_oracle_topk_tie_order_is_index_ascending():
     assert i.tolist() == [[1, 2, 4, 3]]
     m = O.apply_filter(s, [7], {7: {1, 2, 4, 3, 0}})
     assert O.topk(m, 2)[1].tolist() == [[0, 1]]  # all -inf: lowest indices first
+
+
+def _lists(keys, ptr, idx):
+    return {int(k): idx[ptr[j]:ptr[j + 1]].tolist() for j, k in enumerate(keys)}
+
+
+def test_metrics_match_reference():
+    """metrics.py (evaluate_recommendations + the four Metric classes) on the fixture."""
+    g = load_golden("metrics_small.npz")
+    k = int(g["k"])
+    preds = _lists(g["pred_keys"], g["pred_ptr"], g["pred_idx"])
+    truth = _lists(g["truth_keys"], g["truth_ptr"], g["truth_idx"])
+    agg, per = O.evaluate_recommendations(preds, truth, k)
+    assert np.array_equal(per, g["per_user"])  # bitwise: same float64 ops, same order
+    np.testing.assert_allclose([agg[f"map@{k}"], agg[f"recall@{k}"], agg[f"precision@{k}"],
+                                agg[f"ndcg@{k}"]], g["agg"], rtol=1e-13)
+    with pytest.raises(ZeroDivisionError):
+        O.evaluate_recommendations({0: [1]}, {0: []}, k)
+    means, rows = O.metric_classes(g["scores"], g["target"], g["mask"], k)
+    for j, name in enumerate(("map", "recall", "precision", "ndcg")):
+        # the reference accumulates in float32 tensors (metrics.py:16): 1e-6 relative
+        np.testing.assert_allclose(means[name], g[f"cls_{name}"], rtol=2e-6)
+        np.testing.assert_array_equal(rows[:, j].astype(np.float32),
+                                      g[f"cls_{name}_rows"].astype(np.float32))
