@@ -129,7 +129,9 @@ def build_workload(name, rank, world, device, batch, exact=False):
         local = S.widedeep_shard_topk(m, lo, hi, K)
         per_launch = 328450.0 * batch * world * (hi - lo)   # 328,450 FLOP / pair
         info = {"model": "WideDeep", "embedding_dim": 64, "deep_layers": [512, 256, 128]}
-        bound, kernel = "mfma", "widedeep_score_kernel"
+        bound, kernel = "mfma", ("widedeep_score_kernel" if exact else "wdc_scan_kernel")
+        info["scan"] = ("exact fp32" if exact else
+                        "certified split-f16 (3 f16 MFMA passes) pre-filter + exact fp32 re-scoring")
         cpu = None
     elif name == "mf":
         sd = syn.mf_state_dict(U, I, 64, seed=0)
@@ -245,7 +247,7 @@ def main():
 
     users_total = B * world * args.steps
     value = users_total / elapsed
-    f16 = kernel in ("ncf16_scan_kernel", "dot16_scan_kernel")
+    f16 = kernel in ("ncf16_scan_kernel", "dot16_scan_kernel", "wdc_scan_kernel")
     if bound == "hbm":
         achieved = per_launch / (avg_kernel_ms * 1e-3) / 1e9
         peak, punit = HBM_PEAK_GBS, "GB/s"
@@ -263,7 +265,8 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "f16+f32" if (f16 or bound == "hbm") and not args.exact else "f32",
+        "dtype": ("f32" if args.exact or not (f16 or bound == "hbm") else
+                  "f16x3+f32" if kernel == "wdc_scan_kernel" else "f16+f32"),
         "data": "synthetic (PCG64 weights with reference init distributions; H&M shape)",
         "config": {"workload": f"{args.workload}: BASELINE configs[1] NeuralCF dim=64, full H&M "
                                f"shape, batch={B} users/rank, K=12" if args.workload == "ncf"

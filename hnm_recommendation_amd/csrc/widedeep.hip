@@ -140,6 +140,111 @@ __global__ void wd_user_const(hnm_widedeep_weights w, const int64_t* __restrict_
   cu[b] = v;
 }
 
+// One wave's exact fp32 deep score for its user against a 32-item tile (the per-pair
+// arithmetic of widedeep_score_kernel, shared with the certified path's re-scoring kernel
+// so both produce bitwise the same values).  prow / qrow: the user's / lane item's
+// pair-permuted layer-1 rows offset by h * K1P / 2 (LDS or global); returns the lane's
+// half of w_d' . relu(layer 3) (the caller adds the other half with one shfl_xor 32).
+template <int RB2, int OB>
+__device__ __forceinline__ float wd_tile_fp32(const float* __restrict__ prow,
+                                              const float* __restrict__ qrow, int S4,
+                                              const float4* __restrict__ W2f,
+                                              const float4* __restrict__ W3f,
+                                              const float* __restrict__ cb2,
+                                              const float* __restrict__ cb3,
+                                              const float* __restrict__ cwd, int lane, int h) {
+  constexpr int G2 = RB2 < 4 ? RB2 : 4;  // layer-2 row blocks per pass
+  f32x16 acc3[OB > 0 ? OB : 1];
+  float fin = 0.f;
+#pragma unroll
+  for (int ob = 0; ob < (OB > 0 ? OB : 1); ++ob)
+    acc3[ob] = f32x16{0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll
+  for (int g = 0; g < RB2 / G2; ++g) {
+    f32x16 acc2[G2];
+#pragma unroll
+    for (int gi = 0; gi < G2; ++gi)
+      acc2[gi] = f32x16{0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    // ---- layer 2 for row blocks g*G2 .. g*G2+G2-1
+    float4 af[G2];
+#pragma unroll
+    for (int gi = 0; gi < G2; ++gi) af[gi] = W2f[((int64_t)(g * G2 + gi) * S4 + 0) * 64 + lane];
+    for (int s4 = 0; s4 < S4; ++s4) {
+      float4 an[G2];
+      const int sn = s4 + 1 < S4 ? s4 + 1 : s4;
+#pragma unroll
+      for (int gi = 0; gi < G2; ++gi) an[gi] = W2f[((int64_t)(g * G2 + gi) * S4 + sn) * 64 + lane];
+      const float4 pv = *reinterpret_cast<const float4*>(prow + 4 * s4);
+      const float4 qv = *reinterpret_cast<const float4*>(qrow + 4 * s4);
+      const float x0 = fmaxf(pv.x + qv.x, 0.f), x1 = fmaxf(pv.y + qv.y, 0.f);
+      const float x2 = fmaxf(pv.z + qv.z, 0.f), x3 = fmaxf(pv.w + qv.w, 0.f);
+#pragma unroll
+      for (int gi = 0; gi < G2; ++gi) acc2[gi] = mfma32x32x2(af[gi].x, x0, acc2[gi]);
+#pragma unroll
+      for (int gi = 0; gi < G2; ++gi) acc2[gi] = mfma32x32x2(af[gi].y, x1, acc2[gi]);
+#pragma unroll
+      for (int gi = 0; gi < G2; ++gi) acc2[gi] = mfma32x32x2(af[gi].z, x2, acc2[gi]);
+#pragma unroll
+      for (int gi = 0; gi < G2; ++gi) acc2[gi] = mfma32x32x2(af[gi].w, x3, acc2[gi]);
+#pragma unroll
+      for (int gi = 0; gi < G2; ++gi) af[gi] = an[gi];
+    }
+    // ---- relu(D2 + b2') feeds layer 3 (or the final dot for a two-layer tower).
+    // Layer-3 A fragments are streamed one (gi, r4) step ahead; the scheduling barrier
+    // keeps hipcc from hoisting all of them (which spills).
+    float4 a3c[OB > 0 ? OB : 1], a3n[OB > 0 ? OB : 1];
+    if (OB > 0) {
+#pragma unroll
+      for (int ob = 0; ob < (OB > 0 ? OB : 1); ++ob)
+        a3c[ob] = W3f[((int64_t)(ob * RB2 + g * G2) * 4 + 0) * 64 + lane];
+    }
+#pragma unroll
+    for (int gi = 0; gi < G2; ++gi) {
+      const int rb = g * G2 + gi;
+      float hv[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) hv[r] = fmaxf(acc2[gi][r] + cb2[rb * 32 + mfma32_row(r, h)], 0.f);
+      if (OB > 0) {
+#pragma unroll
+        for (int r4 = 0; r4 < 4; ++r4) {
+          const int st = gi * 4 + r4;
+          if (st + 1 < G2 * 4) {
+            const int gn = (st + 1) >> 2, rn = (st + 1) & 3;
+#pragma unroll
+            for (int ob = 0; ob < (OB > 0 ? OB : 1); ++ob)
+              a3n[ob] = W3f[((int64_t)(ob * RB2 + g * G2 + gn) * 4 + rn) * 64 + lane];
+          }
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int ob = 0; ob < (OB > 0 ? OB : 1); ++ob) {
+            acc3[ob] = mfma32x32x2(a3c[ob].x, hv[4 * r4 + 0], acc3[ob]);
+            acc3[ob] = mfma32x32x2(a3c[ob].y, hv[4 * r4 + 1], acc3[ob]);
+            acc3[ob] = mfma32x32x2(a3c[ob].z, hv[4 * r4 + 2], acc3[ob]);
+            acc3[ob] = mfma32x32x2(a3c[ob].w, hv[4 * r4 + 3], acc3[ob]);
+          }
+#pragma unroll
+          for (int ob = 0; ob < (OB > 0 ? OB : 1); ++ob) a3c[ob] = a3n[ob];
+        }
+      } else {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) fin = fmaf(hv[r], cwd[rb * 32 + mfma32_row(r, h)], fin);
+      }
+    }
+  }
+  if (OB > 0) {
+#pragma unroll
+    for (int ob = 0; ob < (OB > 0 ? OB : 1); ++ob) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int o = ob * 32 + mfma32_row(r, h);
+        fin = fmaf(fmaxf(acc3[ob][r] + cb3[o], 0.f), cwd[o], fin);
+      }
+    }
+  }
+  return fin;
+}
+
 // ------------------------------------------------------------------ main kernel
 template <int RB2, int OB, bool DENSE>
 __global__ __launch_bounds__(256, (RB2 >= 8 || OB >= 4) ? 1 : 2) void widedeep_score_kernel(
@@ -149,8 +254,8 @@ __global__ __launch_bounds__(256, (RB2 >= 8 || OB >= 4) ? 1 : 2) void widedeep_s
     const float* __restrict__ wdp, const float* __restrict__ cu, const float* __restrict__ wI,
     int64_t B, int64_t I, int64_t ipp, const int64_t* __restrict__ mptr,
     const int32_t* __restrict__ midx, int K, float* __restrict__ cand_v,
-    int32_t* __restrict__ cand_i, int NP, float* __restrict__ dense, int64_t ldo) {
-  constexpr int G2 = RB2 < 4 ? RB2 : 4;  // layer-2 row blocks per pass
+    int32_t* __restrict__ cand_i, int NP, float* __restrict__ dense, int64_t ldo,
+    const int32_t* __restrict__ rows) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int KS1 = K1P / 2, S4 = K1P / 8, QRS = K1P + 4;
   float* qs = smem;                    // [32][QRS]
@@ -160,7 +265,9 @@ __global__ __launch_bounds__(256, (RB2 >= 8 || OB >= 4) ? 1 : 2) void widedeep_s
   float* cwd = cb3 + OB * 32;          // [32*max(OB,RB2)] w_d'
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5, j = lane & 31;
-  const int64_t b = (int64_t)blockIdx.x * 4 + wave;
+  // rows (the certified path's fallback): slot -> batch row; outputs stay at the slot
+  const int64_t slot = (int64_t)blockIdx.x * 4 + wave;
+  const int64_t b = rows ? (slot < B ? (int64_t)rows[slot] : 0) : slot;
   const int p = blockIdx.y;
   const int64_t part_start = (int64_t)p * ipp;
   const int64_t part_end = std::min<int64_t>(I, part_start + ipp);
@@ -169,13 +276,13 @@ __global__ __launch_bounds__(256, (RB2 >= 8 || OB >= 4) ? 1 : 2) void widedeep_s
     const int r = e / (K1P / 4), c = e % (K1P / 4);
     const int64_t bb = (int64_t)blockIdx.x * 4 + r;
     float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (bb < B) v = *reinterpret_cast<const float4*>(Pu + bb * K1P + 4 * c);
+    if (bb < B) v = *reinterpret_cast<const float4*>(Pu + (rows ? (int64_t)rows[bb] : bb) * K1P + 4 * c);
     *reinterpret_cast<float4*>(&ps[r * K1P + 4 * c]) = v;
   }
   for (int e = tid; e < RB2 * 32; e += 256) cb2[e] = b2p[e];
   for (int e = tid; e < OB * 32; e += 256) cb3[e] = b3p[e];
   for (int e = tid; e < (OB > 0 ? OB : RB2) * 32; e += 256) cwd[e] = wdp[e];
-  const bool active = b < B;
+  const bool active = slot < B;
   const float cub = active ? cu[b] : 0.f;
   WaveTopK<1> L;
   L.init();
@@ -208,94 +315,7 @@ __global__ __launch_bounds__(256, (RB2 >= 8 || OB >= 4) ? 1 : 2) void widedeep_s
 
     const float* prow = &ps[wave * K1P + h * KS1];
     const float* qrow = &qs[j * QRS + h * KS1];
-    f32x16 acc3[OB > 0 ? OB : 1];
-    float fin = 0.f;
-#pragma unroll
-    for (int ob = 0; ob < (OB > 0 ? OB : 1); ++ob)
-      acc3[ob] = f32x16{0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-
-#pragma unroll
-    for (int g = 0; g < RB2 / G2; ++g) {
-      f32x16 acc2[G2];
-#pragma unroll
-      for (int gi = 0; gi < G2; ++gi)
-        acc2[gi] = f32x16{0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-      // ---- layer 2 for row blocks g*G2 .. g*G2+G2-1
-      float4 af[G2];
-#pragma unroll
-      for (int gi = 0; gi < G2; ++gi) af[gi] = W2f[((int64_t)(g * G2 + gi) * S4 + 0) * 64 + lane];
-      for (int s4 = 0; s4 < S4; ++s4) {
-        float4 an[G2];
-        const int sn = s4 + 1 < S4 ? s4 + 1 : s4;
-#pragma unroll
-        for (int gi = 0; gi < G2; ++gi) an[gi] = W2f[((int64_t)(g * G2 + gi) * S4 + sn) * 64 + lane];
-        const float4 pv = *reinterpret_cast<const float4*>(prow + 4 * s4);
-        const float4 qv = *reinterpret_cast<const float4*>(qrow + 4 * s4);
-        const float x0 = fmaxf(pv.x + qv.x, 0.f), x1 = fmaxf(pv.y + qv.y, 0.f);
-        const float x2 = fmaxf(pv.z + qv.z, 0.f), x3 = fmaxf(pv.w + qv.w, 0.f);
-#pragma unroll
-        for (int gi = 0; gi < G2; ++gi) acc2[gi] = mfma32x32x2(af[gi].x, x0, acc2[gi]);
-#pragma unroll
-        for (int gi = 0; gi < G2; ++gi) acc2[gi] = mfma32x32x2(af[gi].y, x1, acc2[gi]);
-#pragma unroll
-        for (int gi = 0; gi < G2; ++gi) acc2[gi] = mfma32x32x2(af[gi].z, x2, acc2[gi]);
-#pragma unroll
-        for (int gi = 0; gi < G2; ++gi) acc2[gi] = mfma32x32x2(af[gi].w, x3, acc2[gi]);
-#pragma unroll
-        for (int gi = 0; gi < G2; ++gi) af[gi] = an[gi];
-      }
-      // ---- relu(D2 + b2') feeds layer 3 (or the final dot for a two-layer tower).
-      // Layer-3 A fragments are streamed one (gi, r4) step ahead; the scheduling barrier
-      // keeps hipcc from hoisting all of them (which spills).
-      float4 a3c[OB > 0 ? OB : 1], a3n[OB > 0 ? OB : 1];
-      if (OB > 0) {
-#pragma unroll
-        for (int ob = 0; ob < (OB > 0 ? OB : 1); ++ob)
-          a3c[ob] = W3f[((int64_t)(ob * RB2 + g * G2) * 4 + 0) * 64 + lane];
-      }
-#pragma unroll
-      for (int gi = 0; gi < G2; ++gi) {
-        const int rb = g * G2 + gi;
-        float hv[16];
-#pragma unroll
-        for (int r = 0; r < 16; ++r) hv[r] = fmaxf(acc2[gi][r] + cb2[rb * 32 + mfma32_row(r, h)], 0.f);
-        if (OB > 0) {
-#pragma unroll
-          for (int r4 = 0; r4 < 4; ++r4) {
-            const int st = gi * 4 + r4;
-            if (st + 1 < G2 * 4) {
-              const int gn = (st + 1) >> 2, rn = (st + 1) & 3;
-#pragma unroll
-              for (int ob = 0; ob < (OB > 0 ? OB : 1); ++ob)
-                a3n[ob] = W3f[((int64_t)(ob * RB2 + g * G2 + gn) * 4 + rn) * 64 + lane];
-            }
-            __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (int ob = 0; ob < (OB > 0 ? OB : 1); ++ob) {
-              acc3[ob] = mfma32x32x2(a3c[ob].x, hv[4 * r4 + 0], acc3[ob]);
-              acc3[ob] = mfma32x32x2(a3c[ob].y, hv[4 * r4 + 1], acc3[ob]);
-              acc3[ob] = mfma32x32x2(a3c[ob].z, hv[4 * r4 + 2], acc3[ob]);
-              acc3[ob] = mfma32x32x2(a3c[ob].w, hv[4 * r4 + 3], acc3[ob]);
-            }
-#pragma unroll
-            for (int ob = 0; ob < (OB > 0 ? OB : 1); ++ob) a3c[ob] = a3n[ob];
-          }
-        } else {
-#pragma unroll
-          for (int r = 0; r < 16; ++r) fin = fmaf(hv[r], cwd[rb * 32 + mfma32_row(r, h)], fin);
-        }
-      }
-    }
-    if (OB > 0) {
-#pragma unroll
-      for (int ob = 0; ob < (OB > 0 ? OB : 1); ++ob) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int o = ob * 32 + mfma32_row(r, h);
-          fin = fmaf(fmaxf(acc3[ob][r] + cb3[o], 0.f), cwd[o], fin);
-        }
-      }
-    }
+    float fin = wd_tile_fp32<RB2, OB>(prow, qrow, S4, W2f, W3f, cb2, cb3, cwd, lane, h);
     fin += __shfl_xor(fin, 32);
     const int64_t item = base + j;
     const bool ivalid = lane < 32 && item < part_end;
@@ -312,7 +332,7 @@ __global__ __launch_bounds__(256, (RB2 >= 8 || OB >= 4) ? 1 : 2) void widedeep_s
       L.offer(score, (int)item, ivalid, K);
     }
   }
-  if (!DENSE && active) L.store(cand_v + (b * NP + p) * K, cand_i + (b * NP + p) * K, K);
+  if (!DENSE && active) L.store(cand_v + (slot * NP + p) * K, cand_i + (slot * NP + p) * K, K);
 }
 
 // ------------------------------------------------------------------ pairwise forward
@@ -385,6 +405,649 @@ __global__ __launch_bounds__(256) void widedeep_pair_kernel(
   }
 }
 
+// ------------------------------------------------------------------ certified f16x3 scan
+// Wide&Deep top-K with a CERTIFIED split-f16 pre-filter and exact fp32 re-scoring.
+//
+// The fp32 MFMA rate is 1/16 of the f16 rate.  A plain f16 scan cannot prune W&D: its
+// rigorous error bound (f16 rounding of every operand, propagated through |W3||W2|) spans
+// a third of the score spread.  Split operands can: every f16 operand is x = x_hi + x_lo
+// (x_hi = f16(x), x_lo = f16(x - x_hi)), each layer runs three f16 MFMA passes
+// W_hi x_hi + W_hi x_lo + W_lo x_hi with fp32 accumulation -- 3/16 of the fp32 MFMA time,
+// and representation error 2^-22 per operand, below the fp32 path's own accumulation error.
+// Nothing the scan computes is returned: it only prunes; every returned score is recomputed
+// by wd_tile_fp32 (the fp32 kernel's own arithmetic), so outputs are bitwise those of the
+// exact fp32 path (tests/test_gpu_prefilter.py).
+//
+// Bound (per pair, real units).  Let x1 = relu(P_u + Q_i) (the fp32 layer-1 values both
+// paths read), x2 = relu(D2 + b2'), x3 = relu(D3 + b3') (this scan's values), and
+// v3 = |w_d'|, v2 = |W3'|^T v3, v1 = |W2'|^T v2 (for a two-layer tower v2 = |w_d'|).
+// The fp32 path's K-term fma chain errs by <= K u sum|terms| (u = 2^-24); the split path's
+// MFMA chain by <= 6u (sum|terms| + |acc|) per MFMA (measured <= 3.4u:
+// profiles/r1_mfma_semantics_probe.txt (c)) plus 3 * 2^-22 for the split operands; ReLU is
+// 1-Lipschitz and errors propagate through |W|, so
+//   |approx - exact| <= rho (g1 v1.x1 + g2 v2.x2 + g3 v3.x3 + g4 (|fin| + |c_u| + |w_I|)
+//                            + cb) + absb
+// with g1 = (2.125 K1 + 22)u, g2 = (2.125 n2 + 22)u (layer 3) or (32 RB2 + 12)u (final dot
+// of a two-layer tower), g3 = (32 NOB + 10)u, g4 = 10u, cb the bias-add roundings, absb the
+// f16 subnormal slack (2^-25 per rounding, scaled back), rho = 1 + 2^-6.  The v.x terms are
+// three dot products per pair computed next to the MFMAs.
+//
+// Selection.  Each (user, item partition) keeps a wave-resident top-K of lower bounds
+// lb = approx - e: its K-th is a lower bound of the exact K-th score at every moment, so an
+// item is appended to the (user, partition) segment when ub = approx + e reaches it (every
+// exact top-K item does).  The K-th of the merged lower-bound lists, L_u, filters the
+// segments; the survivors (a few hundred per user) are re-scored in fp32.  Rows with an
+// unusable bound, fewer than K finite items or an overflowing segment take the exact kernel.
+typedef _Float16 wh8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ f32x16 wd_mfma16(wh8 a, wh8 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+}
+
+struct WdCertParams {
+  unsigned mx[2];       // max|P| over the batch rows, max|Q| over the items (float bits)
+  float s1, sw2, s2, sw3;  // f16 operand scales (powers of two)
+  float c2, c3;            // layer-2 accumulator -> x2 scale, layer-3 accumulator -> real
+  float inv_s2;
+  float g1, g2, g3, g4, cb, absb, rho;
+  int bad;                 // bound unusable: every row takes the exact path
+};
+
+// pair-permuted position t of a layer-1 row -> layer-1 unit (hnm_linear_rows_f32 layout)
+__device__ __forceinline__ int wd_korig(int t, int K1P) {
+  const int half = K1P >> 1;
+  return t < half ? 2 * t : 2 * (t - half) + 1;
+}
+
+__device__ __forceinline__ float wd_pow2_below_inv(float m) {  // largest 2^e with m 2^e <= 1
+  int e;
+  (void)frexpf(m, &e);
+  return ldexpf(1.f, -e);
+}
+
+__device__ __forceinline__ float wd_nmax(float a, float b) { return (b > a || b != b) ? b : a; }
+
+// per-block maxima of |P| (rows [0, B)) and |Q| (items) -> part[blk * 2 + {0, 1}]
+__global__ __launch_bounds__(256) void wdc_stats_kernel(const float* __restrict__ Pu,
+                                                        int64_t nP, const float* __restrict__ Qi,
+                                                        int64_t nQ, float* __restrict__ part) {
+  __shared__ float red[2][4];
+  float mp = 0.f, mq = 0.f;
+  const int64_t stride = (int64_t)gridDim.x * 256 * 4;
+  for (int64_t e = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4; e < nP; e += stride) {
+    const float4 v = *reinterpret_cast<const float4*>(Pu + e);
+    mp = wd_nmax(mp, wd_nmax(wd_nmax(fabsf(v.x), fabsf(v.y)), wd_nmax(fabsf(v.z), fabsf(v.w))));
+  }
+  for (int64_t e = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4; e < nQ; e += stride) {
+    const float4 v = *reinterpret_cast<const float4*>(Qi + e);
+    mq = wd_nmax(mq, wd_nmax(wd_nmax(fabsf(v.x), fabsf(v.y)), wd_nmax(fabsf(v.z), fabsf(v.w))));
+  }
+  for (int o = 32; o >= 1; o >>= 1) {
+    mp = wd_nmax(mp, __shfl_xor(mp, o));
+    mq = wd_nmax(mq, __shfl_xor(mq, o));
+  }
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (lane == 0) {
+    red[0][wave] = mp;
+    red[1][wave] = mq;
+  }
+  __syncthreads();
+  if (threadIdx.x < 2) {
+    float m = red[threadIdx.x][0];
+    for (int w = 1; w < 4; ++w) m = wd_nmax(m, red[threadIdx.x][w]);
+    part[blockIdx.x * 2 + threadIdx.x] = m;
+  }
+}
+
+// One block: bound vectors v1 (pair-permuted positions), v2, scales, coefficients.
+__global__ __launch_bounds__(256) void wdc_params_kernel(hnm_widedeep_weights w, WdPrep p,
+                                                         const float* __restrict__ part, int nblk,
+                                                         float* __restrict__ v1,
+                                                         float* __restrict__ v2,
+                                                         float* __restrict__ b2s,
+                                                         WdCertParams* prm) {
+  __shared__ float sv2[256];
+  __shared__ float red[8][4];
+  __shared__ float bc[8];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int K1P = p.K1P, n2 = p.RB2 * 32, NOB = p.OB > 0 ? p.OB : 1;
+  const int l1 = w.l1, l2 = w.l2, l3 = w.l3;
+  float mp = 0.f, mq = 0.f;
+  for (int b = tid; b < nblk; b += 256) {
+    mp = wd_nmax(mp, part[2 * b]);
+    mq = wd_nmax(mq, part[2 * b + 1]);
+  }
+  // v2 (layer-2 rows): OB > 0: sum_m |W3'_mj| |wd'_m|; two-layer tower: |wd'_j|
+  float mW3 = 0.f, sv2b = 0.f, swdb3 = 0.f, sumwd = 0.f;
+  for (int jx = tid; jx < n2; jx += 256) {
+    float v = 0.f;
+    if (jx < l2) {
+      if (p.OB > 0) {
+        const float a2 = bn_a(w.bn2_w, w.bn2_var, jx, w.eps);
+        for (int m = 0; m < l3; ++m) {
+          const float wv = fabsf(w.w3[(int64_t)m * l2 + jx] * a2);
+          mW3 = wd_nmax(mW3, wv);
+          v = fmaf(wv, fabsf(p.wdp[m]), v);
+        }
+      } else {
+        v = fabsf(p.wdp[jx]);
+      }
+    }
+    sv2[jx] = v;
+    v2[jx] = v;
+    sv2b = fmaf(v, fabsf(p.b2p[jx]), sv2b);
+  }
+  for (int m = tid; m < NOB * 32; m += 256) {
+    if (p.OB > 0) swdb3 = fmaf(fabsf(p.wdp[m]), fabsf(p.b3p[m]), swdb3);
+    sumwd += fabsf(p.wdp[m]);
+  }
+  __syncthreads();
+  // v1 (pair-permuted positions) and layer-2 row statistics
+  float mW2 = 0.f, sv1 = 0.f;
+  for (int t = tid; t < K1P; t += 256) {
+    const int k = wd_korig(t, K1P);
+    float v = 0.f;
+    if (k < l1) {
+      const float a1 = bn_a(w.bn1_w, w.bn1_var, k, w.eps);
+      for (int jx = 0; jx < l2; ++jx) {
+        const float wv = fabsf(w.w2[(int64_t)jx * l1 + k] * a1);
+        mW2 = wd_nmax(mW2, wv);
+        v = fmaf(wv, sv2[jx], v);
+      }
+    }
+    v1[t] = v;
+    sv1 += v;
+  }
+  const float zmax = mp + mq;
+  float m2 = 0.f, sumv2 = 0.f;  // max_j (zmax sum_k |W2'_jk| + |b2'_j|)
+  for (int jx = tid; jx < l2; jx += 256) {
+    float rs = 0.f;
+    for (int k = 0; k < l1; ++k)
+      rs += fabsf(w.w2[(int64_t)jx * l1 + k] * bn_a(w.bn1_w, w.bn1_var, k, w.eps));
+    m2 = wd_nmax(m2, fmaf(zmax, rs, fabsf(p.b2p[jx])));
+    sumv2 += sv2[jx];
+  }
+  float vals[8] = {mp, mq, mW2, mW3, m2, sv1, sv2b, swdb3};
+  for (int q = 0; q < 8; ++q) {
+    float x = vals[q];
+    for (int o = 32; o >= 1; o >>= 1) {
+      const float y = __shfl_xor(x, o);
+      x = q < 5 ? wd_nmax(x, y) : x + y;
+    }
+    if (lane == 0) red[q][wave] = x;
+  }
+  float sums2[2] = {sumv2, sumwd};
+  for (int q = 0; q < 2; ++q)
+    for (int o = 32; o >= 1; o >>= 1) sums2[q] += __shfl_xor(sums2[q], o);
+  __shared__ float red2[2][4];
+  if (lane == 0) {
+    red2[0][wave] = sums2[0];
+    red2[1][wave] = sums2[1];
+  }
+  __syncthreads();
+  if (tid < 8) {
+    float x = red[tid][0];
+    for (int wv = 1; wv < 4; ++wv) x = tid < 5 ? wd_nmax(x, red[tid][wv]) : x + red[tid][wv];
+    bc[tid] = x;
+  }
+  __syncthreads();
+  const float M2 = bc[4];
+  const float lim = 1.0e30f;
+  bool bad = (K1P & 15) != 0;
+  for (int q = 0; q < 8; ++q) bad |= !(bc[q] <= lim);
+  const float F16R = 16384.f;  // scaled operand magnitudes <= 2^14
+  const float s1 = bc[0] + bc[1] > 0.f ? F16R * wd_pow2_below_inv(bc[0] + bc[1]) : 1.f;
+  const float sw2 = bc[2] > 0.f ? F16R * wd_pow2_below_inv(bc[2]) : 1.f;
+  const float s2 = M2 > 0.f ? F16R * wd_pow2_below_inv(M2) : 1.f;
+  const float sw3 = bc[3] > 0.f ? F16R * wd_pow2_below_inv(bc[3]) : 1.f;
+  for (float sc : {s1, sw2, s2, sw3}) bad |= !(sc >= 1e-25f && sc <= 1e25f);
+  // b2' in x2 units
+  for (int jx = tid; jx < n2; jx += 256) b2s[jx] = p.b2p[jx] * s2;
+  if (tid != 0) return;
+  const float u = 5.9604645e-08f;  // 2^-24
+  const float phi = 2.98023224e-08f;  // 2^-25: half the f16 subnormal spacing
+  const float sumv2t = red2[0][0] + red2[0][1] + red2[0][2] + red2[0][3];
+  const float sumwdt = red2[1][0] + red2[1][1] + red2[1][2] + red2[1][3];
+  WdCertParams c;
+  c.mx[0] = __float_as_uint(bc[0]);
+  c.mx[1] = __float_as_uint(bc[1]);
+  c.s1 = s1;
+  c.sw2 = sw2;
+  c.s2 = s2;
+  c.sw3 = sw3;
+  c.c2 = s2 / (s1 * sw2);
+  c.c3 = 1.f / (s2 * sw3);
+  c.inv_s2 = 1.f / s2;
+  c.g1 = (2.125f * K1P + 22.f) * u;
+  c.g2 = (p.OB > 0 ? 2.125f * n2 + 22.f : 32.f * p.RB2 + 12.f) * u;
+  c.g3 = p.OB > 0 ? (32.f * NOB + 10.f) * u : 0.f;
+  c.g4 = 10.f * u;
+  c.cb = 4.f * u * (bc[6] + bc[7]);
+  // subnormal slack: x1 / W2 / x2 / W3 roundings, 2 per operand (hi and lo), doubled
+  c.absb = 4.f * phi *
+           (bc[5] / s1 + sumv2t * K1P * (bc[0] + bc[1]) / sw2 + sumv2t / s2 +
+            (p.OB > 0 ? sumwdt * n2 * M2 / sw3 : 0.f));
+  c.rho = 1.015625f;
+  bad |= !(c.absb <= lim) || !(c.c2 > 0.f && c.c2 <= lim) || !(c.c3 > 0.f && c.c3 <= lim);
+  c.bad = bad;
+  *prm = c;
+}
+
+// Split-f16 A operands.  W2hl[((rb * KB + kb) * 2 + hl) * 64 + lane][t]: row rb*32 +
+// (lane & 31), pair-permuted position 16 kb + 8 (lane >> 5) + t; W3hl[((ob * 2 RB2 + kb3) *
+// 2 + hl) * 64 + lane][t]: row ob*32 + (lane & 31), layer-2 row (kb3 >> 1) * 32 +
+// mfma32_row(8 (kb3 & 1) + t, lane >> 5) -- the order in which layer 2's accumulator
+// registers become layer 3's B operand.
+__global__ __launch_bounds__(256) void wdc_convert_kernel(hnm_widedeep_weights w, WdPrep p,
+                                                          const WdCertParams* __restrict__ prm,
+                                                          wh8* __restrict__ W2hl,
+                                                          wh8* __restrict__ W3hl) {
+  const int K1P = p.K1P, KB = K1P / 16;
+  const float sw2 = prm->sw2, sw3 = prm->sw3;
+  const int64_t n2 = (int64_t)p.RB2 * KB * 64, n3 = (int64_t)p.OB * 2 * p.RB2 * 64;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < n2 + n3;
+       e += (int64_t)gridDim.x * 256) {
+    const int lane = (int)(e & 63), h = lane >> 5, r = lane & 31;
+    wh8 hi, lo;
+    if (e < n2) {
+      const int64_t q = e >> 6;
+      const int kb = (int)(q % KB), rb = (int)(q / KB);
+      const int o = rb * 32 + r;
+      for (int t = 0; t < 8; ++t) {
+        const int k = wd_korig(16 * kb + 8 * h + t, K1P);
+        float v = 0.f;
+        if (o < w.l2 && k < w.l1) v = w.w2[(int64_t)o * w.l1 + k] * bn_a(w.bn1_w, w.bn1_var, k, w.eps);
+        v *= sw2;
+        const _Float16 vh = (_Float16)v;
+        hi[t] = vh;
+        lo[t] = (_Float16)(v - (float)vh);
+      }
+      W2hl[(q * 2 + 0) * 64 + lane] = hi;
+      W2hl[(q * 2 + 1) * 64 + lane] = lo;
+    } else {
+      const int64_t q = (e - n2) >> 6;
+      const int kb3 = (int)(q % (2 * p.RB2)), ob = (int)(q / (2 * p.RB2));
+      const int o = ob * 32 + r;
+      for (int t = 0; t < 8; ++t) {
+        const int jx = (kb3 >> 1) * 32 + mfma32_row(8 * (kb3 & 1) + t, h);
+        float v = 0.f;
+        if (o < w.l3 && jx < w.l2) v = w.w3[(int64_t)o * w.l2 + jx] * bn_a(w.bn2_w, w.bn2_var, jx, w.eps);
+        v *= sw3;
+        const _Float16 vh = (_Float16)v;
+        hi[t] = vh;
+        lo[t] = (_Float16)(v - (float)vh);
+      }
+      W3hl[(q * 2 + 0) * 64 + lane] = hi;
+      W3hl[(q * 2 + 1) * 64 + lane] = lo;
+    }
+  }
+}
+
+struct WdScanArgs {
+  const float* Pu;  // [B, K1P]  pair-permuted layer-1 user part (+ b1)
+  const float* Qi;  // [I, K1P]  pair-permuted layer-1 item part
+  int K1P;
+  const wh8* W2hl;
+  const wh8* W3hl;
+  const float* v1;   // [K1P]
+  const float* v2;   // [RB2*32]
+  const float* b2s;  // [RB2*32] b2' s2
+  const float* b3p;  // [OB*32]
+  const float* wdp;  // [NL*32]
+  const float* cu;   // [B] per-user constant
+  const float* wI;   // [I] wide item weight
+  const WdCertParams* prm;
+  int64_t B, I, ipp;
+  int NP;
+  const int64_t* mptr;
+  const int32_t* midx;
+  int K;
+  float* lbv;    // [B, NP, K] lower-bound lists
+  int32_t* lbi;
+  int32_t* segi;  // [B, NP, cap] appended items
+  float* segu;    // [B, NP, cap] their upper bounds
+  int* cnt;       // [B, NP]
+  int cap;
+  float* dbg_a;   // DEBUG: [B, lda] approx score, bound
+  float* dbg_e;
+  int64_t lda;
+};
+
+#define WDC_THRESH 0
+#define WDC_DEBUG 1
+
+// Block = 4 waves = 4 users (rows blockIdx.x * 4 + wave) x item partition blockIdx.y; the
+// Q tile (32 items, fp32) is shared through LDS.  Per (user, tile) the wave runs layer 2 as
+// 3 x RB2 x K1P/16 split-f16 MFMAs (G2 row blocks per pass over k, the next layer fed from
+// the accumulators as each pass completes), layer 3 as 3 x OB x 2 RB2, then the bound.
+template <int RB2, int OB, int G2, int MODE>
+__global__ __launch_bounds__(256, 2) void wdc_scan_kernel(WdScanArgs A) {
+  constexpr int NOB = OB > 0 ? OB : 1;
+  constexpr int NL = OB > 0 ? OB : RB2;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int K1P = A.K1P, KB = K1P / 16, QRS = K1P + 4;
+  float* qs = smem;               // [32][QRS]
+  float* ps = qs + 32 * QRS;      // [4][K1P]
+  float* v1s = ps + 4 * K1P;      // [K1P]
+  float* b2l = v1s + K1P;         // [RB2*32]
+  float* v2l = b2l + RB2 * 32;    // [RB2*32]
+  float* b3l = v2l + RB2 * 32;    // [NOB*32]
+  float* wdl = b3l + NOB * 32;    // [NL*32]
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5, j = lane & 31;
+  const int64_t ublk = (int64_t)blockIdx.x * 4;
+  const int64_t b = ublk + wave;
+  const int p = blockIdx.y;
+  const int64_t part_start = (int64_t)p * A.ipp;
+  const int64_t part_end = std::min<int64_t>(A.I, part_start + A.ipp);
+  for (int e = tid; e < K1P / 4; e += 256)
+    *reinterpret_cast<float4*>(v1s + 4 * e) = *reinterpret_cast<const float4*>(A.v1 + 4 * e);
+  for (int e = tid; e < K1P; e += 256) {
+    const int r = e / (K1P / 4), c = e % (K1P / 4);
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (ublk + r < A.B) v = *reinterpret_cast<const float4*>(A.Pu + (ublk + r) * K1P + 4 * c);
+    *reinterpret_cast<float4*>(ps + r * K1P + 4 * c) = v;
+  }
+  for (int e = tid; e < RB2 * 32; e += 256) {
+    b2l[e] = A.b2s[e];
+    v2l[e] = A.v2[e];
+  }
+  for (int e = tid; e < NOB * 32; e += 256) b3l[e] = OB > 0 ? A.b3p[e] : 0.f;
+  for (int e = tid; e < NL * 32; e += 256) wdl[e] = A.wdp[e];
+  const float s1 = A.prm->s1, c2 = A.prm->c2, c3 = A.prm->c3, inv_s2 = A.prm->inv_s2;
+  const float g1 = A.prm->g1, g2 = A.prm->g2, g3 = A.prm->g3, g4 = A.prm->g4;
+  const float cbd = A.prm->cb, absb = A.prm->absb, rho = A.prm->rho;
+  const bool active = b < A.B;
+  const float cub = active ? A.cu[b] : 0.f;
+  WaveTopK<1> L;
+  L.init();
+  int nm = WD_INT_BIG, mpos = 0, mend = 0;
+  if (A.mptr && active) {
+    int64_t lo = A.mptr[b], hi = A.mptr[b + 1];
+    while (lo < hi) {
+      const int64_t mid = (lo + hi) >> 1;
+      if (A.midx[mid] < part_start) lo = mid + 1;
+      else hi = mid;
+    }
+    mpos = (int)lo;
+    mend = (int)A.mptr[b + 1];
+    nm = mpos < mend ? A.midx[mpos] : WD_INT_BIG;
+  }
+  int count = 0;
+  const int64_t seg = (b * A.NP + p) * (int64_t)A.cap;
+
+  const int64_t ntiles = part_end > part_start ? hnm_cdiv(part_end - part_start, WD_TILE) : 0;
+  for (int64_t t = 0; t < ntiles; ++t) {
+    const int64_t base = part_start + t * WD_TILE;
+    __syncthreads();
+    for (int e = tid; e < WD_TILE * K1P / 4; e += 256) {
+      const int r = e / (K1P / 4), c = e % (K1P / 4);
+      const int64_t item = base + r;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (item < part_end) v = *reinterpret_cast<const float4*>(A.Qi + item * K1P + 4 * c);
+      *reinterpret_cast<float4*>(&qs[r * QRS + 4 * c]) = v;
+    }
+    __syncthreads();
+    if (!active) continue;
+
+    const float* prow = ps + wave * K1P + 8 * h;
+    const float* qrow = qs + j * QRS + 8 * h;
+    f32x16 acc3[NOB];
+#pragma unroll
+    for (int ob = 0; ob < NOB; ++ob)
+      acc3[ob] = f32x16{0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    float fin = 0.f, bx1 = 0.f, bx2 = 0.f, bx3 = 0.f;
+#pragma unroll 1
+    for (int g = 0; g < RB2 / G2; ++g) {
+      f32x16 acc2[G2];
+#pragma unroll
+      for (int gi = 0; gi < G2; ++gi)
+        acc2[gi] = f32x16{0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      for (int kb = 0; kb < KB; ++kb) {
+        wh8 ah[G2], al[G2];
+#pragma unroll
+        for (int gi = 0; gi < G2; ++gi) {
+          const int64_t q = ((int64_t)(g * G2 + gi) * KB + kb) * 2;
+          ah[gi] = A.W2hl[q * 64 + lane];
+          al[gi] = A.W2hl[(q + 1) * 64 + lane];
+        }
+        const float4 p0 = *reinterpret_cast<const float4*>(prow + 16 * kb);
+        const float4 p1 = *reinterpret_cast<const float4*>(prow + 16 * kb + 4);
+        const float4 q0 = *reinterpret_cast<const float4*>(qrow + 16 * kb);
+        const float4 q1 = *reinterpret_cast<const float4*>(qrow + 16 * kb + 4);
+        float x[8] = {fmaxf(p0.x + q0.x, 0.f), fmaxf(p0.y + q0.y, 0.f), fmaxf(p0.z + q0.z, 0.f),
+                      fmaxf(p0.w + q0.w, 0.f), fmaxf(p1.x + q1.x, 0.f), fmaxf(p1.y + q1.y, 0.f),
+                      fmaxf(p1.z + q1.z, 0.f), fmaxf(p1.w + q1.w, 0.f)};
+        if (g == 0) {
+          const float4 va = *reinterpret_cast<const float4*>(v1s + 16 * kb + 8 * h);
+          const float4 vb = *reinterpret_cast<const float4*>(v1s + 16 * kb + 8 * h + 4);
+          bx1 = fmaf(va.x, x[0], bx1); bx1 = fmaf(va.y, x[1], bx1);
+          bx1 = fmaf(va.z, x[2], bx1); bx1 = fmaf(va.w, x[3], bx1);
+          bx1 = fmaf(vb.x, x[4], bx1); bx1 = fmaf(vb.y, x[5], bx1);
+          bx1 = fmaf(vb.z, x[6], bx1); bx1 = fmaf(vb.w, x[7], bx1);
+        }
+        wh8 xh, xl;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float xs = x[e] * s1;
+          const _Float16 hi = (_Float16)xs;
+          xh[e] = hi;
+          xl[e] = (_Float16)(xs - (float)hi);
+        }
+#pragma unroll
+        for (int gi = 0; gi < G2; ++gi) acc2[gi] = wd_mfma16(ah[gi], xh, acc2[gi]);
+#pragma unroll
+        for (int gi = 0; gi < G2; ++gi) acc2[gi] = wd_mfma16(ah[gi], xl, acc2[gi]);
+#pragma unroll
+        for (int gi = 0; gi < G2; ++gi) acc2[gi] = wd_mfma16(al[gi], xh, acc2[gi]);
+      }
+      // x2 = relu(D2 + b2') in s2 units feeds layer 3 (or the final dot)
+#pragma unroll
+      for (int gi = 0; gi < G2; ++gi) {
+        const int rb = g * G2 + gi;
+        float y[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int row = rb * 32 + mfma32_row(r, h);
+          y[r] = fmaxf(fmaf(acc2[gi][r], c2, b2l[row]), 0.f);
+          bx2 = fmaf(v2l[row], y[r], bx2);
+          if (OB == 0) fin = fmaf(y[r], wdl[row], fin);
+        }
+        if (OB > 0) {
+#pragma unroll
+          for (int half2 = 0; half2 < 2; ++half2) {
+            wh8 yh, yl;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              const float ys = y[8 * half2 + e];
+              const _Float16 hi = (_Float16)ys;
+              yh[e] = hi;
+              yl[e] = (_Float16)(ys - (float)hi);
+            }
+            const int kb3 = 2 * rb + half2;
+            wh8 bh[NOB], bl[NOB];
+#pragma unroll
+            for (int ob = 0; ob < NOB; ++ob) {
+              const int64_t q = ((int64_t)ob * 2 * RB2 + kb3) * 2;
+              bh[ob] = A.W3hl[q * 64 + lane];
+              bl[ob] = A.W3hl[(q + 1) * 64 + lane];
+            }
+#pragma unroll
+            for (int ob = 0; ob < NOB; ++ob) acc3[ob] = wd_mfma16(bh[ob], yh, acc3[ob]);
+#pragma unroll
+            for (int ob = 0; ob < NOB; ++ob) acc3[ob] = wd_mfma16(bh[ob], yl, acc3[ob]);
+#pragma unroll
+            for (int ob = 0; ob < NOB; ++ob) acc3[ob] = wd_mfma16(bl[ob], yh, acc3[ob]);
+          }
+        }
+      }
+    }
+    if (OB > 0) {
+#pragma unroll
+      for (int ob = 0; ob < NOB; ++ob) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int m = ob * 32 + mfma32_row(r, h);
+          const float z = fmaxf(fmaf(acc3[ob][r], c3, b3l[m]), 0.f);
+          fin = fmaf(z, wdl[m], fin);
+          bx3 = fmaf(fabsf(wdl[m]), z, bx3);
+        }
+      }
+    } else {
+      fin *= inv_s2;
+    }
+    fin = hnm_sum_halves(fin);
+    bx1 = hnm_sum_halves(bx1);
+    bx2 = hnm_sum_halves(bx2);
+    bx3 = hnm_sum_halves(bx3);
+    const int64_t item = base + j;
+    const bool ivalid = lane < 32 && item < part_end;
+    const float wi = ivalid ? A.wI[item] : 0.f;
+    const float score = fin + cub + wi;
+    const float e = rho * (g1 * bx1 + g2 * (bx2 * inv_s2) + g3 * bx3 +
+                           g4 * (fabsf(fin) + fabsf(cub) + fabsf(wi)) + cbd) + absb;
+    bool masked = false;
+    const int64_t tile_end = std::min<int64_t>(base + WD_TILE, part_end);
+    while (nm < tile_end) {
+      if (item == nm) masked = true;
+      ++mpos;
+      nm = mpos < mend ? A.midx[mpos] : WD_INT_BIG;
+    }
+    if (MODE == WDC_DEBUG) {
+      if (ivalid) {
+        A.dbg_a[b * A.lda + item] = score;
+        A.dbg_e[b * A.lda + item] = e;
+      }
+      continue;
+    }
+    const bool ok = ivalid && !masked;
+    const float lb = score - e, ub = score + e;
+    L.offer(lb, (int)item, ok, A.K);
+    const bool app = ok && ub >= L.thr_v;
+    const uint64_t m = __ballot(app);
+    const int pos = count + __popcll(m & ((1ull << lane) - 1));
+    if (app && pos < A.cap) {
+      A.segi[seg + pos] = (int32_t)item;
+      A.segu[seg + pos] = ub;
+    }
+    count += __popcll(m);
+  }
+  if (MODE == WDC_THRESH && active) {
+    L.store(A.lbv + (b * A.NP + p) * A.K, A.lbi + (b * A.NP + p) * A.K, A.K);
+    if (lane == 0) A.cnt[b * A.NP + p] = count;
+  }
+}
+
+struct WdRescoreArgs {
+  const float* Pu;
+  const float* Qi;
+  int K1P;
+  const float4* W2f;
+  const float4* W3f;
+  const float* b2p;
+  const float* b3p;
+  const float* wdp;
+  const float* cu;
+  const float* wI;
+  const WdCertParams* prm;
+  int64_t B;
+  int NP, K, cap;
+  const float* Lk;   // [B, K] merged lower-bound lists (slot K-1 = L_u)
+  const int32_t* segi;
+  const float* segu;
+  const int* cnt;
+  int32_t* fbrows;   // rows that take the exact kernel
+  int* nfb;
+  float* ov;
+  int64_t* oi;
+  unsigned long long* stats;  // HNM_OPT_STATS: rows, candidates re-scored, fallback rows
+};
+
+// One wave per row: survivors (ub >= L_u) of the row's segments, 32 at a time, through
+// wd_tile_fp32 -- the exact kernel's arithmetic -- into a wave top-K.
+template <int RB2, int OB>
+__global__ __launch_bounds__(256, 1) void wdc_rescore_kernel(WdRescoreArgs R) {
+  __shared__ int stage[4][96];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5, j = lane & 31;
+  const int64_t b = (int64_t)blockIdx.x * 4 + wave;
+  if (b >= R.B) return;  // no block-level barriers below
+  const int K = R.K;
+  const float Lu = R.Lk[b * K + K - 1];
+  bool fb = R.prm->bad || !(Lu > -__builtin_inff());
+  for (int p = 0; p < R.NP; ++p) fb |= R.cnt[b * R.NP + p] > R.cap;
+  if (fb) {
+    if (lane == 0) {
+      R.fbrows[atomicAdd(R.nfb, 1)] = (int32_t)b;
+      if (R.stats) {
+        atomicAdd(R.stats + 0, 1ull);
+        atomicAdd(R.stats + 2, 1ull);
+      }
+    }
+    return;
+  }
+  int nsurv = 0;
+  const int KS1 = R.K1P / 2, S4 = R.K1P / 8;
+  const float cub = R.cu[b];
+  const float* prow = R.Pu + b * R.K1P + h * KS1;
+  int* st = stage[wave];
+  WaveTopK<1> T;
+  T.init();
+  int ns = 0;
+  auto run_tile = [&](int nv) {
+    const int it = st[j < nv ? j : 0];
+    const float* qrow = R.Qi + (int64_t)it * R.K1P + h * KS1;
+    float fin = wd_tile_fp32<RB2, OB>(prow, qrow, S4, R.W2f, R.W3f, R.b2p, R.b3p, R.wdp, lane, h);
+    fin += __shfl_xor(fin, 32);
+    const bool ivalid = lane < 32 && j < nv;
+    const float score = fin + cub + (ivalid ? R.wI[it] : 0.f);
+    T.offer(score, it, ivalid, K);
+  };
+  for (int p = 0; p < R.NP; ++p) {
+    const int n = R.cnt[b * R.NP + p];
+    const int64_t base = (b * R.NP + p) * (int64_t)R.cap;
+    for (int c0 = 0; c0 < n; c0 += 64) {
+      const int e = c0 + lane;
+      const bool ok = e < n && R.segu[base + e] >= Lu;
+      const uint64_t m = __ballot(ok);
+      if (ok) st[ns + __popcll(m & ((1ull << lane) - 1))] = R.segi[base + e];
+      ns += __popcll(m);
+      nsurv += __popcll(m);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      while (ns >= 32) {
+        run_tile(32);
+        const int rest = ns - 32;
+        const int mv = lane < rest ? st[32 + lane] : 0;
+        __builtin_amdgcn_wave_barrier();
+        if (lane < rest) st[lane] = mv;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        ns = rest;
+      }
+    }
+  }
+  if (ns > 0) run_tile(ns);
+  T.store(R.ov + b * K, R.oi + b * K, K);
+  if (R.stats && lane == 0) {
+    atomicAdd(R.stats + 0, 1ull);
+    atomicAdd(R.stats + 1, (unsigned long long)nsurv);
+  }
+}
+
+// out rows <- the fallback's compact rows
+__global__ void wdc_scatter_kernel(const float* __restrict__ cv, const int64_t* __restrict__ ci,
+                                   const int32_t* __restrict__ rows, int n, int K,
+                                   float* __restrict__ ov, int64_t* __restrict__ oi) {
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  if (e >= n * K) return;
+  const int r = e / K, s = e % K;
+  const int64_t b = rows[r];
+  if (ov) ov[b * K + s] = cv[e];
+  oi[b * K + s] = ci[e];
+}
+
 // ------------------------------------------------------------------ host side
 static hnm_status wd_check(const hnm_widedeep_weights* w) {
   HNM_REQUIRE(w && w->deep_user && w->deep_item && w->w1 && w->b1 && w->w2 && w->b2 &&
@@ -415,47 +1078,64 @@ template <int RB2, int OB, bool DENSE>
 static void launch_wd(hnm_ctx* ctx, dim3 grid, size_t lds, const float* Pu, const float* Qi,
                       int K1P, const WdPrep& pr, const float* cu, const float* wI, int64_t B,
                       int64_t I, int64_t ipp, const int64_t* mptr, const int32_t* midx, int K,
-                      float* cv, int32_t* ci, int NP, float* dense, int64_t ldo) {
+                      float* cv, int32_t* ci, int NP, float* dense, int64_t ldo,
+                      const int32_t* rows = nullptr) {
   hipLaunchKernelGGL((widedeep_score_kernel<RB2, OB, DENSE>), grid, dim3(256), lds, ctx->stream,
                      Pu, Qi, K1P, pr.W2f, pr.W3f, pr.b2p, pr.b3p, pr.wdp, cu, wI, B, I, ipp, mptr,
-                     midx, K, cv, ci, NP, dense, ldo);
+                     midx, K, cv, ci, NP, dense, ldo, rows);
 }
 
-template <bool DENSE>
-static hnm_status wd_common(hnm_ctx* ctx, const hnm_widedeep_weights* w, const int64_t* ids,
-                            int64_t B, const float* ufeat, const int64_t* mptr,
-                            const int32_t* midx, int K, float* ov, int64_t* oi, float* dense,
-                            int64_t ldo) {
+// Per-call preparation shared by the exact and the certified paths: folded weights,
+// layer-1 projections P (batch rows) / Q (all items), per-user constants.  `extra` bytes of
+// caller scratch follow in the same workspace carve.
+struct WdSetup {
+  WdPrep pr;
+  int K1P;
+  float* Pu;
+  float* Qi;
+  float* cu;
+  char* extra;
+};
+
+static hnm_status wd_shape(const hnm_widedeep_weights* w, WdPrep* pr) {
   hnm_status st = wd_check(w);
   if (st) return st;
-  HNM_REQUIRE(ctx && ids, HNM_EINVAL, "widedeep: NULL argument");
-  if (B <= 0) return HNM_OK;
-  const int64_t I = w->num_items;
-  WdPrep pr;
-  pr.K1P = (w->l1 + 7) / 8 * 8;
-  pr.RB2 = pow2_blocks(w->l2);
-  pr.OB = w->l3 > 0 ? pow2_blocks(w->l3) : 0;
-  if (pr.RB2 > 8 || pr.OB > 4) {
-    hnm_set_error("widedeep: unsupported widths");
-    return HNM_EUNSUPPORTED;
-  }
-  // instantiated (RB2, OB) pairs
-  const bool ok = (pr.RB2 == 8 && pr.OB == 4) || (pr.RB2 == 4 && pr.OB == 2) ||
-                  (pr.RB2 == 2 && pr.OB == 1) || (pr.RB2 == 1 && pr.OB == 0) ||
-                  (pr.RB2 == 2 && pr.OB == 0) || (pr.RB2 == 4 && pr.OB == 0) ||
-                  (pr.RB2 == 8 && pr.OB == 0) || (pr.RB2 == 1 && pr.OB == 1) ||
-                  (pr.RB2 == 4 && pr.OB == 4) || (pr.RB2 == 8 && pr.OB == 2);
+  pr->K1P = (w->l1 + 7) / 8 * 8;
+  pr->RB2 = pow2_blocks(w->l2);
+  pr->OB = w->l3 > 0 ? pow2_blocks(w->l3) : 0;
+  const bool ok = (pr->RB2 == 8 && pr->OB == 4) || (pr->RB2 == 4 && pr->OB == 2) ||
+                  (pr->RB2 == 2 && pr->OB == 1) || (pr->RB2 == 1 && pr->OB == 0) ||
+                  (pr->RB2 == 2 && pr->OB == 0) || (pr->RB2 == 4 && pr->OB == 0) ||
+                  (pr->RB2 == 8 && pr->OB == 0) || (pr->RB2 == 1 && pr->OB == 1) ||
+                  (pr->RB2 == 4 && pr->OB == 4) || (pr->RB2 == 8 && pr->OB == 2);
   if (!ok) {
     hnm_set_error("widedeep: layer widths %d/%d not instantiated", w->l2, w->l3);
     return HNM_EUNSUPPORTED;
   }
-  const int K1P = pr.K1P;
+  return HNM_OK;
+}
+
+static void wd_partition(const hnm_ctx* ctx, int64_t B, int64_t I, int64_t* np, int64_t* ipp) {
   const int64_t ublocks = hnm_cdiv(B, 4);
   const int64_t want = std::max<int64_t>(1, hnm_cdiv(2 * (int64_t)ctx->num_cus, ublocks));
-  int64_t np = std::min<int64_t>(want, std::max<int64_t>(1, hnm_cdiv(I, 4 * WD_TILE)));
-  int64_t ipp = hnm_cdiv(hnm_cdiv(I, np), WD_TILE) * WD_TILE;
-  np = hnm_cdiv(I, ipp);
+  int64_t n = std::min<int64_t>(want, std::max<int64_t>(1, hnm_cdiv(I, 4 * WD_TILE)));
+  *ipp = hnm_cdiv(hnm_cdiv(I, n), WD_TILE) * WD_TILE;
+  *np = hnm_cdiv(I, *ipp);
+}
 
+// candidate-list scratch (values + int32 items) of the exact list pass over n rows
+static size_t wd_list_bytes(const hnm_ctx* ctx, int64_t n, int64_t I, int K) {
+  int64_t np, ipp;
+  wd_partition(ctx, n, I, &np, &ipp);
+  return 2 * hnm_align((size_t)n * np * K * 4);
+}
+
+static hnm_status wd_setup(hnm_ctx* ctx, const hnm_widedeep_weights* w, const int64_t* ids,
+                           int64_t B, const float* ufeat, size_t extra, WdSetup* S) {
+  const int64_t I = w->num_items;
+  WdPrep& pr = S->pr;
+  const int K1P = pr.K1P;
+  S->K1P = K1P;
   const int nlast = pr.OB > 0 ? pr.OB : pr.RB2;
   const size_t szW2 = hnm_align((size_t)pr.RB2 * (K1P / 8) * 64 * 16);
   const size_t szW3 = hnm_align((size_t)std::max(pr.OB, 1) * pr.RB2 * 4 * 64 * 16);
@@ -467,11 +1147,9 @@ static hnm_status wd_common(hnm_ctx* ctx, const hnm_widedeep_weights* w, const i
   const size_t szF = ufeat ? hnm_align((size_t)B * w->num_user_features * 4) : 0;
   const size_t szU = hnm_align((size_t)B * 4);
   const size_t szT = w->num_user_features > 0 ? hnm_align((size_t)B * K1P * 4) : 0;
-  const size_t ncand = DENSE ? 0 : (size_t)B * np * K;
-  const size_t szC = hnm_align(ncand * 4);
   void* wsp;
-  st = hnm_workspace(ctx, szW2 + szW3 + szb2 + szb3 + szwd + 256 + szP + szQ + szX + szF + szU +
-                              szT + 2 * szC, &wsp);
+  hnm_status st = hnm_workspace(ctx, szW2 + szW3 + szb2 + szb3 + szwd + 256 + szP + szQ + szX +
+                                         szF + szU + szT + hnm_align(extra), &wsp);
   if (st) return st;
   char* q = (char*)wsp;
   pr.W2f = (float4*)q; q += szW2;
@@ -486,8 +1164,10 @@ static hnm_status wd_common(hnm_ctx* ctx, const hnm_widedeep_weights* w, const i
   float* WFu = (float*)q; q += szF;
   float* cu = (float*)q; q += szU;
   float* Tf = (float*)q; q += szT;
-  float* cv = (float*)q; q += szC;
-  int32_t* ci = (int32_t*)q;
+  S->Pu = Pu;
+  S->Qi = Qi;
+  S->cu = cu;
+  S->extra = q;
 
   hipStream_t s = ctx->stream;
   hipLaunchKernelGGL(wd_prep_w2, dim3(256), dim3(256), 0, s, *w, pr);
@@ -536,15 +1216,35 @@ static hnm_status wd_common(hnm_ctx* ctx, const hnm_widedeep_weights* w, const i
     st = hnm_axpby_f32(ctx, (int64_t)B * K1P, 1.f, Pu, 1.f, Tf, Pu);
     if (st) return st;
   }
+  return HNM_OK;
+}
 
+// Exact fp32 pass: dense scores (dense != nullptr) or the per-partition top-K lists +
+// merge for the rows rows[0, n) (rows == nullptr: batch rows 0 .. n).  cv/ci: list scratch
+// of wd_list_bytes(n) bytes; outputs at the compact row index.
+static hnm_status wd_exact(hnm_ctx* ctx, const hnm_widedeep_weights* w, const WdSetup& S,
+                           int64_t n, const int64_t* mptr, const int32_t* midx, int K,
+                           const int32_t* rows, float* cv, int32_t* ci, float* ov, int64_t* oi,
+                           float* dense, int64_t ldo, bool timed) {
+  const WdPrep& pr = S.pr;
+  const int64_t I = w->num_items;
+  int64_t np, ipp;
+  wd_partition(ctx, n, I, &np, &ipp);
+  const int K1P = S.K1P;
+  const int nlast = pr.OB > 0 ? pr.OB : pr.RB2;
   const size_t lds = (size_t)(WD_TILE * (K1P + 4) + 4 * K1P + (pr.RB2 + pr.OB + nlast) * 32) * 4;
-  dim3 grid((unsigned)ublocks, (unsigned)np);
+  dim3 grid((unsigned)hnm_cdiv(n, 4), (unsigned)np);
   const float* wI = w->wide_item;
-  hnm_timer_begin(ctx, HNM_TIME_SCORE);
-#define WD_CASE(R, O)                                                                     \
-  if (pr.RB2 == R && pr.OB == O)                                                          \
-    launch_wd<R, O, DENSE>(ctx, grid, lds, Pu, Qi, K1P, pr, cu, wI, B, I, ipp, mptr, midx, K, \
-                           cv, ci, (int)np, dense, ldo);
+  if (timed) hnm_timer_begin(ctx, HNM_TIME_SCORE);
+#define WD_CASE(R, O)                                                                         \
+  if (pr.RB2 == R && pr.OB == O) {                                                            \
+    if (dense)                                                                                \
+      launch_wd<R, O, true>(ctx, grid, lds, S.Pu, S.Qi, K1P, pr, S.cu, wI, n, I, ipp, mptr,   \
+                            midx, K, cv, ci, (int)np, dense, ldo, rows);                      \
+    else                                                                                      \
+      launch_wd<R, O, false>(ctx, grid, lds, S.Pu, S.Qi, K1P, pr, S.cu, wI, n, I, ipp, mptr,  \
+                             midx, K, cv, ci, (int)np, dense, ldo, rows);                     \
+  }
   WD_CASE(8, 4)
   WD_CASE(4, 2)
   WD_CASE(2, 1)
@@ -556,9 +1256,235 @@ static hnm_status wd_common(hnm_ctx* ctx, const hnm_widedeep_weights* w, const i
   WD_CASE(4, 4)
   WD_CASE(8, 2)
 #undef WD_CASE
-  hnm_timer_end(ctx, HNM_TIME_SCORE);
+  if (timed) hnm_timer_end(ctx, HNM_TIME_SCORE);
   HNM_LAUNCH_CHECK();
-  if (!DENSE) return hnm_topk_merge_i32(ctx, cv, ci, B, 1, 0, np * K, (int)(np * K), K, ov, oi);
+  if (dense) return HNM_OK;
+  return hnm_topk_merge_i32(ctx, cv, ci, n, 1, 0, np * K, (int)(np * K), K, ov, oi);
+}
+
+// ------------------------------------------------------------------ certified path host
+#define WDC_CAP 1024  // appended candidates per (user, partition) segment
+
+static bool wdc_instantiated(int RB2, int OB) {
+  return (RB2 == 8 && OB == 4) || (RB2 == 4 && OB == 2) || (RB2 == 2 && OB == 1) ||
+         (RB2 == 1 && OB == 1) || (RB2 == 1 && OB == 0) || (RB2 == 2 && OB == 0);
+}
+
+static bool wdc_eligible(const hnm_ctx* ctx, const WdPrep& pr, int64_t I, int K, bool debug) {
+  return (debug || (ctx->prefilter && I >= 4096)) && K <= 64 && pr.K1P % 16 == 0 &&
+         wdc_instantiated(pr.RB2, pr.OB);
+}
+
+struct WdcWs {
+  WdCertParams* prm;
+  wh8* W2hl;
+  wh8* W3hl;
+  float* v1;
+  float* v2;
+  float* b2s;
+  float* part;
+  float* lbv;
+  int32_t* lbi;
+  float* Lv;
+  int64_t* Li;
+  int32_t* segi;
+  float* segu;
+  int* cnt;
+  int32_t* fbrows;
+  int* nfb;
+  float* fcv;
+  int32_t* fci;
+  float* fov;
+  int64_t* foi;
+  int64_t np, ipp;
+  int cap;
+};
+constexpr int WDC_STAT_BLOCKS = 1024;
+
+static size_t wdc_carve(const hnm_ctx* ctx, const WdPrep& pr, int64_t B, int64_t I, int K,
+                        char* base, WdcWs* c) {
+  int64_t np, ipp;
+  wd_partition(ctx, B, I, &np, &ipp);
+  const int cap = (int)std::min<int64_t>(WDC_CAP, ipp);
+  const int K1P = pr.K1P, KB = K1P / 16;
+  const int64_t fbn = 8 * (int64_t)ctx->num_cus + 4 + B;  // bound on n * np(n) over n <= B
+  size_t off = 0;
+  auto take = [&](size_t bytes) {
+    char* p = base ? base + off : nullptr;
+    off += hnm_align(bytes);
+    return p;
+  };
+  WdcWs t;
+  t.prm = (WdCertParams*)take(sizeof(WdCertParams));
+  t.W2hl = (wh8*)take((size_t)pr.RB2 * KB * 2 * 64 * 16);
+  t.W3hl = (wh8*)take((size_t)std::max(pr.OB, 1) * 2 * pr.RB2 * 2 * 64 * 16);
+  t.v1 = (float*)take((size_t)K1P * 4);
+  t.v2 = (float*)take((size_t)pr.RB2 * 32 * 4);
+  t.b2s = (float*)take((size_t)pr.RB2 * 32 * 4);
+  t.part = (float*)take((size_t)WDC_STAT_BLOCKS * 2 * 4);
+  t.lbv = (float*)take((size_t)B * np * K * 4);
+  t.lbi = (int32_t*)take((size_t)B * np * K * 4);
+  t.Lv = (float*)take((size_t)B * K * 4);
+  t.Li = (int64_t*)take((size_t)B * K * 8);
+  t.segi = (int32_t*)take((size_t)B * np * cap * 4);
+  t.segu = (float*)take((size_t)B * np * cap * 4);
+  t.cnt = (int*)take((size_t)B * np * 4);
+  t.fbrows = (int32_t*)take((size_t)B * 4);
+  t.nfb = (int*)take(4);
+  t.fcv = (float*)take((size_t)fbn * K * 4);
+  t.fci = (int32_t*)take((size_t)fbn * K * 4);
+  t.fov = (float*)take((size_t)B * K * 4);
+  t.foi = (int64_t*)take((size_t)B * K * 8);
+  t.np = np;
+  t.ipp = ipp;
+  t.cap = cap;
+  if (c) *c = t;
+  return off;
+}
+
+static hnm_status wdc_prepare(hnm_ctx* ctx, const hnm_widedeep_weights* w, const WdSetup& S,
+                              int64_t B, const WdcWs& c) {
+  hipStream_t s = ctx->stream;
+  const int64_t I = w->num_items;
+  hipLaunchKernelGGL(wdc_stats_kernel, dim3(WDC_STAT_BLOCKS), dim3(256), 0, s, S.Pu,
+                     B * S.K1P, S.Qi, I * S.K1P, c.part);
+  hipLaunchKernelGGL(wdc_params_kernel, dim3(1), dim3(256), 0, s, *w, S.pr, c.part,
+                     WDC_STAT_BLOCKS, c.v1, c.v2, c.b2s, c.prm);
+  hipLaunchKernelGGL(wdc_convert_kernel, dim3(256), dim3(256), 0, s, *w, S.pr, c.prm, c.W2hl,
+                     c.W3hl);
+  HNM_LAUNCH_CHECK();
+  return HNM_OK;
+}
+
+template <int RB2, int OB, int MODE>
+static void wdc_launch_scan(hnm_ctx* ctx, dim3 grid, size_t lds, const WdScanArgs& a) {
+  constexpr int G2 = RB2 < 4 ? RB2 : 4;
+  auto kern = wdc_scan_kernel<RB2, OB, G2, MODE>;
+  hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  hipLaunchKernelGGL(kern, grid, dim3(256), lds, ctx->stream, a);
+}
+
+template <int RB2, int OB>
+static void wdc_launch_rescore(hnm_ctx* ctx, dim3 grid, const WdRescoreArgs& r) {
+  hipLaunchKernelGGL((wdc_rescore_kernel<RB2, OB>), grid, dim3(256), 0, ctx->stream, r);
+}
+
+static hnm_status wdc_scan(hnm_ctx* ctx, const hnm_widedeep_weights* w, const WdSetup& S,
+                           int64_t B, const int64_t* mptr, const int32_t* midx, int K,
+                           const WdcWs& c, int mode, float* dbg_a, float* dbg_e, int64_t lda) {
+  const WdPrep& pr = S.pr;
+  const int NOB = pr.OB > 0 ? pr.OB : 1, NL = pr.OB > 0 ? pr.OB : pr.RB2;
+  WdScanArgs a;
+  a.Pu = S.Pu;
+  a.Qi = S.Qi;
+  a.K1P = S.K1P;
+  a.W2hl = c.W2hl;
+  a.W3hl = c.W3hl;
+  a.v1 = c.v1;
+  a.v2 = c.v2;
+  a.b2s = c.b2s;
+  a.b3p = pr.b3p;
+  a.wdp = pr.wdp;
+  a.cu = S.cu;
+  a.wI = w->wide_item;
+  a.prm = c.prm;
+  a.B = B;
+  a.I = w->num_items;
+  a.ipp = c.ipp;
+  a.NP = (int)c.np;
+  a.mptr = mptr;
+  a.midx = midx;
+  a.K = K;
+  a.lbv = c.lbv;
+  a.lbi = c.lbi;
+  a.segi = c.segi;
+  a.segu = c.segu;
+  a.cnt = c.cnt;
+  a.cap = c.cap;
+  a.dbg_a = dbg_a;
+  a.dbg_e = dbg_e;
+  a.lda = lda;
+  const size_t lds =
+      (size_t)(32 * (S.K1P + 4) + 5 * S.K1P + 2 * pr.RB2 * 32 + NOB * 32 + NL * 32) * 4;
+  dim3 grid((unsigned)hnm_cdiv(B, 4), (unsigned)c.np);
+  if (mode == WDC_THRESH) hnm_timer_begin(ctx, HNM_TIME_SCORE);
+#define WDC_CASE(R, O)                                                        \
+  if (pr.RB2 == R && pr.OB == O) {                                            \
+    if (mode == WDC_THRESH) wdc_launch_scan<R, O, WDC_THRESH>(ctx, grid, lds, a); \
+    else wdc_launch_scan<R, O, WDC_DEBUG>(ctx, grid, lds, a);                 \
+  }
+  WDC_CASE(8, 4)
+  WDC_CASE(4, 2)
+  WDC_CASE(2, 1)
+  WDC_CASE(1, 1)
+  WDC_CASE(1, 0)
+  WDC_CASE(2, 0)
+#undef WDC_CASE
+  if (mode == WDC_THRESH) hnm_timer_end(ctx, HNM_TIME_SCORE);
+  HNM_LAUNCH_CHECK();
+  return HNM_OK;
+}
+
+static hnm_status wdc_topk(hnm_ctx* ctx, const hnm_widedeep_weights* w, const WdSetup& S,
+                           int64_t B, const int64_t* mptr, const int32_t* midx, int K,
+                           const WdcWs& c, float* ov, int64_t* oi) {
+  hnm_status st = wdc_prepare(ctx, w, S, B, c);
+  if (st) return st;
+  st = wdc_scan(ctx, w, S, B, mptr, midx, K, c, WDC_THRESH, nullptr, nullptr, 0);
+  if (st) return st;
+  st = hnm_topk_merge_i32(ctx, c.lbv, c.lbi, B, 1, 0, c.np * K, (int)(c.np * K), K, c.Lv, c.Li);
+  if (st) return st;
+  hipStream_t s = ctx->stream;
+  HNM_HIP_CHECK(hipMemsetAsync(c.nfb, 0, sizeof(int), s));
+  const WdPrep& pr = S.pr;
+  WdRescoreArgs r;
+  r.Pu = S.Pu;
+  r.Qi = S.Qi;
+  r.K1P = S.K1P;
+  r.W2f = pr.W2f;
+  r.W3f = pr.W3f;
+  r.b2p = pr.b2p;
+  r.b3p = pr.b3p;
+  r.wdp = pr.wdp;
+  r.cu = S.cu;
+  r.wI = w->wide_item;
+  r.prm = c.prm;
+  r.B = B;
+  r.NP = (int)c.np;
+  r.K = K;
+  r.cap = c.cap;
+  r.Lk = c.Lv;
+  r.segi = c.segi;
+  r.segu = c.segu;
+  r.cnt = c.cnt;
+  r.fbrows = c.fbrows;
+  r.nfb = c.nfb;
+  r.ov = ov;
+  r.oi = oi;
+  r.stats = ctx->stats_on ? ctx->stats_dev : nullptr;
+  dim3 grid((unsigned)hnm_cdiv(B, 4));
+#define WDC_CASE(R, O) \
+  if (pr.RB2 == R && pr.OB == O) wdc_launch_rescore<R, O>(ctx, grid, r);
+  WDC_CASE(8, 4)
+  WDC_CASE(4, 2)
+  WDC_CASE(2, 1)
+  WDC_CASE(1, 1)
+  WDC_CASE(1, 0)
+  WDC_CASE(2, 0)
+#undef WDC_CASE
+  HNM_LAUNCH_CHECK();
+  // fallback rows: the count comes back to the host (a W&D call is long; one sync is noise)
+  int nfb = 0;
+  HNM_HIP_CHECK(hipMemcpyAsync(&nfb, c.nfb, sizeof(int), hipMemcpyDeviceToHost, s));
+  HNM_HIP_CHECK(hipStreamSynchronize(s));
+  if (nfb > 0) {
+    st = wd_exact(ctx, w, S, nfb, mptr, midx, K, c.fbrows, c.fcv, c.fci, c.fov, c.foi, nullptr,
+                  0, false);
+    if (st) return st;
+    hipLaunchKernelGGL(wdc_scatter_kernel, dim3((unsigned)hnm_cdiv((int64_t)nfb * K, 256)),
+                       dim3(256), 0, s, c.fov, c.foi, c.fbrows, nfb, K, ov, oi);
+    HNM_LAUNCH_CHECK();
+  }
   return HNM_OK;
 }
 
@@ -568,8 +1494,29 @@ extern "C" hnm_status hnm_widedeep_topk_f32(hnm_ctx* ctx, const hnm_widedeep_wei
                                             const int32_t* mask_idx, int k, float* out_val,
                                             int64_t* out_idx) {
   HNM_REQUIRE(k >= 1 && k <= 64 && out_idx, HNM_EINVAL, "widedeep_topk: fused path needs 1 <= k <= 64");
-  return wd_common<false>(ctx, w, user_ids, B, user_features, mask_ptr, mask_idx, k, out_val,
-                          out_idx, nullptr, 0);
+  HNM_REQUIRE(ctx && user_ids, HNM_EINVAL, "widedeep: NULL argument");
+  WdSetup S;
+  hnm_status st = wd_shape(w, &S.pr);
+  if (st) return st;
+  if (B <= 0) return HNM_OK;
+  const int64_t I = w->num_items;
+  if (wdc_eligible(ctx, S.pr, I, k, false)) {
+    const size_t extra = wdc_carve(ctx, S.pr, B, I, k, nullptr, nullptr);
+    st = wd_setup(ctx, w, user_ids, B, user_features, extra, &S);
+    if (st) return st;
+    WdcWs c;
+    wdc_carve(ctx, S.pr, B, I, k, S.extra, &c);
+    return wdc_topk(ctx, w, S, B, mask_ptr, mask_idx, k, c, out_val, out_idx);
+  }
+  const size_t lb = wd_list_bytes(ctx, B, I, k);
+  st = wd_setup(ctx, w, user_ids, B, user_features, lb, &S);
+  if (st) return st;
+  int64_t np, ipp;
+  wd_partition(ctx, B, I, &np, &ipp);
+  float* cv = (float*)S.extra;
+  int32_t* ci = (int32_t*)(S.extra + hnm_align((size_t)B * np * k * 4));
+  return wd_exact(ctx, w, S, B, mask_ptr, mask_idx, k, nullptr, cv, ci, out_val, out_idx,
+                  nullptr, 0, true);
 }
 
 extern "C" hnm_status hnm_widedeep_scores_f32(hnm_ctx* ctx, const hnm_widedeep_weights* w,
@@ -577,8 +1524,40 @@ extern "C" hnm_status hnm_widedeep_scores_f32(hnm_ctx* ctx, const hnm_widedeep_w
                                               const float* user_features, float* out,
                                               int64_t ldo) {
   HNM_REQUIRE(out && w && ldo >= w->num_items, HNM_EINVAL, "widedeep_scores: bad output");
-  return wd_common<true>(ctx, w, user_ids, B, user_features, nullptr, nullptr, 1, nullptr,
-                         nullptr, out, ldo);
+  HNM_REQUIRE(ctx && user_ids, HNM_EINVAL, "widedeep: NULL argument");
+  WdSetup S;
+  hnm_status st = wd_shape(w, &S.pr);
+  if (st) return st;
+  if (B <= 0) return HNM_OK;
+  st = wd_setup(ctx, w, user_ids, B, user_features, 0, &S);
+  if (st) return st;
+  return wd_exact(ctx, w, S, B, nullptr, nullptr, 1, nullptr, nullptr, nullptr, nullptr,
+                  nullptr, out, ldo, true);
+}
+
+extern "C" hnm_status hnm_widedeep_prefilter_debug_f32(hnm_ctx* ctx,
+                                                       const hnm_widedeep_weights* w,
+                                                       const int64_t* user_ids, int64_t B,
+                                                       const float* user_features,
+                                                       float* approx, int64_t lda,
+                                                       float* bound) {
+  HNM_REQUIRE(ctx && user_ids && approx && bound && w && lda >= w->num_items, HNM_EINVAL,
+              "widedeep_prefilter_debug: bad argument");
+  WdSetup S;
+  hnm_status st = wd_shape(w, &S.pr);
+  if (st) return st;
+  HNM_REQUIRE(wdc_eligible(ctx, S.pr, w->num_items, 1, true), HNM_EUNSUPPORTED,
+              "widedeep_prefilter_debug: tower shape not covered by the certified scan");
+  if (B <= 0) return HNM_OK;
+  const int64_t I = w->num_items;
+  const size_t extra = wdc_carve(ctx, S.pr, B, I, 1, nullptr, nullptr);
+  st = wd_setup(ctx, w, user_ids, B, user_features, extra, &S);
+  if (st) return st;
+  WdcWs c;
+  wdc_carve(ctx, S.pr, B, I, 1, S.extra, &c);
+  st = wdc_prepare(ctx, w, S, B, c);
+  if (st) return st;
+  return wdc_scan(ctx, w, S, B, nullptr, nullptr, 1, c, WDC_DEBUG, approx, bound, lda);
 }
 
 extern "C" hnm_status hnm_widedeep_pair_scores_f32(hnm_ctx* ctx, const hnm_widedeep_weights* w,

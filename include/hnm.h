@@ -276,6 +276,14 @@ hnm_status hnm_topk_merge_f32(hnm_ctx* ctx, const float* cand_val, const int64_t
                               int64_t B, int64_t G, int64_t gstride, int64_t bstride,
                               int kc, int k, float* out_val, int64_t* out_idx);
 
+/* Diagnostics of the certified split-f16 pre-filter of hnm_widedeep_topk_f32 (no reference
+ * counterpart): approx[b, i] = the scan's score, bound[b, i] = its certified error bound;
+ * |approx - exact| <= bound for every pair (tests check it on the full catalogue). */
+hnm_status hnm_widedeep_prefilter_debug_f32(hnm_ctx* ctx, const hnm_widedeep_weights* w,
+                                            const int64_t* user_ids, int64_t B,
+                                            const float* user_features, float* approx,
+                                            int64_t lda, float* bound);
+
 /* ---- torch.topk over a dense score matrix (serve.py:350-355, k up to 100) ----------
  * Row top-k of scores[b, :I] (leading dim ld) with the optional CSR -inf mask. k <= 128. */
 hnm_status hnm_topk_rows_f32(hnm_ctx* ctx, const float* scores, int64_t ld, int64_t B,

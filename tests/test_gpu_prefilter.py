@@ -239,3 +239,101 @@ def test_dot_prefilter_masks_ties_fallback():
     ut[11] = 0
     (ev, ei), (pv, pi), stats = dot_both(ut, ids, it, 12)
     assert np.array_equal(ei, pi) and pi[11].tolist() == list(range(12))
+
+
+# ------------------------------------------------------------------ Wide&Deep (split-f16)
+def wd_model(U, I, seed=0, layers=(512, 256, 128), d=64, **kw):
+    from hnm_recommendation_amd import WideDeep
+    sd = syn.widedeep_state_dict(U, I, d, layers, seed=seed, **kw)
+    m = WideDeep(U, I, embedding_dim=d, deep_layers=list(layers),
+                 num_user_features=kw.get("num_user_features", 0))
+    return to_module(m, sd), sd
+
+
+def wd_prefilter_debug(m, users, feats=None):
+    w, keep = m._weights()
+    B, I = users.numel(), m.num_items
+    approx = torch.empty(B, I, device=DEV)
+    bound = torch.empty(B, I, device=DEV)
+    _lib.check(_lib.fn("hnm_widedeep_prefilter_debug_f32")(
+        _lib.ctx(users.device), w, _lib.ptr(users), B, _lib.ptr(feats), _lib.ptr(approx), I,
+        _lib.ptr(bound)), "hnm_widedeep_prefilter_debug_f32")
+    _lib.sync_check(users.device)
+    return approx, bound
+
+
+@pytest.mark.parametrize("kw", [{}, {"bias_scale": 0.05, "randomize_bn": True, "emb_scale": 10.0}])
+def test_wd_bound_holds_full_catalogue(kw):
+    """|approx - exact| <= bound for every pair of 16 users x the H&M catalogue."""
+    m, _ = wd_model(20000, syn.HM_ITEMS, seed=1, **kw)
+    users = torch.from_numpy(syn.user_batch(20000, 16, seed=5)).to(DEV)
+    approx, bound = wd_prefilter_debug(m, users)
+    exact = m.predict_all_items(users)
+    ratio = ((approx - exact).abs() / bound).max().item()
+    print(f"W&D: max |approx - exact| / bound = {ratio:.4f}; mean bound / score std = "
+          f"{(bound.mean(1) / exact.std(1)).mean().item():.4f}")
+    assert torch.isfinite(bound).all()
+    assert ratio <= 1.0, ratio
+
+
+@pytest.mark.parametrize("kw", [{}, {"bias_scale": 0.05, "randomize_bn": True, "emb_scale": 10.0}])
+def test_wd_prefilter_identical_to_exact(kw):
+    m, _ = wd_model(20000, syn.HM_ITEMS, seed=2, **kw)
+    users_np = syn.user_batch(20000, 64 + 3, seed=9)
+    users = torch.from_numpy(users_np).to(DEV)
+    (ev, ei), (pv, pi), stats = topk_both(m, users)
+    assert np.array_equal(ei, pi)
+    assert np.array_equal(ev.view(np.uint32), pv.view(np.uint32))
+    rows, cands, fallback = stats
+    print(f"W&D candidates/row {cands / max(rows - fallback, 1):.1f}, fallback rows {fallback}")
+    assert rows == users_np.size and fallback == 0
+
+
+def test_wd_prefilter_filters_k_fallback():
+    m, _ = wd_model(5000, 12000, seed=3, bias_scale=0.05, randomize_bn=True)
+    users_np = syn.user_batch(5000, 37, seed=2)
+    users = torch.from_numpy(users_np).to(DEV)
+    _lib.set_prefilter(users.device, False)
+    _, top = m.recommend_with_scores(users, k=30)
+    _lib.set_prefilter(users.device, True)
+    top = top.cpu().numpy()
+    rng = np.random.default_rng(1)
+    f = {int(u): set(top[r, ::2].tolist()) | set(rng.integers(0, 12000, 50).tolist())
+         for r, u in enumerate(users_np)}
+    f[int(users_np[5])] = set(range(12000)) - {11, 7000}  # < K items left: exact fallback
+    for k in (1, 12, 64):
+        (ev, ei), (pv, pi), stats = topk_both(m, users, f, k=k)
+        assert np.array_equal(ei, pi), k
+        assert np.array_equal(ev.view(np.uint32), pv.view(np.uint32)), k
+        assert stats[2] >= 1
+        for r, u in enumerate(users_np):
+            assert not (set(pi[r][pi[r] >= 0].tolist()) & f[int(u)])
+    assert pi[5, :2].tolist() == [11, 7000] and np.isneginf(pv[5, 2:]).all()
+
+
+def test_wd_prefilter_small_towers_and_bad_bound():
+    # two-layer tower (RB2 = 1, no layer 3) with user features
+    from hnm_recommendation_amd import WideDeep
+    U, I, F = 3000, 9000, 10
+    sd = syn.widedeep_state_dict(U, I, 16, (64, 32), num_user_features=F, seed=4,
+                                 bias_scale=0.05, randomize_bn=True, emb_scale=10.0)
+    m = to_module(WideDeep(U, I, num_user_features=F, embedding_dim=16, deep_layers=[64, 32]), sd)
+    users = torch.from_numpy(syn.user_batch(U, 21, seed=8)).to(DEV)
+    feats = torch.from_numpy(np.random.default_rng(9).standard_normal((21, F)).astype(np.float32)).to(DEV)
+    _lib.set_prefilter(users.device, False)
+    ev, ei = m.recommend_with_scores(users, feats, k=12)
+    _lib.set_prefilter(users.device, True)
+    pv, pi = m.recommend_with_scores(users, feats, k=12)
+    assert torch.equal(ei, pi) and torch.equal(ev, pv)
+    approx, bound = wd_prefilter_debug(m, users, feats)
+    exact = m.predict_all_items(users, feats)
+    assert ((approx - exact).abs() <= bound).all()
+    # a non-finite weight: the bound is unusable, every row takes the exact kernel
+    m2, _ = wd_model(3000, 8192, seed=5, layers=(128, 64, 32), d=32)
+    with torch.no_grad():
+        m2.deep_item_embedding.weight[17, 3] = float("inf")
+    users = torch.arange(0, 40, device=DEV)
+    (ev, ei), (pv, pi), stats = topk_both(m2, users)
+    assert np.array_equal(ei, pi)
+    assert np.array_equal(ev.view(np.uint32), pv.view(np.uint32))
+    assert stats[2] == 40

@@ -20,11 +20,11 @@ step bench_ncf 300 python bench.py
 step bench_lightgcn 400 python bench.py --workload lightgcn --no-cpu-baseline
 step bench_lightgcn128 400 python bench.py --workload lightgcn128 --no-cpu-baseline
 step bench_mf 300 python bench.py --workload mf --no-cpu-baseline
-step bench_widedeep 600 python bench.py --workload widedeep --steps 3 --warmup 1 --no-cpu-baseline
+step bench_widedeep 600 python bench.py --workload widedeep --steps 10 --warmup 2 --no-cpu-baseline
 cd /tmp && export TMPDIR=/tmp
 for w in ncf lightgcn widedeep; do
   extra="--steps 5 --warmup 2"
-  [ $w = widedeep ] && extra="--steps 2 --warmup 1"
+  [ $w = widedeep ] && extra="--steps 3 --warmup 1"
   timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_$w" -o $w -- \
     python3 "$ROOT/bench.py" --workload $w $extra --no-cpu-baseline > "$OUT/prof_$w.log" 2>&1 \
     || { echo "rocprof $w failed"; exit 1; }
