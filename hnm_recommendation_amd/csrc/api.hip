@@ -74,7 +74,8 @@ extern "C" hnm_status hnm_ctx_set_option(hnm_ctx* ctx, int option, int64_t value
       ctx->stats_on = value != 0;
       return HNM_OK;
     case HNM_OPT_SCAN_USERS:
-      HNM_REQUIRE(value >= 1 && value <= 6, HNM_EINVAL, "HNM_OPT_SCAN_USERS: 1 to 6");
+      HNM_REQUIRE((value >= 1 && value <= 6) || (value > 100 && value < 110), HNM_EINVAL,
+                  "HNM_OPT_SCAN_USERS: 1 to 6 (101.. W&D scan ablations)");
       ctx->scan_users = (int)value;
       return HNM_OK;
     default:

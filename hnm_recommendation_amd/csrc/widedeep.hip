@@ -444,6 +444,34 @@ __device__ __forceinline__ f32x16 wd_mfma16(wh8 a, wh8 b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
 }
 
+// c - (float)h for the low (SEL = 0) or high (SEL = 1) f16 half of a packed register: one
+// v_fma_mix_f32 instead of a convert and a subtract (the split operand's remainder, exact)
+template <int SEL>
+__device__ __forceinline__ float wd_sub_half(unsigned packed, float c) {
+  float d;
+  if (SEL == 0)
+    asm("v_fma_mix_f32 %0, %1, -1.0, %2 op_sel_hi:[1,0,0]" : "=v"(d) : "v"(packed), "v"(c));
+  else
+    asm("v_fma_mix_f32 %0, %1, -1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "=v"(d) : "v"(packed), "v"(c));
+  return d;
+}
+
+// Split 8 fp32 values into f16 hi / lo halves: hi = f16(x), lo = f16(x - hi) (RNE; the
+// remainder is exact in fp32).
+__device__ __forceinline__ void wd_split8(const float* x, wh8& hi, wh8& lo) {
+  typedef _Float16 wh2 __attribute__((ext_vector_type(2)));
+#pragma unroll
+  for (int e = 0; e < 8; e += 2) {
+    wh2 hp;
+    hp[0] = (_Float16)x[e];
+    hp[1] = (_Float16)x[e + 1];
+    hi[e] = hp[0];
+    hi[e + 1] = hp[1];
+    lo[e] = (_Float16)__builtin_fmaf((float)hp[0], -1.f, x[e]);
+    lo[e + 1] = (_Float16)__builtin_fmaf((float)hp[1], -1.f, x[e + 1]);
+  }
+}
+
 struct WdCertParams {
   unsigned mx[2];       // max|P| over the batch rows, max|Q| over the items (float bits)
   float s1, sw2, s2, sw3;  // f16 operand scales (powers of two)
@@ -715,37 +743,50 @@ struct WdScanArgs {
 
 #define WDC_THRESH 0
 #define WDC_DEBUG 1
+#ifndef WDC_INTERLEAVE
+#define WDC_INTERLEAVE 1  // sched_group_barrier interleave of the k loop (0: compiler order)
+#endif
 
-// Block = 4 waves = 4 users (rows blockIdx.x * 4 + wave) x item partition blockIdx.y; the
-// Q tile (32 items, fp32) is shared through LDS.  Per (user, tile) the wave runs layer 2 as
-// 3 x RB2 x K1P/16 split-f16 MFMAs (G2 row blocks per pass over k, the next layer fed from
-// the accumulators as each pass completes), layer 3 as 3 x OB x 2 RB2, then the bound.
-template <int RB2, int OB, int G2, int MODE>
-__global__ __launch_bounds__(256, 2) void wdc_scan_kernel(WdScanArgs A) {
+// Block = 4 waves x UPW users each (rows blockIdx.x * 4 UPW + wave * UPW + v) x item
+// partition blockIdx.y; the Q tile (32 items, fp32) is shared through LDS.  Per tile a wave
+// runs layer 2 as 3 x RB2 x K1P/16 split-f16 MFMAs per user (G2 row blocks per pass over
+// k, the next layer fed from the accumulators as each pass completes), layer 3 as
+// 3 x OB x 2 RB2, then the bound.  UPW = 2: every weight fragment loaded from L2 feeds six
+// MFMAs (two users' B operands) instead of three -- the fragment stream is what bounds the
+// one-user variant (tools/wd_ablation.sh: no weight loads = -19% time).
+template <int RB2, int OB, int G2, int MODE, int UPW, int ABL = 0>
+__global__ __launch_bounds__(256, UPW == 1 ? 2 : 1) void wdc_scan_kernel(WdScanArgs A) {
   constexpr int NOB = OB > 0 ? OB : 1;
   constexpr int NL = OB > 0 ? OB : RB2;
+  constexpr int NU = 4 * UPW;  // users per block
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int K1P = A.K1P, KB = K1P / 16, QRS = K1P + 4;
   float* qs = smem;               // [32][QRS]
-  float* ps = qs + 32 * QRS;      // [4][K1P]
-  float* v1s = ps + 4 * K1P;      // [K1P]
+  float* ps = qs + 32 * QRS;      // [NU][K1P]
+  float* v1s = ps + NU * K1P;     // [K1P]
   float* b2l = v1s + K1P;         // [RB2*32]
   float* v2l = b2l + RB2 * 32;    // [RB2*32]
   float* b3l = v2l + RB2 * 32;    // [NOB*32]
   float* wdl = b3l + NOB * 32;    // [NL*32]
+  float* v0s = wdl + NL * 32;     // [K1P] zeros (the bound row of passes > 0)
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5, j = lane & 31;
-  const int64_t ublk = (int64_t)blockIdx.x * 4;
-  const int64_t b = ublk + wave;
+  const int64_t ublk = (int64_t)blockIdx.x * NU;
   const int p = blockIdx.y;
   const int64_t part_start = (int64_t)p * A.ipp;
   const int64_t part_end = std::min<int64_t>(A.I, part_start + A.ipp);
-  for (int e = tid; e < K1P / 4; e += 256)
-    *reinterpret_cast<float4*>(v1s + 4 * e) = *reinterpret_cast<const float4*>(A.v1 + 4 * e);
+  // P and Q are staged pre-scaled by s1 (a power of two: relu(s1 p + s1 q) = s1 relu(p + q)
+  // exactly), v1 by 1 / s1, so the k loop forms the f16 operands without a multiply
+  const float s1 = A.prm->s1, inv_s1 = 1.f / s1;
   for (int e = tid; e < K1P; e += 256) {
+    v1s[e] = A.v1[e] * inv_s1;
+    v0s[e] = 0.f;
+  }
+  for (int e = tid; e < NU * K1P / 4; e += 256) {
     const int r = e / (K1P / 4), c = e % (K1P / 4);
     float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
     if (ublk + r < A.B) v = *reinterpret_cast<const float4*>(A.Pu + (ublk + r) * K1P + 4 * c);
+    v.x *= s1; v.y *= s1; v.z *= s1; v.w *= s1;
     *reinterpret_cast<float4*>(ps + r * K1P + 4 * c) = v;
   }
   for (int e = tid; e < RB2 * 32; e += 256) {
@@ -754,27 +795,35 @@ __global__ __launch_bounds__(256, 2) void wdc_scan_kernel(WdScanArgs A) {
   }
   for (int e = tid; e < NOB * 32; e += 256) b3l[e] = OB > 0 ? A.b3p[e] : 0.f;
   for (int e = tid; e < NL * 32; e += 256) wdl[e] = A.wdp[e];
-  const float s1 = A.prm->s1, c2 = A.prm->c2, c3 = A.prm->c3, inv_s2 = A.prm->inv_s2;
+  const float c2 = A.prm->c2, c3 = A.prm->c3, inv_s2 = A.prm->inv_s2;
   const float g1 = A.prm->g1, g2 = A.prm->g2, g3 = A.prm->g3, g4 = A.prm->g4;
   const float cbd = A.prm->cb, absb = A.prm->absb, rho = A.prm->rho;
-  const bool active = b < A.B;
-  const float cub = active ? A.cu[b] : 0.f;
-  WaveTopK<1> L;
-  L.init();
-  int nm = WD_INT_BIG, mpos = 0, mend = 0;
-  if (A.mptr && active) {
-    int64_t lo = A.mptr[b], hi = A.mptr[b + 1];
-    while (lo < hi) {
-      const int64_t mid = (lo + hi) >> 1;
-      if (A.midx[mid] < part_start) lo = mid + 1;
-      else hi = mid;
+
+  int64_t bu[UPW];
+  bool act[UPW];
+  float cub[UPW];
+  WaveTopK<1> L[UPW];
+  int nm[UPW], mpos[UPW], mend[UPW], count[UPW];
+#pragma unroll
+  for (int v = 0; v < UPW; ++v) {
+    bu[v] = ublk + wave * UPW + v;
+    act[v] = bu[v] < A.B;
+    cub[v] = act[v] ? A.cu[bu[v]] : 0.f;
+    L[v].init();
+    nm[v] = WD_INT_BIG;
+    mpos[v] = mend[v] = count[v] = 0;
+    if (A.mptr && act[v]) {
+      int64_t lo = A.mptr[bu[v]], hi = A.mptr[bu[v] + 1];
+      while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        if (A.midx[mid] < part_start) lo = mid + 1;
+        else hi = mid;
+      }
+      mpos[v] = (int)lo;
+      mend[v] = (int)A.mptr[bu[v] + 1];
+      nm[v] = mpos[v] < mend[v] ? A.midx[mpos[v]] : WD_INT_BIG;
     }
-    mpos = (int)lo;
-    mend = (int)A.mptr[b + 1];
-    nm = mpos < mend ? A.midx[mpos] : WD_INT_BIG;
   }
-  int count = 0;
-  const int64_t seg = (b * A.NP + p) * (int64_t)A.cap;
 
   const int64_t ntiles = part_end > part_start ? hnm_cdiv(part_end - part_start, WD_TILE) : 0;
   for (int64_t t = 0; t < ntiles; ++t) {
@@ -784,86 +833,139 @@ __global__ __launch_bounds__(256, 2) void wdc_scan_kernel(WdScanArgs A) {
       const int r = e / (K1P / 4), c = e % (K1P / 4);
       const int64_t item = base + r;
       float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (item < part_end) v = *reinterpret_cast<const float4*>(A.Qi + item * K1P + 4 * c);
-      *reinterpret_cast<float4*>(&qs[r * QRS + 4 * c]) = v;
+      if (item < part_end && !((ABL & 4) && t > 0))
+        v = *reinterpret_cast<const float4*>(A.Qi + item * K1P + 4 * c);
+      v.x *= s1; v.y *= s1; v.z *= s1; v.w *= s1;
+      if (!((ABL & 4) && t > 0)) *reinterpret_cast<float4*>(&qs[r * QRS + 4 * c]) = v;
     }
     __syncthreads();
-    if (!active) continue;
+    if (!act[0]) continue;  // users are assigned in order: the wave has none
 
-    const float* prow = ps + wave * K1P + 8 * h;
     const float* qrow = qs + j * QRS + 8 * h;
-    f32x16 acc3[NOB];
+    f32x16 acc3[UPW][NOB];
 #pragma unroll
-    for (int ob = 0; ob < NOB; ++ob)
-      acc3[ob] = f32x16{0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    float fin = 0.f, bx1 = 0.f, bx2 = 0.f, bx3 = 0.f;
+    for (int v = 0; v < UPW; ++v)
+#pragma unroll
+      for (int ob = 0; ob < NOB; ++ob)
+        acc3[v][ob] = f32x16{0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    float fin[UPW], bx1[UPW], bx2[UPW], bx3[UPW];
+#pragma unroll
+    for (int v = 0; v < UPW; ++v) fin[v] = bx1[v] = bx2[v] = bx3[v] = 0.f;
 #pragma unroll 1
     for (int g = 0; g < RB2 / G2; ++g) {
-      f32x16 acc2[G2];
+      f32x16 acc2[UPW][G2];
 #pragma unroll
-      for (int gi = 0; gi < G2; ++gi)
-        acc2[gi] = f32x16{0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      for (int v = 0; v < UPW; ++v)
+#pragma unroll
+        for (int gi = 0; gi < G2; ++gi)
+          acc2[v][gi] = f32x16{0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      // k loop, software-pipelined: the f16 operands of step kb + 1 (LDS reads, relu, split:
+      // ~45 VALU per user) are formed while step kb's 3 G2 UPW MFMAs run -- one wave per
+      // SIMD issues ~5 VALU per 32-cycle MFMA gap nearly for free (MI355X_MICROARCH.md,
+      // cycle constants), so a step costs its MFMAs instead of VALU + MFMA.  hi weight
+      // fragments are prefetched one step ahead, lo fragments at the top of their step (first
+      // used 2 G2 UPW MFMAs later).  v1 . x1 accumulates in pass 0 only: later passes and the
+      // tail step read the zero row v0s, so the loop body stays branch-free for the scheduler.
+      const float* v1p = g == 0 ? v1s : v0s;
+      auto frag = [&](int gi, int kk, int hl) {
+        const int64_t q = (ABL & 1) ? (int64_t)gi * 2 : ((int64_t)(g * G2 + gi) * KB + kk) * 2;
+        return A.W2hl[(q + hl) * 64 + lane];
+      };
+      auto form = [&](int kk, const float* vrow, wh8* oh, wh8* ol) {
+        const float4 q0 = *reinterpret_cast<const float4*>(qrow + 16 * kk);
+        const float4 q1 = *reinterpret_cast<const float4*>(qrow + 16 * kk + 4);
+        const float4 va = *reinterpret_cast<const float4*>(vrow + 16 * kk + 8 * h);
+        const float4 vb = *reinterpret_cast<const float4*>(vrow + 16 * kk + 8 * h + 4);
+#pragma unroll
+        for (int v = 0; v < UPW; ++v) {
+          const float* prow = ps + (wave * UPW + v) * K1P + 8 * h + 16 * kk;
+          const float4 p0 = *reinterpret_cast<const float4*>(prow);
+          const float4 p1 = *reinterpret_cast<const float4*>(prow + 4);
+          // x1 * s1 (P, Q pre-scaled)
+          float x[8] = {fmaxf(p0.x + q0.x, 0.f), fmaxf(p0.y + q0.y, 0.f), fmaxf(p0.z + q0.z, 0.f),
+                        fmaxf(p0.w + q0.w, 0.f), fmaxf(p1.x + q1.x, 0.f), fmaxf(p1.y + q1.y, 0.f),
+                        fmaxf(p1.z + q1.z, 0.f), fmaxf(p1.w + q1.w, 0.f)};
+          float bb = bx1[v];
+          bb = fmaf(va.x, x[0], bb); bb = fmaf(va.y, x[1], bb);
+          bb = fmaf(va.z, x[2], bb); bb = fmaf(va.w, x[3], bb);
+          bb = fmaf(vb.x, x[4], bb); bb = fmaf(vb.y, x[5], bb);
+          bb = fmaf(vb.z, x[6], bb); bb = fmaf(vb.w, x[7], bb);
+          bx1[v] = bb;
+          wd_split8(x, oh[v], ol[v]);
+        }
+      };
+      wh8 xh[UPW], xl[UPW], ahn[G2];
+      form(0, v1p, xh, xl);
+#pragma unroll
+      for (int gi = 0; gi < G2; ++gi) ahn[gi] = frag(gi, 0, 0);
       for (int kb = 0; kb < KB; ++kb) {
-        wh8 ah[G2], al[G2];
+        const bool more = kb + 1 < KB;
+        const int kn = more ? kb + 1 : kb;
+        wh8 ah[G2], al[G2], nxh[UPW], nxl[UPW];
 #pragma unroll
         for (int gi = 0; gi < G2; ++gi) {
-          const int64_t q = ((int64_t)(g * G2 + gi) * KB + kb) * 2;
-          ah[gi] = A.W2hl[q * 64 + lane];
-          al[gi] = A.W2hl[(q + 1) * 64 + lane];
-        }
-        const float4 p0 = *reinterpret_cast<const float4*>(prow + 16 * kb);
-        const float4 p1 = *reinterpret_cast<const float4*>(prow + 16 * kb + 4);
-        const float4 q0 = *reinterpret_cast<const float4*>(qrow + 16 * kb);
-        const float4 q1 = *reinterpret_cast<const float4*>(qrow + 16 * kb + 4);
-        float x[8] = {fmaxf(p0.x + q0.x, 0.f), fmaxf(p0.y + q0.y, 0.f), fmaxf(p0.z + q0.z, 0.f),
-                      fmaxf(p0.w + q0.w, 0.f), fmaxf(p1.x + q1.x, 0.f), fmaxf(p1.y + q1.y, 0.f),
-                      fmaxf(p1.z + q1.z, 0.f), fmaxf(p1.w + q1.w, 0.f)};
-        if (g == 0) {
-          const float4 va = *reinterpret_cast<const float4*>(v1s + 16 * kb + 8 * h);
-          const float4 vb = *reinterpret_cast<const float4*>(v1s + 16 * kb + 8 * h + 4);
-          bx1 = fmaf(va.x, x[0], bx1); bx1 = fmaf(va.y, x[1], bx1);
-          bx1 = fmaf(va.z, x[2], bx1); bx1 = fmaf(va.w, x[3], bx1);
-          bx1 = fmaf(vb.x, x[4], bx1); bx1 = fmaf(vb.y, x[5], bx1);
-          bx1 = fmaf(vb.z, x[6], bx1); bx1 = fmaf(vb.w, x[7], bx1);
-        }
-        wh8 xh, xl;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const float xs = x[e] * s1;
-          const _Float16 hi = (_Float16)xs;
-          xh[e] = hi;
-          xl[e] = (_Float16)(xs - (float)hi);
+          ah[gi] = ahn[gi];
+          ahn[gi] = frag(gi, kn, 0);
+          al[gi] = frag(gi, kb, 1);
         }
 #pragma unroll
-        for (int gi = 0; gi < G2; ++gi) acc2[gi] = wd_mfma16(ah[gi], xh, acc2[gi]);
+        for (int gi = 0; gi < G2; ++gi)
 #pragma unroll
-        for (int gi = 0; gi < G2; ++gi) acc2[gi] = wd_mfma16(ah[gi], xl, acc2[gi]);
+          for (int v = 0; v < UPW; ++v) acc2[v][gi] = wd_mfma16(ah[gi], xh[v], acc2[v][gi]);
 #pragma unroll
-        for (int gi = 0; gi < G2; ++gi) acc2[gi] = wd_mfma16(al[gi], xh, acc2[gi]);
+        for (int gi = 0; gi < G2; ++gi)
+#pragma unroll
+          for (int v = 0; v < UPW; ++v) acc2[v][gi] = wd_mfma16(ah[gi], xl[v], acc2[v][gi]);
+#pragma unroll
+        for (int gi = 0; gi < G2; ++gi)
+#pragma unroll
+          for (int v = 0; v < UPW; ++v) acc2[v][gi] = wd_mfma16(al[gi], xh[v], acc2[v][gi]);
+        form(kn, more ? v1p : v0s, nxh, nxl);
+#pragma unroll
+        for (int v = 0; v < UPW; ++v) {
+          xh[v] = nxh[v];
+          xl[v] = nxl[v];
+        }
+        if (WDC_INTERLEAVE) {
+          // the next step's LDS reads first, then one MFMA + 4 VALU at a time
+          __builtin_amdgcn_sched_group_barrier(0x100, 4 + 2 * UPW, 0);
+#pragma unroll
+          for (int i = 0; i < 3 * G2 * UPW; ++i) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);
+          }
+        }
       }
       // x2 = relu(D2 + b2') in s2 units feeds layer 3 (or the final dot)
 #pragma unroll
       for (int gi = 0; gi < G2; ++gi) {
         const int rb = g * G2 + gi;
-        float y[16];
+        float y[UPW][16];
+        float bias16[16], vv16[16];
+#pragma unroll
+        for (int r4 = 0; r4 < 4; ++r4) {  // rows 8 r4 + 4 h + 0..3: one 16-B read each
+          const float4 bb = *reinterpret_cast<const float4*>(b2l + rb * 32 + 8 * r4 + 4 * h);
+          const float4 vq = *reinterpret_cast<const float4*>(v2l + rb * 32 + 8 * r4 + 4 * h);
+          bias16[4 * r4] = bb.x; bias16[4 * r4 + 1] = bb.y; bias16[4 * r4 + 2] = bb.z; bias16[4 * r4 + 3] = bb.w;
+          vv16[4 * r4] = vq.x; vv16[4 * r4 + 1] = vq.y; vv16[4 * r4 + 2] = vq.z; vv16[4 * r4 + 3] = vq.w;
+        }
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int row = rb * 32 + mfma32_row(r, h);
-          y[r] = fmaxf(fmaf(acc2[gi][r], c2, b2l[row]), 0.f);
-          bx2 = fmaf(v2l[row], y[r], bx2);
-          if (OB == 0) fin = fmaf(y[r], wdl[row], fin);
+          const float bias = bias16[r], vv = vv16[r], wv = wdl[OB == 0 ? row : 0];
+#pragma unroll
+          for (int v = 0; v < UPW; ++v) {
+            y[v][r] = fmaxf(fmaf(acc2[v][gi][r], c2, bias), 0.f);
+            bx2[v] = fmaf(vv, y[v][r], bx2[v]);
+            if (OB == 0) fin[v] = fmaf(y[v][r], wv, fin[v]);
+          }
         }
         if (OB > 0) {
 #pragma unroll
           for (int half2 = 0; half2 < 2; ++half2) {
-            wh8 yh, yl;
+            wh8 yh[UPW], yl[UPW];
 #pragma unroll
-            for (int e = 0; e < 8; ++e) {
-              const float ys = y[8 * half2 + e];
-              const _Float16 hi = (_Float16)ys;
-              yh[e] = hi;
-              yl[e] = (_Float16)(ys - (float)hi);
-            }
+            for (int v = 0; v < UPW; ++v) wd_split8(&y[v][8 * half2], yh[v], yl[v]);
             const int kb3 = 2 * rb + half2;
             wh8 bh[NOB], bl[NOB];
 #pragma unroll
@@ -873,68 +975,88 @@ __global__ __launch_bounds__(256, 2) void wdc_scan_kernel(WdScanArgs A) {
               bl[ob] = A.W3hl[(q + 1) * 64 + lane];
             }
 #pragma unroll
-            for (int ob = 0; ob < NOB; ++ob) acc3[ob] = wd_mfma16(bh[ob], yh, acc3[ob]);
+            for (int ob = 0; ob < NOB; ++ob)
 #pragma unroll
-            for (int ob = 0; ob < NOB; ++ob) acc3[ob] = wd_mfma16(bh[ob], yl, acc3[ob]);
+              for (int v = 0; v < UPW; ++v) acc3[v][ob] = wd_mfma16(bh[ob], yh[v], acc3[v][ob]);
 #pragma unroll
-            for (int ob = 0; ob < NOB; ++ob) acc3[ob] = wd_mfma16(bl[ob], yh, acc3[ob]);
+            for (int ob = 0; ob < NOB; ++ob)
+#pragma unroll
+              for (int v = 0; v < UPW; ++v) acc3[v][ob] = wd_mfma16(bh[ob], yl[v], acc3[v][ob]);
+#pragma unroll
+            for (int ob = 0; ob < NOB; ++ob)
+#pragma unroll
+              for (int v = 0; v < UPW; ++v) acc3[v][ob] = wd_mfma16(bl[ob], yh[v], acc3[v][ob]);
           }
         }
       }
     }
-    if (OB > 0) {
-#pragma unroll
-      for (int ob = 0; ob < NOB; ++ob) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int m = ob * 32 + mfma32_row(r, h);
-          const float z = fmaxf(fmaf(acc3[ob][r], c3, b3l[m]), 0.f);
-          fin = fmaf(z, wdl[m], fin);
-          bx3 = fmaf(fabsf(wdl[m]), z, bx3);
-        }
-      }
-    } else {
-      fin *= inv_s2;
-    }
-    fin = hnm_sum_halves(fin);
-    bx1 = hnm_sum_halves(bx1);
-    bx2 = hnm_sum_halves(bx2);
-    bx3 = hnm_sum_halves(bx3);
     const int64_t item = base + j;
     const bool ivalid = lane < 32 && item < part_end;
     const float wi = ivalid ? A.wI[item] : 0.f;
-    const float score = fin + cub + wi;
-    const float e = rho * (g1 * bx1 + g2 * (bx2 * inv_s2) + g3 * bx3 +
-                           g4 * (fabsf(fin) + fabsf(cub) + fabsf(wi)) + cbd) + absb;
-    bool masked = false;
     const int64_t tile_end = std::min<int64_t>(base + WD_TILE, part_end);
-    while (nm < tile_end) {
-      if (item == nm) masked = true;
-      ++mpos;
-      nm = mpos < mend ? A.midx[mpos] : WD_INT_BIG;
-    }
-    if (MODE == WDC_DEBUG) {
-      if (ivalid) {
-        A.dbg_a[b * A.lda + item] = score;
-        A.dbg_e[b * A.lda + item] = e;
+#pragma unroll
+    for (int v = 0; v < UPW; ++v) {
+      if (OB > 0) {
+#pragma unroll
+        for (int ob = 0; ob < NOB; ++ob) {
+#pragma unroll
+          for (int r4 = 0; r4 < 4; ++r4) {
+            const float4 b3 = *reinterpret_cast<const float4*>(b3l + ob * 32 + 8 * r4 + 4 * h);
+            const float4 w4 = *reinterpret_cast<const float4*>(wdl + ob * 32 + 8 * r4 + 4 * h);
+            const float bq[4] = {b3.x, b3.y, b3.z, b3.w}, wq[4] = {w4.x, w4.y, w4.z, w4.w};
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const float z = fmaxf(fmaf(acc3[v][ob][4 * r4 + e], c3, bq[e]), 0.f);
+              fin[v] = fmaf(z, wq[e], fin[v]);
+              bx3[v] = fmaf(fabsf(wq[e]), z, bx3[v]);
+            }
+          }
+        }
+      } else {
+        fin[v] *= inv_s2;
       }
-      continue;
+      const float fv = hnm_sum_halves(fin[v]);
+      const float b1 = hnm_sum_halves(bx1[v]);
+      const float b2 = hnm_sum_halves(bx2[v]);
+      const float b3 = hnm_sum_halves(bx3[v]);
+      const float score = fv + cub[v] + wi;
+      const float e = rho * (g1 * b1 + g2 * (b2 * inv_s2) + g3 * b3 +
+                             g4 * (fabsf(fv) + fabsf(cub[v]) + fabsf(wi)) + cbd) + absb;
+      bool masked = false;
+      while (nm[v] < tile_end) {
+        if (item == nm[v]) masked = true;
+        ++mpos[v];
+        nm[v] = mpos[v] < mend[v] ? A.midx[mpos[v]] : WD_INT_BIG;
+      }
+      if (!act[v]) continue;
+      if (MODE == WDC_DEBUG) {
+        if (ivalid) {
+          A.dbg_a[bu[v] * A.lda + item] = score;
+          A.dbg_e[bu[v] * A.lda + item] = e;
+        }
+        continue;
+      }
+      const bool ok = ivalid && !masked;
+      const float lb = score - e, ub = score + e;
+      L[v].offer(lb, (int)item, ok, A.K);
+      const bool app = ok && ub >= L[v].thr_v;
+      const uint64_t m = __ballot(app);
+      const int pos = count[v] + __popcll(m & ((1ull << lane) - 1));
+      const int64_t seg = (bu[v] * A.NP + p) * (int64_t)A.cap;
+      if (app && pos < A.cap) {
+        A.segi[seg + pos] = (int32_t)item;
+        A.segu[seg + pos] = ub;
+      }
+      count[v] += __popcll(m);
     }
-    const bool ok = ivalid && !masked;
-    const float lb = score - e, ub = score + e;
-    L.offer(lb, (int)item, ok, A.K);
-    const bool app = ok && ub >= L.thr_v;
-    const uint64_t m = __ballot(app);
-    const int pos = count + __popcll(m & ((1ull << lane) - 1));
-    if (app && pos < A.cap) {
-      A.segi[seg + pos] = (int32_t)item;
-      A.segu[seg + pos] = ub;
-    }
-    count += __popcll(m);
   }
-  if (MODE == WDC_THRESH && active) {
-    L.store(A.lbv + (b * A.NP + p) * A.K, A.lbi + (b * A.NP + p) * A.K, A.K);
-    if (lane == 0) A.cnt[b * A.NP + p] = count;
+  if (MODE == WDC_THRESH) {
+#pragma unroll
+    for (int v = 0; v < UPW; ++v) {
+      if (!act[v]) continue;
+      L[v].store(A.lbv + (bu[v] * A.NP + p) * A.K, A.lbi + (bu[v] * A.NP + p) * A.K, A.K);
+      if (lane == 0) A.cnt[bu[v] * A.NP + p] = count[v];
+    }
   }
 }
 
@@ -1115,8 +1237,9 @@ static hnm_status wd_shape(const hnm_widedeep_weights* w, WdPrep* pr) {
   return HNM_OK;
 }
 
-static void wd_partition(const hnm_ctx* ctx, int64_t B, int64_t I, int64_t* np, int64_t* ipp) {
-  const int64_t ublocks = hnm_cdiv(B, 4);
+static void wd_partition(const hnm_ctx* ctx, int64_t B, int64_t I, int64_t* np, int64_t* ipp,
+                         int upb = 4) {
+  const int64_t ublocks = hnm_cdiv(B, upb);
   const int64_t want = std::max<int64_t>(1, hnm_cdiv(2 * (int64_t)ctx->num_cus, ublocks));
   int64_t n = std::min<int64_t>(want, std::max<int64_t>(1, hnm_cdiv(I, 4 * WD_TILE)));
   *ipp = hnm_cdiv(hnm_cdiv(I, n), WD_TILE) * WD_TILE;
@@ -1301,10 +1424,13 @@ struct WdcWs {
 };
 constexpr int WDC_STAT_BLOCKS = 1024;
 
+// users per wave of the certified scan: 2 for the wide default tower (weight-fragment reuse)
+static int wdc_upw(const WdPrep& pr) { return pr.RB2 == 8 && pr.OB == 4 ? 2 : 1; }
+
 static size_t wdc_carve(const hnm_ctx* ctx, const WdPrep& pr, int64_t B, int64_t I, int K,
                         char* base, WdcWs* c) {
   int64_t np, ipp;
-  wd_partition(ctx, B, I, &np, &ipp);
+  wd_partition(ctx, B, I, &np, &ipp, 4 * wdc_upw(pr));
   const int cap = (int)std::min<int64_t>(WDC_CAP, ipp);
   const int K1P = pr.K1P, KB = K1P / 16;
   const int64_t fbn = 8 * (int64_t)ctx->num_cus + 4 + B;  // bound on n * np(n) over n <= B
@@ -1356,10 +1482,11 @@ static hnm_status wdc_prepare(hnm_ctx* ctx, const hnm_widedeep_weights* w, const
   return HNM_OK;
 }
 
-template <int RB2, int OB, int MODE>
+template <int RB2, int OB, int MODE, int ABL = 0>
 static void wdc_launch_scan(hnm_ctx* ctx, dim3 grid, size_t lds, const WdScanArgs& a) {
   constexpr int G2 = RB2 < 4 ? RB2 : 4;
-  auto kern = wdc_scan_kernel<RB2, OB, G2, MODE>;
+  constexpr int UPW = RB2 == 8 && OB == 4 ? 2 : 1;  // = wdc_upw
+  auto kern = wdc_scan_kernel<RB2, OB, G2, MODE, UPW, ABL>;
   hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   hipLaunchKernelGGL(kern, grid, dim3(256), lds, ctx->stream, a);
 }
@@ -1404,15 +1531,23 @@ static hnm_status wdc_scan(hnm_ctx* ctx, const hnm_widedeep_weights* w, const Wd
   a.dbg_a = dbg_a;
   a.dbg_e = dbg_e;
   a.lda = lda;
+  const int upb = 4 * wdc_upw(pr);
   const size_t lds =
-      (size_t)(32 * (S.K1P + 4) + 5 * S.K1P + 2 * pr.RB2 * 32 + NOB * 32 + NL * 32) * 4;
-  dim3 grid((unsigned)hnm_cdiv(B, 4), (unsigned)c.np);
+      (size_t)(32 * (S.K1P + 4) + (upb + 2) * S.K1P + 2 * pr.RB2 * 32 + NOB * 32 + NL * 32) * 4;
+  dim3 grid((unsigned)hnm_cdiv(B, upb), (unsigned)c.np);
   if (mode == WDC_THRESH) hnm_timer_begin(ctx, HNM_TIME_SCORE);
 #define WDC_CASE(R, O)                                                        \
   if (pr.RB2 == R && pr.OB == O) {                                            \
     if (mode == WDC_THRESH) wdc_launch_scan<R, O, WDC_THRESH>(ctx, grid, lds, a); \
     else wdc_launch_scan<R, O, WDC_DEBUG>(ctx, grid, lds, a);                 \
   }
+  // tuning ablations (HNM_OPT_SCAN_USERS 101..103, timing only: results are garbage)
+  if (pr.RB2 == 8 && pr.OB == 4 && ctx->scan_users > 100 && mode == WDC_THRESH) {
+    if (ctx->scan_users == 101) wdc_launch_scan<8, 4, WDC_THRESH, 1>(ctx, grid, lds, a);
+    if (ctx->scan_users == 102) wdc_launch_scan<8, 4, WDC_THRESH, 2>(ctx, grid, lds, a);
+    if (ctx->scan_users == 103) wdc_launch_scan<8, 4, WDC_THRESH, 3>(ctx, grid, lds, a);
+    if (ctx->scan_users == 104) wdc_launch_scan<8, 4, WDC_THRESH, 4>(ctx, grid, lds, a);
+  } else
   WDC_CASE(8, 4)
   WDC_CASE(4, 2)
   WDC_CASE(2, 1)
