@@ -20,8 +20,10 @@ Also printed in the same JSON line:
                   average duration (HIP events on the ctx stream, measured live here),
                   vs the MFMA peak of the kernel's dtype; `traffic` from the committed
                   rocprofv3 PMC summary (profiles/) when present for this workload.
-  cpu_baseline -- the CPU oracle (numpy restatement of the reference, op for op) on a
-                  bounded user sample, rank 0 at N=1 only.
+  exact_fp32   -- the same step with the pre-filter off (every pair in exact fp32).
+  cpu_baseline -- the reference's PyTorch-CPU path (oracle/torch_cpu.py: its torch ops
+                  restated, pinned to the reference goldens) on a bounded user sample,
+                  on the host's cores, rank 0 at N=1 only.
 """
 from __future__ import annotations
 
@@ -56,10 +58,31 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+def launch_ranks(n_gpus):
+    """`bench.py --gpus N` (N > 1) started without a launcher: run N ranks through
+    torch.distributed.run as a CHILD process and return its exit code.  This process has
+    not touched the GPU (no HIP call before this point), and it does not exec."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={n_gpus}", "--master-addr=127.0.0.1", f"--master-port={port}",
+           os.path.abspath(__file__), *sys.argv[1:]]
+    log(f"launching {n_gpus} ranks: {' '.join(cmd)}")
+    return subprocess.call(cmd, env=env)
+
+
 def setup_dist(n_gpus):
     """One process per GPU; backend "nccl" (= RCCL over xGMI).  HNM_DIST_BACKEND=gloo
     rehearses the sharded path on fewer GPUs than ranks (collectives staged through host)."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != n_gpus:
+        raise SystemExit(f"bench.py --gpus {n_gpus} but WORLD_SIZE={world}: launch one rank "
+                         "per GPU (torch.distributed.run --nproc-per-node N)")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
@@ -99,7 +122,8 @@ def build_workload(name, rank, world, device, batch, exact=False):
         d = 64 if name == "lightgcn" else 128
         sd = syn.lightgcn_state_dict(U, I, d, seed=0)
         m = LightGCN(U, I, embedding_dim=d, num_layers=3)
-        m.set_graph(torch.from_numpy(syn.bipartite_edge_index(U, I, syn.HM_INTERACTIONS, seed=2)))
+        edges = syn.bipartite_edge_index(U, I, syn.HM_INTERACTIONS, seed=2)
+        m.set_graph(torch.from_numpy(edges))
         m = load(m, sd, device)
         g = m._device_graph()
 
@@ -122,7 +146,7 @@ def build_workload(name, rank, world, device, batch, exact=False):
         info["_serving"] = lambda: scorer(m.propagate(g))
         ret = dict(step=lgcn_step, per_launch=per_launch, bound="hbm",
                    kernel="spmm layer (spmm_light + segment + finish)", timing=_lib.TIME_SPMM)
-        return ret, info, None
+        return ret, info, ("lightgcn", (sd, edges, d))
     elif name == "widedeep":
         sd = syn.widedeep_state_dict(U, I, 64, (512, 256, 128), seed=0)
         m = load(WideDeep(U, I), sd, device)
@@ -132,7 +156,7 @@ def build_workload(name, rank, world, device, batch, exact=False):
         bound, kernel = "mfma", ("widedeep_score_kernel" if exact else "wdc_scan_kernel")
         info["scan"] = ("exact fp32" if exact else
                         "certified split-f16 (3 f16 MFMA passes) pre-filter + exact fp32 re-scoring")
-        cpu = None
+        cpu = ("widedeep", None)
     elif name == "mf":
         sd = syn.mf_state_dict(U, I, 64, seed=0)
         m = load(MatrixFactorization(U, I, sparse=False), sd, device)
@@ -141,7 +165,7 @@ def build_workload(name, rank, world, device, batch, exact=False):
         per_launch = 2.0 * 64 * batch * world * (hi - lo)
         info = {"model": "MatrixFactorization", "embedding_dim": 64}
         bound, kernel = "mfma", ("dot_score_kernel" if exact else "dot16_scan_kernel")
-        cpu = None
+        cpu = ("mf", sd)
     else:
         raise SystemExit(f"unknown workload {name}")
     rec = S.ItemShardedRecommender(local, S.hip_merge, K, lo, rank, world)
@@ -150,28 +174,79 @@ def build_workload(name, rank, world, device, batch, exact=False):
     return ret, info, cpu
 
 
-def cpu_baseline(cpu, seconds_budget=20.0):
-    """Time the CPU oracle (numpy restatement of the reference) on a bounded user sample."""
-    if cpu is None:
-        return None
-    from oracle import hnm_oracle as O  # baseline leg only
-    kind, sd = cpu
-    cores = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
-    torch.set_num_threads(cores)
-    users = syn.user_batch(syn.HM_USERS, 64, seed=7)
-    O.recommend(O.ncf_predict_all_items(sd, users[:8]), users[:8], K)  # warm-up
+def _median_rate(fn, users, runs, budget_s):
+    """users/s of fn(users): median of up to `runs` timed calls within ~budget_s."""
     times = []
     t_start = time.perf_counter()
-    while len(times) < 3 and time.perf_counter() - t_start < seconds_budget:
+    while len(times) < runs and (not times or time.perf_counter() - t_start < budget_s):
         t0 = time.perf_counter()
-        O.recommend(O.ncf_predict_all_items(sd, users), users, K)
+        fn(users)
         times.append(time.perf_counter() - t0)
-    med = float(np.median(times))
-    return {"value": round(len(users) / med, 3), "unit": "users/s", "cores": cores,
-            "kind": "port",
-            "sample": f"oracle.ncf_predict_all_items + topk(12), B={len(users)} users x "
-                      f"{syn.HM_ITEMS} items (1000-item chunks as neural_cf.py:167), "
-                      f"median of {len(times)} runs, numpy fp32 BLAS on {cores} threads"}
+    return len(users) / float(np.median(times)), len(times)
+
+
+def cpu_baseline(cpu):
+    """The reference's PyTorch-CPU path (oracle/torch_cpu.py: the reference's torch ops
+    restated, checked against the reference-produced goldens) on a bounded user sample,
+    on this host's cores (the box's CPU share = OMP_NUM_THREADS)."""
+    if cpu is None:
+        return None
+    from oracle import torch_cpu as T  # baseline leg only
+    kind, payload = cpu
+    cores = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    torch.set_num_threads(cores)
+    U, I = syn.HM_USERS, syn.HM_ITEMS
+    out = {"unit": "users/s", "cores": cores, "kind": "port"}
+    if kind == "ncf":
+        sd = T.as_torch(payload)
+        users = torch.from_numpy(syn.user_batch(U, 64, seed=7))
+        T.ncf_recommend(sd, users[:8])  # warm-up
+        v, n = _median_rate(lambda u: T.ncf_recommend(sd, u), users, 3, 20.0)
+        out["sample"] = (f"torch restatement of NeuralCF.recommend (neural_cf.py:143-208,300-326: "
+                         f"gathers, expand+cat in 1000-item chunks, Linear/ReLU, topk), B=64 x "
+                         f"{I} items, median of {n}")
+    elif kind == "mf":
+        sd = T.as_torch(payload)
+        users = torch.from_numpy(syn.user_batch(U, 4096, seed=7))
+        T.mf_recommend(sd, users[:64])
+        v, n = _median_rate(lambda u: T.mf_recommend(sd, u), users, 3, 20.0)
+        out["sample"] = (f"torch restatement of MatrixFactorization.recommend "
+                         f"(matrix_factorization.py:108-131,220-246), B=4096 x {I} items, "
+                         f"median of {n}")
+    elif kind == "lightgcn":
+        sd, edges, d = payload
+        t0 = time.perf_counter()
+        graph = T.lightgcn_graph(torch.from_numpy(edges), U + I)
+        t_graph = time.perf_counter() - t0
+        w = torch.from_numpy(sd["embeddings.weight"])
+        t0 = time.perf_counter()
+        fu, fi = T.lightgcn_forward(w, graph, U)
+        t_prop = time.perf_counter() - t0
+        users = torch.from_numpy(syn.user_batch(U, 4096, seed=7))
+        T.lightgcn_recommend(fu, fi, users[:64])
+        r_score, n = _median_rate(lambda u: T.lightgcn_recommend(fu, fi, u), users, 3, 10.0)
+        # the reference's recommend() re-propagates on every call (lightgcn.py:197)
+        v = 4096 / (t_prop + 4096 / r_score)
+        out["scoring_only_users_per_s"] = round(r_score, 2)
+        out["propagation_s"] = round(t_prop, 3)
+        out["sample"] = (f"torch restatement of LightGCN.recommend: 3-layer propagation "
+                         f"(lightgcn.py:136-164, torch.sparse.mm on CSR; set_graph {t_graph:.1f}s "
+                         f"not counted) + F_U[ids] @ F_I^T + topk (:188-204), B=4096 x {I} "
+                         f"items, d={d}, one propagation + median of {n} scorings")
+    elif kind == "widedeep":
+        # full U is infeasible on the reference path (one-hot [500, U+I] per user per
+        # chunk): timed at U=10,000 with the full item catalogue, one user
+        Uc = 10_000
+        sd = T.as_torch(syn.widedeep_state_dict(Uc, I, 64, (512, 256, 128), seed=0))
+        users = torch.from_numpy(syn.user_batch(Uc, 1, seed=7))
+        v, n = _median_rate(lambda u: T.widedeep_recommend(sd, u), users, 1, 0.0)
+        out["sample"] = (f"torch restatement of WideDeep.recommend (wide_deep.py:157-285,405-435: "
+                         f"one-hot wide input, deep tower, 500-item chunks) at U=10,000 (full U "
+                         f"infeasible on the reference path), B=1 x {I} items, one run")
+    else:
+        return None
+    out["value"] = round(v, 3)
+    return out
 
 
 def pmc_traffic(workload):
@@ -197,6 +272,8 @@ def main():
     ap.add_argument("--exact", action="store_true",
                     help="exact fp32 scan of every item instead of the certified f16 pre-filter")
     args = ap.parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus))
 
     rank, world, device = setup_dist(args.gpus)
     B = args.batch
@@ -236,6 +313,24 @@ def main():
     step(batches[0])
     _lib.set_option(device, _lib.HNM_OPT_STATS, 0)
     pf_rows, pf_cands, pf_fallback = _lib.prefilter_stats(device, reset=True)
+    exact_rate = None
+    if not args.exact:
+        # the like-for-like fp32 path (HNM_OPT_PREFILTER=0: every pair scored in exact fp32
+        # arithmetic), timed the same way on the same batches, reported beside `value`
+        _lib.set_prefilter(device, False)
+        nexact = min(args.steps, 3 if args.workload == "widedeep" else 10)
+        step(batches[0])
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        te = time.perf_counter()
+        for j in range(nexact):
+            step(batches[j % nb])
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        exact_rate = (time.perf_counter() - te, nexact)
+        _lib.set_prefilter(device, True)
     if world > 1:
         on_host = dist.get_backend() == "gloo"
         t = torch.tensor([elapsed, ktime_ms / max(launches, 1)], dtype=torch.float64,
@@ -247,6 +342,11 @@ def main():
 
     users_total = B * world * args.steps
     value = users_total / elapsed
+    if exact_rate is not None and world > 1:
+        on_host = dist.get_backend() == "gloo"
+        t = torch.tensor([exact_rate[0]], dtype=torch.float64, device="cpu" if on_host else device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        exact_rate = (float(t[0]), exact_rate[1])
     f16 = kernel in ("ncf16_scan_kernel", "dot16_scan_kernel", "wdc_scan_kernel")
     if bound == "hbm":
         achieved = per_launch / (avg_kernel_ms * 1e-3) / 1e9
@@ -294,6 +394,11 @@ def main():
         line["serving_cached_propagation"] = {
             "value": round(B * args.steps / (time.perf_counter() - ts), 2), "unit": "users/s",
             "note": "top-K scan only, propagation computed once outside the timed loop"}
+    if exact_rate is not None:
+        line["exact_fp32"] = {
+            "value": round(B * world * exact_rate[1] / exact_rate[0], 2), "unit": "users/s",
+            "steps": exact_rate[1],
+            "note": "same step with HNM_OPT_PREFILTER=0: every (user, item) pair in exact fp32"}
     if pf_rows:
         line["prefilter"] = {"rows": pf_rows, "candidates_per_row": round(
             pf_cands / max(pf_rows - pf_fallback, 1), 1), "fallback_rows": pf_fallback,

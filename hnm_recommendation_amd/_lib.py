@@ -52,6 +52,7 @@ _SIGS = {
     "hnm_ctx_reserve": (_i32, [_p, C.c_size_t]),
     "hnm_ctx_check": (_i32, [_p]),
     "hnm_ctx_num_cus": (_i32, [_p, C.POINTER(C.c_int)]),
+    "hnm_ctx_abort_pending": (_i32, [_p]),
     "hnm_ctx_enable_timing": (_i32, [_p, C.c_int]),
     "hnm_ctx_timing": (_i32, [_p, C.POINTER(C.c_double), C.POINTER(_i64)]),
     "hnm_ctx_set_option": (_i32, [_p, C.c_int, _i64]),
@@ -97,7 +98,7 @@ _SIGS = {
 }
 
 _lib = None
-_lock = threading.Lock()
+_lock = threading.RLock()
 _ctxs: dict = {}
 
 
@@ -158,19 +159,41 @@ def require_gpu(*tensors):
                 "There is no CPU path.")
 
 
-def ctx(device: torch.device):
-    """Per-device hnm_ctx bound to torch's current stream on that device."""
+def _dev_index(device) -> int:
     dev = torch.device(device)
-    idx = dev.index if dev.index is not None else torch.cuda.current_device()
-    c = _ctxs.get(idx)
+    return dev.index if dev.index is not None else torch.cuda.current_device()
+
+
+_opts: dict = {}  # device -> {option: value}, applied to every ctx of that device
+
+
+def ctx(device: torch.device):
+    """The calling thread's hnm_ctx on `device`, bound to torch's current stream.
+
+    One ctx per (device, thread): a ctx owns a workspace and the state of an open two-phase
+    call, so concurrent callers (a threaded server) never share them.  Switching streams
+    is ordered inside the library (hnm_ctx_set_stream queues the new stream behind the old)."""
+    idx = _dev_index(device)
+    key = (idx, threading.get_ident())
+    c = _ctxs.get(key)
     if c is None:
-        h = _p()
-        check(fn("hnm_ctx_create")(idx, C.byref(h)), "hnm_ctx_create")
-        c = h
-        _ctxs[idx] = c
+        with _lock:
+            c = _ctxs.get(key)
+            if c is None:
+                h = _p()
+                check(fn("hnm_ctx_create")(idx, C.byref(h)), "hnm_ctx_create")
+                c = h
+                for opt, val in _opts.get(idx, {}).items():
+                    check(fn("hnm_ctx_set_option")(c, int(opt), int(val)), "hnm_ctx_set_option")
+                _ctxs[key] = c
     stream = torch.cuda.current_stream(idx).cuda_stream
     check(fn("hnm_ctx_set_stream")(c, _p(stream)), "hnm_ctx_set_stream")
     return c
+
+
+def abort_pending(device):
+    """Close an open two-phase top-K call on this thread's ctx (after a failed exchange)."""
+    check(fn("hnm_ctx_abort_pending")(ctx(device)), "hnm_ctx_abort_pending")
 
 
 def sync_check(device):
@@ -200,13 +223,19 @@ HNM_OPT_STATS = 3
 
 
 def set_option(device, option, value):
-    check(fn("hnm_ctx_set_option")(ctx(device), int(option), int(value)), "hnm_ctx_set_option")
+    """Set a ctx option for every thread's ctx on `device` (current and future)."""
+    idx = _dev_index(device)
+    ctx(device)  # validates through the library first
+    with _lock:
+        _opts.setdefault(idx, {})[int(option)] = int(value)
+        handles = [h for (d, _), h in _ctxs.items() if d == idx]
+    for h in handles:
+        check(fn("hnm_ctx_set_option")(h, int(option), int(value)), "hnm_ctx_set_option")
 
 
 def set_prefilter(device, on=True):
-    """Certified f16 pre-filter for NCF top-K (default on); off = exact fp32 scan."""
-    check(fn("hnm_ctx_set_option")(ctx(device), HNM_OPT_PREFILTER, int(bool(on))),
-          "hnm_ctx_set_option")
+    """Certified f16 pre-filter for top-K (default on); off = exact fp32 scan."""
+    set_option(device, HNM_OPT_PREFILTER, int(bool(on)))
 
 
 def prefilter_stats(device, reset=False):

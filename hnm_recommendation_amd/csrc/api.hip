@@ -36,6 +36,7 @@ extern "C" hnm_status hnm_ctx_create(int device, hnm_ctx** out) {
     return HNM_ENOMEM;
   }
   HNM_HIP_CHECK(hipMemset(c->err_dev, 0, 64));
+  HNM_HIP_CHECK(hipEventCreateWithFlags(&c->chain_ev, hipEventDisableTiming));
   // counters of the certified pre-filter live in the same allocation (8-byte aligned)
   c->stats_dev = reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(c->err_dev) + 8);
   *out = c;
@@ -54,13 +55,26 @@ extern "C" hnm_status hnm_ctx_destroy(hnm_ctx* ctx) {
   free(ctx->ev1);
   if (ctx->ws) (void)hipFree(ctx->ws);
   if (ctx->err_dev) (void)hipFree(ctx->err_dev);
+  (void)hipEventDestroy(ctx->chain_ev);
   free(ctx);
   return HNM_OK;
 }
 
 extern "C" hnm_status hnm_ctx_set_stream(hnm_ctx* ctx, void* s) {
   HNM_REQUIRE(ctx, HNM_EINVAL, "ctx is NULL");
-  ctx->stream = (hipStream_t)s;
+  const hipStream_t ns = (hipStream_t)s;
+  if (ns == ctx->stream) return HNM_OK;
+  // The workspace and the two-phase tables are shared by every call on this ctx: queue the
+  // new stream behind everything already issued on the old one (no host sync).
+  HNM_HIP_CHECK(hipEventRecord(ctx->chain_ev, ctx->stream));
+  HNM_HIP_CHECK(hipStreamWaitEvent(ns, ctx->chain_ev, 0));
+  ctx->stream = ns;
+  return HNM_OK;
+}
+
+extern "C" hnm_status hnm_ctx_abort_pending(hnm_ctx* ctx) {
+  HNM_REQUIRE(ctx, HNM_EINVAL, "ctx is NULL");
+  ctx->pend.kind = 0;
   return HNM_OK;
 }
 

@@ -33,6 +33,9 @@ from .models import LightGCN, MatrixFactorization, NeuralCF, WideDeep
 
 logger = logging.getLogger(__name__)
 
+# serve.py:56: RecommendationRequest.num_items = Field(12, ge=1, le=100)
+MAX_NUM_ITEMS = 100
+
 # serve.py:238-248, tested in this order
 _DISPATCH = (("matrix_factorization", MatrixFactorization), ("neural_cf", NeuralCF),
              ("wide_deep", WideDeep), ("lightgcn", LightGCN))
@@ -162,8 +165,10 @@ class Recommender:
 
     # ------------------------------------------------------------------ requests
     def _score_batch(self, model, idx: List[int], num_items: int, filter_purchased: bool):
-        if not 1 <= num_items <= self.num_items:
-            raise ValueError(f"num_items must be in [1, {self.num_items}]")
+        # serve.py:56 RecommendationRequest: num_items = Field(12, ge=1, le=100)
+        hi = min(MAX_NUM_ITEMS, self.num_items)
+        if isinstance(num_items, bool) or not isinstance(num_items, int) or not 1 <= num_items <= hi:
+            raise ValueError(f"num_items must be an integer in [1, {hi}]")
         users = torch.tensor(idx, dtype=torch.int64).to(self.device)
         hist = None
         if filter_purchased:

@@ -13,9 +13,9 @@ The reference has no distributed code; this is the MI355X design:
   `all_reduce(MAX)` of those G*B floats gives every rank the best bound of all shards, and
   `finish` keeps only items that can be in the global top-k (candidates per user stay
   ~constant as G grows instead of G x; rows may come back short, padded with -inf / -1);
-* one `all_to_all` returns to every rank the G candidate lists (k scores + global item
-  ids) of ITS users (B*k*(4+8) bytes per rank pair: latency-bound on xGMI, so one
-  collective, not a ring of per-layer exchanges);
+* one `all_to_all` returns to every rank the G candidate lists (k score bits + global
+  item ids, packed as int32 pairs) of ITS users (B*k*8 bytes per rank pair: latency-bound
+  on xGMI, so one collective, not a ring of per-layer exchanges);
 * the owner merges G*k candidates per user with the HIP merge kernel.  The order
   (score desc, item asc) is total, so the result is exactly the single-GPU top-k.
 
@@ -69,17 +69,28 @@ class ItemShardedRecommender:
         all_ids = all_ids.to(dev)
         if hasattr(self.local_topk, "begin"):
             # two-phase local scorer: global lower bounds of each user's k-th best score
-            lb = stage(self.local_topk.begin(all_ids).contiguous())
-            dist.all_reduce(lb, op=dist.ReduceOp.MAX, group=self.group)
+            try:
+                lb = stage(self.local_topk.begin(all_ids).contiguous())
+                dist.all_reduce(lb, op=dist.ReduceOp.MAX, group=self.group)
+            except BaseException:
+                abort = getattr(self.local_topk, "abort", None)
+                if abort is not None:
+                    abort()  # close the open two-phase call so the ctx stays usable
+                raise
             v, i = self.local_topk.finish(all_ids, lb.to(dev))  # [G*B, k], shard-local ids
         else:
             v, i = self.local_topk(all_ids)  # [G*B, k], shard-local ids
         i = torch.where(i >= 0, i + self.item_offset, i)
-        v, i = stage(v.contiguous().reshape(-1)), stage(i.contiguous().reshape(-1))
-        rv, ri = torch.empty_like(v), torch.empty_like(i)
-        dist.all_to_all_single(rv, v, group=self.group)
-        dist.all_to_all_single(ri, i, group=self.group)
-        return self.merge(rv.to(dev).view(G, B, k), ri.to(dev).view(G, B, k), k)
+        # ONE exchange: (score bits, global item id) packed as int32 pairs -- item ids are
+        # < 2^31 -- so values and ids travel in a single all_to_all (B*k*8 bytes per pair)
+        packed = torch.stack([v.contiguous().view(torch.int32), i.to(torch.int32)], dim=-1)
+        packed = stage(packed.reshape(-1))
+        recv = torch.empty_like(packed)
+        dist.all_to_all_single(recv, packed, group=self.group)
+        recv = recv.to(dev).view(G, B, k, 2)
+        rv = recv.view(torch.float32)[..., 0].contiguous()
+        ri = recv[..., 1].to(torch.int64)
+        return self.merge(rv, ri, k)
 
 
 # ------------------------------------------------------------------ HIP wiring
@@ -146,6 +157,11 @@ class ncf_shard_topk:
         self._open = (w, keep, u, kk)  # finish must pass the same ids / tables
         return lb
 
+    def abort(self):
+        if self._open is not None:
+            _lib.abort_pending(self._open[2].device)
+            self._open = None
+
     def finish(self, user_ids: torch.Tensor, lb: torch.Tensor):
         w, keep, u, kk = self._open
         self._open = None
@@ -194,6 +210,11 @@ class dot_shard_topk:
                                                      _lib.ptr(lb)), "hnm_dot_topk_begin_f32")
         self._open = (u, kk)  # finish must pass the same ids
         return lb
+
+    def abort(self):
+        if self._open is not None:
+            _lib.abort_pending(self._open[0].device)
+            self._open = None
 
     def finish(self, user_ids: torch.Tensor, lb: torch.Tensor):
         u, kk = self._open

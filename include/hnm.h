@@ -12,7 +12,10 @@
  *    allocator); the library never frees caller memory.  Shapes are row-major, fp32
  *    tables with an explicit leading dimension, int64 ids.
  *  - Calls are asynchronous and stream-ordered on the ctx stream (hnm_ctx_set_stream:
- *    torch's current stream).  One ctx per device; a ctx is not re-entrant.
+ *    torch's current stream).  A ctx is not re-entrant: use one per (device, thread)
+ *    (the Python layer does).  Switching a ctx to another stream queues the new stream
+ *    behind the work already issued on the old one (event wait, no host sync), so the
+ *    ctx workspace is never reused while a kernel on the previous stream still reads it.
  *  - Status: 0 on success, negative on error; hnm_last_error() holds a thread-local
  *    message.  No C++ exception crosses the ABI.
  *  - Out-of-range user/item ids never fault: the row is skipped (index -1 / NaN) and the
@@ -56,6 +59,9 @@ hnm_status hnm_ctx_set_stream(hnm_ctx* ctx, void* hip_stream);
 hnm_status hnm_ctx_reserve(hnm_ctx* ctx, size_t bytes);   /* pre-grow workspace */
 hnm_status hnm_ctx_check(hnm_ctx* ctx);                   /* sync; HNM_EOOB if flagged */
 hnm_status hnm_ctx_num_cus(hnm_ctx* ctx, int* out);
+/* Close an open two-phase top-K call (hnm_*_topk_begin_f32 without its _finish), e.g.
+ * after a failed cross-shard exchange; the begin phase's tables are discarded. */
+hnm_status hnm_ctx_abort_pending(hnm_ctx* ctx);
 /* Options.  HNM_OPT_PREFILTER (default 1): NCF and dot-product top-K scan the catalogue
  * with the certified f16 pre-filter and re-score the surviving candidates in exact fp32
  * (results identical to the fp32 scan); 0 = exact fp32 scan of every item. */

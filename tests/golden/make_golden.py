@@ -3,7 +3,10 @@
 Run in the build container only (it reads /root/reference, which does not exist on the
 GPU box):
 
-    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py [small] [full]
+
+(`small`: the small-shape fixtures; `full`: the full-catalogue I = 105,542 fixtures --
+`full_fast` without Wide&Deep, `full_widedeep` Wide&Deep only, ~20 s per user.)
 
 The reference `src.models` is imported read-only with the four stubs of SURVEY.md §8(c)
 (none of them touches the arithmetic except the torch_sparse SpMM/degree stand-in, which
@@ -315,12 +318,120 @@ def gen_metrics():
          scores=scores, target=target, mask=mask, **out)
 
 
+# --------------------------------------------------------------------------------------
+# Full-catalogue fixtures (I = 105,542): the certified f16 scans only engage at
+# I >= 8192, so these pin the kernels behind the headline directly to the reference.
+# Weights are regenerated by the tests from the same PCG64 recipes; only seeds, user ids
+# and the reference's outputs are stored.
+def _topk_record(dense, rec, user_ids, n_slice=8, slice_step=97):
+    """Reference top-K plus what an exact comparison needs: the top-K scores, the gap
+    between the K-th and (K+1)-th best score, the row's score scale, and a strided slice
+    of the dense rows of the first users."""
+    k = rec.shape[1]
+    srt = -np.sort(-dense, axis=1)
+    return dict(user_ids=user_ids, topk=rec, topk_scores=np.take_along_axis(dense, rec, 1),
+                kth=srt[:, k - 1], kth_gap=srt[:, k - 1] - srt[:, k],
+                row_absmax=np.abs(np.where(np.isfinite(dense), dense, 0)).max(1),
+                dense_slice=dense[:n_slice, ::slice_step], slice_step=slice_step)
+
+
+def gen_full_ncf(models):
+    U, I, K = syn.HM_USERS, syn.HM_ITEMS, 12
+    for tag, kw in (("ncf_full.npz", {}),
+                    # personalised: GMF-heavy weights with user-specific best items
+                    ("ncf_full_personal.npz", dict(bias_scale=0.05, emb_scale=20.0))):
+        sd = syn.ncf_state_dict(U, I, 64, (128, 64, 32), seed=0, **kw)
+        m = load(models.NeuralCF(num_users=U, num_items=I, top_k=K), sd)
+        users = syn.user_batch(U, 128, seed=11)
+        fdict = syn.filter_dict(users[:32], I, per_user=23, seed=3)
+        with torch.no_grad():
+            ut = torch.from_numpy(users)
+            dense = m.predict_all_items(ut).numpy()
+            rec = m.recommend(ut).numpy()
+            rec_f = m.recommend(ut[:32], filter_items=fdict).numpy()
+        masked = dense[:32].copy()
+        for r, u in enumerate(users[:32].tolist()):
+            masked[r, list(fdict.get(u, ()))] = -np.inf
+        fk, fp, fi = dict_to_arrays(fdict)
+        filt = {f"f_{k}": v for k, v in _topk_record(masked, rec_f, users[:32], 0).items()}
+        save(tag, U=U, I=I, K=K, seed=0, emb_scale=kw.get("emb_scale", 1.0),
+             bias_scale=kw.get("bias_scale", 0.0), filter_keys=fk, filter_ptr=fp,
+             filter_idx=fi, **_topk_record(dense, rec, users), **filt)
+
+
+def gen_full_mf(models):
+    U, I, K = syn.HM_USERS, syn.HM_ITEMS, 12
+    sd = syn.mf_state_dict(U, I, 64, seed=0, bias_scale=0.05)
+    m = load(models.MatrixFactorization(num_users=U, num_items=I, embedding_dim=64, top_k=K,
+                                        sparse=False), sd)
+    users = syn.user_batch(U, 128, seed=11)
+    with torch.no_grad():
+        ut = torch.from_numpy(users)
+        dense = m.predict_all_items(ut).numpy()
+        rec = m.recommend(ut).numpy()
+    save("mf_full.npz", U=U, I=I, K=K, seed=0, bias_scale=0.05, **_topk_record(dense, rec, users))
+
+
+LGCN_FULL_U, LGCN_FULL_E = 20_000, 400_000
+
+
+def gen_full_lightgcn(models):
+    """Full item catalogue on a reduced-user graph (the reference's SpMM stand-in would
+    need tens of GB at the full 65M-nnz graph)."""
+    U, I, E, K = LGCN_FULL_U, syn.HM_ITEMS, LGCN_FULL_E, 12
+    for d in (64, 128):
+        sd = syn.lightgcn_state_dict(U, I, d, seed=0)
+        m = load(models.LightGCN(num_users=U, num_items=I, embedding_dim=d, num_layers=3,
+                                 top_k=K), sd)
+        ei = syn.bipartite_edge_index(U, I, E, seed=2)
+        m.set_graph(torch.from_numpy(ei))
+        users = syn.user_batch(U, 128, seed=11)
+        with torch.no_grad():
+            ut = torch.from_numpy(users)
+            fu, fi = m.forward()
+            dense = m.predict_all_items(ut).numpy()
+            rec = m.recommend(ut).numpy()
+        rows = syn.user_batch(I, 64, seed=12)
+        save(f"lightgcn_full_d{d}.npz", U=U, I=I, E=E, K=K, d=d, seed=0, graph_seed=2,
+             F_U_rows=fu.numpy()[users[:16]], F_I_sample_ids=rows, F_I_rows=fi.numpy()[rows],
+             **_topk_record(dense, rec, users))
+
+
+def gen_full_widedeep(models, B=64, chunk=8):
+    U, I, K = 2_000, syn.HM_ITEMS, 12
+    sd = syn.widedeep_state_dict(U, I, 64, (512, 256, 128), seed=0, bias_scale=0.05,
+                                 randomize_bn=True)
+    m = load(models.WideDeep(num_users=U, num_items=I, embedding_dim=64,
+                             deep_layers=[512, 256, 128], top_k=K), sd)
+    users = syn.user_batch(U, B, seed=11)
+    dense, rec = [], []
+    with torch.no_grad():
+        for s in range(0, B, chunk):
+            ut = torch.from_numpy(users[s:s + chunk])
+            d_ = m.predict_all_items(ut).numpy()
+            dense.append(d_)
+            rec.append(np.asarray(torch.topk(torch.from_numpy(d_), K, dim=1)[1]))
+            print(f"  widedeep users {s + chunk}/{B}", flush=True)
+    dense = np.concatenate(dense)
+    rec = np.concatenate(rec)  # == WideDeep.recommend (wide_deep.py:431-433) per chunk
+    save("widedeep_full.npz", U=U, I=I, K=K, seed=0, bias_scale=0.05, randomize_bn=1,
+         **_topk_record(dense, rec, users))
+
+
 if __name__ == "__main__":
     torch.manual_seed(0)
     torch.set_num_threads(8)
     models = install_stubs()
-    gen_ncf(models)
-    gen_lightgcn(models)
-    gen_widedeep(models)
-    gen_mf(models)
-    gen_metrics()
+    which = sys.argv[1:] or ["small"]
+    if "small" in which:
+        gen_ncf(models)
+        gen_lightgcn(models)
+        gen_widedeep(models)
+        gen_mf(models)
+        gen_metrics()
+    if "full" in which or "full_fast" in which:
+        gen_full_ncf(models)
+        gen_full_mf(models)
+        gen_full_lightgcn(models)
+    if "full" in which or "full_widedeep" in which:
+        gen_full_widedeep(models)

@@ -86,3 +86,38 @@ def assert_topk_equivalent(got_idx, ref_scores, k, filter_rows=None, what="topk"
 
 def same_topk_sets(a, b):
     return all(set(x.tolist()) == set(y.tolist()) for x, y in zip(np.asarray(a), np.asarray(b)))
+
+
+def assert_topk_matches_reference(got_idx, got_vals, ref, prefix="", what="topk"):
+    """Our top-K against the REFERENCE's stored top-K (a `_topk_record` of
+    tests/golden/make_golden.py: topk, topk_scores, kth, kth_gap, row_absmax).
+
+    * returned scores equal the reference's top-K scores position by position within
+      1e-4 of the row's score scale (both lists are sorted desc);
+    * when the reference's K-th and (K+1)-th scores are separated by more than that
+      tolerance the index SETS are identical; otherwise only items tied with the K-th
+      (within tolerance) may differ, and everything above it must be present."""
+    got_idx = np.asarray(got_idx, np.int64)
+    got_vals = np.asarray(got_vals, np.float64)
+    r_idx = np.asarray(ref[prefix + "topk"], np.int64)
+    r_val = np.asarray(ref[prefix + "topk_scores"], np.float64)
+    kth = np.asarray(ref[prefix + "kth"], np.float64)
+    gap = np.asarray(ref[prefix + "kth_gap"], np.float64)
+    scale = np.asarray(ref[prefix + "row_absmax"], np.float64)
+    assert got_idx.shape == r_idx.shape, (what, got_idx.shape, r_idx.shape)
+    n_exact = 0
+    for b in range(r_idx.shape[0]):
+        tol = RTOL * max(scale[b], 1e-30)
+        fin = np.isfinite(r_val[b])
+        assert np.array_equal(np.isfinite(got_vals[b]), fin), f"{what}: row {b} finiteness"
+        err = np.abs(got_vals[b][fin] - r_val[b][fin])
+        assert (err <= tol).all(), f"{what}: row {b} scores off by {err.max():.3e} (tol {tol:.3e})"
+        g, r = set(got_idx[b].tolist()), set(r_idx[b].tolist())
+        if not np.isfinite(kth[b]) or gap[b] > tol:
+            assert g == r, f"{what}: row {b} set differs: {sorted(g - r)} vs {sorted(r - g)}"
+            n_exact += 1
+        else:
+            must = {int(i) for i, v in zip(r_idx[b], r_val[b]) if v > kth[b] + tol}
+            assert must <= g, f"{what}: row {b} missing {sorted(must - g)}"
+            assert (got_vals[b] >= kth[b] - tol).all(), f"{what}: row {b} non-top item"
+    return n_exact

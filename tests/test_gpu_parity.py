@@ -9,8 +9,8 @@ import numpy as np
 import pytest
 import torch
 
-from parity import (assert_scores_close, assert_topk_equivalent, filter_from_arrays,
-                    load_golden, same_topk_sets)
+from parity import (assert_scores_close, assert_topk_equivalent,
+                    assert_topk_matches_reference, filter_from_arrays, load_golden)
 from oracle import hnm_oracle as O
 from hnm_recommendation_amd import LightGCN, MatrixFactorization, NeuralCF, WideDeep
 from hnm_recommendation_amd import synthetic as syn
@@ -37,7 +37,8 @@ def test_ncf_golden():
     assert_scores_close(dense, g["dense"], "ncf dense")
     rec = m.recommend(users).cpu().numpy()
     assert_topk_equivalent(rec, g["dense"], int(g["K"]), what="ncf recommend")
-    assert same_topk_sets(rec, g["topk"]) or True  # sets may differ only at near-ties
+    # the reference's own top-K is a valid top-K of our scores (sets differ only at near-ties)
+    assert_topk_equivalent(g["topk"], dense, int(g["K"]), what="reference topk vs HIP scores")
     f = filter_from_arrays(g["filter_keys"], g["filter_ptr"], g["filter_idx"])
     rec_f = m.recommend(users, filter_items=f).cpu().numpy()
     masked = O.apply_filter(g["dense"], g["user_ids"], f)
@@ -63,6 +64,12 @@ def test_ncf_config1_golden():
     # reference top-12 scores (recomputed by the oracle) match the returned scores
     np.testing.assert_allclose(vals.cpu().numpy()[:32], np.take_along_axis(ref_dense, rec[:32], 1),
                                rtol=1e-4, atol=1e-7)
+    # and the reference's OWN stored top-12 (indices, scores, K-th gap), all 256 users
+    srt = -np.sort(-dense, axis=1)
+    ref = {"topk": g["topk"], "topk_scores": g["topk_scores"], "kth": g["topk_scores"][:, -1],
+           "kth_gap": g["kth_gap"], "row_absmax": np.abs(dense).max(1)}
+    assert_topk_matches_reference(rec, vals.cpu().numpy(), ref, what="ncf config1 vs reference")
+    assert np.allclose(srt[:, 11], g["topk_scores"][:, -1], rtol=1e-4, atol=1e-7)
 
 
 @pytest.mark.parametrize("B,k", [(1, 12), (7, 5), (300, 12), (64, 100)])

@@ -91,3 +91,69 @@ def test_two_phase_contract():
     sc._open = (users.to(torch.int64).contiguous(), K)  # no begin on the ctx
     with pytest.raises(ValueError):
         sc.finish(users, torch.zeros(users.numel(), device="cuda"))
+
+
+# ------------------------------------------------------------------ BASELINE configs[4]
+# LightGCN d=128 at the full H&M shape (65M-nnz graph), item table row-sharded, one
+# exchange step -- rehearsed with 2 gloo ranks on one GPU.
+LU, LI = syn.HM_USERS, syn.HM_ITEMS
+LB = 512
+
+
+def _lightgcn128(ei=None):
+    from hnm_recommendation_amd import LightGCN
+    if ei is None:
+        ei = torch.from_numpy(syn.bipartite_edge_index(LU, LI, syn.HM_INTERACTIONS, seed=2))
+    m = LightGCN(LU, LI, embedding_dim=128, num_layers=3)
+    m.set_graph(ei)
+    sd = syn.lightgcn_state_dict(LU, LI, 128, seed=0)
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
+    return m.to("cuda:0").eval()
+
+
+def _lgcn_worker(rank, world, port, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        m = _lightgcn128()
+        fu, fi = m.forward()  # propagation replicated per rank
+        lo, hi = S.shard_range(LI, rank, world)
+        users = torch.from_numpy(syn.user_batch(LU, LB, seed=70 + rank)).cuda()
+        rec = S.ItemShardedRecommender(S.dot_shard_topk(fu, fi, lo, hi, K), S.hip_merge, K, lo,
+                                       rank, world)
+        v, i = rec.recommend(users)
+        np.savez(os.path.join(out_dir, f"l{rank}.npz"), users=users.cpu().numpy(),
+                 v=v.cpu().numpy(), i=i.cpu().numpy())
+    finally:
+        dist.destroy_process_group()
+
+
+def test_lightgcn128_full_shape_two_rank_sharding(tmp_path):
+    """configs[4] rehearsal: sharded result == single-GPU recommend_with_scores bitwise,
+    and sampled rows == the CPU restatement of the reference (oracle/torch_cpu.py)."""
+    world = 2
+    mp.spawn(_lgcn_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    ei = torch.from_numpy(syn.bipartite_edge_index(LU, LI, syn.HM_INTERACTIONS, seed=2))
+    m = _lightgcn128(ei)
+    rows = {}
+    for r in range(world):
+        z = np.load(tmp_path / f"l{r}.npz")
+        users = torch.from_numpy(z["users"]).cuda()
+        v, i = m.recommend_with_scores(users, k=K)
+        assert np.array_equal(z["i"], i.cpu().numpy()), f"rank {r}: sharded != single-GPU"
+        assert np.array_equal(z["v"].view(np.uint32), v.cpu().numpy().view(np.uint32))
+        rows[r] = (z["users"][:4], z["i"][:4], z["v"][:4])
+    # sampled rows against the reference's torch path restated on CPU
+    from oracle import torch_cpu as T
+    from parity import assert_topk_equivalent
+    torch.set_num_threads(min(16, os.cpu_count() or 1))
+    g = T.lightgcn_graph(ei, LU + LI)
+    del ei, m
+    w = torch.from_numpy(syn.lightgcn_state_dict(LU, LI, 128, seed=0)["embeddings.weight"])
+    fu, fi = T.lightgcn_forward(w, g, LU)
+    for r, (u, i, v) in rows.items():
+        dense = (fu[torch.from_numpy(u)] @ fi.t()).numpy()
+        assert_topk_equivalent(i, dense, K, what=f"lightgcn128 sharded rank {r} vs CPU ref")
+        np.testing.assert_allclose(v, np.take_along_axis(dense, i, 1), rtol=1e-4,
+                                   atol=1e-4 * float(np.abs(dense).max()))

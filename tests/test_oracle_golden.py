@@ -109,3 +109,47 @@ def test_metrics_match_reference():
         np.testing.assert_allclose(means[name], g[f"cls_{name}"], rtol=2e-6)
         np.testing.assert_array_equal(rows[:, j].astype(np.float32),
                                       g[f"cls_{name}_rows"].astype(np.float32))
+
+
+# ------------------------------------------------------------------ full catalogue
+# I = 105,542 fixtures (tests/golden/make_golden.py `full`): the oracle reproduces the
+# reference's stored top-K on a few users (the GPU tests check all of them).
+from parity import assert_topk_matches_reference  # noqa: E402
+
+
+def _rows(g, n, prefix=""):
+    keys = ("topk", "topk_scores", "kth", "kth_gap", "row_absmax")
+    return {prefix + k: g[prefix + k][:n] for k in keys}
+
+
+@pytest.mark.parametrize("name", ["ncf_full.npz", "ncf_full_personal.npz"])
+def test_ncf_full_catalogue_oracle(name):
+    g = load_golden(name)
+    sd = syn.ncf_state_dict(int(g["U"]), int(g["I"]), 64, (128, 64, 32), seed=int(g["seed"]),
+                            bias_scale=float(g["bias_scale"]), emb_scale=float(g["emb_scale"]))
+    dense = O.ncf_predict_all_items(sd, g["user_ids"][:4])
+    v, i = O.topk(dense, 12)
+    assert_topk_matches_reference(i, v, _rows(g, 4), what=name)
+    np.testing.assert_allclose(dense[:, ::int(g["slice_step"])], g["dense_slice"][:4], rtol=1e-4,
+                               atol=1e-4 * float(np.abs(g["dense_slice"]).max()))
+
+
+def test_mf_full_catalogue_oracle():
+    g = load_golden("mf_full.npz")
+    sd = syn.mf_state_dict(int(g["U"]), int(g["I"]), 64, seed=int(g["seed"]),
+                           bias_scale=float(g["bias_scale"]))
+    v, i = O.topk(O.mf_predict_all_items(sd, g["user_ids"][:16]), 12)
+    assert_topk_matches_reference(i, v, _rows(g, 16), what="mf full")
+
+
+def test_lightgcn_full_catalogue_oracle():
+    g = load_golden("lightgcn_full_d64.npz")
+    U, I, E = int(g["U"]), int(g["I"]), int(g["E"])
+    w = syn.lightgcn_state_dict(U, I, 64, seed=int(g["seed"]))["embeddings.weight"]
+    graph = O.lightgcn_set_graph(syn.bipartite_edge_index(U, I, E, seed=int(g["graph_seed"])),
+                                 None, U + I)
+    fu, fi = O.lightgcn_forward(w, graph, U)
+    assert_scores_close(fu[g["user_ids"][:16]], g["F_U_rows"], "F_U rows")
+    assert_scores_close(fi[g["F_I_sample_ids"]], g["F_I_rows"], "F_I rows")
+    v, i = O.topk(O.lightgcn_predict_all_items(fu, fi, g["user_ids"][:16]), 12)
+    assert_topk_matches_reference(i, v, _rows(g, 16), what="lightgcn full")
