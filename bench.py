@@ -104,16 +104,17 @@ def load(m, sd, device):
     return m.to(device).eval()
 
 
-def build_workload(name, rank, world, device, batch, exact=False):
+def build_workload(name, rank, world, device, batch, exact=False, weights="init"):
     """Returns (step_fn(users) -> (vals, idx), flops_or_bytes_per_launch, bound, info)."""
     U, I = syn.HM_USERS, syn.HM_ITEMS
     lo, hi = S.shard_range(I, rank, world)
     if name == "ncf":
-        sd = syn.ncf_state_dict(U, I, 64, (128, 64, 32), seed=0)
+        kw = dict(bias_scale=0.05, emb_scale=20.0) if weights == "personal" else {}
+        sd = syn.ncf_state_dict(U, I, 64, (128, 64, 32), seed=0, **kw)
         m = load(NeuralCF(U, I), sd, device)
         local = S.ncf_shard_topk(m, lo, hi, K)
         per_launch = 4352.0 * batch * world * (hi - lo)   # SURVEY §8(d): 4,352 FLOP / pair
-        info = {"model": "NeuralCF", "mf_dim": 64, "mlp_dims": [128, 64, 32],
+        info = {"model": "NeuralCF", "mf_dim": 64, "mlp_dims": [128, 64, 32], "weights": weights,
                 "scan": "exact fp32" if exact else
                         "certified f16 pre-filter + exact fp32 re-scoring (ncf_cert.hip)"}
         bound, kernel = "mfma", ("ncf32_kernel" if exact else "ncf16_scan_kernel")
@@ -126,26 +127,34 @@ def build_workload(name, rank, world, device, batch, exact=False):
         m.set_graph(torch.from_numpy(edges))
         m = load(m, sd, device)
         g = m._device_graph()
+        # the reference recomputes the propagation inside every recommend() call
+        # (lightgcn.py:197 predict_all_items -> self.forward()): so does the step, restricted
+        # to the rows that call reads (LightGCN.propagate_for: outputs identical)
+        rec = S.ItemShardedRecommender(S.lightgcn_shard_topk(m, lo, hi, K), S.hip_merge, K, lo,
+                                       rank, world)
 
-        def scorer(F):
-            local = S.dot_shard_topk(F[:U], F[U:], lo, hi, K)
-            return S.ItemShardedRecommender(local, S.hip_merge, K, lo, rank, world).recommend
-
-        def lgcn_step(users):
-            # the reference recomputes the propagation on every recommend() call
-            # (lightgcn.py:197 predict_all_items -> self.forward()): so does the step
-            return scorer(m.propagate(g))(users)
+        def full_step(users):  # whole-graph propagation per call, for comparison
+            F = m.propagate(g)
+            return S.ItemShardedRecommender(S.dot_shard_topk(F[:U], F[U:], lo, hi, K),
+                                            S.hip_merge, K, lo, rank, world).recommend(users)
 
         N = U + I
-        # per propagation layer: CSR (col int32 + val fp32 per nnz, rowptr int64), X read
-        # once, Y written once, acc (alpha-combine) read + written
-        per_launch = g.nnz * 8.0 + (N + 1) * 8.0 + 4.0 * N * d * 4
+        # per whole-graph propagation layer: CSR (col int32 + val fp32 per nnz, rowptr int64),
+        # X read once, Y written once, item-row accumulators read + written (layers 1..L-1;
+        # the restricted last layer is not timed)
+        per_launch = g.nnz * 8.0 + (N + 1) * 8.0 + 2.0 * N * d * 4 + 2.0 * I * d * 4
         info = {"model": "LightGCN", "embedding_dim": d, "num_layers": 3,
                 "interactions": syn.HM_INTERACTIONS, "nnz_with_self_loops": g.nnz,
-                "step": "3-layer propagation (SpMM) + certified top-K scan of the batch"}
-        info["_serving"] = lambda: scorer(m.propagate(g))
-        ret = dict(step=lgcn_step, per_launch=per_launch, bound="hbm",
-                   kernel="spmm layer (spmm_light + segment + finish)", timing=_lib.TIME_SPMM)
+                "step": "3-layer propagation restricted to what recommend() reads (layers 1-2 "
+                        "whole graph, layer 3 on item rows + the step's users; outputs "
+                        "identical to forward()) + certified top-K scan of the batch"}
+        info["_serving"] = lambda: (lambda F: S.ItemShardedRecommender(
+            S.dot_shard_topk(F[:U], F[U:], lo, hi, K), S.hip_merge, K, lo, rank,
+            world).recommend)(m.propagate(g))
+        info["_full_step"] = full_step
+        ret = dict(step=rec.recommend, per_launch=per_launch, bound="hbm",
+                   kernel="spmm layer (spmm_light + segment + finish), whole-graph layers",
+                   timing=_lib.TIME_SPMM)
         return ret, info, ("lightgcn", (sd, edges, d))
     elif name == "widedeep":
         sd = syn.widedeep_state_dict(U, I, 64, (512, 256, 128), seed=0)
@@ -249,6 +258,51 @@ def cpu_baseline(cpu):
     return out
 
 
+def serve_latency(args, device):
+    """Serve-path latency (serve.py:340-357): ONE user per request, 23-item purchase
+    history masked, top-k with scores copied back to the host, for k = 12 and 100.
+    NCF on the full H&M shape; LightGCN with its propagated tables cached (what a server
+    holding the module sees after the first request).  p50/p99 over `--steps` requests,
+    certified path (default) and exact fp32 scan."""
+    U, I = syn.HM_USERS, syn.HM_ITEMS
+    if args.workload == "ncf":
+        m = load(NeuralCF(U, I), syn.ncf_state_dict(U, I, 64, (128, 64, 32), seed=0), device)
+    elif args.workload in ("lightgcn", "lightgcn128"):
+        d = 64 if args.workload == "lightgcn" else 128
+        m = LightGCN(U, I, embedding_dim=d, num_layers=3)
+        m.set_graph(torch.from_numpy(syn.bipartite_edge_index(U, I, syn.HM_INTERACTIONS, seed=2)))
+        m = load(m, syn.lightgcn_state_dict(U, I, d, seed=0), device)
+        m.forward()
+    elif args.workload == "mf":
+        m = load(MatrixFactorization(U, I, sparse=False), syn.mf_state_dict(U, I, 64, seed=0), device)
+    else:
+        raise SystemExit("--latency: ncf, lightgcn, lightgcn128 or mf")
+    users = syn.user_batch(U, max(args.steps, 8), seed=300)
+    hist = syn.filter_dict(users, I, per_user=23, seed=301)
+    out = {"metric": "serve latency (B=1 recommend_with_scores, 23-item history mask, "
+                     "scores to host)", "unit": "ms", "workload": args.workload,
+           "higher_is_better": False, "requests": len(users)}
+    for mode in ("certified", "exact"):
+        _lib.set_prefilter(device, mode == "certified")
+        for k in (12, 100):
+            def one(u):
+                ut = torch.tensor([int(u)], dtype=torch.int64, device=device)
+                v, i = m.recommend_with_scores(ut, filter_items={int(u): hist[int(u)]}, k=k)
+                return v.cpu().tolist(), i.cpu().tolist()
+            for u in users[:5]:
+                one(u)
+            lat = []
+            for u in users:
+                t0 = time.perf_counter()
+                one(u)
+                lat.append((time.perf_counter() - t0) * 1e3)
+            out[f"{mode}_k{k}"] = {"p50": round(float(np.percentile(lat, 50)), 4),
+                                   "p99": round(float(np.percentile(lat, 99)), 4),
+                                   "mean": round(float(np.mean(lat)), 4)}
+    _lib.set_prefilter(device, True)
+    print(json.dumps(out), flush=True)
+
+
 def pmc_traffic(workload):
     """HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC summary."""
     p = os.path.join(REPO, "profiles", f"pmc_{workload}.json")
@@ -269,6 +323,11 @@ def main():
     ap.add_argument("--workload", default="ncf")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--scan-users", type=int, default=0, help="tuning: users per f16 scan iteration")
+    ap.add_argument("--latency", action="store_true",
+                    help="serve-path B=1 latency (p50/p99) instead of the throughput line")
+    ap.add_argument("--weights", default="init", choices=["init", "personal"],
+                    help="init: reference init distributions; personal: NCF weights whose "
+                         "best items are user-specific (emb_scale 20, biases)")
     ap.add_argument("--exact", action="store_true",
                     help="exact fp32 scan of every item instead of the certified f16 pre-filter")
     args = ap.parse_args()
@@ -276,13 +335,17 @@ def main():
         sys.exit(launch_ranks(args.gpus))
 
     rank, world, device = setup_dist(args.gpus)
+    if args.latency:
+        serve_latency(args, device)
+        return
     B = args.batch
     t_setup = time.perf_counter()
     if args.exact:
         _lib.set_prefilter(device, False)
     if args.scan_users:
         _lib.set_option(device, _lib.HNM_OPT_SCAN_USERS, args.scan_users)
-    wl, info, cpu = build_workload(args.workload, rank, world, device, B, args.exact)
+    wl, info, cpu = build_workload(args.workload, rank, world, device, B, args.exact,
+                                   args.weights)
     step, per_launch, bound, kernel = wl["step"], wl["per_launch"], wl["bound"], wl["kernel"]
     # resident user batches: rank-specific, distinct ids
     nb = 4
@@ -399,6 +462,22 @@ def main():
             "value": round(B * world * exact_rate[1] / exact_rate[0], 2), "unit": "users/s",
             "steps": exact_rate[1],
             "note": "same step with HNM_OPT_PREFILTER=0: every (user, item) pair in exact fp32"}
+    if "_full_step" in info:
+        full = info["_full_step"]
+        full(batches[0])
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        tf = time.perf_counter()
+        nfull = min(args.steps, 10)
+        for j in range(nfull):
+            full(batches[j % nb])
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        line["full_propagation_step"] = {
+            "value": round(B * world * nfull / (time.perf_counter() - tf), 2), "unit": "users/s",
+            "note": "same step with the whole-graph 3-layer propagation (all 1.48M rows per layer)"}
     if pf_rows:
         line["prefilter"] = {"rows": pf_rows, "candidates_per_row": round(
             pf_cands / max(pf_rows - pf_fallback, 1), 1), "fallback_rows": pf_fallback,

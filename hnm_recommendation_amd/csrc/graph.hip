@@ -35,6 +35,8 @@ struct hnm_spmm_plan {
   int32_t* seg_hrow;    // [n_seg]  index into heavy_rows
   int64_t* seg_start;   // [n_seg]
   int64_t* seg_end;     // [n_seg]
+  std::vector<int32_t>* h_heavy;  // host copies (row-range launches)
+  std::vector<int64_t>* h_seg_ptr;
 };
 
 // ------------------------------------------------------------------ CSR build kernels
@@ -258,72 +260,156 @@ __device__ __forceinline__ float4 row_sum(const int32_t* __restrict__ col,
   return acc;
 }
 
-__device__ __forceinline__ void spmm_epilogue(int64_t r, int d, int sub, float4 y, float* Y,
-                                              float alpha, const float* acc_in, float* acc_out) {
+// Epilogue of row r (layer combine, lightgcn.py:156-158): Y[r] = y and, for rows with an
+// accumulator (r >= acc_row0), acc_out = fma(alpha, y, acc_in) where acc_in == NULL means
+// beta * X[r] (the alpha_0 E_0 term folded into layer 1).  Accumulators are stored from
+// row acc_row0 on (items only when acc_row0 = num_users).
+struct SpmmEpi {
+  float* Y;
+  float alpha, beta;
+  const float* acc_in;
+  float* acc_out;
+  int64_t acc_row0;
+};
+
+__device__ __forceinline__ void spmm_epilogue(int64_t r, int d, int sub, float4 y,
+                                              const float* __restrict__ X, const SpmmEpi& ep) {
   const int64_t off = r * d + 4 * sub;
-  if (Y) *reinterpret_cast<float4*>(Y + off) = y;
-  if (acc_out) {
-    float4 a = acc_in ? *reinterpret_cast<const float4*>(acc_in + off) : make_float4(0.f, 0.f, 0.f, 0.f);
-    a.x += alpha * y.x;
-    a.y += alpha * y.y;
-    a.z += alpha * y.z;
-    a.w += alpha * y.w;
-    *reinterpret_cast<float4*>(acc_out + off) = a;
+  if (ep.Y) *reinterpret_cast<float4*>(ep.Y + off) = y;
+  if (ep.acc_out && r >= ep.acc_row0) {
+    const int64_t ao = (r - ep.acc_row0) * d + 4 * sub;
+    float4 a;
+    if (ep.acc_in) {
+      a = *reinterpret_cast<const float4*>(ep.acc_in + ao);
+    } else if (ep.beta != 0.f) {
+      const float4 x = *reinterpret_cast<const float4*>(X + off);
+      a = make_float4(ep.beta * x.x, ep.beta * x.y, ep.beta * x.z, ep.beta * x.w);
+    } else {
+      a = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    a.x = fmaf(ep.alpha, y.x, a.x);
+    a.y = fmaf(ep.alpha, y.y, a.y);
+    a.z = fmaf(ep.alpha, y.z, a.z);
+    a.w = fmaf(ep.alpha, y.w, a.w);
+    *reinterpret_cast<float4*>(ep.acc_out + ao) = a;
   }
 }
 
 template <int LPR>
-__global__ __launch_bounds__(256) void spmm_light_kernel(int64_t N, const int64_t* __restrict__ rowptr,
+__global__ __launch_bounds__(256) void spmm_light_kernel(int64_t r0, int64_t r1,
+                                                         const int64_t* __restrict__ rowptr,
                                                          const int32_t* __restrict__ col,
                                                          const float* __restrict__ val,
                                                          const float* __restrict__ X, int d,
-                                                         float* Y, float alpha,
-                                                         const float* acc_in, float* acc_out,
-                                                         int64_t heavy) {
-  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (r >= N) return;
+                                                         SpmmEpi ep, int64_t heavy) {
+  const int64_t r = r0 + (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= r1) return;
   const int lane = threadIdx.x & 63;
   const int64_t s = rowptr[r], e = rowptr[r + 1];
   if (e - s > heavy) return;  // segmented path
   const float4 y = row_sum<LPR>(col, val, X, d, s, e, lane);
-  if (lane < LPR) spmm_epilogue(r, d, lane, y, Y, alpha, acc_in, acc_out);
+  if (lane < LPR) spmm_epilogue(r, d, lane, y, X, ep);
 }
 
 template <int LPR>
-__global__ __launch_bounds__(256) void spmm_segment_kernel(int64_t nseg,
+__global__ __launch_bounds__(256) void spmm_segment_kernel(int64_t sg0, int64_t sg1,
                                                            const int64_t* __restrict__ seg_start,
                                                            const int64_t* __restrict__ seg_end,
                                                            const int32_t* __restrict__ col,
                                                            const float* __restrict__ val,
                                                            const float* __restrict__ X, int d,
                                                            float* __restrict__ partial) {
-  const int64_t sg = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (sg >= nseg) return;
+  const int64_t sg = sg0 + (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (sg >= sg1) return;
   const int lane = threadIdx.x & 63;
   const float4 y = row_sum<LPR>(col, val, X, d, seg_start[sg], seg_end[sg], lane);
-  if (lane < LPR) *reinterpret_cast<float4*>(partial + sg * d + 4 * lane) = y;
+  if (lane < LPR) *reinterpret_cast<float4*>(partial + (sg - sg0) * d + 4 * lane) = y;
 }
 
-__global__ __launch_bounds__(256) void spmm_finish_kernel(int64_t nheavy,
+// One workgroup per heavy row: thread (slice, c) sums float4 column c of the row's segment
+// partials sg = slice, slice + S, ... in order, then a fixed-order LDS tree over the S
+// slices (deterministic; all 256 lanes busy instead of d/4 lanes walking every segment).
+__global__ __launch_bounds__(256) void spmm_finish_kernel(int64_t h0,
                                                           const int32_t* __restrict__ heavy_rows,
                                                           const int64_t* __restrict__ seg_ptr,
+                                                          int64_t sg0,
                                                           const float* __restrict__ partial,
-                                                          int d, float* Y, float alpha,
-                                                          const float* acc_in, float* acc_out) {
-  const int64_t hr = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (hr >= nheavy) return;
-  const int lane = threadIdx.x & 63;
-  const int64_t r = heavy_rows[hr];
-  for (int sub = lane; sub < d / 4; sub += 64) {
-    float4 y = make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int64_t sg = seg_ptr[hr]; sg < seg_ptr[hr + 1]; ++sg) {
-      const float4 v = *reinterpret_cast<const float4*>(partial + sg * d + 4 * sub);
-      y.x += v.x;
-      y.y += v.y;
-      y.z += v.z;
-      y.w += v.w;
+                                                          const float* __restrict__ X, int d,
+                                                          SpmmEpi ep) {
+  __shared__ float4 red[256];
+  const int64_t hr = h0 + blockIdx.x;
+  const int t = threadIdx.x;
+  const int d4 = d / 4;
+  const int S = 256 / d4;  // d4 divides 256 (d in 4..256, powers of two)
+  const int c = t % d4, sl = t / d4;
+  const int64_t s0 = seg_ptr[hr] - sg0, s1 = seg_ptr[hr + 1] - sg0;
+  float4 y = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int64_t sg = s0 + sl; sg < s1; sg += S) {
+    const float4 v = *reinterpret_cast<const float4*>(partial + sg * d + 4 * c);
+    y.x += v.x;
+    y.y += v.y;
+    y.z += v.z;
+    y.w += v.w;
+  }
+  red[t] = y;
+  __syncthreads();
+  for (int w = S / 2; w >= 1; w >>= 1) {
+    if (sl < w) {
+      const float4 o = red[t + w * d4];
+      float4 m = red[t];
+      m.x += o.x;
+      m.y += o.y;
+      m.z += o.z;
+      m.w += o.w;
+      red[t] = m;
     }
-    spmm_epilogue(r, d, sub, y, Y, alpha, acc_in, acc_out);
+    __syncthreads();
+  }
+  if (sl == 0) spmm_epilogue((int64_t)heavy_rows[hr], d, c, red[t], X, ep);
+}
+
+// Final embeddings of listed rows (the batch's users) without their last layer over the
+// whole graph: y = (A_hat E_{L-1})[r] (one wave per row, the light kernel's summation
+// order), out[b] = alpha_0 E_0[r] then fma(alpha_l, E_l[r], .) for l = 1..L-1 and
+// fma(alpha_L, y, .) -- the same operations, in the same order, as the fused combine.
+struct CombineLayers {
+  const float* E[8];
+  float a[9];
+  int L;
+};
+
+template <int LPR>
+__global__ __launch_bounds__(256) void spmm_rows_combine_kernel(
+    const int64_t* __restrict__ rows, int64_t n, int64_t N, const int64_t* __restrict__ rowptr,
+    const int32_t* __restrict__ col, const float* __restrict__ val, int d, CombineLayers cl,
+    float* __restrict__ out, unsigned* err) {
+  const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (b >= n) return;
+  const int lane = threadIdx.x & 63;
+  const int64_t r = rows[b];
+  if (r < 0 || r >= N) {
+    if (lane == 0) hnm_flag(err, HNM_ERR_OOB);
+    for (int c = lane; c < d; c += 64) out[b * d + c] = __builtin_nanf("");
+    return;
+  }
+  const float4 y = row_sum<LPR>(col, val, cl.E[cl.L - 1], d, rowptr[r], rowptr[r + 1], lane);
+  if (lane < LPR) {
+    const int64_t off = r * d + 4 * lane;
+    const float4 x0 = *reinterpret_cast<const float4*>(cl.E[0] + off);
+    float4 a = make_float4(cl.a[0] * x0.x, cl.a[0] * x0.y, cl.a[0] * x0.z, cl.a[0] * x0.w);
+    for (int l = 1; l < cl.L; ++l) {
+      const float4 x = *reinterpret_cast<const float4*>(cl.E[l] + off);
+      a.x = fmaf(cl.a[l], x.x, a.x);
+      a.y = fmaf(cl.a[l], x.y, a.y);
+      a.z = fmaf(cl.a[l], x.z, a.z);
+      a.w = fmaf(cl.a[l], x.w, a.w);
+    }
+    const float aL = cl.a[cl.L];
+    a.x = fmaf(aL, y.x, a.x);
+    a.y = fmaf(aL, y.y, a.y);
+    a.z = fmaf(aL, y.z, a.z);
+    a.w = fmaf(aL, y.w, a.w);
+    *reinterpret_cast<float4*>(out + b * d + 4 * lane) = a;
   }
 }
 
@@ -353,6 +439,8 @@ extern "C" hnm_status hnm_spmm_plan_create(hnm_ctx* ctx, int64_t N, const int64_
   pl->N = N;
   pl->n_heavy = (int64_t)hrows.size();
   pl->n_seg = (int64_t)sstart.size();
+  pl->h_heavy = new std::vector<int32_t>(hrows);
+  pl->h_seg_ptr = new std::vector<int64_t>(sptr);
   if (pl->n_heavy > 0) {
     if (hipMalloc((void**)&pl->heavy_rows, pl->n_heavy * 4) != hipSuccess ||
         hipMalloc((void**)&pl->seg_ptr, (pl->n_heavy + 1) * 8) != hipSuccess ||
@@ -380,6 +468,8 @@ extern "C" hnm_status hnm_spmm_plan_destroy(hnm_spmm_plan* pl) {
   if (pl->seg_hrow) (void)hipFree(pl->seg_hrow);
   if (pl->seg_start) (void)hipFree(pl->seg_start);
   if (pl->seg_end) (void)hipFree(pl->seg_end);
+  delete pl->h_heavy;
+  delete pl->h_seg_ptr;
   free(pl);
   return HNM_OK;
 }
@@ -387,52 +477,110 @@ extern "C" hnm_status hnm_spmm_plan_destroy(hnm_spmm_plan* pl) {
 template <int LPR>
 static hnm_status spmm_launch(hnm_ctx* ctx, const hnm_spmm_plan* pl, int64_t N,
                               const int64_t* rowptr, const int32_t* col, const float* val,
-                              const float* X, int d, float* Y, float alpha, const float* acc_in,
-                              float* acc_out) {
-  const int64_t heavy = (pl && pl->n_heavy > 0) ? HEAVY : INT64_MAX;
-  hnm_timer_begin(ctx, HNM_TIME_SPMM);
-  hipLaunchKernelGGL(spmm_light_kernel<LPR>, dim3((unsigned)hnm_cdiv(N, 4)), dim3(256), 0,
-                     ctx->stream, N, rowptr, col, val, X, d, Y, alpha, acc_in, acc_out, heavy);
-  HNM_LAUNCH_CHECK();
-  if (pl && pl->n_heavy > 0) {
-    void* w;
-    hnm_status s = hnm_workspace(ctx, (size_t)pl->n_seg * d * 4, &w);
-    if (s) return s;
-    float* partial = (float*)w;
-    hipLaunchKernelGGL(spmm_segment_kernel<LPR>, dim3((unsigned)hnm_cdiv(pl->n_seg, 4)), dim3(256),
-                       0, ctx->stream, pl->n_seg, pl->seg_start, pl->seg_end, col, val, X, d,
-                       partial);
-    HNM_LAUNCH_CHECK();
-    hipLaunchKernelGGL(spmm_finish_kernel, dim3((unsigned)hnm_cdiv(pl->n_heavy, 4)), dim3(256), 0,
-                       ctx->stream, pl->n_heavy, pl->heavy_rows, pl->seg_ptr, partial, d, Y,
-                       alpha, acc_in, acc_out);
+                              const float* X, int d, const SpmmEpi& ep, int64_t r0, int64_t r1) {
+  const bool has_heavy = pl && pl->n_heavy > 0;
+  const int64_t heavy = has_heavy ? HEAVY : INT64_MAX;
+  // the live roofline times whole-graph layers only (row-range calls do less work)
+  const bool timed = r0 == 0 && r1 == N;
+  if (timed) hnm_timer_begin(ctx, HNM_TIME_SPMM);
+  if (r1 > r0) {
+    hipLaunchKernelGGL(spmm_light_kernel<LPR>, dim3((unsigned)hnm_cdiv(r1 - r0, 4)), dim3(256), 0,
+                       ctx->stream, r0, r1, rowptr, col, val, X, d, ep, heavy);
     HNM_LAUNCH_CHECK();
   }
-  hnm_timer_end(ctx, HNM_TIME_SPMM);
+  if (has_heavy) {
+    // heavy rows inside [r0, r1): heavy rows are ascending
+    const std::vector<int32_t>& hv = *pl->h_heavy;
+    const int64_t h0 = std::lower_bound(hv.begin(), hv.end(), (int32_t)std::min<int64_t>(r0, INT32_MAX)) - hv.begin();
+    const int64_t h1 = std::lower_bound(hv.begin(), hv.end(), (int32_t)std::min<int64_t>(r1, INT32_MAX)) - hv.begin();
+    if (h1 > h0) {
+      const int64_t sg0 = (*pl->h_seg_ptr)[h0], sg1 = (*pl->h_seg_ptr)[h1];
+      void* w;
+      hnm_status s = hnm_workspace(ctx, (size_t)(sg1 - sg0) * d * 4, &w);
+      if (s) return s;
+      float* partial = (float*)w;
+      hipLaunchKernelGGL(spmm_segment_kernel<LPR>, dim3((unsigned)hnm_cdiv(sg1 - sg0, 4)),
+                         dim3(256), 0, ctx->stream, sg0, sg1, pl->seg_start, pl->seg_end, col, val,
+                         X, d, partial);
+      HNM_LAUNCH_CHECK();
+      hipLaunchKernelGGL(spmm_finish_kernel, dim3((unsigned)(h1 - h0)), dim3(256), 0, ctx->stream,
+                         h0, pl->heavy_rows, pl->seg_ptr, sg0, partial, X, d, ep);
+      HNM_LAUNCH_CHECK();
+    }
+  }
+  if (timed) hnm_timer_end(ctx, HNM_TIME_SPMM);
   return HNM_OK;
 }
 
-extern "C" hnm_status hnm_spmm_csr_f32(hnm_ctx* ctx, const hnm_spmm_plan* plan, int64_t N,
-                                       const int64_t* rowptr, const int32_t* col,
-                                       const float* val, const float* X, int d, float* Y,
-                                       float alpha, const float* acc_in, float* acc_out) {
+#define HNM_SPMM_DISPATCH(FN, ...)                                                        \
+  switch (d) {                                                                            \
+    case 4: return FN<1>(__VA_ARGS__);                                                    \
+    case 8: return FN<2>(__VA_ARGS__);                                                    \
+    case 16: return FN<4>(__VA_ARGS__);                                                   \
+    case 32: return FN<8>(__VA_ARGS__);                                                   \
+    case 64: return FN<16>(__VA_ARGS__);                                                  \
+    case 128: return FN<32>(__VA_ARGS__);                                                 \
+    case 256: return FN<64>(__VA_ARGS__);                                                 \
+    default:                                                                              \
+      hnm_set_error("spmm: d must be one of 4, 8, 16, 32, 64, 128, 256 (got %d)", d);     \
+      return HNM_EUNSUPPORTED;                                                            \
+  }
+
+extern "C" hnm_status hnm_spmm_csr_range_f32(hnm_ctx* ctx, const hnm_spmm_plan* plan, int64_t N,
+                                             const int64_t* rowptr, const int32_t* col,
+                                             const float* val, const float* X, int d, float* Y,
+                                             float alpha, const float* acc_in, float* acc_out,
+                                             float beta, int64_t row_begin, int64_t row_end,
+                                             int64_t acc_row0) {
   HNM_REQUIRE(ctx && rowptr && col && val && X, HNM_EINVAL, "spmm: NULL argument");
   HNM_REQUIRE(!plan || plan->N == N, HNM_EINVAL, "spmm: plan built for a different graph");
   HNM_REQUIRE((uintptr_t)X % 16 == 0 && (!Y || (uintptr_t)Y % 16 == 0) &&
                   (!acc_out || (uintptr_t)acc_out % 16 == 0) &&
                   (!acc_in || (uintptr_t)acc_in % 16 == 0),
               HNM_EUNSUPPORTED, "spmm: buffers must be 16-B aligned");
+  HNM_REQUIRE(0 <= row_begin && row_begin <= row_end && row_end <= N && 0 <= acc_row0 &&
+                  acc_row0 <= N,
+              HNM_EINVAL, "spmm: bad row range");
   if (N <= 0) return HNM_OK;
-  switch (d) {
-    case 4: return spmm_launch<1>(ctx, plan, N, rowptr, col, val, X, d, Y, alpha, acc_in, acc_out);
-    case 8: return spmm_launch<2>(ctx, plan, N, rowptr, col, val, X, d, Y, alpha, acc_in, acc_out);
-    case 16: return spmm_launch<4>(ctx, plan, N, rowptr, col, val, X, d, Y, alpha, acc_in, acc_out);
-    case 32: return spmm_launch<8>(ctx, plan, N, rowptr, col, val, X, d, Y, alpha, acc_in, acc_out);
-    case 64: return spmm_launch<16>(ctx, plan, N, rowptr, col, val, X, d, Y, alpha, acc_in, acc_out);
-    case 128: return spmm_launch<32>(ctx, plan, N, rowptr, col, val, X, d, Y, alpha, acc_in, acc_out);
-    case 256: return spmm_launch<64>(ctx, plan, N, rowptr, col, val, X, d, Y, alpha, acc_in, acc_out);
-    default:
-      hnm_set_error("spmm: d must be one of 4, 8, 16, 32, 64, 128, 256 (got %d)", d);
-      return HNM_EUNSUPPORTED;
+  const SpmmEpi ep{Y, alpha, beta, acc_in, acc_out, acc_row0};
+  HNM_SPMM_DISPATCH(spmm_launch, ctx, plan, N, rowptr, col, val, X, d, ep, row_begin, row_end)
+}
+
+extern "C" hnm_status hnm_spmm_csr_f32(hnm_ctx* ctx, const hnm_spmm_plan* plan, int64_t N,
+                                       const int64_t* rowptr, const int32_t* col,
+                                       const float* val, const float* X, int d, float* Y,
+                                       float alpha, const float* acc_in, float* acc_out) {
+  return hnm_spmm_csr_range_f32(ctx, plan, N, rowptr, col, val, X, d, Y, alpha, acc_in, acc_out,
+                                0.f, 0, N, 0);
+}
+
+template <int LPR>
+static hnm_status combine_launch(hnm_ctx* ctx, const int64_t* rows, int64_t n, int64_t N,
+                                 const int64_t* rowptr, const int32_t* col, const float* val,
+                                 int d, const CombineLayers& cl, float* out) {
+  hipLaunchKernelGGL(spmm_rows_combine_kernel<LPR>, dim3((unsigned)hnm_cdiv(n, 4)), dim3(256), 0,
+                     ctx->stream, rows, n, N, rowptr, col, val, d, cl, out, ctx->err_dev);
+  HNM_LAUNCH_CHECK();
+  return HNM_OK;
+}
+
+extern "C" hnm_status hnm_spmm_rows_combine_f32(hnm_ctx* ctx, int64_t N, const int64_t* rowptr,
+                                                const int32_t* col, const float* val,
+                                                const int64_t* rows, int64_t n, int d,
+                                                const float* const* layers, const float* alphas,
+                                                int L, float* out) {
+  HNM_REQUIRE(ctx && rowptr && col && val && rows && layers && alphas && out, HNM_EINVAL,
+              "spmm_rows_combine: NULL argument");
+  HNM_REQUIRE(L >= 1 && L <= 8, HNM_EUNSUPPORTED, "spmm_rows_combine: 1 <= L <= 8");
+  CombineLayers cl;
+  cl.L = L;
+  for (int l = 0; l < L; ++l) {
+    HNM_REQUIRE(layers[l] && (uintptr_t)layers[l] % 16 == 0, HNM_EINVAL,
+                "spmm_rows_combine: layer %d NULL or not 16-B aligned", l);
+    cl.E[l] = layers[l];
   }
+  for (int l = 0; l <= L; ++l) cl.a[l] = alphas[l];
+  HNM_REQUIRE((uintptr_t)out % 16 == 0, HNM_EINVAL, "spmm_rows_combine: out not 16-B aligned");
+  if (n <= 0) return HNM_OK;
+  HNM_SPMM_DISPATCH(combine_launch, ctx, rows, n, N, rowptr, col, val, d, cl, out)
 }

@@ -325,6 +325,47 @@ __global__ __launch_bounds__(256) void rows_topk_kernel(const float* __restrict_
   L.store(ov ? ov + b * K : nullptr, oi + b * K, K);
 }
 
+// Small batches (serve path: one user per request, k up to 100): each row is cut into P
+// column chunks, one wave per (row, chunk) keeps the chunk's top-K (int32 ids), and the
+// P partial lists are merged by topk_merge (same total order => same result as one wave).
+template <int NS>
+__global__ __launch_bounds__(256) void rows_topk_split_kernel(const float* __restrict__ s,
+                                                              int64_t ld, int64_t B, int64_t I,
+                                                              int64_t chunk,
+                                                              const int64_t* __restrict__ mptr,
+                                                              const int32_t* __restrict__ midx,
+                                                              int K, float* __restrict__ pv,
+                                                              int32_t* __restrict__ pi) {
+  const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (b >= B) return;
+  const int lane = threadIdx.x & 63;
+  const int64_t lo = (int64_t)blockIdx.y * chunk, hi = std::min<int64_t>(I, lo + chunk);
+  WaveTopK<NS> L;
+  L.init();
+  int64_t mpos = 0, mend = 0;
+  int nm = INT_BIG;
+  if (mptr) {
+    mend = mptr[b + 1];
+    mpos = mask_lower_bound(midx, mptr[b], mend, (int)lo);
+    nm = mpos < mend ? midx[mpos] : INT_BIG;
+  }
+  const float* row = s + b * ld;
+  for (int64_t base = lo; base < hi; base += 64) {
+    const int64_t item = base + lane;
+    const bool valid = item < hi;
+    float v = valid ? row[item] : -__builtin_inff();
+    const int64_t end = std::min<int64_t>(base + 64, hi);
+    while (nm < end) {
+      if (item == nm) v = -__builtin_inff();
+      ++mpos;
+      nm = mpos < mend ? midx[mpos] : INT_BIG;
+    }
+    L.offer(v, (int)item, valid, K);
+  }
+  const int64_t o = ((int64_t)blockIdx.y * B + b) * K;
+  L.store(pv + o, pi + o, K);
+}
+
 // ------------------------------------------------------------------ sample K-th (lower bound)
 // For the certified pre-filters: a LOWER BOUND of the K-th best value of each row of a
 // dense [B, Ns] sample (masked columns excluded; column c is item sidx[c], or
@@ -688,6 +729,26 @@ extern "C" hnm_status hnm_topk_rows_f32(hnm_ctx* ctx, const float* scores, int64
   HNM_REQUIRE(k >= 1 && k <= 128 && k <= I && ld >= I, HNM_EINVAL, "topk_rows: bad k/shape");
   HNM_REQUIRE(I < INT_BIG, HNM_EUNSUPPORTED, "topk_rows: too many items");
   if (B <= 0) return HNM_OK;
+  // fewer rows than ~1024 waves: split the rows into column chunks of >= 2048 items
+  const int64_t P = std::min<int64_t>(hnm_cdiv(1024, B), hnm_cdiv(I, 2048));
+  if (P > 1) {
+    const int64_t chunk = hnm_cdiv(I, P);
+    void* w;
+    hnm_status st = hnm_workspace(ctx, (size_t)P * B * k * 8, &w);
+    if (st) return st;
+    float* pv = (float*)w;
+    int32_t* pi = (int32_t*)(pv + P * B * k);
+    dim3 g2((unsigned)hnm_cdiv(B, 4), (unsigned)P);
+    if (k <= 64)
+      hipLaunchKernelGGL(rows_topk_split_kernel<1>, g2, dim3(256), 0, ctx->stream, scores, ld, B,
+                         I, chunk, mask_ptr, mask_idx, k, pv, pi);
+    else
+      hipLaunchKernelGGL(rows_topk_split_kernel<2>, g2, dim3(256), 0, ctx->stream, scores, ld, B,
+                         I, chunk, mask_ptr, mask_idx, k, pv, pi);
+    HNM_LAUNCH_CHECK();
+    return hnm_topk_merge_rows(ctx, pv, pi, B, P, B * k, k, k, k, out_val, out_idx, nullptr,
+                               nullptr);
+  }
   dim3 grid((unsigned)hnm_cdiv(B, 4));
   if (k <= 64)
     hipLaunchKernelGGL(rows_topk_kernel<1>, grid, dim3(256), 0, ctx->stream, scores, ld, B, I,

@@ -56,14 +56,32 @@ class NormalizedGraph:
         self.plan = plan
 
     def spmm(self, X: torch.Tensor, Y: Optional[torch.Tensor], alpha: float,
-             acc: Optional[torch.Tensor]):
-        """Y = A X;  acc += alpha * Y (either output optional)."""
+             acc: Optional[torch.Tensor], acc_in: bool = True, beta: float = 0.0,
+             rows: Optional[Tuple[int, int]] = None, acc_row0: int = 0):
+        """Y = A X on rows [r0, r1) (default all);  acc = fma(alpha, Y, acc or beta * X) on
+        rows >= acc_row0, stored from acc_row0 on (either output optional)."""
+        r0, r1 = (0, self.num_nodes) if rows is None else rows
         c = _lib.ctx(X.device)
-        _lib.check(_lib.fn("hnm_spmm_csr_f32")(c, self.plan, self.num_nodes,
-                                               _lib.ptr(self.rowptr), _lib.ptr(self.col),
-                                               _lib.ptr(self.val), _lib.ptr(X), X.shape[1],
-                                               _lib.ptr(Y), alpha, _lib.ptr(acc), _lib.ptr(acc)),
-                   "hnm_spmm_csr_f32")
+        _lib.check(_lib.fn("hnm_spmm_csr_range_f32")(
+            c, self.plan, self.num_nodes, _lib.ptr(self.rowptr), _lib.ptr(self.col),
+            _lib.ptr(self.val), _lib.ptr(X), X.shape[1], _lib.ptr(Y), alpha,
+            _lib.ptr(acc) if acc_in else None, _lib.ptr(acc), beta, r0, r1, acc_row0),
+            "hnm_spmm_csr_range_f32")
+
+    def rows_combine(self, rows: torch.Tensor, layers, alphas) -> torch.Tensor:
+        """Final embeddings of `rows` from the layer inputs E_0..E_{L-1} (last layer for
+        these rows only): hnm_spmm_rows_combine_f32."""
+        L = len(layers)
+        d = layers[0].shape[1]
+        out = torch.empty(rows.numel(), d, dtype=torch.float32, device=rows.device)
+        ptrs = (C.c_void_p * L)(*[t.data_ptr() for t in layers])
+        al = (C.c_float * (L + 1))(*[float(a) for a in alphas])
+        c = _lib.ctx(rows.device)
+        _lib.check(_lib.fn("hnm_spmm_rows_combine_f32")(
+            c, self.num_nodes, _lib.ptr(self.rowptr), _lib.ptr(self.col), _lib.ptr(self.val),
+            _lib.ptr(rows), rows.numel(), d, ptrs, al, L, _lib.ptr(out)),
+            "hnm_spmm_rows_combine_f32")
+        return out
 
     def __del__(self):
         plan = getattr(self, "plan", None)
@@ -155,21 +173,51 @@ class LightGCN(RecModule):
         return F[: self.num_users], F[self.num_users:]
 
     def propagate(self, g: Optional[NormalizedGraph] = None) -> torch.Tensor:
-        """E_{l+1} = A E_l, F = sum_l alpha_l E_l on the HIP SpMM (no cache)."""
+        """E_{l+1} = A E_l, F = sum_l alpha_l E_l on the HIP SpMM (no cache); the alpha_0 E_0
+        term is folded into layer 1's epilogue."""
         g = self._device_graph() if g is None else g
         E0 = f32c(self.embeddings.weight)
         _lib.require_gpu(E0)
-        c = _lib.ctx(E0.device)
         acc = torch.empty_like(E0)
-        _lib.check(_lib.fn("hnm_axpby_f32")(c, E0.numel(), float(self.alpha[0]), _lib.ptr(E0),
-                                            0.0, None, _lib.ptr(acc)), "hnm_axpby_f32")
+        if self.num_layers == 0:
+            return acc.copy_(E0).mul_(float(self.alpha[0]))
         cur = E0
         for layer in range(self.num_layers):
             last = layer == self.num_layers - 1
             nxt = None if last else torch.empty_like(E0)
-            g.spmm(cur, nxt, float(self.alpha[layer + 1]), acc)
+            g.spmm(cur, nxt, float(self.alpha[layer + 1]), acc, acc_in=layer > 0,
+                   beta=float(self.alpha[0]))
             cur = nxt
         return acc
+
+    def propagate_for(self, user_ids: torch.Tensor,
+                      g: Optional[NormalizedGraph] = None) -> Tuple[torch.Tensor, torch.Tensor]:
+        """What one `recommend(user_ids)` reads of `forward()` (`lightgcn.py:197-199`): the
+        final rows of the listed users [B, d] and every item [I, d], recomputed (no cache).
+
+        Layers 1..L-1 run over the whole graph (every node feeds the last layer); the last
+        layer runs over the item rows only, and the users' final rows come from
+        hnm_spmm_rows_combine_f32.  The layer combine is kept for item rows only.  Outputs
+        are identical to forward()'s rows (same operations in the same order), without the
+        last layer's 1.37M user rows and the users' combine traffic."""
+        g = self._device_graph() if g is None else g
+        U, N, L = self.num_users, self.num_nodes, self.num_layers
+        u = self._ids(user_ids, U)
+        E0 = f32c(self.embeddings.weight)
+        _lib.require_gpu(E0)
+        if L == 0:
+            F = E0 * float(self.alpha[0])
+            return F[u], F[U:]
+        acc = torch.empty(N - U, E0.shape[1], dtype=torch.float32, device=E0.device)
+        layers = [E0]
+        for layer in range(L):
+            last = layer == L - 1
+            nxt = None if last else torch.empty_like(E0)
+            g.spmm(layers[-1], nxt, float(self.alpha[layer + 1]), acc, acc_in=layer > 0,
+                   beta=float(self.alpha[0]), rows=(U, N) if last else None, acc_row0=U)
+            if not last:
+                layers.append(nxt)
+        return g.rows_combine(u, layers, self.alpha), acc
 
     # ------------------------------------------------------------------ scoring
     def predict(self, user_ids: torch.Tensor, item_ids: torch.Tensor) -> torch.Tensor:

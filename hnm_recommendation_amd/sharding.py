@@ -245,3 +245,38 @@ def widedeep_shard_topk(model, lo: int, hi: int, k: int) -> LocalTopK:
                    "hnm_widedeep_topk_f32")
         return _pad(out_v, out_i, k)
     return run
+
+
+class lightgcn_shard_topk:
+    """LightGCN recommend() over item rows [lo, hi) with the propagation recomputed per
+    call, as the reference does (`lightgcn.py:197` -> `forward()`), restricted to what the
+    call reads: `LightGCN.propagate_for(all users of the step)` (layers 1..L-1 whole graph,
+    the last layer on item rows + these users), then the dot top-K over the shard."""
+
+    def __init__(self, model, lo: int, hi: int, k: int):
+        self.model, self.lo, self.hi, self.k = model, lo, hi, k
+        self._dot = None
+
+    def _scorer(self, user_ids):
+        fb, fi = self.model.propagate_for(user_ids)
+        rows = torch.arange(user_ids.numel(), dtype=torch.int64, device=user_ids.device)
+        return dot_shard_topk(fb, fi, self.lo, self.hi, self.k), rows
+
+    def __call__(self, user_ids: torch.Tensor):
+        dot, rows = self._scorer(user_ids)
+        return dot(rows)
+
+    def begin(self, user_ids: torch.Tensor) -> torch.Tensor:
+        dot, rows = self._scorer(user_ids)
+        self._dot = (dot, rows)
+        return dot.begin(rows)
+
+    def abort(self):
+        if self._dot is not None:
+            self._dot[0].abort()
+            self._dot = None
+
+    def finish(self, user_ids: torch.Tensor, lb: torch.Tensor):
+        dot, rows = self._dot
+        self._dot = None
+        return dot.finish(rows, lb)

@@ -315,6 +315,26 @@ hnm_status hnm_spmm_csr_f32(hnm_ctx* ctx, const hnm_spmm_plan* plan, int64_t N,
                             const int64_t* rowptr, const int32_t* col, const float* val,
                             const float* X, int d, float* Y, float alpha,
                             const float* acc_in, float* acc_out);
+/* Row-range form: rows [row_begin, row_end) only.  Accumulators exist for rows >= acc_row0
+ * and are stored from there on (acc[(r - acc_row0) * d]); acc_in NULL means beta * X[r]
+ * (the alpha_0 * E_0 term folded into layer 1: acc_out = fma(alpha, Y, beta * X)).
+ * hnm_spmm_csr_f32 == range [0, N), acc_row0 0, beta 0. */
+hnm_status hnm_spmm_csr_range_f32(hnm_ctx* ctx, const hnm_spmm_plan* plan, int64_t N,
+                                  const int64_t* rowptr, const int32_t* col, const float* val,
+                                  const float* X, int d, float* Y, float alpha,
+                                  const float* acc_in, float* acc_out, float beta,
+                                  int64_t row_begin, int64_t row_end, int64_t acc_row0);
+/* Final embeddings of `n` listed rows (ids < N) after L layers, given the layer inputs
+ * E_0 .. E_{L-1} (host array `layers` of L device pointers, each [N, d]) and alphas[0..L]
+ * (host): out[b] = sum_l alphas[l] E_l[rows[b]] with E_L[r] = (A_hat E_{L-1})[r] computed
+ * for the listed rows only -- the last layer of LightGCN.forward restricted to the users a
+ * recommend() call reads (lightgcn.py:197-199).  Same operations and order as the fused
+ * combine of hnm_spmm_csr_f32 (bitwise equal for rows with <= 2048 neighbours).  An id out
+ * of range flags HNM_EOOB and writes NaN.  1 <= L <= 8. */
+hnm_status hnm_spmm_rows_combine_f32(hnm_ctx* ctx, int64_t N, const int64_t* rowptr,
+                                     const int32_t* col, const float* val, const int64_t* rows,
+                                     int64_t n, int d, const float* const* layers,
+                                     const float* alphas, int L, float* out);
 /* out = alpha * x + beta * y (y may be NULL): the alpha_0 * E_0 term of the combine. */
 hnm_status hnm_axpby_f32(hnm_ctx* ctx, int64_t n, float alpha, const float* x, float beta,
                          const float* y, float* out);

@@ -42,7 +42,7 @@ def check(g, res, what, prefix=""):
     for (v, i), mode in zip(res, ("certified", "exact")):
         n = assert_topk_matches_reference(i.cpu().numpy(), v.cpu().numpy(), g, prefix,
                                           what=f"{what} [{mode}]")
-        assert n >= 0.5 * len(g[prefix + "topk"]), f"{what}: only {n} rows without near-ties"
+        assert n >= 0.25 * len(g[prefix + "topk"]), f"{what}: only {n} rows without near-ties"
     # the two paths agree bitwise (same fp32 arithmetic for every returned score)
     assert torch.equal(res[0][1], res[1][1]) and torch.equal(res[0][0], res[1][0]), what
 

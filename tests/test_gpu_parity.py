@@ -318,3 +318,40 @@ def test_dot_threshold_overflow_fallback_exact_ties():
     rec = m.recommend(t(users), filter_items=f).cpu().numpy()
     assert rec[3].tolist() == list(range(20, 32))
     assert (rec[4] == np.arange(12)).all()
+
+
+@pytest.mark.parametrize("B,k", [(1, 100), (1, 12), (3, 128), (40, 100)])
+def test_row_topk_small_batch_split(B, k):
+    """hnm_topk_rows_f32 at small B cuts each row into column chunks (serve path, k <= 128)
+    and merges the partial lists: same total order as torch.topk with (score desc, idx asc)."""
+    from hnm_recommendation_amd.models.base import dense_topk, filter_csr
+    I = 105_542
+    rng = np.random.Generator(np.random.PCG64(5))
+    s = rng.standard_normal((B, I)).astype(np.float32)
+    s[:, 1000:1010] = 7.0  # exact ties across the chunk boundary region
+    users = torch.arange(B)
+    f = {b: set(rng.choice(I, 23, replace=False).tolist()) | {1003} for b in range(B)}
+    mptr, midx = filter_csr(users, f, I, torch.device(DEV))
+    v, i = dense_topk(t(s), k, mptr, midx)
+    ref = O.apply_filter(s, np.arange(B), f)
+    rv, ri = O.topk(ref, k)
+    np.testing.assert_array_equal(i.cpu().numpy(), ri)
+    np.testing.assert_array_equal(v.cpu().numpy(), rv)
+
+
+@pytest.mark.parametrize("alpha,d", [(None, 64), (0.5, 128)])
+def test_lightgcn_propagate_for_equals_forward(alpha, d):
+    """The batch-restricted propagation (last layer on item rows + the listed users only)
+    returns exactly forward()'s rows, bit for bit, on the full H&M graph (power-law item
+    rows on the segmented path, duplicate and out-of-batch users)."""
+    U, I, E = syn.HM_USERS, syn.HM_ITEMS, syn.HM_INTERACTIONS
+    m = LightGCN(U, I, d, alpha=alpha)
+    m.set_graph(torch.from_numpy(syn.bipartite_edge_index(U, I, E, seed=2)))
+    m = to_module(m, syn.lightgcn_state_dict(U, I, d, seed=0))
+    users = t(np.concatenate([syn.user_batch(U, 1000, seed=4), [0, U - 1, 5, 5]]))
+    fb, fi_b = m.propagate_for(users)
+    fu, fi = m.forward()
+    assert torch.equal(fi_b, fi)
+    assert torch.equal(fb, fu[users])
+    with pytest.raises(IndexError):
+        m.propagate_for(torch.tensor([U]))
