@@ -43,6 +43,12 @@ class WideDeepWeights(C.Structure):
         ("num_user_features", _i32), ("eps", _f32)]
 
 
+class WideDeepItemFeatures(C.Structure):
+    """hnm_widedeep_item_features (include/hnm.h)."""
+    _fields_ = [("dif_w", _p), ("dif_b", _p), ("wif_w", _p), ("wif_b", _p), ("wide_feat", _p),
+                ("num_item_features", _i32)]
+
+
 _SIGS = {
     "hnm_abi_version": (C.c_int, []),
     "hnm_last_error": (C.c_char_p, []),
@@ -95,6 +101,9 @@ _SIGS = {
     "hnm_widedeep_scores_f32": (_i32, [_p, C.POINTER(WideDeepWeights), _p, _i64, _p, _p, _i64]),
     "hnm_widedeep_pair_scores_f32": (_i32, [_p, C.POINTER(WideDeepWeights), _p, _p, _p, _i64,
                                             _p]),
+    "hnm_widedeep_pair_scores_ex_f32": (_i32, [_p, C.POINTER(WideDeepWeights),
+                                               C.POINTER(WideDeepItemFeatures), _p, _p, _p, _p,
+                                               _i64, _p]),
     "hnm_widedeep_prefilter_debug_f32": (_i32, [_p, C.POINTER(WideDeepWeights), _p, _i64, _p, _p,
                                                 _i64, _p]),
     "hnm_rank_metrics_f64": (_i32, [_p, _p, _i64, _i64, _p, C.c_int, _p, _p, _i64, _p, _p, _p,

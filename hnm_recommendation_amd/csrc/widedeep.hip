@@ -340,8 +340,8 @@ __global__ __launch_bounds__(256, (RB2 >= 8 || OB >= 4) ? 1 : 2) void widedeep_s
 // pair, the unfolded reference op order (Linear -> ReLU -> BatchNorm per layer).
 __global__ __launch_bounds__(256) void widedeep_pair_kernel(
     hnm_widedeep_weights w, const int64_t* __restrict__ uids, const int64_t* __restrict__ iids,
-    int64_t n, const float* __restrict__ xu, const float* __restrict__ wide_extra,
-    float* __restrict__ out, unsigned* err) {
+    int64_t n, const float* __restrict__ xu, int ldxu, const float* __restrict__ wide_extra,
+    const float* __restrict__ wide_extra2, float* __restrict__ out, unsigned* err) {
   __shared__ float x0[512], x1[512];
   __shared__ float red[256];
   const int64_t e = blockIdx.x;
@@ -359,7 +359,7 @@ __global__ __launch_bounds__(256) void widedeep_pair_kernel(
     float v;
     if (c < w.d) v = w.deep_user[u * w.d + c];
     else if (c < 2 * w.d) v = w.deep_item[i * w.d + c - w.d];
-    else v = xu[e * w.d + c - 2 * w.d];
+    else v = xu[e * ldxu + c - 2 * w.d];  // [deep user-feature | deep item-feature] chunks
     x0[c] = v;
   }
   __syncthreads();
@@ -399,8 +399,14 @@ __global__ __launch_bounds__(256) void widedeep_pair_kernel(
     __syncthreads();
   }
   if (t == 0) {
-    float v = red[0] + w.wide_user[u] + w.wide_item[i] + w.final_b[0];
+    // wide part in the reference's concat order: user one-hot, item one-hot (both absent
+    // when use_wide_user_item=False), user-feature cross, item-feature cross
+    float v = red[0];
+    if (w.wide_user) v += w.wide_user[u];
+    if (w.wide_item) v += w.wide_item[i];
+    v += w.final_b[0];
     if (wide_extra) v += wide_extra[e];
+    if (wide_extra2) v += wide_extra2[e];
     out[e] = v;
   }
 }
@@ -1695,43 +1701,82 @@ extern "C" hnm_status hnm_widedeep_prefilter_debug_f32(hnm_ctx* ctx,
   return wdc_scan(ctx, w, S, B, nullptr, nullptr, 1, c, WDC_DEBUG, approx, bound, lda);
 }
 
+extern "C" hnm_status hnm_widedeep_pair_scores_ex_f32(hnm_ctx* ctx, const hnm_widedeep_weights* w,
+                                                      const hnm_widedeep_item_features* itf,
+                                                      const int64_t* user_ids,
+                                                      const int64_t* item_ids,
+                                                      const float* user_features,
+                                                      const float* item_features, int64_t n,
+                                                      float* out) {
+  HNM_REQUIRE(ctx && w && user_ids && item_ids && out, HNM_EINVAL, "widedeep_pair: NULL argument");
+  HNM_REQUIRE(w->l1 <= 512 && w->l2 <= 512 && w->l3 <= 512 && w->l1_in <= 512, HNM_EUNSUPPORTED,
+              "widedeep_pair: widths must be <= 512");
+  const int Fu = w->num_user_features, Fi = itf ? itf->num_item_features : 0;
+  const int nch = (Fu > 0) + (Fi > 0);  // deep feature chunks after [e_u; e_i]
+  HNM_REQUIRE(w->l1_in == (2 + nch) * w->d, HNM_EINVAL,
+              "widedeep_pair: layer-1 input %d != %d x embedding_dim (features given)", w->l1_in,
+              2 + nch);
+  if (n <= 0) return HNM_OK;
+  float* xf = nullptr;
+  float* wide = nullptr;
+  float* wide2 = nullptr;
+  const int ldx = nch * w->d;
+  if (nch > 0) {
+    HNM_REQUIRE(Fu == 0 || (user_features && w->duf_w), HNM_EINVAL,
+                "widedeep_pair: user_features required");
+    HNM_REQUIRE(Fi == 0 || (item_features && itf->dif_w), HNM_EINVAL,
+                "widedeep_pair: item_features required");
+    const int Fm = std::max(Fu, Fi);
+    const size_t szx = hnm_align((size_t)n * ldx * 4), szf = hnm_align((size_t)n * Fm * 4);
+    const size_t szw = hnm_align((size_t)n * 4);
+    void* wsp;
+    hnm_status st = hnm_workspace(ctx, szx + szf + 2 * szw, &wsp);
+    if (st) return st;
+    xf = (float*)wsp;
+    float* wf = (float*)((char*)wsp + szx);
+    float* w1 = (float*)((char*)wsp + szx + szf);
+    float* w2 = (float*)((char*)wsp + szx + szf + szw);
+    if (Fu > 0) {  // deep_user_features (wide_deep.py:214-215) + its wide cross (:190-192)
+      st = hnm_linear_rows_f32(ctx, user_features, Fu, nullptr, n, n, Fu, w->duf_w, Fu, w->duf_b,
+                               w->d, xf, ldx, 0);
+      if (st) return st;
+      if (w->wuf_w && w->wide_feat) {
+        st = hnm_linear_rows_f32(ctx, user_features, Fu, nullptr, n, n, Fu, w->wuf_w, Fu,
+                                 w->wuf_b, Fu, wf, Fu, 0);
+        if (st) return st;
+        // wide feature term = wf . final_w[U + I : U + I + Fu]
+        st = hnm_linear_rows_f32(ctx, wf, Fu, nullptr, n, n, Fu, w->wide_feat, Fu, nullptr, 1, w1,
+                                 1, 0);
+        if (st) return st;
+        wide = w1;
+      }
+    }
+    if (Fi > 0) {  // deep_item_features (:216-217) + its wide cross (:193-195)
+      st = hnm_linear_rows_f32(ctx, item_features, Fi, nullptr, n, n, Fi, itf->dif_w, Fi,
+                               itf->dif_b, w->d, xf + (Fu > 0 ? w->d : 0), ldx, 0);
+      if (st) return st;
+      if (itf->wif_w && itf->wide_feat) {
+        st = hnm_linear_rows_f32(ctx, item_features, Fi, nullptr, n, n, Fi, itf->wif_w, Fi,
+                                 itf->wif_b, Fi, wf, Fi, 0);
+        if (st) return st;
+        st = hnm_linear_rows_f32(ctx, wf, Fi, nullptr, n, n, Fi, itf->wide_feat, Fi, nullptr, 1,
+                                 w2, 1, 0);
+        if (st) return st;
+        wide2 = w2;
+      }
+    }
+  }
+  hipLaunchKernelGGL(widedeep_pair_kernel, dim3((unsigned)n), dim3(256), 0, ctx->stream, *w,
+                     user_ids, item_ids, n, xf, ldx, wide, wide2, out, ctx->err_dev);
+  HNM_LAUNCH_CHECK();
+  return HNM_OK;
+}
+
 extern "C" hnm_status hnm_widedeep_pair_scores_f32(hnm_ctx* ctx, const hnm_widedeep_weights* w,
                                                    const int64_t* user_ids,
                                                    const int64_t* item_ids,
                                                    const float* user_features, int64_t n,
                                                    float* out) {
-  HNM_REQUIRE(ctx && w && user_ids && item_ids && out, HNM_EINVAL, "widedeep_pair: NULL argument");
-  HNM_REQUIRE(w->l1 <= 512 && w->l2 <= 512 && w->l3 <= 512 && w->l1_in <= 512, HNM_EUNSUPPORTED,
-              "widedeep_pair: widths must be <= 512");
-  if (n <= 0) return HNM_OK;
-  float* xu = nullptr;
-  float* wide = nullptr;
-  if (w->num_user_features > 0) {
-    HNM_REQUIRE(user_features && w->duf_w, HNM_EINVAL, "widedeep_pair: user_features required");
-    const int F = w->num_user_features;
-    const size_t szx = hnm_align((size_t)n * w->d * 4), szf = hnm_align((size_t)n * F * 4);
-    void* wsp;
-    hnm_status st = hnm_workspace(ctx, szx + szf + hnm_align((size_t)n * 4), &wsp);
-    if (st) return st;
-    xu = (float*)wsp;
-    float* wf = (float*)((char*)wsp + szx);
-    wide = (float*)((char*)wsp + szx + szf);
-    st = hnm_linear_rows_f32(ctx, user_features, F, nullptr, n, n, F, w->duf_w, F, w->duf_b,
-                             w->d, xu, w->d, 0);
-    if (st) return st;
-    if (w->wuf_w && w->wide_feat) {
-      st = hnm_linear_rows_f32(ctx, user_features, F, nullptr, n, n, F, w->wuf_w, F, w->wuf_b, F,
-                               wf, F, 0);
-      if (st) return st;
-      // wide feature term = wf . final_w[U + I : U + I + F]
-      st = hnm_linear_rows_f32(ctx, wf, F, nullptr, n, n, F, w->wide_feat, F, nullptr, 1, wide, 1, 0);
-      if (st) return st;
-    } else {
-      wide = nullptr;
-    }
-  }
-  hipLaunchKernelGGL(widedeep_pair_kernel, dim3((unsigned)n), dim3(256), 0, ctx->stream, *w,
-                     user_ids, item_ids, n, xu, wide, out, ctx->err_dev);
-  HNM_LAUNCH_CHECK();
-  return HNM_OK;
+  return hnm_widedeep_pair_scores_ex_f32(ctx, w, nullptr, user_ids, item_ids, user_features,
+                                         nullptr, n, out);
 }

@@ -11,6 +11,7 @@ projections, and layers 2-3 run as fp32 MFMA chains fused with the top-K.
 """
 from __future__ import annotations
 
+import ctypes as C
 from typing import Dict, List, Optional
 
 import torch
@@ -108,10 +109,17 @@ class WideDeep(RecModule):
         nn.init.zeros_(self.final_layer.bias)
 
     # ------------------------------------------------------------------ HIP plumbing
+    def _wide_zero(self, n, device):
+        """use_wide_user_item=False: the one-hot wide terms are absent (wide_deep.py:179-188);
+        the kernels read an all-zero wide vector instead (adding +0.0 changes no score)."""
+        z = getattr(self, "_zeros", None)
+        if z is None or z.numel() < n or z.device != device:
+            z = torch.zeros(max(n, self.num_users, self.num_items), dtype=torch.float32,
+                            device=device)
+            self._zeros = z
+        return z
+
     def _weights(self):
-        if not self.use_wide_user_item:
-            raise ValueError("the fused Wide&Deep kernel expects use_wide_user_item=True "
-                             "(the reference default and config)")
         lin = [m for m in self.deep_network if isinstance(m, nn.Linear)]
         bns = [m for m in self.deep_network if isinstance(m, nn.BatchNorm1d)]
         if len(lin) not in (2, 3):
@@ -135,12 +143,20 @@ class WideDeep(RecModule):
         fw = t(self.final_layer.weight.reshape(-1))  # [wide_dim + last]
         duf = getattr(self, "deep_user_features", None)
         wuf = getattr(self, "wide_user_features", None) if self.use_wide_features else None
+        # final_layer input order (wide_deep.py:225): [user one-hot | item one-hot]
+        # (use_wide_user_item), [user features | item features] (use_wide_features), deep
+        feat0 = U + I if self.use_wide_user_item else 0
+        if self.use_wide_user_item:
+            wu, wi = fw, fw + 4 * U
+        else:
+            z = self._wide_zero(max(U, I), self.final_layer.weight.device)
+            wu = wi = z.data_ptr()
         ptrs = [t(self.deep_user_embedding.weight), t(self.deep_item_embedding.weight),
                 t(lin[0].weight), t(lin[0].bias), *bn(bns[0]),
                 t(lin[1].weight), t(lin[1].bias), *bn(bns[1]),
                 t(lin[2].weight) if has3 else None, t(lin[2].bias) if has3 else None,
                 *(bn(bns[2]) if has3 else none4),
-                fw, fw + 4 * U, (fw + 4 * (U + I)) if wuf is not None else None,
+                wu, wi, (fw + 4 * feat0) if wuf is not None else None,
                 fw + 4 * self._calculate_wide_dim(), t(self.final_layer.bias),
                 t(duf.weight) if duf is not None else None, t(duf.bias) if duf is not None else None,
                 t(wuf.weight) if wuf is not None else None, t(wuf.bias) if wuf is not None else None]
@@ -151,6 +167,21 @@ class WideDeep(RecModule):
                                  lin[2].out_features if has3 else 0, self.num_user_features,
                                  float(bns[0].eps))
         return w, keep
+
+    def _item_feature_weights(self, keep):
+        """hnm_widedeep_item_features of a model with num_item_features > 0."""
+        dif = self.deep_item_features
+        wif = getattr(self, "wide_item_features", None) if self.use_wide_features else None
+        fw = self.final_layer.weight.reshape(-1)
+        off = (self.num_users + self.num_items if self.use_wide_user_item else 0) + \
+            (self.num_user_features if self.use_wide_features else 0)
+        vals = [f32c(dif.weight), f32c(dif.bias)]
+        if wif is not None:
+            vals += [f32c(wif.weight), f32c(wif.bias),
+                     f32c(fw[off: off + self.num_item_features])]
+        keep.extend(vals)
+        ptrs = [v.data_ptr() for v in vals] + [None] * (5 - len(vals))
+        return _lib.WideDeepItemFeatures(*ptrs, self.num_item_features)
 
     def _features(self, user_features, n, device):
         if self.num_item_features > 0:
@@ -168,22 +199,32 @@ class WideDeep(RecModule):
 
     # ------------------------------------------------------------------ reference API
     def forward(self, user_ids, item_ids, user_features=None, item_features=None):
-        """Pairwise scores (`wide_deep.py:157-230`)."""
-        if item_features is not None and self.num_item_features > 0:
-            raise ValueError("item features are not supported by the HIP pair path")
+        """Pairwise scores (`wide_deep.py:157-230`), user and item side features included.
+        As in the reference, a model built with features needs them: its deep network's
+        input width counts them (`:118-123`)."""
         w, keep = self._weights()
         u = self._ids(user_ids, self.num_users)
         i = self._ids(item_ids, self.num_items, "item_ids")
-        f = None
-        if self.num_user_features > 0 and user_features is not None:
+        f = fi = None
+        if self.num_user_features > 0:
+            if user_features is None:
+                raise ValueError("user_features are required when num_user_features > 0")
             f = f32c(user_features).to(u.device)
-        elif self.num_user_features > 0:
-            raise ValueError("user_features are required when num_user_features > 0")
+            if f.shape != (u.numel(), self.num_user_features):
+                raise ValueError(f"user_features must be [{u.numel()}, {self.num_user_features}]")
+        itf = None
+        if self.num_item_features > 0:
+            if item_features is None:
+                raise ValueError("item_features are required when num_item_features > 0")
+            fi = f32c(item_features).to(u.device)
+            if fi.shape != (u.numel(), self.num_item_features):
+                raise ValueError(f"item_features must be [{u.numel()}, {self.num_item_features}]")
+            itf = self._item_feature_weights(keep)
         out = torch.empty(u.numel(), dtype=torch.float32, device=u.device)
         c = _lib.ctx(u.device)
-        _lib.check(_lib.fn("hnm_widedeep_pair_scores_f32")(c, w, _lib.ptr(u), _lib.ptr(i),
-                                                           _lib.ptr(f), u.numel(), _lib.ptr(out)),
-                   "hnm_widedeep_pair_scores_f32")
+        _lib.check(_lib.fn("hnm_widedeep_pair_scores_ex_f32")(
+            c, w, None if itf is None else C.byref(itf), _lib.ptr(u), _lib.ptr(i), _lib.ptr(f),
+            _lib.ptr(fi), u.numel(), _lib.ptr(out)), "hnm_widedeep_pair_scores_ex_f32")
         _lib.sync_check(u.device)
         return out.squeeze()
 

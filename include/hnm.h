@@ -274,6 +274,25 @@ hnm_status hnm_widedeep_scores_f32(hnm_ctx* ctx, const hnm_widedeep_weights* w,
 hnm_status hnm_widedeep_pair_scores_f32(hnm_ctx* ctx, const hnm_widedeep_weights* w,
                                         const int64_t* user_ids, const int64_t* item_ids,
                                         const float* user_features, int64_t n, float* out);
+/* Item-side feature weights of WideDeep(num_item_features > 0) (wide_deep.py:101-103,
+ * 116-117): deep_item_features [d, Fi] + bias, wide_item_features [Fi, Fi] + bias (NULL
+ * when use_wide_features=False) and its slice of final_layer.weight. */
+typedef struct {
+  const float* dif_w;
+  const float* dif_b;
+  const float* wif_w;
+  const float* wif_b;
+  const float* wide_feat;
+  int32_t num_item_features;
+} hnm_widedeep_item_features;
+/* WideDeep.forward(user_ids, item_ids, user_features, item_features): pairwise scores with
+ * per-pair item features [n, Fi] (wide_deep.py:190-195, 214-217).  itf may be NULL (no
+ * item features).  A NULL w->wide_user / w->wide_item means use_wide_user_item=False. */
+hnm_status hnm_widedeep_pair_scores_ex_f32(hnm_ctx* ctx, const hnm_widedeep_weights* w,
+                                           const hnm_widedeep_item_features* itf,
+                                           const int64_t* user_ids, const int64_t* item_ids,
+                                           const float* user_features, const float* item_features,
+                                           int64_t n, float* out);
 
 /* ---- top-K merge (item partitions, item shards across GPUs) ------------------------
  * Candidates of row b: for g < G: cand[g*gstride + b*bstride + j], j < kc (value, global

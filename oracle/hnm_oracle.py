@@ -204,30 +204,42 @@ def batchnorm_eval(x, sd, prefix, eps=1e-5):
 
 
 def widedeep_forward(sd, user_ids, item_ids, user_features=None, num_users=None,
-                     num_items=None):
-    """`WideDeep.forward` (`wide_deep.py:157-230`) with use_wide_user_item and
-    use_wide_features on.  The one-hot wide input (`:180-188`) times `final_layer.weight`
-    is restated as the two weights it selects: w[u] + w[U + i]; the deep tower is
-    Linear -> ReLU -> BatchNorm(eval) -> Dropout(identity) per layer (`:125-134`)."""
+                     num_items=None, item_features=None):
+    """`WideDeep.forward` (`wide_deep.py:157-230`), use_wide_features on.  The one-hot wide
+    input (`:180-188`, present when use_wide_user_item: the state dict then holds
+    `wide_user_embedding`) times `final_layer.weight` is restated as the two weights it
+    selects: w[u] + w[U + i]; the feature crosses follow in the concat order (`:190-195`);
+    the deep tower is Linear -> ReLU -> BatchNorm(eval) -> Dropout(identity) per layer
+    (`:125-134`) over [e_u; e_i; user-feature proj; item-feature proj] (`:207-219`)."""
     user_ids = np.asarray(user_ids)
     item_ids = np.asarray(item_ids)
     U = num_users if num_users is not None else sd["deep_user_embedding.weight"].shape[0]
     I = num_items if num_items is not None else sd["deep_item_embedding.weight"].shape[0]
     wf = sd["final_layer.weight"][0]
     deep_in = [sd["deep_user_embedding.weight"][user_ids], sd["deep_item_embedding.weight"][item_ids]]
-    wide_terms = wf[user_ids] + wf[U + item_ids]
-    off = U + I
+    wide_terms = np.zeros(len(user_ids), F32)
+    off = 0
+    if "wide_user_embedding.weight" in sd:  # use_wide_user_item
+        wide_terms = wf[user_ids] + wf[U + item_ids]
+        off = U + I
     has_uf = "wide_user_features.weight" in sd
     nuf = sd["wide_user_features.weight"].shape[0] if has_uf else 0
     if has_uf and user_features is not None:
         wuf = linear(user_features, sd["wide_user_features.weight"], sd["wide_user_features.bias"])
         wide_terms = wide_terms + wuf @ wf[off:off + nuf]
     off += nuf
-    if "wide_item_features.weight" in sd:
-        off += sd["wide_item_features.weight"].shape[0]
+    has_if = "wide_item_features.weight" in sd
+    nif = sd["wide_item_features.weight"].shape[0] if has_if else 0
+    if has_if and item_features is not None:
+        wif = linear(item_features, sd["wide_item_features.weight"], sd["wide_item_features.bias"])
+        wide_terms = wide_terms + wif @ wf[off:off + nif]
+    off += nif
     if "deep_user_features.weight" in sd and user_features is not None:
         deep_in.append(linear(user_features, sd["deep_user_features.weight"],
                               sd["deep_user_features.bias"]))
+    if "deep_item_features.weight" in sd and item_features is not None:
+        deep_in.append(linear(item_features, sd["deep_item_features.weight"],
+                              sd["deep_item_features.bias"]))
     x = np.concatenate(deep_in, axis=1)
     for li in widedeep_layers(sd):
         x = relu(linear(x, sd[f"deep_network.{li}.weight"], sd[f"deep_network.{li}.bias"]))

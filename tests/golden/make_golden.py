@@ -241,6 +241,48 @@ def gen_widedeep(models):
          user_ids=users, user_features=feats, dense=dense, topk=rec, **with_prefix("sd/", sdf))
 
 
+def gen_widedeep_edges(models):
+    """WideDeep surface edges: pairwise forward with user AND item features
+    (wide_deep.py:190-195, 214-217), and use_wide_user_item=False (no one-hot wide terms:
+    :179-188, wide_dim :83-90) through predict_all_items / recommend / forward."""
+    U, I = 120, 90
+    Fu, Fi = 6, 5
+    sd = syn.widedeep_state_dict(U, I, 16, (64, 32), num_user_features=Fu, num_item_features=Fi,
+                                 seed=13, bias_scale=0.05, randomize_bn=True, emb_scale=10.0)
+    m = load(models.WideDeep(num_users=U, num_items=I, num_user_features=Fu,
+                             num_item_features=Fi, embedding_dim=16, deep_layers=[64, 32]), sd)
+    rng = np.random.Generator(np.random.PCG64(14))
+    pu = syn.user_batch(U, 40, seed=15)
+    pi = syn.user_batch(I, 40, seed=16)
+    uf = rng.standard_normal((40, Fu)).astype(np.float32)
+    itf = rng.standard_normal((40, Fi)).astype(np.float32)
+    with torch.no_grad():
+        pair = m(torch.from_numpy(pu), torch.from_numpy(pi), torch.from_numpy(uf),
+                 torch.from_numpy(itf)).numpy()
+    save("widedeep_itemfeat.npz", U=U, I=I, Fu=Fu, Fi=Fi, d=16, deep_layers=np.array([64, 32]),
+         pair_users=pu, pair_items=pi, user_features=uf, item_features=itf, pair_scores=pair,
+         **with_prefix("sd/", sd))
+
+    # use_wide_user_item=False: the state dict has no wide_{user,item}_embedding and the
+    # final layer is [1, deep_last]
+    U2, I2, K = 200, 150, 12
+    sd2 = syn.widedeep_state_dict(U2, I2, 32, (128, 64), seed=17, bias_scale=0.05,
+                                  randomize_bn=True, emb_scale=10.0)
+    sd2 = {k: v for k, v in sd2.items() if not k.startswith("wide_")}
+    sd2["final_layer.weight"] = sd2["final_layer.weight"][:, U2 + I2:].copy()
+    m2 = load(models.WideDeep(num_users=U2, num_items=I2, embedding_dim=32, deep_layers=[128, 64],
+                              use_wide_user_item=False, top_k=K), sd2)
+    users = tagged_users(U2, 24, seed=18)
+    with torch.no_grad():
+        ut = torch.from_numpy(users)
+        dense = m2.predict_all_items(ut).numpy()
+        rec = m2.recommend(ut).numpy()
+        pair2 = m2(torch.from_numpy(pu % U2), torch.from_numpy(pi % I2)).numpy()
+    save("widedeep_nowide.npz", U=U2, I=I2, K=K, d=32, deep_layers=np.array([128, 64]),
+         user_ids=users, dense=dense, topk=rec, pair_users=pu % U2, pair_items=pi % I2,
+         pair_scores=pair2, **with_prefix("sd/", sd2))
+
+
 def gen_mf(models):
     U, I, K = 500, 300, 12
     sd = syn.mf_state_dict(U, I, 64, seed=0, bias_scale=0.05)
@@ -423,6 +465,8 @@ if __name__ == "__main__":
     torch.set_num_threads(8)
     models = install_stubs()
     which = sys.argv[1:] or ["small"]
+    if "edges" in which:
+        gen_widedeep_edges(models)
     if "small" in which:
         gen_ncf(models)
         gen_lightgcn(models)

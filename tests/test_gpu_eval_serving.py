@@ -198,3 +198,30 @@ def test_recommendation_metrics_formulas():
     assert abs(float(r["precision_at_k"]) - (1 / 3) / 2) < 1e-12
     idcg = 1 + 1 / np.log2(3)
     assert abs(float(r["ndcg_at_k"]) - (1 / np.log2(3)) / idcg / 2) < 1e-12
+
+
+def test_lightning_checkpoint_fixture_serves_on_gpu():
+    """The committed Lightning-2.x-shaped .ckpt fixtures (tests/golden/lightning/) loaded by
+    Recommender.load_checkpoints onto the GPU serve the same top-K as the oracle run on
+    the checkpoint's own state_dict (NeuralCF and LightGCN with its graph)."""
+    import os
+    from hnm_recommendation_amd.serving import load_checkpoint
+    root = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "lightning")
+    U, I = 60, 40
+    ei = syn.bipartite_edge_index(U, I, 300, seed=23)
+    srv = Recommender(U, I, device=DEV)
+    assert srv.load_checkpoints(root, graph=(torch.from_numpy(ei), None)) == ["lightgcn", "neural_cf"]
+    users = np.arange(0, 50)
+    sd = {k: v.numpy() for k, v in load_checkpoint(
+        os.path.join(root, "neural_cf", "epoch=3-step=1200.ckpt"))["state_dict"].items()}
+    got = srv.models["neural_cf"].recommend(torch.from_numpy(users).to(DEV)).cpu().numpy()
+    assert_topk_equivalent(got, O.ncf_predict_all_items(sd, users), 12, what="ckpt ncf")
+    lsd = load_checkpoint(os.path.join(root, "lightgcn", "epoch=3-step=1200.ckpt"))["state_dict"]
+    fu, fi = O.lightgcn_forward(lsd["embeddings.weight"].numpy(),
+                                O.lightgcn_set_graph(ei, None, U + I), U, 3)
+    got = srv.models["lightgcn"].recommend(torch.from_numpy(users).to(DEV)).cpu().numpy()
+    assert_topk_equivalent(got, O.lightgcn_predict_all_items(fu, fi, users), 12, what="ckpt lgcn")
+    one = srv.get_recommendations(3, model_name="neural_cf", num_items=5, include_scores=True)
+    assert len(one["recommendations"]) == 5
+    with pytest.raises(ValueError):
+        srv.get_recommendations(3, model_name="neural_cf", num_items=101)  # serve.py:56 le=100

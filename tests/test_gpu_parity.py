@@ -355,3 +355,33 @@ def test_lightgcn_propagate_for_equals_forward(alpha, d):
     assert torch.equal(fb, fu[users])
     with pytest.raises(IndexError):
         m.propagate_for(torch.tensor([U]))
+
+
+def test_widedeep_item_features_pair_golden():
+    """WideDeep.forward with user AND item features (wide_deep.py:190-195, 214-217) vs the
+    reference's own outputs."""
+    g = load_golden("widedeep_itemfeat.npz")
+    m = to_module(WideDeep(int(g["U"]), int(g["I"]), num_user_features=int(g["Fu"]),
+                           num_item_features=int(g["Fi"]), embedding_dim=int(g["d"]),
+                           deep_layers=[int(x) for x in g["deep_layers"]]), g["sd"])
+    pair = m(t(g["pair_users"]), t(g["pair_items"]), t(g["user_features"]),
+             t(g["item_features"])).cpu().numpy()
+    assert_scores_close(pair, g["pair_scores"], "wd item-feature pair")
+    with pytest.raises(ValueError):
+        m(t(g["pair_users"]), t(g["pair_items"]), t(g["user_features"]))  # item features missing
+
+
+def test_widedeep_no_wide_user_item_golden():
+    """use_wide_user_item=False (no one-hot wide terms) through recommend / predict_all_items /
+    forward vs the reference's own outputs."""
+    g = load_golden("widedeep_nowide.npz")
+    m = to_module(WideDeep(int(g["U"]), int(g["I"]), embedding_dim=int(g["d"]),
+                           deep_layers=[int(x) for x in g["deep_layers"]],
+                           use_wide_user_item=False, top_k=int(g["K"])), g["sd"])
+    users = t(g["user_ids"])
+    dense = m.predict_all_items(users).cpu().numpy()
+    assert_scores_close(dense, g["dense"], "wd no-wide dense")
+    assert_topk_equivalent(m.recommend(users).cpu().numpy(), g["dense"], int(g["K"]))
+    assert_topk_equivalent(g["topk"], dense, int(g["K"]))
+    pair = m(t(g["pair_users"]), t(g["pair_items"])).cpu().numpy()
+    assert_scores_close(pair, g["pair_scores"], "wd no-wide pair")

@@ -153,3 +153,19 @@ def test_lightgcn_full_catalogue_oracle():
     assert_scores_close(fi[g["F_I_sample_ids"]], g["F_I_rows"], "F_I rows")
     v, i = O.topk(O.lightgcn_predict_all_items(fu, fi, g["user_ids"][:16]), 12)
     assert_topk_matches_reference(i, v, _rows(g, 16), what="lightgcn full")
+
+
+def test_widedeep_item_features_pair_matches_reference():
+    g = load_golden("widedeep_itemfeat.npz")
+    pair = O.widedeep_forward(g["sd"], g["pair_users"], g["pair_items"], g["user_features"],
+                              item_features=g["item_features"])
+    assert_scores_close(pair, g["pair_scores"], "wd item-feature pair")
+
+
+def test_widedeep_no_wide_user_item_matches_reference():
+    g = load_golden("widedeep_nowide.npz")
+    dense = O.widedeep_predict_all_items(g["sd"], g["user_ids"])
+    assert_scores_close(dense, g["dense"], "wd no-wide dense")
+    assert_topk_equivalent(g["topk"], dense, int(g["K"]))
+    pair = O.widedeep_forward(g["sd"], g["pair_users"], g["pair_items"])
+    assert_scores_close(pair, g["pair_scores"], "wd no-wide pair")
