@@ -125,13 +125,14 @@ def test_fallback_rows_exact():
     sd["gmf_item_embedding.weight"] = np.zeros_like(sd["gmf_item_embedding.weight"])
     sd["mlp_item_embedding.weight"][:] = sd["mlp_item_embedding.weight"][:1]  # identical items
     m = to_module(NeuralCF(U, I), sd)
-    users = torch.tensor([1, 2, 3, 4, 5], device=DEV)
+    # 16 rows: below that the library routes the batch to the exact scan (ncf.hip, serve path)
+    users = torch.arange(1, 17, device=DEV)
     f = {3: set(range(I)) - {7, 9000}}
     (ev, ei), (pv, pi), stats = topk_both(m, users, f)
     assert np.array_equal(ei, pi) and np.array_equal(ev.view(np.uint32), pv.view(np.uint32))
     assert pi[0].tolist() == list(range(12))  # ties -> lowest item ids
     assert pi[2, :2].tolist() == [7, 9000] and np.isneginf(pv[2, 2:]).all()
-    assert stats[2] == 5
+    assert stats[2] == 16
 
 
 def test_unusable_bound_falls_back():
