@@ -322,7 +322,6 @@ def main():
     ap.add_argument("--batch", type=int, default=4096)
     ap.add_argument("--workload", default="ncf")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--scan-users", type=int, default=0, help="tuning: users per f16 scan iteration")
     ap.add_argument("--latency", action="store_true",
                     help="serve-path B=1 latency (p50/p99) instead of the throughput line")
     ap.add_argument("--weights", default="init", choices=["init", "personal"],
@@ -342,8 +341,6 @@ def main():
     t_setup = time.perf_counter()
     if args.exact:
         _lib.set_prefilter(device, False)
-    if args.scan_users:
-        _lib.set_option(device, _lib.HNM_OPT_SCAN_USERS, args.scan_users)
     wl, info, cpu = build_workload(args.workload, rank, world, device, B, args.exact,
                                    args.weights)
     step, per_launch, bound, kernel = wl["step"], wl["per_launch"], wl["bound"], wl["kernel"]

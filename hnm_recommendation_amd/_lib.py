@@ -231,7 +231,6 @@ def kernel_timing(device):
 
 
 HNM_OPT_PREFILTER = 1
-HNM_OPT_SCAN_USERS = 2
 HNM_OPT_STATS = 3
 
 

@@ -36,8 +36,11 @@ constexpr int64_t DCERT_MIN_ITEMS = 8192;
 constexpr int64_t DCERT_SAMPLE = 12288;
 constexpr float DCERT_RHO = 0.00146484375f;  // 3 u16 = 3 * 2^-11
 constexpr int DCERT_MAX_NP = 64;
-// scan occupancy (workgroups per CU): the d=128 A operand needs 32 more VGPRs
-__host__ __device__ constexpr int dcert_wg_per_cu(int DP) { return DP > 64 ? 3 : 4; }
+#ifndef DOT_WG64
+#define DOT_WG64 3
+#endif
+// scan occupancy (workgroups per CU): two sub-tiles in flight need up to 168 VGPRs
+__host__ __device__ constexpr int dcert_wg_per_cu(int DP) { return DP > 64 ? 3 : DOT_WG64; }
 
 enum { DM_U, DM_I, DM_NI, DM_IB, DM_N };
 
@@ -315,16 +318,30 @@ __device__ __forceinline__ f32x16 mfma16(h8 a, h8 b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
 }
 
-// A wave holds 32 users' f16 rows as the MFMA A operand; 32-item tiles of I16 stream
-// through LDS (double-buffered, one barrier per tile).  acc[r] = approx dot of user row
-// mfma32_row(r, h) with item lane j.
-template <int DP, int MODE, bool BIAS>
+// A wave holds 32 users' f16 rows as the MFMA A operand; TI-item tiles of I16 (128 items at
+// DP = 64, 64 at DP = 128) stream through LDS, double-buffered with one barrier per tile, so a
+// wave has SUB = TI / 32 sub-tiles of MFMA + test work per barrier and the next tile's loads
+// (LD 16-B chunks per thread) a whole tile of work to land.  acc[r] = approx dot of user row
+// mfma32_row(r, h) with item lane j of the sub-tile.  THRESH: one v_cmp per score straight
+// into a ballot (SGPR pair), OR-reduced on the scalar unit; only a sub-tile with a pass
+// re-ballots its rows and appends.
+// MASK (compile-time): a filter CSR is present.  Its per-row cursor loads are the only global
+// loads inside the tile loop; in a kernel without them the waitcnt pass never has to assume a
+// pending load there (which otherwise costs vmcnt(0) -- the tile prefetch too -- per step).
+template <int DP, int MODE, bool BIAS, bool MASK>
 __global__ __launch_bounds__(256, dcert_wg_per_cu(DP)) void dot16_scan_kernel(DScanArgs A) {
   constexpr int KS = DP / 16;     // f16 MFMA k-steps
   constexpr int RS = DP + 8;      // LDS row stride (halfs): conflict-free b128 reads
   constexpr int CH = DP / 8;      // 16-B chunks per item row
-  constexpr int LD = TILE * CH / 256;  // chunks per thread per tile (1 or 2)
-  __shared__ __attribute__((aligned(16))) _Float16 vs[2][TILE * RS];
+#ifndef DOT_TI
+  constexpr int TI = DP <= 64 ? 128 : 64;  // items per LDS tile
+#else
+  constexpr int TI = DOT_TI;
+#endif
+  constexpr int SUB = TI / TILE;
+  constexpr int LD = TI * CH / 256;  // chunks per thread per tile (4)
+  __shared__ __attribute__((aligned(16))) _Float16 vs[2][TI * RS];
+  __shared__ float ibl[2][BIAS ? TI : 1];  // the tile's scaled item biases
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5, j = lane & 31;
   const int p = blockIdx.x;
@@ -332,7 +349,7 @@ __global__ __launch_bounds__(256, dcert_wg_per_cu(DP)) void dot16_scan_kernel(DS
   const int nu = (int)std::max<int64_t>(0, std::min<int64_t>(32, A.B - b0));
   const int64_t part_start = (int64_t)p * A.ipp;
   const int64_t part_end = std::min<int64_t>(A.I, part_start + A.ipp);
-  const int64_t S = A.istride;
+  const int64_t S = MODE == DSCAN_SAMPLE ? A.istride : 1;  // the strided sample is the only S > 1 pass
 
   h8 a[KS];
 #pragma unroll
@@ -340,11 +357,15 @@ __global__ __launch_bounds__(256, dcert_wg_per_cu(DP)) void dot16_scan_kernel(DS
     h8 z = {};
     a[s] = j < nu ? *reinterpret_cast<const h8*>(A.U16 + (b0 + j) * DP + 16 * s + 8 * h) : z;
   }
-  float tv[16];
+  // THRESH: minus the threshold of accumulator row r's user -- the MFMA chain's initial value,
+  // so the accumulator ends as approx - tau (-inf for rows past the batch: never passes).  The
+  // extra fp32 rounding of the chain by |tau| (a few 2^-24 of the score scale) is inside the
+  // 2^-18 guard dcert_tau_kernel leaves.
+  f32x16 ntv;
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
     const int64_t b = b0 + mfma32_row(r, h);
-    tv[r] = (MODE == DSCAN_THRESH && b < A.B) ? A.tau[b] : __builtin_inff();
+    ntv[r] = (MODE == DSCAN_THRESH && b < A.B) ? -A.tau[b] : -__builtin_inff();
   }
   int ccount = 0;  // THRESH: appends of user row (lane) in this partition
   float rmax[MODE == DSCAN_SAMPLE ? 16 : 1];  // SAMPLE: running max per C row
@@ -352,7 +373,7 @@ __global__ __launch_bounds__(256, dcert_wg_per_cu(DP)) void dot16_scan_kernel(DS
   for (int r = 0; r < (MODE == DSCAN_SAMPLE ? 16 : 1); ++r) rmax[r] = -__builtin_inff();
   int nm = INT_BIG;
   int64_t mpos = 0, mend = 0;
-  const bool masked = MODE != DSCAN_DENSE && A.mptr != nullptr;
+  constexpr bool masked = MODE != DSCAN_DENSE && MASK;
   if (masked && lane < nu) {
     const int64_t lo = A.mptr[b0 + lane], hi = A.mptr[b0 + lane + 1];
     mpos = mask_lower_bound(A.midx, lo, hi, (int)(part_start * S));
@@ -360,11 +381,15 @@ __global__ __launch_bounds__(256, dcert_wg_per_cu(DP)) void dot16_scan_kernel(DS
     nm = mpos < mend ? A.midx[mpos] : INT_BIG;
   }
   int32_t* seg = MODE == DSCAN_THRESH ? A.buf + (b0 * A.NP + p) * (int64_t)A.capp : nullptr;
-  const int64_t segstride = (int64_t)A.NP * A.capp;
+  const int segstride = A.NP * A.capp;  // row r's segment at r * segstride (< 2^31 / 32)
+  // Appends are queued in two registers per lane and stored once per tile, after the tile's
+  // prefetch has landed: vmcnt waits are in order, so a store inside the tile would make the
+  // next wait (at the first MFMA after it) also wait for the prefetch issued before it
+  int qo0 = -1, qo1 = -1, qi0 = 0, qi1 = 0;
 
-  const int64_t ntiles = part_end > part_start ? hnm_cdiv(part_end - part_start, TILE) : 0;
+  const int64_t ntiles = part_end > part_start ? hnm_cdiv(part_end - part_start, TI) : 0;
   h8 st[LD];
-  float nib = 0.f;
+  float nib = 0.f;  // thread tid < TI: the bias of tile item tid
   auto fetch = [&](int64_t base) {
 #pragma unroll
     for (int q = 0; q < LD; ++q) {
@@ -373,7 +398,7 @@ __global__ __launch_bounds__(256, dcert_wg_per_cu(DP)) void dot16_scan_kernel(DS
       h8 z = {};
       st[q] = n < part_end ? *reinterpret_cast<const h8*>(A.I16 + n * S * DP + 8 * c) : z;
     }
-    if (BIAS) nib = A.ibs[std::min<int64_t>(base + j, part_end - 1) * S];
+    if (BIAS && tid < TI) nib = A.ibs[std::min<int64_t>(base + tid, part_end - 1) * S];
   };
   auto stash = [&](int bf) {
 #pragma unroll
@@ -381,87 +406,133 @@ __global__ __launch_bounds__(256, dcert_wg_per_cu(DP)) void dot16_scan_kernel(DS
       const int f = tid + 256 * q, row = f / CH, c = f % CH;
       *reinterpret_cast<h8*>(&vs[bf][row * RS + 8 * c]) = st[q];
     }
+    if (BIAS && tid < TI) ibl[bf][tid] = nib;
   };
   if (ntiles > 0) {
     fetch(part_start);
     stash(0);
   }
   __syncthreads();
+  // drain every prologue load on every path into the loop (incl. ntiles == 0): otherwise the
+  // waitcnt pass merges a pending prologue load into the loop and waits vmcnt(0) -- i.e. for
+  // the tile prefetch too -- at the first use of a prologue register in every iteration
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0) (gfx9 encoding: expcnt 7, lgkmcnt 15)
   for (int64_t t = 0; t < ntiles; ++t) {
-    const int64_t base = part_start + t * TILE;
+    const int64_t tbase = part_start + t * TI;
     const int cur = (int)(t & 1);
-    const float ib = nib;
-    if (t + 1 < ntiles) fetch(base + TILE);
+    if (t + 1 < ntiles) fetch(tbase + TI);
     if (nu > 0) {
-      f32x16 acc = {};
-#pragma unroll
-      for (int s = 0; s < KS; ++s)
-        acc = mfma16(a[s], *reinterpret_cast<const h8*>(&vs[cur][j * RS + 16 * s + 8 * h]), acc);
-      const int64_t n = base + j;
-      const bool ivalid = n < part_end;
-      float sc[16];
-#pragma unroll
-      for (int r = 0; r < 16; ++r) sc[r] = BIAS ? acc[r] + ib : acc[r];
-      if (MODE == DSCAN_DENSE) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int64_t b = b0 + mfma32_row(r, h);
-          if (ivalid && b < A.B) A.dense[b * A.ldo + n] = sc[r];
-        }
-      } else {
+      // filtered (user, item) pairs of the sub-tile at base -> -inf (rare path)
+      auto apply_mask = [&](f32x16& sc, int64_t base, int64_t n) {
         const int64_t tile_end = std::min<int64_t>(base + TILE, part_end);
-        if (masked) {  // -inf for filtered (user, item) pairs of this tile (rare path)
-          const int64_t real_end = (tile_end - 1) * S + 1;  // real ids of this tile are < real_end
-          uint64_t mm = __ballot(lane < 32 && nm < real_end) & 0xffffffffull;
-          while (mm) {
-            const int u = __builtin_ctzll(mm);
-            mm &= mm - 1;
-            while (true) {
-              const int tgt = hnm_readlane_i(nm, u);
-              if (tgt >= real_end) break;
-              if (tgt % S == 0) {
+        const int64_t real_end = (tile_end - 1) * S + 1;  // real ids of this tile are < real_end
+        uint64_t mm = __ballot(lane < 32 && nm < real_end) & 0xffffffffull;
+        while (mm) {
+          const int uu = __builtin_ctzll(mm);
+          mm &= mm - 1;
+          while (true) {
+            const int tgt = hnm_readlane_i(nm, uu);
+            if (tgt >= real_end) break;
+            if (tgt % S == 0) {
 #pragma unroll
-                for (int r = 0; r < 16; ++r)
-                  if (mfma32_row(r, h) == u && n == tgt / S) sc[r] = -__builtin_inff();
-              }
-              if (lane == u) {
-                ++mpos;
-                nm = mpos < mend ? A.midx[mpos] : INT_BIG;
-              }
+              for (int r = 0; r < 16; ++r)
+                if (mfma32_row(r, h) == uu && n == tgt / S) sc[r] = -__builtin_inff();
+            }
+            if (lane == uu) {
+              ++mpos;
+              nm = mpos < mend ? A.midx[mpos] : INT_BIG;
             }
           }
         }
-        if (MODE == DSCAN_SAMPLE) {
+      };
+      // THRESH: acc[r] = approx - tau of row r's user (the MFMA chain starts from -tau), so a
+      // lane's test is one max3 tree over its 16 rows, + the item bias, and one ballot; only
+      // lanes with a pass compute their row bits and are walked (about one pass per 32 x 32
+      // sub-tile at ~100 candidates per row) -- no per-row ballots on the scalar unit
+      auto thresh = [&](const f32x16& acc, float ib, int64_t base, bool ivalid) {
+        float lm = acc[0];
 #pragma unroll
-          for (int r = 0; r < 16; ++r)
-            if (ivalid) rmax[r] = (sc[r] > rmax[r] || sc[r] != sc[r]) ? sc[r] : rmax[r];  // NaN sticks
-        } else {
-        // any pass in this tile?  one compare per score (v_cmp + s_or); with ~100 candidates
-        // per user about one tile in two has an append, so the append path stays lean:
-        // per row a ballot (a v_cmp into SGPRs) and the store only where it fired
-        bool any = false;
+        for (int r = 1; r < 16; ++r) lm = fmaxf(lm, acc[r]);
+        uint64_t lanes = __ballot(ivalid && !(lm + ib < 0.f));
+        if (!lanes) return;
+        unsigned bits = 0;
 #pragma unroll
-        for (int r = 0; r < 16; ++r) any |= !(sc[r] < tv[r]);
-        if (__ballot(ivalid && any)) {
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const uint64_t m = __ballot(ivalid && !(sc[r] < tv[r]));
-            if (!m) continue;
-            const unsigned lo = (unsigned)m, hi = (unsigned)(m >> 32);
-            const int i0 = mfma32_row(r, 0), i1 = mfma32_row(r, 1);  // compile-time rows
-            const int c0 = hnm_readlane_i(ccount, i0), c1 = hnm_readlane_i(ccount, i1);
-            const unsigned mine = h ? hi : lo;
-            const int pos = (h ? c1 : c0) + __popc(mine & ((1u << j) - 1));
-            if (((mine >> j) & 1) && pos < A.capp)
-              seg[(h ? i1 : i0) * segstride + pos] = (int32_t)n;
-            if (lane == i0) ccount += __popc(lo);
-            if (lane == i1) ccount += __popc(hi);
+        for (int r = 0; r < 16; ++r) bits |= !(acc[r] + ib < 0.f) ? 1u << r : 0u;
+        while (lanes) {  // uniform
+          const int l = __builtin_ctzll(lanes);
+          lanes &= lanes - 1;
+          unsigned rr = (unsigned)hnm_readlane_i((int)bits, l);
+          const int nl = (int)(base + (l & 31));
+          while (rr) {
+            const int r = __builtin_ctz(rr);
+            rr &= rr - 1;
+            const int row = (r & 3) + 8 * (r >> 2) + 4 * (l >> 5);  // mfma32_row(r, l >> 5)
+            if (lane == row) {  // the row's owner lane queues the append
+              if (ccount < A.capp) {
+                const int off = row * segstride + ccount;
+                if (qo0 < 0) {
+                  qo0 = off;
+                  qi0 = nl;
+                } else if (qo1 < 0) {
+                  qo1 = off;
+                  qi1 = nl;
+                } else {
+                  seg[off] = nl;  // queue full (rare)
+                }
+              }
+              ++ccount;
+            }
           }
         }
-        }  // THRESH
+      };
+      // two sub-tiles per step: both MFMA chains are issued before either is tested, so one
+      // chain's latency runs under the other's MFMAs and the first test
+#pragma unroll 1
+      for (int u = 0; u < SUB; u += 2) {
+        const int64_t baseA = tbase + TILE * u, baseB = baseA + TILE;
+        if (baseA >= part_end) break;  // uniform: partial last tile
+        const bool hasB = baseB < part_end;
+        f32x16 accA = MODE == DSCAN_THRESH ? ntv : f32x16{}, accB = accA;
+#pragma unroll
+        for (int s = 0; s < KS; ++s) {
+          accA = mfma16(a[s], *reinterpret_cast<const h8*>(&vs[cur][(TILE * u + j) * RS + 16 * s + 8 * h]), accA);
+          accB = mfma16(a[s], *reinterpret_cast<const h8*>(&vs[cur][(TILE * (u + 1) + j) * RS + 16 * s + 8 * h]), accB);
+        }
+#pragma unroll
+        for (int v = 0; v < 2; ++v) {
+          if (v == 1 && !hasB) break;
+          const int64_t base = v ? baseB : baseA;
+          const int64_t n = base + j;
+          const bool ivalid = n < part_end;
+          f32x16 acc = v ? accB : accA;
+          const float ib = BIAS ? ibl[cur][TILE * (u + v) + j] : 0.f;
+          if (masked) apply_mask(acc, base, n);
+          if (MODE == DSCAN_THRESH) {
+            thresh(acc, ib, base, ivalid);
+            continue;
+          }
+#pragma unroll
+          for (int r = 0; r < 16; ++r) acc[r] = BIAS ? acc[r] + ib : acc[r];
+          if (MODE == DSCAN_DENSE) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+              const int64_t b = b0 + mfma32_row(r, h);
+              if (ivalid && b < A.B) A.dense[b * A.ldo + n] = acc[r];
+            }
+          } else {  // SAMPLE
+#pragma unroll
+            for (int r = 0; r < 16; ++r)
+              if (ivalid) rmax[r] = (acc[r] > rmax[r] || acc[r] != acc[r]) ? acc[r] : rmax[r];  // NaN sticks
+          }
+        }
       }
     }
     if (t + 1 < ntiles) stash(cur ^ 1);
+    if (MODE == DSCAN_THRESH) {  // flush the queued appends (the prefetch has landed)
+      if (qo0 >= 0) seg[qo0] = qi0;
+      if (qo1 >= 0) seg[qo1] = qi1;
+      qo0 = qo1 = -1;
+    }
     __syncthreads();
   }
   if (MODE == DSCAN_THRESH && lane < nu) A.cnt[(b0 + lane) * A.NP + p] = ccount;
@@ -665,17 +736,26 @@ hnm_status dcert_prepare(hnm_ctx* ctx, const DotArgs& a, const DotCertShape& sh,
 
 template <int MODE>
 void launch_dscan(hnm_ctx* ctx, dim3 grid, const DScanArgs& s, int DP, bool bias) {
-#define HNM_DS(DPV)                                                                             \
-  if (bias)                                                                                     \
-    hipLaunchKernelGGL((dot16_scan_kernel<DPV, MODE, true>), grid, dim3(256), 0, ctx->stream, s); \
-  else                                                                                          \
-    hipLaunchKernelGGL((dot16_scan_kernel<DPV, MODE, false>), grid, dim3(256), 0, ctx->stream, s);
+#define HNM_DS2(DPV, BV)                                                                      \
+  if (s.mptr && MODE != DSCAN_DENSE)                                                          \
+    hipLaunchKernelGGL((dot16_scan_kernel<DPV, MODE, BV, MODE != DSCAN_DENSE>), grid,         \
+                       dim3(256), 0, ctx->stream, s);                                         \
+  else                                                                                        \
+    hipLaunchKernelGGL((dot16_scan_kernel<DPV, MODE, BV, false>), grid, dim3(256), 0,         \
+                       ctx->stream, s);
+#define HNM_DS(DPV)    \
+  if (bias) {          \
+    HNM_DS2(DPV, true) \
+  } else {             \
+    HNM_DS2(DPV, false) \
+  }
   if (DP == 64) {
     HNM_DS(64)
   } else {
     HNM_DS(128)
   }
 #undef HNM_DS
+#undef HNM_DS2
 }
 
 DScanArgs dscan_args(const DotCertWs& x, const DotArgs& a) {

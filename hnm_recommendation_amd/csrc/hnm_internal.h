@@ -26,7 +26,6 @@ struct hnm_ctx {
   hipEvent_t* ev0;
   hipEvent_t* ev1;
   int prefilter;                   // HNM_OPT_PREFILTER (default 1)
-  int scan_users;                  // HNM_OPT_SCAN_USERS (tuning: users per scan iteration)
   unsigned long long* stats_dev;   // pre-filter counters: rows, candidates, fallback rows
   int stats_on;                    // HNM_OPT_STATS (default 0: counting costs same-address atomics)
   // open two-phase top-K call (hnm_*_topk_begin_f32 ... hnm_*_topk_finish_f32): the

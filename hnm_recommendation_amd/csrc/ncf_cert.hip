@@ -380,27 +380,33 @@ __device__ __forceinline__ f32x16 mfma16(h8 a, h8 b, f32x16 c) {
 }
 
 // A wave owns 32 users, a workgroup 128; 32-item tiles of Q16/G16 go through LDS.
-// Per (user, tile): 4 f16 MFMAs for layer 2 (B = clamp(P~ + Q~), built with 16 packed
-// adds), 2 f16 MFMAs for wm . relu(H) (the accumulator tile reused as the B operand),
-// GMF once per tile for all 32 users (4 MFMAs).  v_mfma_f32_32x32x16_f16 B operand:
-// lane (j, h) holds B[k = 8h + e][col j], e = 0..7.
-// ABL: ablation bits for tools/scan_ablation.hip only (0 in the library): 1 = no threshold
-// test, 2 = no wm epilogue, 4 = no layer-2 MFMA, 8 = no P~ LDS reads, 16 = no GMF,
-// 32 = no tile loads (zero tiles staged; skipping the LDS stores instead lets the compiler
-// delete the work on the undefined tiles), 64 = no cross-half swap (EPI 2).
-template <int MODE, int EPI, int ABL = 0>
-__global__ __launch_bounds__(256, EPI == 4 ? 2 : HNM_SCAN_OCC) void ncf16_scan_kernel(ScanArgs A) {
+// Per (user pair, tile): layer 2 as 4 + 4 v_mfma_f32_32x32x16_f16 (two independent chains;
+// A = W2~, B = clamp(P~ + Q~) built with 16 packed adds per user; v_mfma_f32_32x32x16_f16 B
+// operand: lane (j, h) holds B[k = 8h + e][col j], e = 0..7), GMF once per tile for all 32
+// users (4 MFMAs).  THRESH / SAMPLE: the epilogue wm . relu(H~) of BOTH users runs on the matrix
+// pipe as 4 v_mfma_f32_16x16x32_f16 -- relu(H~) by the [0, 1] clamp of the f32 -> f16
+// converts, the 16x16x32 B operand taking each lane's 8 converted accumulator rows as they lie
+// (k-group g = lanes 16g..16g+15 = half g >> 1, items 16 (g & 1) + c), A rows 0/1 = wm on user
+// a's k-groups of items 0-15 / 16-31, rows 2/3 the same for user b -- so one MFMA sums both
+// halves of a column (no cross-lane swap), and the accumulator is seeded with the tile's folded
+// per-pair term (GMF + bound - threshold, pair-interleaved in LDS so lanes 0-15 read their 4
+// seeds as one b128).  Lanes 0-15 end with the 64 test values; 4 ballots assemble the pair's
+// 64-bit pass mask with bit u*32 + item (the lane layout of the append).  Measured against the
+// earlier packed-dot epilogue (16 v_dot2c + a permlane32 swap per pair, 1.94 ms) and a
+// software-pipelined two-waves-per-SIMD variant (2.1-2.2 ms): 1.87 ms (tools/scan_ablation.hip,
+// profiles/r2_ncf_scan_variants.txt).  DEBUG keeps a VALU epilogue (packed dots + swap).
+template <int MODE>
+__global__ __launch_bounds__(256, HNM_SCAN_OCC) void ncf16_scan_kernel(ScanArgs A) {
   constexpr int RS = 72;   // LDS row stride in halfs (144 B): conflict-free b128 reads
   constexpr int NU = 128;  // users per workgroup
+  constexpr bool FOLD = MODE == SCAN_THRESH || MODE == SCAN_SAMPLE;
   __shared__ __attribute__((aligned(16))) _Float16 qs[2][TILE * RS];  // double-buffered tiles
   __shared__ __attribute__((aligned(16))) _Float16 gs[2][TILE * RS];
   __shared__ __attribute__((aligned(16))) _Float16 ps[NU * 64];
-  __shared__ float gsm[4][32][33];
-  // EPI 2 (THRESH / SAMPLE): the per-user test terms are folded into the GMF table once per
-  // tile, gsm' = gmf + sgn * e_i - tau (sgn = +1 for the threshold test, -1 for the sample's
-  // lower bound); ut holds (tau or 0, cu) per user
-  constexpr bool FOLD = (EPI == 2 || EPI == 4 || EPI == 5 || EPI == 6) && (MODE == SCAN_THRESH || MODE == SCAN_SAMPLE);
-  __shared__ float2 ut[FOLD ? 4 : 1][32];
+  // per wave: the GMF table of its 32 users x the tile's 32 items (FOLD: folded test terms,
+  // pair-interleaved: g7 index below; DEBUG: gsm[row][item])
+  __shared__ __attribute__((aligned(16))) float gsm[4][32][33];
+  __shared__ float2 ut[4][32];  // FOLD: (tau or 0, cu) per user
 
   const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, j = lane & 31;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // uniform: scalar loop state
@@ -419,7 +425,7 @@ __global__ __launch_bounds__(256, EPI == 4 ? 2 : HNM_SCAN_OCC) void ncf16_scan_k
     if (ublk + r < A.B) v = *reinterpret_cast<const h8*>(A.P16 + (ublk + r) * 64 + 8 * c);
     *reinterpret_cast<h8*>(&ps[r * 64 + 8 * c]) = v;
   }
-  h8 aw[4], awm[2];
+  h8 aw[4];
 #pragma unroll
   for (int s = 0; s < 4; ++s) aw[s] = *reinterpret_cast<const h8*>(A.W2h + j * 64 + 16 * s + 8 * h);
   h8 ag[4];  // GMF A operand: this wave's users' wp*g_u rows
@@ -428,28 +434,32 @@ __global__ __launch_bounds__(256, EPI == 4 ? 2 : HNM_SCAN_OCC) void ncf16_scan_k
     h8 z = {};
     ag[s] = j < nu ? *reinterpret_cast<const h8*>(A.WG16 + (u0 + j) * 64 + 16 * s + 8 * h) : z;
   }
-#pragma unroll
-  for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-    for (int e = 0; e < 8; ++e) awm[s2][e] = A.wmh[mfma32_row(8 * s2 + e, h)];
-  // EPI 5: the wm rows of the pair epilogue -- user a's MFMAs carry wm in A row 0, user b's
-  // in A row 4, so one accumulator ends with a's total at (row 0 -> lanes 0-31, r = 0) and
-  // b's at (row 4 -> lanes 32-63, r = 0)
-  h8 awa[2], awb[2];
-#pragma unroll
-  for (int s2 = 0; s2 < 2; ++s2) {
-    awa[s2] = j == 0 ? awm[s2] : (h8){};
-    awb[s2] = j == 4 ? awm[s2] : (h8){};
-  }
-  h2 wm2[8];  // EPI 1: wm of this lane's accumulator rows, in pairs
-#pragma unroll
-  for (int r = 0; r < 16; r += 2)
-    wm2[r >> 1] = (h2){A.wmh[mfma32_row(r, h)], A.wmh[mfma32_row(r + 1, h)]};
   f32x16 b2c;
 #pragma unroll
   for (int r = 0; r < 16; ++r) b2c[r] = A.b2s[mfma32_row(r, h)];
-  const float cg = A.prm->cg;
-  const float ru = CERT_RHO * A.prm->unit;
+  // epilogue A operands (16x16x32: lane holds A[row lane & 15][k = 8 (lane >> 4) + e])
+  h8 ewa[2], ewb[2];
+  h2 wm2[8];  // DEBUG: wm of this lane's accumulator rows, in pairs
+  {
+    const int erow = lane & 15, eg = lane >> 4;
+#pragma unroll
+    for (int f = 0; f < 2; ++f)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const _Float16 wv = A.wmh[mfma32_row(8 * f + e, eg >> 1)];
+        ewa[f][e] = erow == (eg & 1) ? wv : (_Float16)0.f;
+        ewb[f][e] = erow == 2 + (eg & 1) ? wv : (_Float16)0.f;
+      }
+#pragma unroll
+    for (int r = 0; r < 16; r += 2)
+      wm2[r >> 1] = (h2){A.wmh[mfma32_row(r, h)], A.wmh[mfma32_row(r + 1, h)]};
+  }
+  float* const g7 = &gsm[wave][0][0];
+  // uniform scalars in SGPRs (the compiler cannot prove prm read-only, so it would keep them
+  // in VGPRs -- which are the scarce resource at three waves per SIMD)
+  const float cg = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(A.prm->cg)));
+  const float ru =
+      __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(CERT_RHO * A.prm->unit)));
   // per-user registers: lane u < nu follows user u0 + u
   const float cu = lane < nu ? ru * A.Cu[u0 + lane] : 0.f;
   float tv = __builtin_inff(), eu = 0.f;
@@ -473,24 +483,43 @@ __global__ __launch_bounds__(256, EPI == 4 ? 2 : HNM_SCAN_OCC) void ncf16_scan_k
   // tile staging: thread (row, c) moves 16 B of Q~ and of G~; tile t + 1 is fetched into
   // registers while tile t is scored, then stored to the other LDS buffer (one barrier
   // per tile)
-  const int srow = tid >> 3, sc = tid & 7;
+  // (row, 16-B chunk) of the thread's staging slot, recomputed where used: held across the
+  // tile loop they were spilled, and a spill reload's vmcnt wait also waits for the prefetch
+  auto srow_of = [&]() {
+    int v;
+    asm volatile("v_lshrrev_b32 %0, 3, %1" : "=v"(v) : "v"(tid));
+    return v;
+  };
+  auto sc_of = [&]() {
+    int v;
+    asm volatile("v_and_b32 %0, 7, %1" : "=v"(v) : "v"(tid));
+    return v;
+  };
   h8 nq = {}, ng = {};
   float nb = 0.f, nd = 0.f;  // per-item bound terms of lane j's next item
+  // the champion gather map is a SAMPLE-pass input only (compile-time null elsewhere: no
+  // dependent index loads, hence no mid-tile vmcnt waits, in the THRESH scan)
+  const int32_t* const sidx = MODE == SCAN_SAMPLE ? A.sidx : nullptr;
+  // 32-bit element offsets from the (uniform) table bases: the loads take an SGPR base and a
+  // VGPR offset, so no 64-bit per-lane addresses stay live across the tile loop (I * 64 <
+  // 2^31 is checked by the host)
   auto fetch = [&](int64_t base) {
-    const int64_t n = base + srow;
+    const int srow = srow_of(), sc = sc_of();
+    const int n = (int)(base + srow);
     nq = (h8){};
     ng = (h8){};
-    if (n < part_end && !(ABL & 32)) {
-      const int64_t it = A.sidx ? (int64_t)A.sidx[n] : n;
-      nq = *reinterpret_cast<const h8*>(A.Q16 + it * 64 + 8 * sc);
-      ng = *reinterpret_cast<const h8*>(A.G16 + it * 64 + 8 * sc);
+    if (n < part_end) {
+      const int it = sidx ? sidx[n] : n;
+      nq = *reinterpret_cast<const h8*>(A.Q16 + (uint32_t)(it * 64 + 8 * sc));
+      ng = *reinterpret_cast<const h8*>(A.G16 + (uint32_t)(it * 64 + 8 * sc));
     }
-    const int64_t cj = std::min<int64_t>(base + j, part_end - 1);
-    const int64_t nj = A.sidx ? (int64_t)A.sidx[cj] : cj;
-    nb = A.Bi[nj];
-    nd = A.Di[nj];
+    const int cj = (int)std::min<int64_t>(base + j, part_end - 1);
+    const int nj = sidx ? sidx[cj] : cj;
+    nb = A.Bi[(uint32_t)nj];
+    nd = A.Di[(uint32_t)nj];
   };
   auto stash = [&](int buf) {
+    const int srow = srow_of(), sc = sc_of();
     *reinterpret_cast<h8*>(&qs[buf][srow * RS + 8 * sc]) = nq;
     *reinterpret_cast<h8*>(&gs[buf][srow * RS + 8 * sc]) = ng;
   };
@@ -500,6 +529,10 @@ __global__ __launch_bounds__(256, EPI == 4 ? 2 : HNM_SCAN_OCC) void ncf16_scan_k
     stash(0);
   }
   __syncthreads();
+  // drain every prologue load on every path into the loop (incl. ntiles == 0): otherwise the
+  // waitcnt pass merges a pending prologue load into the loop and waits vmcnt(0) -- i.e. for
+  // the tile prefetch too -- at the first use of a prologue register in every iteration
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0) (gfx9 encoding: expcnt 7, lgkmcnt 15)
   for (int cur = 0; t < ntiles; cur ^= 1) {
     const int64_t base = part_start + t * TILE;
     const int64_t tn = t + 1;
@@ -507,20 +540,25 @@ __global__ __launch_bounds__(256, EPI == 4 ? 2 : HNM_SCAN_OCC) void ncf16_scan_k
     // the prefetch is the only global load in the tile body (vmcnt waits are in order: any
     // later load's wait would also wait for it)
     if (tn < ntiles) fetch(part_start + tn * TILE);
+    int lrow;  // lane (j, h)'s operand row offset in the tile buffers (recomputed: see srow_of)
+    asm volatile("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(lrow) : "v"(j), "v"(RS), "v"(8 * h));
 
     if (nu > 0) {
-    if (!(ABL & 16)) {  // GMF of the wave's 32 users x 32 items, in score units
+    {  // GMF of the wave's 32 users x 32 items, in score units
       f32x16 gacc = {};
 #pragma unroll
       for (int s = 0; s < 4; ++s)
-        gacc = mfma16(ag[s], *reinterpret_cast<const h8*>(&gs[cur][j * RS + 16 * s + 8 * h]), gacc);
+        gacc = mfma16(ag[s], *reinterpret_cast<const h8*>(&gs[cur][lrow + 16 * s]), gacc);
       if constexpr (FOLD) {
+        // folded test term gmf + sgn * e_i - tau (sgn = +1 for the threshold test, -1 for the
+        // sample's lower bound)
         constexpr float sgn = MODE == SCAN_THRESH ? 1.f : -1.f;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int row = mfma32_row(r, h);
           const float2 tc = ut[wave][row];
-          gsm[wave][row][j] = (gacc[r] * cg + sgn * fmaf(tc.y, dj, bj)) - tc.x;
+          g7[(((row >> 1) * 16 + (j & 15)) << 2) + ((row & 1) << 1) + (j >> 4)] =
+              (gacc[r] * cg + sgn * fmaf(tc.y, dj, bj)) - tc.x;
         }
       } else {
 #pragma unroll
@@ -529,10 +567,11 @@ __global__ __launch_bounds__(256, EPI == 4 ? 2 : HNM_SCAN_OCC) void ncf16_scan_k
     }
     h8 q[4];
 #pragma unroll
-    for (int s = 0; s < 4; ++s) q[s] = *reinterpret_cast<const h8*>(&qs[cur][j * RS + 16 * s + 8 * h]);
+    for (int s = 0; s < 4; ++s) q[s] = *reinterpret_cast<const h8*>(&qs[cur][lrow + 16 * s]);
     const int64_t n = base + j;
-    const bool ivalid = h == 0 && n < part_end;
     const int64_t tile_end = std::min<int64_t>(base + TILE, part_end);
+    const int nv = (int)(tile_end - base);  // valid items of the tile
+    const uint64_t vm32 = nv >= 32 ? 0xffffffffull : ((1ull << nv) - 1ull);
     unsigned mbits = 0;
     if (masked) {  // scanned items are real items here (identity map in the THRESH pass)
       uint64_t pend = __ballot(lane < 32 && nm < tile_end) & 0xffffffffull;
@@ -551,280 +590,105 @@ __global__ __launch_bounds__(256, EPI == 4 ? 2 : HNM_SCAN_OCC) void ncf16_scan_k
       }
     }
 
-    if constexpr (EPI == 2 || EPI == 4 || EPI == 5 || EPI == 6) {
-      // Two users per iteration: independent MFMA chains for users a and b, and ONE
-      // epilogue for both -- after the packed-dot partials, a single permlane32 swap of
-      // (a's partials, b's partials) and an add leave a's totals in lanes 0-31 and b's in
-      // lanes 32-63 (same fp32 operations and order as the one-user epilogue), so the GMF
-      // read, the bound, the test and the ballot are shared by the pair.  EPI 4 reads the
-      // next pair's P~ fragments and GMF term one iteration ahead.
-      constexpr bool PF = EPI == 4;
-      const float* gsmh = &gsm[wave][h][j];
-      h8 pn[8];
-      float gn = 0.f;
-      auto pload = [&](int ua_, int ub_) {
+    const _Float16* pw = &ps[(wave * 32) * 64 + 8 * h];  // user r, k-step s: pw[r * 64 + 16 s]
+    for (int u = 0; u < nu; u += 2) {
+      // user b = u + 1 even past nu (zero P~ rows; FOLD: folded term -inf / not stored)
+      const int ua = u, ub = u + 1;
+      const bool hasb = ub < nu;
+      const int uh = h ? ub : ua;
+      f32x16 acc0 = b2c, acc1 = b2c;
 #pragma unroll
-        for (int s = 0; s < 4; ++s) {
-          pn[s] = (ABL & 8) ? q[s] : *reinterpret_cast<const h8*>(&ps[(wave * 32 + ua_) * 64 + 8 * h + 16 * s]);
-          pn[4 + s] = (ABL & 8) ? q[(s + 1) & 3] : *reinterpret_cast<const h8*>(&ps[(wave * 32 + ub_) * 64 + 8 * h + 16 * s]);
+      for (int s = 0; s < 4; ++s) {
+        // each fragment is read right before its MFMA (fewer live registers than a prefetch)
+        const h8 pa = *reinterpret_cast<const h8*>(&pw[ua * 64 + 16 * s]);
+        const h8 pb = *reinterpret_cast<const h8*>(&pw[ub * 64 + 16 * s]);
+        h8 x = pa + q[s];
+        x = __builtin_elementwise_min(__builtin_elementwise_max(x, (h8){}), (h8)(_Float16)1.f);
+        h8 y = pb + q[s];
+        y = __builtin_elementwise_min(__builtin_elementwise_max(y, (h8){}), (h8)(_Float16)1.f);
+        acc0 = mfma16(aw[s], x, acc0);
+        acc1 = mfma16(aw[s], y, acc1);
+      }
+      if constexpr (FOLD) {
+        h8 ya[2], yb[2];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          ya[0][e] = (_Float16)acc0[e];
+          ya[1][e] = (_Float16)acc0[8 + e];
+          yb[0][e] = (_Float16)acc1[e];
+          yb[1][e] = (_Float16)acc1[8 + e];
         }
-        gn = (ABL & 16) ? 0.f : gsm[wave][h ? ub_ : ua_][j];
-      };
-      if (PF) pload(0, std::min(1, nu - 1));
-      for (int u = 0; u < nu; u += 2) {
-        // FOLD: user b = u + 1 even past nu (zero P~ rows, folded term -inf / not stored)
-        const int ua = u, ub = FOLD ? u + 1 : std::min(u + 1, nu - 1);
-        const bool hasb = u + 1 < nu;
-        const int uh = h ? ub : ua;
-        // FOLD: lane (j, h) reads its own user's row u + h (= uh) through a per-lane base
-        if (!PF) gn = (ABL & 16) ? 0.f : FOLD ? gsmh[u * 33] : gsm[wave][uh][j];
-        const float gmu = gn;
-        h8 pc[8];  // EPI 4: this pair's prefetched fragments (the next pair's go to pn)
 #pragma unroll
-        for (int c = 0; c < 8; ++c) pc[c] = pn[c];
-        if (PF && u + 2 < nu) pload(u + 2, std::min(u + 3, nu - 1));
-        f32x16 acc0 = b2c, acc1 = b2c;
-#pragma unroll
-        for (int s = 0; s < 4; ++s) {
-          // without the prefetch each fragment is read right before its MFMA (fewer live
-          // registers than the 8-fragment prefetch)
-          const h8 pa = PF ? pc[s] : (ABL & 8) ? q[s] : *reinterpret_cast<const h8*>(&ps[(wave * 32 + ua) * 64 + 8 * h + 16 * s]);
-          const h8 pb = PF ? pc[4 + s] : (ABL & 8) ? q[(s + 1) & 3] : *reinterpret_cast<const h8*>(&ps[(wave * 32 + ub) * 64 + 8 * h + 16 * s]);
-          h8 x = pa + q[s];
-          x = __builtin_elementwise_min(__builtin_elementwise_max(x, (h8){}), (h8)(_Float16)1.f);
-          h8 y = pb + q[s];
-          y = __builtin_elementwise_min(__builtin_elementwise_max(y, (h8){}), (h8)(_Float16)1.f);
-          if (ABL & 4) {
-            acc0[s] += (float)x[0] + (float)x[7];
-            acc1[s] += (float)y[0] + (float)y[7];
-          } else {
-            acc0 = mfma16(aw[s], x, acc0);
-            acc1 = mfma16(aw[s], y, acc1);
-          }
+        for (int f = 0; f < 2; ++f) {
+          ya[f] = __builtin_elementwise_min(__builtin_elementwise_max(ya[f], (h8){}), (h8)(_Float16)1.f);
+          yb[f] = __builtin_elementwise_min(__builtin_elementwise_max(yb[f], (h8){}), (h8)(_Float16)1.f);
         }
-        if constexpr (FOLD) {
-          // wm . relu(H~): the chains of user a / b are seeded with the folded term of that
-          // user's half; after the swap, lanes 0-31 hold user a's test value, lanes 32-63 b's
-          float val;
-          if constexpr (EPI == 5) {
-            // wm . relu(H~) of both users on the matrix pipe (4 MFMAs into one accumulator
-            // seeded with the folded term); relu by the [0, 1] clamp of the converts
-            h8 y[4];
-#pragma unroll
-            for (int e = 0; e < 8; ++e) {
-              y[0][e] = (_Float16)acc0[e];
-              y[1][e] = (_Float16)acc0[8 + e];
-              y[2][e] = (_Float16)acc1[e];
-              y[3][e] = (_Float16)acc1[8 + e];
-            }
-#pragma unroll
-            for (int c = 0; c < 4; ++c)
-              y[c] = __builtin_elementwise_min(__builtin_elementwise_max(y[c], (h8){}), (h8)(_Float16)1.f);
-            f32x16 d = {};
-            d[0] = gmu;
-            d = mfma16(awa[0], y[0], d);
-            d = mfma16(awa[1], y[1], d);
-            d = mfma16(awb[0], y[2], d);
-            d = mfma16(awb[1], y[3], d);
-            val = d[0];
-          } else {
-          float ma0 = h ? 0.f : gmu, mb0 = h ? gmu : 0.f, ma1 = 0.f, mb1 = 0.f;
-          if (ABL & 2) {
-            ma1 = acc0[0] + acc0[15];
-            mb1 = acc1[0] + acc1[15];
-          } else if (EPI == 6) {
-            // fma-mix reduction (co-issues with the MFMA pipe, twice the VALU count)
-#pragma unroll
-            for (int r = 0; r < 16; r += 2) {
-              h2 ya = {(_Float16)acc0[r], (_Float16)acc0[r + 1]};
-              ya = __builtin_elementwise_min(__builtin_elementwise_max(ya, (h2){}), (h2)(_Float16)1.f);
-              h2 yb = {(_Float16)acc1[r], (_Float16)acc1[r + 1]};
-              yb = __builtin_elementwise_min(__builtin_elementwise_max(yb, (h2){}), (h2)(_Float16)1.f);
-              const h2 wv = wm2[r >> 1];
-              ma0 = hnm_fma_mix_lo(ya, wv, ma0);
-              ma1 = hnm_fma_mix_hi(ya, wv, ma1);
-              mb0 = hnm_fma_mix_lo(yb, wv, mb0);
-              mb1 = hnm_fma_mix_hi(yb, wv, mb1);
-            }
-          } else {
-            // packed dots: half the VALU count of fma-mix; the dot unit shares the matrix pipe
-            // (tools/issue_probe.hip), which the layer-2 MFMAs leave ~60% idle
-#pragma unroll
-            for (int r = 0; r < 16; r += 2) {
-              h2 ya = {(_Float16)acc0[r], (_Float16)acc0[r + 1]};
-              ya = __builtin_elementwise_min(__builtin_elementwise_max(ya, (h2){}), (h2)(_Float16)1.f);
-              h2 yb = {(_Float16)acc1[r], (_Float16)acc1[r + 1]};
-              yb = __builtin_elementwise_min(__builtin_elementwise_max(yb, (h2){}), (h2)(_Float16)1.f);
-              ma0 = __builtin_amdgcn_fdot2(ya, wm2[r >> 1], ma0, false);
-              mb0 = __builtin_amdgcn_fdot2(yb, wm2[r >> 1], mb0, false);
-            }
-          }
-          const float ma = EPI == 6 || (ABL & 2) ? ma0 + ma1 : ma0;
-          const float mb = EPI == 6 || (ABL & 2) ? mb0 + mb1 : mb0;
-          if (ABL & 64) {
-            val = h ? mb : ma;
-          } else {
-            const auto sw2 = __builtin_amdgcn_permlane32_swap(__float_as_uint(ma), __float_as_uint(mb),
-                                                              false, false);
-            val = __uint_as_float(sw2[0]) + __uint_as_float(sw2[1]);
-          }
-          }  // EPI
-          const bool lvalid = n < part_end && (h == 0 || hasb);
-          if (MODE == SCAN_SAMPLE) {
-            if (lvalid) A.dense[(u0 + uh) * A.ldo + n] = val;  // score - e_i
-          } else if (ABL & 1) {
-            tv += val;  // keep the value live, no test
-          } else {
-            uint64_t m = __ballot(lvalid && !(val < 0.f));      // !(score + e_i < tau)
-            if (masked) {  // uniform: filtered items of the two users
-              const int mba = hnm_readlane_i((int)mbits, ua), mbb = hnm_readlane_i((int)mbits, ub);
-              m &= __ballot(!(((h ? mbb : mba) >> j) & 1));
-            }
-            const bool pass = (m >> lane) & 1;
-            if (m) {
-              const unsigned mh = (unsigned)(m >> (32 * h));
-              const int ca = hnm_readlane_i(ccount, ua), cb = hnm_readlane_i(ccount, ub);
-              const int pos = (h ? cb : ca) + __builtin_popcount(mh & ((1u << j) - 1u));
-              if (pass && pos < A.capp) seg[uh * segstride + pos] = (int32_t)n;
-              if (lane == ua) ccount += __builtin_popcount((unsigned)m);
-              if (lane == ub && hasb) ccount += __builtin_popcount((unsigned)(m >> 32));
-            }
-          }
-          continue;
-        }
-        float ma[2] = {0.f, 0.f}, mb[2] = {0.f, 0.f};
-#pragma unroll
-        for (int r = 0; r < 16; r += 2) {
-          h2 ya = {(_Float16)acc0[r], (_Float16)acc0[r + 1]};
-          ya = __builtin_elementwise_min(__builtin_elementwise_max(ya, (h2){}), (h2)(_Float16)1.f);
-          ma[(r >> 1) & 1] = __builtin_amdgcn_fdot2(ya, wm2[r >> 1], ma[(r >> 1) & 1], false);
-          h2 yb = {(_Float16)acc1[r], (_Float16)acc1[r + 1]};
-          yb = __builtin_elementwise_min(__builtin_elementwise_max(yb, (h2){}), (h2)(_Float16)1.f);
-          mb[(r >> 1) & 1] = __builtin_amdgcn_fdot2(yb, wm2[r >> 1], mb[(r >> 1) & 1], false);
-        }
-        const auto sw2 = __builtin_amdgcn_permlane32_swap(__float_as_uint(ma[0] + ma[1]),
-                                                          __float_as_uint(mb[0] + mb[1]), false, false);
-        const float score = (__uint_as_float(sw2[0]) + __uint_as_float(sw2[1])) + gmu;
-        const float cua = hnm_readlane_f(cu, ua), cub = hnm_readlane_f(cu, ub);
-        const float cuh = h ? cub : cua;
-        const float ei = fmaf(cuh, dj, bj);
-        const bool lvalid = n < part_end && (h == 0 || hasb);
+        // lanes 0-15: (a, c), (a, c + 16), (b, c), (b, c + 16); other lanes' rows are unused
+        f32x4 d = *reinterpret_cast<const f32x4*>(&g7[((u >> 1) * 16 + (lane & 15)) << 2]);
+        d = __builtin_amdgcn_mfma_f32_16x16x32_f16(ewa[0], ya[0], d, 0, 0, 0);
+        d = __builtin_amdgcn_mfma_f32_16x16x32_f16(ewa[1], ya[1], d, 0, 0, 0);
+        d = __builtin_amdgcn_mfma_f32_16x16x32_f16(ewb[0], yb[0], d, 0, 0, 0);
+        d = __builtin_amdgcn_mfma_f32_16x16x32_f16(ewb[1], yb[1], d, 0, 0, 0);
+        const uint64_t vmask = vm32 | (hasb ? vm32 << 32 : 0ull);
         if (MODE == SCAN_SAMPLE) {
-          if (lvalid) A.dense[(u0 + uh) * A.ldo + n] = score - ei;
-        } else if (MODE == SCAN_DEBUG) {
-          const float eua = hnm_readlane_f(eu, ua), eub = hnm_readlane_f(eu, ub);
-          const float euh = h ? eub : eua;
-          if (lvalid) {
-            A.dense[(u0 + uh) * A.ldo + n] = score;
-            A.dense2[(u0 + uh) * A.ldo + n] = euh + ei;
+          if (lane < 16) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int it = lane + 16 * (r & 1);
+              if ((vmask >> (32 * (r >> 1) + it)) & 1)
+                A.dense[(u0 + ua + (r >> 1)) * A.ldo + base + it] = d[r];  // score - e_i
+            }
           }
-        } else if (ABL & 1) {
-          tv += score + ei;
         } else {
-          const float tva = hnm_readlane_f(tv, ua), tvb = hnm_readlane_f(tv, ub);
-          const float tvh = h ? tvb : tva;
-          bool pass = lvalid && !(score + ei < tvh);
-          if (masked) {
-            const int mba = hnm_readlane_i((int)mbits, ua), mbb = hnm_readlane_i((int)mbits, ub);
-            const int mb_ = h ? mbb : mba;
-            pass = pass && !((mb_ >> j) & 1);
+          const uint64_t m0 = __ballot(!(d[0] < 0.f)) & 0xffffull;
+          const uint64_t m1 = __ballot(!(d[1] < 0.f)) & 0xffffull;
+          const uint64_t m2 = __ballot(!(d[2] < 0.f)) & 0xffffull;
+          const uint64_t m3 = __ballot(!(d[3] < 0.f)) & 0xffffull;
+          uint64_t m = (m0 | (m1 << 16) | (m2 << 32) | (m3 << 48)) & vmask;  // !(score + e_i < tau)
+          if (masked) {  // uniform: filtered items of the two users
+            const unsigned mba = (unsigned)hnm_readlane_i((int)mbits, ua);
+            const unsigned mbb = (unsigned)hnm_readlane_i((int)mbits, ub);
+            m &= ~((uint64_t)mba | ((uint64_t)mbb << 32));
           }
-          const uint64_t m = __ballot(pass);
           if (m) {
+            const bool pass = (m >> lane) & 1;
             const unsigned mh = (unsigned)(m >> (32 * h));
             const int ca = hnm_readlane_i(ccount, ua), cb = hnm_readlane_i(ccount, ub);
-            const int base_c = h ? cb : ca;
-            const int pos = base_c + __builtin_popcount(mh & ((1u << j) - 1u));
+            const int pos = (h ? cb : ca) + __builtin_popcount(mh & ((1u << j) - 1u));
             if (pass && pos < A.capp) seg[uh * segstride + pos] = (int32_t)n;
             if (lane == ua) ccount += __builtin_popcount((unsigned)m);
             if (lane == ub && hasb) ccount += __builtin_popcount((unsigned)(m >> 32));
           }
         }
-      }
-    } else {
-      // EPI 0: MFMA epilogue; 1: packed-dot epilogue (one user per iteration; reading the
-      // next user's P~ one iteration ahead measured slower at occupancy 3)
-      h8 pc[4];
-      float gmn = 0.f;
-      auto pload = [&](int uu) {
+      } else {  // DEBUG: approx score and the whole bound, per pair, in scaled units
+        float ma = 0.f, mb = 0.f;
 #pragma unroll
-        for (int s = 0; s < 4; ++s)
-          pc[s] = (ABL & 8) ? q[s] : *reinterpret_cast<const h8*>(&ps[(wave * 32 + uu) * 64 + 8 * h + 16 * s]);
-        gmn = (ABL & 16) ? 0.f : gsm[wave][uu][j];
-      };
-      for (int u = 0; u < nu; ++u) {
-        const int ui = u;
-        pload(u);
-        const float gmu = gmn;
-        h8 x[4];
-#pragma unroll
-        for (int s = 0; s < 4; ++s) {
-          x[s] = pc[s] + q[s];
-          x[s] = __builtin_elementwise_min(__builtin_elementwise_max(x[s], (h8){}), (h8)(_Float16)1.f);
+        for (int r = 0; r < 16; r += 2) {
+          h2 ya = {(_Float16)acc0[r], (_Float16)acc0[r + 1]};
+          ya = __builtin_elementwise_min(__builtin_elementwise_max(ya, (h2){}), (h2)(_Float16)1.f);
+          h2 yb = {(_Float16)acc1[r], (_Float16)acc1[r + 1]};
+          yb = __builtin_elementwise_min(__builtin_elementwise_max(yb, (h2){}), (h2)(_Float16)1.f);
+          ma = __builtin_amdgcn_fdot2(ya, wm2[r >> 1], ma, false);
+          mb = __builtin_amdgcn_fdot2(yb, wm2[r >> 1], mb, false);
         }
-        f32x16 acc = b2c;
-#pragma unroll
-        for (int s = 0; s < 4; ++s) {
-          if (ABL & 4) acc[s] += (float)x[s][0] + (float)x[s][7];
-          else acc = mfma16(aw[s], x[s], acc);
-        }
-        float score;
-        if (ABL & 2) {
-          score = acc[0] + acc[15] + gmu;
-        } else if (EPI == 0) {
-          // relu(H~) as the [0, 1] clamp of the convert (|H~| < 1 by the choice of sw); the
-          // accumulator tile is the B operand of wm . relu(H~)
-          h8 y0, y1;
-#pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            y0[e] = (_Float16)acc[e];
-            y1[e] = (_Float16)acc[8 + e];
-          }
-          y0 = __builtin_elementwise_min(__builtin_elementwise_max(y0, (h8){}), (h8)(_Float16)1.f);
-          y1 = __builtin_elementwise_min(__builtin_elementwise_max(y1, (h8){}), (h8)(_Float16)1.f);
-          f32x16 d = {};
-          d = mfma16(awm[0], y0, d);
-          d = mfma16(awm[1], y1, d);
-          score = d[0] + gmu;
-        } else {
-          // wm . relu(H~) on the VALU: 8 packed f16 dots per half + one cross-half add
-          float m2[2] = {0.f, 0.f};
-#pragma unroll
-          for (int r = 0; r < 16; r += 2) {
-            h2 y = {(_Float16)acc[r], (_Float16)acc[r + 1]};
-            y = __builtin_elementwise_min(__builtin_elementwise_max(y, (h2){}), (h2)(_Float16)1.f);
-            m2[(r >> 1) & 1] = __builtin_amdgcn_fdot2(y, wm2[r >> 1], m2[(r >> 1) & 1], false);
-          }
-          score = hnm_sum_halves(m2[0] + m2[1]) + gmu;
-        }
-        const float ei = fmaf(hnm_readlane_f(cu, ui), dj, bj);
-        if (MODE == SCAN_SAMPLE) {
-          if (ivalid) A.dense[(u0 + ui) * A.ldo + n] = score - ei;
-        } else if (MODE == SCAN_DEBUG) {
-          if (ivalid) {
-            A.dense[(u0 + ui) * A.ldo + n] = score;
-            A.dense2[(u0 + ui) * A.ldo + n] = hnm_readlane_f(eu, ui) + ei;
-          }
-        } else if (ABL & 1) {
-          tv += score + ei;  // keep the score live, no test
-        } else {
-          bool pass = ivalid && !(score + ei < hnm_readlane_f(tv, ui));
-          if (masked) pass = pass && !((hnm_readlane_i((int)mbits, ui) >> j) & 1);
-          const uint64_t m = __ballot(pass);
-          if (m) {
-            const int pos = hnm_readlane_i(ccount, ui) + __popcll(m & ((1ull << lane) - 1));
-            if (pass && pos < A.capp) seg[ui * segstride + pos] = (int32_t)n;
-            if (lane == ui) ccount += __popcll(m);
-          }
+        // after the swap lanes 0-31 hold user a's total, lanes 32-63 user b's
+        const auto sw2 = __builtin_amdgcn_permlane32_swap(__float_as_uint(ma), __float_as_uint(mb),
+                                                          false, false);
+        const float score = (__uint_as_float(sw2[0]) + __uint_as_float(sw2[1])) + gsm[wave][uh][j];
+        const float cuh = h ? hnm_readlane_f(cu, ub) : hnm_readlane_f(cu, ua);
+        const float euh = h ? hnm_readlane_f(eu, ub) : hnm_readlane_f(eu, ua);
+        if (n < part_end && (h == 0 || hasb)) {
+          A.dense[(u0 + uh) * A.ldo + n] = score;
+          A.dense2[(u0 + uh) * A.ldo + n] = euh + fmaf(cuh, dj, bj);
         }
       }
-    }  // EPI
+    }
     }  // nu > 0
     if (tn < ntiles) stash(cur ^ 1);
     __syncthreads();
     t = tn;
   }
-  if (MODE == SCAN_THRESH && lane < nu) A.cnt[(u0 + lane) * A.NP + p] = ccount + ((ABL & 1) ? (int)tv : 0);
+  if (MODE == SCAN_THRESH && lane < nu) A.cnt[(u0 + lane) * A.NP + p] = ccount;
 }
 
 // Per row: Eu = user-constant part of the bound (scaled): 6u unit (c0 + A_u) + unit abs.
@@ -1163,22 +1027,7 @@ hnm_status cert_prepare(hnm_ctx* ctx, const hnm_ncf_weights* w, const NcfTabs& t
 
 template <int MODE>
 void launch_scan(hnm_ctx* ctx, dim3 grid, const ScanArgs& a) {
-  // tuning knob HNM_OPT_SCAN_USERS: 1 = packed-dot epilogue, 2 = two users per iteration
-  // with the folded test (default), 3 = MFMA epilogue, 4 = as 2 with the next pair's LDS
-  // operands prefetched, at 2 workgroups per CU, 5 = as 2 with the wm reduction on the
-  // matrix pipe, 6 = as 2 with fma-mix reduction
-  if (ctx->scan_users == 6)
-    hipLaunchKernelGGL((ncf16_scan_kernel<MODE, 6>), grid, dim3(256), 0, ctx->stream, a);
-  else if (ctx->scan_users == 5)
-    hipLaunchKernelGGL((ncf16_scan_kernel<MODE, 5>), grid, dim3(256), 0, ctx->stream, a);
-  else if (ctx->scan_users == 4)
-    hipLaunchKernelGGL((ncf16_scan_kernel<MODE, 4>), grid, dim3(256), 0, ctx->stream, a);
-  else if (ctx->scan_users == 2)
-    hipLaunchKernelGGL((ncf16_scan_kernel<MODE, 2>), grid, dim3(256), 0, ctx->stream, a);
-  else if (ctx->scan_users == 3)
-    hipLaunchKernelGGL((ncf16_scan_kernel<MODE, 0>), grid, dim3(256), 0, ctx->stream, a);
-  else
-    hipLaunchKernelGGL((ncf16_scan_kernel<MODE, 1>), grid, dim3(256), 0, ctx->stream, a);
+  hipLaunchKernelGGL((ncf16_scan_kernel<MODE>), grid, dim3(256), 0, ctx->stream, a);
 }
 
 ScanArgs scan_args(const CertWs& x, int64_t B) {
@@ -1207,7 +1056,10 @@ bool ncf_cert_eligible(const hnm_ncf_weights* w, int K) {
          w->num_items >= CERT_MIN_ITEMS && w->num_items >= 64 * (int64_t)K;
 }
 
-int ncf_cert_wg(const hnm_ctx* ctx) { return ctx->scan_users == 4 ? 2 : CERT_WG_PER_CU; }
+int ncf_cert_wg(const hnm_ctx* ctx) {
+  (void)ctx;
+  return CERT_WG_PER_CU;
+}
 
 size_t ncf_cert_bytes(int64_t B, int64_t I, int K, int num_cus, int wg) {
   return cert_carve(nullptr, B, I, K, num_cus, wg, nullptr);

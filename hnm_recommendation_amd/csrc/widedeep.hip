@@ -1547,13 +1547,6 @@ static hnm_status wdc_scan(hnm_ctx* ctx, const hnm_widedeep_weights* w, const Wd
     if (mode == WDC_THRESH) wdc_launch_scan<R, O, WDC_THRESH>(ctx, grid, lds, a); \
     else wdc_launch_scan<R, O, WDC_DEBUG>(ctx, grid, lds, a);                 \
   }
-  // tuning ablations (HNM_OPT_SCAN_USERS 101..103, timing only: results are garbage)
-  if (pr.RB2 == 8 && pr.OB == 4 && ctx->scan_users > 100 && mode == WDC_THRESH) {
-    if (ctx->scan_users == 101) wdc_launch_scan<8, 4, WDC_THRESH, 1>(ctx, grid, lds, a);
-    if (ctx->scan_users == 102) wdc_launch_scan<8, 4, WDC_THRESH, 2>(ctx, grid, lds, a);
-    if (ctx->scan_users == 103) wdc_launch_scan<8, 4, WDC_THRESH, 3>(ctx, grid, lds, a);
-    if (ctx->scan_users == 104) wdc_launch_scan<8, 4, WDC_THRESH, 4>(ctx, grid, lds, a);
-  } else
   WDC_CASE(8, 4)
   WDC_CASE(4, 2)
   WDC_CASE(2, 1)

@@ -66,11 +66,6 @@ hnm_status hnm_ctx_abort_pending(hnm_ctx* ctx);
  * with the certified f16 pre-filter and re-score the surviving candidates in exact fp32
  * (results identical to the fp32 scan); 0 = exact fp32 scan of every item. */
 enum { HNM_OPT_PREFILTER = 1,
-       HNM_OPT_SCAN_USERS = 2, /* tuning: NCF scan variant -- 1 one user per iteration, packed
-                                  dots; 2 (default) two users per iteration, threshold test
-                                  folded into the GMF table; 3 one user, MFMA epilogue; 4 as 2
-                                  with the next pair prefetched (2 workgroups/CU); 5 as 2 with
-                                  the wm reduction on the matrix pipe; 6 as 2 with fma-mix */
        HNM_OPT_STATS = 3       /* 1: count pre-filter candidates / fallback rows (diagnostics) */ };
 hnm_status hnm_ctx_set_option(hnm_ctx* ctx, int option, int64_t value);
 /* Pre-filter counters since the last reset (syncs; counted only while HNM_OPT_STATS is 1):

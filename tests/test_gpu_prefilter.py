@@ -70,18 +70,8 @@ def test_bound_holds_full_catalogue(kw):
     assert ratio <= 1.0, ratio
 
 
-@pytest.fixture(params=[1, 2, 3, 4, 5, 6],
-                ids=["epi-dot", "epi-pair", "epi-mfma", "epi-pair-pf", "epi-pair-mfma", "epi-pair-mix"])
-def scan_users(request):
-    """The scan kernel's epilogue variants (HNM_OPT_SCAN_USERS): all must be identical."""
-    dev = torch.device(DEV, 0)
-    _lib.set_option(dev, _lib.HNM_OPT_SCAN_USERS, request.param)
-    yield request.param
-    _lib.set_option(dev, _lib.HNM_OPT_SCAN_USERS, 2)
-
-
 @pytest.mark.parametrize("kw", [{}, {"bias_scale": 0.1, "emb_scale": 30.0}])
-def test_prefilter_identical_to_exact_scan(kw, scan_users):
+def test_prefilter_identical_to_exact_scan(kw):
     m = full_model(seed=3, **kw)
     users_np = syn.user_batch(syn.HM_USERS, 1024 - 23, seed=9)  # odd users in the last wave
     users = torch.from_numpy(users_np).to(DEV)
@@ -97,7 +87,7 @@ def test_prefilter_identical_to_exact_scan(kw, scan_users):
     assert_topk_equivalent(pi[:3], ref, 12, what="prefilter vs oracle")
 
 
-def test_prefilter_with_filters_and_k(scan_users):
+def test_prefilter_with_filters_and_k():
     m = full_model(seed=4)
     users_np = syn.user_batch(syn.HM_USERS, 201, seed=2)
     users = torch.from_numpy(users_np).to(DEV)

@@ -1,5 +1,7 @@
-// Ablation timing of ncf16_scan_kernel (THRESH mode, no appends) at the bench shape
-// (B = 4096 users x 105,542 items, 24 partitions).  Diagnostic build only:
+// Timing harness of ncf16_scan_kernel (THRESH mode, no appends) at the bench shape
+// (B = 4096 users x 105,542 items, 24 partitions): kernel-only time, best of 7 after a
+// clock warm-up, so scan variants can be compared without the rest of the step.
+// Diagnostic build only:
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -c tools/scan_ablation.hip -o build/scan_ablation.o
 //   hipcc --offload-arch=gfx950 build/scan_ablation.o build/obj/{api,score,ncf,graph,widedeep}.o \
 //         -o build/scan_ablation
@@ -21,15 +23,14 @@ static T* dev_fill(size_t n, float lo, float hi, unsigned seed) {
   return d;
 }
 
-template <int ABL, int EPI = 0>
-static float time_variant(dim3 grid, const ScanArgs& a) {
+static float time_scan(dim3 grid, const ScanArgs& a) {
   hipEvent_t e0, e1;
   (void)hipEventCreate(&e0);
   (void)hipEventCreate(&e1);
   float best = 1e30f;
-  for (int rep = 0; rep < 4; ++rep) {
+  for (int rep = 0; rep < 8; ++rep) {
     (void)hipEventRecord(e0);
-    hipLaunchKernelGGL((ncf16_scan_kernel<SCAN_THRESH, EPI, ABL>), grid, dim3(256), 0, 0, a);
+    hipLaunchKernelGGL((ncf16_scan_kernel<SCAN_THRESH>), grid, dim3(256), 0, 0, a);
     (void)hipEventRecord(e1);
     (void)hipEventSynchronize(e1);
     if (hipGetLastError() != hipSuccess) printf("launch error\n");
@@ -73,12 +74,13 @@ int main() {
   dim3 grid((unsigned)sh.part.np, (unsigned)hnm_cdiv(B, 128));
   const double pairs = (double)B * I, useful = 4352.0 * pairs;
   printf("grid %u x %u, ipp %ld\n", grid.x, grid.y, (long)sh.part.ipp);
-#define V(ABL, EPI)                                                                          \
-  {                                                                                          \
-    const float ms = time_variant<ABL, EPI>(grid, a);                                        \
-    printf("EPI=%d ABL=%2d  %7.3f ms  %6.1f TF useful  %5.2f cyc/user-tile/SIMD @2.2GHz\n", EPI, \
-           ABL, ms, useful / (ms * 1e-3) / 1e12, ms * 1e-3 * 2.2e9 / (pairs / 32 / 1024));   \
+  for (int w = 0; w < 100; ++w)  // clock warm-up (~0.2 s of scan work)
+    hipLaunchKernelGGL((ncf16_scan_kernel<SCAN_THRESH>), grid, dim3(256), 0, 0, a);
+  (void)hipDeviceSynchronize();
+  for (int rep = 0; rep < 3; ++rep) {
+    const float ms = time_scan(grid, a);
+    printf("ncf16_scan  %7.3f ms  %6.1f TF useful  %5.2f cyc/user-tile/SIMD @2.2GHz\n", ms,
+           useful / (ms * 1e-3) / 1e12, ms * 1e-3 * 2.2e9 / (pairs / 32 / 1024));
   }
-  V(0, 2) V(0, 5) V(0, 6) V(0, 2) V(0, 5) V(0, 6) V(0, 2) V(0, 5) V(0, 6) V(0, 1)
   return 0;
 }
