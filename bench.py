@@ -30,6 +30,7 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import subprocess
 import sys
 import time
 
@@ -314,6 +315,56 @@ def pmc_traffic(workload):
         return None
 
 
+# the other BASELINE configs, run by the default (NCF, N = 1) invocation as child processes so
+# that the driver's record carries every workload line (configs[2] lightgcn, configs[3]
+# widedeep, configs[4]'s per-GPU work lightgcn128; mf is the MatrixFactorization extension)
+EXTRA_WORKLOADS = (("lightgcn", "configs[2]: LightGCN 3-layer dim=64, full H&M adjacency"),
+                   ("widedeep", "configs[3]: Wide&Deep dim=64, 512-256-128 tower"),
+                   ("lightgcn128", "configs[4] per-GPU work at N=1: LightGCN dim=128"),
+                   ("mf", "MatrixFactorization dim=64 (SURVEY §8(f))"))
+
+
+def run_child(argv, timeout):
+    """One bench.py child process; returns its JSON line (None on failure, logged)."""
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT")}
+    cmd = [sys.executable, os.path.abspath(__file__), *argv]
+    try:
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, env=env)
+    except subprocess.TimeoutExpired:
+        log(f"child {' '.join(argv)} timed out")
+        return None
+    lines = [ln for ln in r.stdout.strip().splitlines() if ln.startswith("{")]
+    if r.returncode != 0 or not lines:
+        log(f"child {' '.join(argv)} failed rc={r.returncode}: {r.stderr[-800:]}")
+        return None
+    return json.loads(lines[-1])
+
+
+def run_extras(args):
+    """Every other workload's bench line and the B = 1 serve latencies, measured by child
+    processes after the headline line's timed region (one process per workload: each
+    holds only its own tables)."""
+    out, lat = {}, {}
+    for w, what in EXTRA_WORKLOADS:
+        steps, warmup = (5, 1) if w == "widedeep" else (args.steps, args.warmup)
+        argv = ["--workload", w, "--steps", str(steps), "--warmup", str(warmup), "--no-extras"]
+        if args.no_cpu_baseline:
+            argv.append("--no-cpu-baseline")
+        t0 = time.perf_counter()
+        line = run_child(argv, 900)
+        log(f"extra workload {w}: {time.perf_counter() - t0:.1f}s")
+        if line is not None:
+            line["config"]["baseline_config"] = what
+            out[w] = line
+    for w in ("ncf", "lightgcn"):
+        line = run_child(["--latency", "--workload", w, "--steps", "200", "--no-extras"], 600)
+        log(f"serve latency {w} done")
+        if line is not None:
+            lat[w] = line
+    return out, lat
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -329,6 +380,9 @@ def main():
                          "best items are user-specific (emb_scale 20, biases)")
     ap.add_argument("--exact", action="store_true",
                     help="exact fp32 scan of every item instead of the certified f16 pre-filter")
+    ap.add_argument("--no-extras", action="store_true",
+                    help="default NCF run only: skip the other workloads' lines and the B=1 "
+                         "serve latencies (otherwise measured after the headline, N=1 only)")
     args = ap.parse_args()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(launch_ranks(args.gpus))
@@ -484,6 +538,11 @@ def main():
             line["cpu_baseline"] = cpu_baseline(cpu)
         except Exception as e:  # baseline is reported, never fatal
             log(f"cpu baseline failed: {e!r}")
+    if (rank == 0 and world == 1 and args.workload == "ncf" and not args.no_extras
+            and not args.exact and args.weights == "init"):
+        others, lat = run_extras(args)
+        line["other_configs"] = others
+        line["serve_latency_b1"] = lat
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:

@@ -12,7 +12,9 @@ import threading
 import torch
 
 PKG = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(PKG, "libhnm_mi355x.so")
+# HNM_LIB_PATH: load another build of the same library (A/B timing of kernel variants built
+# from tools/; the in-tree build is the product and the default)
+LIB_PATH = os.environ.get("HNM_LIB_PATH") or os.path.join(PKG, "libhnm_mi355x.so")
 
 HNM_OK, HNM_EINVAL, HNM_EOOB, HNM_EHIP, HNM_ENOMEM, HNM_EUNSUPPORTED = 0, -1, -2, -3, -4, -5
 

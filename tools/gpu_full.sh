@@ -1,6 +1,7 @@
 #!/bin/bash
-# Full GPU session: parity tests, every bench workload (+ personalised weights, B=1 latency,
-# 2-rank launcher rehearsal) and optional rocprofv3 kernel stats.
+# Full GPU session: parity tests, the default bench line (NCF headline + every other workload
+# + B=1 serve latencies, as the driver runs it), personalised NCF weights, the 2-rank
+# launcher rehearsal, and optional rocprofv3 kernel stats per workload.
 #   bash tools/gpu_full.sh <tag> [prof]     (outputs under gpurun_out/<tag>/)
 set -uo pipefail
 TAG=${1:-r}
@@ -16,17 +17,11 @@ step() {  # name timeout cmd...
   local rc=$?
   echo "$name rc=$rc" >> "$OUT/status.txt"
   if [ $rc -ne 0 ]; then echo "step $name failed rc=$rc"; tail -30 "$OUT/$name.out"; tail -20 "$OUT/$name.err"; exit $rc; fi
-  tail -1 "$OUT/$name.out"
+  tail -c 600 "$OUT/$name.out"; echo
 }
 step tests 1000 python -u -m pytest tests -x -v -m gpu --timeout 180 --timeout-method thread
-step bench_ncf 300 python bench.py
+step bench_default 900 python bench.py
 step bench_ncf_personal 300 python bench.py --weights personal --no-cpu-baseline
-step bench_lightgcn 400 python bench.py --workload lightgcn --no-cpu-baseline
-step bench_lightgcn128 400 python bench.py --workload lightgcn128 --no-cpu-baseline
-step bench_mf 300 python bench.py --workload mf --no-cpu-baseline
-step bench_widedeep 600 python bench.py --workload widedeep --steps 10 --warmup 2 --no-cpu-baseline
-step lat_ncf 300 python bench.py --latency --steps 200
-step lat_lightgcn 300 python bench.py --latency --workload lightgcn --steps 200
 HNM_DIST_BACKEND=gloo step bench_2rank 400 python bench.py --gpus 2 --workload lightgcn128 --steps 5 --warmup 2
 if [ -n "$PROF" ]; then
   cd /tmp && export TMPDIR=/tmp
@@ -35,7 +30,7 @@ if [ -n "$PROF" ]; then
     [ $w = widedeep ] && extra="--steps 3 --warmup 1"
     echo "== prof $w $(date +%T)"
     timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_$w" -o $w -- \
-      python3 "$ROOT/bench.py" --workload $w $extra --no-cpu-baseline > "$OUT/prof_$w.log" 2>&1 \
+      python3 "$ROOT/bench.py" --workload $w $extra --no-cpu-baseline --no-extras > "$OUT/prof_$w.log" 2>&1 \
       || { echo "rocprof $w failed"; exit 1; }
   done
 fi
