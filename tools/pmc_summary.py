@@ -1,9 +1,11 @@
 """Summarize rocprofv3 PMC passes (tools/pmc_profile.sh) into profiles/pmc_<workload>.json.
 
-    python tools/pmc_summary.py <pmc run dir> <workload> <kernel substring[,substring...]> [out.json]
+    python tools/pmc_summary.py <pmc run dir> <workload> <kernel substring[;substring...]> [out.json]
 
-Several comma-separated substrings: the per-launch figures are the SUM over those kernels
-(e.g. one LightGCN propagation layer = spmm_light + spmm_segment + spmm_finish).
+Several ";"-separated substrings (kernel names contain commas): the per-launch figures are the SUM over those kernels
+(e.g. one LightGCN propagation layer = spmm_light + spmm_segment + spmm_finish).  A
+substring ending in "@max" keeps only that kernel's dispatches with its largest grid (the
+whole-graph SpMM layers, not the restricted last layer's row-range launches).
 
 HBM traffic per launch of the dominant kernel, corrected as MI355X_MICROARCH.md's
 HBM/rocprofv3 section prescribes: FETCH_SIZE (kB) counts L2 -> fabric read requests and on
@@ -22,16 +24,26 @@ import sys
 def main():
     run, workload, ksub = sys.argv[1], sys.argv[2], sys.argv[3]
     out = sys.argv[4] if len(sys.argv) > 4 else os.path.join("profiles", f"pmc_{workload}.json")
-    subs = ksub.split(",")
+    subs = ksub.split(";")
     per = {sub: collections.defaultdict(list) for sub in subs}
     names = set()
+    rows = []
     for f in sorted(glob.glob(os.path.join(run, "p*", "*counter_collection.csv"))):
-        for r in csv.DictReader(open(f)):
-            for sub in subs:
-                if sub in r["Kernel_Name"]:
-                    names.add(r["Kernel_Name"])
-                    per[sub][r["Counter_Name"]].append(float(r["Counter_Value"]))
+        rows += list(csv.DictReader(open(f)))
+    maxgrid = {}
+    for r in rows:
+        for sub in subs:
+            if sub.endswith("@max") and sub[:-4] in r["Kernel_Name"]:
+                maxgrid[sub] = max(maxgrid.get(sub, 0), int(r["Grid_Size"]))
+    for r in rows:
+        for sub in subs:
+            key = sub[:-4] if sub.endswith("@max") else sub
+            if key in r["Kernel_Name"]:
+                if sub in maxgrid and int(r["Grid_Size"]) != maxgrid[sub]:
                     break
+                names.add(r["Kernel_Name"])
+                per[sub][r["Counter_Name"]].append(float(r["Counter_Value"]))
+                break
     if not any(per.values()):
         raise SystemExit(f"no dispatches of a kernel matching {ksub!r} under {run}")
     avg = collections.defaultdict(float)  # per-launch sum over the listed kernels
