@@ -342,6 +342,7 @@ __global__ __launch_bounds__(256, dcert_wg_per_cu(DP)) void dot16_scan_kernel(DS
   constexpr int LD = TI * CH / 256;  // chunks per thread per tile (4)
   __shared__ __attribute__((aligned(16))) _Float16 vs[2][TI * RS];
   __shared__ float ibl[2][BIAS ? TI : 1];  // the tile's scaled item biases
+  __shared__ int lcnt[4][MODE == DSCAN_THRESH ? 32 : 1];  // THRESH: appends per (wave, user row)
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5, j = lane & 31;
   const int p = blockIdx.x;
@@ -361,13 +362,20 @@ __global__ __launch_bounds__(256, dcert_wg_per_cu(DP)) void dot16_scan_kernel(DS
   // so the accumulator ends as approx - tau (-inf for rows past the batch: never passes).  The
   // extra fp32 rounding of the chain by |tau| (a few 2^-24 of the score scale) is inside the
   // 2^-18 guard dcert_tau_kernel leaves.
+  // (loads unconditional at a clamped row, then a select: a load inside the branch would be
+  // waited for right there, 16 serial round trips)
   f32x16 ntv;
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
     const int64_t b = b0 + mfma32_row(r, h);
-    ntv[r] = (MODE == DSCAN_THRESH && b < A.B) ? -A.tau[b] : -__builtin_inff();
+    if (MODE == DSCAN_THRESH) {
+      const float tb = A.tau[std::min<int64_t>(b, A.B - 1)];
+      ntv[r] = b < A.B ? -tb : -__builtin_inff();
+    } else {
+      ntv[r] = -__builtin_inff();
+    }
   }
-  int ccount = 0;  // THRESH: appends of user row (lane) in this partition
+  if (MODE == DSCAN_THRESH && lane < 32) lcnt[wave][lane] = 0;
   float rmax[MODE == DSCAN_SAMPLE ? 16 : 1];  // SAMPLE: running max per C row
 #pragma unroll
   for (int r = 0; r < (MODE == DSCAN_SAMPLE ? 16 : 1); ++r) rmax[r] = -__builtin_inff();
@@ -420,7 +428,11 @@ __global__ __launch_bounds__(256, dcert_wg_per_cu(DP)) void dot16_scan_kernel(DS
   for (int64_t t = 0; t < ntiles; ++t) {
     const int64_t tbase = part_start + t * TI;
     const int cur = (int)(t & 1);
-    if (t + 1 < ntiles) fetch(tbase + TI);
+    // fetch / stash run on every iteration (the last one re-reads its own tile into the idle
+    // buffer): made conditional, the waitcnt pass assumes the tile loads may still be pending
+    // at the loop head and waits vmcnt(0) there -- which waits for the append stores flushed
+    // just before the barrier (a store round trip per tile)
+    fetch(t + 1 < ntiles ? tbase + TI : tbase);
     if (nu > 0) {
       // filtered (user, item) pairs of the sub-tile at base -> -inf (rare path)
       auto apply_mask = [&](f32x16& sc, int64_t base, int64_t n) {
@@ -446,41 +458,38 @@ __global__ __launch_bounds__(256, dcert_wg_per_cu(DP)) void dot16_scan_kernel(DS
         }
       };
       // THRESH: acc[r] = approx - tau of row r's user (the MFMA chain starts from -tau), so a
-      // lane's test is one max3 tree over its 16 rows, + the item bias, and one ballot; only
-      // lanes with a pass compute their row bits and are walked (about one pass per 32 x 32
-      // sub-tile at ~100 candidates per row) -- no per-row ballots on the scalar unit
+      // lane's test is one max3 tree over its 16 rows, + the item bias, and one ballot (about
+      // one pass per 32 x 32 sub-tile at ~100 candidates per row).  On a pass, every passing
+      // lane appends its own (row, item) passes: slot = the wave's LDS counter of that user
+      // row (ds_add_rtn), the store queued.  Measured against a scalar-unit walk of the
+      // passing lanes by the rows' owner lanes: 0.094 vs 0.107 ms (the walk alone 0.027 ms of
+      // it), and a per-quarter test (4 maxima, 4 ballots): 4-6 % slower
+      // (tools/dot_scan_timing.hip, profiles/r2_dot_scan_timing.txt).
       auto thresh = [&](const f32x16& acc, float ib, int64_t base, bool ivalid) {
         float lm = acc[0];
 #pragma unroll
         for (int r = 1; r < 16; ++r) lm = fmaxf(lm, acc[r]);
-        uint64_t lanes = __ballot(ivalid && !(lm + ib < 0.f));
-        if (!lanes) return;
-        unsigned bits = 0;
+        if (!__ballot(ivalid && !(lm + ib < 0.f))) return;
+        unsigned rb = 0;
 #pragma unroll
-        for (int r = 0; r < 16; ++r) bits |= !(acc[r] + ib < 0.f) ? 1u << r : 0u;
-        while (lanes) {  // uniform
-          const int l = __builtin_ctzll(lanes);
-          lanes &= lanes - 1;
-          unsigned rr = (unsigned)hnm_readlane_i((int)bits, l);
-          const int nl = (int)(base + (l & 31));
-          while (rr) {
-            const int r = __builtin_ctz(rr);
-            rr &= rr - 1;
-            const int row = (r & 3) + 8 * (r >> 2) + 4 * (l >> 5);  // mfma32_row(r, l >> 5)
-            if (lane == row) {  // the row's owner lane queues the append
-              if (ccount < A.capp) {
-                const int off = row * segstride + ccount;
-                if (qo0 < 0) {
-                  qo0 = off;
-                  qi0 = nl;
-                } else if (qo1 < 0) {
-                  qo1 = off;
-                  qi1 = nl;
-                } else {
-                  seg[off] = nl;  // queue full (rare)
-                }
-              }
-              ++ccount;
+        for (int r = 0; r < 16; ++r) rb |= !(acc[r] + ib < 0.f) ? 1u << r : 0u;
+        if (!ivalid) rb = 0;
+        const int nl = (int)(base + j);
+        while (rb) {  // divergent: usually one pass in one lane
+          const int r = __builtin_ctz(rb);
+          rb &= rb - 1;
+          const int row = (r & 3) + 8 * (r >> 2) + 4 * h;  // mfma32_row(r, h)
+          const int slot = atomicAdd(&lcnt[wave][row], 1);
+          if (slot < A.capp) {
+            const int off = row * segstride + slot;
+            if (qo0 < 0) {
+              qo0 = off;
+              qi0 = nl;
+            } else if (qo1 < 0) {
+              qo1 = off;
+              qi1 = nl;
+            } else {
+              seg[off] = nl;  // queue full (rare)
             }
           }
         }
@@ -527,7 +536,7 @@ __global__ __launch_bounds__(256, dcert_wg_per_cu(DP)) void dot16_scan_kernel(DS
         }
       }
     }
-    if (t + 1 < ntiles) stash(cur ^ 1);
+    stash(cur ^ 1);
     if (MODE == DSCAN_THRESH) {  // flush the queued appends (the prefetch has landed)
       if (qo0 >= 0) seg[qo0] = qi0;
       if (qo1 >= 0) seg[qo1] = qi1;
@@ -535,7 +544,7 @@ __global__ __launch_bounds__(256, dcert_wg_per_cu(DP)) void dot16_scan_kernel(DS
     }
     __syncthreads();
   }
-  if (MODE == DSCAN_THRESH && lane < nu) A.cnt[(b0 + lane) * A.NP + p] = ccount;
+  if (MODE == DSCAN_THRESH && lane < nu) A.cnt[(b0 + lane) * A.NP + p] = lcnt[wave][lane];
   if (MODE == DSCAN_SAMPLE) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) {

@@ -15,6 +15,7 @@
 #endif
 
 #include <stdio.h>
+#include <stdlib.h>
 #include <vector>
 
 static _Float16* dev_h16(size_t n, float a, unsigned seed) {
@@ -30,7 +31,9 @@ static _Float16* dev_h16(size_t n, float a, unsigned seed) {
   return d;
 }
 
-int main() {
+int main(int argc, char** argv) {
+  // argv[1]: threshold in sigmas (default 3.1; 100 = no appends: the cost of the append path)
+  const float fac = argc > 1 ? (float)atof(argv[1]) : 3.1f;
   const int64_t B = 4096, I = 105542;
   const int K = 12;
   int cus = 256;
@@ -38,7 +41,7 @@ int main() {
   if (hipGetDeviceProperties(&pr, 0) == hipSuccess) cus = pr.multiProcessorCount;
   const DotCertShape sh = dcert_shape(B, I, 64, K, cus);
   const float a = 0.125f, sigma = 8.f * a * a / 3.f;
-  std::vector<float> ht(B, 3.1f * sigma);
+  std::vector<float> ht(B, fac * sigma);
   DScanArgs s{};
   s.U16 = dev_h16(B * 64, a, 1);
   s.I16 = dev_h16(I * 64, a, 2);
@@ -77,6 +80,6 @@ int main() {
   double tot = 0;
   for (int v : hc) tot += v;
   const double flops = 2.0 * 64 * B * I;
-  printf("dot16_scan  %7.4f ms  %6.1f TF  appends/row %.1f\n", best, flops / (best * 1e-3) / 1e12, tot / B);
+  printf("tau %5.2f sigma  dot16_scan  %7.4f ms  %6.1f TF  appends/row %.1f\n", fac, best, flops / (best * 1e-3) / 1e12, tot / B);
   return 0;
 }
