@@ -58,6 +58,8 @@ class ItemShardedRecommender:
         B = user_ids.numel()
         if G == 1:
             v, i = self.local_topk(user_ids)
+            if self.item_offset == 0:  # ids are already global (no elementwise pass)
+                return v, i
             return v, torch.where(i >= 0, i + self.item_offset, i)
         dev = user_ids.device
         # gloo (CPU tests, single-GPU rehearsal) moves host tensors; RCCL moves device tensors

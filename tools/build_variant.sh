@@ -8,6 +8,9 @@ ROOT=$(cd "$(dirname "$0")/.." && pwd)
 python -c "import sys; sys.path.insert(0, '$ROOT'); from hnm_recommendation_amd.build import build_library; build_library(verbose=False)"
 mkdir -p "$ROOT/tools/bin/obj_$TAG"
 base=$(basename "$SRC" .hip)
+# the variant source must carry the name of the object it replaces (e.g. an old version in
+# another directory: git show HEAD:.../ncf_cert.hip > /tmp/old/ncf_cert.hip)
+[ -f "$ROOT/build/obj/$base.o" ] || { echo "no build/obj/$base.o to replace"; exit 1; }
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -I"$ROOT/hnm_recommendation_amd/csrc" -I"$ROOT/include" "$@" -c "$SRC" -o "$ROOT/tools/bin/obj_$TAG/$base.o"
 objs=()
 for o in "$ROOT"/build/obj/*.o; do
