@@ -304,6 +304,14 @@ def serve_latency(args, device):
     print(json.dumps(out), flush=True)
 
 
+# algorithmic FLOP per (user, item) pair and the f16 MFMA FLOP the certified
+# scans issue per pair: NCF 4,096 layer 2 + 1,024 16x16x32 epilogue (64 useful) + 128 GMF;
+# W&D the 3-pass split of layer 2 (3 x 262,144) and layer 3 (3 x 65,536); dot d = 64: 128
+ALG_FLOP_PER_PAIR = {"ncf": 4352.0, "widedeep": 328450.0, "mf": 128.0}
+ISSUED_F16_FLOP_PER_PAIR = {"ncf": 5248.0, "widedeep": 983040.0, "mf": 128.0}
+RANDOM_DATA_F16_TFLOPS = 1235.0  # bare f16 MFMA loop, random operands: 1,190-1,291 TF/s
+
+
 def pmc_traffic(workload):
     """HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC summary."""
     p = os.path.join(REPO, "profiles", f"pmc_{workload}.json")
@@ -496,6 +504,17 @@ def main():
                      "traffic": pmc_traffic(args.workload)},
         "cpu_baseline": None,
     }
+    issued = ISSUED_F16_FLOP_PER_PAIR.get(args.workload)
+    if f16 and issued and not args.exact:
+        # f16 MFMA FLOP the scan actually issues per pair (epilogue / split passes included)
+        # against the rate a bare f16 MFMA loop sustains on random data at this occupancy:
+        # the chip's power limit, not the nominal peak, caps an MFMA-dense scan
+        rate = issued * per_launch / ALG_FLOP_PER_PAIR[args.workload] / (avg_kernel_ms * 1e-3) / 1e12
+        line["roofline"]["issued"] = {
+            "flop_per_pair": issued, "tflops": round(rate, 1),
+            "random_data_mfma_rate": RANDOM_DATA_F16_TFLOPS,
+            "frac_of_random_data_rate": round(rate / RANDOM_DATA_F16_TFLOPS, 3),
+            "source": "tools/mfma_shape_probe.hip, profiles/r2_mfma_shape_probe.txt"}
     if "_serving" in info and rank == 0 and world == 1:
         # serving rate with the propagation computed once (weights unchanged between calls);
         # reported beside `value`, never as it
