@@ -252,24 +252,26 @@ extern "C" hnm_status hnm_gather_rows_f32(hnm_ctx* ctx, const float* table, int6
 }
 
 // ------------------------------------------------------------------ projection
-// Y[r, c(n)] = sum_k X[x(r), k] W[n, k] (+ b[n]).  64 rows x 64 outputs per block, K in
-// chunks of 32 staged through LDS; each thread owns a 4 x 4 output patch.  fp32 FMA
-// chain in k order (a per-item / per-user precompute: <1 % of any scoring kernel).
-#define LIN_TM 64
+// Y[r, c(n)] = sum_k X[x(r), k] W[n, k] (+ b[n]).  TM rows x 64 outputs per block (TM = 64,
+// or 16 for short inputs -- a batch of users -- so the grid still covers the CUs), K in
+// chunks of 32 staged through LDS; each thread owns a TM/16 x 4 output patch.  fp32 FMA
+// chain in k order whatever TM (a per-item / per-user precompute: <1 % of any scoring kernel).
 #define LIN_TN 64
 #define LIN_TK 32
+template <int LIN_TM>
 __global__ __launch_bounds__(256) void linear_rows_kernel(
     const float* __restrict__ X, int64_t ldx, const int64_t* __restrict__ ids, int64_t x_rows,
     int64_t M, int K, const float* __restrict__ W, int64_t ldw, const float* __restrict__ bias,
     int N, float* __restrict__ Y, int64_t ldy, int pair_permute, unsigned* err) {
+  constexpr int RPT = LIN_TM / 16;  // rows per thread
   __shared__ float xs[LIN_TK][LIN_TM + 1];
   __shared__ float ws[LIN_TK][LIN_TN + 1];
   const int t = threadIdx.x;
   const int64_t m0 = (int64_t)blockIdx.x * LIN_TM;
   const int n0 = blockIdx.y * LIN_TN;
-  const int tr = (t >> 4) * 4;  // rows tr..tr+3
-  const int tc = (t & 15) * 4;  // cols tc..tc+3
-  float acc[4][4] = {};
+  const int tr = (t >> 4) * RPT;  // rows tr..tr+RPT-1
+  const int tc = (t & 15) * 4;    // cols tc..tc+3
+  float acc[RPT][4] = {};
   // each thread loads 8 X elements and 8 W elements per K chunk
   for (int k0 = 0; k0 < K; k0 += LIN_TK) {
     for (int e = t; e < LIN_TM * LIN_TK; e += 256) {
@@ -296,20 +298,20 @@ __global__ __launch_bounds__(256) void linear_rows_kernel(
     __syncthreads();
     const int kmax = min(LIN_TK, K - k0);
     for (int kk = 0; kk < kmax; ++kk) {
-      float xv[4], wv[4];
+      float xv[RPT], wv[4];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) xv[i] = xs[kk][tr + i];
+      for (int i = 0; i < RPT; ++i) xv[i] = xs[kk][tr + i];
 #pragma unroll
       for (int j = 0; j < 4; ++j) wv[j] = ws[kk][tc + j];
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < RPT; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = fmaf(xv[i], wv[j], acc[i][j]);
     }
     __syncthreads();
   }
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
+  for (int i = 0; i < RPT; ++i) {
     const int64_t m = m0 + tr + i;
     if (m >= M) continue;
 #pragma unroll
@@ -334,10 +336,17 @@ extern "C" hnm_status hnm_linear_rows_f32(hnm_ctx* ctx, const float* X, int64_t 
   HNM_REQUIRE(!pair_permute || (ldy % 2 == 0 && N <= ldy), HNM_EINVAL,
               "linear_rows: pair_permute needs an even ldy");
   if (M <= 0) return HNM_OK;
-  dim3 grid((unsigned)hnm_cdiv(M, LIN_TM), (unsigned)hnm_cdiv(N, LIN_TN));
-  hipLaunchKernelGGL(linear_rows_kernel, grid, dim3(256), 0, ctx->stream, X, ldx, ids,
-                     ids ? x_rows : M, M, K, W, ldw, bias, N, Y, ldy, pair_permute,
-                     ctx->err_dev);
+  const bool short_in = hnm_cdiv(M, 64) < 2 * (int64_t)ctx->num_cus;
+  const int tm = short_in ? 16 : 64;
+  dim3 grid((unsigned)hnm_cdiv(M, tm), (unsigned)hnm_cdiv(N, LIN_TN));
+  if (short_in)
+    hipLaunchKernelGGL(linear_rows_kernel<16>, grid, dim3(256), 0, ctx->stream, X, ldx, ids,
+                       ids ? x_rows : M, M, K, W, ldw, bias, N, Y, ldy, pair_permute,
+                       ctx->err_dev);
+  else
+    hipLaunchKernelGGL(linear_rows_kernel<64>, grid, dim3(256), 0, ctx->stream, X, ldx, ids,
+                       ids ? x_rows : M, M, K, W, ldw, bias, N, Y, ldy, pair_permute,
+                       ctx->err_dev);
   HNM_LAUNCH_CHECK();
   return HNM_OK;
 }

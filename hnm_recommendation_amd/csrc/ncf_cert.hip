@@ -110,17 +110,29 @@ __global__ __launch_bounds__(256) void cert_stats_kernel(NcfTabs t, int64_t B, i
   float m0 = 0.f, m1 = 0.f, m2 = 0.f, m3 = 0.f;  // items: Q, G, B, D / users: P, WG
   const bool items = (int)blockIdx.x < item_blocks;
   if (items) {
-    for (int64_t i = (int64_t)blockIdx.x * 4 + wave; i < I; i += (int64_t)item_blocks * 4) {
-      const float aq = fabsf(t.Qi[i * 64 + lane]);
-      const float g = lane < mf ? t.G[i * t.ldg + lane] : 0.f;
-      m0 = nmax(m0, aq);
-      m1 = nmax(m1, fabsf(g));
-      const float bq = wave_sum(vt * aq), dq = sqrtf(wave_sum(g * g));
-      m2 = nmax(m2, bq);
-      m3 = nmax(m3, dq);
-      if (lane == 0) {
-        Bi[i] = bq;
-        Di[i] = dq;
+    // four items per step, their loads issued together (one item a step waited on each)
+    const int64_t stride = (int64_t)item_blocks * 4;
+    for (int64_t i0 = (int64_t)blockIdx.x * 4 + wave; i0 < I; i0 += 4 * stride) {
+      float aq[4], g[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int64_t i = std::min<int64_t>(i0 + u * stride, I - 1);
+        aq[u] = fabsf(t.Qi[i * 64 + lane]);
+        g[u] = lane < mf ? t.G[i * t.ldg + lane] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int64_t i = i0 + u * stride;
+        if (i >= I) break;  // uniform
+        m0 = nmax(m0, aq[u]);
+        m1 = nmax(m1, fabsf(g[u]));
+        const float bq = wave_sum(vt * aq[u]), dq = sqrtf(wave_sum(g[u] * g[u]));
+        m2 = nmax(m2, bq);
+        m3 = nmax(m3, dq);
+        if (lane == 0) {
+          Bi[i] = bq;
+          Di[i] = dq;
+        }
       }
     }
   } else {
