@@ -306,9 +306,10 @@ def serve_latency(args, device):
 
 # algorithmic FLOP per (user, item) pair and the f16 MFMA FLOP the certified
 # scans issue per pair: NCF 4,096 layer 2 + 1,024 16x16x32 epilogue (64 useful) + 128 GMF;
-# W&D the 3-pass split of layer 2 (3 x 262,144) and layer 3 (3 x 65,536); dot d = 64: 128
+# W&D the 2-pass split (W_hi x_hi + W_hi x_lo) of layer 2 (2 x 262,144) and layer 3
+# (2 x 65,536); dot d = 64: 128
 ALG_FLOP_PER_PAIR = {"ncf": 4352.0, "widedeep": 328450.0, "mf": 128.0}
-ISSUED_F16_FLOP_PER_PAIR = {"ncf": 5248.0, "widedeep": 983040.0, "mf": 128.0}
+ISSUED_F16_FLOP_PER_PAIR = {"ncf": 5248.0, "widedeep": 655360.0, "mf": 128.0}
 RANDOM_DATA_F16_TFLOPS = 1235.0  # bare f16 MFMA loop, random operands: 1,190-1,291 TF/s
 
 
@@ -488,7 +489,7 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": ("f32" if args.exact or not (f16 or bound == "hbm") else
-                  "f16x3+f32" if kernel == "wdc_scan_kernel" else "f16+f32"),
+                  "f16x2+f32" if kernel == "wdc_scan_kernel" else "f16+f32"),
         "data": "synthetic (PCG64 weights with reference init distributions; H&M shape)",
         "config": {"workload": f"{args.workload}: BASELINE configs[1] NeuralCF dim=64, full H&M "
                                f"shape, batch={B} users/rank, K=12" if args.workload == "ncf"

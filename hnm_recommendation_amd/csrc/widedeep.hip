@@ -417,9 +417,10 @@ __global__ __launch_bounds__(256) void widedeep_pair_kernel(
 // The fp32 MFMA rate is 1/16 of the f16 rate.  A plain f16 scan cannot prune W&D: its
 // rigorous error bound (f16 rounding of every operand, propagated through |W3||W2|) spans
 // a third of the score spread.  Split operands can: every f16 operand is x = x_hi + x_lo
-// (x_hi = f16(x), x_lo = f16(x - x_hi)), each layer runs three f16 MFMA passes
-// W_hi x_hi + W_hi x_lo + W_lo x_hi with fp32 accumulation -- 3/16 of the fp32 MFMA time,
-// and representation error 2^-22 per operand, below the fp32 path's own accumulation error.
+// (x_hi = f16(x), x_lo = f16(x - x_hi)), each layer runs f16 MFMA passes W_hi x_hi + W_hi x_lo
+// (+ W_lo x_hi with WD_SPLIT_PASSES = 3) with fp32 accumulation: the activation's split error
+// is 2^-22, below the fp32 path's own accumulation error, and the weights' residual
+// R = W - W_hi (known, fixed per call) enters the bound exactly: (|R|^T v) . x per layer.
 // Nothing the scan computes is returned: it only prunes; every returned score is recomputed
 // by wd_tile_fp32 (the fp32 kernel's own arithmetic), so outputs are bitwise those of the
 // exact fp32 path (tests/test_gpu_prefilter.py).
@@ -433,6 +434,7 @@ __global__ __launch_bounds__(256) void widedeep_pair_kernel(
 // 1-Lipschitz and errors propagate through |W|, so
 //   |approx - exact| <= rho (g1 v1.x1 + g2 v2.x2 + g3 v3.x3 + g4 (|fin| + |c_u| + |w_I|)
 //                            + cb) + absb
+// and with two passes v1 += (|R2|^T v2) / g1, v2 += (|R3|^T v3) / g2 (the dropped W_lo x_hi).
 // with g1 = (2.125 K1 + 22)u, g2 = (2.125 n2 + 22)u (layer 3) or (32 RB2 + 12)u (final dot
 // of a two-layer tower), g3 = (32 NOB + 10)u, g4 = 10u, cb the bias-add roundings, absb the
 // f16 subnormal slack (2^-25 per rounding, scaled back), rho = 1 + 2^-6.  The v.x terms are
@@ -445,6 +447,18 @@ __global__ __launch_bounds__(256) void widedeep_pair_kernel(
 // segments; the survivors (a few hundred per user) are re-scored in fp32.  Rows with an
 // unusable bound, fewer than K finite items or an overflowing segment take the exact kernel.
 typedef _Float16 wh8 __attribute__((ext_vector_type(8)));
+
+// f16 MFMA passes per split layer: 3 = W_hi x_hi + W_hi x_lo + W_lo x_hi; 2 drops W_lo x_hi
+// and bounds it explicitly: the dropped term of layer 2 is R2 x1 with R2 = W2' - W2'_hi the
+// known residual of the f16 weights, so the bound adds (|R2|^T v2) . x1 (and (|R3|^T v3) . x2
+// for layer 3), folded into v1 / v2 by wdc_params_kernel -- a per-element residual, about
+// 2^-12.5 |W| on average instead of the 2^-11 worst case.
+#ifndef WD_SPLIT_PASSES
+#define WD_SPLIT_PASSES 2  // layer 2
+#endif
+#ifndef WD_SPLIT_PASSES3
+#define WD_SPLIT_PASSES3 WD_SPLIT_PASSES  // layer 3
+#endif
 
 __device__ __forceinline__ f32x16 wd_mfma16(wh8 a, wh8 b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
@@ -637,6 +651,38 @@ __global__ __launch_bounds__(256) void wdc_params_kernel(hnm_widedeep_weights w,
   for (float sc : {s1, sw2, s2, sw3}) bad |= !(sc >= 1e-25f && sc <= 1e25f);
   // b2' in x2 units
   for (int jx = tid; jx < n2; jx += 256) b2s[jx] = p.b2p[jx] * s2;
+  if ((WD_SPLIT_PASSES == 2 || WD_SPLIT_PASSES3 == 2) && !bad) {
+    // the dropped W_lo x_hi passes (see WD_SPLIT_PASSES): v1 += (|R2|^T v2) / g1 and, with a
+    // third layer, v2 += (|R3|^T v3) / g2, R = W' - f16(W' sw) / sw exactly as wdc_convert_kernel
+    // rounds it; 1 + 2^-10 covers |x_hi| <= (1 + 2^-11)|x| and the fp32 sums.  Each thread
+    // updates the entries it wrote above (same t / jx mapping).
+    const float uu = 5.9604645e-08f;
+    const float g1c = (2.125f * K1P + 22.f) * uu;
+    const float g2c = (2.125f * n2 + 22.f) * uu;
+    const float fr = 1.0009765625f;
+    for (int t = tid; t < K1P && WD_SPLIT_PASSES == 2; t += 256) {
+      const int k = wd_korig(t, K1P);
+      if (k >= l1) continue;
+      float r = 0.f;
+      for (int jx = 0; jx < l2; ++jx) {
+        float v = w.w2[(int64_t)jx * l1 + k] * bn_a(w.bn1_w, w.bn1_var, k, w.eps);
+        v *= sw2;
+        r = fmaf(fabsf(v - (float)(_Float16)v), sv2[jx], r);
+      }
+      v1[t] += fr * (r / sw2) / g1c;
+    }
+    if (p.OB > 0 && WD_SPLIT_PASSES3 == 2) {
+      for (int jx = tid; jx < l2; jx += 256) {
+        float r = 0.f;
+        for (int m = 0; m < l3; ++m) {
+          float v = w.w3[(int64_t)m * l2 + jx] * bn_a(w.bn2_w, w.bn2_var, jx, w.eps);
+          v *= sw3;
+          r = fmaf(fabsf(v - (float)(_Float16)v), fabsf(p.wdp[m]), r);
+        }
+        v2[jx] += fr * (r / sw3) / g2c;
+      }
+    }
+  }
   if (tid != 0) return;
   const float u = 5.9604645e-08f;  // 2^-24
   const float phi = 2.98023224e-08f;  // 2^-25: half the f16 subnormal spacing
@@ -912,7 +958,7 @@ __global__ __launch_bounds__(256, UPW == 1 ? 2 : 1) void wdc_scan_kernel(WdScanA
         for (int gi = 0; gi < G2; ++gi) {
           ah[gi] = ahn[gi];
           ahn[gi] = frag(gi, kn, 0);
-          al[gi] = frag(gi, kb, 1);
+          if (WD_SPLIT_PASSES == 3) al[gi] = frag(gi, kb, 1);
         }
 #pragma unroll
         for (int gi = 0; gi < G2; ++gi)
@@ -922,10 +968,12 @@ __global__ __launch_bounds__(256, UPW == 1 ? 2 : 1) void wdc_scan_kernel(WdScanA
         for (int gi = 0; gi < G2; ++gi)
 #pragma unroll
           for (int v = 0; v < UPW; ++v) acc2[v][gi] = wd_mfma16(ah[gi], xl[v], acc2[v][gi]);
+        if (WD_SPLIT_PASSES == 3) {
 #pragma unroll
-        for (int gi = 0; gi < G2; ++gi)
+          for (int gi = 0; gi < G2; ++gi)
 #pragma unroll
-          for (int v = 0; v < UPW; ++v) acc2[v][gi] = wd_mfma16(al[gi], xh[v], acc2[v][gi]);
+            for (int v = 0; v < UPW; ++v) acc2[v][gi] = wd_mfma16(al[gi], xh[v], acc2[v][gi]);
+        }
         form(kn, more ? v1p : v0s, nxh, nxl);
 #pragma unroll
         for (int v = 0; v < UPW; ++v) {
@@ -936,7 +984,7 @@ __global__ __launch_bounds__(256, UPW == 1 ? 2 : 1) void wdc_scan_kernel(WdScanA
           // the next step's LDS reads first, then one MFMA + 4 VALU at a time
           __builtin_amdgcn_sched_group_barrier(0x100, 4 + 2 * UPW, 0);
 #pragma unroll
-          for (int i = 0; i < 3 * G2 * UPW; ++i) {
+          for (int i = 0; i < WD_SPLIT_PASSES * G2 * UPW; ++i) {
             __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
             __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);
           }
@@ -978,7 +1026,7 @@ __global__ __launch_bounds__(256, UPW == 1 ? 2 : 1) void wdc_scan_kernel(WdScanA
             for (int ob = 0; ob < NOB; ++ob) {
               const int64_t q = ((int64_t)ob * 2 * RB2 + kb3) * 2;
               bh[ob] = A.W3hl[q * 64 + lane];
-              bl[ob] = A.W3hl[(q + 1) * 64 + lane];
+              if (WD_SPLIT_PASSES3 == 3) bl[ob] = A.W3hl[(q + 1) * 64 + lane];
             }
 #pragma unroll
             for (int ob = 0; ob < NOB; ++ob)
@@ -988,10 +1036,12 @@ __global__ __launch_bounds__(256, UPW == 1 ? 2 : 1) void wdc_scan_kernel(WdScanA
             for (int ob = 0; ob < NOB; ++ob)
 #pragma unroll
               for (int v = 0; v < UPW; ++v) acc3[v][ob] = wd_mfma16(bh[ob], yl[v], acc3[v][ob]);
+            if (WD_SPLIT_PASSES3 == 3) {
 #pragma unroll
-            for (int ob = 0; ob < NOB; ++ob)
+              for (int ob = 0; ob < NOB; ++ob)
 #pragma unroll
-              for (int v = 0; v < UPW; ++v) acc3[v][ob] = wd_mfma16(bl[ob], yh[v], acc3[v][ob]);
+                for (int v = 0; v < UPW; ++v) acc3[v][ob] = wd_mfma16(bl[ob], yh[v], acc3[v][ob]);
+            }
           }
         }
       }
