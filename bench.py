@@ -165,7 +165,7 @@ def build_workload(name, rank, world, device, batch, exact=False, weights="init"
         info = {"model": "WideDeep", "embedding_dim": 64, "deep_layers": [512, 256, 128]}
         bound, kernel = "mfma", ("widedeep_score_kernel" if exact else "wdc_scan_kernel")
         info["scan"] = ("exact fp32" if exact else
-                        "certified split-f16 (3 f16 MFMA passes) pre-filter + exact fp32 re-scoring")
+                        "certified split-f16 (2 f16 MFMA passes, weight residual bounded) pre-filter + exact fp32 re-scoring")
         cpu = ("widedeep", None)
     elif name == "mf":
         sd = syn.mf_state_dict(U, I, 64, seed=0)
