@@ -417,10 +417,10 @@ __global__ __launch_bounds__(256) void widedeep_pair_kernel(
 // The fp32 MFMA rate is 1/16 of the f16 rate.  A plain f16 scan cannot prune W&D: its
 // rigorous error bound (f16 rounding of every operand, propagated through |W3||W2|) spans
 // a third of the score spread.  Split operands can: every f16 operand is x = x_hi + x_lo
-// (x_hi = f16(x), x_lo = f16(x - x_hi)), each layer runs f16 MFMA passes W_hi x_hi + W_hi x_lo
-// (+ W_lo x_hi with WD_SPLIT_PASSES = 3) with fp32 accumulation: the activation's split error
-// is 2^-22, below the fp32 path's own accumulation error, and the weights' residual
-// R = W - W_hi (known, fixed per call) enters the bound exactly: (|R|^T v) . x per layer.
+// (x_hi = f16(x), x_lo = f16(x - x_hi)); layer 2 runs the f16 MFMA passes W_hi x_hi + W_hi x_lo,
+// layer 3 W_hi x_hi only (WD_SPLIT_PASSES / WD_SPLIT_PASSES3), with fp32 accumulation: the
+// activation's split error is 2^-22 (x_lo kept) or 2^-11 |x| (dropped), and the weights'
+// residual R = W - W_hi (known, fixed per call) enters the bound exactly: (|R|^T v) . x.
 // Nothing the scan computes is returned: it only prunes; every returned score is recomputed
 // by wd_tile_fp32 (the fp32 kernel's own arithmetic), so outputs are bitwise those of the
 // exact fp32 path (tests/test_gpu_prefilter.py).
@@ -434,7 +434,8 @@ __global__ __launch_bounds__(256) void widedeep_pair_kernel(
 // 1-Lipschitz and errors propagate through |W|, so
 //   |approx - exact| <= rho (g1 v1.x1 + g2 v2.x2 + g3 v3.x3 + g4 (|fin| + |c_u| + |w_I|)
 //                            + cb) + absb
-// and with two passes v1 += (|R2|^T v2) / g1, v2 += (|R3|^T v3) / g2 (the dropped W_lo x_hi).
+// and for the dropped passes v1 += (|R2|^T v2) / g1, v2 += (|R3|^T v3) / g2 (W_lo x_hi), and
+// v2 *= 1 + 2^-11 / g2 for layer 3's dropped W_hi x_lo (wdc_params_kernel).
 // with g1 = (2.125 K1 + 22)u, g2 = (2.125 n2 + 22)u (layer 3) or (32 RB2 + 12)u (final dot
 // of a two-layer tower), g3 = (32 NOB + 10)u, g4 = 10u, cb the bias-add roundings, absb the
 // f16 subnormal slack (2^-25 per rounding, scaled back), rho = 1 + 2^-6.  The v.x terms are
@@ -453,11 +454,14 @@ typedef _Float16 wh8 __attribute__((ext_vector_type(8)));
 // known residual of the f16 weights, so the bound adds (|R2|^T v2) . x1 (and (|R3|^T v3) . x2
 // for layer 3), folded into v1 / v2 by wdc_params_kernel -- a per-element residual, about
 // 2^-12.5 |W| on average instead of the 2^-11 worst case.
+// Measured (random-init bench weights, 4,096 users x 105,542 items): 3/3 passes 392 ms (51
+// candidates a row), 2/2 295 ms (360), **2/1 275 ms (393)**, 3/2 375 ms (56), 2/3 314 ms (349);
+// one pass on layer 2 (x_lo bounded by 2^-11 |x|) overflows every row's segments.
 #ifndef WD_SPLIT_PASSES
 #define WD_SPLIT_PASSES 2  // layer 2
 #endif
 #ifndef WD_SPLIT_PASSES3
-#define WD_SPLIT_PASSES3 WD_SPLIT_PASSES  // layer 3
+#define WD_SPLIT_PASSES3 1  // layer 3: W_hi x_hi only (both residuals bounded)
 #endif
 
 __device__ __forceinline__ f32x16 wd_mfma16(wh8 a, wh8 b, f32x16 c) {
@@ -651,7 +655,7 @@ __global__ __launch_bounds__(256) void wdc_params_kernel(hnm_widedeep_weights w,
   for (float sc : {s1, sw2, s2, sw3}) bad |= !(sc >= 1e-25f && sc <= 1e25f);
   // b2' in x2 units
   for (int jx = tid; jx < n2; jx += 256) b2s[jx] = p.b2p[jx] * s2;
-  if ((WD_SPLIT_PASSES == 2 || WD_SPLIT_PASSES3 == 2) && !bad) {
+  if ((WD_SPLIT_PASSES < 3 || WD_SPLIT_PASSES3 < 3) && !bad) {
     // the dropped W_lo x_hi passes (see WD_SPLIT_PASSES): v1 += (|R2|^T v2) / g1 and, with a
     // third layer, v2 += (|R3|^T v3) / g2, R = W' - f16(W' sw) / sw exactly as wdc_convert_kernel
     // rounds it; 1 + 2^-10 covers |x_hi| <= (1 + 2^-11)|x| and the fp32 sums.  Each thread
@@ -660,7 +664,10 @@ __global__ __launch_bounds__(256) void wdc_params_kernel(hnm_widedeep_weights w,
     const float g1c = (2.125f * K1P + 22.f) * uu;
     const float g2c = (2.125f * n2 + 22.f) * uu;
     const float fr = 1.0009765625f;
-    for (int t = tid; t < K1P && WD_SPLIT_PASSES == 2; t += 256) {
+    // one pass also drops W_hi x_lo: |x_lo| <= 2^-11 |x| (RNE), i.e. v += 2^-11 v / g
+    const float xl1 = WD_SPLIT_PASSES == 1 ? 4.8828125e-4f : 0.f;
+    const float xl3 = WD_SPLIT_PASSES3 == 1 ? 4.8828125e-4f : 0.f;
+    for (int t = tid; t < K1P && WD_SPLIT_PASSES < 3; t += 256) {
       const int k = wd_korig(t, K1P);
       if (k >= l1) continue;
       float r = 0.f;
@@ -669,9 +676,9 @@ __global__ __launch_bounds__(256) void wdc_params_kernel(hnm_widedeep_weights w,
         v *= sw2;
         r = fmaf(fabsf(v - (float)(_Float16)v), sv2[jx], r);
       }
-      v1[t] += fr * (r / sw2) / g1c;
+      v1[t] = v1[t] * (1.f + fr * xl1 / g1c) + fr * (r / sw2) / g1c;
     }
-    if (p.OB > 0 && WD_SPLIT_PASSES3 == 2) {
+    if (p.OB > 0 && WD_SPLIT_PASSES3 < 3) {
       for (int jx = tid; jx < l2; jx += 256) {
         float r = 0.f;
         for (int m = 0; m < l3; ++m) {
@@ -679,7 +686,7 @@ __global__ __launch_bounds__(256) void wdc_params_kernel(hnm_widedeep_weights w,
           v *= sw3;
           r = fmaf(fabsf(v - (float)(_Float16)v), fabsf(p.wdp[m]), r);
         }
-        v2[jx] += fr * (r / sw3) / g2c;
+        v2[jx] = v2[jx] * (1.f + fr * xl3 / g2c) + fr * (r / sw3) / g2c;
       }
     }
   }
@@ -967,7 +974,8 @@ __global__ __launch_bounds__(256, UPW == 1 ? 2 : 1) void wdc_scan_kernel(WdScanA
 #pragma unroll
         for (int gi = 0; gi < G2; ++gi)
 #pragma unroll
-          for (int v = 0; v < UPW; ++v) acc2[v][gi] = wd_mfma16(ah[gi], xl[v], acc2[v][gi]);
+          for (int v = 0; v < UPW; ++v)
+            if (WD_SPLIT_PASSES >= 2) acc2[v][gi] = wd_mfma16(ah[gi], xl[v], acc2[v][gi]);
         if (WD_SPLIT_PASSES == 3) {
 #pragma unroll
           for (int gi = 0; gi < G2; ++gi)
@@ -1035,7 +1043,8 @@ __global__ __launch_bounds__(256, UPW == 1 ? 2 : 1) void wdc_scan_kernel(WdScanA
 #pragma unroll
             for (int ob = 0; ob < NOB; ++ob)
 #pragma unroll
-              for (int v = 0; v < UPW; ++v) acc3[v][ob] = wd_mfma16(bh[ob], yl[v], acc3[v][ob]);
+              for (int v = 0; v < UPW; ++v)
+                if (WD_SPLIT_PASSES3 >= 2) acc3[v][ob] = wd_mfma16(bh[ob], yl[v], acc3[v][ob]);
             if (WD_SPLIT_PASSES3 == 3) {
 #pragma unroll
               for (int ob = 0; ob < NOB; ++ob)
