@@ -455,8 +455,10 @@ typedef _Float16 wh8 __attribute__((ext_vector_type(8)));
 // for layer 3), folded into v1 / v2 by wdc_params_kernel -- a per-element residual, about
 // 2^-12.5 |W| on average instead of the 2^-11 worst case.
 // Measured (random-init bench weights, 4,096 users x 105,542 items): 3/3 passes 392 ms (51
-// candidates a row), 2/2 295 ms (360), **2/1 275 ms (393)**, 3/2 375 ms (56), 2/3 314 ms (349);
-// one pass on layer 2 (x_lo bounded by 2^-11 |x|) overflows every row's segments.
+// candidates a row), 2/2 295 ms (360), **2/1 272-275 ms (393)**, 3/2 375 ms (56), 2/3 314 ms
+// (349); one pass on layer 2 with x_lo bounded by 2^-11 |x| overflows every row's segments,
+// with the per-pair exact x_lo term (v1o . |x - x_hi|, WD_SPLIT_PASSES = 1) it holds (788
+// candidates a row) but runs 283 ms: at half the MFMAs the k loop's operand VALU bounds it.
 #ifndef WD_SPLIT_PASSES
 #define WD_SPLIT_PASSES 2  // layer 2
 #endif
@@ -557,7 +559,8 @@ __global__ __launch_bounds__(256) void wdc_params_kernel(hnm_widedeep_weights w,
                                                          float* __restrict__ v1,
                                                          float* __restrict__ v2,
                                                          float* __restrict__ b2s,
-                                                         WdCertParams* prm) {
+                                                         WdCertParams* prm,
+                                                         float* __restrict__ v1o) {
   __shared__ float sv2[256];
   __shared__ float red[8][4];
   __shared__ float bc[8];
@@ -608,6 +611,7 @@ __global__ __launch_bounds__(256) void wdc_params_kernel(hnm_widedeep_weights w,
       }
     }
     v1[t] = v;
+    v1o[t] = v;  // before the dropped-pass terms: the per-pair x_lo term of a one-pass layer 2
     sv1 += v;
   }
   const float zmax = mp + mq;
@@ -664,8 +668,9 @@ __global__ __launch_bounds__(256) void wdc_params_kernel(hnm_widedeep_weights w,
     const float g1c = (2.125f * K1P + 22.f) * uu;
     const float g2c = (2.125f * n2 + 22.f) * uu;
     const float fr = 1.0009765625f;
-    // one pass also drops W_hi x_lo: |x_lo| <= 2^-11 |x| (RNE), i.e. v += 2^-11 v / g
-    const float xl1 = WD_SPLIT_PASSES == 1 ? 4.8828125e-4f : 0.f;
+    // one pass on layer 3 also drops W_hi x_lo: |x_lo| <= 2^-11 |x| (RNE), i.e. v2 += 2^-11 v2 /
+    // g2; a one-pass layer 2 bounds its x_lo term per pair instead (scan: v1o . |x - x_hi|)
+    const float xl1 = 0.f;
     const float xl3 = WD_SPLIT_PASSES3 == 1 ? 4.8828125e-4f : 0.f;
     for (int t = tid; t < K1P && WD_SPLIT_PASSES < 3; t += 256) {
       const int k = wd_korig(t, K1P);
@@ -777,6 +782,7 @@ struct WdScanArgs {
   const wh8* W2hl;
   const wh8* W3hl;
   const float* v1;   // [K1P]
+  const float* v1o;  // [K1P] v1 without the dropped-pass terms (one-pass layer 2)
   const float* v2;   // [RB2*32]
   const float* b2s;  // [RB2*32] b2' s2
   const float* b3p;  // [OB*32]
@@ -828,6 +834,7 @@ __global__ __launch_bounds__(256, UPW == 1 ? 2 : 1) void wdc_scan_kernel(WdScanA
   float* b3l = v2l + RB2 * 32;    // [NOB*32]
   float* wdl = b3l + NOB * 32;    // [NL*32]
   float* v0s = wdl + NL * 32;     // [K1P] zeros (the bound row of passes > 0)
+  float* v1os = v0s + K1P;        // [K1P] v1o (one-pass layer 2: the per-pair x_lo term)
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5, j = lane & 31;
   const int64_t ublk = (int64_t)blockIdx.x * NU;
@@ -840,6 +847,7 @@ __global__ __launch_bounds__(256, UPW == 1 ? 2 : 1) void wdc_scan_kernel(WdScanA
   for (int e = tid; e < K1P; e += 256) {
     v1s[e] = A.v1[e] * inv_s1;
     v0s[e] = 0.f;
+    v1os[e] = WD_SPLIT_PASSES == 1 ? A.v1o[e] * inv_s1 : 0.f;
   }
   for (int e = tid; e < NU * K1P / 4; e += 256) {
     const int r = e / (K1P / 4), c = e % (K1P / 4);
@@ -907,9 +915,9 @@ __global__ __launch_bounds__(256, UPW == 1 ? 2 : 1) void wdc_scan_kernel(WdScanA
 #pragma unroll
       for (int ob = 0; ob < NOB; ++ob)
         acc3[v][ob] = f32x16{0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    float fin[UPW], bx1[UPW], bx2[UPW], bx3[UPW];
+    float fin[UPW], bx1[UPW], bx2[UPW], bx3[UPW], bxl[UPW];
 #pragma unroll
-    for (int v = 0; v < UPW; ++v) fin[v] = bx1[v] = bx2[v] = bx3[v] = 0.f;
+    for (int v = 0; v < UPW; ++v) fin[v] = bx1[v] = bx2[v] = bx3[v] = bxl[v] = 0.f;
 #pragma unroll 1
     for (int g = 0; g < RB2 / G2; ++g) {
       f32x16 acc2[UPW][G2];
@@ -926,15 +934,21 @@ __global__ __launch_bounds__(256, UPW == 1 ? 2 : 1) void wdc_scan_kernel(WdScanA
       // used 2 G2 UPW MFMAs later).  v1 . x1 accumulates in pass 0 only: later passes and the
       // tail step read the zero row v0s, so the loop body stays branch-free for the scheduler.
       const float* v1p = g == 0 ? v1s : v0s;
+      const float* vop = g == 0 ? v1os : v0s;
       auto frag = [&](int gi, int kk, int hl) {
         const int64_t q = (ABL & 1) ? (int64_t)gi * 2 : ((int64_t)(g * G2 + gi) * KB + kk) * 2;
         return A.W2hl[(q + hl) * 64 + lane];
       };
-      auto form = [&](int kk, const float* vrow, wh8* oh, wh8* ol) {
+      auto form = [&](int kk, const float* vrow, const float* vorow, wh8* oh, wh8* ol) {
         const float4 q0 = *reinterpret_cast<const float4*>(qrow + 16 * kk);
         const float4 q1 = *reinterpret_cast<const float4*>(qrow + 16 * kk + 4);
         const float4 va = *reinterpret_cast<const float4*>(vrow + 16 * kk + 8 * h);
         const float4 vb = *reinterpret_cast<const float4*>(vrow + 16 * kk + 8 * h + 4);
+        float4 oa = {}, ob = {};
+        if (WD_SPLIT_PASSES == 1) {
+          oa = *reinterpret_cast<const float4*>(vorow + 16 * kk + 8 * h);
+          ob = *reinterpret_cast<const float4*>(vorow + 16 * kk + 8 * h + 4);
+        }
 #pragma unroll
         for (int v = 0; v < UPW; ++v) {
           const float* prow = ps + (wave * UPW + v) * K1P + 8 * h + 16 * kk;
@@ -950,11 +964,24 @@ __global__ __launch_bounds__(256, UPW == 1 ? 2 : 1) void wdc_scan_kernel(WdScanA
           bb = fmaf(vb.x, x[4], bb); bb = fmaf(vb.y, x[5], bb);
           bb = fmaf(vb.z, x[6], bb); bb = fmaf(vb.w, x[7], bb);
           bx1[v] = bb;
-          wd_split8(x, oh[v], ol[v]);
+          if (WD_SPLIT_PASSES == 1) {
+            // layer 2 runs W_hi x_hi only: its x_lo term, v1o . |x - f32(x_hi)| (exact residual)
+            const float vo[8] = {oa.x, oa.y, oa.z, oa.w, ob.x, ob.y, ob.z, ob.w};
+            float bl = bxl[v];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              const _Float16 hv = (_Float16)x[e];
+              oh[v][e] = hv;
+              bl = fmaf(vo[e], fabsf(x[e] - (float)hv), bl);
+            }
+            bxl[v] = bl;
+          } else {
+            wd_split8(x, oh[v], ol[v]);
+          }
         }
       };
       wh8 xh[UPW], xl[UPW], ahn[G2];
-      form(0, v1p, xh, xl);
+      form(0, v1p, vop, xh, xl);
 #pragma unroll
       for (int gi = 0; gi < G2; ++gi) ahn[gi] = frag(gi, 0, 0);
       for (int kb = 0; kb < KB; ++kb) {
@@ -982,7 +1009,7 @@ __global__ __launch_bounds__(256, UPW == 1 ? 2 : 1) void wdc_scan_kernel(WdScanA
 #pragma unroll
             for (int v = 0; v < UPW; ++v) acc2[v][gi] = wd_mfma16(al[gi], xh[v], acc2[v][gi]);
         }
-        form(kn, more ? v1p : v0s, nxh, nxl);
+        form(kn, more ? v1p : v0s, more ? vop : v0s, nxh, nxl);
 #pragma unroll
         for (int v = 0; v < UPW; ++v) {
           xh[v] = nxh[v];
@@ -1082,10 +1109,12 @@ __global__ __launch_bounds__(256, UPW == 1 ? 2 : 1) void wdc_scan_kernel(WdScanA
       }
       const float fv = hnm_sum_halves(fin[v]);
       const float b1 = hnm_sum_halves(bx1[v]);
+      // one-pass layer 2's x_lo term (x 1 + 2^-10: |W_hi| <= (1 + 2^-11)|W'| and the sums)
+      const float bl1 = WD_SPLIT_PASSES == 1 ? 1.0009765625f * hnm_sum_halves(bxl[v]) : 0.f;
       const float b2 = hnm_sum_halves(bx2[v]);
       const float b3 = hnm_sum_halves(bx3[v]);
       const float score = fv + cub[v] + wi;
-      const float e = rho * (g1 * b1 + g2 * (b2 * inv_s2) + g3 * b3 +
+      const float e = rho * (g1 * b1 + bl1 + g2 * (b2 * inv_s2) + g3 * b3 +
                              g4 * (fabsf(fv) + fabsf(cub[v]) + fabsf(wi)) + cbd) + absb;
       bool masked = false;
       while (nm[v] < tile_end) {
@@ -1451,7 +1480,7 @@ static hnm_status wd_exact(hnm_ctx* ctx, const hnm_widedeep_weights* w, const Wd
 }
 
 // ------------------------------------------------------------------ certified path host
-#define WDC_CAP 1024  // appended candidates per (user, partition) segment
+#define WDC_CAP (WD_SPLIT_PASSES == 1 ? 4096 : 1024)  // appended candidates per (user, partition) segment
 
 static bool wdc_instantiated(int RB2, int OB) {
   return (RB2 == 8 && OB == 4) || (RB2 == 4 && OB == 2) || (RB2 == 2 && OB == 1) ||
@@ -1468,6 +1497,7 @@ struct WdcWs {
   wh8* W2hl;
   wh8* W3hl;
   float* v1;
+  float* v1o;
   float* v2;
   float* b2s;
   float* part;
@@ -1510,6 +1540,7 @@ static size_t wdc_carve(const hnm_ctx* ctx, const WdPrep& pr, int64_t B, int64_t
   t.W2hl = (wh8*)take((size_t)pr.RB2 * KB * 2 * 64 * 16);
   t.W3hl = (wh8*)take((size_t)std::max(pr.OB, 1) * 2 * pr.RB2 * 2 * 64 * 16);
   t.v1 = (float*)take((size_t)K1P * 4);
+  t.v1o = (float*)take((size_t)K1P * 4);
   t.v2 = (float*)take((size_t)pr.RB2 * 32 * 4);
   t.b2s = (float*)take((size_t)pr.RB2 * 32 * 4);
   t.part = (float*)take((size_t)WDC_STAT_BLOCKS * 2 * 4);
@@ -1540,7 +1571,7 @@ static hnm_status wdc_prepare(hnm_ctx* ctx, const hnm_widedeep_weights* w, const
   hipLaunchKernelGGL(wdc_stats_kernel, dim3(WDC_STAT_BLOCKS), dim3(256), 0, s, S.Pu,
                      B * S.K1P, S.Qi, I * S.K1P, c.part);
   hipLaunchKernelGGL(wdc_params_kernel, dim3(1), dim3(256), 0, s, *w, S.pr, c.part,
-                     WDC_STAT_BLOCKS, c.v1, c.v2, c.b2s, c.prm);
+                     WDC_STAT_BLOCKS, c.v1, c.v2, c.b2s, c.prm, c.v1o);
   hipLaunchKernelGGL(wdc_convert_kernel, dim3(256), dim3(256), 0, s, *w, S.pr, c.prm, c.W2hl,
                      c.W3hl);
   HNM_LAUNCH_CHECK();
@@ -1573,6 +1604,7 @@ static hnm_status wdc_scan(hnm_ctx* ctx, const hnm_widedeep_weights* w, const Wd
   a.W2hl = c.W2hl;
   a.W3hl = c.W3hl;
   a.v1 = c.v1;
+  a.v1o = c.v1o;
   a.v2 = c.v2;
   a.b2s = c.b2s;
   a.b3p = pr.b3p;
@@ -1598,7 +1630,7 @@ static hnm_status wdc_scan(hnm_ctx* ctx, const hnm_widedeep_weights* w, const Wd
   a.lda = lda;
   const int upb = 4 * wdc_upw(pr);
   const size_t lds =
-      (size_t)(32 * (S.K1P + 4) + (upb + 2) * S.K1P + 2 * pr.RB2 * 32 + NOB * 32 + NL * 32) * 4;
+      (size_t)(32 * (S.K1P + 4) + (upb + 3) * S.K1P + 2 * pr.RB2 * 32 + NOB * 32 + NL * 32) * 4;
   dim3 grid((unsigned)hnm_cdiv(B, upb), (unsigned)c.np);
   if (mode == WDC_THRESH) hnm_timer_begin(ctx, HNM_TIME_SCORE);
 #define WDC_CASE(R, O)                                                        \
