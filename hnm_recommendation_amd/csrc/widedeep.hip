@@ -1583,7 +1583,7 @@ static void wdc_launch_scan(hnm_ctx* ctx, dim3 grid, size_t lds, const WdScanArg
   constexpr int G2 = RB2 < 4 ? RB2 : 4;
   constexpr int UPW = RB2 == 8 && OB == 4 ? 2 : 1;  // = wdc_upw
   auto kern = wdc_scan_kernel<RB2, OB, G2, MODE, UPW, ABL>;
-  hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   hipLaunchKernelGGL(kern, grid, dim3(256), lds, ctx->stream, a);
 }
 
