@@ -1016,7 +1016,8 @@ __global__ __launch_bounds__(256, UPW == 1 ? 2 : 1) void wdc_scan_kernel(WdScanA
           xl[v] = nxl[v];
         }
         if (WDC_INTERLEAVE) {
-          // the next step's LDS reads first, then one MFMA + 4 VALU at a time
+          // the next step's LDS reads first, then one MFMA + 4 VALU at a time (2+1 passes:
+          // 268-272 ms; 2, 3, 5, 6, 8 VALU per MFMA 305-315 ms, compiler order 331 ms)
           __builtin_amdgcn_sched_group_barrier(0x100, 4 + 2 * UPW, 0);
 #pragma unroll
           for (int i = 0; i < WD_SPLIT_PASSES * G2 * UPW; ++i) {
