@@ -36,6 +36,9 @@ extern "C" hnm_status hnm_ctx_create(int device, hnm_ctx** out) {
   }
   HNM_HIP_CHECK(hipMemset(c->err_dev, 0, 64));
   HNM_HIP_CHECK(hipEventCreateWithFlags(&c->chain_ev, hipEventDisableTiming));
+  HNM_HIP_CHECK(hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
+  HNM_HIP_CHECK(hipEventCreateWithFlags(&c->side_in, hipEventDisableTiming));
+  HNM_HIP_CHECK(hipEventCreateWithFlags(&c->side_out, hipEventDisableTiming));
   // counters of the certified pre-filter live in the same allocation (8-byte aligned)
   c->stats_dev = reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(c->err_dev) + 8);
   *out = c;
@@ -55,6 +58,9 @@ extern "C" hnm_status hnm_ctx_destroy(hnm_ctx* ctx) {
   if (ctx->ws) (void)hipFree(ctx->ws);
   if (ctx->err_dev) (void)hipFree(ctx->err_dev);
   (void)hipEventDestroy(ctx->chain_ev);
+  (void)hipEventDestroy(ctx->side_in);
+  (void)hipEventDestroy(ctx->side_out);
+  (void)hipStreamDestroy(ctx->side);
   free(ctx);
   return HNM_OK;
 }

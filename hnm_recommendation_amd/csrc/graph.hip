@@ -28,6 +28,9 @@
 #ifndef SEG
 #define SEG 2048
 #endif
+#ifndef SPMM_SIDE_STREAM  // heavy-row segments on the ctx's side stream, beside the light kernel
+#define SPMM_SIDE_STREAM 1
+#endif
 
 struct hnm_spmm_plan {
   int device;
@@ -489,11 +492,10 @@ static hnm_status spmm_launch(hnm_ctx* ctx, const hnm_spmm_plan* pl, int64_t N,
   // the live roofline times whole-graph layers only (row-range calls do less work)
   const bool timed = r0 == 0 && r1 == N;
   if (timed) hnm_timer_begin(ctx, HNM_TIME_SPMM);
-  if (r1 > r0) {
-    hipLaunchKernelGGL(spmm_light_kernel<LPR>, dim3((unsigned)hnm_cdiv(r1 - r0, 4)), dim3(256), 0,
-                       ctx->stream, r0, r1, rowptr, col, val, X, d, ep, heavy);
-    HNM_LAUNCH_CHECK();
-  }
+  // the heavy rows' segments + finish run on the ctx's side stream, concurrent with the light
+  // kernel (disjoint output rows, X read-only): they fill the CUs the light kernel's long item
+  // rows leave idle at its tail; the ctx stream joins before anything reads Y
+  bool forked = false;
   if (has_heavy) {
     // heavy rows inside [r0, r1): heavy rows are ascending
     const std::vector<int32_t>& hv = *pl->h_heavy;
@@ -505,15 +507,31 @@ static hnm_status spmm_launch(hnm_ctx* ctx, const hnm_spmm_plan* pl, int64_t N,
       hnm_status s = hnm_workspace(ctx, (size_t)(sg1 - sg0) * d * 4, &w);
       if (s) return s;
       float* partial = (float*)w;
+      hipStream_t hs = ctx->stream;
+      if (SPMM_SIDE_STREAM) {
+        HNM_HIP_CHECK(hipEventRecord(ctx->side_in, ctx->stream));
+        HNM_HIP_CHECK(hipStreamWaitEvent(ctx->side, ctx->side_in, 0));
+        hs = ctx->side;
+      }
       hipLaunchKernelGGL(spmm_segment_kernel<LPR>, dim3((unsigned)hnm_cdiv(sg1 - sg0, 4)),
-                         dim3(256), 0, ctx->stream, sg0, sg1, pl->seg_start, pl->seg_end, col, val,
+                         dim3(256), 0, hs, sg0, sg1, pl->seg_start, pl->seg_end, col, val,
                          X, d, partial);
       HNM_LAUNCH_CHECK();
-      hipLaunchKernelGGL(spmm_finish_kernel, dim3((unsigned)(h1 - h0)), dim3(256), 0, ctx->stream,
+      hipLaunchKernelGGL(spmm_finish_kernel, dim3((unsigned)(h1 - h0)), dim3(256), 0, hs,
                          h0, pl->heavy_rows, pl->seg_ptr, sg0, partial, X, d, ep);
       HNM_LAUNCH_CHECK();
+      if (SPMM_SIDE_STREAM) {
+        HNM_HIP_CHECK(hipEventRecord(ctx->side_out, ctx->side));
+        forked = true;
+      }
     }
   }
+  if (r1 > r0) {
+    hipLaunchKernelGGL(spmm_light_kernel<LPR>, dim3((unsigned)hnm_cdiv(r1 - r0, 4)), dim3(256), 0,
+                       ctx->stream, r0, r1, rowptr, col, val, X, d, ep, heavy);
+    HNM_LAUNCH_CHECK();
+  }
+  if (forked) HNM_HIP_CHECK(hipStreamWaitEvent(ctx->stream, ctx->side_out, 0));
   if (timed) hnm_timer_end(ctx, HNM_TIME_SPMM);
   return HNM_OK;
 }

@@ -14,6 +14,8 @@ struct hnm_ctx {
   hipStream_t stream;   // borrowed from the caller (torch's current stream); 0 = null stream
   hipEvent_t chain_ev;  // stream switch: recorded on the old stream, waited on by the new one,
                         // so all work of this ctx (and its workspace reuse) stays ordered
+  hipStream_t side;     // owned side stream: independent work overlapped with the ctx stream
+  hipEvent_t side_in, side_out;  // fork (ctx stream -> side) / join (side -> ctx stream)
   void* ws;             // grow-only device workspace owned by the ctx
   size_t ws_size;
   unsigned* err_dev;    // device error word (HNM_ERR_* bits), read by hnm_ctx_check
