@@ -808,6 +808,9 @@ struct WdScanArgs {
 
 #define WDC_THRESH 0
 #define WDC_DEBUG 1
+#ifndef WDC_G2
+#define WDC_G2 4  // layer-2 row blocks per pass over k (the x operands are formed once per pass)
+#endif
 #ifndef WDC_INTERLEAVE
 #define WDC_INTERLEAVE 1  // sched_group_barrier interleave of the k loop (0: compiler order)
 #endif
@@ -835,6 +838,8 @@ __global__ __launch_bounds__(256, UPW == 1 ? 2 : 1) void wdc_scan_kernel(WdScanA
   float* wdl = b3l + NOB * 32;    // [NL*32]
   float* v0s = wdl + NL * 32;     // [K1P] zeros (the bound row of passes > 0)
   float* v1os = v0s + K1P;        // [K1P] v1o (one-pass layer 2: the per-pair x_lo term)
+  // qs / qn (offset qn_off): the Q tile being scored and the next one, filled during its k loop
+  const int qn_off = (int)(v1os + K1P - smem);
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5, j = lane & 31;
   const int64_t ublk = (int64_t)blockIdx.x * NU;
@@ -893,28 +898,47 @@ __global__ __launch_bounds__(256, UPW == 1 ? 2 : 1) void wdc_scan_kernel(WdScanA
   }
 
   const int64_t ntiles = part_end > part_start ? hnm_cdiv(part_end - part_start, WD_TILE) : 0;
+  // Q tiles are double-buffered: tile t + 1 is copied into the other buffer while tile t is
+  // scored, one 8-column slice of its 32 rows per k step (K1P / 8 = NG KB / QPS steps; a
+  // thread moves one dword of row tid / 8): step s writes the slice loaded during step s - 1
+  // and loads slice s + 1 -- no exposed load latency, one barrier a tile, no branches in the
+  // k loop (kernel 270 -> 261 ms; the tile load + barrier it replaces cost 6 %).  The loads are
+  // buffer loads over the next tile's valid rows (a scalar column offset; rows past the
+  // partition, and the slice after the last, read as 0 by the bounds check).  Q is staged
+  // unscaled: the k loop forms s1 x1 = fma(q, s1, p s1), which rounds exactly like s1 (p + q)
+  // (s1 is a power of two; scaling in the copy instead, one more VALU a step: 275 ms).
+  constexpr int NG = RB2 / G2, QPS = 2 / NG;
+  static_assert(NG * QPS == 2, "one tile's copy spans the tile's k steps");
+  const int qrow_t = tid >> 3, qcol_t = tid & 7;
+  const int qvoff = (qrow_t * K1P + qcol_t) * 4;
+  auto qrsrc = [&](int64_t nb) {  // the tile at nb: its rows inside the partition
+    const int64_t rows = std::max<int64_t>(0, std::min<int64_t>(WD_TILE, part_end - nb));
+    const float* src = A.Qi + std::min<int64_t>(nb, part_end - 1) * K1P;
+    return __builtin_amdgcn_make_buffer_rsrc((void*)src, 0, (int)(rows * K1P * 4), 0x00020000);
+  };
+  auto qload = [&](__amdgpu_buffer_rsrc_t rs, int c) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, qvoff, c * 4, 0));
+  };
+  if (ntiles > 0) {
+    const __amdgpu_buffer_rsrc_t rs = qrsrc(part_start);
+    for (int c = 0; c < K1P; c += 8) smem[qrow_t * QRS + qcol_t + c] = qload(rs, c);
+  }
   for (int64_t t = 0; t < ntiles; ++t) {
     const int64_t base = part_start + t * WD_TILE;
+    const int cur_off = (t & 1) ? qn_off : 0, nxt_off = (t & 1) ? 0 : qn_off;
+    const __amdgpu_buffer_rsrc_t qrs = qrsrc(base + WD_TILE);
+    float* const qdst = smem + nxt_off + qrow_t * QRS + qcol_t;
     __syncthreads();
-    for (int e = tid; e < WD_TILE * K1P / 4; e += 256) {
-      const int r = e / (K1P / 4), c = e % (K1P / 4);
-      const int64_t item = base + r;
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (item < part_end && !((ABL & 4) && t > 0))
-        v = *reinterpret_cast<const float4*>(A.Qi + item * K1P + 4 * c);
-      v.x *= s1; v.y *= s1; v.z *= s1; v.w *= s1;
-      if (!((ABL & 4) && t > 0)) *reinterpret_cast<float4*>(&qs[r * QRS + 4 * c]) = v;
+    if (!act[0]) {  // users are assigned in order: the wave has none, it only copies
+      for (int c = 0; c < K1P; c += 8) qdst[c] = qload(qrs, c);
+      continue;
     }
-    __syncthreads();
-    if (!act[0]) continue;  // users are assigned in order: the wave has none
+    float qv[QPS];
+#pragma unroll
+    for (int e = 0; e < QPS; ++e) qv[e] = qload(qrs, 8 * e);
 
-    const float* qrow = qs + j * QRS + 8 * h;
+    const float* qrow = smem + cur_off + j * QRS + 8 * h;
     f32x16 acc3[UPW][NOB];
-#pragma unroll
-    for (int v = 0; v < UPW; ++v)
-#pragma unroll
-      for (int ob = 0; ob < NOB; ++ob)
-        acc3[v][ob] = f32x16{0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     float fin[UPW], bx1[UPW], bx2[UPW], bx3[UPW], bxl[UPW];
 #pragma unroll
     for (int v = 0; v < UPW; ++v) fin[v] = bx1[v] = bx2[v] = bx3[v] = bxl[v] = 0.f;
@@ -954,10 +978,11 @@ __global__ __launch_bounds__(256, UPW == 1 ? 2 : 1) void wdc_scan_kernel(WdScanA
           const float* prow = ps + (wave * UPW + v) * K1P + 8 * h + 16 * kk;
           const float4 p0 = *reinterpret_cast<const float4*>(prow);
           const float4 p1 = *reinterpret_cast<const float4*>(prow + 4);
-          // x1 * s1 (P, Q pre-scaled)
-          float x[8] = {fmaxf(p0.x + q0.x, 0.f), fmaxf(p0.y + q0.y, 0.f), fmaxf(p0.z + q0.z, 0.f),
-                        fmaxf(p0.w + q0.w, 0.f), fmaxf(p1.x + q1.x, 0.f), fmaxf(p1.y + q1.y, 0.f),
-                        fmaxf(p1.z + q1.z, 0.f), fmaxf(p1.w + q1.w, 0.f)};
+          // x1 * s1 (P pre-scaled, Q scaled here)
+          float x[8] = {fmaxf(fmaf(q0.x, s1, p0.x), 0.f), fmaxf(fmaf(q0.y, s1, p0.y), 0.f),
+                        fmaxf(fmaf(q0.z, s1, p0.z), 0.f), fmaxf(fmaf(q0.w, s1, p0.w), 0.f),
+                        fmaxf(fmaf(q1.x, s1, p1.x), 0.f), fmaxf(fmaf(q1.y, s1, p1.y), 0.f),
+                        fmaxf(fmaf(q1.z, s1, p1.z), 0.f), fmaxf(fmaf(q1.w, s1, p1.w), 0.f)};
           float bb = bx1[v];
           bb = fmaf(va.x, x[0], bb); bb = fmaf(va.y, x[1], bb);
           bb = fmaf(va.z, x[2], bb); bb = fmaf(va.w, x[3], bb);
@@ -980,18 +1005,16 @@ __global__ __launch_bounds__(256, UPW == 1 ? 2 : 1) void wdc_scan_kernel(WdScanA
           }
         }
       };
-      wh8 xh[UPW], xl[UPW], ahn[G2];
-      form(0, v1p, vop, xh, xl);
-#pragma unroll
-      for (int gi = 0; gi < G2; ++gi) ahn[gi] = frag(gi, 0, 0);
-      for (int kb = 0; kb < KB; ++kb) {
+      // one k step: MFMAs on the (ah, xh, xl) set while the other set is loaded / formed for
+      // step kb + 1
+      auto step = [&](int kb, const wh8 (&ah)[G2], wh8 (&an)[G2], const wh8 (&xh)[UPW],
+                      const wh8 (&xl)[UPW], wh8 (&nxh)[UPW], wh8 (&nxl)[UPW]) {
         const bool more = kb + 1 < KB;
         const int kn = more ? kb + 1 : kb;
-        wh8 ah[G2], al[G2], nxh[UPW], nxl[UPW];
+        wh8 al[G2];
 #pragma unroll
         for (int gi = 0; gi < G2; ++gi) {
-          ah[gi] = ahn[gi];
-          ahn[gi] = frag(gi, kn, 0);
+          an[gi] = frag(gi, kn, 0);
           if (WD_SPLIT_PASSES == 3) al[gi] = frag(gi, kb, 1);
         }
 #pragma unroll
@@ -1010,10 +1033,12 @@ __global__ __launch_bounds__(256, UPW == 1 ? 2 : 1) void wdc_scan_kernel(WdScanA
             for (int v = 0; v < UPW; ++v) acc2[v][gi] = wd_mfma16(al[gi], xh[v], acc2[v][gi]);
         }
         form(kn, more ? v1p : v0s, more ? vop : v0s, nxh, nxl);
+        // next tile's copy: write the slice loaded last step, load the next one
 #pragma unroll
-        for (int v = 0; v < UPW; ++v) {
-          xh[v] = nxh[v];
-          xl[v] = nxl[v];
+        for (int e = 0; e < QPS; ++e) {
+          const int c = 8 * ((g * KB + kb) * QPS + e);
+          qdst[c] = qv[e];
+          qv[e] = qload(qrs, c + 8 * QPS);
         }
         if (WDC_INTERLEAVE) {
           // the next step's LDS reads first, then one MFMA + 4 VALU at a time (2+1 passes:
@@ -1025,10 +1050,35 @@ __global__ __launch_bounds__(256, UPW == 1 ? 2 : 1) void wdc_scan_kernel(WdScanA
             __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);
           }
         }
+      };
+      wh8 fa[G2], fb[G2], xha[UPW], xla[UPW], xhb[UPW], xlb[UPW];
+      form(0, v1p, vop, xha, xla);
+#pragma unroll
+      for (int gi = 0; gi < G2; ++gi) fa[gi] = frag(gi, 0, 0);
+      // (steps in pairs with the two register sets swapped instead of copied: 266 ms vs 261)
+      for (int kb = 0; kb < KB; ++kb) {
+        step(kb, fa, fb, xha, xla, xhb, xlb);
+#pragma unroll
+        for (int gi = 0; gi < G2; ++gi) fa[gi] = fb[gi];
+#pragma unroll
+        for (int v = 0; v < UPW; ++v) {
+          xha[v] = xhb[v];
+          xla[v] = xlb[v];
+        }
+      }
+      if (G2 < RB2 && g == 0) {  // zeroed after the k loop (G2 = RB2: by the first MFMA's C = 0)
+#pragma unroll
+        for (int v = 0; v < UPW; ++v)
+#pragma unroll
+          for (int ob = 0; ob < NOB; ++ob)
+            acc3[v][ob] = f32x16{0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
       }
       // x2 = relu(D2 + b2') in s2 units feeds layer 3 (or the final dot)
 #pragma unroll
       for (int gi = 0; gi < G2; ++gi) {
+        // fence: keeps the scheduler from hoisting every row block's layer-3 fragment loads
+        // (G2 = 8: 64 x 16 B a lane) above the first block's MFMAs
+        if (G2 == RB2) __builtin_amdgcn_sched_barrier(0);
         const int rb = g * G2 + gi;
         float y[UPW][16];
         float bias16[16], vv16[16];
@@ -1060,14 +1110,19 @@ __global__ __launch_bounds__(256, UPW == 1 ? 2 : 1) void wdc_scan_kernel(WdScanA
             wh8 bh[NOB], bl[NOB];
 #pragma unroll
             for (int ob = 0; ob < NOB; ++ob) {
-              const int64_t q = ((int64_t)ob * 2 * RB2 + kb3) * 2;
+              const int64_t q = (ABL & 8) ? (int64_t)ob * 2 : ((int64_t)ob * 2 * RB2 + kb3) * 2;
               bh[ob] = A.W3hl[q * 64 + lane];
               if (WD_SPLIT_PASSES3 == 3) bl[ob] = A.W3hl[(q + 1) * 64 + lane];
             }
+            // G2 = RB2: the chain starts at the first row block with C = 0 (an inline constant),
+            // so acc3 becomes live only as acc2's registers are consumed
+            const bool first = G2 == RB2 && gi == 0 && half2 == 0;
+            const f32x16 zero16 = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll
             for (int ob = 0; ob < NOB; ++ob)
 #pragma unroll
-              for (int v = 0; v < UPW; ++v) acc3[v][ob] = wd_mfma16(bh[ob], yh[v], acc3[v][ob]);
+              for (int v = 0; v < UPW; ++v)
+                acc3[v][ob] = wd_mfma16(bh[ob], yh[v], first ? zero16 : acc3[v][ob]);
 #pragma unroll
             for (int ob = 0; ob < NOB; ++ob)
 #pragma unroll
@@ -1579,9 +1634,12 @@ static hnm_status wdc_prepare(hnm_ctx* ctx, const hnm_widedeep_weights* w, const
   return HNM_OK;
 }
 
-template <int RB2, int OB, int MODE, int ABL = 0>
+#ifndef WDC_ABL  // timing ablations (wrong scores; tools only): 1 W2 / 8 W3 fragments from one
+#define WDC_ABL 0  // address
+#endif
+template <int RB2, int OB, int MODE, int ABL = WDC_ABL>
 static void wdc_launch_scan(hnm_ctx* ctx, dim3 grid, size_t lds, const WdScanArgs& a) {
-  constexpr int G2 = RB2 < 4 ? RB2 : 4;
+  constexpr int G2 = RB2 < WDC_G2 ? RB2 : WDC_G2;
   constexpr int UPW = RB2 == 8 && OB == 4 ? 2 : 1;  // = wdc_upw
   auto kern = wdc_scan_kernel<RB2, OB, G2, MODE, UPW, ABL>;
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -1631,7 +1689,7 @@ static hnm_status wdc_scan(hnm_ctx* ctx, const hnm_widedeep_weights* w, const Wd
   a.lda = lda;
   const int upb = 4 * wdc_upw(pr);
   const size_t lds =
-      (size_t)(32 * (S.K1P + 4) + (upb + 3) * S.K1P + 2 * pr.RB2 * 32 + NOB * 32 + NL * 32) * 4;
+      (size_t)(2 * 32 * (S.K1P + 4) + (upb + 3) * S.K1P + 2 * pr.RB2 * 32 + NOB * 32 + NL * 32) * 4;
   dim3 grid((unsigned)hnm_cdiv(B, upb), (unsigned)c.np);
   if (mode == WDC_THRESH) hnm_timer_begin(ctx, HNM_TIME_SCORE);
 #define WDC_CASE(R, O)                                                        \
