@@ -120,18 +120,41 @@ __global__ __launch_bounds__(256) void cert_stats_kernel(NcfTabs t, int64_t B, i
         aq[u] = fabsf(t.Qi[i * 64 + lane]);
         g[u] = lane < mf ? t.G[i * t.ldg + lane] : 0.f;
       }
+      // the 8 wave sums (vt . |q|, |g|^2 of the 4 items) as one reduce-scatter butterfly: each
+      // xor step halves the values a lane carries (10 shuffles instead of 48); every sum is
+      // formed along the same xor 32, 16, ..., 1 pairing as wave_sum, so bitwise the same
+      float v8[8];
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        const int64_t i = i0 + u * stride;
-        if (i >= I) break;  // uniform
-        m0 = nmax(m0, aq[u]);
-        m1 = nmax(m1, fabsf(g[u]));
-        const float bq = wave_sum(vt * aq[u]), dq = sqrtf(wave_sum(g[u] * g[u]));
-        m2 = nmax(m2, bq);
-        m3 = nmax(m3, dq);
-        if (lane == 0) {
-          Bi[i] = bq;
-          Di[i] = dq;
+        v8[u] = vt * aq[u];
+        v8[4 + u] = g[u] * g[u];
+        if (i0 + u * stride < I) {  // uniform
+          m0 = nmax(m0, aq[u]);
+          m1 = nmax(m1, fabsf(g[u]));
+        }
+      }
+      const bool b5 = lane & 32, b4 = lane & 16, b3 = lane & 8;
+      float w4[4], w2[2];
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        w4[q] = (b5 ? v8[2 * q + 1] : v8[2 * q]) + __shfl_xor(b5 ? v8[2 * q] : v8[2 * q + 1], 32);
+#pragma unroll
+      for (int q = 0; q < 2; ++q)
+        w2[q] = (b4 ? w4[2 * q + 1] : w4[2 * q]) + __shfl_xor(b4 ? w4[2 * q] : w4[2 * q + 1], 16);
+      float w1 = (b3 ? w2[1] : w2[0]) + __shfl_xor(b3 ? w2[0] : w2[1], 8);
+      w1 += __shfl_xor(w1, 4);
+      w1 += __shfl_xor(w1, 2);
+      w1 += __shfl_xor(w1, 1);
+      const int idx = (b5 ? 1 : 0) + (b4 ? 2 : 0) + (b3 ? 4 : 0);  // the sum this lane holds
+      const int64_t i = i0 + (idx & 3) * stride;
+      if (i < I) {
+        if (idx < 4) {
+          m2 = nmax(m2, w1);
+          if ((lane & 7) == 0) Bi[i] = w1;
+        } else {
+          const float dq = sqrtf(w1);
+          m3 = nmax(m3, dq);
+          if ((lane & 7) == 0) Di[i] = dq;
         }
       }
     }
@@ -219,11 +242,18 @@ __global__ __launch_bounds__(256) void cert_scales_kernel(const float* __restric
     mW = nmax(mW, w);
     vsum += fabsf(wm[e / h1]) * w;
   }
-  float mrow = 0.f;  // max_j sum_k |W2_jk|
-  for (int j = tid; j < h2; j += 256) {
+  float mrow = 0.f;  // max_j sum_k |W2_jk|: 8 threads a row, strided partials + 3 xor steps
+  for (int j0 = 0; j0 < h2; j0 += 32) {
+    const int j = j0 + (tid >> 3);
     float rs = 0.f;
-    for (int k = 0; k < h1; ++k) rs += fabsf(W2[j * h1 + k]);
+    if (j < h2)
+      for (int k = tid & 7; k < h1; k += 8) rs += fabsf(W2[j * h1 + k]);
+    rs += __shfl_xor(rs, 1);
+    rs += __shfl_xor(rs, 2);
+    rs += __shfl_xor(rs, 4);
     mrow = nmax(mrow, rs);
+  }
+  for (int j = tid; j < h2; j += 256) {
     mwm = nmax(mwm, fabsf(wm[j]));
     mb2 = nmax(mb2, fabsf(b2[j]));
     c0 += fabsf(wm[j]) * fabsf(b2[j]);
@@ -792,6 +822,10 @@ __global__ __launch_bounds__(256) void cert_champion_kernel(const float* __restr
 // (score desc, item asc) top-K.  Candidates sit in NP per-partition segments; a row with a
 // flagged bound, an overflowing segment or fewer than K candidates is queued for the
 // fallback.
+#ifndef RESCORE_ABL  // timing ablations (tools only; wrong results): 1 no top-K, 2 fixed items,
+                     // 4 at most 64 candidates a row
+#define RESCORE_ABL 0
+#endif
 __global__ __launch_bounds__(256, 2) void ncf_rescore_kernel(
     NcfTabs t, int mf, const float* __restrict__ W2, int h1, int h2, const float* __restrict__ b2,
     const float* __restrict__ wm, const float* __restrict__ bp, int64_t B,
@@ -823,7 +857,11 @@ __global__ __launch_bounds__(256, 2) void ncf_rescore_kernel(
   }
   __syncthreads();
   if (!live) return;
+#if RESCORE_ABL & 4
+  const int n = std::min(hnm_readlane_i(incl, 63), 64);
+#else
   const int n = hnm_readlane_i(incl, 63);
+#endif
   const bool over = __ballot(c > capp) != 0;
   // fewer than K candidates: the row's bound came from another item shard (short_ok: the
   // merge across shards completes the list) or the threshold is unusable -> fallback
@@ -864,6 +902,8 @@ __global__ __launch_bounds__(256, 2) void ncf_rescore_kernel(
   const float bpv = bp[0];
   WaveTopK<1> L;
   L.init();
+  float abl_sink = 0.f;
+  (void)abl_sink;
   const int32_t* rowbuf = buf + b * (int64_t)NP * capp;
   for (int c0 = 0; c0 < n; c0 += 32) {
     const int g = c0 + j;
@@ -878,6 +918,9 @@ __global__ __launch_bounds__(256, 2) void ncf_rescore_kernel(
       }
       item = rowbuf[(int64_t)lo * capp + (g - pref[wave][lo])];
     }
+#if RESCORE_ABL & 2
+    item = j;
+#endif
     // GMF: fma chain in the f32 MFMA's order (k = 2s, then 2s + 1) over all 64 k (zero
     // beyond mf, as the fp32 kernel's padded operands); loads in two batches of 8 float4
     // issued together (a runtime-bounded loop would wait on each load)
@@ -917,8 +960,15 @@ __global__ __launch_bounds__(256, 2) void ncf_rescore_kernel(
     const float mlp = (m4[0] + m4[1]) + (m4[2] + m4[3]);
     const float tot = hnm_sum_halves(mlp + (h == 0 ? gm : 0.f));
     const float score = tot + bpv;
+#if RESCORE_ABL & 1
+    abl_sink = fmaxf(abl_sink, score);
+#else
     L.offer(score, item, ok && h == 0, K);
+#endif
   }
+#if RESCORE_ABL & 1
+  if (abl_sink == 1234.5f) oi[b * K] = 0;
+#endif
   L.store(ov ? ov + b * K : nullptr, oi + b * K, K);
 }
 
