@@ -808,6 +808,9 @@ struct WdScanArgs {
 
 #define WDC_THRESH 0
 #define WDC_DEBUG 1
+#ifndef WDC_VPM
+#define WDC_VPM 4  // VALU instructions scheduled per MFMA in the k loop's interleave
+#endif
 #ifndef WDC_G2
 #define WDC_G2 4  // layer-2 row blocks per pass over k (the x operands are formed once per pass)
 #endif
@@ -1047,7 +1050,7 @@ __global__ __launch_bounds__(256, UPW == 1 ? 2 : 1) void wdc_scan_kernel(WdScanA
 #pragma unroll
           for (int i = 0; i < WD_SPLIT_PASSES * G2 * UPW; ++i) {
             __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-            __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);
+            __builtin_amdgcn_sched_group_barrier(0x002, WDC_VPM, 0);
           }
         }
       };
