@@ -357,6 +357,26 @@ def test_lightgcn_propagate_for_equals_forward(alpha, d):
         m.propagate_for(torch.tensor([U]))
 
 
+def test_lightgcn_propagation_on_other_streams_bitwise():
+    """The SpMM forks its heavy rows onto the ctx's side stream and joins back: forward() on
+    a non-default torch stream, and again on the default one after it, returns the default
+    stream's tables bit for bit (full H&M graph: the segmented heavy-row path is live)."""
+    U, I, E = syn.HM_USERS, syn.HM_ITEMS, syn.HM_INTERACTIONS
+    m = LightGCN(U, I, 64)
+    m.set_graph(torch.from_numpy(syn.bipartite_edge_index(U, I, E, seed=2)))
+    m = to_module(m, syn.lightgcn_state_dict(U, I, 64, seed=0))
+    fu, fi = m.forward()
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        fu2, fi2 = m.forward()
+    torch.cuda.current_stream().wait_stream(side)
+    fu3, fi3 = m.forward()
+    torch.cuda.synchronize()
+    assert torch.equal(fu2, fu) and torch.equal(fi2, fi)
+    assert torch.equal(fu3, fu) and torch.equal(fi3, fi)
+
+
 def test_widedeep_item_features_pair_golden():
     """WideDeep.forward with user AND item features (wide_deep.py:190-195, 214-217) vs the
     reference's own outputs."""
