@@ -835,11 +835,16 @@ __global__ __launch_bounds__(256, 2) void ncf_rescore_kernel(
     unsigned long long* __restrict__ stats) {
   constexpr int KS = 32;
   __shared__ __attribute__((aligned(16))) float wgs[4][64];
+  __shared__ __attribute__((aligned(16))) float b2l[32], wml[32];  // 0 beyond h2
   __shared__ int pref[4][CERT_MAX_NP + 1];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5, j = lane & 31;
   const int64_t b = (int64_t)blockIdx.x * 4 + wave;
   const bool live = b < B;
   int c = 0;
+  if (tid < 32) {
+    b2l[tid] = tid < h2 ? b2[tid] : 0.f;
+    wml[tid] = tid < h2 ? wm[tid] : 0.f;
+  }
   if (live) {
     wgs[wave][lane] = t.WGu[b * 64 + lane];  // pair-permuted wp*g_u
     c = lane < NP ? cnt[b * NP + lane] : 0;
@@ -885,14 +890,6 @@ __global__ __launch_bounds__(256, 2) void ncf_rescore_kernel(
     const int k = 2 * s + h;
     a[s] = (j < h2 && k < h1) ? W2[j * h1 + k] : 0.f;
   }
-  f32x16 b2acc;
-  float wmr[16];
-#pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const int i = mfma32_row(r, h);
-    b2acc[r] = i < h2 ? b2[i] : 0.f;
-    wmr[r] = i < h2 ? wm[i] : 0.f;
-  }
   float p[KS];
 #pragma unroll
   for (int s4 = 0; s4 < KS / 4; ++s4) {
@@ -905,19 +902,28 @@ __global__ __launch_bounds__(256, 2) void ncf_rescore_kernel(
   float abl_sink = 0.f;
   (void)abl_sink;
   const int32_t* rowbuf = buf + b * (int64_t)NP * capp;
-  for (int c0 = 0; c0 < n; c0 += 32) {
-    const int g = c0 + j;
-    const bool ok = g < n;
-    int item = 0;
-    if (ok) {  // segment of candidate g: last p with pref[p] <= g
+  // candidate g's item (0 past the row's n): segment = last p with pref[p] <= g
+  auto cand = [&](int g) {
+    int it = 0;
+    if (g < n) {
       int lo = 0, hi = NP;
       while (hi - lo > 1) {
         const int mid = (lo + hi) >> 1;
         if (pref[wave][mid] <= g) lo = mid;
         else hi = mid;
       }
-      item = rowbuf[(int64_t)lo * capp + (g - pref[wave][lo])];
+      it = rowbuf[(int64_t)lo * capp + (g - pref[wave][lo])];
     }
+    return it;
+  };
+  // the next chunk's candidate id is loaded while this chunk is scored (one dependent
+  // round trip less per chunk); b2 / wm come from LDS (16 + 16 VGPRs freed)
+  int item_next = cand(j);
+  for (int c0 = 0; c0 < n; c0 += 32) {
+    const int g = c0 + j;
+    const bool ok = g < n;
+    int item = item_next;
+    item_next = cand(g + 32);
 #if RESCORE_ABL & 2
     item = j;
 #endif
@@ -951,7 +957,15 @@ __global__ __launch_bounds__(256, 2) void ncf_rescore_kernel(
       const float4 v = *reinterpret_cast<const float4*>(qrow + 4 * s4);
       q[4 * s4] = v.x; q[4 * s4 + 1] = v.y; q[4 * s4 + 2] = v.z; q[4 * s4 + 3] = v.w;
     }
-    f32x16 acc = b2acc;
+    f32x16 acc;
+    float wmr[16];
+#pragma unroll
+    for (int r4 = 0; r4 < 4; ++r4) {  // rows mfma32_row(4 r4 + e, h) = 8 r4 + 4 h + e
+      const float4 bb = *reinterpret_cast<const float4*>(&b2l[8 * r4 + 4 * h]);
+      const float4 ww = *reinterpret_cast<const float4*>(&wml[8 * r4 + 4 * h]);
+      acc[4 * r4] = bb.x; acc[4 * r4 + 1] = bb.y; acc[4 * r4 + 2] = bb.z; acc[4 * r4 + 3] = bb.w;
+      wmr[4 * r4] = ww.x; wmr[4 * r4 + 1] = ww.y; wmr[4 * r4 + 2] = ww.z; wmr[4 * r4 + 3] = ww.w;
+    }
 #pragma unroll
     for (int s = 0; s < KS; ++s) acc = mfma32x32x2(a[s], fmaxf(p[s] + q[s], 0.f), acc);
     float m4[4] = {0.f, 0.f, 0.f, 0.f};
@@ -1161,10 +1175,12 @@ hnm_status ncf_cert_begin(hnm_ctx* ctx, const hnm_ncf_weights* w, const NcfTabs&
   c.sidx = x.sidx;
   c.dense = x.cdense;
   c.ldo = sh.nch;
-  const Partition pc = scan_partition(sh.nch, ublocks, ctx->num_cus, wg);
-  c.ipp = pc.ipp;
-  c.NP = pc.np;
-  launch_scan<SCAN_SAMPLE>(ctx, dim3((unsigned)pc.np, (unsigned)ublocks), c);
+  // as many partitions as one round of workgroups holds (the main scan's >= 4-tile,
+  // multiple-of-8 partitions would leave a third of the slots idle on 2,048 champions)
+  const int64_t npc = std::max<int64_t>(1, (int64_t)wg * ctx->num_cus / ublocks);
+  c.ipp = hnm_cdiv(hnm_cdiv(sh.nch, npc), TILE) * TILE;
+  c.NP = (int)hnm_cdiv(sh.nch, c.ipp);
+  launch_scan<SCAN_SAMPLE>(ctx, dim3((unsigned)c.NP, (unsigned)ublocks), c);
   HNM_LAUNCH_CHECK();
   st = hnm_sample_kth(ctx, x.cdense, sh.nch, B, sh.nch, mptr, midx, K, 1, 1, x.sidx, x.kthv);
   if (st) return st;
