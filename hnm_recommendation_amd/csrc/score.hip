@@ -392,6 +392,19 @@ __global__ __launch_bounds__(256) void sample_kth_kernel(const float* __restrict
     mend = mptr[b + 1];
     nm = mpos < mend ? midx[mpos] : INT_BIG;
   }
+  // column -> item (increasing in the column), matched against the row's sorted mask
+  auto item_of = [&](int64_t c) { return sidx ? (int64_t)sidx[c] : (c / grp) * period + c % grp; };
+  auto insert = [&](float x) {  // into the lane's sorted top-4
+    nan |= x != x;
+    if (x > t3) {
+      const float a = fminf(x, t2), c2 = fmaxf(x, t2);
+      t3 = a;
+      t2 = fminf(c2, t1);
+      const float c1 = fmaxf(c2, t1);
+      t1 = fminf(c1, t0);
+      t0 = fmaxf(c1, t0);
+    }
+  };
   const float* row = s + b * ld;
   for (int64_t base = 0; base < Ns; base += 256) {  // 4 loads per lane in flight
     float v[4];
@@ -404,8 +417,6 @@ __global__ __launch_bounds__(256) void sample_kth_kernel(const float* __restrict
     for (int q = 0; q < 4; ++q) {
       const int64_t cb = base + 64 * q;
       if (mptr && cb < Ns) {
-        // column -> item (increasing in the column), matched against the row's sorted mask
-        auto item_of = [&](int64_t c) { return sidx ? (int64_t)sidx[c] : (c / grp) * period + c % grp; };
         const int64_t c = std::min<int64_t>(cb + lane, Ns - 1);
         const int64_t cl = std::min<int64_t>(cb + 64, Ns) - 1;
         const int64_t it = item_of(c), end = item_of(cl) + 1;  // real ids < end
@@ -415,24 +426,27 @@ __global__ __launch_bounds__(256) void sample_kth_kernel(const float* __restrict
           nm = mpos < mend ? midx[mpos] : INT_BIG;
         }
       }
-      nan |= v[q] != v[q];
-      if (v[q] > t3) {  // insert into the lane's sorted top-4
-        const float a = fminf(v[q], t2), c2 = fmaxf(v[q], t2);
-        t3 = a;
-        t2 = fminf(c2, t1);
-        const float c1 = fmaxf(c2, t1);
-        t1 = fminf(c1, t0);
-        t0 = fmaxf(c1, t0);
-      }
+      insert(v[q]);
     }
   }
-  WaveTopK<1> L;
-  L.init();
-  L.offer(t0, lane, true, K);
-  L.offer(t1, 64 + lane, true, K);
-  L.offer(t2, 128 + lane, true, K);
-  L.offer(t3, 192 + lane, true, K);
-  const float kv = hnm_readlane_f(L.v[0], K - 1);
+  // K-th largest of the 64 x 4 survivors (a multiset: the value is unique whatever the tie
+  // order): K rounds of popping the wave maximum off its lane's sorted list (NaN never
+  // enters a list; -inf once the survivors run out)
+  float kv = -__builtin_inff();
+  for (int r = 0; r < K; ++r) {
+    float m = t0;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+    kv = m;
+    if (m == -__builtin_inff()) break;  // wave-uniform
+    const int w = __builtin_ctzll(__ballot(t0 == m));
+    if (lane == w) {
+      t0 = t1;
+      t1 = t2;
+      t2 = t3;
+      t3 = -__builtin_inff();
+    }
+  }
   if (lane == 0) out[b * K + (K - 1)] = __ballot(nan) ? __builtin_nanf("") : kv;
 }
 
