@@ -157,3 +157,39 @@ def test_lightgcn128_full_shape_two_rank_sharding(tmp_path):
         assert_topk_equivalent(i, dense, K, what=f"lightgcn128 sharded rank {r} vs CPU ref")
         np.testing.assert_allclose(v, np.take_along_axis(dense, i, 1), rtol=1e-4,
                                    atol=1e-4 * float(np.abs(dense).max()))
+
+
+# ------------------------------------------------------------------ N = 8 per-rank shape
+# What one rank runs in the driver's 8-GPU scaling bench (bench.py --gpus 8, NCF default):
+# the all-gathered 8 x 4,096 users against its 1/8 item shard of the full catalogue.  One
+# process, no collective: the two-phase call with the rank's own bounds (an all_reduce(MAX)
+# over 8 ranks only raises them) and the one-shot call must both equal the exact fp32 scan
+# of the shard bit for bit, with no fallback rows.
+def test_ncf_eight_way_rank_shape_certified_equals_exact():
+    from hnm_recommendation_amd import _lib
+    UU, II, world, rank = 200_000, syn.HM_ITEMS, 8, 7
+    sd = syn.ncf_state_dict(UU, II, 64, (128, 64, 32), seed=0)
+    m = NeuralCF(UU, II)
+    m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in sd.items()})
+    m = m.to("cuda:0").eval()
+    lo, hi = S.shard_range(II, rank, world)
+    users = torch.from_numpy(syn.user_batch(UU, world * 4096, seed=81)).cuda()
+    sc = S.ncf_shard_topk(m, lo, hi, K)
+    _lib.set_prefilter(users.device, False)
+    try:
+        ev, ei = sc(users)
+    finally:
+        _lib.set_prefilter(users.device, True)
+    _lib.prefilter_stats(users.device, reset=True)
+    _lib.set_option(users.device, _lib.HNM_OPT_STATS, 1)
+    v1, i1 = sc(users)
+    lb = sc.begin(users)
+    v2, i2 = sc.finish(users, lb)
+    _lib.set_option(users.device, _lib.HNM_OPT_STATS, 0)
+    rows, cands, fallback = _lib.prefilter_stats(users.device, reset=True)
+    print(f"rank shape {users.numel()} x {hi - lo}: candidates/row "
+          f"{cands / max(rows - fallback, 1):.1f}, fallback rows {fallback} of {rows}")
+    assert fallback == 0
+    for v, i in ((v1, i1), (v2, i2)):
+        assert torch.equal(i, ei)
+        assert torch.equal(v.view(torch.int32), ev.view(torch.int32))
