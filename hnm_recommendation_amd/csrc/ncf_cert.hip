@@ -406,6 +406,7 @@ struct ScanArgs {
   const int32_t* sidx;  // SAMPLE: scanned item n is item sidx[n] (gather map), if set
   int64_t ipp;
   int NP;
+  int upw;  // users per wave (32; fewer for the 8-row proxy pass: every wave gets a pair)
   const int64_t* mptr;
   const int32_t* midx;
   const float* tau;  // [B] scaled thresholds (THRESH)
@@ -454,9 +455,10 @@ __global__ __launch_bounds__(256, HNM_SCAN_OCC) void ncf16_scan_kernel(ScanArgs 
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // uniform: scalar loop state
   // grid: x = item partition (NP a multiple of 8), y = user block -> the round-robin
   // workgroup -> XCD placement keeps partition p on XCD p % 8 (its tiles stay in that L2)
-  const int64_t ublk = (int64_t)blockIdx.y * NU;
-  const int64_t u0 = ublk + wave * 32;
-  const int nu = (int)std::max<int64_t>(0, std::min<int64_t>(32, A.B - u0));
+  const int upw = A.upw;  // <= 32 (NU / 4)
+  const int64_t ublk = (int64_t)blockIdx.y * 4 * upw;
+  const int64_t u0 = ublk + wave * upw;
+  const int nu = (int)std::max<int64_t>(0, std::min<int64_t>(upw, A.B - u0));
   const int p = blockIdx.x;
   const int64_t part_start = (int64_t)p * A.ipp;
   const int64_t part_end = std::min<int64_t>(A.I, part_start + A.ipp);
@@ -632,7 +634,7 @@ __global__ __launch_bounds__(256, HNM_SCAN_OCC) void ncf16_scan_kernel(ScanArgs 
       }
     }
 
-    const _Float16* pw = &ps[(wave * 32) * 64 + 8 * h];  // user r, k-step s: pw[r * 64 + 16 s]
+    const _Float16* pw = &ps[(wave * upw) * 64 + 8 * h];  // user r, k-step s: pw[r * 64 + 16 s]
     for (int u = 0; u < nu; u += 2) {
       // user b = u + 1 even past nu (zero P~ rows; FOLD: folded term -inf / not stored)
       const int ua = u, ub = u + 1;
@@ -1122,6 +1124,7 @@ ScanArgs scan_args(const CertWs& x, int64_t B) {
   a.prm = x.prm;
   a.B = B;
   a.sidx = nullptr;
+  a.upw = 32;
   return a;
 }
 
@@ -1165,6 +1168,7 @@ hnm_status ncf_cert_begin(hnm_ctx* ctx, const hnm_ncf_weights* w, const NcfTabs&
   const int64_t np = std::min<int64_t>(3 * (int64_t)ctx->num_cus, hnm_cdiv(I, 4 * TILE));
   a.ipp = hnm_cdiv(hnm_cdiv(I, np), TILE) * TILE;
   a.NP = (int)hnm_cdiv(I, a.ipp);
+  a.upw = 2;  // the <= 8 proxy rows as one user pair per wave (4x shorter per tile than one wave)
   launch_scan<SCAN_SAMPLE>(ctx, dim3((unsigned)a.NP, 1), a);
   HNM_LAUNCH_CHECK();
   hipLaunchKernelGGL(cert_champion_kernel, dim3((unsigned)hnm_cdiv(sh.nch, 4)), dim3(256), 0,
