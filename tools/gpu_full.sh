@@ -26,7 +26,7 @@ HNM_DIST_BACKEND=gloo step bench_2rank 400 python bench.py --gpus 2 --workload l
 if [ -n "$PROF" ]; then
   cd /tmp && export TMPDIR=/tmp
   for w in ncf lightgcn widedeep mf; do
-    extra="--steps 5 --warmup 2"
+    extra=""  # the bench defaults, so the averages match the bench line's HIP-event timing
     [ $w = widedeep ] && extra="--steps 3 --warmup 1"
     echo "== prof $w $(date +%T)"
     timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_$w" -o $w -- \
