@@ -828,7 +828,7 @@ __global__ __launch_bounds__(256) void cert_champion_kernel(const float* __restr
                      // 4 at most 64 candidates a row
 #define RESCORE_ABL 0
 #endif
-__global__ __launch_bounds__(256, 2) void ncf_rescore_kernel(
+__global__ __launch_bounds__(256, 3) void ncf_rescore_kernel(
     NcfTabs t, int mf, const float* __restrict__ W2, int h1, int h2, const float* __restrict__ b2,
     const float* __restrict__ wm, const float* __restrict__ bp, int64_t B,
     const int* __restrict__ flag, const int* __restrict__ cnt, const int32_t* __restrict__ buf,
@@ -839,6 +839,11 @@ __global__ __launch_bounds__(256, 2) void ncf_rescore_kernel(
   __shared__ __attribute__((aligned(16))) float wgs[4][64];
   __shared__ __attribute__((aligned(16))) float b2l[32], wml[32];  // 0 beyond h2
   __shared__ int pref[4][CERT_MAX_NP + 1];
+  // the layer-2 MFMA operands that do not change along a row -- W2 fragments (k step s, lane)
+  // and the user's P row -- come from LDS (a broadcast read per MFMA) instead of 64 VGPRs, so
+  // three waves per SIMD fit without spills
+  __shared__ float w2l[KS * 64];
+  __shared__ __attribute__((aligned(16))) float pl[4][64];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5, j = lane & 31;
   const int64_t b = (int64_t)blockIdx.x * 4 + wave;
   const bool live = b < B;
@@ -847,8 +852,13 @@ __global__ __launch_bounds__(256, 2) void ncf_rescore_kernel(
     b2l[tid] = tid < h2 ? b2[tid] : 0.f;
     wml[tid] = tid < h2 ? wm[tid] : 0.f;
   }
+  for (int e = tid; e < KS * 64; e += 256) {
+    const int s = e >> 6, jj = e & 31, k = 2 * s + ((e >> 5) & 1);
+    w2l[e] = (jj < h2 && k < h1) ? W2[jj * h1 + k] : 0.f;
+  }
   if (live) {
     wgs[wave][lane] = t.WGu[b * 64 + lane];  // pair-permuted wp*g_u
+    pl[wave][lane] = t.Pu[b * 64 + lane];
     c = lane < NP ? cnt[b * NP + lane] : 0;
   }
   // inclusive scan of the segment counts over the lanes
@@ -885,18 +895,6 @@ __global__ __launch_bounds__(256, 2) void ncf_rescore_kernel(
   if (stats && lane == 0) {
     atomicAdd(&stats[1], (unsigned long long)n);
     if (b == 0) atomicAdd(&stats[0], (unsigned long long)B);
-  }
-  float a[KS];
-#pragma unroll
-  for (int s = 0; s < KS; ++s) {
-    const int k = 2 * s + h;
-    a[s] = (j < h2 && k < h1) ? W2[j * h1 + k] : 0.f;
-  }
-  float p[KS];
-#pragma unroll
-  for (int s4 = 0; s4 < KS / 4; ++s4) {
-    const float4 v = *reinterpret_cast<const float4*>(t.Pu + b * 64 + h * KS + 4 * s4);
-    p[4 * s4] = v.x; p[4 * s4 + 1] = v.y; p[4 * s4 + 2] = v.z; p[4 * s4 + 3] = v.w;
   }
   const float bpv = bp[0];
   WaveTopK<1> L;
@@ -969,7 +967,16 @@ __global__ __launch_bounds__(256, 2) void ncf_rescore_kernel(
       wmr[4 * r4] = ww.x; wmr[4 * r4 + 1] = ww.y; wmr[4 * r4 + 2] = ww.z; wmr[4 * r4 + 3] = ww.w;
     }
 #pragma unroll
-    for (int s = 0; s < KS; ++s) acc = mfma32x32x2(a[s], fmaxf(p[s] + q[s], 0.f), acc);
+    for (int s = 0; s < KS; ++s) {
+      // both reads issued right before their MFMA (hoisted by the compiler, they would hold
+      // 64 VGPRs again and spill); LDS byte offsets are the low 32 bits of the generic address
+      float w2v, pv;
+      asm volatile("ds_read_b32 %0, %2\n\tds_read_b32 %1, %3\n\ts_waitcnt lgkmcnt(0)"
+                   : "=&v"(w2v), "=&v"(pv)
+                   : "v"((unsigned)(uintptr_t)&w2l[s * 64 + lane]),
+                     "v"((unsigned)(uintptr_t)&pl[wave][h * KS + s]));
+      acc = mfma32x32x2(w2v, fmaxf(pv + q[s], 0.f), acc);
+    }
     float m4[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int r = 0; r < 16; ++r) m4[r & 3] = fmaf(fmaxf(acc[r], 0.f), wmr[r], m4[r & 3]);
