@@ -604,7 +604,7 @@ __global__ __launch_bounds__(256) void dcert_tau_kernel(const float* __restrict_
 // (k = 0 .. DP-1, zero padding included) the f32 MFMA computes, then (acc + ub) + ib as
 // dot_score_kernel does; exact (score desc, item asc) top-K.
 template <int DP, bool BIAS>
-__global__ __launch_bounds__(256) void dcert_rescore_kernel(
+__global__ __launch_bounds__(256, 4) void dcert_rescore_kernel(
     DotArgs a, const float* __restrict__ ubr, const int* __restrict__ flag,
     const int* __restrict__ cnt, const int32_t* __restrict__ buf, int NP, int capp, int K,
     int short_ok, float* __restrict__ ov, int64_t* __restrict__ oi, int32_t* __restrict__ ovf_rows,
@@ -664,21 +664,21 @@ __global__ __launch_bounds__(256) void dcert_rescore_kernel(
   // Rounds of 128 slots: slots 0..K-1 carry the running top-K, slots K..127 take the next
   // candidates; one bitonic sort per round (no serial list inserts).
   auto score = [&](int it) -> float {
-    // 64 dims = 16 float4 loads issued together (addresses clamped in range, zero padding by
-    // select); groups of 64 run one after another
+    // 32 dims = 8 float4 loads issued together (addresses clamped in range, zero padding by
+    // select); groups of 32 run one after another (32 VGPRs of row data: four waves per SIMD)
     const float* r0 = a.it + (int64_t)it * a.ldi;
     float acc = 0.f;
 #pragma unroll 1
-    for (int g = 0; g < DP / 64; ++g) {
-      float4 v[16];
+    for (int g = 0; g < DP / 32; ++g) {
+      float4 v[8];
 #pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        const int k = 64 * g + 4 * q;
+      for (int q = 0; q < 8; ++q) {
+        const int k = 32 * g + 4 * q;
         v[q] = *reinterpret_cast<const float4*>(r0 + std::min(k, a.d - 4));
       }
 #pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        const int k = 64 * g + 4 * q;
+      for (int q = 0; q < 8; ++q) {
+        const int k = 32 * g + 4 * q;
         const bool in = k < a.d;
         const float4 uv = *reinterpret_cast<const float4*>(&urow[wave][k]);
         acc = fmaf(uv.x, in ? v[q].x : 0.f, acc);
