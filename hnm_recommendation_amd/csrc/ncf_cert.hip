@@ -969,12 +969,13 @@ __global__ __launch_bounds__(256, 3) void ncf_rescore_kernel(
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
       // both reads issued right before their MFMA (hoisted by the compiler, they would hold
-      // 64 VGPRs again and spill); LDS byte offsets are the low 32 bits of the generic address
+      // 64 VGPRs again and spill); operands are LDS byte offsets (address-space-3 pointers)
+      typedef __attribute__((address_space(3))) const float* lds_ptr;
       float w2v, pv;
       asm volatile("ds_read_b32 %0, %2\n\tds_read_b32 %1, %3\n\ts_waitcnt lgkmcnt(0)"
                    : "=&v"(w2v), "=&v"(pv)
-                   : "v"((unsigned)(uintptr_t)&w2l[s * 64 + lane]),
-                     "v"((unsigned)(uintptr_t)&pl[wave][h * KS + s]));
+                   : "v"((unsigned)(uintptr_t)(lds_ptr)&w2l[s * 64 + lane]),
+                     "v"((unsigned)(uintptr_t)(lds_ptr)&pl[wave][h * KS + s]));
       acc = mfma32x32x2(w2v, fmaxf(pv + q[s], 0.f), acc);
     }
     float m4[4] = {0.f, 0.f, 0.f, 0.f};
