@@ -175,3 +175,12 @@ def test_lightning_checkpoint_fixture_loads_like_serve_py():
     assert srv.model_metrics["neural_cf"]["test_map"] == pytest.approx(0.0123)
     assert type(srv.models["lightgcn"]).__name__ == "LightGCN"
     assert srv.models["lightgcn"].embedding_dim == 16
+
+
+def test_build_tracks_every_csrc_header():
+    """Incremental builds rebuild every object when any csrc header changes (a header left
+    out of build.HEADERS once left stale objects calling an old signature)."""
+    import glob
+    from hnm_recommendation_amd import build
+    hdrs = {os.path.basename(p) for p in glob.glob(os.path.join(build.CSRC, "*.h"))}
+    assert hdrs <= set(build.HEADERS), sorted(hdrs - set(build.HEADERS))
