@@ -41,7 +41,7 @@ import torch.distributed as dist
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
-from hnm_recommendation_amd import LightGCN, MatrixFactorization, NeuralCF, WideDeep  # noqa: E402
+from hnm_recommendation_amd import LightGCN, MatrixFactorization, NeuralCF, UserHistory, WideDeep  # noqa: E402
 from hnm_recommendation_amd import _lib  # noqa: E402
 from hnm_recommendation_amd import sharding as S  # noqa: E402
 from hnm_recommendation_amd import synthetic as syn  # noqa: E402
@@ -109,15 +109,19 @@ def build_workload(name, rank, world, device, batch, exact=False, weights="init"
     """Returns (step_fn(users) -> (vals, idx), flops_or_bytes_per_launch, bound, info)."""
     U, I = syn.HM_USERS, syn.HM_ITEMS
     lo, hi = S.shard_range(I, rank, world)
+    info = {}
     if name == "ncf":
         kw = dict(bias_scale=0.05, emb_scale=20.0) if weights == "personal" else {}
         sd = syn.ncf_state_dict(U, I, 64, (128, 64, 32), seed=0, **kw)
         m = load(NeuralCF(U, I), sd, device)
         local = S.ncf_shard_topk(m, lo, hi, K)
+        info["_filtered"] = lambda hist: S.ItemShardedRecommender(
+            S.ncf_shard_topk(m, lo, hi, K, hist), S.hip_merge, K, lo, rank, world).recommend
+        info["_module"] = m
         per_launch = 4352.0 * batch * world * (hi - lo)   # SURVEY §8(d): 4,352 FLOP / pair
-        info = {"model": "NeuralCF", "mf_dim": 64, "mlp_dims": [128, 64, 32], "weights": weights,
-                "scan": "exact fp32" if exact else
-                        "certified f16 pre-filter + exact fp32 re-scoring (ncf_cert.hip)"}
+        info.update({"model": "NeuralCF", "mf_dim": 64, "mlp_dims": [128, 64, 32], "weights": weights,
+                     "scan": "exact fp32" if exact else
+                             "certified f16 pre-filter + exact fp32 re-scoring (ncf_cert.hip)"})
         bound, kernel = "mfma", ("ncf32_kernel" if exact else "ncf16_scan_kernel")
         cpu = ("ncf", sd)
     elif name in ("lightgcn", "lightgcn128"):
@@ -144,11 +148,14 @@ def build_workload(name, rank, world, device, batch, exact=False, weights="init"
         # X read once, Y written once, item-row accumulators read + written (layers 1..L-1;
         # the restricted last layer is not timed)
         per_launch = g.nnz * 8.0 + (N + 1) * 8.0 + 2.0 * N * d * 4 + 2.0 * I * d * 4
-        info = {"model": "LightGCN", "embedding_dim": d, "num_layers": 3,
+        info["_filtered"] = lambda hist: S.ItemShardedRecommender(
+            S.lightgcn_shard_topk(m, lo, hi, K, hist), S.hip_merge, K, lo, rank, world).recommend
+        info["_module"] = m
+        info.update({"model": "LightGCN", "embedding_dim": d, "num_layers": 3,
                 "interactions": syn.HM_INTERACTIONS, "nnz_with_self_loops": g.nnz,
                 "step": "3-layer propagation restricted to what recommend() reads (layers 1-2 "
                         "whole graph, layer 3 on item rows + the step's users; outputs "
-                        "identical to forward()) + certified top-K scan of the batch"}
+                        "identical to forward()) + certified top-K scan of the batch"})
         info["_serving"] = lambda: (lambda F: S.ItemShardedRecommender(
             S.dot_shard_topk(F[:U], F[U:], lo, hi, K), S.hip_merge, K, lo, rank,
             world).recommend)(m.propagate(g))
@@ -162,7 +169,7 @@ def build_workload(name, rank, world, device, batch, exact=False, weights="init"
         m = load(WideDeep(U, I), sd, device)
         local = S.widedeep_shard_topk(m, lo, hi, K)
         per_launch = 328450.0 * batch * world * (hi - lo)   # 328,450 FLOP / pair
-        info = {"model": "WideDeep", "embedding_dim": 64, "deep_layers": [512, 256, 128]}
+        info.update({"model": "WideDeep", "embedding_dim": 64, "deep_layers": [512, 256, 128]})
         bound, kernel = "mfma", ("widedeep_score_kernel" if exact else "wdc_scan_kernel")
         info["scan"] = ("exact fp32" if exact else
                         "certified split-f16 (layer 2: 2 f16 MFMA passes, layer 3: 1; weight / activation residuals bounded) pre-filter + exact fp32 re-scoring")
@@ -173,7 +180,8 @@ def build_workload(name, rank, world, device, batch, exact=False, weights="init"
         local = S.dot_shard_topk(m.user_embeddings.weight.detach(), m.item_embeddings.weight.detach(),
                                  lo, hi, K)
         per_launch = 2.0 * 64 * batch * world * (hi - lo)
-        info = {"model": "MatrixFactorization", "embedding_dim": 64}
+        info["_module"] = m
+        info.update({"model": "MatrixFactorization", "embedding_dim": 64})
         bound, kernel = "mfma", ("dot_score_kernel" if exact else "dot16_scan_kernel")
         cpu = ("mf", sd)
     else:
@@ -182,6 +190,28 @@ def build_workload(name, rank, world, device, batch, exact=False, weights="init"
     ret = dict(step=rec.recommend, per_launch=per_launch, bound=bound, kernel=kernel,
                timing=_lib.TIME_SCORE)
     return ret, info, cpu
+
+
+def timed_rate(fn, batches, steps, world, B):
+    """users/s of `steps` calls of fn over the resident batches (one warm call first),
+    bracketed like the headline loop (sync + barrier on both sides, max over ranks)."""
+    fn(batches[0])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for j in range(steps):
+        fn(batches[j % len(batches)])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        on_host = dist.get_backend() == "gloo"
+        t = torch.tensor([el], dtype=torch.float64, device="cpu" if on_host else "cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t[0])
+    return B * world * steps / el
 
 
 def _median_rate(fn, users, runs, budget_s):
@@ -533,6 +563,51 @@ def main():
             "value": round(B * world * exact_rate[1] / exact_rate[0], 2), "unit": "users/s",
             "steps": exact_rate[1],
             "note": "same step with HNM_OPT_PREFILTER=0: every (user, item) pair in exact fp32"}
+    if "_filtered" in info and not args.exact:
+        # purchase-history filter (the reference's filter_items / serve.py:350-352): every
+        # user's history = its interactions in the synthetic H&M transactions (the LightGCN
+        # graph's edges, mean 23.2 items), held on the device as a UserHistory; each step
+        # gathers the batch's rows on the GPU (hnm_mask_gather_csr) and masks them in-kernel
+        tH = time.perf_counter()
+        hu, hi_ = syn.interactions(syn.HM_USERS, syn.HM_ITEMS, syn.HM_INTERACTIONS, seed=2)
+        hist = UserHistory.from_interactions(hu, hi_, syn.HM_USERS, syn.HM_ITEMS, device)
+        del hu, hi_
+        t_hist = time.perf_counter() - tH
+        fstep = info["_filtered"](hist)
+        nf = min(args.steps, 10 if args.workload == "lightgcn128" else 20)
+        rate = timed_rate(fstep, batches, nf, world, B)
+        per_row = float((hist.hist_ptr[batches[0] + 1] - hist.hist_ptr[batches[0]]).float().mean())
+        line["filtered"] = {
+            "value": round(rate, 2), "unit": "users/s", "steps": nf,
+            "vs_unfiltered": round(rate / value, 4),
+            "history_items_per_user": round(per_row, 2),
+            "history": f"device-resident CSR of all {syn.HM_USERS} users' interactions "
+                       f"({hist.nnz} unique items; built once in {t_hist:.1f}s, outside timing)",
+            "note": "same step with each user's purchase history masked (-inf) in-kernel; "
+                    "mask rows gathered on the GPU per step"}
+        if "_module" in info and world == 1:
+            m = info["_module"]
+            host = [b.cpu() for b in batches]
+            ms = {}
+            ms["recommend_with_scores_device_ids"] = timed_rate(
+                lambda u: m.recommend_with_scores(u), batches, nf, world, B)
+            ms["recommend_host_ids"] = timed_rate(
+                lambda j: m.recommend(host[j]), list(range(len(host))), nf, world, B)
+            ms["recommend_with_scores_history_filter"] = timed_rate(
+                lambda u: m.recommend_with_scores(u, filter_items=hist), batches, nf, world, B)
+            out = {k: round(v, 2) for k, v in ms.items()}
+            out["vs_value"] = {k: round(v / value, 4) for k, v in ms.items()}
+            out["note"] = (
+                "the reference's own module surface (model.recommend / recommend_with_scores, what "
+                "serve.py and evaluation call) timed on the same batches: device ids are range-"
+                "checked by the kernels' error word (one stream sync per call, IndexError raised "
+                "at the call); host ids are checked on the host (no sync; includes the 32 KB "
+                "H2D copy of the ids)" + (
+                    "; LightGCN's module caches forward() (propagation once, reused while the "
+                    "weights are unchanged), so these rates exclude the per-call propagation "
+                    "`value` includes" if args.workload.startswith("lightgcn") else ""))
+            line["module_surface"] = out
+        del hist
     if "_full_step" in info:
         full = info["_full_step"]
         full(batches[0])

@@ -5,6 +5,7 @@ as hand-written gfx950 HIP kernels behind the C ABI in include/hnm.h (libhnm_mi3
 exposed through modules that mirror the reference's `src/models` surface.
 """
 from .evaluation import RecommendationMetrics
-from .models import LightGCN, MatrixFactorization, NeuralCF, WideDeep
+from .models import LightGCN, MatrixFactorization, NeuralCF, UserHistory, WideDeep
 
-__all__ = ["NeuralCF", "LightGCN", "WideDeep", "MatrixFactorization", "RecommendationMetrics"]
+__all__ = ["NeuralCF", "LightGCN", "WideDeep", "MatrixFactorization", "RecommendationMetrics",
+           "UserHistory"]

@@ -8,6 +8,7 @@ from __future__ import annotations
 import ctypes as C
 import os
 import threading
+import weakref
 
 import torch
 
@@ -108,13 +109,15 @@ _SIGS = {
                                                _i64, _p]),
     "hnm_widedeep_prefilter_debug_f32": (_i32, [_p, C.POINTER(WideDeepWeights), _p, _i64, _p, _p,
                                                 _i64, _p]),
+    "hnm_mask_gather_csr": (_i32, [_p, _p, _p, _i64, _p, _i64, _i64, _i64, _i64, _p, _p]),
     "hnm_rank_metrics_f64": (_i32, [_p, _p, _i64, _i64, _p, C.c_int, _p, _p, _i64, _p, _p, _p,
                                     _p, _p]),
 }
 
 _lib = None
 _lock = threading.RLock()
-_ctxs: dict = {}
+_tls = threading.local()        # .ctxs: {device index: _Ctx} of the calling thread
+_live = weakref.WeakSet()       # every live _Ctx (all threads), for device-wide options/stats
 
 
 def declared_symbols():
@@ -182,28 +185,68 @@ def _dev_index(device) -> int:
 _opts: dict = {}  # device -> {option: value}, applied to every ctx of that device
 
 
+class _Ctx:
+    """One hnm_ctx, owned by the thread-local slot of the thread that created it: when the
+    thread exits its slot is cleared and the ctx (workspace, side stream, events) destroyed,
+    so a server whose worker threads come and go does not accumulate contexts, and a new
+    thread never inherits a dead thread's ctx (or its open two-phase call)."""
+    __slots__ = ("handle", "device", "__weakref__")
+
+    def __init__(self, device: int):
+        h = _p()
+        check(fn("hnm_ctx_create")(device, C.byref(h)), "hnm_ctx_create")
+        self.handle, self.device = h, device
+
+    def __del__(self):
+        h, self.handle = self.handle, None
+        lib = _lib
+        if h and lib is not None:
+            try:
+                lib.hnm_ctx_destroy(h)  # synchronizes the device before freeing
+            except Exception:
+                pass
+
+
+def _thread_ctx(idx: int) -> "_Ctx":
+    slots = getattr(_tls, "ctxs", None)
+    if slots is None:
+        slots = _tls.ctxs = {}
+    c = slots.get(idx)
+    if c is None:
+        c = _Ctx(idx)
+        with _lock:
+            for opt, val in _opts.get(idx, {}).items():
+                check(fn("hnm_ctx_set_option")(c.handle, int(opt), int(val)), "hnm_ctx_set_option")
+            _live.add(c)
+        slots[idx] = c
+    return c
+
+
+def _device_ctxs(idx: int):
+    with _lock:
+        return [c for c in list(_live) if c.device == idx and c.handle]
+
+
+def live_contexts(device=None) -> int:
+    """Number of live hnm_ctx objects (all threads), optionally on one device."""
+    if device is None:
+        with _lock:
+            return sum(1 for c in list(_live) if c.handle)
+    return len(_device_ctxs(_dev_index(device)))
+
+
 def ctx(device: torch.device):
     """The calling thread's hnm_ctx on `device`, bound to torch's current stream.
 
     One ctx per (device, thread): a ctx owns a workspace and the state of an open two-phase
-    call, so concurrent callers (a threaded server) never share them.  Switching streams
-    is ordered inside the library (hnm_ctx_set_stream queues the new stream behind the old)."""
+    call, so concurrent callers (a threaded server) never share them; it lives as long as
+    its thread.  Switching streams is ordered inside the library (hnm_ctx_set_stream queues
+    the new stream behind the old one)."""
     idx = _dev_index(device)
-    key = (idx, threading.get_ident())
-    c = _ctxs.get(key)
-    if c is None:
-        with _lock:
-            c = _ctxs.get(key)
-            if c is None:
-                h = _p()
-                check(fn("hnm_ctx_create")(idx, C.byref(h)), "hnm_ctx_create")
-                c = h
-                for opt, val in _opts.get(idx, {}).items():
-                    check(fn("hnm_ctx_set_option")(c, int(opt), int(val)), "hnm_ctx_set_option")
-                _ctxs[key] = c
+    c = _thread_ctx(idx)
     stream = torch.cuda.current_stream(idx).cuda_stream
-    check(fn("hnm_ctx_set_stream")(c, _p(stream)), "hnm_ctx_set_stream")
-    return c
+    check(fn("hnm_ctx_set_stream")(c.handle, _p(stream)), "hnm_ctx_set_stream")
+    return c.handle
 
 
 def abort_pending(device):
@@ -212,7 +255,8 @@ def abort_pending(device):
 
 
 def sync_check(device):
-    """Synchronize the ctx stream and raise IndexError if a kernel saw an out-of-range id."""
+    """Synchronize this thread's ctx stream and raise IndexError if one of this thread's
+    calls saw an out-of-range id (per thread: each caller checks its own calls)."""
     check(fn("hnm_ctx_check")(ctx(device)), "hnm_ctx_check")
 
 
@@ -225,7 +269,8 @@ def enable_timing(device, on=True):
 
 
 def kernel_timing(device):
-    """(summed dominant-kernel ms, launches) since enable_timing; syncs the stream."""
+    """(summed dominant-kernel ms, launches) of this thread's calls since enable_timing;
+    syncs the stream (per thread, like enable_timing)."""
     t = C.c_double()
     n = _i64()
     check(fn("hnm_ctx_timing")(ctx(device), C.byref(t), C.byref(n)), "hnm_ctx_timing")
@@ -242,9 +287,8 @@ def set_option(device, option, value):
     ctx(device)  # validates through the library first
     with _lock:
         _opts.setdefault(idx, {})[int(option)] = int(value)
-        handles = [h for (d, _), h in _ctxs.items() if d == idx]
-    for h in handles:
-        check(fn("hnm_ctx_set_option")(h, int(option), int(value)), "hnm_ctx_set_option")
+    for c in _device_ctxs(idx):
+        check(fn("hnm_ctx_set_option")(c.handle, int(option), int(value)), "hnm_ctx_set_option")
 
 
 def set_prefilter(device, on=True):
@@ -253,11 +297,17 @@ def set_prefilter(device, on=True):
 
 
 def prefilter_stats(device, reset=False):
-    """(rows scored, candidates re-scored in fp32, rows that took the exact fallback);
-    counted only while HNM_OPT_STATS is on (set_option(dev, HNM_OPT_STATS, 1))."""
-    out = (_i64 * 3)()
-    check(fn("hnm_ctx_prefilter_stats")(ctx(device), out, int(reset)), "hnm_ctx_prefilter_stats")
-    return tuple(int(v) for v in out)
+    """(rows scored, candidates re-scored in fp32, rows that took the exact fallback) summed
+    over every thread's ctx on `device`; counted only while HNM_OPT_STATS is on
+    (set_option(dev, HNM_OPT_STATS, 1))."""
+    ctx(device)
+    tot = [0, 0, 0]
+    for c in _device_ctxs(_dev_index(device)):
+        out = (_i64 * 3)()
+        check(fn("hnm_ctx_prefilter_stats")(c.handle, out, int(reset)), "hnm_ctx_prefilter_stats")
+        for j in range(3):
+            tot[j] += int(out[j])
+    return tuple(tot)
 
 
 def ptr(t):

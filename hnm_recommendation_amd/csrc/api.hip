@@ -212,6 +212,11 @@ extern "C" hnm_status hnm_ctx_check(hnm_ctx* ctx) {
       hnm_set_error("index out of range in self (an id exceeded the embedding table)");
       return HNM_EOOB;
     }
+    if (h & HNM_ERR_MASK_CAP) {
+      hnm_set_error("hnm_mask_gather_csr: the batch's history ids exceeded the mask capacity "
+                    "(rows were truncated)");
+      return HNM_EINVAL;
+    }
   }
   return HNM_OK;
 }
@@ -551,6 +556,128 @@ extern "C" hnm_status hnm_pair_dot_f32(hnm_ctx* ctx, const float* user_tab, int6
   hipLaunchKernelGGL(pair_dot_kernel, dim3((unsigned)hnm_cdiv(n, 4)), dim3(256), 0, ctx->stream,
                      user_tab, num_users, ldu, item_tab, num_items, ldi, d, user_ids, item_ids, n,
                      user_bias, item_bias, const_bias, out, ctx->err_dev);
+  HNM_LAUNCH_CHECK();
+  return HNM_OK;
+}
+
+// ------------------------------------------------------------------ a11: history mask gather
+// The -inf mask of one recommend() batch from a device-resident per-user history CSR
+// (the purchase-history filter of serve.py:350-352 / each recommend's filter loop,
+// neural_cf.py:316-321): row b masks the ids of hist_idx[hist_ptr[u] .. hist_ptr[u + 1])
+// (sorted) of u = user_ids[b] that fall in the item range [lo, hi), renumbered to i - lo
+// (an item shard's local ids).  Two launches, no host sync: one workgroup scans the B row
+// lengths into mask_ptr (rows of out-of-range users are empty; the scoring kernel flags
+// them), then one wave per row copies its ids (coalesced int32 runs).  Offsets past
+// `capacity` are clamped (the row is truncated, HNM_ERR_MASK_CAP raised) so no reader can
+// run off the buffer.
+__device__ __forceinline__ void hist_run(const int64_t* __restrict__ hist_ptr,
+                                         const int32_t* __restrict__ hist_idx, int64_t u,
+                                         int32_t lo, int32_t hi, bool whole, int64_t& a,
+                                         int64_t& z) {
+  a = hist_ptr[u];
+  z = hist_ptr[u + 1];
+  if (whole) return;
+  int64_t l = a, r = z;  // first position >= lo
+  while (l < r) {
+    const int64_t m = (l + r) >> 1;
+    if (hist_idx[m] < lo) l = m + 1;
+    else r = m;
+  }
+  int64_t l2 = l, r2 = z;  // first position >= hi
+  while (l2 < r2) {
+    const int64_t m = (l2 + r2) >> 1;
+    if (hist_idx[m] < hi) l2 = m + 1;
+    else r2 = m;
+  }
+  a = l;
+  z = l2;
+}
+
+__global__ __launch_bounds__(1024) void mask_scan_kernel(const int64_t* __restrict__ hist_ptr,
+                                                         const int32_t* __restrict__ hist_idx,
+                                                         int64_t num_users,
+                                                         const int64_t* __restrict__ uid,
+                                                         int64_t B, int32_t lo, int32_t hi,
+                                                         bool whole, int64_t capacity,
+                                                         int64_t* __restrict__ mptr,
+                                                         unsigned* err) {
+  __shared__ int64_t wsum[16];
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int64_t per = hnm_cdiv(B, 1024);
+  const int64_t b0 = (int64_t)t * per, b1 = b0 + per < B ? b0 + per : B;
+  int64_t mine = 0;
+  for (int64_t b = b0; b < b1; ++b) {
+    const int64_t u = uid[b];
+    if (u < 0 || u >= num_users) continue;
+    int64_t a, z;
+    hist_run(hist_ptr, hist_idx, u, lo, hi, whole, a, z);
+    mine += z - a;
+  }
+  // inclusive wave scan, then the 16 wave totals
+  int64_t inc = mine;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int64_t v = __shfl_up(inc, o);
+    if (lane >= o) inc += v;
+  }
+  if (lane == 63) wsum[wv] = inc;
+  __syncthreads();
+  int64_t base = 0;
+  for (int w = 0; w < wv; ++w) base += wsum[w];
+  int64_t off = base + inc - mine;
+  for (int64_t b = b0; b < b1; ++b) {
+    mptr[b] = off < capacity ? off : capacity;
+    const int64_t u = uid[b];
+    if (u < 0 || u >= num_users) continue;
+    int64_t a, z;
+    hist_run(hist_ptr, hist_idx, u, lo, hi, whole, a, z);
+    off += z - a;
+  }
+  if (t == 1023) {
+    const int64_t total = base + inc;
+    mptr[B] = total < capacity ? total : capacity;
+    if (total > capacity) hnm_flag(err, HNM_ERR_MASK_CAP);
+  }
+}
+
+__global__ __launch_bounds__(256) void mask_copy_kernel(const int64_t* __restrict__ hist_ptr,
+                                                        const int32_t* __restrict__ hist_idx,
+                                                        int64_t num_users,
+                                                        const int64_t* __restrict__ uid, int64_t B,
+                                                        int32_t lo, int32_t hi, bool whole,
+                                                        const int64_t* __restrict__ mptr,
+                                                        int32_t* __restrict__ midx) {
+  const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (b >= B) return;
+  const int lane = threadIdx.x & 63;
+  const int64_t u = uid[b];
+  if (u < 0 || u >= num_users) return;
+  int64_t a, z;
+  hist_run(hist_ptr, hist_idx, u, lo, hi, whole, a, z);
+  const int64_t dst = mptr[b], n = mptr[b + 1] - dst;
+  for (int64_t j = lane; j < n; j += 64) midx[dst + j] = hist_idx[a + j] - lo;
+}
+
+extern "C" hnm_status hnm_mask_gather_csr(hnm_ctx* ctx, const int64_t* hist_ptr,
+                                          const int32_t* hist_idx, int64_t num_users,
+                                          const int64_t* user_ids, int64_t B, int64_t item_lo,
+                                          int64_t item_hi, int64_t capacity, int64_t* mask_ptr,
+                                          int32_t* mask_idx) {
+  HNM_REQUIRE(ctx && hist_ptr && user_ids && mask_ptr && (hist_idx || capacity == 0) &&
+                  (mask_idx || capacity == 0),
+              HNM_EINVAL, "mask_gather: NULL argument");
+  HNM_REQUIRE(num_users >= 0 && B >= 0 && capacity >= 0 && 0 <= item_lo && item_lo <= item_hi,
+              HNM_EINVAL, "mask_gather: bad size or item range");
+  if (B == 0) return HNM_OK;
+  const int32_t lo = (int32_t)item_lo;
+  const int32_t hi = (int32_t)std::min<int64_t>(item_hi, INT32_MAX);
+  const bool whole = item_lo == 0 && item_hi >= INT32_MAX;
+  hipLaunchKernelGGL(mask_scan_kernel, dim3(1), dim3(1024), 0, ctx->stream, hist_ptr, hist_idx,
+                     num_users, user_ids, B, lo, hi, whole, capacity, mask_ptr, ctx->err_dev);
+  HNM_LAUNCH_CHECK();
+  hipLaunchKernelGGL(mask_copy_kernel, dim3((unsigned)hnm_cdiv(B, 4)), dim3(256), 0, ctx->stream,
+                     hist_ptr, hist_idx, num_users, user_ids, B, lo, hi, whole, mask_ptr,
+                     mask_idx);
   HNM_LAUNCH_CHECK();
   return HNM_OK;
 }

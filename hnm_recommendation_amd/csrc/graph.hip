@@ -378,9 +378,15 @@ __global__ __launch_bounds__(256) void spmm_finish_kernel(int64_t h0,
 }
 
 // Final embeddings of listed rows (the batch's users) without their last layer over the
-// whole graph: y = (A_hat E_{L-1})[r] (one wave per row, the light kernel's summation
-// order), out[b] = alpha_0 E_0[r] then fma(alpha_l, E_l[r], .) for l = 1..L-1 and
-// fma(alpha_L, y, .) -- the same operations, in the same order, as the fused combine.
+// whole graph: y = (A_hat E_{L-1})[r] (one wave per row), out[b] = alpha_0 E_0[r] then
+// fma(alpha_l, E_l[r], .) for l = 1..L-1 and fma(alpha_L, y, .) -- the same operations, in
+// the same order, as the fused combine.  y is summed in the order the planned SpMM uses for
+// that row: the light kernel's order for rows of <= HEAVY neighbours; for longer rows the
+// SEG-long segments (row_sum each, as spmm_segment_kernel), S = 256 / LPR slices summing
+// segments sl, sl + S, ... in order from 0, then the pairwise tree over the slices
+// (w = S/2 .. 1), as spmm_finish_kernel does -- so listed heavy rows are bitwise equal to
+// forward() too.  Each lane only touches its own float4 column of the slice sums (LDS, one
+// S x LPR block per wave), so the wave needs no barrier.
 struct CombineLayers {
   const float* E[8];
   float a[9];
@@ -401,7 +407,41 @@ __global__ __launch_bounds__(256) void spmm_rows_combine_kernel(
     for (int c = lane; c < d; c += 64) out[b * d + c] = __builtin_nanf("");
     return;
   }
-  const float4 y = row_sum<LPR>(col, val, cl.E[cl.L - 1], d, rowptr[r], rowptr[r + 1], lane);
+  const int64_t rs = rowptr[r], re = rowptr[r + 1];
+  float4 y;
+  if (re - rs <= HEAVY) {
+    y = row_sum<LPR>(col, val, cl.E[cl.L - 1], d, rs, re, lane);
+  } else {
+    constexpr int S = 256 / LPR;
+    __shared__ float4 slices[4][S * LPR];
+    float4* red = slices[threadIdx.x >> 6];
+    const int64_t nseg = hnm_cdiv(re - rs, SEG);
+    for (int sl = 0; sl < S; ++sl) {
+      float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+      for (int64_t sg = sl; sg < nseg; sg += S) {
+        const int64_t a = rs + sg * SEG, z = a + SEG < re ? a + SEG : re;
+        const float4 v = row_sum<LPR>(col, val, cl.E[cl.L - 1], d, a, z, lane);
+        acc.x += v.x;
+        acc.y += v.y;
+        acc.z += v.z;
+        acc.w += v.w;
+      }
+      if (lane < LPR) red[sl * LPR + lane] = acc;
+    }
+    if (lane < LPR) {
+      for (int w = S / 2; w >= 1; w >>= 1)
+        for (int sl = 0; sl < w; ++sl) {
+          const float4 o = red[(sl + w) * LPR + lane];
+          float4 m = red[sl * LPR + lane];
+          m.x += o.x;
+          m.y += o.y;
+          m.z += o.z;
+          m.w += o.w;
+          red[sl * LPR + lane] = m;
+        }
+      y = red[lane];
+    }
+  }
   if (lane < LPR) {
     const int64_t off = r * d + 4 * lane;
     const float4 x0 = *reinterpret_cast<const float4*>(cl.E[0] + off);

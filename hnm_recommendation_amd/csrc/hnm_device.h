@@ -210,6 +210,7 @@ __device__ __forceinline__ int64_t mask_lower_bound(const int32_t* midx, int64_t
 
 // Error word in device memory (ctx-owned): bit 0 = an id out of range was seen.
 #define HNM_ERR_OOB 1u
+#define HNM_ERR_MASK_CAP 4u  // hnm_mask_gather_csr: the batch mask exceeded its capacity
 __device__ __forceinline__ void hnm_flag(unsigned* err, unsigned bit) {
   if (err) atomicOr(err, bit);
 }

@@ -2,6 +2,7 @@
 from .lightgcn import LightGCN
 from .matrix_factorization import MatrixFactorization
 from .neural_cf import NeuralCF
+from .base import UserHistory
 from .wide_deep import WideDeep
 
-__all__ = ["NeuralCF", "LightGCN", "WideDeep", "MatrixFactorization"]
+__all__ = ["NeuralCF", "LightGCN", "WideDeep", "MatrixFactorization", "UserHistory"]

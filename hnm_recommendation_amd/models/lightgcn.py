@@ -202,7 +202,7 @@ class LightGCN(RecModule):
         last layer's 1.37M user rows and the users' combine traffic."""
         g = self._device_graph() if g is None else g
         U, N, L = self.num_users, self.num_nodes, self.num_layers
-        u = self._ids(user_ids, U)
+        u, hu = self._ids(user_ids, U)
         E0 = f32c(self.embeddings.weight)
         _lib.require_gpu(E0)
         if L == 0:
@@ -223,8 +223,8 @@ class LightGCN(RecModule):
     def predict(self, user_ids: torch.Tensor, item_ids: torch.Tensor) -> torch.Tensor:
         """Pairwise dot of propagated embeddings (`lightgcn.py:166-186`)."""
         fu, fi = self.forward()
-        u = self._ids(user_ids, self.num_users)
-        i = self._ids(item_ids, self.num_items, "item_ids")
+        u, hu = self._ids(user_ids, self.num_users)
+        i, hi = self._ids(item_ids, self.num_items, "item_ids")
         out = torch.empty(u.numel(), dtype=torch.float32, device=u.device)
         d = self.embedding_dim
         c = _lib.ctx(u.device)
@@ -232,13 +232,13 @@ class LightGCN(RecModule):
                                                self.num_items, d, d, _lib.ptr(u), _lib.ptr(i),
                                                u.numel(), None, None, None, _lib.ptr(out)),
                    "hnm_pair_dot_f32")
-        _lib.sync_check(u.device)
+        self._check(u.device, hu, hi)
         return out
 
     def predict_all_items(self, user_ids: torch.Tensor) -> torch.Tensor:
         """Dense scores F_U[ids] @ F_I^T, [B, num_items] (`lightgcn.py:188-204`)."""
         fu, fi = self.forward()
-        u = self._ids(user_ids, self.num_users)
+        u, hu = self._ids(user_ids, self.num_users)
         out = torch.empty(u.numel(), self.num_items, dtype=torch.float32, device=u.device)
         d = self.embedding_dim
         c = _lib.ctx(u.device)
@@ -246,7 +246,7 @@ class LightGCN(RecModule):
                                                  u.numel(), _lib.ptr(fi), self.num_items, d, d,
                                                  None, None, None, _lib.ptr(out), out.stride(0)),
                    "hnm_dot_scores_f32")
-        _lib.sync_check(u.device)
+        self._check(u.device, hu)
         return out
 
     def recommend_with_scores(self, user_ids: torch.Tensor,
@@ -255,7 +255,7 @@ class LightGCN(RecModule):
         """(scores [B, k], items [B, k]) sorted by score desc, item asc."""
         k = self.top_k if k is None else k
         fu, fi = self.forward()
-        u = self._ids(user_ids, self.num_users)
+        u, hu = self._ids(user_ids, self.num_users)
         n_items = fi.shape[0]
         mptr, midx = filter_csr(u, filter_items, self.num_items, u.device)
         kk = min(k, n_items)
@@ -271,7 +271,7 @@ class LightGCN(RecModule):
                                                None, None, None, _lib.ptr(mptr), _lib.ptr(midx),
                                                kk, _lib.ptr(out_v), _lib.ptr(out_i)),
                    "hnm_dot_topk_f32")
-        _lib.sync_check(u.device)
+        self._check(u.device, hu)
         return out_v, out_i
 
     def recommend(self, user_ids: torch.Tensor,

@@ -59,8 +59,8 @@ class MatrixFactorization(RecModule):
     def forward(self, user_ids: torch.Tensor, item_ids: torch.Tensor) -> torch.Tensor:
         """u.i + b_u + b_i + g per pair (`matrix_factorization.py:80-106`)."""
         U, V, ub, ib, gb = self._tabs()
-        u = self._ids(user_ids, self.num_users)
-        i = self._ids(item_ids, self.num_items, "item_ids")
+        u, hu = self._ids(user_ids, self.num_users)
+        i, hi = self._ids(item_ids, self.num_items, "item_ids")
         out = torch.empty(u.numel(), dtype=torch.float32, device=u.device)
         d = self.embedding_dim
         c = _lib.ctx(u.device)
@@ -68,12 +68,12 @@ class MatrixFactorization(RecModule):
                                                self.num_items, d, d, _lib.ptr(u), _lib.ptr(i),
                                                u.numel(), _lib.ptr(ub), _lib.ptr(ib),
                                                _lib.ptr(gb), _lib.ptr(out)), "hnm_pair_dot_f32")
-        _lib.sync_check(u.device)
+        self._check(u.device, hu, hi)
         return out
 
     def predict_all_items(self, user_ids: torch.Tensor) -> torch.Tensor:
         U, V, ub, ib, gb = self._tabs()
-        u = self._ids(user_ids, self.num_users)
+        u, hu = self._ids(user_ids, self.num_users)
         out = torch.empty(u.numel(), self.num_items, dtype=torch.float32, device=u.device)
         d = self.embedding_dim
         c = _lib.ctx(u.device)
@@ -82,14 +82,14 @@ class MatrixFactorization(RecModule):
                                                  _lib.ptr(ub), _lib.ptr(ib), _lib.ptr(gb),
                                                  _lib.ptr(out), out.stride(0)),
                    "hnm_dot_scores_f32")
-        _lib.sync_check(u.device)
+        self._check(u.device, hu)
         return out
 
     def recommend_with_scores(self, user_ids, filter_items: Optional[Dict[int, set]] = None,
                               k: Optional[int] = None):
         k = self.top_k if k is None else k
         U, V, ub, ib, gb = self._tabs()
-        u = self._ids(user_ids, self.num_users)
+        u, hu = self._ids(user_ids, self.num_users)
         mptr, midx = filter_csr(u, filter_items, self.num_items, u.device)
         kk = min(k, self.num_items)
         if kk > 64:
@@ -104,7 +104,7 @@ class MatrixFactorization(RecModule):
                                                _lib.ptr(mptr), _lib.ptr(midx), kk,
                                                _lib.ptr(out_v), _lib.ptr(out_i)),
                    "hnm_dot_topk_f32")
-        _lib.sync_check(u.device)
+        self._check(u.device, hu)
         return out_v, out_i
 
     def recommend(self, user_ids, filter_items: Optional[Dict[int, set]] = None):

@@ -94,24 +94,24 @@ class NeuralCF(RecModule):
     def forward(self, user_ids: torch.Tensor, item_ids: torch.Tensor) -> torch.Tensor:
         """Pairwise scores (`neural_cf.py:112-141`); `.squeeze()` semantics kept."""
         w, keep = self._weights()
-        u = self._ids(user_ids, self.num_users)
-        i = self._ids(item_ids, self.num_items, "item_ids")
+        u, hu = self._ids(user_ids, self.num_users)
+        i, hi = self._ids(item_ids, self.num_items, "item_ids")
         out = torch.empty(u.numel(), dtype=torch.float32, device=u.device)
         c = _lib.ctx(u.device)
         _lib.check(_lib.fn("hnm_ncf_pair_scores_f32")(c, w, _lib.ptr(u), _lib.ptr(i), u.numel(),
                                                       _lib.ptr(out)), "hnm_ncf_pair_scores_f32")
-        _lib.sync_check(u.device)
+        self._check(u.device, hu, hi)
         return out.squeeze()
 
     def predict_all_items(self, user_ids: torch.Tensor) -> torch.Tensor:
         """Dense scores [B, num_items] (`neural_cf.py:143-208`)."""
         w, keep = self._weights()
-        u = self._ids(user_ids, self.num_users)
+        u, hu = self._ids(user_ids, self.num_users)
         out = torch.empty(u.numel(), self.num_items, dtype=torch.float32, device=u.device)
         c = _lib.ctx(u.device)
         _lib.check(_lib.fn("hnm_ncf_scores_f32")(c, w, _lib.ptr(u), u.numel(), _lib.ptr(out),
                                                  out.stride(0)), "hnm_ncf_scores_f32")
-        _lib.sync_check(u.device)
+        self._check(u.device, hu)
         return out
 
     def recommend_with_scores(self, user_ids: torch.Tensor,
@@ -120,7 +120,7 @@ class NeuralCF(RecModule):
         """(scores [B, k], items [B, k]) sorted by score desc, item asc."""
         k = self.top_k if k is None else k
         w, keep = self._weights()
-        u = self._ids(user_ids, self.num_users)
+        u, hu = self._ids(user_ids, self.num_users)
         mptr, midx = filter_csr(u, filter_items, self.num_items, u.device)
         kk = min(k, self.num_items)
         if kk > 64:  # serve path k up to 100 (serve.py:56): dense + row top-k kernel
@@ -132,7 +132,7 @@ class NeuralCF(RecModule):
         _lib.check(_lib.fn("hnm_ncf_topk_f32")(c, w, _lib.ptr(u), u.numel(), _lib.ptr(mptr),
                                                _lib.ptr(midx), kk, _lib.ptr(out_v),
                                                _lib.ptr(out_i)), "hnm_ncf_topk_f32")
-        _lib.sync_check(u.device)
+        self._check(u.device, hu)
         return out_v, out_i
 
     def recommend(self, user_ids: torch.Tensor,

@@ -203,8 +203,8 @@ class WideDeep(RecModule):
         As in the reference, a model built with features needs them: its deep network's
         input width counts them (`:118-123`)."""
         w, keep = self._weights()
-        u = self._ids(user_ids, self.num_users)
-        i = self._ids(item_ids, self.num_items, "item_ids")
+        u, hu = self._ids(user_ids, self.num_users)
+        i, hi = self._ids(item_ids, self.num_items, "item_ids")
         f = fi = None
         if self.num_user_features > 0:
             if user_features is None:
@@ -225,20 +225,20 @@ class WideDeep(RecModule):
         _lib.check(_lib.fn("hnm_widedeep_pair_scores_ex_f32")(
             c, w, None if itf is None else C.byref(itf), _lib.ptr(u), _lib.ptr(i), _lib.ptr(f),
             _lib.ptr(fi), u.numel(), _lib.ptr(out)), "hnm_widedeep_pair_scores_ex_f32")
-        _lib.sync_check(u.device)
+        self._check(u.device, hu, hi)
         return out.squeeze()
 
     def predict_all_items(self, user_ids, user_features=None):
         """Dense scores [B, num_items] (`wide_deep.py:232-285`)."""
         w, keep = self._weights()
-        u = self._ids(user_ids, self.num_users)
+        u, hu = self._ids(user_ids, self.num_users)
         f = self._features(user_features, u.numel(), u.device)
         out = torch.empty(u.numel(), self.num_items, dtype=torch.float32, device=u.device)
         c = _lib.ctx(u.device)
         _lib.check(_lib.fn("hnm_widedeep_scores_f32")(c, w, _lib.ptr(u), u.numel(), _lib.ptr(f),
                                                       _lib.ptr(out), out.stride(0)),
                    "hnm_widedeep_scores_f32")
-        _lib.sync_check(u.device)
+        self._check(u.device, hu)
         return out
 
     def recommend_with_scores(self, user_ids, user_features=None,
@@ -246,7 +246,7 @@ class WideDeep(RecModule):
                               k: Optional[int] = None):
         k = self.top_k if k is None else k
         w, keep = self._weights()
-        u = self._ids(user_ids, self.num_users)
+        u, hu = self._ids(user_ids, self.num_users)
         f = self._features(user_features, u.numel(), u.device)
         mptr, midx = filter_csr(u, filter_items, self.num_items, u.device)
         kk = min(k, self.num_items)
@@ -259,7 +259,7 @@ class WideDeep(RecModule):
                                                     _lib.ptr(mptr), _lib.ptr(midx), kk,
                                                     _lib.ptr(out_v), _lib.ptr(out_i)),
                    "hnm_widedeep_topk_f32")
-        _lib.sync_check(u.device)
+        self._check(u.device, hu)
         return out_v, out_i
 
     def recommend(self, user_ids, user_features=None,

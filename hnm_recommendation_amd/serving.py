@@ -30,6 +30,7 @@ from typing import Dict, List, Optional, Sequence, Union
 import torch
 
 from .models import LightGCN, MatrixFactorization, NeuralCF, WideDeep
+from .models.base import UserHistory
 
 logger = logging.getLogger(__name__)
 
@@ -94,6 +95,7 @@ class Recommender:
         self.models: Dict[str, torch.nn.Module] = {}
         self.model_metrics: Dict[str, Dict[str, float]] = {}
         self.user_history = user_history or {}
+        self._history_dev: Optional[UserHistory] = None
         self.customer_index = customer_index
         self.article_ids = article_ids
         for name, m in (models or {}).items():
@@ -121,6 +123,21 @@ class Recommender:
                 self.model_metrics[name] = dict(ckpt.get("metrics", {}) or {})
                 loaded.append(name)
         return loaded
+
+    def set_user_history(self, user_history: Dict[int, set]):
+        """Replace the purchase history (the device copy is rebuilt on the next request)."""
+        self.user_history = user_history or {}
+        self._history_dev = None
+
+    def _device_history(self) -> Optional[UserHistory]:
+        """The purchase history as a device-resident CSR (built once, on first use): each
+        filtered batch gathers its rows on the GPU instead of building a mask on the host."""
+        if not self.user_history:
+            return None
+        if self._history_dev is None:
+            self._history_dev = UserHistory(self.user_history, self.num_users, self.num_items,
+                                            self.device)
+        return self._history_dev
 
     # ------------------------------------------------------------------ lookups
     def get_user_idx(self, user_id: Union[int, str]) -> Optional[int]:
@@ -169,13 +186,13 @@ class Recommender:
         hi = min(MAX_NUM_ITEMS, self.num_items)
         if isinstance(num_items, bool) or not isinstance(num_items, int) or not 1 <= num_items <= hi:
             raise ValueError(f"num_items must be an integer in [1, {hi}]")
-        users = torch.tensor(idx, dtype=torch.int64).to(self.device)
-        hist = None
-        if filter_purchased:
-            hist = {u: self.user_history[u] for u in set(idx) if u in self.user_history}
+        # host ids: range-checked on the host by the model (no device-side check / sync),
+        # then one fused scoring + history-mask + top-k call; the history mask is gathered
+        # on the GPU from the device-resident history (serve.py:350-352)
+        users = torch.tensor(idx, dtype=torch.int64)
+        hist = self._device_history() if filter_purchased else None
         with torch.no_grad():
-            vals, items = model.recommend_with_scores(users, filter_items=hist or None,
-                                                      k=num_items)
+            vals, items = model.recommend_with_scores(users, filter_items=hist, k=num_items)
         return vals.cpu().tolist(), items.cpu().tolist()
 
     def _result(self, user_id, model_name, vals, items, include_scores):

@@ -43,7 +43,10 @@ def shard_range(num_items: int, rank: int, world: int) -> Tuple[int, int]:
 
 class ItemShardedRecommender:
     def __init__(self, local_topk: LocalTopK, merge: Merge, k: int, item_offset: int,
-                 rank: int = 0, world: int = 1, group=None):
+                 rank: int = 0, world: int = 1, group=None, exchange: Optional[bool] = None):
+        """exchange: run the collective path (all_gather, bound all_reduce, all_to_all,
+        merge) -- the default whenever world > 1; True forces it at world == 1 as well
+        (a 1-rank process group: the RCCL calls of the multi-GPU path on one GPU)."""
         self.local_topk = local_topk
         self.merge = merge
         self.k = k
@@ -51,12 +54,15 @@ class ItemShardedRecommender:
         self.rank = rank
         self.world = world
         self.group = group
+        self.exchange = world > 1 if exchange is None else bool(exchange)
+        if self.exchange and not dist.is_initialized():
+            raise RuntimeError("the item-shard exchange needs an initialized process group")
 
     def recommend(self, user_ids: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
         """Top-k (scores, global item ids) for this rank's users [B] (same B on all ranks)."""
         G, k = self.world, self.k
         B = user_ids.numel()
-        if G == 1:
+        if not self.exchange:
             v, i = self.local_topk(user_ids)
             if self.item_offset == 0:  # ids are already global (no elementwise pass)
                 return v, i
@@ -119,14 +125,23 @@ def hip_merge(cand_v: torch.Tensor, cand_i: torch.Tensor, k: int):
     return out_v, out_i
 
 
+def _mask(history, u, lo, hi):
+    """The batch's -inf mask restricted to the shard's items (UserHistory on the device)."""
+    if history is None:
+        return None, None
+    return history.mask_for(u, (lo, hi))
+
+
 class ncf_shard_topk:
     """Fused NCF score + top-K over item rows [lo, hi) of `model` (a NeuralCF on a GPU).
 
     Called directly: one hnm_ncf_topk_f32.  `begin` / `finish`: the two phases of
-    hnm_ncf_topk_begin_f32 / _finish_f32 around a cross-shard bound exchange."""
+    hnm_ncf_topk_begin_f32 / _finish_f32 around a cross-shard bound exchange.  `history`
+    (a UserHistory): mask each user's history items, gathered on the device per call."""
 
-    def __init__(self, model, lo: int, hi: int, k: int):
+    def __init__(self, model, lo: int, hi: int, k: int, history=None):
         self.model, self.lo, self.hi, self.k = model, lo, hi, k
+        self.history = history
         self._open = None
 
     def _args(self, user_ids):
@@ -144,19 +159,21 @@ class ncf_shard_topk:
 
     def __call__(self, user_ids: torch.Tensor):
         w, keep, u, kk = self._args(user_ids)
+        mp, mi = _mask(self.history, u, self.lo, self.hi)
         out_v, out_i = self._out(u, kk)
-        _lib.check(_lib.fn("hnm_ncf_topk_f32")(_lib.ctx(u.device), w, _lib.ptr(u), u.numel(), None,
-                                               None, kk, _lib.ptr(out_v), _lib.ptr(out_i)),
-                   "hnm_ncf_topk_f32")
+        _lib.check(_lib.fn("hnm_ncf_topk_f32")(_lib.ctx(u.device), w, _lib.ptr(u), u.numel(),
+                                               _lib.ptr(mp), _lib.ptr(mi), kk, _lib.ptr(out_v),
+                                               _lib.ptr(out_i)), "hnm_ncf_topk_f32")
         return _pad(out_v, out_i, self.k)
 
     def begin(self, user_ids: torch.Tensor) -> torch.Tensor:
         w, keep, u, kk = self._args(user_ids)
+        mp, mi = _mask(self.history, u, self.lo, self.hi)
         lb = torch.empty(u.numel(), dtype=torch.float32, device=u.device)
         _lib.check(_lib.fn("hnm_ncf_topk_begin_f32")(_lib.ctx(u.device), w, _lib.ptr(u), u.numel(),
-                                                     None, None, kk, _lib.ptr(lb)),
+                                                     _lib.ptr(mp), _lib.ptr(mi), kk, _lib.ptr(lb)),
                    "hnm_ncf_topk_begin_f32")
-        self._open = (w, keep, u, kk)  # finish must pass the same ids / tables
+        self._open = (w, keep, u, kk, mp, mi)  # finish must pass the same ids / tables / mask
         return lb
 
     def abort(self):
@@ -165,13 +182,13 @@ class ncf_shard_topk:
             self._open = None
 
     def finish(self, user_ids: torch.Tensor, lb: torch.Tensor):
-        w, keep, u, kk = self._open
+        w, keep, u, kk, mp, mi = self._open
         self._open = None
         lb = lb.to(torch.float32).contiguous()
         out_v, out_i = self._out(u, kk)
         _lib.check(_lib.fn("hnm_ncf_topk_finish_f32")(_lib.ctx(u.device), w, _lib.ptr(u), u.numel(),
-                                                      None, None, kk, _lib.ptr(lb), 1,
-                                                      _lib.ptr(out_v), _lib.ptr(out_i)),
+                                                      _lib.ptr(mp), _lib.ptr(mi), kk, _lib.ptr(lb),
+                                                      1, _lib.ptr(out_v), _lib.ptr(out_i)),
                    "hnm_ncf_topk_finish_f32")
         return _pad(out_v, out_i, self.k)
 
@@ -180,17 +197,28 @@ class dot_shard_topk:
     """Fused dot score + top-K (LightGCN / MF without biases) over item rows [lo, hi).
 
     Called directly: one hnm_dot_topk_f32.  `begin` / `finish`: the two phases of
-    hnm_dot_topk_begin_f32 / _finish_f32 around a cross-shard bound exchange."""
+    hnm_dot_topk_begin_f32 / _finish_f32 around a cross-shard bound exchange.  `history`
+    (a UserHistory): mask each user's history items (user_ids must then be the history's
+    user ids: `rows` maps the table rows scored to them when they differ, e.g. LightGCN's
+    per-call user rows)."""
 
-    def __init__(self, user_tab: torch.Tensor, item_tab: torch.Tensor, lo: int, hi: int, k: int):
+    def __init__(self, user_tab: torch.Tensor, item_tab: torch.Tensor, lo: int, hi: int, k: int,
+                 history=None):
         self.user_tab, self.shard, self.k = user_tab, item_tab[lo:hi], k
-        self.n = hi - lo
+        self.lo, self.hi, self.n = lo, hi, hi - lo
+        self.history = history
+        self.mask_users = None   # ids the history is keyed by, when the table rows differ
         self._open = None
 
-    def _common(self, u):
+    def _common(self, u, mask=(None, None)):
         ut, sh = self.user_tab, self.shard
         return (_lib.ptr(ut), ut.shape[0], ut.stride(0), _lib.ptr(u), u.numel(), _lib.ptr(sh),
-                self.n, sh.stride(0), ut.shape[1], None, None, None, None, None)
+                self.n, sh.stride(0), ut.shape[1], None, None, None, _lib.ptr(mask[0]),
+                _lib.ptr(mask[1]))
+
+    def _mask(self, u):
+        return _mask(self.history, u if self.mask_users is None else self.mask_users,
+                     self.lo, self.hi)
 
     def _out(self, u, kk):
         return (torch.empty(u.numel(), kk, dtype=torch.float32, device=u.device),
@@ -200,17 +228,19 @@ class dot_shard_topk:
         u = user_ids.to(torch.int64).contiguous()
         kk = min(self.k, self.n)
         out_v, out_i = self._out(u, kk)
-        _lib.check(_lib.fn("hnm_dot_topk_f32")(_lib.ctx(u.device), *self._common(u), kk,
-                                               _lib.ptr(out_v), _lib.ptr(out_i)), "hnm_dot_topk_f32")
+        _lib.check(_lib.fn("hnm_dot_topk_f32")(_lib.ctx(u.device), *self._common(u, self._mask(u)),
+                                               kk, _lib.ptr(out_v), _lib.ptr(out_i)),
+                   "hnm_dot_topk_f32")
         return _pad(out_v, out_i, self.k)
 
     def begin(self, user_ids: torch.Tensor) -> torch.Tensor:
         u = user_ids.to(torch.int64).contiguous()
         kk = min(self.k, self.n)
+        mask = self._mask(u)
         lb = torch.empty(u.numel(), dtype=torch.float32, device=u.device)
-        _lib.check(_lib.fn("hnm_dot_topk_begin_f32")(_lib.ctx(u.device), *self._common(u), kk,
+        _lib.check(_lib.fn("hnm_dot_topk_begin_f32")(_lib.ctx(u.device), *self._common(u, mask), kk,
                                                      _lib.ptr(lb)), "hnm_dot_topk_begin_f32")
-        self._open = (u, kk)  # finish must pass the same ids
+        self._open = (u, kk, mask)  # finish must pass the same ids and mask
         return lb
 
     def abort(self):
@@ -219,18 +249,19 @@ class dot_shard_topk:
             self._open = None
 
     def finish(self, user_ids: torch.Tensor, lb: torch.Tensor):
-        u, kk = self._open
+        u, kk, mask = self._open
         self._open = None
         lb = lb.to(torch.float32).contiguous()
         out_v, out_i = self._out(u, kk)
-        _lib.check(_lib.fn("hnm_dot_topk_finish_f32")(_lib.ctx(u.device), *self._common(u), kk,
+        _lib.check(_lib.fn("hnm_dot_topk_finish_f32")(_lib.ctx(u.device), *self._common(u, mask), kk,
                                                       _lib.ptr(lb), 1, _lib.ptr(out_v),
                                                       _lib.ptr(out_i)), "hnm_dot_topk_finish_f32")
         return _pad(out_v, out_i, self.k)
 
 
-def widedeep_shard_topk(model, lo: int, hi: int, k: int) -> LocalTopK:
-    """Fused Wide&Deep score + top-K over item rows [lo, hi) of `model` (a WideDeep on a GPU)."""
+def widedeep_shard_topk(model, lo: int, hi: int, k: int, history=None) -> LocalTopK:
+    """Fused Wide&Deep score + top-K over item rows [lo, hi) of `model` (a WideDeep on a GPU);
+    `history` (a UserHistory) masks each user's history items."""
     def run(user_ids: torch.Tensor):
         w, keep = model._weights()
         d = model.embedding_dim
@@ -238,12 +269,14 @@ def widedeep_shard_topk(model, lo: int, hi: int, k: int) -> LocalTopK:
         w.wide_item = w.wide_item + lo * 4
         w.num_items = hi - lo
         u = user_ids.to(torch.int64).contiguous()
+        mp, mi = _mask(history, u, lo, hi)
         kk = min(k, hi - lo)
         out_v = torch.empty(u.numel(), kk, dtype=torch.float32, device=u.device)
         out_i = torch.empty(u.numel(), kk, dtype=torch.int64, device=u.device)
         c = _lib.ctx(u.device)
-        _lib.check(_lib.fn("hnm_widedeep_topk_f32")(c, w, _lib.ptr(u), u.numel(), None, None,
-                                                    None, kk, _lib.ptr(out_v), _lib.ptr(out_i)),
+        _lib.check(_lib.fn("hnm_widedeep_topk_f32")(c, w, _lib.ptr(u), u.numel(), None,
+                                                    _lib.ptr(mp), _lib.ptr(mi), kk,
+                                                    _lib.ptr(out_v), _lib.ptr(out_i)),
                    "hnm_widedeep_topk_f32")
         return _pad(out_v, out_i, k)
     return run
@@ -255,14 +288,17 @@ class lightgcn_shard_topk:
     call reads: `LightGCN.propagate_for(all users of the step)` (layers 1..L-1 whole graph,
     the last layer on item rows + these users), then the dot top-K over the shard."""
 
-    def __init__(self, model, lo: int, hi: int, k: int):
+    def __init__(self, model, lo: int, hi: int, k: int, history=None):
         self.model, self.lo, self.hi, self.k = model, lo, hi, k
+        self.history = history
         self._dot = None
 
     def _scorer(self, user_ids):
         fb, fi = self.model.propagate_for(user_ids)
         rows = torch.arange(user_ids.numel(), dtype=torch.int64, device=user_ids.device)
-        return dot_shard_topk(fb, fi, self.lo, self.hi, self.k), rows
+        dot = dot_shard_topk(fb, fi, self.lo, self.hi, self.k, self.history)
+        dot.mask_users = user_ids.to(torch.int64).contiguous()   # history keyed by user id
+        return dot, rows
 
     def __call__(self, user_ids: torch.Tensor):
         dot, rows = self._scorer(user_ids)

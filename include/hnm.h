@@ -13,9 +13,13 @@
  *    tables with an explicit leading dimension, int64 ids.
  *  - Calls are asynchronous and stream-ordered on the ctx stream (hnm_ctx_set_stream:
  *    torch's current stream).  A ctx is not re-entrant: use one per (device, thread)
- *    (the Python layer does).  Switching a ctx to another stream queues the new stream
- *    behind the work already issued on the old one (event wait, no host sync), so the
- *    ctx workspace is never reused while a kernel on the previous stream still reads it.
+ *    (the Python layer does: one per thread, destroyed when the thread exits).  Switching
+ *    a ctx to another stream queues the new stream behind the work already issued on the
+ *    old one (an event recorded on the old stream, waited on by the new one; no host sync),
+ *    so the ctx workspace is never reused while a kernel on the previous stream still reads
+ *    it.  A stream handed to hnm_ctx_set_stream must therefore stay alive until the ctx has
+ *    been switched away from it (torch's pooled streams always do; a caller-owned
+ *    hipStream_t / torch.cuda.ExternalStream must outlive that switch).
  *  - Status: 0 on success, negative on error; hnm_last_error() holds a thread-local
  *    message.  No C++ exception crosses the ABI.
  *  - Out-of-range user/item ids never fault: the row is skipped (index -1 / NaN) and the
@@ -304,6 +308,21 @@ hnm_status hnm_widedeep_prefilter_debug_f32(hnm_ctx* ctx, const hnm_widedeep_wei
                                             const float* user_features, float* approx,
                                             int64_t lda, float* bound);
 
+/* ---- a11: batch mask from a device-resident history CSR --------------------------------
+ * The purchase-history filter (serve.py:350-352; the filter_items loop of every recommend,
+ * neural_cf.py:316-321) without a host round trip: hist_ptr[num_users + 1] / hist_idx (per
+ * user, sorted ascending, unique, in [0, num_items)) stay on the device; for a batch of
+ * user_ids[B] this writes the CSR mask the top-K entry points take: mask_ptr[B + 1] and
+ * mask_idx[mask_ptr[B]] with row b = the history ids i of user_ids[b] with
+ * item_lo <= i < item_hi, as i - item_lo (an item shard's local ids; pass 0 / INT64_MAX for
+ * the whole catalogue).  Users outside [0, num_users) get empty rows (the scoring call flags
+ * them).  capacity = the mask_idx length (B x the longest history always suffices); beyond
+ * it rows are truncated and hnm_ctx_check() returns HNM_EINVAL.  Asynchronous, two launches. */
+hnm_status hnm_mask_gather_csr(hnm_ctx* ctx, const int64_t* hist_ptr, const int32_t* hist_idx,
+                               int64_t num_users, const int64_t* user_ids, int64_t B,
+                               int64_t item_lo, int64_t item_hi, int64_t capacity,
+                               int64_t* mask_ptr, int32_t* mask_idx);
+
 /* ---- torch.topk over a dense score matrix (serve.py:350-355, k up to 100) ----------
  * Row top-k of scores[b, :I] (leading dim ld) with the optional CSR -inf mask. k <= 128. */
 hnm_status hnm_topk_rows_f32(hnm_ctx* ctx, const float* scores, int64_t ld, int64_t B,
@@ -343,8 +362,9 @@ hnm_status hnm_spmm_csr_range_f32(hnm_ctx* ctx, const hnm_spmm_plan* plan, int64
  * (host): out[b] = sum_l alphas[l] E_l[rows[b]] with E_L[r] = (A_hat E_{L-1})[r] computed
  * for the listed rows only -- the last layer of LightGCN.forward restricted to the users a
  * recommend() call reads (lightgcn.py:197-199).  Same operations and order as the fused
- * combine of hnm_spmm_csr_f32 (bitwise equal for rows with <= 2048 neighbours).  An id out
- * of range flags HNM_EOOB and writes NaN.  1 <= L <= 8. */
+ * combine of hnm_spmm_csr_f32 with a plan (bitwise equal, heavy rows included: rows of more
+ * than 2048 neighbours are summed in the plan's segment + finish order).  An id out of range
+ * flags HNM_EOOB and writes NaN.  1 <= L <= 8. */
 hnm_status hnm_spmm_rows_combine_f32(hnm_ctx* ctx, int64_t N, const int64_t* rowptr,
                                      const int32_t* col, const float* val, const int64_t* rows,
                                      int64_t n, int d, const float* const* layers,

@@ -405,3 +405,38 @@ def test_widedeep_no_wide_user_item_golden():
     assert_topk_equivalent(g["topk"], dense, int(g["K"]))
     pair = m(t(g["pair_users"]), t(g["pair_items"])).cpu().numpy()
     assert_scores_close(pair, g["pair_scores"], "wd no-wide pair")
+
+
+@pytest.mark.parametrize("d", [64, 128])
+def test_lightgcn_propagate_for_heavy_user_rows_bitwise(d):
+    """Listed users whose rows exceed the SpMM's HEAVY = 2048 entries (segmented path in
+    forward(): SEG-long partials + the finish kernel's slice tree) come back from
+    propagate_for bit-identical to forward(): rows_combine sums them in the plan's order.
+    Row lengths include the self-loop: 2047 edges -> 2048 entries (light), 2048 -> 2049
+    (heavy, one extra segment), 5000, 40000 (20 segments: more than the 16 / 8 slices)."""
+    U, I = 3000, 50_000
+    rng = np.random.default_rng(5)
+    base = syn.bipartite_edge_index(U, I, 60_000, seed=2)
+    extra_u, extra_i = [], []
+    for u, n in ((0, 2047), (1, 2048), (2, 5000), (3, 40_000)):
+        items = rng.choice(I, size=n, replace=False) + U
+        extra_u.append(np.full(n, u))
+        extra_i.append(items)
+    eu, ei = np.concatenate(extra_u), np.concatenate(extra_i)
+    edges = np.concatenate([base, np.stack([np.concatenate([eu, ei]), np.concatenate([ei, eu])])],
+                           axis=1)
+    m = LightGCN(U, I, d)
+    m.set_graph(torch.from_numpy(edges))
+    m = to_module(m, syn.lightgcn_state_dict(U, I, d, seed=1))
+    users = t(np.array([3, 0, 1, 2, 3, 17, 2999]))
+    fb, fi_b = m.propagate_for(users)
+    fu, fi = m.forward()
+    assert torch.equal(fi_b, fi)
+    assert torch.equal(fb, fu[users])
+    # and the same rows match the reference's propagation restated on CPU (1e-4)
+    from oracle import torch_cpu as T
+    g = T.lightgcn_graph(torch.from_numpy(edges), U + I)
+    w = torch.from_numpy(syn.lightgcn_state_dict(U, I, d, seed=1)["embeddings.weight"])
+    cu, _ = T.lightgcn_forward(w, g, U)
+    ref = cu[users.cpu()].numpy()
+    np.testing.assert_allclose(fb.cpu().numpy(), ref, rtol=1e-4, atol=1e-4 * float(np.abs(ref).max()))

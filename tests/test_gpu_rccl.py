@@ -1,0 +1,121 @@
+"""GPU: the multi-GPU exchange branch of `ItemShardedRecommender` through a REAL RCCL
+process group (backend "nccl" = RCCL on ROCm) -- a 1-rank group on the box's one GPU, with
+`exchange=True` forcing the collective path.  This executes, on device tensors, exactly the
+calls the 8-GPU run makes (sharding.py: `all_gather_into_tensor` of user ids,
+`all_reduce(MAX)` of the certified bounds, `all_to_all_single` of packed candidates) plus the
+HIP merge, and checks the result bit for bit against single-GPU `recommend_with_scores` for
+NCF (two-phase certified), the dot scorer on LightGCN d=128 propagated tables (two-phase
+certified) and Wide&Deep (one-shot certified).  An exception injected into the bound
+all_reduce must abort the open two-phase call so the next recommend on the same ctx works.
+
+The group runs in a spawned child (RCCL state stays out of the pytest process); any
+assertion in the child fails `mp.spawn`.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from hnm_recommendation_amd import LightGCN, NeuralCF, WideDeep
+from hnm_recommendation_amd import _lib
+from hnm_recommendation_amd import sharding as S
+from hnm_recommendation_amd import synthetic as syn
+
+pytestmark = pytest.mark.gpu
+K = 12
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _load(m, sd):
+    m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in sd.items()})
+    return m.to("cuda:0").eval()
+
+
+def _same(a, b, what):
+    (av, ai), (bv, bi) = a, b
+    assert torch.equal(ai, bi), f"{what}: item ids differ from single-GPU"
+    assert torch.equal(av.view(torch.int32), bv.view(torch.int32)), f"{what}: score bits differ"
+
+
+def _rccl_worker(rank, port):
+    os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0,
+                            world_size=1, device_id=dev)
+    try:
+        assert dist.get_backend() == "nccl"
+        # ---- NeuralCF, full catalogue (certified two-phase path engages at I >= 8192)
+        U, I = 20_000, syn.HM_ITEMS
+        m = _load(NeuralCF(U, I), syn.ncf_state_dict(U, I, 64, (128, 64, 32), seed=5))
+        users = torch.from_numpy(syn.user_batch(U, 1000, seed=9)).to(dev)
+        sc = S.ncf_shard_topk(m, 0, I, K)
+        rec = S.ItemShardedRecommender(sc, S.hip_merge, K, 0, exchange=True)
+        ref = m.recommend_with_scores(users)
+        _same(rec.recommend(users), ref, "ncf rccl exchange")
+
+        # the purchase-history filter through the exchange (device-gathered per-shard mask)
+        from hnm_recommendation_amd import UserHistory
+        hist_d = syn.filter_dict(users.cpu().numpy(), I, per_user=23, seed=4)
+        frec = S.ItemShardedRecommender(S.ncf_shard_topk(m, 0, I, K, UserHistory(hist_d, U, I, dev)),
+                                        S.hip_merge, K, 0, exchange=True)
+        _same(frec.recommend(users), m.recommend_with_scores(users, filter_items=hist_d),
+              "ncf rccl exchange, filtered")
+
+        # injected failure inside the exchange: the open two-phase call is aborted, the
+        # error propagates, and the same thread's ctx serves the next call
+        real = dist.all_reduce
+        calls = {"n": 0}
+
+        def failing(*a, **kw):
+            calls["n"] += 1
+            raise RuntimeError("injected all_reduce failure")
+        S.dist.all_reduce = failing
+        try:
+            with pytest.raises(RuntimeError, match="injected"):
+                rec.recommend(users)
+        finally:
+            S.dist.all_reduce = real
+        assert calls["n"] == 1 and sc._open is None
+        _same(rec.recommend(users), ref, "ncf rccl exchange after abort")
+        _same(m.recommend_with_scores(users), ref, "ncf single-GPU after abort")
+
+        # ---- dot scorer on LightGCN d=128 propagated tables
+        LU, LE = 30_000, 600_000
+        lg = LightGCN(LU, I, embedding_dim=128, num_layers=3)
+        lg.set_graph(torch.from_numpy(syn.bipartite_edge_index(LU, I, LE, seed=2)))
+        lg = _load(lg, syn.lightgcn_state_dict(LU, I, 128, seed=0))
+        fu, fi = lg.forward()
+        lusers = torch.from_numpy(syn.user_batch(LU, 777, seed=11)).to(dev)
+        drec = S.ItemShardedRecommender(S.dot_shard_topk(fu, fi, 0, I, K), S.hip_merge, K, 0,
+                                        exchange=True)
+        _same(drec.recommend(lusers), lg.recommend_with_scores(lusers), "lightgcn128 rccl")
+        # the per-call-propagation scorer (what bench.py's LightGCN step runs)
+        prec = S.ItemShardedRecommender(S.lightgcn_shard_topk(lg, 0, I, K), S.hip_merge, K, 0,
+                                        exchange=True)
+        _same(prec.recommend(lusers), lg.recommend_with_scores(lusers), "lightgcn128 per-call")
+
+        # ---- Wide&Deep (one-shot certified scorer, full K-lists exchanged)
+        WU, WI = 5_000, 20_000
+        wd = _load(WideDeep(WU, WI), syn.widedeep_state_dict(WU, WI, 64, (512, 256, 128), seed=3))
+        wusers = torch.from_numpy(syn.user_batch(WU, 96, seed=12)).to(dev)
+        wrec = S.ItemShardedRecommender(S.widedeep_shard_topk(wd, 0, WI, K), S.hip_merge, K, 0,
+                                        exchange=True)
+        _same(wrec.recommend(wusers), wd.recommend_with_scores(wusers), "widedeep rccl")
+        _lib.sync_check(dev)
+        torch.cuda.synchronize()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_rccl_one_rank_exchange_matches_single_gpu():
+    mp.spawn(_rccl_worker, args=(_free_port(),), nprocs=1, join=True)

@@ -108,3 +108,79 @@ def test_shard_ranges_cover_items():
         r = [S.shard_range(105542, g, G) for g in range(G)]
         assert r[0][0] == 0 and r[-1][1] == 105542
         assert all(a[1] == b[0] for a, b in zip(r, r[1:]))
+
+
+def _one_rank_worker(rank, port, q):
+    """exchange=True on a 1-rank group: the collective branch at world 1 (the shape of the
+    GPU RCCL test), and an exception injected into the bound all_reduce aborts the open
+    two-phase call before it propagates."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=0, world_size=1)
+    try:
+        sd = syn.ncf_state_dict(U, I, 64, (128, 64, 32), seed=0, bias_scale=0.05, emb_scale=20.0)
+
+        class TwoPhase:
+            def __init__(self):
+                self.open, self.aborts = False, 0
+
+            def _topk(self, all_ids):
+                v, i = O.topk(O.ncf_predict_all_items(sd, all_ids.numpy()), K)
+                return torch.from_numpy(v.astype(np.float32)), torch.from_numpy(i)
+
+            def begin(self, all_ids):
+                assert not self.open
+                self.open = True
+                return self._topk(all_ids)[0][:, K - 1].clone()
+
+            def finish(self, all_ids, lb):
+                assert self.open
+                self.open = False
+                return self._topk(all_ids)
+
+            def abort(self):
+                self.open = False
+                self.aborts += 1
+
+        users = torch.from_numpy(syn.user_batch(U, B, seed=31))
+        sc = TwoPhase()
+        rec = S.ItemShardedRecommender(sc, _np_merge, K, 0, exchange=True)
+        v, i = rec.recommend(users)
+        real = dist.all_reduce
+
+        def failing(*a, **kw):
+            raise RuntimeError("injected")
+        S.dist.all_reduce = failing
+        try:
+            rec.recommend(users)
+            raise AssertionError("the injected failure did not propagate")
+        except RuntimeError as e:
+            assert "injected" in str(e)
+        finally:
+            S.dist.all_reduce = real
+        assert sc.aborts == 1 and not sc.open
+        v2, i2 = rec.recommend(users)
+        assert torch.equal(i, i2) and torch.equal(v, v2)
+        q.put((users.numpy(), v.numpy(), i.numpy()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_forced_exchange_one_rank_and_abort():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_one_rank_worker, args=(0, _free_port(), q))
+    p.start()
+    users, v, i = q.get(timeout=300)
+    p.join(timeout=120)
+    assert p.exitcode == 0
+    sd = syn.ncf_state_dict(U, I, 64, (128, 64, 32), seed=0, bias_scale=0.05, emb_scale=20.0)
+    rv, ri = O.topk(O.ncf_predict_all_items(sd, users), K)
+    assert np.array_equal(i, ri)
+    np.testing.assert_array_equal(v, rv.astype(np.float32))
+
+
+def test_exchange_requires_process_group():
+    if dist.is_initialized():
+        pytest.skip("a process group is live in this process")
+    with pytest.raises(RuntimeError, match="process group"):
+        S.ItemShardedRecommender(lambda u: u, _np_merge, K, 0, exchange=True)

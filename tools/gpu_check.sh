@@ -1,5 +1,6 @@
 #!/bin/bash
-# GPU session: parity tests + default bench + 2-rank launcher rehearsal (gloo on one GPU).
+# GPU session: parity tests + smoke() + default bench (all workloads) + 2-rank launcher
+# rehearsal (gloo on one GPU).
 #   bash tools/gpu_check.sh <tag> [pytest -k expr]   (outputs under gpurun_out/<tag>/)
 set -uo pipefail
 TAG=${1:-r}
@@ -22,7 +23,8 @@ if [ -n "$KEXPR" ]; then
 else
   step tests 1000 python -u -m pytest tests -x -v -m gpu --timeout 180 --timeout-method thread
 fi
-step bench_ncf 300 python bench.py
+step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
+step bench_ncf 900 python bench.py
 export HNM_DIST_BACKEND=gloo
 step bench_2rank 400 python bench.py --gpus 2 --workload lightgcn128 --steps 5 --warmup 2
 echo ok
