@@ -122,7 +122,10 @@ class UserHistory:
 
     def _set(self, ptr, idx, num_users, num_items, device):
         self.num_users, self.num_items = int(num_users), int(num_items)
-        self.device = torch.device(device)
+        dev = torch.device(device)
+        if dev.type == "cuda" and dev.index is None:
+            dev = torch.device("cuda", torch.cuda.current_device())
+        self.device = dev
         lens = np.diff(ptr)
         self.max_len = int(lens.max()) if lens.size else 0
         self.nnz = int(ptr[-1])
