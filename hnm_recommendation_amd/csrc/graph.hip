@@ -28,6 +28,9 @@
 #ifndef SEG
 #define SEG 2048
 #endif
+#ifndef SPMM_GROUPED  // light rows: one LPR-lane group per row (64 / LPR rows per wave)
+#define SPMM_GROUPED 0
+#endif
 #ifndef SPMM_SIDE_STREAM  // heavy-row segments on the ctx's side stream, beside the light kernel
 #define SPMM_SIDE_STREAM 1
 #endif
@@ -320,6 +323,63 @@ __global__ __launch_bounds__(256) void spmm_light_kernel(int64_t r0, int64_t r1,
   if (lane < LPR) spmm_epilogue(r, d, lane, y, X, ep);
 }
 
+// Grouped light rows: lane group g = lane / LPR owns row r, lane sub = lane % LPR its float4
+// column; the group walks the row's entries in order (4 loads in flight per group, 64 / LPR
+// rows per wave) with one fma chain per column -- no cross-group tree.
+template <int LPR>
+__device__ __forceinline__ float4 row_sum_grouped(const int32_t* __restrict__ col,
+                                                  const float* __restrict__ val,
+                                                  const float* __restrict__ X, int d, int64_t s,
+                                                  int64_t e, int sub) {
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  int64_t p = s;
+  for (; p + 3 < e; p += 4) {
+    int c[4];
+    float w[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      c[u] = col[p + u];
+      w[u] = val[p + u];
+    }
+    float4 x[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) x[u] = *reinterpret_cast<const float4*>(X + (int64_t)c[u] * d + 4 * sub);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      acc.x = fmaf(w[u], x[u].x, acc.x);
+      acc.y = fmaf(w[u], x[u].y, acc.y);
+      acc.z = fmaf(w[u], x[u].z, acc.z);
+      acc.w = fmaf(w[u], x[u].w, acc.w);
+    }
+  }
+  for (; p < e; ++p) {
+    const int c = col[p];
+    const float w = val[p];
+    const float4 x = *reinterpret_cast<const float4*>(X + (int64_t)c * d + 4 * sub);
+    acc.x = fmaf(w, x.x, acc.x);
+    acc.y = fmaf(w, x.y, acc.y);
+    acc.z = fmaf(w, x.z, acc.z);
+    acc.w = fmaf(w, x.w, acc.w);
+  }
+  return acc;
+}
+
+template <int LPR>
+__global__ __launch_bounds__(256) void spmm_grouped_kernel(int64_t r0, int64_t r1,
+                                                           const int64_t* __restrict__ rowptr,
+                                                           const int32_t* __restrict__ col,
+                                                           const float* __restrict__ val,
+                                                           const float* __restrict__ X, int d,
+                                                           SpmmEpi ep, int64_t heavy) {
+  constexpr int RPW = 64 / LPR;
+  const int lane = threadIdx.x & 63, sub = lane % LPR;
+  const int64_t r = r0 + ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW + lane / LPR;
+  if (r >= r1) return;
+  const int64_t s = rowptr[r], e = rowptr[r + 1];
+  if (e - s > heavy) return;  // segmented path
+  spmm_epilogue(r, d, sub, row_sum_grouped<LPR>(col, val, X, d, s, e, sub), X, ep);
+}
+
 template <int LPR>
 __global__ __launch_bounds__(256) void spmm_segment_kernel(int64_t sg0, int64_t sg1,
                                                            const int64_t* __restrict__ seg_start,
@@ -378,7 +438,7 @@ __global__ __launch_bounds__(256) void spmm_finish_kernel(int64_t h0,
 }
 
 // Final embeddings of listed rows (the batch's users) without their last layer over the
-// whole graph: y = (A_hat E_{L-1})[r] (one wave per row), out[b] = alpha_0 E_0[r] then
+// whole graph: y = (A_hat E_{L-1})[r], out[b] = alpha_0 E_0[r] then
 // fma(alpha_l, E_l[r], .) for l = 1..L-1 and fma(alpha_L, y, .) -- the same operations, in
 // the same order, as the fused combine.  y is summed in the order the planned SpMM uses for
 // that row: the light kernel's order for rows of <= HEAVY neighbours; for longer rows the
@@ -386,79 +446,129 @@ __global__ __launch_bounds__(256) void spmm_finish_kernel(int64_t h0,
 // segments sl, sl + S, ... in order from 0, then the pairwise tree over the slices
 // (w = S/2 .. 1), as spmm_finish_kernel does -- so listed heavy rows are bitwise equal to
 // forward() too.  Each lane only touches its own float4 column of the slice sums (LDS, one
-// S x LPR block per wave), so the wave needs no barrier.
+// S x LPR block per wave), so the wave needs no barrier.  Light rows use the light kernel's
+// layout (one wave per row, or with SPMM_GROUPED one LPR-lane group per row).
 struct CombineLayers {
   const float* E[8];
   float a[9];
   int L;
 };
 
+// y = (A_hat X)[r] for a row of more than HEAVY entries, in the plan's segment + finish
+// order (see above); the whole wave works on the row, the result is valid in lanes < LPR.
+template <int LPR>
+__device__ float4 heavy_row_sum(const int32_t* __restrict__ col, const float* __restrict__ val,
+                                const float* __restrict__ X, int d, int64_t rs, int64_t re,
+                                int lane, float4* red) {
+  constexpr int S = 256 / LPR;
+  const int64_t nseg = hnm_cdiv(re - rs, SEG);
+  for (int sl = 0; sl < S; ++sl) {
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int64_t sg = sl; sg < nseg; sg += S) {
+      const int64_t a = rs + sg * SEG, z = a + SEG < re ? a + SEG : re;
+      const float4 v = row_sum<LPR>(col, val, X, d, a, z, lane);
+      acc.x += v.x;
+      acc.y += v.y;
+      acc.z += v.z;
+      acc.w += v.w;
+    }
+    if (lane < LPR) red[sl * LPR + lane] = acc;
+  }
+  float4 y = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (lane < LPR) {
+    for (int w = S / 2; w >= 1; w >>= 1)
+      for (int sl = 0; sl < w; ++sl) {
+        const float4 o = red[(sl + w) * LPR + lane];
+        float4 m = red[sl * LPR + lane];
+        m.x += o.x;
+        m.y += o.y;
+        m.z += o.z;
+        m.w += o.w;
+        red[sl * LPR + lane] = m;
+      }
+    y = red[lane];
+  }
+  return y;
+}
+
+// out[b] = alpha_0 E_0[r] + sum_l alpha_l E_l[r] (fma chain in layer order) + alpha_L y
+__device__ __forceinline__ void combine_store(const CombineLayers& cl, int64_t r, int d, int sub,
+                                              float4 y, float* __restrict__ out, int64_t b) {
+  const int64_t off = r * d + 4 * sub;
+  const float4 x0 = *reinterpret_cast<const float4*>(cl.E[0] + off);
+  float4 a = make_float4(cl.a[0] * x0.x, cl.a[0] * x0.y, cl.a[0] * x0.z, cl.a[0] * x0.w);
+  for (int l = 1; l < cl.L; ++l) {
+    const float4 x = *reinterpret_cast<const float4*>(cl.E[l] + off);
+    a.x = fmaf(cl.a[l], x.x, a.x);
+    a.y = fmaf(cl.a[l], x.y, a.y);
+    a.z = fmaf(cl.a[l], x.z, a.z);
+    a.w = fmaf(cl.a[l], x.w, a.w);
+  }
+  const float aL = cl.a[cl.L];
+  a.x = fmaf(aL, y.x, a.x);
+  a.y = fmaf(aL, y.y, a.y);
+  a.z = fmaf(aL, y.z, a.z);
+  a.w = fmaf(aL, y.w, a.w);
+  *reinterpret_cast<float4*>(out + b * d + 4 * sub) = a;
+}
+
 template <int LPR>
 __global__ __launch_bounds__(256) void spmm_rows_combine_kernel(
     const int64_t* __restrict__ rows, int64_t n, int64_t N, const int64_t* __restrict__ rowptr,
     const int32_t* __restrict__ col, const float* __restrict__ val, int d, CombineLayers cl,
     float* __restrict__ out, unsigned* err) {
-  const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (b >= n) return;
+  __shared__ float4 slices[4][256];
   const int lane = threadIdx.x & 63;
-  const int64_t r = rows[b];
-  if (r < 0 || r >= N) {
-    if (lane == 0) hnm_flag(err, HNM_ERR_OOB);
-    for (int c = lane; c < d; c += 64) out[b * d + c] = __builtin_nanf("");
+  const float* Xl = cl.E[cl.L - 1];
+  if (!SPMM_GROUPED) {
+    const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (b >= n) return;
+    const int64_t r = rows[b];
+    if (r < 0 || r >= N) {
+      if (lane == 0) hnm_flag(err, HNM_ERR_OOB);
+      for (int c = lane; c < d; c += 64) out[b * d + c] = __builtin_nanf("");
+      return;
+    }
+    const int64_t rs = rowptr[r], re = rowptr[r + 1];
+    const float4 y = re - rs <= HEAVY
+                         ? row_sum<LPR>(col, val, Xl, d, rs, re, lane)
+                         : heavy_row_sum<LPR>(col, val, Xl, d, rs, re, lane, slices[threadIdx.x >> 6]);
+    if (lane < LPR) combine_store(cl, r, d, lane, y, out, b);
     return;
   }
-  const int64_t rs = rowptr[r], re = rowptr[r + 1];
-  float4 y;
-  if (re - rs <= HEAVY) {
-    y = row_sum<LPR>(col, val, cl.E[cl.L - 1], d, rs, re, lane);
-  } else {
-    constexpr int S = 256 / LPR;
-    __shared__ float4 slices[4][S * LPR];
-    float4* red = slices[threadIdx.x >> 6];
-    const int64_t nseg = hnm_cdiv(re - rs, SEG);
-    for (int sl = 0; sl < S; ++sl) {
-      float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-      for (int64_t sg = sl; sg < nseg; sg += S) {
-        const int64_t a = rs + sg * SEG, z = a + SEG < re ? a + SEG : re;
-        const float4 v = row_sum<LPR>(col, val, cl.E[cl.L - 1], d, a, z, lane);
-        acc.x += v.x;
-        acc.y += v.y;
-        acc.z += v.z;
-        acc.w += v.w;
-      }
-      if (lane < LPR) red[sl * LPR + lane] = acc;
-    }
-    if (lane < LPR) {
-      for (int w = S / 2; w >= 1; w >>= 1)
-        for (int sl = 0; sl < w; ++sl) {
-          const float4 o = red[(sl + w) * LPR + lane];
-          float4 m = red[sl * LPR + lane];
-          m.x += o.x;
-          m.y += o.y;
-          m.z += o.z;
-          m.w += o.w;
-          red[sl * LPR + lane] = m;
-        }
-      y = red[lane];
+  // grouped: group g = lane / LPR owns listed row b; light rows in the grouped order, heavy
+  // rows afterwards by the whole wave (uniform loop over the wave's groups)
+  constexpr int RPW = 64 / LPR;
+  const int g = lane / LPR, sub = lane % LPR;
+  const int64_t b0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW;
+  if (b0 >= n) return;
+  const int64_t b = b0 + g;
+  int64_t r = -1, rs = 0, re = 0;
+  bool ok = false;
+  if (b < n) {
+    r = rows[b];
+    ok = r >= 0 && r < N;
+    if (!ok) {
+      if (sub == 0) hnm_flag(err, HNM_ERR_OOB);
+      const float nan = __builtin_nanf("");
+      *reinterpret_cast<float4*>(out + b * d + 4 * sub) = make_float4(nan, nan, nan, nan);
+    } else {
+      rs = rowptr[r];
+      re = rowptr[r + 1];
+      if (re - rs <= HEAVY)
+        combine_store(cl, r, d, sub, row_sum_grouped<LPR>(col, val, Xl, d, rs, re, sub), out, b);
     }
   }
-  if (lane < LPR) {
-    const int64_t off = r * d + 4 * lane;
-    const float4 x0 = *reinterpret_cast<const float4*>(cl.E[0] + off);
-    float4 a = make_float4(cl.a[0] * x0.x, cl.a[0] * x0.y, cl.a[0] * x0.z, cl.a[0] * x0.w);
-    for (int l = 1; l < cl.L; ++l) {
-      const float4 x = *reinterpret_cast<const float4*>(cl.E[l] + off);
-      a.x = fmaf(cl.a[l], x.x, a.x);
-      a.y = fmaf(cl.a[l], x.y, a.y);
-      a.z = fmaf(cl.a[l], x.z, a.z);
-      a.w = fmaf(cl.a[l], x.w, a.w);
-    }
-    const float aL = cl.a[cl.L];
-    a.x = fmaf(aL, y.x, a.x);
-    a.y = fmaf(aL, y.y, a.y);
-    a.z = fmaf(aL, y.z, a.z);
-    a.w = fmaf(aL, y.w, a.w);
-    *reinterpret_cast<float4*>(out + b * d + 4 * lane) = a;
+  const bool heavy = ok && re - rs > HEAVY;
+  uint64_t hm = __ballot(heavy && sub == 0);
+  while (hm) {
+    const int src = __builtin_ctzll(hm) ;
+    hm &= hm - 1;
+    const int64_t hb = b0 + src / LPR;
+    const int64_t hr = rows[hb];
+    const int64_t hs = rowptr[hr], he = rowptr[hr + 1];
+    const float4 y = heavy_row_sum<LPR>(col, val, Xl, d, hs, he, lane, slices[threadIdx.x >> 6]);
+    if (lane < LPR) combine_store(cl, hr, d, lane, y, out, hb);
   }
 }
 
@@ -567,8 +677,12 @@ static hnm_status spmm_launch(hnm_ctx* ctx, const hnm_spmm_plan* pl, int64_t N,
     }
   }
   if (r1 > r0) {
-    hipLaunchKernelGGL(spmm_light_kernel<LPR>, dim3((unsigned)hnm_cdiv(r1 - r0, 4)), dim3(256), 0,
-                       ctx->stream, r0, r1, rowptr, col, val, X, d, ep, heavy);
+    if (SPMM_GROUPED)
+      hipLaunchKernelGGL(spmm_grouped_kernel<LPR>, dim3((unsigned)hnm_cdiv(r1 - r0, 4 * (64 / LPR))),
+                         dim3(256), 0, ctx->stream, r0, r1, rowptr, col, val, X, d, ep, heavy);
+    else
+      hipLaunchKernelGGL(spmm_light_kernel<LPR>, dim3((unsigned)hnm_cdiv(r1 - r0, 4)), dim3(256), 0,
+                         ctx->stream, r0, r1, rowptr, col, val, X, d, ep, heavy);
     HNM_LAUNCH_CHECK();
   }
   if (forked) HNM_HIP_CHECK(hipStreamWaitEvent(ctx->stream, ctx->side_out, 0));
@@ -622,7 +736,9 @@ template <int LPR>
 static hnm_status combine_launch(hnm_ctx* ctx, const int64_t* rows, int64_t n, int64_t N,
                                  const int64_t* rowptr, const int32_t* col, const float* val,
                                  int d, const CombineLayers& cl, float* out) {
-  hipLaunchKernelGGL(spmm_rows_combine_kernel<LPR>, dim3((unsigned)hnm_cdiv(n, 4)), dim3(256), 0,
+  const int64_t rows_per_block = SPMM_GROUPED ? 4 * (64 / LPR) : 4;
+  hipLaunchKernelGGL(spmm_rows_combine_kernel<LPR>, dim3((unsigned)hnm_cdiv(n, rows_per_block)),
+                     dim3(256), 0,
                      ctx->stream, rows, n, N, rowptr, col, val, d, cl, out, ctx->err_dev);
   HNM_LAUNCH_CHECK();
   return HNM_OK;
