@@ -28,9 +28,16 @@
 #ifndef SEG
 #define SEG 2048
 #endif
-#ifndef SPMM_GROUPED  // light rows: one LPR-lane group per row (64 / LPR rows per wave)
-#define SPMM_GROUPED 0
+// Row classes by entry count L (self-loop included), decided per row so that every kernel that
+// sums a row (the layer kernels, rows_combine) uses the same order:
+//   short  L <= SPMM_SHORT           one LPR-lane group per row, 64 / LPR rows per wave
+//   long   SPMM_SHORT < L <= HEAVY   one wave per row (4 neighbour groups + a fixed tree)
+//   heavy  L > HEAVY                 SEG-long segments + a finish kernel
+// SPMM_SHORT 0 puts every light row in the long class (the round-2 kernel).
+#ifndef SPMM_SHORT
+#define SPMM_SHORT 128
 #endif
+#define SPMM_GROUPED (SPMM_SHORT > 0)
 #ifndef SPMM_SIDE_STREAM  // heavy-row segments on the ctx's side stream, beside the light kernel
 #define SPMM_SIDE_STREAM 1
 #endif
@@ -41,6 +48,9 @@ struct hnm_spmm_plan {
   int64_t n_heavy;
   int64_t n_seg;
   int32_t* heavy_rows;  // [n_heavy]
+  int64_t n_long;
+  int32_t* long_rows;   // [n_long] rows of the long class, ascending (SPMM_SHORT > 0)
+  std::vector<int32_t>* h_long;
   int64_t* seg_ptr;     // [n_heavy + 1]
   int32_t* seg_hrow;    // [n_seg]  index into heavy_rows
   int64_t* seg_start;   // [n_seg]
@@ -364,19 +374,34 @@ __device__ __forceinline__ float4 row_sum_grouped(const int32_t* __restrict__ co
   return acc;
 }
 
+// One launch for the light rows of [r0, r1): blocks [0, nlb) take the long rows listed in
+// long_rows[l0, l1) (one wave per row, the light kernel's order; first, so the longest work
+// starts first), the other blocks the short rows (one LPR-lane group per row), skipping rows
+// of the other classes.
 template <int LPR>
-__global__ __launch_bounds__(256) void spmm_grouped_kernel(int64_t r0, int64_t r1,
-                                                           const int64_t* __restrict__ rowptr,
-                                                           const int32_t* __restrict__ col,
-                                                           const float* __restrict__ val,
-                                                           const float* __restrict__ X, int d,
-                                                           SpmmEpi ep, int64_t heavy) {
+__global__ __launch_bounds__(256) void spmm_mixed_kernel(int64_t r0, int64_t r1,
+                                                         const int32_t* __restrict__ long_rows,
+                                                         int64_t l0, int64_t l1, int64_t nlb,
+                                                         const int64_t* __restrict__ rowptr,
+                                                         const int32_t* __restrict__ col,
+                                                         const float* __restrict__ val,
+                                                         const float* __restrict__ X, int d,
+                                                         SpmmEpi ep) {
+  const int lane = threadIdx.x & 63;
+  if ((int64_t)blockIdx.x < nlb) {
+    const int64_t q = l0 + (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (q >= l1) return;
+    const int64_t r = long_rows[q];
+    const float4 y = row_sum<LPR>(col, val, X, d, rowptr[r], rowptr[r + 1], lane);
+    if (lane < LPR) spmm_epilogue(r, d, lane, y, X, ep);
+    return;
+  }
   constexpr int RPW = 64 / LPR;
-  const int lane = threadIdx.x & 63, sub = lane % LPR;
-  const int64_t r = r0 + ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW + lane / LPR;
+  const int sub = lane % LPR;
+  const int64_t r = r0 + ((int64_t)(blockIdx.x - nlb) * 4 + (threadIdx.x >> 6)) * RPW + lane / LPR;
   if (r >= r1) return;
   const int64_t s = rowptr[r], e = rowptr[r + 1];
-  if (e - s > heavy) return;  // segmented path
+  if (e - s > SPMM_SHORT) return;  // long / heavy class
   spmm_epilogue(r, d, sub, row_sum_grouped<LPR>(col, val, X, d, s, e, sub), X, ep);
 }
 
@@ -446,8 +471,8 @@ __global__ __launch_bounds__(256) void spmm_finish_kernel(int64_t h0,
 // segments sl, sl + S, ... in order from 0, then the pairwise tree over the slices
 // (w = S/2 .. 1), as spmm_finish_kernel does -- so listed heavy rows are bitwise equal to
 // forward() too.  Each lane only touches its own float4 column of the slice sums (LDS, one
-// S x LPR block per wave), so the wave needs no barrier.  Light rows use the light kernel's
-// layout (one wave per row, or with SPMM_GROUPED one LPR-lane group per row).
+// S x LPR block per wave), so the wave needs no barrier.  Every row is summed in the order of
+// its class (short: grouped; long: one wave; heavy: segments), as the layer kernels do.
 struct CombineLayers {
   const float* E[8];
   float a[9];
@@ -536,8 +561,8 @@ __global__ __launch_bounds__(256) void spmm_rows_combine_kernel(
     if (lane < LPR) combine_store(cl, r, d, lane, y, out, b);
     return;
   }
-  // grouped: group g = lane / LPR owns listed row b; light rows in the grouped order, heavy
-  // rows afterwards by the whole wave (uniform loop over the wave's groups)
+  // grouped: group g = lane / LPR owns listed row b; short rows in the grouped order, long and
+  // heavy rows afterwards by the whole wave (uniform loop over the wave's groups)
   constexpr int RPW = 64 / LPR;
   const int g = lane / LPR, sub = lane % LPR;
   const int64_t b0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW;
@@ -555,19 +580,21 @@ __global__ __launch_bounds__(256) void spmm_rows_combine_kernel(
     } else {
       rs = rowptr[r];
       re = rowptr[r + 1];
-      if (re - rs <= HEAVY)
+      if (re - rs <= SPMM_SHORT)
         combine_store(cl, r, d, sub, row_sum_grouped<LPR>(col, val, Xl, d, rs, re, sub), out, b);
     }
   }
-  const bool heavy = ok && re - rs > HEAVY;
-  uint64_t hm = __ballot(heavy && sub == 0);
+  // long and heavy rows: the whole wave, one row at a time
+  uint64_t hm = __ballot(ok && re - rs > SPMM_SHORT && sub == 0);
   while (hm) {
-    const int src = __builtin_ctzll(hm) ;
+    const int src = __builtin_ctzll(hm);
     hm &= hm - 1;
     const int64_t hb = b0 + src / LPR;
     const int64_t hr = rows[hb];
     const int64_t hs = rowptr[hr], he = rowptr[hr + 1];
-    const float4 y = heavy_row_sum<LPR>(col, val, Xl, d, hs, he, lane, slices[threadIdx.x >> 6]);
+    const float4 y = he - hs <= HEAVY
+                         ? row_sum<LPR>(col, val, Xl, d, hs, he, lane)
+                         : heavy_row_sum<LPR>(col, val, Xl, d, hs, he, lane, slices[threadIdx.x >> 6]);
     if (lane < LPR) combine_store(cl, hr, d, lane, y, out, hb);
   }
 }
@@ -580,8 +607,10 @@ extern "C" hnm_status hnm_spmm_plan_create(hnm_ctx* ctx, int64_t N, const int64_
   HNM_HIP_CHECK(hipStreamSynchronize(ctx->stream));
   std::vector<int32_t> hrows, shrow;
   std::vector<int64_t> sptr{0}, sstart, send;
+  std::vector<int32_t> lrows;
   for (int64_t r = 0; r < N; ++r) {
     const int64_t s = rp[r], e = rp[r + 1];
+    if (SPMM_GROUPED && e - s > SPMM_SHORT && e - s <= HEAVY) lrows.push_back((int32_t)r);
     if (e - s <= HEAVY) continue;
     const int32_t hi = (int32_t)hrows.size();
     hrows.push_back((int32_t)r);
@@ -600,6 +629,16 @@ extern "C" hnm_status hnm_spmm_plan_create(hnm_ctx* ctx, int64_t N, const int64_
   pl->n_seg = (int64_t)sstart.size();
   pl->h_heavy = new std::vector<int32_t>(hrows);
   pl->h_seg_ptr = new std::vector<int64_t>(sptr);
+  pl->n_long = (int64_t)lrows.size();
+  pl->h_long = new std::vector<int32_t>(lrows);
+  if (pl->n_long > 0) {
+    if (hipMalloc((void**)&pl->long_rows, pl->n_long * 4) != hipSuccess) {
+      hnm_spmm_plan_destroy(pl);
+      hnm_set_error("spmm_plan: hipMalloc failed");
+      return HNM_ENOMEM;
+    }
+    HNM_HIP_CHECK(hipMemcpy(pl->long_rows, lrows.data(), pl->n_long * 4, hipMemcpyHostToDevice));
+  }
   if (pl->n_heavy > 0) {
     if (hipMalloc((void**)&pl->heavy_rows, pl->n_heavy * 4) != hipSuccess ||
         hipMalloc((void**)&pl->seg_ptr, (pl->n_heavy + 1) * 8) != hipSuccess ||
@@ -627,6 +666,8 @@ extern "C" hnm_status hnm_spmm_plan_destroy(hnm_spmm_plan* pl) {
   if (pl->seg_hrow) (void)hipFree(pl->seg_hrow);
   if (pl->seg_start) (void)hipFree(pl->seg_start);
   if (pl->seg_end) (void)hipFree(pl->seg_end);
+  if (pl->long_rows) (void)hipFree(pl->long_rows);
+  delete pl->h_long;
   delete pl->h_heavy;
   delete pl->h_seg_ptr;
   free(pl);
@@ -677,12 +718,19 @@ static hnm_status spmm_launch(hnm_ctx* ctx, const hnm_spmm_plan* pl, int64_t N,
     }
   }
   if (r1 > r0) {
-    if (SPMM_GROUPED)
-      hipLaunchKernelGGL(spmm_grouped_kernel<LPR>, dim3((unsigned)hnm_cdiv(r1 - r0, 4 * (64 / LPR))),
-                         dim3(256), 0, ctx->stream, r0, r1, rowptr, col, val, X, d, ep, heavy);
-    else
+    if (SPMM_GROUPED && pl) {
+      // long rows inside [r0, r1) (ascending list) + every short row of the range
+      const std::vector<int32_t>& lv = *pl->h_long;
+      const int64_t l0 = std::lower_bound(lv.begin(), lv.end(), (int32_t)std::min<int64_t>(r0, INT32_MAX)) - lv.begin();
+      const int64_t l1 = std::lower_bound(lv.begin(), lv.end(), (int32_t)std::min<int64_t>(r1, INT32_MAX)) - lv.begin();
+      const int64_t nlb = hnm_cdiv(l1 - l0, 4), nsb = hnm_cdiv(r1 - r0, 4 * (64 / LPR));
+      hipLaunchKernelGGL(spmm_mixed_kernel<LPR>, dim3((unsigned)(nlb + nsb)), dim3(256), 0,
+                         ctx->stream, r0, r1, pl->long_rows, l0, l1, nlb, rowptr, col, val, X, d,
+                         ep);
+    } else {
       hipLaunchKernelGGL(spmm_light_kernel<LPR>, dim3((unsigned)hnm_cdiv(r1 - r0, 4)), dim3(256), 0,
                          ctx->stream, r0, r1, rowptr, col, val, X, d, ep, heavy);
+    }
     HNM_LAUNCH_CHECK();
   }
   if (forked) HNM_HIP_CHECK(hipStreamWaitEvent(ctx->stream, ctx->side_out, 0));

@@ -54,6 +54,9 @@ constexpr int CERT_MAX_NP = 64;           // item partitions (candidate segments
 constexpr int CERT_PROXY_USERS = 8;       // batch rows that pick the champion sample
 constexpr int64_t CERT_CHAMPIONS = 2048;  // champion sample size (item groups), at most
 constexpr int64_t CERT_GROUP_MIN = 48;    // items per champion group, at least
+#ifndef NCF_EPI_HYBRID  // THRESH epilogue: user a on the matrix pipe, user b by packed dots
+#define NCF_EPI_HYBRID 0
+#endif
 #ifndef HNM_SCAN_OCC
 #define HNM_SCAN_OCC 3
 #endif
@@ -339,10 +342,17 @@ __global__ __launch_bounds__(256) void cert_convert_kernel(
     _Float16* __restrict__ P16, _Float16* __restrict__ WG16, _Float16* __restrict__ Q16,
     _Float16* __restrict__ G16, const float* __restrict__ W2, int h1, int h2,
     const float* __restrict__ b2, const float* __restrict__ wm, _Float16* __restrict__ W2h,
-    _Float16* __restrict__ wmh, float* __restrict__ b2s) {
+    _Float16* __restrict__ wmh, float* __restrict__ b2s, const float* __restrict__ Bi,
+    const float* __restrict__ Cu, float* __restrict__ Bs, float* __restrict__ Cs) {
   const float s1 = prm->s1, sgu = prm->sgu, sgi = prm->sgi;
+  // the scan's bound terms in test units (CERT_RHO * unit * B_i, ... * C_u): the same fp32
+  // products the scan formed itself before, computed once here so the scan keeps no scale
+  // factor live across its tile loop
   const int64_t nthreads = (int64_t)gridDim.x * 256;
   const int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const float ru = CERT_RHO * prm->unit;
+  for (int64_t e = g; e < I; e += nthreads) Bs[e] = ru * Bi[e];
+  for (int64_t e = g; e < B; e += nthreads) Cs[e] = ru * Cu[e];
   // items: 16 chunks of 4 per row
   for (int64_t e = g; e < I * 16; e += nthreads) {
     const int64_t i = e >> 4;
@@ -396,9 +406,9 @@ struct ScanArgs {
   const _Float16* W2h;   // [32, 64]
   const _Float16* wmh;   // [32]
   const float* b2s;      // [32]
-  const float* Bi;       // [Itot] per-item bound terms
+  const float* Bi;       // [Itot] per-item bound terms (x CERT_RHO * unit: test units)
   const float* Di;
-  const float* Cu;       // [B] per-user bound terms
+  const float* Cu;       // [B] per-user bound terms (x CERT_RHO * unit)
   const float* Eu;       // [B] user-constant part of the bound, scaled (DEBUG)
   const CertParams* prm;
   int64_t B;
@@ -483,7 +493,7 @@ __global__ __launch_bounds__(256, HNM_SCAN_OCC) void ncf16_scan_kernel(ScanArgs 
   for (int r = 0; r < 16; ++r) b2c[r] = A.b2s[mfma32_row(r, h)];
   // epilogue A operands (16x16x32: lane holds A[row lane & 15][k = 8 (lane >> 4) + e])
   h8 ewa[2], ewb[2];
-  h2 wm2[8];  // DEBUG: wm of this lane's accumulator rows, in pairs
+  h2 wm2[8];  // DEBUG / hybrid THRESH: wm of this lane's accumulator rows, in pairs
   {
     const int erow = lane & 15, eg = lane >> 4;
 #pragma unroll
@@ -502,10 +512,8 @@ __global__ __launch_bounds__(256, HNM_SCAN_OCC) void ncf16_scan_kernel(ScanArgs 
   // uniform scalars in SGPRs (the compiler cannot prove prm read-only, so it would keep them
   // in VGPRs -- which are the scarce resource at three waves per SIMD)
   const float cg = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(A.prm->cg)));
-  const float ru =
-      __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(CERT_RHO * A.prm->unit)));
   // per-user registers: lane u < nu follows user u0 + u
-  const float cu = lane < nu ? ru * A.Cu[u0 + lane] : 0.f;
+  const float cu = lane < nu ? A.Cu[u0 + lane] : 0.f;
   float tv = __builtin_inff(), eu = 0.f;
   if (MODE == SCAN_THRESH && lane < nu) tv = A.tau[u0 + lane];
   if (MODE == SCAN_DEBUG && lane < nu) eu = A.Eu[u0 + lane];
@@ -580,7 +588,7 @@ __global__ __launch_bounds__(256, HNM_SCAN_OCC) void ncf16_scan_kernel(ScanArgs 
   for (int cur = 0; t < ntiles; cur ^= 1) {
     const int64_t base = part_start + t * TILE;
     const int64_t tn = t + 1;
-    const float bj = ru * nb, dj = nd;  // bound terms of this tile's item j
+    const float bj = nb, dj = nd;  // bound terms of this tile's item j (test units)
     // the prefetch is the only global load in the tile body (vmcnt waits are in order: any
     // later load's wait would also wait for it)
     if (tn < ntiles) fetch(part_start + tn * TILE);
@@ -671,8 +679,26 @@ __global__ __launch_bounds__(256, HNM_SCAN_OCC) void ncf16_scan_kernel(ScanArgs 
         f32x4 d = *reinterpret_cast<const f32x4*>(&g7[((u >> 1) * 16 + (lane & 15)) << 2]);
         d = __builtin_amdgcn_mfma_f32_16x16x32_f16(ewa[0], ya[0], d, 0, 0, 0);
         d = __builtin_amdgcn_mfma_f32_16x16x32_f16(ewa[1], ya[1], d, 0, 0, 0);
-        d = __builtin_amdgcn_mfma_f32_16x16x32_f16(ewb[0], yb[0], d, 0, 0, 0);
-        d = __builtin_amdgcn_mfma_f32_16x16x32_f16(ewb[1], yb[1], d, 0, 0, 0);
+        const bool hybrid = NCF_EPI_HYBRID && MODE == SCAN_THRESH;
+        float tb = 0.f;  // hybrid: user b's test value at lane j (item j), lanes 0-31
+        if (hybrid) {
+          // user b by packed dots: lane (j, h) sums its 16 accumulator rows, the two halves
+          // meet by one permlane32 swap (the DEBUG epilogue's arithmetic), + the folded term
+          float mb = 0.f;
+#pragma unroll
+          for (int f = 0; f < 2; ++f)
+#pragma unroll
+            for (int e = 0; e < 8; e += 2)
+              mb = __builtin_amdgcn_fdot2((h2){yb[f][e], yb[f][e + 1]}, wm2[(8 * f + e) >> 1], mb,
+                                          false);
+          const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(mb),
+                                                           __float_as_uint(mb), false, false);
+          const float gb = g7[(((u >> 1) * 16 + (j & 15)) << 2) + 2 + (j >> 4)];
+          tb = (__uint_as_float(sw[0]) + __uint_as_float(sw[1])) + gb;
+        } else {
+          d = __builtin_amdgcn_mfma_f32_16x16x32_f16(ewb[0], yb[0], d, 0, 0, 0);
+          d = __builtin_amdgcn_mfma_f32_16x16x32_f16(ewb[1], yb[1], d, 0, 0, 0);
+        }
         const uint64_t vmask = vm32 | (hasb ? vm32 << 32 : 0ull);
         if (MODE == SCAN_SAMPLE) {
           if (lane < 16) {
@@ -686,9 +712,15 @@ __global__ __launch_bounds__(256, HNM_SCAN_OCC) void ncf16_scan_kernel(ScanArgs 
         } else {
           const uint64_t m0 = __ballot(!(d[0] < 0.f)) & 0xffffull;
           const uint64_t m1 = __ballot(!(d[1] < 0.f)) & 0xffffull;
-          const uint64_t m2 = __ballot(!(d[2] < 0.f)) & 0xffffull;
-          const uint64_t m3 = __ballot(!(d[3] < 0.f)) & 0xffffull;
-          uint64_t m = (m0 | (m1 << 16) | (m2 << 32) | (m3 << 48)) & vmask;  // !(score + e_i < tau)
+          uint64_t mhi;
+          if (hybrid) {
+            mhi = (__ballot(!(tb < 0.f)) & 0xffffffffull) << 32;
+          } else {
+            const uint64_t m2 = __ballot(!(d[2] < 0.f)) & 0xffffull;
+            const uint64_t m3 = __ballot(!(d[3] < 0.f)) & 0xffffull;
+            mhi = (m2 << 32) | (m3 << 48);
+          }
+          uint64_t m = (m0 | (m1 << 16) | mhi) & vmask;  // !(score + e_i < tau)
           if (masked) {  // uniform: filtered items of the two users
             const unsigned mba = (unsigned)hnm_readlane_i((int)mbits, ua);
             const unsigned mbb = (unsigned)hnm_readlane_i((int)mbits, ub);
@@ -1009,6 +1041,7 @@ __global__ void cert_unscale_kernel(float* __restrict__ a, float* __restrict__ e
 struct CertWs {
   CertParams* prm;
   float *Au, *Cu, *Bi, *Di, *tau, *Eu, *b2s, *kthv, *lb, *pdense, *cdense, *part;
+  float *Bs, *Cs;  // Bi, Cu in the scan's test units (cert_convert_kernel)
   int32_t* sidx;  // champion items
   int64_t* kthi;
   int *cnt, *flag;
@@ -1061,6 +1094,8 @@ size_t cert_carve(char* base, int64_t B, int64_t I, int K, int num_cus, int wg, 
   x.prm = (CertParams*)take(sizeof(CertParams));
   x.Au = (float*)take(B * 4);
   x.Cu = (float*)take(B * 4);
+  x.Cs = (float*)take(B * 4);
+  x.Bs = (float*)take(I * 4);
   x.part = (float*)take(4 * 4 * (1024 + 256));
   x.Bi = (float*)take(I * 4);
   x.Di = (float*)take(I * 4);
@@ -1106,7 +1141,7 @@ hnm_status cert_prepare(hnm_ctx* ctx, const hnm_ncf_weights* w, const NcfTabs& t
   const int cb = (int)std::min<int64_t>(2048, std::max<int64_t>(1, hnm_cdiv(I * 16, 256)));
   hipLaunchKernelGGL(cert_convert_kernel, dim3(cb), dim3(256), 0, ctx->stream, t, B, I, w->mf,
                      x.prm, x.P16, x.WG16, x.Q16, x.G16, w->w2, w->h1, w->h2, w->b2,
-                     w->wp + w->mf, x.W2h, x.wmh, x.b2s);
+                     w->wp + w->mf, x.W2h, x.wmh, x.b2s, x.Bi, x.Cu, x.Bs, x.Cs);
   HNM_LAUNCH_CHECK();
   return HNM_OK;
 }
@@ -1125,9 +1160,9 @@ ScanArgs scan_args(const CertWs& x, int64_t B) {
   a.W2h = x.W2h;
   a.wmh = x.wmh;
   a.b2s = x.b2s;
-  a.Bi = x.Bi;
+  a.Bi = x.Bs;
   a.Di = x.Di;
-  a.Cu = x.Cu;
+  a.Cu = x.Cs;
   a.Eu = x.Eu;
   a.prm = x.prm;
   a.B = B;
