@@ -54,9 +54,6 @@ constexpr int CERT_MAX_NP = 64;           // item partitions (candidate segments
 constexpr int CERT_PROXY_USERS = 8;       // batch rows that pick the champion sample
 constexpr int64_t CERT_CHAMPIONS = 2048;  // champion sample size (item groups), at most
 constexpr int64_t CERT_GROUP_MIN = 48;    // items per champion group, at least
-#ifndef NCF_EPI_HYBRID  // THRESH epilogue: user a on the matrix pipe, user b by packed dots
-#define NCF_EPI_HYBRID 0
-#endif
 #ifndef HNM_SCAN_OCC
 #define HNM_SCAN_OCC 3
 #endif
@@ -447,7 +444,9 @@ __device__ __forceinline__ f32x16 mfma16(h8 a, h8 b, f32x16 c) {
 // 64-bit pass mask with bit u*32 + item (the lane layout of the append).  Measured against the
 // earlier packed-dot epilogue (16 v_dot2c + a permlane32 swap per pair, 1.94 ms) and a
 // software-pipelined two-waves-per-SIMD variant (2.1-2.2 ms): 1.87 ms (tools/scan_ablation.hip,
-// profiles/r2_ncf_scan_variants.txt).  DEBUG keeps a VALU epilogue (packed dots + swap).
+// profiles/r2_ncf_scan_variants.txt); splitting it (user a on the matrix pipe, user b by packed
+// dots) measured 2.03 vs 1.88 ms (round 3, profiles/r3c_ncf_epilogue_ab.txt): the VALU side is
+// the binding one.  DEBUG keeps a VALU epilogue (packed dots + swap).
 template <int MODE>
 __global__ __launch_bounds__(256, HNM_SCAN_OCC) void ncf16_scan_kernel(ScanArgs A) {
   constexpr int RS = 72;   // LDS row stride in halfs (144 B): conflict-free b128 reads
@@ -493,7 +492,7 @@ __global__ __launch_bounds__(256, HNM_SCAN_OCC) void ncf16_scan_kernel(ScanArgs 
   for (int r = 0; r < 16; ++r) b2c[r] = A.b2s[mfma32_row(r, h)];
   // epilogue A operands (16x16x32: lane holds A[row lane & 15][k = 8 (lane >> 4) + e])
   h8 ewa[2], ewb[2];
-  h2 wm2[8];  // DEBUG / hybrid THRESH: wm of this lane's accumulator rows, in pairs
+  h2 wm2[8];  // DEBUG: wm of this lane's accumulator rows, in pairs
   {
     const int erow = lane & 15, eg = lane >> 4;
 #pragma unroll
@@ -679,26 +678,8 @@ __global__ __launch_bounds__(256, HNM_SCAN_OCC) void ncf16_scan_kernel(ScanArgs 
         f32x4 d = *reinterpret_cast<const f32x4*>(&g7[((u >> 1) * 16 + (lane & 15)) << 2]);
         d = __builtin_amdgcn_mfma_f32_16x16x32_f16(ewa[0], ya[0], d, 0, 0, 0);
         d = __builtin_amdgcn_mfma_f32_16x16x32_f16(ewa[1], ya[1], d, 0, 0, 0);
-        const bool hybrid = NCF_EPI_HYBRID && MODE == SCAN_THRESH;
-        float tb = 0.f;  // hybrid: user b's test value at lane j (item j), lanes 0-31
-        if (hybrid) {
-          // user b by packed dots: lane (j, h) sums its 16 accumulator rows, the two halves
-          // meet by one permlane32 swap (the DEBUG epilogue's arithmetic), + the folded term
-          float mb = 0.f;
-#pragma unroll
-          for (int f = 0; f < 2; ++f)
-#pragma unroll
-            for (int e = 0; e < 8; e += 2)
-              mb = __builtin_amdgcn_fdot2((h2){yb[f][e], yb[f][e + 1]}, wm2[(8 * f + e) >> 1], mb,
-                                          false);
-          const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(mb),
-                                                           __float_as_uint(mb), false, false);
-          const float gb = g7[(((u >> 1) * 16 + (j & 15)) << 2) + 2 + (j >> 4)];
-          tb = (__uint_as_float(sw[0]) + __uint_as_float(sw[1])) + gb;
-        } else {
-          d = __builtin_amdgcn_mfma_f32_16x16x32_f16(ewb[0], yb[0], d, 0, 0, 0);
-          d = __builtin_amdgcn_mfma_f32_16x16x32_f16(ewb[1], yb[1], d, 0, 0, 0);
-        }
+        d = __builtin_amdgcn_mfma_f32_16x16x32_f16(ewb[0], yb[0], d, 0, 0, 0);
+        d = __builtin_amdgcn_mfma_f32_16x16x32_f16(ewb[1], yb[1], d, 0, 0, 0);
         const uint64_t vmask = vm32 | (hasb ? vm32 << 32 : 0ull);
         if (MODE == SCAN_SAMPLE) {
           if (lane < 16) {
@@ -712,15 +693,9 @@ __global__ __launch_bounds__(256, HNM_SCAN_OCC) void ncf16_scan_kernel(ScanArgs 
         } else {
           const uint64_t m0 = __ballot(!(d[0] < 0.f)) & 0xffffull;
           const uint64_t m1 = __ballot(!(d[1] < 0.f)) & 0xffffull;
-          uint64_t mhi;
-          if (hybrid) {
-            mhi = (__ballot(!(tb < 0.f)) & 0xffffffffull) << 32;
-          } else {
-            const uint64_t m2 = __ballot(!(d[2] < 0.f)) & 0xffffull;
-            const uint64_t m3 = __ballot(!(d[3] < 0.f)) & 0xffffull;
-            mhi = (m2 << 32) | (m3 << 48);
-          }
-          uint64_t m = (m0 | (m1 << 16) | mhi) & vmask;  // !(score + e_i < tau)
+          const uint64_t m2 = __ballot(!(d[2] < 0.f)) & 0xffffull;
+          const uint64_t m3 = __ballot(!(d[3] < 0.f)) & 0xffffull;
+          uint64_t m = (m0 | (m1 << 16) | (m2 << 32) | (m3 << 48)) & vmask;  // !(score + e_i < tau)
           if (masked) {  // uniform: filtered items of the two users
             const unsigned mba = (unsigned)hnm_readlane_i((int)mbits, ua);
             const unsigned mbb = (unsigned)hnm_readlane_i((int)mbits, ub);

@@ -74,20 +74,32 @@ class NeuralCF(RecModule):
 
     # ------------------------------------------------------------------ HIP plumbing
     def _weights(self):
+        """(hnm_ncf_weights, tensors it points into).  When every parameter already is a
+        contiguous fp32 GPU tensor the struct points at the parameters themselves and is reused
+        while their storages are unchanged (keyed on the data pointers: the kernels read the
+        values at call time, so in-place updates need no rebuild)."""
         lin = [m for m in self.mlp_layers if isinstance(m, nn.Linear)]
         if len(lin) != 2:
             raise ValueError(
                 "the fused NeuralCF kernel covers the reference's two-layer MLP tower "
                 f"(mlp_dims of length 3, e.g. [128, 64, 32]); got mlp_dims={self.mlp_dims}")
         l1, l2 = lin
-        keep = [f32c(self.gmf_user_embedding.weight), f32c(self.gmf_item_embedding.weight),
-                f32c(self.mlp_user_embedding.weight), f32c(self.mlp_item_embedding.weight),
-                f32c(l1.weight), f32c(l1.bias), f32c(l2.weight), f32c(l2.bias),
-                f32c(self.prediction_layer.weight).reshape(-1), f32c(self.prediction_layer.bias)]
+        params = (self.gmf_user_embedding.weight, self.gmf_item_embedding.weight,
+                  self.mlp_user_embedding.weight, self.mlp_item_embedding.weight,
+                  l1.weight, l1.bias, l2.weight, l2.bias, self.prediction_layer.weight,
+                  self.prediction_layer.bias)
+        key = tuple(p.data_ptr() for p in params)
+        cached = getattr(self, "_wcache", None)
+        if cached is not None and cached[0] == key:
+            return cached[1], cached[2]
+        keep = [f32c(p) for p in params]
+        keep[8] = keep[8].reshape(-1)
         _lib.require_gpu(*keep)
         w = _lib.NcfWeights(*[t.data_ptr() for t in keep], self.num_users, self.num_items,
                             self.mf_dim, self.mlp_dims[0] // 2, l1.out_features,
                             l2.out_features)
+        if all(t.data_ptr() == p.data_ptr() for t, p in zip(keep, params)):
+            self._wcache = (key, w, keep)   # no conversion copies: safe to reuse
         return w, keep
 
     # ------------------------------------------------------------------ reference API

@@ -146,6 +146,7 @@ class ncf_shard_topk:
 
     def _args(self, user_ids):
         w, keep = self.model._weights()
+        w = _lib.NcfWeights.from_buffer_copy(w)  # the module may reuse its struct: shift a copy
         mf, h0 = self.model.mf_dim, self.model.mlp_dims[0] // 2
         w.gmf_item = w.gmf_item + self.lo * mf * 4
         w.mlp_item = w.mlp_item + self.lo * h0 * 4
@@ -264,6 +265,7 @@ def widedeep_shard_topk(model, lo: int, hi: int, k: int, history=None) -> LocalT
     `history` (a UserHistory) masks each user's history items."""
     def run(user_ids: torch.Tensor):
         w, keep = model._weights()
+        w = _lib.WideDeepWeights.from_buffer_copy(w)
         d = model.embedding_dim
         w.deep_item = w.deep_item + lo * d * 4
         w.wide_item = w.wide_item + lo * 4

@@ -158,3 +158,5 @@ def test_sharded_history_masks_merge_to_full():
             ci.append(torch.where(i >= 0, i + lo, i))
         got = S.hip_merge(torch.stack(cv), torch.stack(ci), K)
         _same(got, ref, f"{name} 3-shard filtered")
+    # the shard scorers shift copies of the module's (cached) weight struct, never the struct
+    _same(ncf.recommend_with_scores(u, filter_items=h), cases[0][2], "ncf module after shards")
