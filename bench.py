@@ -214,6 +214,54 @@ def timed_rate(fn, batches, steps, world, B):
     return B * world * steps / el
 
 
+def pipelined_rate(fn, batches, steps, B, nstreams=3):
+    """users/s with `nstreams` independent batches in flight: one worker thread per torch
+    stream (hence one hnm_ctx each), batches dealt round-robin, every call complete (nothing
+    shared across calls, no work skipped); the outputs are compared bitwise with the
+    sequential answers of the same batches.  3 streams, not 2: with GPU_MAX_HW_QUEUES = 4 two
+    pool streams can land on one hardware queue and serialize."""
+    import threading
+    ref = [fn(b) for b in batches]
+    torch.cuda.synchronize()
+    streams = [torch.cuda.Stream() for _ in range(nstreams)]
+    outs = [None] * steps
+    errs = []
+    start = threading.Barrier(nstreams + 1)
+    dev = torch.cuda.current_device()
+
+    def work(w):
+        try:
+            torch.cuda.set_device(dev)
+            with torch.cuda.stream(streams[w]):
+                fn(batches[w % len(batches)])  # this thread's ctx + workspace
+                torch.cuda.current_stream().synchronize()
+                start.wait()
+                for j in range(w, steps, nstreams):
+                    outs[j] = fn(batches[j % len(batches)])
+                torch.cuda.current_stream().synchronize()
+        except BaseException as e:  # reported below
+            errs.append(e)
+            start.abort()
+
+    ts = [threading.Thread(target=work, args=(w,)) for w in range(nstreams)]
+    for t in ts:
+        t.start()
+    try:
+        start.wait()
+    except threading.BrokenBarrierError:
+        pass
+    t0 = time.perf_counter()
+    for t in ts:
+        t.join()
+    el = time.perf_counter() - t0
+    if errs:
+        raise errs[0]
+    same = all(torch.equal(outs[j][1], ref[j % len(batches)][1]) and
+               torch.equal(outs[j][0].view(torch.int32), ref[j % len(batches)][0].view(torch.int32))
+               for j in range(steps))
+    return B * steps / el, same
+
+
 def _median_rate(fn, users, runs, budget_s):
     """users/s of fn(users): median of up to `runs` timed calls within ~budget_s."""
     times = []
@@ -419,6 +467,10 @@ def main():
                          "best items are user-specific (emb_scale 20, biases)")
     ap.add_argument("--exact", action="store_true",
                     help="exact fp32 scan of every item instead of the certified f16 pre-filter")
+    ap.add_argument("--profile-only", action="store_true",
+                    help="the headline timed loop only (no exact / filtered / module-surface / "
+                         "pipelined / baseline legs): what the rocprofv3 kernel stats in "
+                         "profiles/ are collected over, so their averages match `roofline`")
     ap.add_argument("--no-extras", action="store_true",
                     help="default NCF run only: skip the other workloads' lines and the B=1 "
                          "serve latencies (otherwise measured after the headline, N=1 only)")
@@ -467,7 +519,9 @@ def main():
     _lib.set_option(device, _lib.HNM_OPT_STATS, 0)
     pf_rows, pf_cands, pf_fallback = _lib.prefilter_stats(device, reset=True)
     exact_rate = None
-    if not args.exact:
+    if args.profile_only:
+        args.no_extras = args.no_cpu_baseline = True
+    if not args.exact and not args.profile_only:
         # the like-for-like fp32 path (HNM_OPT_PREFILTER=0: every pair scored in exact fp32
         # arithmetic), timed the same way on the same batches, reported beside `value`
         _lib.set_prefilter(device, False)
@@ -546,7 +600,7 @@ def main():
             "random_data_mfma_rate": RANDOM_DATA_F16_TFLOPS,
             "frac_of_random_data_rate": round(rate / RANDOM_DATA_F16_TFLOPS, 3),
             "source": "tools/mfma_shape_probe.hip, profiles/r2_mfma_shape_probe.txt"}
-    if "_serving" in info and rank == 0 and world == 1:
+    if "_serving" in info and rank == 0 and world == 1 and not args.profile_only:
         # serving rate with the propagation computed once (weights unchanged between calls);
         # reported beside `value`, never as it
         serve = info["_serving"]()
@@ -563,7 +617,7 @@ def main():
             "value": round(B * world * exact_rate[1] / exact_rate[0], 2), "unit": "users/s",
             "steps": exact_rate[1],
             "note": "same step with HNM_OPT_PREFILTER=0: every (user, item) pair in exact fp32"}
-    if "_filtered" in info and not args.exact:
+    if "_filtered" in info and not args.exact and not args.profile_only:
         # purchase-history filter (the reference's filter_items / serve.py:350-352): every
         # user's history = its interactions in the synthetic H&M transactions (the LightGCN
         # graph's edges, mean 23.2 items), held on the device as a UserHistory; each step
@@ -608,7 +662,22 @@ def main():
                     "`value` includes" if args.workload.startswith("lightgcn") else ""))
             line["module_surface"] = out
         del hist
-    if "_full_step" in info:
+    if (world == 1 and args.workload in ("ncf", "mf", "lightgcn") and not args.exact
+            and not args.profile_only):
+        # serving throughput with independent batches overlapped on 3 HIP streams (the small
+        # per-call kernels and re-scoring of one batch run beside another batch's scan);
+        # reported beside `value` (one batch in flight), never as it
+        try:
+            np_ = min(args.steps * 2, 60)
+            prate, same = pipelined_rate(step, batches, np_, B)
+            line["pipelined_3_streams"] = {
+                "value": round(prate, 2), "unit": "users/s", "steps": np_,
+                "vs_value": round(prate / value, 4), "bitwise_equal_to_sequential": same,
+                "note": "3 worker threads, each with its own torch stream and hnm_ctx, full "
+                        "recommend() calls on independent batches; what a threaded server gets"}
+        except Exception as e:  # reported, never fatal
+            log(f"pipelined leg failed: {e!r}")
+    if "_full_step" in info and not args.profile_only:
         full = info["_full_step"]
         full(batches[0])
         torch.cuda.synchronize()

@@ -30,7 +30,7 @@ if [ -n "$PROF" ]; then
     [ $w = widedeep ] && extra="--steps 3 --warmup 1"
     echo "== prof $w $(date +%T)"
     timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_$w" -o $w -- \
-      python3 "$ROOT/bench.py" --workload $w $extra --no-cpu-baseline --no-extras > "$OUT/prof_$w.log" 2>&1 \
+      python3 "$ROOT/bench.py" --workload $w $extra --profile-only > "$OUT/prof_$w.log" 2>&1 \
       || { echo "rocprof $w failed"; exit 1; }
   done
 fi
