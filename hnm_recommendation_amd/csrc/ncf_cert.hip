@@ -696,7 +696,9 @@ __global__ __launch_bounds__(256, HNM_SCAN_OCC) void ncf16_scan_kernel(ScanArgs 
           const uint64_t m2 = __ballot(!(d[2] < 0.f)) & 0xffffull;
           const uint64_t m3 = __ballot(!(d[3] < 0.f)) & 0xffffull;
           uint64_t m = (m0 | (m1 << 16) | (m2 << 32) | (m3 << 48)) & vmask;  // !(score + e_i < tau)
-          if (masked) {  // uniform: filtered items of the two users
+          // filtered items of the two users, looked up only for a pair with a pass (a few % of
+          // pairs): two readlanes per pair in the issue-bound loop cost ~7 % of the scan
+          if (masked && m) {  // uniform
             const unsigned mba = (unsigned)hnm_readlane_i((int)mbits, ua);
             const unsigned mbb = (unsigned)hnm_readlane_i((int)mbits, ub);
             m &= ~((uint64_t)mba | ((uint64_t)mbb << 32));
