@@ -18,6 +18,7 @@
 // Layer-2 row blocks are processed 4 at a time (64 accumulator registers) and fed into
 // the layer-3 accumulators (64 registers) as they complete.
 #include <algorithm>
+#include <type_traits>
 
 #include "hnm_device.h"
 #include "hnm_internal.h"
@@ -465,6 +466,16 @@ typedef _Float16 wh8 __attribute__((ext_vector_type(8)));
 #ifndef WD_SPLIT_PASSES3
 #define WD_SPLIT_PASSES3 1  // layer 3: W_hi x_hi only (both residuals bounded)
 #endif
+// One-pass layer 2 (WD_SPLIT_PASSES = 1) with the bound's layer-2 terms on the matrix pipe: per k
+// step and user two v_mfma_f32_16x16x32_f16 whose A rows 0 / 1 carry sb v1 (B = x_hi) and
+// sb (v1 + 1.001 v1o / g1) (B = |x_lo|) for the items c / c + 16 of the 32x32 operand layout,
+// rounded UP to f16 (wdc_boundfrag_kernel), accumulated over the first row-block pass only:
+//   g1 v1.x + 1.001 v1o.|x - x_hi|  <=  g1 (v1.x_hi + (v1 + 1.001 v1o / g1).|x_lo|)
+// (x = x_hi + x_lo exactly, |x_lo| rounded to f16 costs 2^-10 relative, in the A rows).  This
+// replaces the 16 VALU fmas per user and k step that bound the VALU-bound one-pass kernel.
+#ifndef WD_BOUND_MFMA
+#define WD_BOUND_MFMA 1
+#endif
 
 __device__ __forceinline__ f32x16 wd_mfma16(wh8 a, wh8 b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
@@ -504,6 +515,7 @@ struct WdCertParams {
   float c2, c3;            // layer-2 accumulator -> x2 scale, layer-3 accumulator -> real
   float inv_s2;
   float g1, g2, g3, g4, cb, absb, rho;
+  float sb, inv_sb;        // scale of the bound A rows (one-pass layer 2, WD_BOUND_MFMA)
   int bad;                 // bound unusable: every row takes the exact path
 };
 
@@ -695,7 +707,19 @@ __global__ __launch_bounds__(256) void wdc_params_kernel(hnm_widedeep_weights w,
       }
     }
   }
+  // scale of the bound A rows (WD_BOUND_MFMA): max over k of v1 + (1.001 / g1) v1o, the larger row
+  __shared__ float ared[4];
+  __syncthreads();  // every thread's v1 / v1o entries are written
+  float amax = 0.f;
+  if (WD_SPLIT_PASSES == 1 && WD_BOUND_MFMA) {
+    const float g1c = (2.125f * K1P + 22.f) * 5.9604645e-08f;
+    for (int t = tid; t < K1P; t += 256) amax = wd_nmax(amax, v1[t] + (1.0009765625f / g1c) * v1o[t]);
+  }
+  for (int o = 32; o >= 1; o >>= 1) amax = wd_nmax(amax, __shfl_xor(amax, o));
+  if (lane == 0) ared[wave] = amax;
+  __syncthreads();
   if (tid != 0) return;
+  amax = wd_nmax(wd_nmax(ared[0], ared[1]), wd_nmax(ared[2], ared[3]));
   const float u = 5.9604645e-08f;  // 2^-24
   const float phi = 2.98023224e-08f;  // 2^-25: half the f16 subnormal spacing
   const float sumv2t = red2[0][0] + red2[0][1] + red2[0][2] + red2[0][3];
@@ -720,6 +744,9 @@ __global__ __launch_bounds__(256) void wdc_params_kernel(hnm_widedeep_weights w,
            (bc[5] / s1 + sumv2t * K1P * (bc[0] + bc[1]) / sw2 + sumv2t / s2 +
             (p.OB > 0 ? sumwdt * n2 * M2 / sw3 : 0.f));
   c.rho = 1.015625f;
+  c.sb = amax > 0.f ? 16384.f * wd_pow2_below_inv(amax * 1.01f) : 1.f;
+  c.inv_sb = 1.f / c.sb;
+  bad |= !(amax <= lim) || !(c.sb >= 1e-30f && c.sb <= 1e30f);
   bad |= !(c.absb <= lim) || !(c.c2 > 0.f && c.c2 <= lim) || !(c.c3 > 0.f && c.c3 <= lim);
   c.bad = bad;
   *prm = c;
@@ -775,12 +802,49 @@ __global__ __launch_bounds__(256) void wdc_convert_kernel(hnm_widedeep_weights w
   }
 }
 
+// f16 rounded toward +inf (for v >= 0: every bound operand is nonnegative)
+__device__ __forceinline__ _Float16 wd_f16_up(float v) {
+  _Float16 h = (_Float16)v;
+  if ((float)h < v) h = __builtin_bit_cast(_Float16, (unsigned short)(__builtin_bit_cast(unsigned short, h) + 1));
+  return h;
+}
+
+// Bound A fragments of the one-pass layer 2 (WD_BOUND_MFMA): WBf[(typ * KB + kb) * 64 + lane], the
+// 16x16x32 A operand (lane l holds A[l & 15][8 (l >> 4) + t]).  Row 0 takes the k-groups of items
+// c (lane groups 0 / 2 of the 32x32 B layout: k = 16 kb + 8 (g >> 1) + t), row 1 those of items
+// c + 16 (groups 1 / 3); every other entry is 0.  typ 0 multiplies x_hi: sb v1; typ 1 multiplies
+// |x_lo|: sb (v1 + 1.001 v1o / g1) (1 + 2^-10) -- the 2^-10 covers |x_lo|'s f16 rounding, the
+// 2^-20 the fp32 evaluation; rounded up.
+__global__ __launch_bounds__(256) void wdc_boundfrag_kernel(const WdCertParams* __restrict__ prm,
+                                                            const float* __restrict__ v1,
+                                                            const float* __restrict__ v1o, int K1P,
+                                                            wh8* __restrict__ WBf) {
+  const int KB = K1P / 16;
+  const float sb = prm->sb;
+  const float c1 = 1.0009765625f / ((2.125f * K1P + 22.f) * 5.9604645e-08f);
+  for (int e = blockIdx.x * 256 + threadIdx.x; e < KB * 2 * 64; e += gridDim.x * 256) {
+    const int lane = e & 63, q = e >> 6, kb = q % KB, typ = q / KB;
+    const int row = lane & 15, g = lane >> 4;
+    wh8 out = {};
+    if (row == (g & 1)) {
+#pragma unroll
+      for (int t = 0; t < 8; ++t) {
+        const int k = 16 * kb + 8 * (g >> 1) + t;
+        const float v = typ == 0 ? v1[k] : (v1[k] + c1 * v1o[k]) * (1.0009765625f * 1.00000095367f);
+        out[t] = wd_f16_up(v * sb);
+      }
+    }
+    WBf[e] = out;
+  }
+}
+
 struct WdScanArgs {
   const float* Pu;  // [B, K1P]  pair-permuted layer-1 user part (+ b1)
   const float* Qi;  // [I, K1P]  pair-permuted layer-1 item part
   int K1P;
   const wh8* W2hl;
   const wh8* W3hl;
+  const wh8* WBf;    // [KB * 2 * 64] bound A fragments (WD_BOUND_MFMA)
   const float* v1;   // [K1P]
   const float* v1o;  // [K1P] v1 without the dropped-pass terms (one-pass layer 2)
   const float* v2;   // [RB2*32]
@@ -830,6 +894,7 @@ __global__ __launch_bounds__(256, UPW == 1 ? 2 : 1) void wdc_scan_kernel(WdScanA
   constexpr int NOB = OB > 0 ? OB : 1;
   constexpr int NL = OB > 0 ? OB : RB2;
   constexpr int NU = 4 * UPW;  // users per block
+  constexpr bool BM = WD_SPLIT_PASSES == 1 && WD_BOUND_MFMA;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int K1P = A.K1P, KB = K1P / 16, QRS = K1P + 4;
   float* qs = smem;               // [32][QRS]
@@ -945,8 +1010,18 @@ __global__ __launch_bounds__(256, UPW == 1 ? 2 : 1) void wdc_scan_kernel(WdScanA
     float fin[UPW], bx1[UPW], bx2[UPW], bx3[UPW], bxl[UPW];
 #pragma unroll
     for (int v = 0; v < UPW; ++v) fin[v] = bx1[v] = bx2[v] = bx3[v] = bxl[v] = 0.f;
+    // the bound's layer-2 terms on the matrix pipe (WD_BOUND_MFMA): 16x16 accumulators, rows 0 / 1
+    // of lanes 0-15 = items c / c + 16
+    f32x4 accb[UPW];
+#pragma unroll
+    for (int v = 0; v < UPW; ++v) accb[v] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // one pass over k per G2 row blocks (NG passes); the bound MFMAs: with NG = 2 pass 0 takes
+    // the x_hi rows, pass 1 the |x_lo| rows (one 16x16x32 MFMA per user and k step each); NG = 1
+    // both.  One loop body for every pass: duplicating it for the passes spilled 300+ registers
+    constexpr int NG2 = RB2 / G2;
+    static_assert(!BM || NG2 <= 2, "bound MFMA split assumes at most two row-block passes");
 #pragma unroll 1
-    for (int g = 0; g < RB2 / G2; ++g) {
+    for (int g = 0; g < NG2; ++g) {
       f32x16 acc2[UPW][G2];
 #pragma unroll
       for (int v = 0; v < UPW; ++v)
@@ -986,6 +1061,11 @@ __global__ __launch_bounds__(256, UPW == 1 ? 2 : 1) void wdc_scan_kernel(WdScanA
                         fmaxf(fmaf(q0.z, s1, p0.z), 0.f), fmaxf(fmaf(q0.w, s1, p0.w), 0.f),
                         fmaxf(fmaf(q1.x, s1, p1.x), 0.f), fmaxf(fmaf(q1.y, s1, p1.y), 0.f),
                         fmaxf(fmaf(q1.z, s1, p1.z), 0.f), fmaxf(fmaf(q1.w, s1, p1.w), 0.f)};
+          if constexpr (BM) {  // x_hi and |x_lo| (the bound MFMAs' B operands)
+            wd_split8(x, oh[v], ol[v]);
+            ol[v] = __builtin_elementwise_abs(ol[v]);
+            continue;
+          }
           float bb = bx1[v];
           bb = fmaf(va.x, x[0], bb); bb = fmaf(va.y, x[1], bb);
           bb = fmaf(va.z, x[2], bb); bb = fmaf(va.w, x[3], bb);
@@ -1011,7 +1091,8 @@ __global__ __launch_bounds__(256, UPW == 1 ? 2 : 1) void wdc_scan_kernel(WdScanA
       // one k step: MFMAs on the (ah, xh, xl) set while the other set is loaded / formed for
       // step kb + 1
       auto step = [&](int kb, const wh8 (&ah)[G2], wh8 (&an)[G2], const wh8 (&xh)[UPW],
-                      const wh8 (&xl)[UPW], wh8 (&nxh)[UPW], wh8 (&nxl)[UPW]) {
+                      const wh8 (&xl)[UPW], wh8 (&nxh)[UPW], wh8 (&nxl)[UPW], const wh8 (&bc)[2],
+                      wh8 (&bn)[2]) {
         const bool more = kb + 1 < KB;
         const int kn = more ? kb + 1 : kb;
         wh8 al[G2];
@@ -1019,6 +1100,10 @@ __global__ __launch_bounds__(256, UPW == 1 ? 2 : 1) void wdc_scan_kernel(WdScanA
         for (int gi = 0; gi < G2; ++gi) {
           an[gi] = frag(gi, kn, 0);
           if (WD_SPLIT_PASSES == 3) al[gi] = frag(gi, kb, 1);
+        }
+        if constexpr (BM) {
+          bn[0] = A.WBf[((NG2 == 1 ? 0 : g) * KB + kn) * 64 + lane];
+          if (NG2 == 1) bn[1] = A.WBf[(KB + kn) * 64 + lane];
         }
 #pragma unroll
         for (int gi = 0; gi < G2; ++gi)
@@ -1035,6 +1120,18 @@ __global__ __launch_bounds__(256, UPW == 1 ? 2 : 1) void wdc_scan_kernel(WdScanA
 #pragma unroll
             for (int v = 0; v < UPW; ++v) acc2[v][gi] = wd_mfma16(al[gi], xh[v], acc2[v][gi]);
         }
+        if constexpr (BM) {
+#pragma unroll
+          for (int v = 0; v < UPW; ++v) {
+            if (NG2 == 1) {
+              accb[v] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bc[0], xh[v], accb[v], 0, 0, 0);
+              accb[v] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bc[1], xl[v], accb[v], 0, 0, 0);
+            } else {
+              const wh8 bop = g == 0 ? xh[v] : xl[v];
+              accb[v] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bc[0], bop, accb[v], 0, 0, 0);
+            }
+          }
+        }
         form(kn, more ? v1p : v0s, more ? vop : v0s, nxh, nxl);
         // next tile's copy: write the slice loaded last step, load the next one
 #pragma unroll
@@ -1048,21 +1145,29 @@ __global__ __launch_bounds__(256, UPW == 1 ? 2 : 1) void wdc_scan_kernel(WdScanA
           // 268-272 ms; 2, 3, 5, 6, 8 VALU per MFMA 305-315 ms, compiler order 331 ms)
           __builtin_amdgcn_sched_group_barrier(0x100, 4 + 2 * UPW, 0);
 #pragma unroll
-          for (int i = 0; i < WD_SPLIT_PASSES * G2 * UPW; ++i) {
+          for (int i = 0; i < WD_SPLIT_PASSES * G2 * UPW + (BM ? (3 - NG2) * UPW : 0); ++i) {
             __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
             __builtin_amdgcn_sched_group_barrier(0x002, WDC_VPM, 0);
           }
         }
       };
-      wh8 fa[G2], fb[G2], xha[UPW], xla[UPW], xhb[UPW], xlb[UPW];
+      wh8 fa[G2], fb[G2], xha[UPW], xla[UPW], xhb[UPW], xlb[UPW], ba[2], bb[2];
       form(0, v1p, vop, xha, xla);
 #pragma unroll
       for (int gi = 0; gi < G2; ++gi) fa[gi] = frag(gi, 0, 0);
+      if constexpr (BM) {
+        ba[0] = A.WBf[((NG2 == 1 ? 0 : g) * KB) * 64 + lane];
+        if (NG2 == 1) ba[1] = A.WBf[KB * 64 + lane];
+      }
       // (steps in pairs with the two register sets swapped instead of copied: 266 ms vs 261)
       for (int kb = 0; kb < KB; ++kb) {
-        step(kb, fa, fb, xha, xla, xhb, xlb);
+        step(kb, fa, fb, xha, xla, xhb, xlb, ba, bb);
 #pragma unroll
         for (int gi = 0; gi < G2; ++gi) fa[gi] = fb[gi];
+        if constexpr (BM) {
+          ba[0] = bb[0];
+          ba[1] = bb[1];
+        }
 #pragma unroll
         for (int v = 0; v < UPW; ++v) {
           xha[v] = xhb[v];
@@ -1167,9 +1272,17 @@ __global__ __launch_bounds__(256, UPW == 1 ? 2 : 1) void wdc_scan_kernel(WdScanA
         fin[v] *= inv_s2;
       }
       const float fv = hnm_sum_halves(fin[v]);
-      const float b1 = hnm_sum_halves(bx1[v]);
-      // one-pass layer 2's x_lo term (x 1 + 2^-10: |W_hi| <= (1 + 2^-11)|W'| and the sums)
-      const float bl1 = WD_SPLIT_PASSES == 1 ? 1.0009765625f * hnm_sum_halves(bxl[v]) : 0.f;
+      float b1, bl1;
+      if constexpr (BM) {
+        // item j's row of the bound accumulators: lane j (< 16) row 0, lane j - 16 row 1
+        const float d0 = __shfl(accb[v][0], lane & 15), d1 = __shfl(accb[v][1], lane & 15);
+        b1 = ((lane & 31) < 16 ? d0 : d1) * (A.prm->inv_sb * inv_s1);
+        bl1 = 0.f;  // inside b1 (A rows of the |x_lo| operand)
+      } else {
+        b1 = hnm_sum_halves(bx1[v]);
+        // one-pass layer 2's x_lo term (x 1 + 2^-10: |W_hi| <= (1 + 2^-11)|W'| and the sums)
+        bl1 = WD_SPLIT_PASSES == 1 ? 1.0009765625f * hnm_sum_halves(bxl[v]) : 0.f;
+      }
       const float b2 = hnm_sum_halves(bx2[v]);
       const float b3 = hnm_sum_halves(bx3[v]);
       const float score = fv + cub[v] + wi;
@@ -1555,6 +1668,7 @@ struct WdcWs {
   WdCertParams* prm;
   wh8* W2hl;
   wh8* W3hl;
+  wh8* WBf;
   float* v1;
   float* v1o;
   float* v2;
@@ -1598,6 +1712,7 @@ static size_t wdc_carve(const hnm_ctx* ctx, const WdPrep& pr, int64_t B, int64_t
   t.prm = (WdCertParams*)take(sizeof(WdCertParams));
   t.W2hl = (wh8*)take((size_t)pr.RB2 * KB * 2 * 64 * 16);
   t.W3hl = (wh8*)take((size_t)std::max(pr.OB, 1) * 2 * pr.RB2 * 2 * 64 * 16);
+  t.WBf = (wh8*)take((size_t)KB * 2 * 64 * 16);
   t.v1 = (float*)take((size_t)K1P * 4);
   t.v1o = (float*)take((size_t)K1P * 4);
   t.v2 = (float*)take((size_t)pr.RB2 * 32 * 4);
@@ -1633,6 +1748,9 @@ static hnm_status wdc_prepare(hnm_ctx* ctx, const hnm_widedeep_weights* w, const
                      WDC_STAT_BLOCKS, c.v1, c.v2, c.b2s, c.prm, c.v1o);
   hipLaunchKernelGGL(wdc_convert_kernel, dim3(256), dim3(256), 0, s, *w, S.pr, c.prm, c.W2hl,
                      c.W3hl);
+  if (WD_SPLIT_PASSES == 1 && WD_BOUND_MFMA)
+    hipLaunchKernelGGL(wdc_boundfrag_kernel, dim3((unsigned)hnm_cdiv(S.K1P / 16 * 2 * 64, 256)),
+                       dim3(256), 0, s, c.prm, c.v1, c.v1o, S.K1P, c.WBf);
   HNM_LAUNCH_CHECK();
   return HNM_OK;
 }
@@ -1665,6 +1783,7 @@ static hnm_status wdc_scan(hnm_ctx* ctx, const hnm_widedeep_weights* w, const Wd
   a.K1P = S.K1P;
   a.W2hl = c.W2hl;
   a.W3hl = c.W3hl;
+  a.WBf = c.WBf;
   a.v1 = c.v1;
   a.v1o = c.v1o;
   a.v2 = c.v2;
