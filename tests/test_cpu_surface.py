@@ -96,6 +96,28 @@ def test_filter_csr_host_logic():
         filter_csr(ids, {7: {10}}, 10, torch.device("cpu"))
 
 
+def test_user_history_csr_host_logic():
+    """UserHistory's host-side CSR (the device gather itself is a GPU test): per user sorted,
+    de-duplicated, negative ids wrapped, users outside [0, U) and empty sets ignored; the
+    interaction-array builder gives the same CSR as the dict builder."""
+    from hnm_recommendation_amd import UserHistory
+    U, I = 6, 10
+    h = {1: {3, 1, 1, -1}, 4: {2}, 5: set(), 9: {1}}
+    uh = UserHistory(h, U, I, "cpu")
+    assert uh.hist_ptr.tolist() == [0, 0, 3, 3, 3, 4, 4]
+    assert uh.hist_idx.tolist() == [1, 3, 9, 2]
+    assert uh.max_len == 3 and uh.nnz == 4
+    u = np.array([1, 1, 1, 1, 4])
+    i = np.array([3, 1, 1, 9, 2])
+    ui = UserHistory.from_interactions(u, i, U, I, "cpu")
+    assert torch.equal(ui.hist_ptr, uh.hist_ptr) and torch.equal(ui.hist_idx, uh.hist_idx)
+    with pytest.raises(IndexError):
+        UserHistory({0: {10}}, U, I, "cpu")
+    with pytest.raises(IndexError):
+        UserHistory.from_interactions(np.array([0]), np.array([I]), U, I, "cpu")
+    assert UserHistory({}, U, I, "cpu").mask_for(torch.tensor([0])) == (None, None)
+
+
 # ------------------------------------------------------------------ serving / checkpoints
 def test_checkpoint_dispatch_on_cpu(tmp_path):
     """serve.py:216-258: directory-name substring -> class, hparams override, state load
