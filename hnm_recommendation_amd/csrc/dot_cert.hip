@@ -33,7 +33,13 @@ typedef _Float16 h8 __attribute__((ext_vector_type(8)));
 namespace {
 
 constexpr int64_t DCERT_MIN_ITEMS = 8192;
-constexpr int64_t DCERT_SAMPLE = 12288;
+#ifndef DCERT_SAMPLE_N
+#define DCERT_SAMPLE_N 12288
+#endif
+constexpr int64_t DCERT_SAMPLE = DCERT_SAMPLE_N;
+#ifndef DCERT_MIN_STRIDE
+#define DCERT_MIN_STRIDE 8
+#endif  // sampled items: stride max(8, I / this)
 constexpr float DCERT_RHO = 0.00146484375f;  // 3 u16 = 3 * 2^-11
 constexpr int DCERT_MAX_NP = 64;
 #ifndef DOT_WG64
@@ -101,7 +107,7 @@ Partition xcd_partition(int64_t I, int64_t ublocks, int num_cus, int DP) {
 DotCertShape dcert_shape(int64_t B, int64_t I, int d, int K, int num_cus) {
   DotCertShape sh;
   sh.DP = d <= 64 ? 64 : 128;
-  sh.stride = std::max<int64_t>(8, I / DCERT_SAMPLE);  // sample <= 1/8 of the items (shards too)
+  sh.stride = std::max<int64_t>(DCERT_MIN_STRIDE, I / DCERT_SAMPLE);  // sample <= 1/stride of the items
   sh.Ns = hnm_cdiv(I, sh.stride);
   sh.part = xcd_partition(I, hnm_cdiv(B, 128), num_cus, sh.DP);
   sh.spart = xcd_partition(sh.Ns, hnm_cdiv(B, 128), num_cus, sh.DP);
@@ -506,6 +512,21 @@ __global__ __launch_bounds__(256, dcert_wg_per_cu(DP)) void dot16_scan_kernel(DS
         for (int s = 0; s < KS; ++s) {
           accA = mfma16(a[s], *reinterpret_cast<const h8*>(&vs[cur][(TILE * u + j) * RS + 16 * s + 8 * h]), accA);
           accB = mfma16(a[s], *reinterpret_cast<const h8*>(&vs[cur][(TILE * (u + 1) + j) * RS + 16 * s + 8 * h]), accB);
+        }
+        if (MODE == DSCAN_SAMPLE && hasB && baseB + TILE <= part_end) {
+          // both sub-tiles fully inside the partition (uniform): per row one v_max3 over the
+          // pair.  No NaN handling needed: a non-finite table entry marks the whole call bad
+          // (dcert_scales_kernel, NaN-propagating maxima) and every row takes the exact path
+          if (masked) {
+            apply_mask(accA, baseA, baseA + j);
+            apply_mask(accB, baseB, baseB + j);
+          }
+          const float ibA = BIAS ? ibl[cur][TILE * u + j] : 0.f;
+          const float ibB = BIAS ? ibl[cur][TILE * (u + 1) + j] : 0.f;
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            rmax[r] = fmaxf(rmax[r], fmaxf(BIAS ? accA[r] + ibA : accA[r], BIAS ? accB[r] + ibB : accB[r]));
+          continue;
         }
 #pragma unroll
         for (int v = 0; v < 2; ++v) {
