@@ -493,6 +493,23 @@ __device__ __forceinline__ float wd_sub_half(unsigned packed, float c) {
   return d;
 }
 
+// One-pass layer 2 operands from the unclamped layer-1 sums z (WD_BOUND_MFMA): per pair of
+// elements one packed fma (z = q s1 + p), one RNE convert, one packed max: x_hi = relu(z)_hi
+// (= max(f16(z), 0): rounding is monotonic), and |x_lo| = |f16(z - f16(z))| by v_fma_mix{lo,hi}
+// (exact difference, one RNE rounding) + one and.  For z < 0 the true x_lo is 0, so |x_lo| here
+// only over-estimates the bound term it feeds.  6 VALU per 2 elements instead of 9.
+typedef _Float16 wh2 __attribute__((ext_vector_type(2)));
+typedef float wf2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void wd_split_relu2(wf2 z, wh2& hi, unsigned& alo) {
+  const wh2 hu = __builtin_convertvector(z, wh2);
+  hi = __builtin_elementwise_max(hu, (wh2){(_Float16)0.f, (_Float16)0.f});
+  const unsigned hub = __builtin_bit_cast(unsigned, hu);
+  unsigned d = 0;
+  asm("v_fma_mixlo_f16 %0, %1, -1.0, %2 op_sel_hi:[1,0,0]" : "+v"(d) : "v"(hub), "v"(z.x));
+  asm("v_fma_mixhi_f16 %0, %1, -1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "+v"(d) : "v"(hub), "v"(z.y));
+  alo = d & 0x7fff7fffu;
+}
+
 // Split 8 fp32 values into f16 hi / lo halves: hi = f16(x), lo = f16(x - hi) (RNE; the
 // remainder is exact in fp32).
 __device__ __forceinline__ void wd_split8(const float* x, wh8& hi, wh8& lo) {
@@ -1056,16 +1073,28 @@ __global__ __launch_bounds__(256, UPW == 1 ? 2 : 1) void wdc_scan_kernel(WdScanA
           const float* prow = ps + (wave * UPW + v) * K1P + 8 * h + 16 * kk;
           const float4 p0 = *reinterpret_cast<const float4*>(prow);
           const float4 p1 = *reinterpret_cast<const float4*>(prow + 4);
+          if constexpr (BM) {  // x_hi and |x_lo| (the bound MFMAs' B operands), packed
+            const wf2 s2v = {s1, s1};
+            const wf2 zq[4] = {{q0.x, q0.y}, {q0.z, q0.w}, {q1.x, q1.y}, {q1.z, q1.w}};
+            const wf2 zp[4] = {{p0.x, p0.y}, {p0.z, p0.w}, {p1.x, p1.y}, {p1.z, p1.w}};
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              wh2 hi;
+              unsigned alo;
+              wd_split_relu2(__builtin_elementwise_fma(zq[e], s2v, zp[e]), hi, alo);
+              const wh2 lo2 = __builtin_bit_cast(wh2, alo);
+              oh[v][2 * e] = hi[0];
+              oh[v][2 * e + 1] = hi[1];
+              ol[v][2 * e] = lo2[0];
+              ol[v][2 * e + 1] = lo2[1];
+            }
+            continue;
+          }
           // x1 * s1 (P pre-scaled, Q scaled here)
           float x[8] = {fmaxf(fmaf(q0.x, s1, p0.x), 0.f), fmaxf(fmaf(q0.y, s1, p0.y), 0.f),
                         fmaxf(fmaf(q0.z, s1, p0.z), 0.f), fmaxf(fmaf(q0.w, s1, p0.w), 0.f),
                         fmaxf(fmaf(q1.x, s1, p1.x), 0.f), fmaxf(fmaf(q1.y, s1, p1.y), 0.f),
                         fmaxf(fmaf(q1.z, s1, p1.z), 0.f), fmaxf(fmaf(q1.w, s1, p1.w), 0.f)};
-          if constexpr (BM) {  // x_hi and |x_lo| (the bound MFMAs' B operands)
-            wd_split8(x, oh[v], ol[v]);
-            ol[v] = __builtin_elementwise_abs(ol[v]);
-            continue;
-          }
           float bb = bx1[v];
           bb = fmaf(va.x, x[0], bb); bb = fmaf(va.y, x[1], bb);
           bb = fmaf(va.z, x[2], bb); bb = fmaf(va.w, x[3], bb);
