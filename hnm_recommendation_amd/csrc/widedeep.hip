@@ -460,8 +460,12 @@ typedef _Float16 wh8 __attribute__((ext_vector_type(8)));
 // (349); one pass on layer 2 with x_lo bounded by 2^-11 |x| overflows every row's segments,
 // with the per-pair exact x_lo term (v1o . |x - x_hi|, WD_SPLIT_PASSES = 1) it holds (788
 // candidates a row) but runs 283 ms: at half the MFMAs the k loop's operand VALU bounds it.
+// Round 3: one pass on layer 2 with the bound's layer-2 terms on the matrix pipe
+// (WD_BOUND_MFMA below) and packed operand formation: 232 ms (1,145 candidates a row; their
+// exact fp32 re-scoring ~14 ms) vs 2 passes 262-267 ms (393) -- W&D 15.1 k -> 16.5 k users/s
+// (profiles/r3g_widedeep_ab.txt).
 #ifndef WD_SPLIT_PASSES
-#define WD_SPLIT_PASSES 2  // layer 2
+#define WD_SPLIT_PASSES 1  // layer 2
 #endif
 #ifndef WD_SPLIT_PASSES3
 #define WD_SPLIT_PASSES3 1  // layer 3: W_hi x_hi only (both residuals bounded)
