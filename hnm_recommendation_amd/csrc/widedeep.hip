@@ -508,9 +508,10 @@ __device__ __forceinline__ void wd_split_relu2(wf2 z, wh2& hi, unsigned& alo) {
   const wh2 hu = __builtin_convertvector(z, wh2);
   hi = __builtin_elementwise_max(hu, (wh2){(_Float16)0.f, (_Float16)0.f});
   const unsigned hub = __builtin_bit_cast(unsigned, hu);
-  unsigned d = 0;
-  asm("v_fma_mixlo_f16 %0, %1, -1.0, %2 op_sel_hi:[1,0,0]" : "+v"(d) : "v"(hub), "v"(z.x));
-  asm("v_fma_mixhi_f16 %0, %1, -1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "+v"(d) : "v"(hub), "v"(z.y));
+  unsigned d;  // both halves written by the pair (no initialising move)
+  asm("v_fma_mixlo_f16 %0, %1, -1.0, %2 op_sel_hi:[1,0,0]\n\t"
+      "v_fma_mixhi_f16 %0, %1, -1.0, %3 op_sel:[1,0,0] op_sel_hi:[1,0,0]"
+      : "=&v"(d) : "v"(hub), "v"(z.x), "v"(z.y));
   alo = d & 0x7fff7fffu;
 }
 
@@ -1192,19 +1193,26 @@ __global__ __launch_bounds__(256, UPW == 1 ? 2 : 1) void wdc_scan_kernel(WdScanA
         ba[0] = A.WBf[((NG2 == 1 ? 0 : g) * KB) * 64 + lane];
         if (NG2 == 1) ba[1] = A.WBf[KB * 64 + lane];
       }
-      // (steps in pairs with the two register sets swapped instead of copied: 266 ms vs 261)
-      for (int kb = 0; kb < KB; ++kb) {
-        step(kb, fa, fb, xha, xla, xhb, xlb, ba, bb);
-#pragma unroll
-        for (int gi = 0; gi < G2; ++gi) fa[gi] = fb[gi];
-        if constexpr (BM) {
-          ba[0] = bb[0];
-          ba[1] = bb[1];
+      if constexpr (BM) {
+        // steps in pairs with the two register sets swapped (the one-pass kernel is issue-bound:
+        // the copies of the copy form below were 28 v_mov per step; the 2-pass kernel was
+        // MFMA-bound and measured 266 vs 261 ms the other way round)
+        int kb = 0;
+        for (; kb + 1 < KB; kb += 2) {
+          step(kb, fa, fb, xha, xla, xhb, xlb, ba, bb);
+          step(kb + 1, fb, fa, xhb, xlb, xha, xla, bb, ba);
         }
+        if (kb < KB) step(kb, fa, fb, xha, xla, xhb, xlb, ba, bb);
+      } else {
+        for (int kb = 0; kb < KB; ++kb) {
+          step(kb, fa, fb, xha, xla, xhb, xlb, ba, bb);
 #pragma unroll
-        for (int v = 0; v < UPW; ++v) {
-          xha[v] = xhb[v];
-          xla[v] = xlb[v];
+          for (int gi = 0; gi < G2; ++gi) fa[gi] = fb[gi];
+#pragma unroll
+          for (int v = 0; v < UPW; ++v) {
+            xha[v] = xhb[v];
+            xla[v] = xlb[v];
+          }
         }
       }
       if (G2 < RB2 && g == 0) {  // zeroed after the k loop (G2 = RB2: by the first MFMA's C = 0)
