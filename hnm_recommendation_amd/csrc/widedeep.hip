@@ -1185,13 +1185,63 @@ __global__ __launch_bounds__(256, UPW == 1 ? 2 : 1) void wdc_scan_kernel(WdScanA
           }
         }
       };
+      // BM: the weight and bound fragments of step kb + 2 are loaded into the registers step kb's
+      // MFMAs have just read -- a two-step prefetch distance with two register sets (the
+      // one-pass step is half as long as a two-pass one, so one step ahead left its MFMAs
+      // waiting on L2)
+      auto stepd = [&](int kb, wh8 (&a)[G2], const wh8 (&xh)[UPW], const wh8 (&xl)[UPW],
+                       wh8 (&nxh)[UPW], wh8 (&nxl)[UPW], wh8 (&bq)[2]) {
+        const bool more = kb + 1 < KB;
+        const int kn = more ? kb + 1 : kb;
+        const int kf = kb + 2 < KB ? kb + 2 : KB - 1;
+#pragma unroll
+        for (int gi = 0; gi < G2; ++gi)
+#pragma unroll
+          for (int v = 0; v < UPW; ++v) acc2[v][gi] = wd_mfma16(a[gi], xh[v], acc2[v][gi]);
+#pragma unroll
+        for (int v = 0; v < UPW; ++v) {
+          if (NG2 == 1) {
+            accb[v] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bq[0], xh[v], accb[v], 0, 0, 0);
+            accb[v] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bq[1], xl[v], accb[v], 0, 0, 0);
+          } else {
+            const wh8 bop = g == 0 ? xh[v] : xl[v];
+            accb[v] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bq[0], bop, accb[v], 0, 0, 0);
+          }
+        }
+#pragma unroll
+        for (int gi = 0; gi < G2; ++gi) a[gi] = frag(gi, kf, 0);
+        bq[0] = A.WBf[((NG2 == 1 ? 0 : g) * KB + kf) * 64 + lane];
+        if (NG2 == 1) bq[1] = A.WBf[(KB + kf) * 64 + lane];
+        form(kn, v0s, v0s, nxh, nxl);
+#pragma unroll
+        for (int e = 0; e < QPS; ++e) {
+          const int c = 8 * ((g * KB + kb) * QPS + e);
+          qdst[c] = qv[e];
+          qv[e] = qload(qrs, c + 8 * QPS);
+        }
+        if (WDC_INTERLEAVE) {
+          __builtin_amdgcn_sched_group_barrier(0x100, 4 + 2 * UPW, 0);
+#pragma unroll
+          for (int i = 0; i < G2 * UPW + (3 - NG2) * UPW; ++i) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x002, WDC_VPM, 0);
+          }
+        }
+      };
       wh8 fa[G2], fb[G2], xha[UPW], xla[UPW], xhb[UPW], xlb[UPW], ba[2], bb[2];
       form(0, v1p, vop, xha, xla);
 #pragma unroll
       for (int gi = 0; gi < G2; ++gi) fa[gi] = frag(gi, 0, 0);
       if constexpr (BM) {
+        const int k1 = KB > 1 ? 1 : 0;
+#pragma unroll
+        for (int gi = 0; gi < G2; ++gi) fb[gi] = frag(gi, k1, 0);
         ba[0] = A.WBf[((NG2 == 1 ? 0 : g) * KB) * 64 + lane];
-        if (NG2 == 1) ba[1] = A.WBf[KB * 64 + lane];
+        bb[0] = A.WBf[((NG2 == 1 ? 0 : g) * KB + k1) * 64 + lane];
+        if (NG2 == 1) {
+          ba[1] = A.WBf[KB * 64 + lane];
+          bb[1] = A.WBf[(KB + k1) * 64 + lane];
+        }
       }
       if constexpr (BM) {
         // steps in pairs with the two register sets swapped (the one-pass kernel is issue-bound:
@@ -1199,10 +1249,10 @@ __global__ __launch_bounds__(256, UPW == 1 ? 2 : 1) void wdc_scan_kernel(WdScanA
         // MFMA-bound and measured 266 vs 261 ms the other way round)
         int kb = 0;
         for (; kb + 1 < KB; kb += 2) {
-          step(kb, fa, fb, xha, xla, xhb, xlb, ba, bb);
-          step(kb + 1, fb, fa, xhb, xlb, xha, xla, bb, ba);
+          stepd(kb, fa, xha, xla, xhb, xlb, ba);
+          stepd(kb + 1, fb, xhb, xlb, xha, xla, bb);
         }
-        if (kb < KB) step(kb, fa, fb, xha, xla, xhb, xlb, ba, bb);
+        if (kb < KB) stepd(kb, fa, xha, xla, xhb, xlb, ba);
       } else {
         for (int kb = 0; kb < KB; ++kb) {
           step(kb, fa, fb, xha, xla, xhb, xlb, ba, bb);
