@@ -480,6 +480,9 @@ typedef _Float16 wh8 __attribute__((ext_vector_type(8)));
 #ifndef WD_BOUND_MFMA
 #define WD_BOUND_MFMA 1
 #endif
+#ifndef WD_PREFETCH  // one-pass k loop: weight fragments this many k steps ahead (2 or 3)
+#define WD_PREFETCH 2
+#endif
 
 __device__ __forceinline__ f32x16 wd_mfma16(wh8 a, wh8 b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
@@ -1193,7 +1196,7 @@ __global__ __launch_bounds__(256, UPW == 1 ? 2 : 1) void wdc_scan_kernel(WdScanA
                        wh8 (&nxh)[UPW], wh8 (&nxl)[UPW], wh8 (&bq)[2]) {
         const bool more = kb + 1 < KB;
         const int kn = more ? kb + 1 : kb;
-        const int kf = kb + 2 < KB ? kb + 2 : KB - 1;
+        const int kf = kb + WD_PREFETCH < KB ? kb + WD_PREFETCH : KB - 1;
 #pragma unroll
         for (int gi = 0; gi < G2; ++gi)
 #pragma unroll
@@ -1232,15 +1235,22 @@ __global__ __launch_bounds__(256, UPW == 1 ? 2 : 1) void wdc_scan_kernel(WdScanA
       form(0, v1p, vop, xha, xla);
 #pragma unroll
       for (int gi = 0; gi < G2; ++gi) fa[gi] = frag(gi, 0, 0);
+      wh8 fc[G2], bc3[2];  // third fragment set (WD_PREFETCH 3)
       if constexpr (BM) {
-        const int k1 = KB > 1 ? 1 : 0;
+        const int k1 = KB > 1 ? 1 : 0, k2 = KB > 2 ? 2 : KB - 1;
 #pragma unroll
-        for (int gi = 0; gi < G2; ++gi) fb[gi] = frag(gi, k1, 0);
-        ba[0] = A.WBf[((NG2 == 1 ? 0 : g) * KB) * 64 + lane];
-        bb[0] = A.WBf[((NG2 == 1 ? 0 : g) * KB + k1) * 64 + lane];
+        for (int gi = 0; gi < G2; ++gi) {
+          fb[gi] = frag(gi, k1, 0);
+          if (WD_PREFETCH == 3) fc[gi] = frag(gi, k2, 0);
+        }
+        const int bo = (NG2 == 1 ? 0 : g) * KB;
+        ba[0] = A.WBf[bo * 64 + lane];
+        bb[0] = A.WBf[(bo + k1) * 64 + lane];
+        if (WD_PREFETCH == 3) bc3[0] = A.WBf[(bo + k2) * 64 + lane];
         if (NG2 == 1) {
           ba[1] = A.WBf[KB * 64 + lane];
           bb[1] = A.WBf[(KB + k1) * 64 + lane];
+          if (WD_PREFETCH == 3) bc3[1] = A.WBf[(KB + k2) * 64 + lane];
         }
       }
       if constexpr (BM) {
@@ -1248,11 +1258,28 @@ __global__ __launch_bounds__(256, UPW == 1 ? 2 : 1) void wdc_scan_kernel(WdScanA
         // the copies of the copy form below were 28 v_mov per step; the 2-pass kernel was
         // MFMA-bound and measured 266 vs 261 ms the other way round)
         int kb = 0;
-        for (; kb + 1 < KB; kb += 2) {
-          stepd(kb, fa, xha, xla, xhb, xlb, ba);
-          stepd(kb + 1, fb, xhb, xlb, xha, xla, bb);
+        if (WD_PREFETCH == 3) {
+          // three fragment sets x two operand sets: six steps per iteration, guarded tail
+          for (; kb + 5 < KB; kb += 6) {
+            stepd(kb, fa, xha, xla, xhb, xlb, ba);
+            stepd(kb + 1, fb, xhb, xlb, xha, xla, bb);
+            stepd(kb + 2, fc, xha, xla, xhb, xlb, bc3);
+            stepd(kb + 3, fa, xhb, xlb, xha, xla, ba);
+            stepd(kb + 4, fb, xha, xla, xhb, xlb, bb);
+            stepd(kb + 5, fc, xhb, xlb, xha, xla, bc3);
+          }
+          if (kb < KB) stepd(kb, fa, xha, xla, xhb, xlb, ba);
+          if (kb + 1 < KB) stepd(kb + 1, fb, xhb, xlb, xha, xla, bb);
+          if (kb + 2 < KB) stepd(kb + 2, fc, xha, xla, xhb, xlb, bc3);
+          if (kb + 3 < KB) stepd(kb + 3, fa, xhb, xlb, xha, xla, ba);
+          if (kb + 4 < KB) stepd(kb + 4, fb, xha, xla, xhb, xlb, bb);
+        } else {
+          for (; kb + 1 < KB; kb += 2) {
+            stepd(kb, fa, xha, xla, xhb, xlb, ba);
+            stepd(kb + 1, fb, xhb, xlb, xha, xla, bb);
+          }
+          if (kb < KB) stepd(kb, fa, xha, xla, xhb, xlb, ba);
         }
-        if (kb < KB) stepd(kb, fa, xha, xla, xhb, xlb, ba);
       } else {
         for (int kb = 0; kb < KB; ++kb) {
           step(kb, fa, fb, xha, xla, xhb, xlb, ba, bb);
