@@ -480,8 +480,11 @@ typedef _Float16 wh8 __attribute__((ext_vector_type(8)));
 #ifndef WD_BOUND_MFMA
 #define WD_BOUND_MFMA 1
 #endif
+#ifndef WD_LO_EXACT  // |x_lo| := 0 where z < 0 (exact) instead of |f16(z - f16(z))|
+#define WD_LO_EXACT 0
+#endif
 #ifndef WD_PREFETCH  // one-pass k loop: weight fragments this many k steps ahead (2 or 3)
-#define WD_PREFETCH 2
+#define WD_PREFETCH 3
 #endif
 
 __device__ __forceinline__ f32x16 wd_mfma16(wh8 a, wh8 b, f32x16 c) {
@@ -515,7 +518,14 @@ __device__ __forceinline__ void wd_split_relu2(wf2 z, wh2& hi, unsigned& alo) {
   asm("v_fma_mixlo_f16 %0, %1, -1.0, %2 op_sel_hi:[1,0,0]\n\t"
       "v_fma_mixhi_f16 %0, %1, -1.0, %3 op_sel:[1,0,0] op_sel_hi:[1,0,0]"
       : "=&v"(d) : "v"(hub), "v"(z.x), "v"(z.y));
-  alo = d & 0x7fff7fffu;
+  if (WD_LO_EXACT) {
+    // halves whose z < 0 (sign bit of the unclamped hi) have x = relu(z) = 0, hence x_lo = 0:
+    // clear them together with the sign bits (|x_lo| exact instead of over-estimated)
+    const unsigned neg = ((hub >> 15) & 0x00010001u) * 0xffffu;
+    alo = d & ~(neg | 0x80008000u);
+  } else {
+    alo = d & 0x7fff7fffu;
+  }
 }
 
 // Split 8 fp32 values into f16 hi / lo halves: hi = f16(x), lo = f16(x - hi) (RNE; the
