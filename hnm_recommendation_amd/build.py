@@ -16,7 +16,7 @@ CSRC = os.path.join(PKG, "csrc")
 BUILD = os.path.join(REPO, "build", "obj")
 LIB = os.path.join(PKG, "libhnm_mi355x.so")
 SOURCES = ["api.hip", "score.hip", "dot_cert.hip", "ncf.hip", "ncf_cert.hip", "graph.hip",
-           "widedeep.hip", "eval.hip"]
+           "widedeep.hip", "eval.hip", "topk_sort.hip"]
 HEADERS = ["hnm_device.h", "hnm_internal.h", "dot_internal.h", "ncf_internal.h"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-Wall",

@@ -86,6 +86,10 @@ void hnm_set_error(const char* fmt, ...);
 // the ctx workspace if needed.  Growth synchronizes the stream (the old buffer may still
 // be read by queued kernels); call hnm_ctx_reserve() before graph capture.
 hnm_status hnm_workspace(hnm_ctx* ctx, size_t bytes, void** out);
+// row top-k for k > 128 by a stable segmented radix sort of whole rows (topk_sort.hip)
+hnm_status hnm_topk_rows_sort(hnm_ctx* ctx, const float* scores, int64_t ld, int64_t B,
+                              int64_t I, const int64_t* mask_ptr, const int32_t* mask_idx, int k,
+                              float* out_val, int64_t* out_idx);
 
 static inline size_t hnm_align(size_t x, size_t a = 256) { return (x + a - 1) / a * a; }
 __host__ __device__ static inline int64_t hnm_cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }

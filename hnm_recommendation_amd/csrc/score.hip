@@ -740,9 +740,11 @@ extern "C" hnm_status hnm_topk_rows_f32(hnm_ctx* ctx, const float* scores, int64
                                         const int32_t* mask_idx, int k, float* out_val,
                                         int64_t* out_idx) {
   HNM_REQUIRE(ctx && scores && out_idx, HNM_EINVAL, "topk_rows: NULL argument");
-  HNM_REQUIRE(k >= 1 && k <= 128 && k <= I && ld >= I, HNM_EINVAL, "topk_rows: bad k/shape");
+  HNM_REQUIRE(k >= 1 && k <= I && ld >= I, HNM_EINVAL, "topk_rows: bad k/shape");
   HNM_REQUIRE(I < INT_BIG, HNM_EUNSUPPORTED, "topk_rows: too many items");
   if (B <= 0) return HNM_OK;
+  if (k > 128)  // whole-row stable sort (topk_sort.hip)
+    return hnm_topk_rows_sort(ctx, scores, ld, B, I, mask_ptr, mask_idx, k, out_val, out_idx);
   // fewer rows than ~1024 waves: split the rows into column chunks of >= 2048 items
   const int64_t P = std::min<int64_t>(hnm_cdiv(1024, B), hnm_cdiv(I, 2048));
   if (P > 1) {

@@ -53,6 +53,13 @@ class RecModule(nn.Module):
                 raise IndexError(f"index out of range in self ({what} must be in [0, {bound}))")
         return ids.to(device=dev, dtype=torch.int64).contiguous(), host
 
+    def _check_top_k(self):
+        """`recommend()` ends in `torch.topk(scores, self.top_k, dim=1)` (e.g. neural_cf.py:324),
+        which raises for top_k outside [0, num_items]; so does the mirror, before any launch.
+        `recommend_with_scores(k=...)` (the serve path's per-request k) clamps k instead."""
+        if not 0 <= self.top_k <= self.num_items:
+            raise RuntimeError("selected index k out of range")
+
     @staticmethod
     def _check(device, *host_checked):
         """Raise IndexError for out-of-range device ids (syncs the stream) -- skipped when
@@ -177,6 +184,14 @@ def filter_csr(user_ids: torch.Tensor, filter_items, num_items: int, device: tor
     if ptr[-1] == 0:
         return None, None
     return (torch.from_numpy(ptr).to(device), torch.from_numpy(idx).to(device))
+
+
+def empty_topk(k: int, u: torch.Tensor):
+    """torch.topk's k = 0 result ([B, 0] scores and ids); k < 0 raises as torch.topk does."""
+    if k < 0:
+        raise RuntimeError("selected index k out of range")
+    return (torch.empty(u.numel(), 0, dtype=torch.float32, device=u.device),
+            torch.empty(u.numel(), 0, dtype=torch.int64, device=u.device))
 
 
 def dense_topk(scores: torch.Tensor, k: int, mptr=None, midx=None):

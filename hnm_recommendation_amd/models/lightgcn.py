@@ -21,7 +21,7 @@ import torch.nn as nn
 
 from .. import _lib
 from ..evaluation import RecommendationMetrics
-from .base import RecModule, dense_topk, f32c, filter_csr
+from .base import RecModule, dense_topk, empty_topk, f32c, filter_csr
 
 
 class NormalizedGraph:
@@ -259,6 +259,8 @@ class LightGCN(RecModule):
         n_items = fi.shape[0]
         mptr, midx = filter_csr(u, filter_items, self.num_items, u.device)
         kk = min(k, n_items)
+        if kk <= 0:
+            return empty_topk(k, u)
         if kk > 64:
             scores = self.predict_all_items(u)
             return dense_topk(scores, kk, mptr, midx)
@@ -277,6 +279,7 @@ class LightGCN(RecModule):
     def recommend(self, user_ids: torch.Tensor,
                   filter_items: Optional[Dict[int, set]] = None) -> torch.Tensor:
         """Top-`top_k` item ids per user (`lightgcn.py:332-358`)."""
+        self._check_top_k()
         self.eval()
         with torch.no_grad():
             return self.recommend_with_scores(user_ids, filter_items)[1]

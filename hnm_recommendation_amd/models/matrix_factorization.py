@@ -12,7 +12,7 @@ import torch.nn as nn
 
 from .. import _lib
 from ..evaluation import RecommendationMetrics
-from .base import RecModule, dense_topk, f32c, filter_csr
+from .base import RecModule, dense_topk, empty_topk, f32c, filter_csr
 
 
 class MatrixFactorization(RecModule):
@@ -92,6 +92,8 @@ class MatrixFactorization(RecModule):
         u, hu = self._ids(user_ids, self.num_users)
         mptr, midx = filter_csr(u, filter_items, self.num_items, u.device)
         kk = min(k, self.num_items)
+        if kk <= 0:
+            return empty_topk(k, u)
         if kk > 64:
             return dense_topk(self.predict_all_items(u), kk, mptr, midx)
         out_v = torch.empty(u.numel(), kk, dtype=torch.float32, device=u.device)
@@ -109,6 +111,7 @@ class MatrixFactorization(RecModule):
 
     def recommend(self, user_ids, filter_items: Optional[Dict[int, set]] = None):
         """Top-`top_k` item ids per user (`matrix_factorization.py:220-246`)."""
+        self._check_top_k()
         self.eval()
         with torch.no_grad():
             return self.recommend_with_scores(user_ids, filter_items)[1]

@@ -17,7 +17,7 @@ import torch.nn as nn
 
 from .. import _lib
 from ..evaluation import RecommendationMetrics
-from .base import RecModule, dense_topk, f32c, filter_csr
+from .base import RecModule, dense_topk, empty_topk, f32c, filter_csr
 
 
 class NeuralCF(RecModule):
@@ -135,6 +135,8 @@ class NeuralCF(RecModule):
         u, hu = self._ids(user_ids, self.num_users)
         mptr, midx = filter_csr(u, filter_items, self.num_items, u.device)
         kk = min(k, self.num_items)
+        if kk <= 0:
+            return empty_topk(k, u)
         if kk > 64:  # serve path k up to 100 (serve.py:56): dense + row top-k kernel
             scores = self.predict_all_items(u)
             return dense_topk(scores, kk, mptr, midx)
@@ -150,6 +152,7 @@ class NeuralCF(RecModule):
     def recommend(self, user_ids: torch.Tensor,
                   filter_items: Optional[Dict[int, set]] = None) -> torch.Tensor:
         """Top-`top_k` item ids per user (`neural_cf.py:300-326`)."""
+        self._check_top_k()
         self.eval()
         with torch.no_grad():
             return self.recommend_with_scores(user_ids, filter_items)[1]

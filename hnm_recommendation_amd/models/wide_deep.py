@@ -19,7 +19,7 @@ import torch.nn as nn
 
 from .. import _lib
 from ..evaluation import RecommendationMetrics
-from .base import RecModule, dense_topk, f32c, filter_csr
+from .base import RecModule, dense_topk, empty_topk, f32c, filter_csr
 
 
 class WideDeep(RecModule):
@@ -250,6 +250,8 @@ class WideDeep(RecModule):
         f = self._features(user_features, u.numel(), u.device)
         mptr, midx = filter_csr(u, filter_items, self.num_items, u.device)
         kk = min(k, self.num_items)
+        if kk <= 0:
+            return empty_topk(k, u)
         if kk > 64:
             return dense_topk(self.predict_all_items(u, user_features), kk, mptr, midx)
         out_v = torch.empty(u.numel(), kk, dtype=torch.float32, device=u.device)
@@ -265,6 +267,7 @@ class WideDeep(RecModule):
     def recommend(self, user_ids, user_features=None,
                   filter_items: Optional[Dict[int, set]] = None):
         """Top-`top_k` item ids per user (`wide_deep.py:405-435`)."""
+        self._check_top_k()
         self.eval()
         with torch.no_grad():
             return self.recommend_with_scores(user_ids, user_features, filter_items)[1]

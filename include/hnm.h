@@ -324,7 +324,9 @@ hnm_status hnm_mask_gather_csr(hnm_ctx* ctx, const int64_t* hist_ptr, const int3
                                int64_t* mask_ptr, int32_t* mask_idx);
 
 /* ---- torch.topk over a dense score matrix (serve.py:350-355, k up to 100) ----------
- * Row top-k of scores[b, :I] (leading dim ld) with the optional CSR -inf mask. k <= 128. */
+ * Row top-k of scores[b, :I] (leading dim ld) with the optional CSR -inf mask, 1 <= k <= I
+ * (torch.topk's range).  k <= 128: row-select kernels; larger k: a stable segmented radix
+ * sort of whole rows in chunks (same (score desc, item asc) order; workspace ~512 MB). */
 hnm_status hnm_topk_rows_f32(hnm_ctx* ctx, const float* scores, int64_t ld, int64_t B,
                              int64_t I, const int64_t* mask_ptr, const int32_t* mask_idx,
                              int k, float* out_val, int64_t* out_idx);

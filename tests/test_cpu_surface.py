@@ -164,6 +164,14 @@ def test_recommender_host_logic():
         srv.get_recommendations(1, model_name="mf")
 
 
+def test_recommend_top_k_range_like_torch_topk():
+    """recommend() ends in torch.topk(scores, top_k) (neural_cf.py:324 and the other models):
+    top_k > num_items raises RuntimeError -- checked before any launch, so also here on CPU."""
+    for m in (NeuralCF(10, 5), MatrixFactorization(10, 5), WideDeep(10, 5)):
+        with pytest.raises(RuntimeError, match="out of range"):
+            m.recommend(torch.tensor([0]))
+
+
 def test_metrics_need_gpu():
     from hnm_recommendation_amd import evaluation as EV
     with pytest.raises(RuntimeError):
