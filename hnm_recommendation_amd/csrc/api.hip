@@ -251,7 +251,7 @@ __global__ __launch_bounds__(256) void gather_rows_kernel(const float* __restric
 extern "C" hnm_status hnm_gather_rows_f32(hnm_ctx* ctx, const float* table, int64_t rows,
                                           int64_t ld, int d, const int64_t* ids, int64_t n,
                                           float* out, int64_t ldo) {
-  HNM_REQUIRE(ctx && table && ids && out, HNM_EINVAL, "gather: NULL argument");
+  HNM_REQUIRE(ctx && table && ((ids && out) || n == 0), HNM_EINVAL, "gather: NULL argument");
   HNM_REQUIRE(d > 0 && ld >= d && ldo >= d && rows > 0, HNM_EINVAL, "gather: bad shape");
   if (n <= 0) return HNM_OK;
   const bool vec4 = (d % 4 == 0) && (ld % 4 == 0) && (ldo % 4 == 0) &&
@@ -421,7 +421,7 @@ __global__ __launch_bounds__(256) void axpby_kernel(int64_t n, float a, const fl
 
 extern "C" hnm_status hnm_axpby_f32(hnm_ctx* ctx, int64_t n, float alpha, const float* x,
                                     float beta, const float* y, float* out) {
-  HNM_REQUIRE(ctx && x && out, HNM_EINVAL, "axpby: NULL argument");
+  HNM_REQUIRE(ctx && ((x && out) || n == 0), HNM_EINVAL, "axpby: NULL argument");
   if (n <= 0) return HNM_OK;
   const unsigned grid = (unsigned)std::min<int64_t>(hnm_cdiv(n, 256), 8 * 2048);
   hipLaunchKernelGGL(axpby_kernel, dim3(grid), dim3(256), 0, ctx->stream, n, alpha, x, beta,
@@ -502,7 +502,7 @@ extern "C" hnm_status hnm_topk_merge_f32(hnm_ctx* ctx, const float* cand_val,
                                          const int64_t* cand_idx, int64_t B, int64_t G,
                                          int64_t gstride, int64_t bstride, int kc, int k,
                                          float* out_val, int64_t* out_idx) {
-  HNM_REQUIRE(ctx && cand_val && cand_idx && out_idx, HNM_EINVAL, "merge: NULL argument");
+  HNM_REQUIRE(ctx && ((cand_val && cand_idx && out_idx) || B == 0), HNM_EINVAL, "merge: NULL argument");
   HNM_REQUIRE(k >= 1 && k <= 128 && kc >= 1 && G >= 1, HNM_EINVAL, "merge: bad k/kc/G");
   if (B <= 0) return HNM_OK;
   return launch_merge<int64_t>(ctx, cand_val, cand_idx, B, G, gstride, bstride, kc, k,
@@ -549,7 +549,7 @@ extern "C" hnm_status hnm_pair_dot_f32(hnm_ctx* ctx, const float* user_tab, int6
                                        const int64_t* item_ids, int64_t n,
                                        const float* user_bias, const float* item_bias,
                                        const float* const_bias, float* out) {
-  HNM_REQUIRE(ctx && user_tab && item_tab && user_ids && item_ids && out, HNM_EINVAL,
+  HNM_REQUIRE(ctx && user_tab && item_tab && ((user_ids && item_ids && out) || n == 0), HNM_EINVAL,
               "pair_dot: NULL argument");
   HNM_REQUIRE(d >= 1 && ldu >= d && ldi >= d, HNM_EINVAL, "pair_dot: bad shape");
   if (n <= 0) return HNM_OK;
@@ -663,7 +663,7 @@ extern "C" hnm_status hnm_mask_gather_csr(hnm_ctx* ctx, const int64_t* hist_ptr,
                                           const int64_t* user_ids, int64_t B, int64_t item_lo,
                                           int64_t item_hi, int64_t capacity, int64_t* mask_ptr,
                                           int32_t* mask_idx) {
-  HNM_REQUIRE(ctx && hist_ptr && user_ids && mask_ptr && (hist_idx || capacity == 0) &&
+  HNM_REQUIRE(ctx && hist_ptr && (user_ids || B == 0) && mask_ptr && (hist_idx || capacity == 0) &&
                   (mask_idx || capacity == 0),
               HNM_EINVAL, "mask_gather: NULL argument");
   HNM_REQUIRE(num_users >= 0 && B >= 0 && capacity >= 0 && 0 <= item_lo && item_lo <= item_hi,

@@ -797,8 +797,8 @@ extern "C" hnm_status hnm_spmm_rows_combine_f32(hnm_ctx* ctx, int64_t N, const i
                                                 const int64_t* rows, int64_t n, int d,
                                                 const float* const* layers, const float* alphas,
                                                 int L, float* out) {
-  HNM_REQUIRE(ctx && rowptr && col && val && rows && layers && alphas && out, HNM_EINVAL,
-              "spmm_rows_combine: NULL argument");
+  HNM_REQUIRE(ctx && rowptr && col && val && layers && alphas && ((rows && out) || n == 0),
+              HNM_EINVAL, "spmm_rows_combine: NULL argument");
   HNM_REQUIRE(L >= 1 && L <= 8, HNM_EUNSUPPORTED, "spmm_rows_combine: 1 <= L <= 8");
   CombineLayers cl;
   cl.L = L;
@@ -808,7 +808,7 @@ extern "C" hnm_status hnm_spmm_rows_combine_f32(hnm_ctx* ctx, int64_t N, const i
     cl.E[l] = layers[l];
   }
   for (int l = 0; l <= L; ++l) cl.a[l] = alphas[l];
-  HNM_REQUIRE((uintptr_t)out % 16 == 0, HNM_EINVAL, "spmm_rows_combine: out not 16-B aligned");
   if (n <= 0) return HNM_OK;
+  HNM_REQUIRE((uintptr_t)out % 16 == 0, HNM_EINVAL, "spmm_rows_combine: out not 16-B aligned");
   HNM_SPMM_DISPATCH(combine_launch, ctx, rows, n, N, rowptr, col, val, d, cl, out)
 }

@@ -684,7 +684,7 @@ static hnm_status ncf_common(hnm_ctx* ctx, const hnm_ncf_weights* w, const int64
                              float* ov, int64_t* oi, float* dense, int64_t ldo) {
   hnm_status st = ncf_check(w);
   if (st) return st;
-  HNM_REQUIRE(ctx && ids, HNM_EINVAL, "ncf: NULL argument");
+  HNM_REQUIRE(ctx && (ids || B == 0), HNM_EINVAL, "ncf: NULL argument");
   if (B <= 0) return HNM_OK;
   const int64_t I = w->num_items;
   const bool big = w->h1 > 64 || w->mf > 64;
@@ -732,7 +732,7 @@ extern "C" hnm_status hnm_ncf_topk_f32(hnm_ctx* ctx, const hnm_ncf_weights* w,
                                        const int64_t* user_ids, int64_t B,
                                        const int64_t* mask_ptr, const int32_t* mask_idx, int k,
                                        float* out_val, int64_t* out_idx) {
-  HNM_REQUIRE(k >= 1 && k <= 64 && out_idx, HNM_EINVAL, "ncf_topk: fused path needs 1 <= k <= 64");
+  HNM_REQUIRE(k >= 1 && k <= 64 && (out_idx || B == 0), HNM_EINVAL, "ncf_topk: fused path needs 1 <= k <= 64");
   return ncf_common<false>(ctx, w, user_ids, B, mask_ptr, mask_idx, k, out_val, out_idx,
                            nullptr, 0);
 }
@@ -750,7 +750,7 @@ extern "C" hnm_status hnm_ncf_topk_begin_f32(hnm_ctx* ctx, const hnm_ncf_weights
                                              int k, float* lower_bound) {
   hnm_status st = ncf_check(w);
   if (st) return st;
-  HNM_REQUIRE(ctx && user_ids && lower_bound && k >= 1 && k <= 64, HNM_EINVAL,
+  HNM_REQUIRE(ctx && ((user_ids && lower_bound) || B == 0) && k >= 1 && k <= 64, HNM_EINVAL,
               "ncf_topk_begin: bad argument");
   HNM_REQUIRE(!ctx->pend.kind, HNM_EINVAL, "ncf_topk_begin: a two-phase call is already open");
   if (B <= 0) return HNM_OK;
@@ -777,7 +777,7 @@ extern "C" hnm_status hnm_ncf_topk_finish_f32(hnm_ctx* ctx, const hnm_ncf_weight
                                               const int64_t* mask_ptr, const int32_t* mask_idx,
                                               int k, const float* lower_bound, int short_ok,
                                               float* out_val, int64_t* out_idx) {
-  HNM_REQUIRE(ctx && w && out_idx, HNM_EINVAL, "ncf_topk_finish: bad argument");
+  HNM_REQUIRE(ctx && w && (out_idx || B == 0), HNM_EINVAL, "ncf_topk_finish: bad argument");
   if (B <= 0) return HNM_OK;
   const int kind = ctx->pend.kind;
   HNM_REQUIRE((kind == HNM_PEND_NCF_CERT || kind == HNM_PEND_NCF_EXACT) && ctx->pend.B == B &&
@@ -801,7 +801,7 @@ extern "C" hnm_status hnm_ncf_topk_finish_f32(hnm_ctx* ctx, const hnm_ncf_weight
 extern "C" hnm_status hnm_ncf_scores_f32(hnm_ctx* ctx, const hnm_ncf_weights* w,
                                          const int64_t* user_ids, int64_t B, float* out,
                                          int64_t ldo) {
-  HNM_REQUIRE(out && w && ldo >= w->num_items, HNM_EINVAL, "ncf_scores: bad output");
+  HNM_REQUIRE((out || B == 0) && w && ldo >= w->num_items, HNM_EINVAL, "ncf_scores: bad output");
   return ncf_common<true>(ctx, w, user_ids, B, nullptr, nullptr, 1, nullptr, nullptr, out, ldo);
 }
 
@@ -826,7 +826,7 @@ extern "C" hnm_status hnm_ncf_pair_scores_f32(hnm_ctx* ctx, const hnm_ncf_weight
                                               int64_t n, float* out) {
   hnm_status st = ncf_check(w);
   if (st) return st;
-  HNM_REQUIRE(ctx && user_ids && item_ids && out, HNM_EINVAL, "ncf_pair: NULL argument");
+  HNM_REQUIRE(ctx && ((user_ids && item_ids && out) || n == 0), HNM_EINVAL, "ncf_pair: NULL argument");
   if (n <= 0) return HNM_OK;
   hipLaunchKernelGGL(ncf_pair_kernel, dim3((unsigned)hnm_cdiv(n, 256)), dim3(256), 0, ctx->stream,
                      *w, user_ids, item_ids, n, out, ctx->err_dev);

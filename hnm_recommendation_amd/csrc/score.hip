@@ -497,8 +497,9 @@ static void launch_dot(hnm_ctx* ctx, dim3 grid, const DotArgs& a, bool bias) {
 #define THRESH_SAMPLE 4096
 
 static hnm_status dot_validate(hnm_ctx* ctx, const float* ut, int64_t U, int64_t ldu,
-                               const int64_t* ids, const float* it, int64_t I, int64_t ldi, int d) {
-  HNM_REQUIRE(ctx && ut && ids && it, HNM_EINVAL, "dot: NULL argument");
+                               const int64_t* ids, int64_t B, const float* it, int64_t I,
+                               int64_t ldi, int d) {
+  HNM_REQUIRE(ctx && ut && (ids || B == 0) && it, HNM_EINVAL, "dot: NULL argument");
   HNM_REQUIRE(d >= 1 && d <= 128 && ldu >= d && ldi >= d && U > 0 && I > 0, HNM_EINVAL,
               "dot: bad shape (d=%d)", d);
   HNM_REQUIRE(d % 4 == 0 && ldu % 4 == 0 && ldi % 4 == 0 && (uintptr_t)ut % 16 == 0 &&
@@ -549,9 +550,9 @@ extern "C" hnm_status hnm_dot_topk_f32(hnm_ctx* ctx, const float* user_tab, int6
                                        const float* const_bias, const int64_t* mask_ptr,
                                        const int32_t* mask_idx, int k, float* out_val,
                                        int64_t* out_idx) {
-  hnm_status st = dot_validate(ctx, user_tab, num_users, ldu, user_ids, item_tab, num_items, ldi, d);
+  hnm_status st = dot_validate(ctx, user_tab, num_users, ldu, user_ids, B, item_tab, num_items, ldi, d);
   if (st) return st;
-  HNM_REQUIRE(k >= 1 && k <= 64 && out_idx, HNM_EINVAL, "dot_topk: fused path needs 1 <= k <= 64");
+  HNM_REQUIRE(k >= 1 && k <= 64 && (out_idx || B == 0), HNM_EINVAL, "dot_topk: fused path needs 1 <= k <= 64");
   if (B <= 0) return HNM_OK;
   const int64_t I = num_items;
   const bool bias = user_bias || item_bias || const_bias;
@@ -655,9 +656,9 @@ extern "C" hnm_status hnm_dot_topk_begin_f32(hnm_ctx* ctx, const float* user_tab
                                              const float* item_bias, const float* const_bias,
                                              const int64_t* mask_ptr, const int32_t* mask_idx,
                                              int k, float* lower_bound) {
-  hnm_status st = dot_validate(ctx, user_tab, num_users, ldu, user_ids, item_tab, num_items, ldi, d);
+  hnm_status st = dot_validate(ctx, user_tab, num_users, ldu, user_ids, B, item_tab, num_items, ldi, d);
   if (st) return st;
-  HNM_REQUIRE(k >= 1 && k <= 64 && lower_bound, HNM_EINVAL, "dot_topk_begin: bad argument");
+  HNM_REQUIRE(k >= 1 && k <= 64 && (lower_bound || B == 0), HNM_EINVAL, "dot_topk_begin: bad argument");
   HNM_REQUIRE(!ctx->pend.kind, HNM_EINVAL, "dot_topk_begin: a two-phase call is already open");
   if (B <= 0) return HNM_OK;
   const bool cert = ctx->prefilter && dot_cert_eligible(d, num_items, k);
@@ -687,7 +688,7 @@ extern "C" hnm_status hnm_dot_topk_finish_f32(hnm_ctx* ctx, const float* user_ta
                                               const int64_t* mask_ptr, const int32_t* mask_idx,
                                               int k, const float* lower_bound, int short_ok,
                                               float* out_val, int64_t* out_idx) {
-  HNM_REQUIRE(ctx && out_idx, HNM_EINVAL, "dot_topk_finish: bad argument");
+  HNM_REQUIRE(ctx && (out_idx || B == 0), HNM_EINVAL, "dot_topk_finish: bad argument");
   if (B <= 0) return HNM_OK;
   const int kind = ctx->pend.kind;
   HNM_REQUIRE((kind == HNM_PEND_DOT_CERT || kind == HNM_PEND_DOT_EXACT) && ctx->pend.B == B &&
@@ -700,7 +701,7 @@ extern "C" hnm_status hnm_dot_topk_finish_f32(hnm_ctx* ctx, const float* user_ta
                             d, user_bias, item_bias, const_bias, mask_ptr, mask_idx, k, out_val,
                             out_idx);
   HNM_REQUIRE(lower_bound, HNM_EINVAL, "dot_topk_finish: lower_bound is NULL");
-  hnm_status st = dot_validate(ctx, user_tab, num_users, ldu, user_ids, item_tab, num_items, ldi, d);
+  hnm_status st = dot_validate(ctx, user_tab, num_users, ldu, user_ids, B, item_tab, num_items, ldi, d);
   if (st) return st;
   HNM_REQUIRE(ctx->ws && ctx->ws_size >= dot_cert_bytes(B, num_items, d, k, ctx->num_cus),
               HNM_EINVAL, "dot_topk_finish: the begin phase's workspace is gone");
@@ -715,9 +716,9 @@ extern "C" hnm_status hnm_dot_scores_f32(hnm_ctx* ctx, const float* user_tab, in
                                          const float* item_tab, int64_t num_items, int64_t ldi,
                                          int d, const float* user_bias, const float* item_bias,
                                          const float* const_bias, float* out, int64_t ldo) {
-  hnm_status st = dot_validate(ctx, user_tab, num_users, ldu, user_ids, item_tab, num_items, ldi, d);
+  hnm_status st = dot_validate(ctx, user_tab, num_users, ldu, user_ids, B, item_tab, num_items, ldi, d);
   if (st) return st;
-  HNM_REQUIRE(out && ldo >= num_items, HNM_EINVAL, "dot_scores: bad output");
+  HNM_REQUIRE((out || B == 0) && ldo >= num_items, HNM_EINVAL, "dot_scores: bad output");
   if (B <= 0) return HNM_OK;
   DotArgs a = dot_args(ctx, user_tab, num_users, ldu, user_ids, B, item_tab, num_items, ldi, d,
                        user_bias, item_bias, const_bias, nullptr, nullptr, 1);
@@ -739,7 +740,7 @@ extern "C" hnm_status hnm_topk_rows_f32(hnm_ctx* ctx, const float* scores, int64
                                         int64_t I, const int64_t* mask_ptr,
                                         const int32_t* mask_idx, int k, float* out_val,
                                         int64_t* out_idx) {
-  HNM_REQUIRE(ctx && scores && out_idx, HNM_EINVAL, "topk_rows: NULL argument");
+  HNM_REQUIRE(ctx && ((scores && out_idx) || B == 0), HNM_EINVAL, "topk_rows: NULL argument");
   HNM_REQUIRE(k >= 1 && k <= I && ld >= I, HNM_EINVAL, "topk_rows: bad k/shape");
   HNM_REQUIRE(I < INT_BIG, HNM_EUNSUPPORTED, "topk_rows: too many items");
   if (B <= 0) return HNM_OK;
@@ -784,7 +785,7 @@ extern "C" hnm_status hnm_dot_prefilter_debug_f32(hnm_ctx* ctx, const float* use
                                                   int64_t ldi, int d, const float* user_bias,
                                                   const float* item_bias, const float* const_bias,
                                                   float* approx, int64_t lda, float* bound) {
-  hnm_status st = dot_validate(ctx, user_tab, num_users, ldu, user_ids, item_tab, num_items, ldi, d);
+  hnm_status st = dot_validate(ctx, user_tab, num_users, ldu, user_ids, B, item_tab, num_items, ldi, d);
   if (st) return st;
   HNM_REQUIRE(approx && bound && lda >= num_items, HNM_EINVAL, "dot_prefilter_debug: bad output");
   if (B <= 0) return HNM_OK;

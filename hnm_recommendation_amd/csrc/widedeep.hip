@@ -2027,8 +2027,8 @@ extern "C" hnm_status hnm_widedeep_topk_f32(hnm_ctx* ctx, const hnm_widedeep_wei
                                             const float* user_features, const int64_t* mask_ptr,
                                             const int32_t* mask_idx, int k, float* out_val,
                                             int64_t* out_idx) {
-  HNM_REQUIRE(k >= 1 && k <= 64 && out_idx, HNM_EINVAL, "widedeep_topk: fused path needs 1 <= k <= 64");
-  HNM_REQUIRE(ctx && user_ids, HNM_EINVAL, "widedeep: NULL argument");
+  HNM_REQUIRE(k >= 1 && k <= 64 && (out_idx || B == 0), HNM_EINVAL, "widedeep_topk: fused path needs 1 <= k <= 64");
+  HNM_REQUIRE(ctx && (user_ids || B == 0), HNM_EINVAL, "widedeep: NULL argument");
   WdSetup S;
   hnm_status st = wd_shape(w, &S.pr);
   if (st) return st;
@@ -2057,8 +2057,8 @@ extern "C" hnm_status hnm_widedeep_scores_f32(hnm_ctx* ctx, const hnm_widedeep_w
                                               const int64_t* user_ids, int64_t B,
                                               const float* user_features, float* out,
                                               int64_t ldo) {
-  HNM_REQUIRE(out && w && ldo >= w->num_items, HNM_EINVAL, "widedeep_scores: bad output");
-  HNM_REQUIRE(ctx && user_ids, HNM_EINVAL, "widedeep: NULL argument");
+  HNM_REQUIRE((out || B == 0) && w && ldo >= w->num_items, HNM_EINVAL, "widedeep_scores: bad output");
+  HNM_REQUIRE(ctx && (user_ids || B == 0), HNM_EINVAL, "widedeep: NULL argument");
   WdSetup S;
   hnm_status st = wd_shape(w, &S.pr);
   if (st) return st;
@@ -2101,7 +2101,7 @@ extern "C" hnm_status hnm_widedeep_pair_scores_ex_f32(hnm_ctx* ctx, const hnm_wi
                                                       const float* user_features,
                                                       const float* item_features, int64_t n,
                                                       float* out) {
-  HNM_REQUIRE(ctx && w && user_ids && item_ids && out, HNM_EINVAL, "widedeep_pair: NULL argument");
+  HNM_REQUIRE(ctx && w && ((user_ids && item_ids && out) || n == 0), HNM_EINVAL, "widedeep_pair: NULL argument");
   HNM_REQUIRE(w->l1 <= 512 && w->l2 <= 512 && w->l3 <= 512 && w->l1_in <= 512, HNM_EUNSUPPORTED,
               "widedeep_pair: widths must be <= 512");
   const int Fu = w->num_user_features, Fi = itf ? itf->num_item_features : 0;

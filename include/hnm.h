@@ -10,7 +10,9 @@
  * Conventions
  *  - Every pointer argument is a DEVICE pointer owned by the caller (the torch caching
  *    allocator); the library never frees caller memory.  Shapes are row-major, fp32
- *    tables with an explicit leading dimension, int64 ids.
+ *    tables with an explicit leading dimension, int64 ids.  An empty batch (B == 0 or
+ *    n == 0) is a no-op whose per-row pointers (ids, outputs, bounds) may be NULL -- what
+ *    torch hands over for an empty tensor.
  *  - Calls are asynchronous and stream-ordered on the ctx stream (hnm_ctx_set_stream:
  *    torch's current stream).  A ctx is not re-entrant: use one per (device, thread)
  *    (the Python layer does: one per thread, destroyed when the thread exits).  Switching
