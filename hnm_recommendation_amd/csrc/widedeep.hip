@@ -483,12 +483,63 @@ typedef _Float16 wh8 __attribute__((ext_vector_type(8)));
 #ifndef WD_LO_EXACT  // |x_lo| := 0 where z < 0 (exact) instead of |f16(z - f16(z))|
 #define WD_LO_EXACT 0
 #endif
-#ifndef WD_PREFETCH  // one-pass k loop: weight fragments this many k steps ahead (2 or 3)
-#define WD_PREFETCH 3
+#ifndef WD_PAIRS  // one-pass k loop in register-set pairs (0: one step per iteration + copies)
+#define WD_PAIRS 1
 #endif
+#ifndef WD_PREFETCH  // one-pass k loop: weight fragments this many k steps ahead (2 or 3)
+#define WD_PREFETCH 2
+#endif
+
+// one 16-B fragment per lane from a buffer: a uniform byte offset (SGPR) + lane * 16, so a
+// fragment costs one scalar add instead of a 64-bit per-lane address (8 of those held across
+// the k loop were spilled and reloaded every step, each reload's vmcnt wait also waiting for
+// the prefetched fragments)
+__device__ __forceinline__ wh8 wd_frag(__amdgpu_buffer_rsrc_t rs, int lane, int byte_off) {
+  return __builtin_bit_cast(wh8, __builtin_amdgcn_raw_buffer_load_b128(rs, lane * 16, byte_off, 0));
+}
 
 __device__ __forceinline__ f32x16 wd_mfma16(wh8 a, wh8 b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+}
+
+// One pass over k with every layer-2 row block (G2 = RB2 = 8, two users: 256 accumulator
+// registers = the whole AGPR file).  Every other accumulator is pinned by inline asm so the
+// compiler keeps layer 2's in place (left to it, it moved ~140 accumulator registers per k step
+// between the files): the bound MFMAs' in VGPRs ("+v"), layer 3's in the AGPRs layer 2 has
+// released ("=a" / "+a").  Layer 2's own MFMAs stay builtins: as asm they were issued in one
+// block, with no vector work between them (a step then costs MFMA + VALU time, not the max).
+// Wait states (nothing is padded inside an asm string): NOP = 2 states before an MFMA whose
+// B operand a VALU instruction may just have written; an accumulate chain (C = the previous
+// MFMA's D, same shape) needs none; the results -> any other reader: the s_nop fences after
+// each loop.
+#ifndef WD_ASM_ACC
+#define WD_ASM_ACC 1
+#endif
+#ifndef WD_ASM_BOUND  // (0: the bound MFMAs as builtins: measured 128 accumulator moves a step)
+#define WD_ASM_BOUND 1
+#endif
+template <bool NOP>
+__device__ __forceinline__ void wd_mfma16x_accv(f32x4& c, const wh8& a, const wh8& b) {
+  if (NOP)
+    asm volatile("s_nop 1\n\tv_mfma_f32_16x16x32_f16 %0, %1, %2, %0" : "+v"(c) : "v"(a), "v"(b));
+  else
+    asm volatile("v_mfma_f32_16x16x32_f16 %0, %1, %2, %0" : "+v"(c) : "v"(a), "v"(b));
+}
+// D = a b (C = 0), D in accumulator registers
+template <bool NOP>
+__device__ __forceinline__ void wd_mfma_acc0(f32x16& d, const wh8& a, const wh8& b) {
+  if (NOP)
+    asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_f16 %0, %1, %2, 0" : "=a"(d) : "v"(a), "v"(b));
+  else
+    asm volatile("v_mfma_f32_32x32x16_f16 %0, %1, %2, 0" : "=a"(d) : "v"(a), "v"(b));
+}
+// c += a b in place, c in accumulator registers
+template <bool NOP>
+__device__ __forceinline__ void wd_mfma_acc(f32x16& c, const wh8& a, const wh8& b) {
+  if (NOP)
+    asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_f16 %0, %1, %2, %0" : "+a"(c) : "v"(a), "v"(b));
+  else
+    asm volatile("v_mfma_f32_32x32x16_f16 %0, %1, %2, %0" : "+a"(c) : "v"(a), "v"(b));
 }
 
 // c - (float)h for the low (SEL = 0) or high (SEL = 1) f16 half of a packed register: one
@@ -911,7 +962,7 @@ struct WdScanArgs {
 #define WDC_VPM 4  // VALU instructions scheduled per MFMA in the k loop's interleave
 #endif
 #ifndef WDC_G2
-#define WDC_G2 4  // layer-2 row blocks per pass over k (the x operands are formed once per pass)
+#define WDC_G2 8  // layer-2 row blocks per pass over k (the x operands are formed once per pass)
 #endif
 #ifndef WDC_INTERLEAVE
 #define WDC_INTERLEAVE 1  // sched_group_barrier interleave of the k loop (0: compiler order)
@@ -919,17 +970,21 @@ struct WdScanArgs {
 
 // Block = 4 waves x UPW users each (rows blockIdx.x * 4 UPW + wave * UPW + v) x item
 // partition blockIdx.y; the Q tile (32 items, fp32) is shared through LDS.  Per tile a wave
-// runs layer 2 as 3 x RB2 x K1P/16 split-f16 MFMAs per user (G2 row blocks per pass over
-// k, the next layer fed from the accumulators as each pass completes), layer 3 as
-// 3 x OB x 2 RB2, then the bound.  UPW = 2: every weight fragment loaded from L2 feeds six
-// MFMAs (two users' B operands) instead of three -- the fragment stream is what bounds the
-// one-user variant (tools/wd_ablation.sh: no weight loads = -19% time).
+// runs layer 2 as WD_SPLIT_PASSES x RB2 x K1P/16 f16 MFMAs per user (G2 row blocks per pass
+// over k, the next layer fed from the accumulators as each pass completes), layer 3 as
+// WD_SPLIT_PASSES3 x OB x 2 RB2, then the bound.  UPW = 2: every weight fragment loaded from
+// L2 feeds two users' MFMAs -- the fragment stream is what bounds the one-user variant
+// (tools/wd_ablation.sh: no weight loads = -19% time).  Round 3 product: G2 = RB2 = 8, one
+// pass over k (the x operands, most of the k loop's vector work, formed once per tile instead
+// of once per pass: 217 -> 160-164 ms), layer 2's 256 accumulators in the AGPR file, layer 3
+// after all of layer 2 (ASMACC below).
 template <int RB2, int OB, int G2, int MODE, int UPW, int ABL = 0>
 __global__ __launch_bounds__(256, UPW == 1 ? 2 : 1) void wdc_scan_kernel(WdScanArgs A) {
   constexpr int NOB = OB > 0 ? OB : 1;
   constexpr int NL = OB > 0 ? OB : RB2;
   constexpr int NU = 4 * UPW;  // users per block
   constexpr bool BM = WD_SPLIT_PASSES == 1 && WD_BOUND_MFMA;
+  constexpr bool ASMACC = BM && WD_ASM_ACC && G2 == RB2 && WD_PAIRS;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int K1P = A.K1P, KB = K1P / 16, QRS = K1P + 4;
   float* qs = smem;               // [32][QRS]
@@ -945,6 +1000,12 @@ __global__ __launch_bounds__(256, UPW == 1 ? 2 : 1) void wdc_scan_kernel(WdScanA
   const int qn_off = (int)(v1os + K1P - smem);
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5, j = lane & 31;
+  const __amdgpu_buffer_rsrc_t w2rs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)A.W2hl, 0, RB2 * KB * 2 * 1024, 0x00020000);
+  const __amdgpu_buffer_rsrc_t wbrs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)A.WBf, 0, KB * 2 * 1024, 0x00020000);
+  const __amdgpu_buffer_rsrc_t w3rs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)A.W3hl, 0, NOB * 2 * RB2 * 2 * 1024, 0x00020000);
   const int64_t ublk = (int64_t)blockIdx.x * NU;
   const int p = blockIdx.y;
   const int64_t part_start = (int64_t)p * A.ipp;
@@ -1073,8 +1134,8 @@ __global__ __launch_bounds__(256, UPW == 1 ? 2 : 1) void wdc_scan_kernel(WdScanA
       const float* v1p = g == 0 ? v1s : v0s;
       const float* vop = g == 0 ? v1os : v0s;
       auto frag = [&](int gi, int kk, int hl) {
-        const int64_t q = (ABL & 1) ? (int64_t)gi * 2 : ((int64_t)(g * G2 + gi) * KB + kk) * 2;
-        return A.W2hl[(q + hl) * 64 + lane];
+        const int q = (ABL & 1) ? gi * 2 : ((g * G2 + gi) * KB + kk) * 2;
+        return wd_frag(w2rs, lane, (q + hl) * 1024);
       };
       auto form = [&](int kk, const float* vrow, const float* vorow, wh8* oh, wh8* ol) {
         const float4 q0 = *reinterpret_cast<const float4*>(qrow + 16 * kk);
@@ -1149,8 +1210,8 @@ __global__ __launch_bounds__(256, UPW == 1 ? 2 : 1) void wdc_scan_kernel(WdScanA
           if (WD_SPLIT_PASSES == 3) al[gi] = frag(gi, kb, 1);
         }
         if constexpr (BM) {
-          bn[0] = A.WBf[((NG2 == 1 ? 0 : g) * KB + kn) * 64 + lane];
-          if (NG2 == 1) bn[1] = A.WBf[(KB + kn) * 64 + lane];
+          bn[0] = wd_frag(wbrs, lane, (int)(((NG2 == 1 ? 0 : g) * KB + kn)) * 1024);
+          if (NG2 == 1) bn[1] = wd_frag(wbrs, lane, (int)((KB + kn)) * 1024);
         }
 #pragma unroll
         for (int gi = 0; gi < G2; ++gi)
@@ -1210,10 +1271,15 @@ __global__ __launch_bounds__(256, UPW == 1 ? 2 : 1) void wdc_scan_kernel(WdScanA
 #pragma unroll
         for (int gi = 0; gi < G2; ++gi)
 #pragma unroll
-          for (int v = 0; v < UPW; ++v) acc2[v][gi] = wd_mfma16(a[gi], xh[v], acc2[v][gi]);
+          for (int v = 0; v < UPW; ++v) {
+            acc2[v][gi] = wd_mfma16(a[gi], xh[v], acc2[v][gi]);
+          }
 #pragma unroll
         for (int v = 0; v < UPW; ++v) {
-          if (NG2 == 1) {
+          if constexpr (ASMACC && WD_ASM_BOUND && NG2 == 1) {
+            wd_mfma16x_accv<true>(accb[v], bq[0], xh[v]);
+            wd_mfma16x_accv<true>(accb[v], bq[1], xl[v]);
+          } else if (NG2 == 1) {
             accb[v] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bq[0], xh[v], accb[v], 0, 0, 0);
             accb[v] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bq[1], xl[v], accb[v], 0, 0, 0);
           } else {
@@ -1223,8 +1289,8 @@ __global__ __launch_bounds__(256, UPW == 1 ? 2 : 1) void wdc_scan_kernel(WdScanA
         }
 #pragma unroll
         for (int gi = 0; gi < G2; ++gi) a[gi] = frag(gi, kf, 0);
-        bq[0] = A.WBf[((NG2 == 1 ? 0 : g) * KB + kf) * 64 + lane];
-        if (NG2 == 1) bq[1] = A.WBf[(KB + kf) * 64 + lane];
+        bq[0] = wd_frag(wbrs, lane, (int)(((NG2 == 1 ? 0 : g) * KB + kf)) * 1024);
+        if (NG2 == 1) bq[1] = wd_frag(wbrs, lane, (int)((KB + kf)) * 1024);
         form(kn, v0s, v0s, nxh, nxl);
 #pragma unroll
         for (int e = 0; e < QPS; ++e) {
@@ -1254,16 +1320,16 @@ __global__ __launch_bounds__(256, UPW == 1 ? 2 : 1) void wdc_scan_kernel(WdScanA
           if (WD_PREFETCH == 3) fc[gi] = frag(gi, k2, 0);
         }
         const int bo = (NG2 == 1 ? 0 : g) * KB;
-        ba[0] = A.WBf[bo * 64 + lane];
-        bb[0] = A.WBf[(bo + k1) * 64 + lane];
-        if (WD_PREFETCH == 3) bc3[0] = A.WBf[(bo + k2) * 64 + lane];
+        ba[0] = wd_frag(wbrs, lane, (int)(bo) * 1024);
+        bb[0] = wd_frag(wbrs, lane, (int)((bo + k1)) * 1024);
+        if (WD_PREFETCH == 3) bc3[0] = wd_frag(wbrs, lane, (int)((bo + k2)) * 1024);
         if (NG2 == 1) {
-          ba[1] = A.WBf[KB * 64 + lane];
-          bb[1] = A.WBf[(KB + k1) * 64 + lane];
-          if (WD_PREFETCH == 3) bc3[1] = A.WBf[(KB + k2) * 64 + lane];
+          ba[1] = wd_frag(wbrs, lane, (int)(KB) * 1024);
+          bb[1] = wd_frag(wbrs, lane, (int)((KB + k1)) * 1024);
+          if (WD_PREFETCH == 3) bc3[1] = wd_frag(wbrs, lane, (int)((KB + k2)) * 1024);
         }
       }
-      if constexpr (BM) {
+      if constexpr (BM && WD_PAIRS) {
         // steps in pairs with the two register sets swapped (the one-pass kernel is issue-bound:
         // the copies of the copy form below were 28 v_mov per step; the 2-pass kernel was
         // MFMA-bound and measured 266 vs 261 ms the other way round)
@@ -1295,6 +1361,10 @@ __global__ __launch_bounds__(256, UPW == 1 ? 2 : 1) void wdc_scan_kernel(WdScanA
           step(kb, fa, fb, xha, xla, xhb, xlb, ba, bb);
 #pragma unroll
           for (int gi = 0; gi < G2; ++gi) fa[gi] = fb[gi];
+          if constexpr (BM) {
+            ba[0] = bb[0];
+            ba[1] = bb[1];
+          }
 #pragma unroll
           for (int v = 0; v < UPW; ++v) {
             xha[v] = xhb[v];
@@ -1302,12 +1372,109 @@ __global__ __launch_bounds__(256, UPW == 1 ? 2 : 1) void wdc_scan_kernel(WdScanA
           }
         }
       }
+      if constexpr (ASMACC) {
+        // the last MFMAs' results -> any reader: 8-pass XDL, 12+ wait states; the fence names
+        // every accumulator so no read is scheduled above it
+        asm volatile("s_nop 7\n\ts_nop 7");
+#pragma unroll
+        for (int v = 0; v < UPW; ++v)
+#pragma unroll
+          for (int gi = 0; gi < G2; ++gi) asm volatile("" : "+a"(acc2[v][gi]));
+#pragma unroll
+        for (int v = 0; v < UPW; ++v) asm volatile("" : "+v"(accb[v]));
+      }
       if (G2 < RB2 && g == 0) {  // zeroed after the k loop (G2 = RB2: by the first MFMA's C = 0)
 #pragma unroll
         for (int v = 0; v < UPW; ++v)
 #pragma unroll
           for (int ob = 0; ob < NOB; ++ob)
             acc3[v][ob] = f32x16{0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      }
+      // One pass over k (G2 = RB2) with a layer 3: every row block's x2 first (its f16 B operand
+      // kept in 8 registers per row block and user, its bound term summed), then layer 3 -- so
+      // layer 3's accumulators take the registers of layer 2's, which are all dead by then
+      // (one phase per row block kept both sets live and spilled).
+      if constexpr (G2 == RB2 && OB > 0 && WD_SPLIT_PASSES3 == 1) {
+        // in halves of RH row blocks: x2 of the half's blocks (their f16 B operands, their
+        // bound terms), then their layer-3 MFMAs -- layer 3's accumulators take the registers of
+        // the first half's layer-2 ones (all 256 accumulator registers hold layer 2 until then)
+        constexpr int RH = RB2 >= 2 ? RB2 / 2 : 1;
+        // the bias / bound rows are loop-invariant LDS reads: an opaque offset per tile keeps
+        // them from being hoisted out of the tile loop (256 registers held across it: spilled)
+        int lz = 0;
+        asm volatile("" : "+v"(lz));
+        const float* b2t = b2l + lz;
+        const float* v2t = v2l + lz;
+        const f32x16 zero16 = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int r0 = 0; r0 < RB2; r0 += RH) {
+          wh8 yh_h[UPW][RH][2];
+#pragma unroll
+          for (int rr = 0; rr < RH; ++rr) {
+            // one row block at a time: hoisting every block's accumulator reads needs 256 VGPRs
+            __builtin_amdgcn_sched_barrier(0);
+            const int rb = r0 + rr;
+            float bias16[16], vv16[16];
+#pragma unroll
+            for (int r4 = 0; r4 < 4; ++r4) {
+              const float4 bb = *reinterpret_cast<const float4*>(b2t + rb * 32 + 8 * r4 + 4 * h);
+              const float4 vq = *reinterpret_cast<const float4*>(v2t + rb * 32 + 8 * r4 + 4 * h);
+              bias16[4 * r4] = bb.x; bias16[4 * r4 + 1] = bb.y; bias16[4 * r4 + 2] = bb.z; bias16[4 * r4 + 3] = bb.w;
+              vv16[4 * r4] = vq.x; vv16[4 * r4 + 1] = vq.y; vv16[4 * r4 + 2] = vq.z; vv16[4 * r4 + 3] = vq.w;
+            }
+#pragma unroll
+            for (int v = 0; v < UPW; ++v) {
+#pragma unroll
+              for (int r = 0; r < 16; ++r) {
+                const float y = fmaxf(fmaf(acc2[v][rb][r], c2, bias16[r]), 0.f);
+                bx2[v] = fmaf(vv16[r], y, bx2[v]);
+                yh_h[v][rr][r >> 3][r & 7] = (_Float16)y;
+              }
+              // the bound sum is due here: otherwise it is sunk to its use after layer 3,
+              // holding every fp32 x2 value live (spilled)
+              asm volatile("" : "+v"(bx2[v]));
+            }
+          }
+#pragma unroll
+          for (int rr = 0; rr < RH; ++rr) {
+#pragma unroll
+            for (int half2 = 0; half2 < 2; ++half2) {
+              __builtin_amdgcn_sched_barrier(0);
+              const int kb3 = 2 * (r0 + rr) + half2;
+              wh8 bh[NOB];
+#pragma unroll
+              for (int ob = 0; ob < NOB; ++ob) {
+                const int q = (ABL & 8) ? ob * 2 : (ob * 2 * RB2 + kb3) * 2;
+                bh[ob] = wd_frag(w3rs, lane, q * 1024);
+              }
+              const bool first = r0 == 0 && rr == 0 && half2 == 0;
+#pragma unroll
+              for (int ob = 0; ob < NOB; ++ob)
+#pragma unroll
+                for (int v = 0; v < UPW; ++v) {
+                  if constexpr (ASMACC) {
+                    if (first) {
+                      if (ob == 0) wd_mfma_acc0<true>(acc3[v][ob], bh[ob], yh_h[v][rr][half2]);
+                      else wd_mfma_acc0<false>(acc3[v][ob], bh[ob], yh_h[v][rr][half2]);
+                    } else {
+                      if (ob == 0) wd_mfma_acc<true>(acc3[v][ob], bh[ob], yh_h[v][rr][half2]);
+                      else wd_mfma_acc<false>(acc3[v][ob], bh[ob], yh_h[v][rr][half2]);
+                    }
+                  } else {
+                    acc3[v][ob] = wd_mfma16(bh[ob], yh_h[v][rr][half2], first ? zero16 : acc3[v][ob]);
+                  }
+                }
+            }
+          }
+        }
+        if constexpr (ASMACC) {  // layer 3's results -> the VALU readers below
+          asm volatile("s_nop 7\n\ts_nop 7");
+#pragma unroll
+          for (int v = 0; v < UPW; ++v)
+#pragma unroll
+            for (int ob = 0; ob < NOB; ++ob) asm volatile("" : "+a"(acc3[v][ob]));
+        }
+        continue;
       }
       // x2 = relu(D2 + b2') in s2 units feeds layer 3 (or the final dot)
 #pragma unroll
@@ -1346,9 +1513,9 @@ __global__ __launch_bounds__(256, UPW == 1 ? 2 : 1) void wdc_scan_kernel(WdScanA
             wh8 bh[NOB], bl[NOB];
 #pragma unroll
             for (int ob = 0; ob < NOB; ++ob) {
-              const int64_t q = (ABL & 8) ? (int64_t)ob * 2 : ((int64_t)ob * 2 * RB2 + kb3) * 2;
-              bh[ob] = A.W3hl[q * 64 + lane];
-              if (WD_SPLIT_PASSES3 == 3) bl[ob] = A.W3hl[(q + 1) * 64 + lane];
+              const int q = (ABL & 8) ? ob * 2 : (ob * 2 * RB2 + kb3) * 2;
+              bh[ob] = wd_frag(w3rs, lane, q * 1024);
+              if (WD_SPLIT_PASSES3 == 3) bl[ob] = wd_frag(w3rs, lane, (q + 1) * 1024);
             }
             // G2 = RB2: the chain starts at the first row block with C = 0 (an inline constant),
             // so acc3 becomes live only as acc2's registers are consumed
