@@ -387,7 +387,7 @@ def serve_latency(args, device):
 # W&D the 2-pass split (W_hi x_hi + W_hi x_lo) of layer 2 (2 x 262,144) and one pass of
 # layer 3 (65,536); dot d = 64: 128
 ALG_FLOP_PER_PAIR = {"ncf": 4352.0, "widedeep": 328450.0, "mf": 128.0}
-ISSUED_F16_FLOP_PER_PAIR = {"ncf": 5248.0, "widedeep": 589824.0, "mf": 128.0}
+ISSUED_F16_FLOP_PER_PAIR = {"ncf": 5248.0, "widedeep": 360448.0, "mf": 128.0}
 RANDOM_DATA_F16_TFLOPS = 1235.0  # bare f16 MFMA loop, random operands: 1,190-1,291 TF/s
 
 

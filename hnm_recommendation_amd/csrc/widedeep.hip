@@ -494,8 +494,14 @@ typedef _Float16 wh8 __attribute__((ext_vector_type(8)));
 // fragment costs one scalar add instead of a 64-bit per-lane address (8 of those held across
 // the k loop were spilled and reloaded every step, each reload's vmcnt wait also waiting for
 // the prefetched fragments)
-__device__ __forceinline__ wh8 wd_frag(__amdgpu_buffer_rsrc_t rs, int lane, int byte_off) {
-  return __builtin_bit_cast(wh8, __builtin_amdgcn_raw_buffer_load_b128(rs, lane * 16, byte_off, 0));
+// Fragments are held as 4 x 32-bit registers and viewed as 8 f16 only at the MFMA: arrays of
+// wh8 were merged into one <64 x half> value whose lane moves the backend emitted as
+// v_bfi_b32 "copies" of freshly loaded fragments, each waiting for its load (the prefetch
+// distance dropped to zero)
+typedef unsigned wfr __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ wh8 wd_h(wfr f) { return __builtin_bit_cast(wh8, f); }
+__device__ __forceinline__ wfr wd_frag(__amdgpu_buffer_rsrc_t rs, int lane, int byte_off) {
+  return __builtin_bit_cast(wfr, __builtin_amdgcn_raw_buffer_load_b128(rs, lane * 16, byte_off, 0));
 }
 
 __device__ __forceinline__ f32x16 wd_mfma16(wh8 a, wh8 b, f32x16 c) {
@@ -514,6 +520,9 @@ __device__ __forceinline__ f32x16 wd_mfma16(wh8 a, wh8 b, f32x16 c) {
 // each loop.
 #ifndef WD_ASM_ACC
 #define WD_ASM_ACC 1
+#endif
+#ifndef WD_ASM_L3  // layer 3's MFMAs as asm (0: builtins)
+#define WD_ASM_L3 1
 #endif
 #ifndef WD_ASM_BOUND  // (0: the bound MFMAs as builtins: measured 128 accumulator moves a step)
 #define WD_ASM_BOUND 1
@@ -964,6 +973,19 @@ struct WdScanArgs {
 #ifndef WDC_G2
 #define WDC_G2 8  // layer-2 row blocks per pass over k (the x operands are formed once per pass)
 #endif
+#ifndef WD_STAMPS  // diagnostic builds only: per-phase s_memtime cycle sums (tools/wd_stamps.py)
+#define WD_STAMPS 0
+#endif
+#if WD_STAMPS
+__device__ unsigned long long wd_stamp_acc[4];  // k loop, layer-2 epilogue + layer 3, final, tiles
+extern "C" int hnm_debug_wd_stamps(unsigned long long* out) {
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(wd_stamp_acc), sizeof(wd_stamp_acc));
+}
+extern "C" int hnm_debug_wd_stamps_reset() {
+  const unsigned long long z[4] = {0, 0, 0, 0};
+  return (int)hipMemcpyToSymbol(HIP_SYMBOL(wd_stamp_acc), z, sizeof(z));
+}
+#endif
 #ifndef WDC_INTERLEAVE
 #define WDC_INTERLEAVE 1  // sched_group_barrier interleave of the k loop (0: compiler order)
 #endif
@@ -1076,6 +1098,7 @@ __global__ __launch_bounds__(256, UPW == 1 ? 2 : 1) void wdc_scan_kernel(WdScanA
   const int qrow_t = tid >> 3, qcol_t = tid & 7;
   const int qvoff = (qrow_t * K1P + qcol_t) * 4;
   auto qrsrc = [&](int64_t nb) {  // the tile at nb: its rows inside the partition
+    if (ABL & 2) nb = part_start;  // ablation: every tile's copy reads the first (cache-hot) tile
     const int64_t rows = std::max<int64_t>(0, std::min<int64_t>(WD_TILE, part_end - nb));
     const float* src = A.Qi + std::min<int64_t>(nb, part_end - 1) * K1P;
     return __builtin_amdgcn_make_buffer_rsrc((void*)src, 0, (int)(rows * K1P * 4), 0x00020000);
@@ -1087,7 +1110,9 @@ __global__ __launch_bounds__(256, UPW == 1 ? 2 : 1) void wdc_scan_kernel(WdScanA
     const __amdgpu_buffer_rsrc_t rs = qrsrc(part_start);
     for (int c = 0; c < K1P; c += 8) smem[qrow_t * QRS + qcol_t + c] = qload(rs, c);
   }
+  unsigned long long st_acc[4] = {0, 0, 0, 0}, st_t0 = 0, st_t1 = 0;
   for (int64_t t = 0; t < ntiles; ++t) {
+    if (WD_STAMPS) st_t0 = __builtin_amdgcn_s_memtime();
     const int64_t base = part_start + t * WD_TILE;
     const int cur_off = (t & 1) ? qn_off : 0, nxt_off = (t & 1) ? 0 : qn_off;
     const __amdgpu_buffer_rsrc_t qrs = qrsrc(base + WD_TILE);
@@ -1198,12 +1223,12 @@ __global__ __launch_bounds__(256, UPW == 1 ? 2 : 1) void wdc_scan_kernel(WdScanA
       };
       // one k step: MFMAs on the (ah, xh, xl) set while the other set is loaded / formed for
       // step kb + 1
-      auto step = [&](int kb, const wh8 (&ah)[G2], wh8 (&an)[G2], const wh8 (&xh)[UPW],
-                      const wh8 (&xl)[UPW], wh8 (&nxh)[UPW], wh8 (&nxl)[UPW], const wh8 (&bc)[2],
-                      wh8 (&bn)[2]) {
+      auto step = [&](int kb, const wfr (&ah)[G2], wfr (&an)[G2], const wh8 (&xh)[UPW],
+                      const wh8 (&xl)[UPW], wh8 (&nxh)[UPW], wh8 (&nxl)[UPW], const wfr (&bc)[2],
+                      wfr (&bn)[2]) {
         const bool more = kb + 1 < KB;
         const int kn = more ? kb + 1 : kb;
-        wh8 al[G2];
+        wfr al[G2];
 #pragma unroll
         for (int gi = 0; gi < G2; ++gi) {
           an[gi] = frag(gi, kn, 0);
@@ -1216,27 +1241,27 @@ __global__ __launch_bounds__(256, UPW == 1 ? 2 : 1) void wdc_scan_kernel(WdScanA
 #pragma unroll
         for (int gi = 0; gi < G2; ++gi)
 #pragma unroll
-          for (int v = 0; v < UPW; ++v) acc2[v][gi] = wd_mfma16(ah[gi], xh[v], acc2[v][gi]);
+          for (int v = 0; v < UPW; ++v) acc2[v][gi] = wd_mfma16(wd_h(ah[gi]), xh[v], acc2[v][gi]);
 #pragma unroll
         for (int gi = 0; gi < G2; ++gi)
 #pragma unroll
           for (int v = 0; v < UPW; ++v)
-            if (WD_SPLIT_PASSES >= 2) acc2[v][gi] = wd_mfma16(ah[gi], xl[v], acc2[v][gi]);
+            if (WD_SPLIT_PASSES >= 2) acc2[v][gi] = wd_mfma16(wd_h(ah[gi]), xl[v], acc2[v][gi]);
         if (WD_SPLIT_PASSES == 3) {
 #pragma unroll
           for (int gi = 0; gi < G2; ++gi)
 #pragma unroll
-            for (int v = 0; v < UPW; ++v) acc2[v][gi] = wd_mfma16(al[gi], xh[v], acc2[v][gi]);
+            for (int v = 0; v < UPW; ++v) acc2[v][gi] = wd_mfma16(wd_h(al[gi]), xh[v], acc2[v][gi]);
         }
         if constexpr (BM) {
 #pragma unroll
           for (int v = 0; v < UPW; ++v) {
             if (NG2 == 1) {
-              accb[v] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bc[0], xh[v], accb[v], 0, 0, 0);
-              accb[v] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bc[1], xl[v], accb[v], 0, 0, 0);
+              accb[v] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wd_h(bc[0]), xh[v], accb[v], 0, 0, 0);
+              accb[v] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wd_h(bc[1]), xl[v], accb[v], 0, 0, 0);
             } else {
               const wh8 bop = g == 0 ? xh[v] : xl[v];
-              accb[v] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bc[0], bop, accb[v], 0, 0, 0);
+              accb[v] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wd_h(bc[0]), bop, accb[v], 0, 0, 0);
             }
           }
         }
@@ -1263,8 +1288,8 @@ __global__ __launch_bounds__(256, UPW == 1 ? 2 : 1) void wdc_scan_kernel(WdScanA
       // MFMAs have just read -- a two-step prefetch distance with two register sets (the
       // one-pass step is half as long as a two-pass one, so one step ahead left its MFMAs
       // waiting on L2)
-      auto stepd = [&](int kb, wh8 (&a)[G2], const wh8 (&xh)[UPW], const wh8 (&xl)[UPW],
-                       wh8 (&nxh)[UPW], wh8 (&nxl)[UPW], wh8 (&bq)[2]) {
+      auto stepd = [&](int kb, wfr (&a)[G2], const wh8 (&xh)[UPW], const wh8 (&xl)[UPW],
+                       wh8 (&nxh)[UPW], wh8 (&nxl)[UPW], wfr (&bq)[2]) {
         const bool more = kb + 1 < KB;
         const int kn = more ? kb + 1 : kb;
         const int kf = kb + WD_PREFETCH < KB ? kb + WD_PREFETCH : KB - 1;
@@ -1272,19 +1297,19 @@ __global__ __launch_bounds__(256, UPW == 1 ? 2 : 1) void wdc_scan_kernel(WdScanA
         for (int gi = 0; gi < G2; ++gi)
 #pragma unroll
           for (int v = 0; v < UPW; ++v) {
-            acc2[v][gi] = wd_mfma16(a[gi], xh[v], acc2[v][gi]);
+            acc2[v][gi] = wd_mfma16(wd_h(a[gi]), xh[v], acc2[v][gi]);
           }
 #pragma unroll
         for (int v = 0; v < UPW; ++v) {
           if constexpr (ASMACC && WD_ASM_BOUND && NG2 == 1) {
-            wd_mfma16x_accv<true>(accb[v], bq[0], xh[v]);
-            wd_mfma16x_accv<true>(accb[v], bq[1], xl[v]);
+            wd_mfma16x_accv<true>(accb[v], wd_h(bq[0]), xh[v]);
+            wd_mfma16x_accv<true>(accb[v], wd_h(bq[1]), xl[v]);
           } else if (NG2 == 1) {
-            accb[v] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bq[0], xh[v], accb[v], 0, 0, 0);
-            accb[v] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bq[1], xl[v], accb[v], 0, 0, 0);
+            accb[v] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wd_h(bq[0]), xh[v], accb[v], 0, 0, 0);
+            accb[v] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wd_h(bq[1]), xl[v], accb[v], 0, 0, 0);
           } else {
             const wh8 bop = g == 0 ? xh[v] : xl[v];
-            accb[v] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bq[0], bop, accb[v], 0, 0, 0);
+            accb[v] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wd_h(bq[0]), bop, accb[v], 0, 0, 0);
           }
         }
 #pragma unroll
@@ -1307,11 +1332,12 @@ __global__ __launch_bounds__(256, UPW == 1 ? 2 : 1) void wdc_scan_kernel(WdScanA
           }
         }
       };
-      wh8 fa[G2], fb[G2], xha[UPW], xla[UPW], xhb[UPW], xlb[UPW], ba[2], bb[2];
+      wfr fa[G2], fb[G2], ba[2], bb[2];
+      wh8 xha[UPW], xla[UPW], xhb[UPW], xlb[UPW];
       form(0, v1p, vop, xha, xla);
 #pragma unroll
       for (int gi = 0; gi < G2; ++gi) fa[gi] = frag(gi, 0, 0);
-      wh8 fc[G2], bc3[2];  // third fragment set (WD_PREFETCH 3)
+      wfr fc[G2], bc3[2];  // third fragment set (WD_PREFETCH 3)
       if constexpr (BM) {
         const int k1 = KB > 1 ? 1 : 0, k2 = KB > 2 ? 2 : KB - 1;
 #pragma unroll
@@ -1382,6 +1408,10 @@ __global__ __launch_bounds__(256, UPW == 1 ? 2 : 1) void wdc_scan_kernel(WdScanA
           for (int gi = 0; gi < G2; ++gi) asm volatile("" : "+a"(acc2[v][gi]));
 #pragma unroll
         for (int v = 0; v < UPW; ++v) asm volatile("" : "+v"(accb[v]));
+        if (WD_STAMPS) {
+          st_t1 = __builtin_amdgcn_s_memtime();
+          st_acc[0] += st_t1 - st_t0;
+        }
       }
       if (G2 < RB2 && g == 0) {  // zeroed after the k loop (G2 = RB2: by the first MFMA's C = 0)
 #pragma unroll
@@ -1406,6 +1436,19 @@ __global__ __launch_bounds__(256, UPW == 1 ? 2 : 1) void wdc_scan_kernel(WdScanA
         const float* b2t = b2l + lz;
         const float* v2t = v2l + lz;
         const f32x16 zero16 = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        // layer 3's weight fragments, W3D row-block halves (kb3 steps) ahead of their MFMAs: the
+        // first ones are in flight while layer 2's accumulators are converted
+        constexpr int W3D = 2, NK3 = 2 * RB2;
+        wfr w3b[W3D + 1][NOB];
+        auto w3load = [&](int kb3) {
+#pragma unroll
+          for (int ob = 0; ob < NOB; ++ob) {
+            const int q = (ABL & 8) ? ob * 2 : (ob * 2 * RB2 + kb3) * 2;
+            w3b[kb3 % (W3D + 1)][ob] = wd_frag(w3rs, lane, q * 1024);
+          }
+        };
+#pragma unroll
+        for (int k3 = 0; k3 < W3D && k3 < NK3; ++k3) w3load(k3);
 #pragma unroll
         for (int r0 = 0; r0 < RB2; r0 += RH) {
           wh8 yh_h[UPW][RH][2];
@@ -1424,12 +1467,16 @@ __global__ __launch_bounds__(256, UPW == 1 ? 2 : 1) void wdc_scan_kernel(WdScanA
             }
 #pragma unroll
             for (int v = 0; v < UPW; ++v) {
+              // four independent chains (a nonnegative sum: its rounding is inside rho in any
+              // order) instead of one 16-deep dependent chain per row block
+              float part[4] = {bx2[v], 0.f, 0.f, 0.f};
 #pragma unroll
               for (int r = 0; r < 16; ++r) {
                 const float y = fmaxf(fmaf(acc2[v][rb][r], c2, bias16[r]), 0.f);
-                bx2[v] = fmaf(vv16[r], y, bx2[v]);
+                part[r & 3] = fmaf(vv16[r], y, part[r & 3]);
                 yh_h[v][rr][r >> 3][r & 7] = (_Float16)y;
               }
+              bx2[v] = (part[0] + part[1]) + (part[2] + part[3]);
               // the bound sum is due here: otherwise it is sunk to its use after layer 3,
               // holding every fp32 x2 value live (spilled)
               asm volatile("" : "+v"(bx2[v]));
@@ -1441,27 +1488,23 @@ __global__ __launch_bounds__(256, UPW == 1 ? 2 : 1) void wdc_scan_kernel(WdScanA
             for (int half2 = 0; half2 < 2; ++half2) {
               __builtin_amdgcn_sched_barrier(0);
               const int kb3 = 2 * (r0 + rr) + half2;
-              wh8 bh[NOB];
-#pragma unroll
-              for (int ob = 0; ob < NOB; ++ob) {
-                const int q = (ABL & 8) ? ob * 2 : (ob * 2 * RB2 + kb3) * 2;
-                bh[ob] = wd_frag(w3rs, lane, q * 1024);
-              }
+              if (kb3 + W3D < NK3) w3load(kb3 + W3D);
+              const wfr* bh = w3b[kb3 % (W3D + 1)];
               const bool first = r0 == 0 && rr == 0 && half2 == 0;
 #pragma unroll
               for (int ob = 0; ob < NOB; ++ob)
 #pragma unroll
                 for (int v = 0; v < UPW; ++v) {
-                  if constexpr (ASMACC) {
+                  if constexpr (ASMACC && WD_ASM_L3) {
                     if (first) {
-                      if (ob == 0) wd_mfma_acc0<true>(acc3[v][ob], bh[ob], yh_h[v][rr][half2]);
-                      else wd_mfma_acc0<false>(acc3[v][ob], bh[ob], yh_h[v][rr][half2]);
+                      if (ob == 0) wd_mfma_acc0<true>(acc3[v][ob], wd_h(bh[ob]), yh_h[v][rr][half2]);
+                      else wd_mfma_acc0<false>(acc3[v][ob], wd_h(bh[ob]), yh_h[v][rr][half2]);
                     } else {
-                      if (ob == 0) wd_mfma_acc<true>(acc3[v][ob], bh[ob], yh_h[v][rr][half2]);
-                      else wd_mfma_acc<false>(acc3[v][ob], bh[ob], yh_h[v][rr][half2]);
+                      if (ob == 0) wd_mfma_acc<true>(acc3[v][ob], wd_h(bh[ob]), yh_h[v][rr][half2]);
+                      else wd_mfma_acc<false>(acc3[v][ob], wd_h(bh[ob]), yh_h[v][rr][half2]);
                     }
                   } else {
-                    acc3[v][ob] = wd_mfma16(bh[ob], yh_h[v][rr][half2], first ? zero16 : acc3[v][ob]);
+                    acc3[v][ob] = wd_mfma16(wd_h(bh[ob]), yh_h[v][rr][half2], first ? zero16 : acc3[v][ob]);
                   }
                 }
             }
@@ -1473,6 +1516,11 @@ __global__ __launch_bounds__(256, UPW == 1 ? 2 : 1) void wdc_scan_kernel(WdScanA
           for (int v = 0; v < UPW; ++v)
 #pragma unroll
             for (int ob = 0; ob < NOB; ++ob) asm volatile("" : "+a"(acc3[v][ob]));
+        }
+        if (WD_STAMPS) {
+          const unsigned long long t2 = __builtin_amdgcn_s_memtime();
+          st_acc[1] += t2 - st_t1;
+          st_t1 = t2;
         }
         continue;
       }
@@ -1514,8 +1562,8 @@ __global__ __launch_bounds__(256, UPW == 1 ? 2 : 1) void wdc_scan_kernel(WdScanA
 #pragma unroll
             for (int ob = 0; ob < NOB; ++ob) {
               const int q = (ABL & 8) ? ob * 2 : (ob * 2 * RB2 + kb3) * 2;
-              bh[ob] = wd_frag(w3rs, lane, q * 1024);
-              if (WD_SPLIT_PASSES3 == 3) bl[ob] = wd_frag(w3rs, lane, (q + 1) * 1024);
+              bh[ob] = wd_h(wd_frag(w3rs, lane, q * 1024));
+              if (WD_SPLIT_PASSES3 == 3) bl[ob] = wd_h(wd_frag(w3rs, lane, (q + 1) * 1024));
             }
             // G2 = RB2: the chain starts at the first row block with C = 0 (an inline constant),
             // so acc3 becomes live only as acc2's registers are consumed
@@ -1548,6 +1596,9 @@ __global__ __launch_bounds__(256, UPW == 1 ? 2 : 1) void wdc_scan_kernel(WdScanA
 #pragma unroll
     for (int v = 0; v < UPW; ++v) {
       if (OB > 0) {
+        // four independent chains each (at most 16 NOB + 3 roundings on any path, within the
+        // 32 NOB of g3) instead of two 16 NOB-deep dependent chains
+        float fp[4] = {fin[v], 0.f, 0.f, 0.f}, bp[4] = {bx3[v], 0.f, 0.f, 0.f};
 #pragma unroll
         for (int ob = 0; ob < NOB; ++ob) {
 #pragma unroll
@@ -1558,11 +1609,13 @@ __global__ __launch_bounds__(256, UPW == 1 ? 2 : 1) void wdc_scan_kernel(WdScanA
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
               const float z = fmaxf(fmaf(acc3[v][ob][4 * r4 + e], c3, bq[e]), 0.f);
-              fin[v] = fmaf(z, wq[e], fin[v]);
-              bx3[v] = fmaf(fabsf(wq[e]), z, bx3[v]);
+              fp[e] = fmaf(z, wq[e], fp[e]);
+              bp[e] = fmaf(fabsf(wq[e]), z, bp[e]);
             }
           }
         }
+        fin[v] = (fp[0] + fp[1]) + (fp[2] + fp[3]);
+        bx3[v] = (bp[0] + bp[1]) + (bp[2] + bp[3]);
       } else {
         fin[v] *= inv_s2;
       }
@@ -1610,6 +1663,17 @@ __global__ __launch_bounds__(256, UPW == 1 ? 2 : 1) void wdc_scan_kernel(WdScanA
       }
       count[v] += __popcll(m);
     }
+    if (WD_STAMPS) {
+      const unsigned long long t3 = __builtin_amdgcn_s_memtime();
+      st_acc[2] += t3 - st_t1;
+      st_acc[3] += t3 - st_t0;
+    }
+  }
+  if (WD_STAMPS && lane == 0) {
+#if WD_STAMPS
+#pragma unroll
+    for (int i = 0; i < 4; ++i) atomicAdd(&wd_stamp_acc[i], st_acc[i]);
+#endif
   }
   if (MODE == WDC_THRESH) {
 #pragma unroll
