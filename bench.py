@@ -172,7 +172,7 @@ def build_workload(name, rank, world, device, batch, exact=False, weights="init"
         info.update({"model": "WideDeep", "embedding_dim": 64, "deep_layers": [512, 256, 128]})
         bound, kernel = "mfma", ("widedeep_score_kernel" if exact else "wdc_scan_kernel")
         info["scan"] = ("exact fp32" if exact else
-                        "certified split-f16 (layer 2: 2 f16 MFMA passes, layer 3: 1; weight / activation residuals bounded) pre-filter + exact fp32 re-scoring")
+                        "certified f16 (layers 2 and 3: one W_hi.x_hi MFMA pass each; weight and activation residuals bounded exactly, the layer-2 bound terms on the matrix pipe) pre-filter + exact fp32 re-scoring")
         cpu = ("widedeep", None)
     elif name == "mf":
         sd = syn.mf_state_dict(U, I, 64, seed=0)
@@ -384,8 +384,8 @@ def serve_latency(args, device):
 
 # algorithmic FLOP per (user, item) pair and the f16 MFMA FLOP the certified
 # scans issue per pair: NCF 4,096 layer 2 + 1,024 16x16x32 epilogue (64 useful) + 128 GMF;
-# W&D the 2-pass split (W_hi x_hi + W_hi x_lo) of layer 2 (2 x 262,144) and one pass of
-# layer 3 (65,536); dot d = 64: 128
+# W&D one W_hi x_hi pass of layer 2 (262,144), its two bound MFMAs (16x16x32 against x_hi and
+# |x_lo|: 32,768) and one pass of layer 3 (65,536); dot d = 64: 128
 ALG_FLOP_PER_PAIR = {"ncf": 4352.0, "widedeep": 328450.0, "mf": 128.0}
 ISSUED_F16_FLOP_PER_PAIR = {"ncf": 5248.0, "widedeep": 360448.0, "mf": 128.0}
 RANDOM_DATA_F16_TFLOPS = 1235.0  # bare f16 MFMA loop, random operands: 1,190-1,291 TF/s
@@ -573,7 +573,7 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": ("f32" if args.exact or not (f16 or bound == "hbm") else
-                  "f16 split+f32" if kernel == "wdc_scan_kernel" else "f16+f32"),
+                  "f16+f32"),
         "data": "synthetic (PCG64 weights with reference init distributions; H&M shape)",
         "config": {"workload": f"{args.workload}: BASELINE configs[1] NeuralCF dim=64, full H&M "
                                f"shape, batch={B} users/rank, K=12" if args.workload == "ncf"
