@@ -96,7 +96,7 @@ _SIGS = {
     "hnm_spmm_csr_f32": (_i32, [_p, _p, _i64, _p, _p, _p, _p, C.c_int, _p, _f32, _p, _p]),
     "hnm_spmm_csr_range_f32": (_i32, [_p, _p, _i64, _p, _p, _p, _p, C.c_int, _p, _f32, _p, _p,
                                       _f32, _i64, _i64, _i64]),
-    "hnm_spmm_rows_combine_f32": (_i32, [_p, _i64, _p, _p, _p, _p, _i64, C.c_int,
+    "hnm_spmm_rows_combine_f32": (_i32, [_p, _p, _i64, _p, _p, _p, _p, _i64, C.c_int,
                                          C.POINTER(_p), C.POINTER(_f32), C.c_int, _p]),
     "hnm_axpby_f32": (_i32, [_p, _i64, _f32, _p, _f32, _p, _p]),
     "hnm_widedeep_topk_f32": (_i32, [_p, C.POINTER(WideDeepWeights), _p, _i64, _p, _p, _p,

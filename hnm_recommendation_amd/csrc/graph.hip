@@ -17,6 +17,10 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <cstring>
+#include <mutex>
+#include <queue>
+#include <thread>
 #include <vector>
 
 #include "hnm_device.h"
@@ -41,6 +45,21 @@
 #ifndef SPMM_SIDE_STREAM  // heavy-row segments on the ctx's side stream, beside the light kernel
 #define SPMM_SIDE_STREAM 1
 #endif
+// Round 3: rows of more than SPMM_SHORT entries (the item half of the bipartite graph) by the
+// user-ordered walk (spmm_walk_kernel, below) instead of the long / heavy classes.
+#ifndef SPMM_WALK
+#define SPMM_WALK 1
+#endif
+// 0: walk on the side stream beside the short rows; 1: walk then short rows; 2: short then walk
+// (measured, d=64 layer: 1.725 / 1.700 / 1.689 ms; 0 with a normal-priority side stream 1.732)
+#ifndef SPMM_WALK_MODE
+#define SPMM_WALK_MODE 2
+#endif
+#define WALK_THREADS 1024
+#define WALK_LDS_F4 9216        // 144 KiB of float4 row accumulators per workgroup
+#define WALK_GROUPS_TARGET 16384  // total LPR-lane groups of a big graph's walk (all d)
+
+struct WalkSched;
 
 struct hnm_spmm_plan {
   int device;
@@ -57,6 +76,20 @@ struct hnm_spmm_plan {
   int64_t* seg_end;     // [n_seg]
   std::vector<int32_t>* h_heavy;  // host copies (row-range launches)
   std::vector<int64_t>* h_seg_ptr;
+  // user-ordered walk of the rows of more than SPMM_SHORT entries (SPMM_WALK)
+  int walk;
+  int64_t walk_cap;     // entries per piece: a row of L entries is cut into cdiv(L, cap) pieces
+  int64_t n_walk, walk_nnz;
+  int32_t* walk_rows;   // [n_walk] ascending (device)
+  int64_t* walk_ptr;    // [n_walk + 1] offsets into wcol / wval (device)
+  int32_t* wcol;        // [walk_nnz] each walk row's entries sorted by (col, CSR position)
+  float* wval;
+  std::vector<int32_t>* h_walk_rows;
+  std::vector<int64_t>* h_walk_ptr;
+  std::vector<int32_t>* h_wcol;
+  std::vector<float>* h_wval;
+  std::mutex* mu;       // lazy preparation (first call with col/val, first call per d)
+  WalkSched* sched[7];  // per d = 4 << i
 };
 
 // ------------------------------------------------------------------ CSR build kernels
@@ -462,6 +495,203 @@ __global__ __launch_bounds__(256) void spmm_finish_kernel(int64_t h0,
   if (sl == 0) spmm_epilogue((int64_t)heavy_rows[hr], d, c, red[t], X, ep);
 }
 
+// ---------------------------------------------------------------- user-ordered walk
+// Rows of more than SPMM_SHORT entries (the item half: each item row gathers ~300 random rows
+// of the 351 MB user table) as ONE persistent launch whose gathers move through the table in
+// ascending column order.  Each walk row's entries are sorted by (col, CSR position) and cut
+// into pieces: a row of L entries has n = cdiv(L, cap) pieces, piece j holding the sorted
+// entries j, j + n, j + 2n, ... (so every piece spans the whole column range).  A workgroup
+// (one per CU, 1024 threads) owns up to maxloc pieces with their fp32 accumulators in LDS;
+// each LPR-lane group walks ONE list -- its pieces' entries merged by column, packed as
+// col << 10 | slot -- and adds val * X[col] into the slot's accumulator.  All lists of the
+// chip advance through the columns at the same pace, so the rows gathered at any moment lie
+// in a narrow window of X that the XCD L2s hold: measured on the synthetic H&M item half
+// (tools/slice_walk_probe.hip) 0.85 ms vs 1.16 ms for the segmented pull in CSR order.
+// Order: piece j = fma chain from 0 over its entries in (col, position) order; y = p_0 for an
+// unsplit row, else per-slice sums of the pieces and a fixed tree (spmm_walk_finish_kernel);
+// rows_combine repeats it from wcol / wval (walk_row_sum), so listed rows stay bitwise equal
+// to the layer kernels.
+template <int LPR>
+__global__ __launch_bounds__(WALK_THREADS) void spmm_walk_kernel(
+    const int64_t* __restrict__ gptr, const uint32_t* __restrict__ ent,
+    const float* __restrict__ wt, const int32_t* __restrict__ slot_out,
+    const int32_t* __restrict__ nslot, int maxloc, const float* __restrict__ X, int d,
+    float* __restrict__ partial, SpmmEpi ep, int64_t r0, int64_t r1) {
+  constexpr int NG = WALK_THREADS / LPR;
+  __shared__ float4 acc[WALK_LDS_F4];
+  const int tid = threadIdx.x, g = tid / LPR, sub = tid % LPR;
+  const int ns = nslot[blockIdx.x];
+  for (int i = tid; i < ns * LPR; i += WALK_THREADS) acc[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+  __syncthreads();
+  // 4 entries per step (2: 1.741 ms per d=64 layer, 4: 1.694, 8: 1.848; records prefetched a
+  // step ahead as 16-B vectors with 8 or 16 gathers in flight: 1.812 / 1.823)
+  int64_t p = gptr[(int64_t)blockIdx.x * NG + g];
+  const int64_t e = gptr[(int64_t)blockIdx.x * NG + g + 1];
+  for (; p + 3 < e; p += 4) {
+    uint32_t c[4];
+    float w[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      c[u] = ent[p + u];
+      w[u] = wt[p + u];
+    }
+    float4 x[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      x[u] = *reinterpret_cast<const float4*>(X + (int64_t)(c[u] >> 10) * d + 4 * sub);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {  // in list order: a slot's entries stay one fma chain
+      float4* a = &acc[(c[u] & 1023u) * LPR + sub];
+      float4 v = *a;
+      v.x = fmaf(w[u], x[u].x, v.x);
+      v.y = fmaf(w[u], x[u].y, v.y);
+      v.z = fmaf(w[u], x[u].z, v.z);
+      v.w = fmaf(w[u], x[u].w, v.w);
+      *a = v;
+    }
+  }
+  for (; p < e; ++p) {
+    const uint32_t c = ent[p];
+    const float w = wt[p];
+    const float4 x = *reinterpret_cast<const float4*>(X + (int64_t)(c >> 10) * d + 4 * sub);
+    float4* a = &acc[(c & 1023u) * LPR + sub];
+    float4 v = *a;
+    v.x = fmaf(w, x.x, v.x);
+    v.y = fmaf(w, x.y, v.y);
+    v.z = fmaf(w, x.z, v.z);
+    v.w = fmaf(w, x.w, v.w);
+    *a = v;
+  }
+  __syncthreads();
+  for (int i = tid; i < ns * LPR; i += WALK_THREADS) {
+    const int o = slot_out[(int64_t)blockIdx.x * maxloc + i / LPR], c = i % LPR;
+    if (o >= 0) {
+      if (o >= r0 && o < r1) spmm_epilogue(o, d, c, acc[i], X, ep);
+    } else {
+      *reinterpret_cast<float4*>(partial + (int64_t)(-o - 1) * d + 4 * c) = acc[i];
+    }
+  }
+}
+
+// Split rows, one workgroup per row: thread (slice sl, column c) sums pieces sl, sl + S, ...
+// (S = 256 / (d/4) slices) in order from 0, then the fixed pairwise tree over the slices, as
+// spmm_finish_kernel does for segments (a per-row sequential sum over ~1,500 pieces of the most
+// popular item took 70 us).
+__global__ __launch_bounds__(256) void spmm_walk_finish_kernel(
+    const int32_t* __restrict__ split_rows, const int64_t* __restrict__ split_ptr,
+    const float* __restrict__ partial, const float* __restrict__ X, int d, SpmmEpi ep,
+    int64_t r0, int64_t r1) {
+  __shared__ float4 red[256];
+  const int64_t r = split_rows[blockIdx.x];
+  if (r < r0 || r >= r1) return;  // uniform
+  const int t = threadIdx.x, d4 = d / 4, S = 256 / d4, c = t % d4, sl = t / d4;
+  const int64_t a = split_ptr[blockIdx.x], n = split_ptr[blockIdx.x + 1] - a;
+  float4 y = make_float4(0.f, 0.f, 0.f, 0.f);
+  int64_t j = sl;
+  for (; j + 3 * S < n; j += 4 * S) {  // 4 loads in flight, added in piece order
+    float4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const float4*>(partial + (a + j + u * S) * d + 4 * c);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      y.x += v[u].x;
+      y.y += v[u].y;
+      y.z += v[u].z;
+      y.w += v[u].w;
+    }
+  }
+  for (; j < n; j += S) {
+    const float4 v = *reinterpret_cast<const float4*>(partial + (a + j) * d + 4 * c);
+    y.x += v.x;
+    y.y += v.y;
+    y.z += v.z;
+    y.w += v.w;
+  }
+  red[t] = y;
+  __syncthreads();
+  for (int w = S / 2; w >= 1; w >>= 1) {
+    if (sl < w) {
+      const float4 o = red[t + w * d4];
+      float4 m = red[t];
+      m.x += o.x;
+      m.y += o.y;
+      m.z += o.z;
+      m.w += o.w;
+      red[t] = m;
+    }
+    __syncthreads();
+  }
+  if (sl == 0) spmm_epilogue(r, d, c, red[t], X, ep);
+}
+
+// Walk order of one row for a listed-row kernel (the whole wave calls it; valid in lanes <
+// LPR): the pieces' fma chains over the sorted entries; one piece -> its chain; several ->
+// the finish kernel's slices (S = 256 / LPR, pieces sl, sl + S, ... from 0) and pairwise tree.
+template <int LPR>
+__device__ float4 walk_row_sum(const int32_t* __restrict__ wcol, const float* __restrict__ wval,
+                               int64_t ws, int64_t L, int64_t cap, const float* __restrict__ X,
+                               int d, int lane, float4* red) {
+  constexpr int S = 256 / LPR;
+  const int sub = lane % LPR;
+  const int64_t n = hnm_cdiv(L, cap);
+  auto chain = [&](int64_t j) {
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int64_t q = j; q < L; q += n) {
+      const float w = wval[ws + q];
+      const float4 x = *reinterpret_cast<const float4*>(X + (int64_t)wcol[ws + q] * d + 4 * sub);
+      v.x = fmaf(w, x.x, v.x);
+      v.y = fmaf(w, x.y, v.y);
+      v.z = fmaf(w, x.z, v.z);
+      v.w = fmaf(w, x.w, v.w);
+    }
+    return v;
+  };
+  if (n == 1) return chain(0);
+  for (int sl = 0; sl < S; ++sl) {
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int64_t j = sl; j < n; j += S) {
+      const float4 v = chain(j);
+      acc.x += v.x;
+      acc.y += v.y;
+      acc.z += v.z;
+      acc.w += v.w;
+    }
+    if (lane < LPR) red[sl * LPR + lane] = acc;
+  }
+  float4 y = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (lane < LPR) {
+    for (int w = S / 2; w >= 1; w >>= 1)
+      for (int sl = 0; sl < w; ++sl) {
+        const float4 o = red[(sl + w) * LPR + lane];
+        float4 m = red[sl * LPR + lane];
+        m.x += o.x;
+        m.y += o.y;
+        m.z += o.z;
+        m.w += o.w;
+        red[sl * LPR + lane] = m;
+      }
+    y = red[lane];
+  }
+  return y;
+}
+
+// walk rows' entries gathered into one contiguous array (one workgroup per row), for the
+// host-side sort of the schedule build
+__global__ __launch_bounds__(256) void walk_gather_kernel(const int32_t* __restrict__ rows,
+                                                          const int64_t* __restrict__ wptr,
+                                                          const int64_t* __restrict__ rowptr,
+                                                          const int32_t* __restrict__ col,
+                                                          const float* __restrict__ val,
+                                                          int32_t* __restrict__ ocol,
+                                                          float* __restrict__ oval) {
+  const int64_t k = blockIdx.x;
+  const int64_t s = rowptr[rows[k]], o = wptr[k], L = wptr[k + 1] - o;
+  for (int64_t q = threadIdx.x; q < L; q += 256) {
+    ocol[o + q] = col[s + q];
+    oval[o + q] = val[s + q];
+  }
+}
+
 // Final embeddings of listed rows (the batch's users) without their last layer over the
 // whole graph: y = (A_hat E_{L-1})[r], out[b] = alpha_0 E_0[r] then
 // fma(alpha_l, E_l[r], .) for l = 1..L-1 and fma(alpha_L, y, .) -- the same operations, in
@@ -537,11 +767,20 @@ __device__ __forceinline__ void combine_store(const CombineLayers& cl, int64_t r
   *reinterpret_cast<float4*>(out + b * d + 4 * sub) = a;
 }
 
+// a plan's walk rows for rows_combine (n == 0: no walk, the long / heavy orders)
+struct WalkRows {
+  const int32_t* rows;
+  const int64_t* ptr;
+  const int32_t* col;
+  const float* val;
+  int64_t n, cap;
+};
+
 template <int LPR>
 __global__ __launch_bounds__(256) void spmm_rows_combine_kernel(
     const int64_t* __restrict__ rows, int64_t n, int64_t N, const int64_t* __restrict__ rowptr,
     const int32_t* __restrict__ col, const float* __restrict__ val, int d, CombineLayers cl,
-    float* __restrict__ out, unsigned* err) {
+    WalkRows wk, float* __restrict__ out, unsigned* err) {
   __shared__ float4 slices[4][256];
   const int lane = threadIdx.x & 63;
   const float* Xl = cl.E[cl.L - 1];
@@ -592,11 +831,254 @@ __global__ __launch_bounds__(256) void spmm_rows_combine_kernel(
     const int64_t hb = b0 + src / LPR;
     const int64_t hr = rows[hb];
     const int64_t hs = rowptr[hr], he = rowptr[hr + 1];
-    const float4 y = he - hs <= HEAVY
-                         ? row_sum<LPR>(col, val, Xl, d, hs, he, lane)
-                         : heavy_row_sum<LPR>(col, val, Xl, d, hs, he, lane, slices[threadIdx.x >> 6]);
+    float4 y;
+    if (wk.n > 0) {  // the walk's order (every row of this class is a walk row)
+      int64_t lo = 0, hi = wk.n;
+      while (hi - lo > 1) {
+        const int64_t mid = (lo + hi) >> 1;
+        if (wk.rows[mid] <= hr) lo = mid; else hi = mid;
+      }
+      const int64_t ws = wk.ptr[lo];
+      y = walk_row_sum<LPR>(wk.col, wk.val, ws, wk.ptr[lo + 1] - ws, wk.cap, Xl, d, lane,
+                            slices[threadIdx.x >> 6]);
+    } else {
+      y = he - hs <= HEAVY
+              ? row_sum<LPR>(col, val, Xl, d, hs, he, lane)
+              : heavy_row_sum<LPR>(col, val, Xl, d, hs, he, lane, slices[threadIdx.x >> 6]);
+    }
     if (lane < LPR) combine_store(cl, hr, d, lane, y, out, hb);
   }
+}
+
+// ---------------------------------------------------------------- walk schedule (host)
+struct WalkSched {
+  int lpr, ng, nwg, maxloc;
+  int64_t* gptr;       // [nwg * ng + 1]
+  uint32_t* ent;       // [walk_nnz] col << 10 | slot
+  float* wt;
+  int32_t* slot_out;   // [nwg * maxloc]: row (unsplit piece) or -(partial index) - 1
+  int32_t* nslot;      // [nwg]
+  int64_t n_split, n_part;
+  int32_t* split_rows;  // [n_split]
+  int64_t* split_ptr;   // [n_split + 1] partial indices, pieces in order
+};
+
+static void walk_sched_free(WalkSched* w) {
+  if (!w) return;
+  (void)hipFree(w->gptr);
+  (void)hipFree(w->ent);
+  (void)hipFree(w->wt);
+  (void)hipFree(w->slot_out);
+  (void)hipFree(w->nslot);
+  (void)hipFree(w->split_rows);
+  (void)hipFree(w->split_ptr);
+  delete w;
+}
+
+template <typename F>
+static void parallel_for(int64_t n, F fn) {
+  const int nt = (int)std::max<int64_t>(1, std::min<int64_t>(
+      std::min<unsigned>(16, std::max(1u, std::thread::hardware_concurrency())), n / 64 + 1));
+  std::vector<std::thread> th;
+  for (int t = 0; t < nt; ++t)
+    th.emplace_back([&, t] {
+      for (int64_t i = t; i < n; i += nt) fn(i);
+    });
+  for (auto& x : th) x.join();
+}
+
+template <typename T>
+static hnm_status upload(T** dst, const T* src, size_t n) {
+  if (hipMalloc((void**)dst, std::max<size_t>(n, 1) * sizeof(T)) != hipSuccess) {
+    hnm_set_error("spmm walk: hipMalloc of %zu bytes failed", n * sizeof(T));
+    return HNM_ENOMEM;
+  }
+  if (n) HNM_HIP_CHECK(hipMemcpy(*dst, src, n * sizeof(T), hipMemcpyHostToDevice));
+  return HNM_OK;
+}
+
+// First call with col / val: each walk row's entries sorted by (col, CSR position), on the
+// device (rows_combine) and on the host (schedule builds).  Caller holds pl->mu.
+static hnm_status walk_prepare(hnm_ctx* ctx, hnm_spmm_plan* pl, const int64_t* rowptr,
+                               const int32_t* col, const float* val) {
+  if (pl->wcol) return HNM_OK;
+  const int64_t T = pl->walk_nnz;
+  int32_t* tcol;
+  float* tval;
+  if (hipMalloc((void**)&tcol, std::max<int64_t>(T, 1) * 4) != hipSuccess) {
+    hnm_set_error("spmm walk: hipMalloc failed");
+    return HNM_ENOMEM;
+  }
+  if (hipMalloc((void**)&tval, std::max<int64_t>(T, 1) * 4) != hipSuccess) {
+    (void)hipFree(tcol);
+    hnm_set_error("spmm walk: hipMalloc failed");
+    return HNM_ENOMEM;
+  }
+  hipLaunchKernelGGL(walk_gather_kernel, dim3((unsigned)pl->n_walk), dim3(256), 0, ctx->stream,
+                     pl->walk_rows, pl->walk_ptr, rowptr, col, val, tcol, tval);
+  HNM_LAUNCH_CHECK();
+  std::vector<int32_t> c0(T);
+  std::vector<float> v0(T);
+  HNM_HIP_CHECK(hipMemcpyAsync(c0.data(), tcol, T * 4, hipMemcpyDeviceToHost, ctx->stream));
+  HNM_HIP_CHECK(hipMemcpyAsync(v0.data(), tval, T * 4, hipMemcpyDeviceToHost, ctx->stream));
+  HNM_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+  const std::vector<int64_t>& wp = *pl->h_walk_ptr;
+  pl->h_wcol = new std::vector<int32_t>(T);
+  pl->h_wval = new std::vector<float>(T);
+  std::vector<int32_t>& hc = *pl->h_wcol;
+  std::vector<float>& hv = *pl->h_wval;
+  parallel_for(pl->n_walk, [&](int64_t k) {
+    const int64_t a = wp[k], L = wp[k + 1] - a;
+    std::vector<int32_t> ix((size_t)L);
+    for (int64_t q = 0; q < L; ++q) ix[q] = (int32_t)q;
+    std::stable_sort(ix.begin(), ix.end(), [&](int32_t x, int32_t y) { return c0[a + x] < c0[a + y]; });
+    for (int64_t q = 0; q < L; ++q) {
+      hc[a + q] = c0[a + ix[q]];
+      hv[a + q] = v0[a + ix[q]];
+    }
+  });
+  HNM_HIP_CHECK(hipMemcpy(tcol, hc.data(), T * 4, hipMemcpyHostToDevice));
+  HNM_HIP_CHECK(hipMemcpy(tval, hv.data(), T * 4, hipMemcpyHostToDevice));
+  pl->wcol = tcol;
+  pl->wval = tval;
+  return HNM_OK;
+}
+
+// Schedule for d (LPR = d / 4 lanes per row): pieces to workgroups (greedy, longest first,
+// least-loaded workgroup with a free slot), then to the workgroup's groups (least-loaded), then
+// each group's pieces merged by column.  The placement only moves work between lanes; the
+// order inside each piece (and so every result) is fixed by the pieces themselves.
+static hnm_status walk_build(hnm_spmm_plan* pl, int d, WalkSched** out) {
+  const int lpr = d / 4, ng = WALK_THREADS / lpr;
+  const int maxloc = std::min(1023, WALK_LDS_F4 / lpr);
+  const std::vector<int64_t>& wp = *pl->h_walk_ptr;
+  const std::vector<int32_t>& wr = *pl->h_walk_rows;
+  const int64_t cap = pl->walk_cap, T = pl->walk_nnz;
+  struct Piece {
+    int32_t k;     // walk row
+    int32_t j, n;  // piece j of n
+    int64_t len;
+  };
+  std::vector<Piece> pcs;
+  for (int64_t k = 0; k < pl->n_walk; ++k) {
+    const int64_t L = wp[k + 1] - wp[k];
+    const int n = (int)hnm_cdiv(L, cap);
+    for (int j = 0; j < n; ++j) pcs.push_back({(int32_t)k, j, n, (L - j + n - 1) / n});
+  }
+  std::stable_sort(pcs.begin(), pcs.end(), [](const Piece& a, const Piece& b) { return a.len > b.len; });
+  int64_t nwg = std::max<int64_t>(1, std::min<int64_t>(hnm_cdiv(WALK_GROUPS_TARGET, ng),
+                                                        hnm_cdiv(T, (int64_t)ng * 256)));
+  while ((int64_t)pcs.size() > nwg * maxloc * 7 / 8) nwg *= 2;
+  std::vector<std::vector<int32_t>> wgp((size_t)nwg);
+  {
+    std::vector<int64_t> load((size_t)nwg, 0);
+    using E = std::pair<int64_t, int64_t>;
+    std::priority_queue<E, std::vector<E>, std::greater<E>> q;
+    for (int64_t w = 0; w < nwg; ++w) q.push({0, w});
+    for (int32_t pi = 0; pi < (int32_t)pcs.size(); ++pi) {
+      E t = q.top();
+      q.pop();
+      while ((int64_t)wgp[t.second].size() >= maxloc) {  // full: drop it from the heap
+        t = q.top();
+        q.pop();
+      }
+      wgp[t.second].push_back(pi);
+      q.push({t.first + pcs[pi].len, t.second});
+    }
+  }
+  // partial indices of split rows: row k's pieces j = 0..n-1 at split_ptr[si] + j
+  std::vector<int32_t> srows;
+  std::vector<int64_t> sptr{0}, kpart((size_t)pl->n_walk, -1);
+  for (int64_t k = 0; k < pl->n_walk; ++k) {
+    const int n = (int)hnm_cdiv(wp[k + 1] - wp[k], cap);
+    if (n <= 1) continue;
+    kpart[k] = sptr.back();
+    srows.push_back(wr[k]);
+    sptr.push_back(sptr.back() + n);
+  }
+  std::vector<int32_t> slot_out((size_t)(nwg * maxloc), 0), nslot((size_t)nwg);
+  std::vector<int64_t> gcount((size_t)(nwg * ng), 0);
+  std::vector<std::vector<std::vector<int32_t>>> gslots((size_t)nwg);
+  for (int64_t w = 0; w < nwg; ++w) {
+    nslot[w] = (int32_t)wgp[w].size();
+    gslots[w].resize(ng);
+    std::vector<int64_t> gl((size_t)ng, 0);
+    for (int sl = 0; sl < (int)wgp[w].size(); ++sl) {
+      const Piece& pc = pcs[wgp[w][sl]];
+      const int gb = (int)(std::min_element(gl.begin(), gl.end()) - gl.begin());
+      gslots[w][gb].push_back(sl);
+      gl[gb] += pc.len;
+      gcount[w * ng + gb] += pc.len;
+      slot_out[w * maxloc + sl] = pc.n == 1 ? wr[pc.k] : (int32_t)(-(kpart[pc.k] + pc.j) - 1);
+    }
+  }
+  std::vector<int64_t> gptr((size_t)(nwg * ng + 1), 0);
+  for (int64_t i = 0; i < nwg * ng; ++i) gptr[i + 1] = gptr[i] + gcount[i];
+  std::vector<uint32_t> ent((size_t)T);
+  std::vector<float> wt((size_t)T);
+  const std::vector<int32_t>& hc = *pl->h_wcol;
+  const std::vector<float>& hv = *pl->h_wval;
+  parallel_for(nwg, [&](int64_t w) {
+    std::vector<std::pair<uint64_t, float>> Lst;
+    for (int g = 0; g < ng; ++g) {
+      Lst.clear();
+      for (int sl : gslots[w][g]) {
+        const Piece& pc = pcs[wgp[w][sl]];
+        const int64_t a = wp[pc.k], L = wp[pc.k + 1] - a;
+        for (int64_t q = pc.j; q < L; q += pc.n)
+          Lst.push_back({((uint64_t)(uint32_t)hc[a + q] << 10) | (uint64_t)sl, hv[a + q]});
+      }
+      std::stable_sort(Lst.begin(), Lst.end(),
+                       [](const auto& x, const auto& y) { return (x.first >> 10) < (y.first >> 10); });
+      int64_t o = gptr[w * ng + g];
+      for (const auto& x : Lst) {
+        ent[o] = (uint32_t)x.first;
+        wt[o++] = x.second;
+      }
+    }
+  });
+  WalkSched* ws = new WalkSched();
+  memset(ws, 0, sizeof(WalkSched));
+  ws->lpr = lpr;
+  ws->ng = ng;
+  ws->nwg = (int)nwg;
+  ws->maxloc = maxloc;
+  ws->n_split = (int64_t)srows.size();
+  ws->n_part = sptr.back();
+  hnm_status st;
+  if ((st = upload(&ws->gptr, gptr.data(), gptr.size())) || (st = upload(&ws->ent, ent.data(), ent.size())) ||
+      (st = upload(&ws->wt, wt.data(), wt.size())) ||
+      (st = upload(&ws->slot_out, slot_out.data(), slot_out.size())) ||
+      (st = upload(&ws->nslot, nslot.data(), nslot.size())) ||
+      (st = upload(&ws->split_rows, srows.data(), srows.size())) ||
+      (st = upload(&ws->split_ptr, sptr.data(), sptr.size()))) {
+    walk_sched_free(ws);
+    return st;
+  }
+  *out = ws;
+  return HNM_OK;
+}
+
+static int walk_index(int d) {
+  int i = 0;
+  while ((4 << i) < d) ++i;
+  return i;
+}
+
+// The walk schedule for d, built on first use (col / val are first seen by the SpMM call).
+static hnm_status walk_get(hnm_ctx* ctx, const hnm_spmm_plan* cpl, const int64_t* rowptr,
+                           const int32_t* col, const float* val, int d, const WalkSched** out) {
+  hnm_spmm_plan* pl = const_cast<hnm_spmm_plan*>(cpl);
+  std::lock_guard<std::mutex> lk(*pl->mu);
+  const int i = walk_index(d);
+  if (!pl->sched[i]) {
+    hnm_status s = walk_prepare(ctx, pl, rowptr, col, val);
+    if (s) return s;
+    s = walk_build(pl, d, &pl->sched[i]);
+    if (s) return s;
+  }
+  *out = pl->sched[i];
+  return HNM_OK;
 }
 
 extern "C" hnm_status hnm_spmm_plan_create(hnm_ctx* ctx, int64_t N, const int64_t* rowptr,
@@ -631,6 +1113,37 @@ extern "C" hnm_status hnm_spmm_plan_create(hnm_ctx* ctx, int64_t N, const int64_
   pl->h_seg_ptr = new std::vector<int64_t>(sptr);
   pl->n_long = (int64_t)lrows.size();
   pl->h_long = new std::vector<int32_t>(lrows);
+  pl->mu = new std::mutex();
+  // walk rows: every row of more than SPMM_SHORT entries (col << 10 must fit 32 bits)
+  pl->walk = SPMM_WALK && SPMM_GROUPED && N <= (int64_t)1 << 22;
+  if (pl->walk) {
+    std::vector<int32_t> wr;
+    std::vector<int64_t> wp{0};
+    for (int64_t r = 0; r < N; ++r) {
+      const int64_t L = rp[r + 1] - rp[r];
+      if (L <= SPMM_SHORT) continue;
+      wr.push_back((int32_t)r);
+      wp.push_back(wp.back() + L);
+    }
+    pl->n_walk = (int64_t)wr.size();
+    pl->walk_nnz = wp.back();
+    // pieces of at most cap entries: half a group's share of a big graph's walk (so the
+    // longest list is ~2x the mean), never below 512
+    pl->walk_cap = std::max<int64_t>(512, hnm_cdiv(pl->walk_nnz, 2 * WALK_GROUPS_TARGET));
+    pl->h_walk_rows = new std::vector<int32_t>(wr);
+    pl->h_walk_ptr = new std::vector<int64_t>(wp);
+    if (pl->n_walk == 0) {
+      pl->walk = 0;
+    } else if (hipMalloc((void**)&pl->walk_rows, pl->n_walk * 4) != hipSuccess ||
+               hipMalloc((void**)&pl->walk_ptr, (pl->n_walk + 1) * 8) != hipSuccess) {
+      hnm_spmm_plan_destroy(pl);
+      hnm_set_error("spmm_plan: hipMalloc failed");
+      return HNM_ENOMEM;
+    } else {
+      HNM_HIP_CHECK(hipMemcpy(pl->walk_rows, wr.data(), pl->n_walk * 4, hipMemcpyHostToDevice));
+      HNM_HIP_CHECK(hipMemcpy(pl->walk_ptr, wp.data(), (pl->n_walk + 1) * 8, hipMemcpyHostToDevice));
+    }
+  }
   if (pl->n_long > 0) {
     if (hipMalloc((void**)&pl->long_rows, pl->n_long * 4) != hipSuccess) {
       hnm_spmm_plan_destroy(pl);
@@ -667,6 +1180,16 @@ extern "C" hnm_status hnm_spmm_plan_destroy(hnm_spmm_plan* pl) {
   if (pl->seg_start) (void)hipFree(pl->seg_start);
   if (pl->seg_end) (void)hipFree(pl->seg_end);
   if (pl->long_rows) (void)hipFree(pl->long_rows);
+  for (WalkSched* w : pl->sched) walk_sched_free(w);
+  if (pl->walk_rows) (void)hipFree(pl->walk_rows);
+  if (pl->walk_ptr) (void)hipFree(pl->walk_ptr);
+  if (pl->wcol) (void)hipFree(pl->wcol);
+  if (pl->wval) (void)hipFree(pl->wval);
+  delete pl->h_walk_rows;
+  delete pl->h_walk_ptr;
+  delete pl->h_wcol;
+  delete pl->h_wval;
+  delete pl->mu;
   delete pl->h_long;
   delete pl->h_heavy;
   delete pl->h_seg_ptr;
@@ -682,6 +1205,57 @@ static hnm_status spmm_launch(hnm_ctx* ctx, const hnm_spmm_plan* pl, int64_t N,
   const int64_t heavy = has_heavy ? HEAVY : INT64_MAX;
   // the live roofline times whole-graph layers only (row-range calls do less work)
   const bool timed = r0 == 0 && r1 == N;
+  if (pl && pl->walk) {
+    // walk rows (> SPMM_SHORT entries) by the user-ordered walk on the side stream, short rows
+    // by the grouped kernel on the ctx stream, concurrently (disjoint output rows)
+    const WalkSched* ws;
+    hnm_status s = walk_get(ctx, pl, rowptr, col, val, d, &ws);
+    if (s) return s;
+    const std::vector<int32_t>& wr = *pl->h_walk_rows;
+    const bool any = std::lower_bound(wr.begin(), wr.end(), (int32_t)std::min<int64_t>(r0, INT32_MAX)) !=
+                     std::lower_bound(wr.begin(), wr.end(), (int32_t)std::min<int64_t>(r1, INT32_MAX));
+    float* partial = nullptr;
+    if (any && ws->n_part > 0) {
+      void* w;
+      s = hnm_workspace(ctx, (size_t)ws->n_part * d * 4, &w);
+      if (s) return s;
+      partial = (float*)w;
+    }
+    if (timed) hnm_timer_begin(ctx, HNM_TIME_SPMM);
+    const bool fork = any && SPMM_WALK_MODE == 0;
+    hipStream_t wst = fork ? ctx->side : ctx->stream;
+    auto short_rows = [&]() -> hnm_status {
+      if (r1 > r0) {
+        hipLaunchKernelGGL(spmm_mixed_kernel<LPR>,
+                           dim3((unsigned)hnm_cdiv(r1 - r0, 4 * (64 / LPR))), dim3(256), 0,
+                           ctx->stream, r0, r1, pl->long_rows, (int64_t)0, (int64_t)0, (int64_t)0,
+                           rowptr, col, val, X, d, ep);
+        HNM_LAUNCH_CHECK();
+      }
+      return HNM_OK;
+    };
+    if (SPMM_WALK_MODE == 2 && (s = short_rows())) return s;
+    if (fork) {
+      HNM_HIP_CHECK(hipEventRecord(ctx->side_in, ctx->stream));
+      HNM_HIP_CHECK(hipStreamWaitEvent(ctx->side, ctx->side_in, 0));
+    }
+    if (any) {
+      hipLaunchKernelGGL(spmm_walk_kernel<LPR>, dim3((unsigned)ws->nwg), dim3(WALK_THREADS), 0,
+                         wst, ws->gptr, ws->ent, ws->wt, ws->slot_out, ws->nslot, ws->maxloc,
+                         X, d, partial, ep, r0, r1);
+      HNM_LAUNCH_CHECK();
+      if (ws->n_split > 0) {
+        hipLaunchKernelGGL(spmm_walk_finish_kernel, dim3((unsigned)ws->n_split), dim3(256), 0,
+                           wst, ws->split_rows, ws->split_ptr, partial, X, d, ep, r0, r1);
+        HNM_LAUNCH_CHECK();
+      }
+    }
+    if (fork) HNM_HIP_CHECK(hipEventRecord(ctx->side_out, ctx->side));
+    if (SPMM_WALK_MODE != 2 && (s = short_rows())) return s;
+    if (fork) HNM_HIP_CHECK(hipStreamWaitEvent(ctx->stream, ctx->side_out, 0));
+    if (timed) hnm_timer_end(ctx, HNM_TIME_SPMM);
+    return HNM_OK;
+  }
   if (timed) hnm_timer_begin(ctx, HNM_TIME_SPMM);
   // the heavy rows' segments + finish run on the ctx's side stream, concurrent with the light
   // kernel (disjoint output rows, X read-only): they fill the CUs the light kernel's long item
@@ -783,22 +1357,34 @@ extern "C" hnm_status hnm_spmm_csr_f32(hnm_ctx* ctx, const hnm_spmm_plan* plan, 
 template <int LPR>
 static hnm_status combine_launch(hnm_ctx* ctx, const int64_t* rows, int64_t n, int64_t N,
                                  const int64_t* rowptr, const int32_t* col, const float* val,
-                                 int d, const CombineLayers& cl, float* out) {
+                                 int d, const CombineLayers& cl, const WalkRows& wk, float* out) {
   const int64_t rows_per_block = SPMM_GROUPED ? 4 * (64 / LPR) : 4;
   hipLaunchKernelGGL(spmm_rows_combine_kernel<LPR>, dim3((unsigned)hnm_cdiv(n, rows_per_block)),
                      dim3(256), 0,
-                     ctx->stream, rows, n, N, rowptr, col, val, d, cl, out, ctx->err_dev);
+                     ctx->stream, rows, n, N, rowptr, col, val, d, cl, wk, out, ctx->err_dev);
   HNM_LAUNCH_CHECK();
   return HNM_OK;
 }
 
-extern "C" hnm_status hnm_spmm_rows_combine_f32(hnm_ctx* ctx, int64_t N, const int64_t* rowptr,
+extern "C" hnm_status hnm_spmm_rows_combine_f32(hnm_ctx* ctx, const hnm_spmm_plan* plan,
+                                                int64_t N, const int64_t* rowptr,
                                                 const int32_t* col, const float* val,
                                                 const int64_t* rows, int64_t n, int d,
                                                 const float* const* layers, const float* alphas,
                                                 int L, float* out) {
   HNM_REQUIRE(ctx && rowptr && col && val && layers && alphas && ((rows && out) || n == 0),
               HNM_EINVAL, "spmm_rows_combine: NULL argument");
+  HNM_REQUIRE(!plan || plan->N == N, HNM_EINVAL, "spmm_rows_combine: plan built for a different graph");
+  WalkRows wk{};
+  if (plan && plan->walk && n > 0) {
+    hnm_spmm_plan* pl = const_cast<hnm_spmm_plan*>(plan);
+    {
+      std::lock_guard<std::mutex> lk(*pl->mu);
+      hnm_status s = walk_prepare(ctx, pl, rowptr, col, val);
+      if (s) return s;
+    }
+    wk = WalkRows{pl->walk_rows, pl->walk_ptr, pl->wcol, pl->wval, pl->n_walk, pl->walk_cap};
+  }
   HNM_REQUIRE(L >= 1 && L <= 8, HNM_EUNSUPPORTED, "spmm_rows_combine: 1 <= L <= 8");
   CombineLayers cl;
   cl.L = L;
@@ -810,5 +1396,5 @@ extern "C" hnm_status hnm_spmm_rows_combine_f32(hnm_ctx* ctx, int64_t N, const i
   for (int l = 0; l <= L; ++l) cl.a[l] = alphas[l];
   if (n <= 0) return HNM_OK;
   HNM_REQUIRE((uintptr_t)out % 16 == 0, HNM_EINVAL, "spmm_rows_combine: out not 16-B aligned");
-  HNM_SPMM_DISPATCH(combine_launch, ctx, rows, n, N, rowptr, col, val, d, cl, out)
+  HNM_SPMM_DISPATCH(combine_launch, ctx, rows, n, N, rowptr, col, val, d, cl, wk, out)
 }

@@ -78,7 +78,7 @@ class NormalizedGraph:
         al = (C.c_float * (L + 1))(*[float(a) for a in alphas])
         c = _lib.ctx(rows.device)
         _lib.check(_lib.fn("hnm_spmm_rows_combine_f32")(
-            c, self.num_nodes, _lib.ptr(self.rowptr), _lib.ptr(self.col), _lib.ptr(self.val),
+            c, self.plan, self.num_nodes, _lib.ptr(self.rowptr), _lib.ptr(self.col), _lib.ptr(self.val),
             _lib.ptr(rows), rows.numel(), d, ptrs, al, L, _lib.ptr(out)),
             "hnm_spmm_rows_combine_f32")
         return out

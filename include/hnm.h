@@ -343,8 +343,13 @@ hnm_status hnm_csr_build_norm(hnm_ctx* ctx, const int64_t* edge_index, const flo
 /* ---- a6: LightGCN.forward propagation -----------------------------------------------
  * Y = A_hat X (graph @ all_embeddings, lightgcn.py:152), with the layer combine fused:
  * acc_out = acc_in + alpha * Y (lightgcn.py:156-158).  Y and acc_out may be NULL.
- * d in {4, 8, 16, 32, 64, 128, 256}.  The plan splits power-law rows (item rows with
- * up to ~1e6 neighbours) into fixed segments summed in a fixed order (deterministic). */
+ * d in {4, 8, 16, 32, 64, 128, 256}.  With a plan, rows of more than 128 entries (the item
+ * rows: ~300 neighbours each, power-law up to ~1e6) are summed by the user-ordered walk: the
+ * row's entries sorted by (col, CSR position) and cut into pieces of at most `cap` entries
+ * (piece j = sorted entries j, j + n, ...), each piece one fp32 fma chain, several pieces
+ * summed in 256/(d/4) interleaved slices and a fixed pairwise tree -- deterministic; the
+ * first call per d builds the walk schedule (host, one-time).
+ * Without a plan: one wave per row (deterministic, slower on power-law rows). */
 hnm_status hnm_spmm_plan_create(hnm_ctx* ctx, int64_t N, const int64_t* rowptr,
                                 hnm_spmm_plan** out);
 hnm_status hnm_spmm_plan_destroy(hnm_spmm_plan* plan);
@@ -366,10 +371,11 @@ hnm_status hnm_spmm_csr_range_f32(hnm_ctx* ctx, const hnm_spmm_plan* plan, int64
  * (host): out[b] = sum_l alphas[l] E_l[rows[b]] with E_L[r] = (A_hat E_{L-1})[r] computed
  * for the listed rows only -- the last layer of LightGCN.forward restricted to the users a
  * recommend() call reads (lightgcn.py:197-199).  Same operations and order as the fused
- * combine of hnm_spmm_csr_f32 with a plan (bitwise equal, heavy rows included: rows of more
- * than 2048 neighbours are summed in the plan's segment + finish order).  An id out of range
- * flags HNM_EOOB and writes NaN.  1 <= L <= 8. */
-hnm_status hnm_spmm_rows_combine_f32(hnm_ctx* ctx, int64_t N, const int64_t* rowptr,
+ * combine of hnm_spmm_csr_f32 with the same plan (bitwise equal, long rows included: they are
+ * summed in the plan's walk order; plan NULL: the plan-less SpMM's order).  An id out of
+ * range flags HNM_EOOB and writes NaN.  1 <= L <= 8. */
+hnm_status hnm_spmm_rows_combine_f32(hnm_ctx* ctx, const hnm_spmm_plan* plan, int64_t N,
+                                     const int64_t* rowptr,
                                      const int32_t* col, const float* val, const int64_t* rows,
                                      int64_t n, int d, const float* const* layers,
                                      const float* alphas, int L, float* out);

@@ -407,6 +407,52 @@ def test_widedeep_no_wide_user_item_golden():
     assert_scores_close(pair, g["pair_scores"], "wd no-wide pair")
 
 
+@pytest.mark.parametrize("d", [4, 64, 256])
+def test_spmm_walk_rows(d):
+    """Rows of more than 128 entries go through the user-ordered walk (graph.hip
+    spmm_walk_kernel): whole-row pieces, rows split into interleaved pieces (an item with
+    every user: 40,000 entries -> dozens of pieces, summed by spmm_walk_finish_kernel),
+    duplicate edges, rows at the 128 / 129 class boundary.  Checked against A_hat X in
+    float64 from the device CSR itself (1e-5 of sum |a||x|), run-to-run bitwise, and the
+    row-range form (rows [U, N): walk rows outside it left untouched) bitwise equal to the
+    whole-graph call (lightgcn.py:152)."""
+    U, I = 40_000, 2_000
+    rng = np.random.default_rng(7)
+    base = syn.bipartite_edge_index(U, I, 150_000, seed=3)
+    hub = np.stack([np.arange(U), np.zeros(U, dtype=np.int64) + U])     # item 0: every user
+    dup = base[:, :5000]                                                # duplicated edges
+    fix = []
+    for u, n in ((5, 127), (6, 128), (7, 129)):                         # user rows at the boundary
+        it = rng.choice(np.arange(1, I), size=n, replace=False) + U
+        fix.append(np.stack([np.full(n, u), it]))
+    one = np.concatenate([hub, dup] + fix, axis=1)
+    edges = np.concatenate([base, one, one[::-1]], axis=1)
+    m = LightGCN(U, I, d)
+    m.set_graph(torch.from_numpy(edges))
+    m = m.to(DEV)
+    g = m._device_graph()
+    N = U + I
+    x = torch.randn(N, d, generator=torch.Generator().manual_seed(1)).to(DEV)
+    y1, y2 = torch.empty_like(x), torch.empty_like(x)
+    g.spmm(x, y1, 0.0, None)
+    g.spmm(x, y2, 0.0, None)
+    yr = torch.zeros_like(x)
+    g.spmm(x, yr, 0.0, None, rows=(U, N))
+    torch.cuda.synchronize()
+    assert torch.equal(y1, y2)
+    assert torch.equal(yr[U:], y1[U:])
+    assert not yr[:U].any()
+    import scipy.sparse as sp
+    rp, col, val = (a.cpu().numpy() for a in (g.rowptr, g.col, g.val))
+    assert (np.diff(rp) > 128).sum() >= 100 and np.diff(rp).max() > 40_000
+    A = sp.csr_matrix((val.astype(np.float64), col, rp), shape=(N, N))
+    xd = x.double().cpu().numpy()
+    ref = A @ xd
+    mag = abs(A) @ np.abs(xd)
+    err = np.abs(y1.double().cpu().numpy() - ref)
+    assert (err <= 1e-5 * mag + 1e-30).all(), float((err / (mag + 1e-30)).max())
+
+
 @pytest.mark.parametrize("d", [64, 128])
 def test_lightgcn_propagate_for_heavy_user_rows_bitwise(d):
     """Listed users whose rows exceed the SpMM's HEAVY = 2048 entries (segmented path in

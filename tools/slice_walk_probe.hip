@@ -72,7 +72,7 @@ __global__ __launch_bounds__(256) void pull_segments(const int64_t* __restrict__
   if (lane < 16) *reinterpret_cast<float4*>(part + sg * D + 4 * sub) = acc;
 }
 
-template <int SYNC>
+template <int MODE>
 __global__ __launch_bounds__(1024) void slice_walk(const int64_t* __restrict__ gptr,
                                                    const uint32_t* __restrict__ ent,
                                                    const float* __restrict__ wt,
@@ -87,6 +87,7 @@ __global__ __launch_bounds__(1024) void slice_walk(const int64_t* __restrict__ g
   __syncthreads();
   int64_t p = gptr[blockIdx.x * NG + g];
   const int64_t e = gptr[blockIdx.x * NG + g + 1];
+  float4 ra = make_float4(0.f, 0.f, 0.f, 0.f);
   for (; p + 3 < e; p += 4) {
     uint32_t c[4];
     float w[4];
@@ -96,6 +97,14 @@ __global__ __launch_bounds__(1024) void slice_walk(const int64_t* __restrict__ g
 #pragma unroll
     for (int u = 0; u < 4; ++u)
       x[u] = *reinterpret_cast<const float4*>(X + (int64_t)(c[u] >> 10) * D + 4 * sub);
+    if (MODE == 1) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        ra.x = fmaf(w[u], x[u].x, ra.x); ra.y = fmaf(w[u], x[u].y, ra.y);
+        ra.z = fmaf(w[u], x[u].z, ra.z); ra.w = fmaf(w[u], x[u].w, ra.w);
+      }
+      continue;
+    }
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       float4* a = &acc[(c[u] & 1023u) * 16 + sub];
@@ -105,6 +114,7 @@ __global__ __launch_bounds__(1024) void slice_walk(const int64_t* __restrict__ g
       *a = v;
     }
   }
+  if (MODE == 1) acc[(g & 31) * 16 + sub] = ra;
   for (; p < e; ++p) {
     const uint32_t c = ent[p];
     const float w = wt[p];
@@ -120,11 +130,67 @@ __global__ __launch_bounds__(1024) void slice_walk(const int64_t* __restrict__ g
     *reinterpret_cast<float4*>(Y + (int64_t)slot_item[blockIdx.x * MAXLOC + (i >> 4)] * D + 4 * (i & 15)) = acc[i];
 }
 
+// v2: NB gathers in flight per group, the next batch's records prefetched one batch ahead
+template <int NB>
+__global__ __launch_bounds__(1024) void slice_walk2(const int64_t* __restrict__ gptr,
+                                                    const uint32_t* __restrict__ ent,
+                                                    const float* __restrict__ wt,
+                                                    const int32_t* __restrict__ slot_item,
+                                                    const int32_t* __restrict__ nslot,
+                                                    const float* __restrict__ X,
+                                                    float* __restrict__ Y) {
+  __shared__ float4 acc[MAXLOC * 16];
+  const int tid = threadIdx.x, g = tid >> 4, sub = tid & 15;
+  const int ns = nslot[blockIdx.x];
+  for (int i = tid; i < ns * 16; i += 1024) acc[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+  __syncthreads();
+  int64_t p = gptr[blockIdx.x * NG + g];
+  const int64_t e = gptr[blockIdx.x * NG + g + 1];
+  uint32_t c[NB];
+  float w[NB];
+#pragma unroll
+  for (int u = 0; u < NB; ++u) {
+    const bool ok = p + u < e;
+    c[u] = ok ? ent[p + u] : 0u;
+    w[u] = ok ? wt[p + u] : 0.f;
+  }
+  for (; p < e; p += NB) {
+    float4 x[NB];
+#pragma unroll
+    for (int u = 0; u < NB; ++u)
+      x[u] = *reinterpret_cast<const float4*>(X + (int64_t)(c[u] >> 10) * D + 4 * sub);
+    uint32_t cn[NB];
+    float wn[NB];
+#pragma unroll
+    for (int u = 0; u < NB; ++u) {
+      const bool ok = p + NB + u < e;
+      cn[u] = ok ? ent[p + NB + u] : 0u;
+      wn[u] = ok ? wt[p + NB + u] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < NB; ++u) {
+      if (p + u < e) {
+        float4* a = &acc[(c[u] & 1023u) * 16 + sub];
+        float4 v = *a;
+        v.x = fmaf(w[u], x[u].x, v.x); v.y = fmaf(w[u], x[u].y, v.y);
+        v.z = fmaf(w[u], x[u].z, v.z); v.w = fmaf(w[u], x[u].w, v.w);
+        *a = v;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < NB; ++u) { c[u] = cn[u]; w[u] = wn[u]; }
+  }
+  __syncthreads();
+  for (int i = tid; i < ns * 16; i += 1024)
+    *reinterpret_cast<float4*>(Y + (int64_t)slot_item[blockIdx.x * MAXLOC + (i >> 4)] * D + 4 * (i & 15)) = acc[i];
+}
+
 static uint64_t rs = 88172645463325252ull;
 static inline uint64_t xr() { rs ^= rs << 13; rs ^= rs >> 7; rs ^= rs << 17; return rs; }
 
 int main(int argc, char** argv) {
   const int64_t U = 1371980, I = 105542, E = 31800000;
+  const bool shuffle = argc > 1 && argv[1][0] == 's';
   int nwg = 256;
   hipDeviceProp_t prop;
   CK(hipGetDeviceProperties(&prop, 0));
@@ -164,7 +230,7 @@ int main(int argc, char** argv) {
   for (int64_t i = 0; i < I; ++i)
     for (int64_t a = rp[i]; a < rp[i + 1]; a += 2048) { sst.push_back(a); sen.push_back(std::min(a + 2048, rp[i + 1])); }
   // B: pieces (items split interleaved when deg > cap), greedy to workgroups then groups
-  const int64_t cap = E / nwg / 2;
+  const int64_t cap = E / ((int64_t)nwg * NG) / 2;
   struct Piece { int32_t item, k, n; int64_t len; };
   std::vector<Piece> pcs;
   for (int64_t i = 0; i < I; ++i) {
@@ -210,7 +276,11 @@ int main(int argc, char** argv) {
         for (int64_t q = rp[pc.item] + pc.k; q < rp[pc.item + 1]; q += pc.n)
           L.push_back({((uint32_t)col[q] << 10) | (uint32_t)sl, val[q]});
       }
-      std::stable_sort(L.begin(), L.end(), [](auto& a, auto& b) { return (a.first >> 10) < (b.first >> 10); });
+      if (shuffle) {
+        for (int64_t k = (int64_t)L.size() - 1; k > 0; --k) std::swap(L[k], L[xr() % (k + 1)]);
+      } else {
+        std::stable_sort(L.begin(), L.end(), [](auto& a, auto& b) { return (a.first >> 10) < (b.first >> 10); });
+      }
       for (auto& x : L) { ent.push_back(x.first); wt.push_back(x.second); }
       gptr[w * NG + g + 1] = (int64_t)ent.size();
     }
@@ -271,7 +341,18 @@ int main(int argc, char** argv) {
     hipLaunchKernelGGL(slice_walk<0>, dim3(nwg), dim3(1024), 0, 0, gp_d, ent_d, wt_d, si_d, ns_d, X, Y);
   });
   CK(hipGetLastError());
-  printf("B slice walk (user order):      %.3f ms  %.2f TB/s gathered\n", tb, gb / tb);
+  printf("B slice walk (%s order):      %.3f ms  %.2f TB/s gathered\n", shuffle ? "random" : "user", tb, gb / tb);
+  const float tc = timeit([&] {
+    hipLaunchKernelGGL(slice_walk<1>, dim3(nwg), dim3(1024), 0, 0, gp_d, ent_d, wt_d, si_d, ns_d, X, Y);
+  });
+  printf("C walk, register acc only (no LDS per edge): %.3f ms  %.2f TB/s gathered\n", tc, gb / tc);
+  const float t4 = timeit([&] {
+    hipLaunchKernelGGL(slice_walk2<4>, dim3(nwg), dim3(1024), 0, 0, gp_d, ent_d, wt_d, si_d, ns_d, X, Y);
+  });
+  const float t8 = timeit([&] {
+    hipLaunchKernelGGL(slice_walk2<8>, dim3(nwg), dim3(1024), 0, 0, gp_d, ent_d, wt_d, si_d, ns_d, X, Y);
+  });
+  printf("B2 prefetched records, 4 / 8 in flight: %.3f / %.3f ms  %.2f / %.2f TB/s\n", t4, t8, gb / t4, gb / t8);
   // check: B's unsplit items vs A's segment partial sums (same edges, different order)
   std::vector<float> hp(sst.size() * D), hy(I * D);
   CK(hipMemcpy(hp.data(), part, hp.size() * 4, hipMemcpyDeviceToHost));
