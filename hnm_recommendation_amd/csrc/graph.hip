@@ -56,6 +56,13 @@
 #define SPMM_WALK_MODE 2
 #endif
 #define WALK_THREADS 1024
+// Column windows: each group's list is cut at WALK_WIN column bounds and the workgroup's groups
+// meet at a barrier after every window, so a CU's 64 lists stay inside one window of X (without
+// it a short list runs ahead of a long one through the table).  d=64 layer: no windows 1.635 ms,
+// 4: 1.499, 8: 1.448, 16: 1.431-1.451, 32: 1.474, 64: 1.508 (per-window imbalance grows).
+#ifndef WALK_WIN
+#define WALK_WIN 16
+#endif
 #define WALK_LDS_F4 9216        // 144 KiB of float4 row accumulators per workgroup
 #define WALK_GROUPS_TARGET 16384  // total LPR-lane groups of a big graph's walk (all d)
 
@@ -525,8 +532,10 @@ __global__ __launch_bounds__(WALK_THREADS) void spmm_walk_kernel(
   __syncthreads();
   // 4 entries per step (2: 1.741 ms per d=64 layer, 4: 1.694, 8: 1.848; records prefetched a
   // step ahead as 16-B vectors with 8 or 16 gathers in flight: 1.812 / 1.823)
-  int64_t p = gptr[(int64_t)blockIdx.x * NG + g];
-  const int64_t e = gptr[(int64_t)blockIdx.x * NG + g + 1];
+  constexpr int K = WALK_WIN > 1 ? WALK_WIN : 1;
+  for (int k = 0; k < K; ++k) {
+  int64_t p = gptr[((int64_t)blockIdx.x * NG + g) * K + k];
+  const int64_t e = gptr[((int64_t)blockIdx.x * NG + g) * K + k + 1];
   for (; p + 3 < e; p += 4) {
     uint32_t c[4];
     float w[4];
@@ -561,6 +570,8 @@ __global__ __launch_bounds__(WALK_THREADS) void spmm_walk_kernel(
     v.z = fmaf(w, x.z, v.z);
     v.w = fmaf(w, x.w, v.w);
     *a = v;
+  }
+  if (K > 1) __syncthreads();
   }
   __syncthreads();
   for (int i = tid; i < ns * LPR; i += WALK_THREADS) {
@@ -853,7 +864,7 @@ __global__ __launch_bounds__(256) void spmm_rows_combine_kernel(
 // ---------------------------------------------------------------- walk schedule (host)
 struct WalkSched {
   int lpr, ng, nwg, maxloc;
-  int64_t* gptr;       // [nwg * ng + 1]
+  int64_t* gptr;       // [nwg * ng * K + 1] (K column windows per group list, WALK_WIN)
   uint32_t* ent;       // [walk_nnz] col << 10 | slot
   float* wt;
   int32_t* slot_out;   // [nwg * maxloc]: row (unsplit piece) or -(partial index) - 1
@@ -950,7 +961,9 @@ static hnm_status walk_prepare(hnm_ctx* ctx, hnm_spmm_plan* pl, const int64_t* r
 // order inside each piece (and so every result) is fixed by the pieces themselves.
 static hnm_status walk_build(hnm_spmm_plan* pl, int d, WalkSched** out) {
   const int lpr = d / 4, ng = WALK_THREADS / lpr;
-  const int maxloc = std::min(1023, WALK_LDS_F4 / lpr);
+  // WALK_WIN > 1: slot maxloc absorbs the windows' padding entries (never stored)
+  const int maxloc = WALK_WIN > 1 ? std::min(1022, WALK_LDS_F4 / lpr - 1)
+                                  : std::min(1023, WALK_LDS_F4 / lpr);
   const std::vector<int64_t>& wp = *pl->h_walk_ptr;
   const std::vector<int32_t>& wr = *pl->h_walk_rows;
   const int64_t cap = pl->walk_cap, T = pl->walk_nnz;
@@ -1012,12 +1025,28 @@ static hnm_status walk_build(hnm_spmm_plan* pl, int d, WalkSched** out) {
       slot_out[w * maxloc + sl] = pc.n == 1 ? wr[pc.k] : (int32_t)(-(kpart[pc.k] + pc.j) - 1);
     }
   }
-  std::vector<int64_t> gptr((size_t)(nwg * ng + 1), 0);
-  for (int64_t i = 0; i < nwg * ng; ++i) gptr[i + 1] = gptr[i] + gcount[i];
-  std::vector<uint32_t> ent((size_t)T);
-  std::vector<float> wt((size_t)T);
+  // WALK_WIN > 1: each group's list is cut at K column bounds (k + 1) * cdiv(N, K), each window
+  // padded to a multiple of 4 entries; the kernel syncs its groups after every window
+  constexpr int K = WALK_WIN > 1 ? WALK_WIN : 1;
+  const int64_t wlen = hnm_cdiv(pl->N, K);
   const std::vector<int32_t>& hc = *pl->h_wcol;
   const std::vector<float>& hv = *pl->h_wval;
+  std::vector<int64_t> wcnt((size_t)(nwg * ng * K), 0);
+  parallel_for(nwg, [&](int64_t w) {
+    for (int g = 0; g < ng; ++g)
+      for (int sl : gslots[w][g]) {
+        const Piece& pc = pcs[wgp[w][sl]];
+        const int64_t a = wp[pc.k], L = wp[pc.k + 1] - a;
+        for (int64_t q = pc.j; q < L; q += pc.n) ++wcnt[(w * ng + g) * K + hc[a + q] / wlen];
+      }
+  });
+  std::vector<int64_t> gptr((size_t)(nwg * ng * K + 1), 0);
+  for (int64_t i = 0; i < nwg * ng * K; ++i)
+    gptr[i + 1] = gptr[i] + (K > 1 ? hnm_cdiv(wcnt[i], 4) * 4 : wcnt[i]);
+  (void)gcount;
+  const int64_t Tp = gptr.back();
+  std::vector<uint32_t> ent((size_t)Tp, (uint32_t)maxloc);  // padding: col 0, spare slot, 0.0
+  std::vector<float> wt((size_t)Tp, 0.f);
   parallel_for(nwg, [&](int64_t w) {
     std::vector<std::pair<uint64_t, float>> Lst;
     for (int g = 0; g < ng; ++g) {
@@ -1030,10 +1059,13 @@ static hnm_status walk_build(hnm_spmm_plan* pl, int d, WalkSched** out) {
       }
       std::stable_sort(Lst.begin(), Lst.end(),
                        [](const auto& x, const auto& y) { return (x.first >> 10) < (y.first >> 10); });
-      int64_t o = gptr[w * ng + g];
-      for (const auto& x : Lst) {
-        ent[o] = (uint32_t)x.first;
-        wt[o++] = x.second;
+      size_t i = 0;
+      for (int k = 0; k < K; ++k) {
+        int64_t o = gptr[(w * ng + g) * K + k];
+        for (; i < Lst.size() && (int64_t)(Lst[i].first >> 10) / wlen == k; ++i) {
+          ent[o] = (uint32_t)Lst[i].first;
+          wt[o++] = Lst[i].second;
+        }
       }
     }
   });
