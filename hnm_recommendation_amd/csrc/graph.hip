@@ -534,44 +534,44 @@ __global__ __launch_bounds__(WALK_THREADS) void spmm_walk_kernel(
   // step ahead as 16-B vectors with 8 or 16 gathers in flight: 1.812 / 1.823)
   constexpr int K = WALK_WIN > 1 ? WALK_WIN : 1;
   for (int k = 0; k < K; ++k) {
-  int64_t p = gptr[((int64_t)blockIdx.x * NG + g) * K + k];
-  const int64_t e = gptr[((int64_t)blockIdx.x * NG + g) * K + k + 1];
-  for (; p + 3 < e; p += 4) {
-    uint32_t c[4];
-    float w[4];
+    int64_t p = gptr[((int64_t)blockIdx.x * NG + g) * K + k];
+    const int64_t e = gptr[((int64_t)blockIdx.x * NG + g) * K + k + 1];
+    for (; p + 3 < e; p += 4) {
+      uint32_t c[4];
+      float w[4];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      c[u] = ent[p + u];
-      w[u] = wt[p + u];
+      for (int u = 0; u < 4; ++u) {
+        c[u] = ent[p + u];
+        w[u] = wt[p + u];
+      }
+      float4 x[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        x[u] = *reinterpret_cast<const float4*>(X + (int64_t)(c[u] >> 10) * d + 4 * sub);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {  // in list order: a slot's entries stay one fma chain
+        float4* a = &acc[(c[u] & 1023u) * LPR + sub];
+        float4 v = *a;
+        v.x = fmaf(w[u], x[u].x, v.x);
+        v.y = fmaf(w[u], x[u].y, v.y);
+        v.z = fmaf(w[u], x[u].z, v.z);
+        v.w = fmaf(w[u], x[u].w, v.w);
+        *a = v;
+      }
     }
-    float4 x[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u)
-      x[u] = *reinterpret_cast<const float4*>(X + (int64_t)(c[u] >> 10) * d + 4 * sub);
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {  // in list order: a slot's entries stay one fma chain
-      float4* a = &acc[(c[u] & 1023u) * LPR + sub];
+    for (; p < e; ++p) {
+      const uint32_t c = ent[p];
+      const float w = wt[p];
+      const float4 x = *reinterpret_cast<const float4*>(X + (int64_t)(c >> 10) * d + 4 * sub);
+      float4* a = &acc[(c & 1023u) * LPR + sub];
       float4 v = *a;
-      v.x = fmaf(w[u], x[u].x, v.x);
-      v.y = fmaf(w[u], x[u].y, v.y);
-      v.z = fmaf(w[u], x[u].z, v.z);
-      v.w = fmaf(w[u], x[u].w, v.w);
+      v.x = fmaf(w, x.x, v.x);
+      v.y = fmaf(w, x.y, v.y);
+      v.z = fmaf(w, x.z, v.z);
+      v.w = fmaf(w, x.w, v.w);
       *a = v;
     }
-  }
-  for (; p < e; ++p) {
-    const uint32_t c = ent[p];
-    const float w = wt[p];
-    const float4 x = *reinterpret_cast<const float4*>(X + (int64_t)(c >> 10) * d + 4 * sub);
-    float4* a = &acc[(c & 1023u) * LPR + sub];
-    float4 v = *a;
-    v.x = fmaf(w, x.x, v.x);
-    v.y = fmaf(w, x.y, v.y);
-    v.z = fmaf(w, x.z, v.z);
-    v.w = fmaf(w, x.w, v.w);
-    *a = v;
-  }
-  if (K > 1) __syncthreads();
+    if (K > 1) __syncthreads();
   }
   __syncthreads();
   for (int i = tid; i < ns * LPR; i += WALK_THREADS) {
