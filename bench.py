@@ -52,6 +52,8 @@ FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: fp32 matrix (= vector) pe
 # x 2.4 GHz (MI355X_MICROARCH.md "Peak BF16/FP16 MFMA ~2.5 PF dense")
 F16_MFMA_PEAK_TFLOPS = 2516.6
 HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md: HBM3E spec peak
+L2_GATHER_TBPS = 17.8           # MI355X_MICROARCH.md "Indexed rows": rows shared via the XCD L2
+MALL_GATHER_TBPS = 8.6          # same table: 38 MB uniformly random rows (Infinity Cache)
 K = 12
 
 
@@ -162,7 +164,7 @@ def build_workload(name, rank, world, device, batch, exact=False, weights="init"
         info["_full_step"] = full_step
         ret = dict(step=rec.recommend, per_launch=per_launch, bound="hbm",
                    kernel="spmm layer (spmm_mixed short rows + spmm_walk rows + walk finish), whole-graph layers",
-                   timing=_lib.TIME_SPMM)
+                   timing=_lib.TIME_SPMM, gathered=g.nnz * d * 4.0)
         return ret, info, ("lightgcn", (sd, edges, d))
     elif name == "widedeep":
         sd = syn.widedeep_state_dict(U, I, 64, (512, 256, 128), seed=0)
@@ -428,11 +430,36 @@ def run_child(argv, timeout):
     return json.loads(lines[-1])
 
 
+def compact_line(line):
+    """The fields of a workload's line that the headline line repeats under `other_configs`
+    (its full line is printed on its own stdout line before the headline): small enough that
+    the headline JSON line with every workload fits a driver's 8 KB output tail."""
+    r = line.get("roofline") or {}
+    out = {"value": line["value"], "ms_per_step": line["ms_per_step"], "steps": line["steps"],
+           "dtype": line["dtype"], "baseline_config": line["config"].get("baseline_config"),
+           "roofline": {k: r.get(k) for k in ("bound", "kernel", "achieved", "peak", "unit",
+                                              "frac", "avg_kernel_ms", "launches",
+                                              "algorithmic_per_launch", "traffic")}}
+    if r.get("gather_ceiling"):
+        out["roofline"]["gather_ceiling"] = {k: r["gather_ceiling"].get(k)
+                                             for k in ("bytes", "ms", "frac")}
+    for k in ("cpu_baseline", "exact_fp32", "filtered", "serving_cached_propagation",
+              "pipelined_3_streams", "full_propagation_step"):
+        if line.get(k):
+            out[k] = line[k]["value"]
+    if line.get("prefilter"):
+        out["candidates_per_row"] = line["prefilter"]["candidates_per_row"]
+        out["fallback_rows"] = line["prefilter"]["fallback_rows"]
+    return out
+
+
 def run_extras(args):
     """Every other workload's bench line and the B = 1 serve latencies, measured by child
     processes after the headline line's timed region (one process per workload: each
-    holds only its own tables)."""
-    out, lat = {}, {}
+    holds only its own tables).  Each full line is printed on stdout as
+    `workload_line <name> {...}` (the headline stays the one line that starts with "{");
+    configs[2] (lightgcn) last, right above the headline, so a tail of the output keeps it."""
+    out, lat, full = {}, {}, {}
     for w, what in EXTRA_WORKLOADS:
         steps, warmup = (5, 1) if w == "widedeep" else (args.steps, args.warmup)
         argv = ["--workload", w, "--steps", str(steps), "--warmup", str(warmup), "--no-extras"]
@@ -443,12 +470,16 @@ def run_extras(args):
         log(f"extra workload {w}: {time.perf_counter() - t0:.1f}s")
         if line is not None:
             line["config"]["baseline_config"] = what
-            out[w] = line
+            full[w] = line
+            out[w] = compact_line(line)
     for w in ("ncf", "lightgcn"):
         line = run_child(["--latency", "--workload", w, "--steps", "200", "--no-extras"], 600)
         log(f"serve latency {w} done")
         if line is not None:
-            lat[w] = line
+            print("serve_latency_line " + json.dumps(line), flush=True)
+            lat[w] = {k: v["p50"] for k, v in line.items() if isinstance(v, dict) and "p50" in v}
+    for w in sorted(full, key=lambda w: w == "lightgcn"):
+        print(f"workload_line {w} " + json.dumps(full[w]), flush=True)
     return out, lat
 
 
@@ -600,6 +631,18 @@ def main():
             "random_data_mfma_rate": RANDOM_DATA_F16_TFLOPS,
             "frac_of_random_data_rate": round(rate / RANDOM_DATA_F16_TFLOPS, 3),
             "source": "tools/mfma_shape_probe.hip, profiles/r2_mfma_shape_probe.txt"}
+    if wl.get("gathered"):
+        # gather-aware ceiling beside the algorithmic one: every CSR entry gathers one whole
+        # d-float row; MI355X_MICROARCH.md "Indexed rows": 16.8-18.8 TB/s from an XCD's L2,
+        # 8.6 TB/s for a uniformly random table in the Infinity Cache
+        gb = wl["gathered"]
+        ach = gb / (avg_kernel_ms * 1e-3) / 1e12
+        line["roofline"]["gather_ceiling"] = {
+            "bytes": gb, "achieved_TBps": round(ach, 3),
+            "l2_rate_TBps": L2_GATHER_TBPS, "infinity_cache_rate_TBps": MALL_GATHER_TBPS,
+            "ms": round(gb / (L2_GATHER_TBPS * 1e12) * 1e3, 4),
+            "frac": round(ach / L2_GATHER_TBPS, 4),
+            "frac_of_infinity_cache_rate": round(ach / MALL_GATHER_TBPS, 4)}
     if "_serving" in info and rank == 0 and world == 1 and not args.profile_only:
         # serving rate with the propagation computed once (weights unchanged between calls);
         # reported beside `value`, never as it
@@ -706,7 +749,17 @@ def main():
             and not args.exact and args.weights == "init"):
         others, lat = run_extras(args)
         line["other_configs"] = others
-        line["serve_latency_b1"] = lat
+        line["serve_latency_b1_p50_ms"] = lat
+        # the headline's own explanatory notes stay in its full line (printed above): the
+        # line the driver parses must fit its output tail together with every workload
+        print("workload_line ncf " + json.dumps(line), flush=True)
+        for v in line.values():
+            if isinstance(v, dict):
+                v.pop("note", None)
+                v.pop("history", None)
+                v.pop("source", None)
+        if isinstance(line.get("cpu_baseline"), dict):
+            line["cpu_baseline"]["sample"] = line["cpu_baseline"]["sample"][:90]
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:

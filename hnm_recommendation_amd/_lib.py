@@ -33,6 +33,14 @@ class NcfWeights(C.Structure):
                 ("h1", _i32), ("h2", _i32)]
 
 
+class NcfDeepWeights(C.Structure):
+    """hnm_ncf_deep_weights (include/hnm.h)."""
+    _fields_ = [("gmf_user", _p), ("gmf_item", _p), ("mlp_user", _p), ("mlp_item", _p),
+                ("w", _p * 8), ("b", _p * 8), ("wp", _p), ("bp", _p),
+                ("num_users", _i64), ("num_items", _i64), ("mf", _i32), ("nl", _i32),
+                ("dims", _i32 * 9)]
+
+
 class WideDeepWeights(C.Structure):
     """hnm_widedeep_weights (include/hnm.h)."""
     _fields_ = [(n, _p) for n in (
@@ -86,12 +94,14 @@ _SIGS = {
     "hnm_ncf_topk_finish_f32": (_i32, [_p, C.POINTER(NcfWeights), _p, _i64, _p, _p, C.c_int, _p,
                                        C.c_int, _p, _p]),
     "hnm_ncf_scores_f32": (_i32, [_p, C.POINTER(NcfWeights), _p, _i64, _p, _i64]),
+    "hnm_ncf_deep_scores_f32": (_i32, [_p, C.POINTER(NcfDeepWeights), _p, _i64, _p, _p, _i64]),
     "hnm_ncf_pair_scores_f32": (_i32, [_p, C.POINTER(NcfWeights), _p, _p, _i64, _p]),
     "hnm_ncf_prefilter_debug_f32": (_i32, [_p, C.POINTER(NcfWeights), _p, _i64, _p, _i64, _p]),
     "hnm_topk_merge_f32": (_i32, [_p, _p, _p, _i64, _i64, _i64, _i64, C.c_int, C.c_int, _p, _p]),
     "hnm_topk_rows_f32": (_i32, [_p, _p, _i64, _i64, _i64, _p, _p, C.c_int, _p, _p]),
     "hnm_csr_build_norm": (_i32, [_p, _p, _p, _i64, _i64, _p, _p, _p]),
     "hnm_spmm_plan_create": (_i32, [_p, _i64, _p, C.POINTER(_p)]),
+    "hnm_spmm_plan_prepare": (_i32, [_p, _p, _p, _p, C.c_int]),
     "hnm_spmm_plan_destroy": (_i32, [_p]),
     "hnm_spmm_csr_f32": (_i32, [_p, _p, _i64, _p, _p, _p, _p, C.c_int, _p, _f32, _p, _p]),
     "hnm_spmm_csr_range_f32": (_i32, [_p, _p, _i64, _p, _p, _p, _p, C.c_int, _p, _f32, _p, _p,

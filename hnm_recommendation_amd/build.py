@@ -15,7 +15,7 @@ REPO = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
 BUILD = os.path.join(REPO, "build", "obj")
 LIB = os.path.join(PKG, "libhnm_mi355x.so")
-SOURCES = ["api.hip", "score.hip", "dot_cert.hip", "ncf.hip", "ncf_cert.hip", "graph.hip",
+SOURCES = ["api.hip", "score.hip", "dot_cert.hip", "ncf.hip", "ncf_cert.hip", "ncf_deep.hip", "graph.hip",
            "widedeep.hip", "eval.hip", "topk_sort.hip"]
 HEADERS = ["hnm_device.h", "hnm_internal.h", "dot_internal.h", "ncf_internal.h"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")

@@ -65,12 +65,30 @@
 #endif
 #define WALK_LDS_F4 9216        // 144 KiB of float4 row accumulators per workgroup
 #define WALK_GROUPS_TARGET 16384  // total LPR-lane groups of a big graph's walk (all d)
+// Round 4: the short rows (<= SPMM_SHORT entries: every user row) by a column-ordered walk too
+// (spmm_swalk_kernel): blocks of consecutive rows hold their accumulators in LDS and every
+// lane group walks its rows' entries merged in column order, so the chip's gathers move through
+// the item table together and an XCD's L2 serves them instead of the Infinity Cache.
+#ifndef SPMM_SWALK
+#define SPMM_SWALK 1
+#endif
+// column windows of the short walk (1: none; a barrier after each window otherwise)
+#ifndef SWALK_WIN
+#define SWALK_WIN 1
+#endif
+// persistent short-walk workgroups per CU
+#ifndef SWALK_WG_PER_CU
+#define SWALK_WG_PER_CU 1
+#endif
 
 struct WalkSched;
+struct ShortSched;
 
 struct hnm_spmm_plan {
   int device;
-  int64_t N;
+  int num_cus;
+  int64_t N, nnz;
+  std::vector<int64_t>* h_rowptr;
   int64_t n_heavy;
   int64_t n_seg;
   int32_t* heavy_rows;  // [n_heavy]
@@ -85,18 +103,23 @@ struct hnm_spmm_plan {
   std::vector<int64_t>* h_seg_ptr;
   // user-ordered walk of the rows of more than SPMM_SHORT entries (SPMM_WALK)
   int walk;
+  int swalk;            // short rows by the column-ordered short walk (SPMM_SWALK)
   int64_t walk_cap;     // entries per piece: a row of L entries is cut into cdiv(L, cap) pieces
   int64_t n_walk, walk_nnz;
-  int32_t* walk_rows;   // [n_walk] ascending (device)
-  int64_t* walk_ptr;    // [n_walk + 1] offsets into wcol / wval (device)
-  int32_t* wcol;        // [walk_nnz] each walk row's entries sorted by (col, CSR position)
-  float* wval;
-  std::vector<int32_t>* h_walk_rows;
-  std::vector<int64_t>* h_walk_ptr;
-  std::vector<int32_t>* h_wcol;
-  std::vector<float>* h_wval;
+  std::vector<int32_t>* h_walk_rows;  // ascending
+  std::vector<int32_t>* h_short_rows; // rows of <= SPMM_SHORT entries, ascending
+  // The graph values the plan is bound to (first prepare / SpMM / rows_combine call): every
+  // row's entries sorted by (col, CSR position) in CSR layout, on the device (rows_combine) and
+  // on the host (schedule builds).  Later calls must pass the same col / val pointers.
+  const int32_t* bound_col;
+  const float* bound_val;
+  int32_t* scol;
+  float* sval;
+  std::vector<int32_t>* h_scol;
+  std::vector<float>* h_sval;
   std::mutex* mu;       // lazy preparation (first call with col/val, first call per d)
   WalkSched* sched[7];  // per d = 4 << i
+  ShortSched* ssched[7];
 };
 
 // ------------------------------------------------------------------ CSR build kernels
@@ -584,6 +607,69 @@ __global__ __launch_bounds__(WALK_THREADS) void spmm_walk_kernel(
   }
 }
 
+// ------------------------------------------------------------- short walk (round 4)
+// Rows of at most SPMM_SHORT entries (every user row of the bipartite graph: ~24 entries
+// gathering the 27 MB item table at d=64) in blocks of up to S consecutive rows.  A persistent
+// workgroup (one per CU) takes blocks b0 + blockIdx.x, + gridDim.x, ...; the block's rows hold
+// their fp32 accumulators in LDS (slot = row - first row of the block, spare slot S for
+// padding), each LPR-lane group owns a set of the block's rows and walks their entries merged by
+// column (col << 10 | slot records, padded to 4 per list), adding val * X[col] into the slot.
+// Every block's lists span the same column range at a similar pace, so the rows the 32 CUs of
+// an XCD gather at any moment lie in a narrow window of the item table that their L2 holds.
+// Order: row r's value is one fma chain from 0 over its entries sorted by (col, CSR position)
+// -- rows_combine repeats it over the plan's sorted copy (row_sum_grouped on scol / sval).
+template <int LPR>
+__global__ __launch_bounds__(WALK_THREADS) void spmm_swalk_kernel(
+    const int64_t* __restrict__ gptr, const uint32_t* __restrict__ ent,
+    const float* __restrict__ wt, const int32_t* __restrict__ srow,
+    const int32_t* __restrict__ nslot, int S, const float* __restrict__ X, int d, SpmmEpi ep,
+    int64_t r0, int64_t r1, int64_t b0, int64_t b1) {
+  constexpr int NG = WALK_THREADS / LPR;
+  constexpr int K = SWALK_WIN > 1 ? SWALK_WIN : 1;
+  __shared__ float4 acc[WALK_LDS_F4];
+  const int tid = threadIdx.x, g = tid / LPR, sub = tid % LPR;
+  for (int i = tid; i < WALK_LDS_F4; i += WALK_THREADS) acc[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+  __syncthreads();
+  for (int64_t b = b0 + blockIdx.x; b < b1; b += gridDim.x) {
+    for (int k = 0; k < K; ++k) {
+      int64_t p = gptr[(b * NG + g) * K + k];
+      const int64_t e = gptr[(b * NG + g) * K + k + 1];
+      for (; p + 3 < e; p += 4) {  // lists are padded to multiples of 4
+        uint32_t c[4];
+        float w[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          c[u] = ent[p + u];
+          w[u] = wt[p + u];
+        }
+        float4 x[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          x[u] = *reinterpret_cast<const float4*>(X + (int64_t)(c[u] >> 10) * d + 4 * sub);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {  // list order: a slot's entries stay one fma chain
+          float4* a = &acc[(c[u] & 1023u) * LPR + sub];
+          float4 v = *a;
+          v.x = fmaf(w[u], x[u].x, v.x);
+          v.y = fmaf(w[u], x[u].y, v.y);
+          v.z = fmaf(w[u], x[u].z, v.z);
+          v.w = fmaf(w[u], x[u].w, v.w);
+          *a = v;
+        }
+      }
+      if (K > 1) __syncthreads();
+    }
+    __syncthreads();
+    const int ns = nslot[b];
+    for (int i = tid; i < ns * LPR; i += WALK_THREADS) {
+      const int64_t r = srow[b * S + i / LPR];
+      if (r >= r0 && r < r1) spmm_epilogue(r, d, i % LPR, acc[i], X, ep);
+      acc[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    __syncthreads();
+  }
+}
+
 // Split rows, one workgroup per row: thread (slice sl, column c) sums pieces sl, sl + S, ...
 // (S = 256 / (d/4) slices) in order from 0, then the fixed pairwise tree over the slices, as
 // spmm_finish_kernel does for segments (a per-row sequential sum over ~1,500 pieces of the most
@@ -686,23 +772,6 @@ __device__ float4 walk_row_sum(const int32_t* __restrict__ wcol, const float* __
   return y;
 }
 
-// walk rows' entries gathered into one contiguous array (one workgroup per row), for the
-// host-side sort of the schedule build
-__global__ __launch_bounds__(256) void walk_gather_kernel(const int32_t* __restrict__ rows,
-                                                          const int64_t* __restrict__ wptr,
-                                                          const int64_t* __restrict__ rowptr,
-                                                          const int32_t* __restrict__ col,
-                                                          const float* __restrict__ val,
-                                                          int32_t* __restrict__ ocol,
-                                                          float* __restrict__ oval) {
-  const int64_t k = blockIdx.x;
-  const int64_t s = rowptr[rows[k]], o = wptr[k], L = wptr[k + 1] - o;
-  for (int64_t q = threadIdx.x; q < L; q += 256) {
-    ocol[o + q] = col[s + q];
-    oval[o + q] = val[s + q];
-  }
-}
-
 // Final embeddings of listed rows (the batch's users) without their last layer over the
 // whole graph: y = (A_hat E_{L-1})[r], out[b] = alpha_0 E_0[r] then
 // fma(alpha_l, E_l[r], .) for l = 1..L-1 and fma(alpha_L, y, .) -- the same operations, in
@@ -713,7 +782,7 @@ __global__ __launch_bounds__(256) void walk_gather_kernel(const int32_t* __restr
 // (w = S/2 .. 1), as spmm_finish_kernel does -- so listed heavy rows are bitwise equal to
 // forward() too.  Each lane only touches its own float4 column of the slice sums (LDS, one
 // S x LPR block per wave), so the wave needs no barrier.  Every row is summed in the order of
-// its class (short: grouped; long: one wave; heavy: segments), as the layer kernels do.
+// its class as the layer kernels of the same plan sum it (CombineOrder below).
 struct CombineLayers {
   const float* E[8];
   float a[9];
@@ -778,24 +847,28 @@ __device__ __forceinline__ void combine_store(const CombineLayers& cl, int64_t r
   *reinterpret_cast<float4*>(out + b * d + 4 * sub) = a;
 }
 
-// a plan's walk rows for rows_combine (n == 0: no walk, the long / heavy orders)
-struct WalkRows {
-  const int32_t* rows;
-  const int64_t* ptr;
-  const int32_t* col;
-  const float* val;
-  int64_t n, cap;
+// The summation order rows_combine must repeat (the plan's): mode 0 plan-less (one wave per
+// row, row_sum, every row: spmm_light_kernel with no heavy class); mode 1 a plan without the
+// walks (short rows grouped in CSR order, long rows one wave, heavy rows segments); mode 2 a
+// walk plan (long rows in the walk's piece order over the sorted copy scol / sval; short rows
+// grouped over the sorted copy when the short walk is on, else over col / val).
+struct CombineOrder {
+  int mode;
+  int short_sorted;
+  const int32_t* scol;
+  const float* sval;
+  int64_t cap;
 };
 
 template <int LPR>
 __global__ __launch_bounds__(256) void spmm_rows_combine_kernel(
     const int64_t* __restrict__ rows, int64_t n, int64_t N, const int64_t* __restrict__ rowptr,
     const int32_t* __restrict__ col, const float* __restrict__ val, int d, CombineLayers cl,
-    WalkRows wk, float* __restrict__ out, unsigned* err) {
+    CombineOrder co, float* __restrict__ out, unsigned* err) {
   __shared__ float4 slices[4][256];
   const int lane = threadIdx.x & 63;
   const float* Xl = cl.E[cl.L - 1];
-  if (!SPMM_GROUPED) {
+  if (!SPMM_GROUPED || co.mode == 0) {
     const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (b >= n) return;
     const int64_t r = rows[b];
@@ -805,7 +878,7 @@ __global__ __launch_bounds__(256) void spmm_rows_combine_kernel(
       return;
     }
     const int64_t rs = rowptr[r], re = rowptr[r + 1];
-    const float4 y = re - rs <= HEAVY
+    const float4 y = co.mode == 0 || re - rs <= HEAVY
                          ? row_sum<LPR>(col, val, Xl, d, rs, re, lane)
                          : heavy_row_sum<LPR>(col, val, Xl, d, rs, re, lane, slices[threadIdx.x >> 6]);
     if (lane < LPR) combine_store(cl, r, d, lane, y, out, b);
@@ -820,6 +893,8 @@ __global__ __launch_bounds__(256) void spmm_rows_combine_kernel(
   const int64_t b = b0 + g;
   int64_t r = -1, rs = 0, re = 0;
   bool ok = false;
+  const int32_t* scl = co.short_sorted ? co.scol : col;
+  const float* svl = co.short_sorted ? co.sval : val;
   if (b < n) {
     r = rows[b];
     ok = r >= 0 && r < N;
@@ -831,7 +906,7 @@ __global__ __launch_bounds__(256) void spmm_rows_combine_kernel(
       rs = rowptr[r];
       re = rowptr[r + 1];
       if (re - rs <= SPMM_SHORT)
-        combine_store(cl, r, d, sub, row_sum_grouped<LPR>(col, val, Xl, d, rs, re, sub), out, b);
+        combine_store(cl, r, d, sub, row_sum_grouped<LPR>(scl, svl, Xl, d, rs, re, sub), out, b);
     }
   }
   // long and heavy rows: the whole wave, one row at a time
@@ -843,14 +918,8 @@ __global__ __launch_bounds__(256) void spmm_rows_combine_kernel(
     const int64_t hr = rows[hb];
     const int64_t hs = rowptr[hr], he = rowptr[hr + 1];
     float4 y;
-    if (wk.n > 0) {  // the walk's order (every row of this class is a walk row)
-      int64_t lo = 0, hi = wk.n;
-      while (hi - lo > 1) {
-        const int64_t mid = (lo + hi) >> 1;
-        if (wk.rows[mid] <= hr) lo = mid; else hi = mid;
-      }
-      const int64_t ws = wk.ptr[lo];
-      y = walk_row_sum<LPR>(wk.col, wk.val, ws, wk.ptr[lo + 1] - ws, wk.cap, Xl, d, lane,
+    if (co.mode == 2) {  // the walk's order (every row of this class is a walk row)
+      y = walk_row_sum<LPR>(co.scol, co.sval, hs, he - hs, co.cap, Xl, d, lane,
                             slices[threadIdx.x >> 6]);
     } else {
       y = he - hs <= HEAVY
@@ -861,7 +930,8 @@ __global__ __launch_bounds__(256) void spmm_rows_combine_kernel(
   }
 }
 
-// ---------------------------------------------------------------- walk schedule (host)
+
+// ---------------------------------------------------------------- walk schedules (host)
 struct WalkSched {
   int lpr, ng, nwg, maxloc;
   int64_t* gptr;       // [nwg * ng * K + 1] (K column windows per group list, WALK_WIN)
@@ -886,6 +956,28 @@ static void walk_sched_free(WalkSched* w) {
   delete w;
 }
 
+// short walk: nb blocks of up to S consecutive short rows, ng lists per block (K windows each)
+struct ShortSched {
+  int lpr, ng, S, nwg;
+  int64_t nb;
+  int64_t* gptr;     // [nb * ng * K + 1] (K = SWALK_WIN)
+  uint32_t* ent;     // col << 10 | slot (slot S: padding, weight 0)
+  float* wt;
+  int32_t* srow;     // [nb * S] row of each slot
+  int32_t* nslot;    // [nb]
+  std::vector<int32_t> first, last;  // first / last row of each block (row-range launches)
+};
+
+static void short_sched_free(ShortSched* w) {
+  if (!w) return;
+  (void)hipFree(w->gptr);
+  (void)hipFree(w->ent);
+  (void)hipFree(w->wt);
+  (void)hipFree(w->srow);
+  (void)hipFree(w->nslot);
+  delete w;
+}
+
 template <typename F>
 static void parallel_for(int64_t n, F fn) {
   const int nt = (int)std::max<int64_t>(1, std::min<int64_t>(
@@ -901,6 +993,7 @@ static void parallel_for(int64_t n, F fn) {
 template <typename T>
 static hnm_status upload(T** dst, const T* src, size_t n) {
   if (hipMalloc((void**)dst, std::max<size_t>(n, 1) * sizeof(T)) != hipSuccess) {
+    *dst = nullptr;
     hnm_set_error("spmm walk: hipMalloc of %zu bytes failed", n * sizeof(T));
     return HNM_ENOMEM;
   }
@@ -908,50 +1001,51 @@ static hnm_status upload(T** dst, const T* src, size_t n) {
   return HNM_OK;
 }
 
-// First call with col / val: each walk row's entries sorted by (col, CSR position), on the
-// device (rows_combine) and on the host (schedule builds).  Caller holds pl->mu.
-static hnm_status walk_prepare(hnm_ctx* ctx, hnm_spmm_plan* pl, const int64_t* rowptr,
-                               const int32_t* col, const float* val) {
-  if (pl->wcol) return HNM_OK;
-  const int64_t T = pl->walk_nnz;
-  int32_t* tcol;
-  float* tval;
-  if (hipMalloc((void**)&tcol, std::max<int64_t>(T, 1) * 4) != hipSuccess) {
-    hnm_set_error("spmm walk: hipMalloc failed");
-    return HNM_ENOMEM;
+// Binds the plan to col / val on first use.  A walk plan then copies the CSR to the host,
+// stable-sorts every row's entries by column (the walks' summation order: (col, CSR position))
+// and uploads the sorted copy (rows_combine repeats the walks' order from it).  Later calls
+// must pass the same col / val: a plan snapshots the graph's values.  Caller holds pl->mu.
+static hnm_status plan_bind(hnm_ctx* ctx, hnm_spmm_plan* pl, const int32_t* col, const float* val) {
+  if (pl->bound_col) {
+    HNM_REQUIRE(col == pl->bound_col && val == pl->bound_val, HNM_EINVAL,
+                "spmm: this plan is bound to the col / val of its first use (it snapshots the "
+                "graph's values); create a new plan for other values");
+    return HNM_OK;
   }
-  if (hipMalloc((void**)&tval, std::max<int64_t>(T, 1) * 4) != hipSuccess) {
-    (void)hipFree(tcol);
-    hnm_set_error("spmm walk: hipMalloc failed");
-    return HNM_ENOMEM;
+  if (pl->walk) {
+    const int64_t T = pl->nnz;
+    const std::vector<int64_t>& rp = *pl->h_rowptr;
+    std::vector<int32_t> c0((size_t)T);
+    std::vector<float> v0((size_t)T);
+    HNM_HIP_CHECK(hipMemcpyAsync(c0.data(), col, T * 4, hipMemcpyDeviceToHost, ctx->stream));
+    HNM_HIP_CHECK(hipMemcpyAsync(v0.data(), val, T * 4, hipMemcpyDeviceToHost, ctx->stream));
+    HNM_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    pl->h_scol = new std::vector<int32_t>((size_t)T);
+    pl->h_sval = new std::vector<float>((size_t)T);
+    std::vector<int32_t>& hc = *pl->h_scol;
+    std::vector<float>& hv = *pl->h_sval;
+    const int64_t nchunk = hnm_cdiv(pl->N, 4096);
+    parallel_for(nchunk, [&](int64_t ch) {
+      std::vector<int32_t> ix;
+      const int64_t r1 = std::min<int64_t>(pl->N, (ch + 1) * 4096);
+      for (int64_t r = ch * 4096; r < r1; ++r) {
+        const int64_t a = rp[r], L = rp[r + 1] - a;
+        ix.resize((size_t)L);
+        for (int64_t q = 0; q < L; ++q) ix[q] = (int32_t)q;
+        std::stable_sort(ix.begin(), ix.end(),
+                         [&](int32_t x, int32_t y) { return c0[a + x] < c0[a + y]; });
+        for (int64_t q = 0; q < L; ++q) {
+          hc[a + q] = c0[a + ix[q]];
+          hv[a + q] = v0[a + ix[q]];
+        }
+      }
+    });
+    hnm_status st;
+    if ((st = upload(&pl->scol, hc.data(), (size_t)T)) || (st = upload(&pl->sval, hv.data(), (size_t)T)))
+      return st;
   }
-  hipLaunchKernelGGL(walk_gather_kernel, dim3((unsigned)pl->n_walk), dim3(256), 0, ctx->stream,
-                     pl->walk_rows, pl->walk_ptr, rowptr, col, val, tcol, tval);
-  HNM_LAUNCH_CHECK();
-  std::vector<int32_t> c0(T);
-  std::vector<float> v0(T);
-  HNM_HIP_CHECK(hipMemcpyAsync(c0.data(), tcol, T * 4, hipMemcpyDeviceToHost, ctx->stream));
-  HNM_HIP_CHECK(hipMemcpyAsync(v0.data(), tval, T * 4, hipMemcpyDeviceToHost, ctx->stream));
-  HNM_HIP_CHECK(hipStreamSynchronize(ctx->stream));
-  const std::vector<int64_t>& wp = *pl->h_walk_ptr;
-  pl->h_wcol = new std::vector<int32_t>(T);
-  pl->h_wval = new std::vector<float>(T);
-  std::vector<int32_t>& hc = *pl->h_wcol;
-  std::vector<float>& hv = *pl->h_wval;
-  parallel_for(pl->n_walk, [&](int64_t k) {
-    const int64_t a = wp[k], L = wp[k + 1] - a;
-    std::vector<int32_t> ix((size_t)L);
-    for (int64_t q = 0; q < L; ++q) ix[q] = (int32_t)q;
-    std::stable_sort(ix.begin(), ix.end(), [&](int32_t x, int32_t y) { return c0[a + x] < c0[a + y]; });
-    for (int64_t q = 0; q < L; ++q) {
-      hc[a + q] = c0[a + ix[q]];
-      hv[a + q] = v0[a + ix[q]];
-    }
-  });
-  HNM_HIP_CHECK(hipMemcpy(tcol, hc.data(), T * 4, hipMemcpyHostToDevice));
-  HNM_HIP_CHECK(hipMemcpy(tval, hv.data(), T * 4, hipMemcpyHostToDevice));
-  pl->wcol = tcol;
-  pl->wval = tval;
+  pl->bound_col = col;
+  pl->bound_val = val;
   return HNM_OK;
 }
 
@@ -964,7 +1058,7 @@ static hnm_status walk_build(hnm_spmm_plan* pl, int d, WalkSched** out) {
   // WALK_WIN > 1: slot maxloc absorbs the windows' padding entries (never stored)
   const int maxloc = WALK_WIN > 1 ? std::min(1022, WALK_LDS_F4 / lpr - 1)
                                   : std::min(1023, WALK_LDS_F4 / lpr);
-  const std::vector<int64_t>& wp = *pl->h_walk_ptr;
+  const std::vector<int64_t>& rp = *pl->h_rowptr;
   const std::vector<int32_t>& wr = *pl->h_walk_rows;
   const int64_t cap = pl->walk_cap, T = pl->walk_nnz;
   struct Piece {
@@ -974,7 +1068,7 @@ static hnm_status walk_build(hnm_spmm_plan* pl, int d, WalkSched** out) {
   };
   std::vector<Piece> pcs;
   for (int64_t k = 0; k < pl->n_walk; ++k) {
-    const int64_t L = wp[k + 1] - wp[k];
+    const int64_t L = rp[wr[k] + 1] - rp[wr[k]];
     const int n = (int)hnm_cdiv(L, cap);
     for (int j = 0; j < n; ++j) pcs.push_back({(int32_t)k, j, n, (L - j + n - 1) / n});
   }
@@ -984,7 +1078,6 @@ static hnm_status walk_build(hnm_spmm_plan* pl, int d, WalkSched** out) {
   while ((int64_t)pcs.size() > nwg * maxloc * 7 / 8) nwg *= 2;
   std::vector<std::vector<int32_t>> wgp((size_t)nwg);
   {
-    std::vector<int64_t> load((size_t)nwg, 0);
     using E = std::pair<int64_t, int64_t>;
     std::priority_queue<E, std::vector<E>, std::greater<E>> q;
     for (int64_t w = 0; w < nwg; ++w) q.push({0, w});
@@ -1003,14 +1096,13 @@ static hnm_status walk_build(hnm_spmm_plan* pl, int d, WalkSched** out) {
   std::vector<int32_t> srows;
   std::vector<int64_t> sptr{0}, kpart((size_t)pl->n_walk, -1);
   for (int64_t k = 0; k < pl->n_walk; ++k) {
-    const int n = (int)hnm_cdiv(wp[k + 1] - wp[k], cap);
+    const int n = (int)hnm_cdiv(rp[wr[k] + 1] - rp[wr[k]], cap);
     if (n <= 1) continue;
     kpart[k] = sptr.back();
     srows.push_back(wr[k]);
     sptr.push_back(sptr.back() + n);
   }
   std::vector<int32_t> slot_out((size_t)(nwg * maxloc), 0), nslot((size_t)nwg);
-  std::vector<int64_t> gcount((size_t)(nwg * ng), 0);
   std::vector<std::vector<std::vector<int32_t>>> gslots((size_t)nwg);
   for (int64_t w = 0; w < nwg; ++w) {
     nslot[w] = (int32_t)wgp[w].size();
@@ -1021,7 +1113,6 @@ static hnm_status walk_build(hnm_spmm_plan* pl, int d, WalkSched** out) {
       const int gb = (int)(std::min_element(gl.begin(), gl.end()) - gl.begin());
       gslots[w][gb].push_back(sl);
       gl[gb] += pc.len;
-      gcount[w * ng + gb] += pc.len;
       slot_out[w * maxloc + sl] = pc.n == 1 ? wr[pc.k] : (int32_t)(-(kpart[pc.k] + pc.j) - 1);
     }
   }
@@ -1029,21 +1120,20 @@ static hnm_status walk_build(hnm_spmm_plan* pl, int d, WalkSched** out) {
   // padded to a multiple of 4 entries; the kernel syncs its groups after every window
   constexpr int K = WALK_WIN > 1 ? WALK_WIN : 1;
   const int64_t wlen = hnm_cdiv(pl->N, K);
-  const std::vector<int32_t>& hc = *pl->h_wcol;
-  const std::vector<float>& hv = *pl->h_wval;
+  const std::vector<int32_t>& hc = *pl->h_scol;
+  const std::vector<float>& hv = *pl->h_sval;
   std::vector<int64_t> wcnt((size_t)(nwg * ng * K), 0);
   parallel_for(nwg, [&](int64_t w) {
     for (int g = 0; g < ng; ++g)
       for (int sl : gslots[w][g]) {
         const Piece& pc = pcs[wgp[w][sl]];
-        const int64_t a = wp[pc.k], L = wp[pc.k + 1] - a;
+        const int64_t a = rp[wr[pc.k]], L = rp[wr[pc.k] + 1] - a;
         for (int64_t q = pc.j; q < L; q += pc.n) ++wcnt[(w * ng + g) * K + hc[a + q] / wlen];
       }
   });
   std::vector<int64_t> gptr((size_t)(nwg * ng * K + 1), 0);
   for (int64_t i = 0; i < nwg * ng * K; ++i)
     gptr[i + 1] = gptr[i] + (K > 1 ? hnm_cdiv(wcnt[i], 4) * 4 : wcnt[i]);
-  (void)gcount;
   const int64_t Tp = gptr.back();
   std::vector<uint32_t> ent((size_t)Tp, (uint32_t)maxloc);  // padding: col 0, spare slot, 0.0
   std::vector<float> wt((size_t)Tp, 0.f);
@@ -1053,7 +1143,7 @@ static hnm_status walk_build(hnm_spmm_plan* pl, int d, WalkSched** out) {
       Lst.clear();
       for (int sl : gslots[w][g]) {
         const Piece& pc = pcs[wgp[w][sl]];
-        const int64_t a = wp[pc.k], L = wp[pc.k + 1] - a;
+        const int64_t a = rp[wr[pc.k]], L = rp[wr[pc.k] + 1] - a;
         for (int64_t q = pc.j; q < L; q += pc.n)
           Lst.push_back({((uint64_t)(uint32_t)hc[a + q] << 10) | (uint64_t)sl, hv[a + q]});
       }
@@ -1091,25 +1181,170 @@ static hnm_status walk_build(hnm_spmm_plan* pl, int d, WalkSched** out) {
   return HNM_OK;
 }
 
+// Short-walk schedule for d: the short rows cut into nb blocks of consecutive rows at equal
+// shares of their entries (at most S rows a block; nb a multiple of the persistent grid once the
+// graph fills it), each block's rows dealt to its ng lane groups (longest first, least-loaded
+// group), each group's rows' entries merged by column, cut at SWALK_WIN column bounds (quantiles
+// of all short entries' columns) and padded to multiples of 4 with weight-0 entries into the
+// spare slot S.  The placement only moves rows between lanes; each row's chain order is its
+// sorted entries' order.
+static hnm_status swalk_build(hnm_spmm_plan* pl, int d, ShortSched** out) {
+  const int lpr = d / 4, ng = WALK_THREADS / lpr;
+  const int S = std::min(1022, WALK_LDS_F4 / lpr - 1);
+  const std::vector<int64_t>& rp = *pl->h_rowptr;
+  const std::vector<int32_t>& sr = *pl->h_short_rows;
+  const std::vector<int32_t>& hc = *pl->h_scol;
+  const std::vector<float>& hv = *pl->h_sval;
+  const int64_t ns = (int64_t)sr.size();
+  const int64_t nwg_full = (int64_t)std::max(1, pl->num_cus) * SWALK_WG_PER_CU;
+  std::vector<int64_t> cum((size_t)ns + 1, 0);
+  for (int64_t i = 0; i < ns; ++i) cum[i + 1] = cum[i] + (rp[sr[i] + 1] - rp[sr[i]]);
+  const int64_t total = cum[ns];
+  int64_t nb0 = std::max<int64_t>(1, hnm_cdiv(ns, S));
+  int64_t nb = nb0 >= nwg_full ? hnm_cdiv(nb0, nwg_full) * nwg_full : nb0;
+  std::vector<int64_t> bstart;  // first short-row index of each block (+ end)
+  for (;;) {
+    bstart.assign(1, 0);
+    int64_t i = 0;
+    for (int64_t b = 0; b < nb; ++b) {
+      const int64_t target = total * (b + 1) / nb;
+      int64_t j = i;
+      while (j < ns && j - i < S && (b == nb - 1 || cum[j + 1] <= target || j == i)) ++j;
+      i = j;
+      bstart.push_back(i);
+    }
+    if (i >= ns) break;
+    nb += nb >= nwg_full ? nwg_full : 1;  // the last block overflowed S rows
+  }
+  constexpr int K = SWALK_WIN > 1 ? SWALK_WIN : 1;
+  // column bounds of the windows: quantiles of every short entry's column
+  std::vector<int32_t> cb;
+  if (K > 1 && total > 0) {
+    std::vector<int64_t> hist((size_t)pl->N + 1, 0);
+    for (int64_t i = 0; i < ns; ++i)
+      for (int64_t q = rp[sr[i]]; q < rp[sr[i] + 1]; ++q) ++hist[hc[q]];
+    int64_t c = 0, acc = 0;
+    for (int k = 1; k < K; ++k) {
+      const int64_t want = total * k / K;
+      while (c < pl->N && acc + hist[c] <= want) acc += hist[c++];
+      cb.push_back((int32_t)c);  // window k starts at column cb[k - 1]
+    }
+  }
+  auto win = [&](int32_t c) {
+    return (int)(std::upper_bound(cb.begin(), cb.end(), c) - cb.begin());
+  };
+  std::vector<int32_t> srow((size_t)(nb * S), -1), nslot((size_t)nb, 0);
+  std::vector<int64_t> wcnt((size_t)(nb * ng * K), 0);
+  std::vector<std::vector<std::vector<int32_t>>> gslot((size_t)nb);  // per block, per group: slots
+  parallel_for(nb, [&](int64_t b) {
+    const int64_t i0 = bstart[b], n = bstart[b + 1] - i0;
+    nslot[b] = (int32_t)n;
+    std::vector<int32_t> ord((size_t)n);
+    for (int64_t s = 0; s < n; ++s) {
+      srow[b * S + s] = sr[i0 + s];
+      ord[s] = (int32_t)s;
+    }
+    std::stable_sort(ord.begin(), ord.end(), [&](int32_t x, int32_t y) {
+      return cum[i0 + x + 1] - cum[i0 + x] > cum[i0 + y + 1] - cum[i0 + y];
+    });
+    gslot[b].assign(ng, {});
+    std::vector<int64_t> gl((size_t)ng, 0);
+    for (int32_t s : ord) {
+      const int g = (int)(std::min_element(gl.begin(), gl.end()) - gl.begin());
+      gslot[b][g].push_back(s);
+      gl[g] += cum[i0 + s + 1] - cum[i0 + s];
+      const int32_t r = sr[i0 + s];
+      for (int64_t q = rp[r]; q < rp[r + 1]; ++q) ++wcnt[(b * ng + g) * K + win(hc[q])];
+    }
+  });
+  std::vector<int64_t> gptr((size_t)(nb * ng * K + 1), 0);
+  for (int64_t i = 0; i < nb * ng * K; ++i) gptr[i + 1] = gptr[i] + hnm_cdiv(wcnt[i], 4) * 4;
+  const int64_t Tp = gptr.back();
+  std::vector<uint32_t> ent((size_t)Tp, (uint32_t)S);
+  std::vector<float> wt((size_t)Tp, 0.f);
+  parallel_for(nb, [&](int64_t b) {
+    const int64_t i0 = bstart[b];
+    std::vector<std::pair<uint64_t, float>> Lst;
+    for (int g = 0; g < ng; ++g) {
+      Lst.clear();
+      std::vector<int32_t> sl = gslot[b][g];
+      std::sort(sl.begin(), sl.end());
+      for (int32_t s : sl) {
+        const int32_t r = sr[i0 + s];
+        for (int64_t q = rp[r]; q < rp[r + 1]; ++q)
+          Lst.push_back({((uint64_t)(uint32_t)hc[q] << 10) | (uint64_t)s, hv[q]});
+      }
+      std::stable_sort(Lst.begin(), Lst.end(),
+                       [](const auto& x, const auto& y) { return (x.first >> 10) < (y.first >> 10); });
+      size_t i = 0;
+      for (int k = 0; k < K; ++k) {
+        int64_t o = gptr[(b * ng + g) * K + k];
+        const int64_t e = gptr[(b * ng + g) * K + k + 1];
+        uint32_t pad = (uint32_t)S;
+        for (; i < Lst.size() && win((int32_t)(Lst[i].first >> 10)) == k; ++i) {
+          ent[o] = (uint32_t)Lst[i].first;
+          wt[o++] = Lst[i].second;
+          pad = (uint32_t)((Lst[i].first >> 10) << 10) | (uint32_t)S;  // re-gather a cached row
+        }
+        for (; o < e; ++o) ent[o] = pad;
+      }
+    }
+  });
+  ShortSched* ws = new ShortSched();
+  ws->lpr = lpr;
+  ws->ng = ng;
+  ws->S = S;
+  ws->nb = nb;
+  ws->nwg = (int)std::min<int64_t>(nb, nwg_full);
+  ws->gptr = nullptr;
+  ws->ent = nullptr;
+  ws->wt = nullptr;
+  ws->srow = nullptr;
+  ws->nslot = nullptr;
+  ws->first.resize((size_t)nb);
+  ws->last.resize((size_t)nb);
+  for (int64_t b = 0; b < nb; ++b) {
+    const int64_t n = bstart[b + 1] - bstart[b];
+    ws->first[b] = n ? sr[bstart[b]] : (b ? ws->last[b - 1] : 0);
+    ws->last[b] = n ? sr[bstart[b + 1] - 1] : ws->first[b];
+  }
+  hnm_status st;
+  if ((st = upload(&ws->gptr, gptr.data(), gptr.size())) || (st = upload(&ws->ent, ent.data(), ent.size())) ||
+      (st = upload(&ws->wt, wt.data(), wt.size())) || (st = upload(&ws->srow, srow.data(), srow.size())) ||
+      (st = upload(&ws->nslot, nslot.data(), nslot.size()))) {
+    short_sched_free(ws);
+    return st;
+  }
+  *out = ws;
+  return HNM_OK;
+}
+
 static int walk_index(int d) {
   int i = 0;
   while ((4 << i) < d) ++i;
   return i;
 }
 
-// The walk schedule for d, built on first use (col / val are first seen by the SpMM call).
-static hnm_status walk_get(hnm_ctx* ctx, const hnm_spmm_plan* cpl, const int64_t* rowptr,
-                           const int32_t* col, const float* val, int d, const WalkSched** out) {
+static bool spmm_d_ok(int d) {
+  for (int i = 0; i < 7; ++i)
+    if (d == (4 << i)) return true;
+  return false;
+}
+
+// Binding + the walk schedules for d, built on first use (one-time, host work with stream syncs).
+static hnm_status walk_get(hnm_ctx* ctx, const hnm_spmm_plan* cpl, const int32_t* col,
+                           const float* val, int d, const WalkSched** out,
+                           const ShortSched** sout) {
   hnm_spmm_plan* pl = const_cast<hnm_spmm_plan*>(cpl);
   std::lock_guard<std::mutex> lk(*pl->mu);
+  hnm_status s = plan_bind(ctx, pl, col, val);
+  if (s) return s;
+  if (!pl->walk || d <= 0) return HNM_OK;
   const int i = walk_index(d);
-  if (!pl->sched[i]) {
-    hnm_status s = walk_prepare(ctx, pl, rowptr, col, val);
-    if (s) return s;
-    s = walk_build(pl, d, &pl->sched[i]);
-    if (s) return s;
-  }
-  *out = pl->sched[i];
+  if (!pl->sched[i] && (s = walk_build(pl, d, &pl->sched[i]))) return s;
+  if (pl->swalk && !pl->ssched[i] && (s = swalk_build(pl, d, &pl->ssched[i]))) return s;
+  if (out) *out = pl->sched[i];
+  if (sout) *sout = pl->ssched[i];
   return HNM_OK;
 }
 
@@ -1124,6 +1359,7 @@ extern "C" hnm_status hnm_spmm_plan_create(hnm_ctx* ctx, int64_t N, const int64_
   std::vector<int32_t> lrows;
   for (int64_t r = 0; r < N; ++r) {
     const int64_t s = rp[r], e = rp[r + 1];
+    HNM_REQUIRE(e >= s, HNM_EINVAL, "spmm_plan: rowptr decreases at row %lld", (long long)r);
     if (SPMM_GROUPED && e - s > SPMM_SHORT && e - s <= HEAVY) lrows.push_back((int32_t)r);
     if (e - s <= HEAVY) continue;
     const int32_t hi = (int32_t)hrows.size();
@@ -1138,7 +1374,9 @@ extern "C" hnm_status hnm_spmm_plan_create(hnm_ctx* ctx, int64_t N, const int64_
   hnm_spmm_plan* pl = (hnm_spmm_plan*)calloc(1, sizeof(hnm_spmm_plan));
   HNM_REQUIRE(pl, HNM_ENOMEM, "spmm_plan: out of host memory");
   pl->device = ctx->device;
+  pl->num_cus = ctx->num_cus;
   pl->N = N;
+  pl->nnz = rp[N] - rp[0];
   pl->n_heavy = (int64_t)hrows.size();
   pl->n_seg = (int64_t)sstart.size();
   pl->h_heavy = new std::vector<int32_t>(hrows);
@@ -1147,34 +1385,28 @@ extern "C" hnm_status hnm_spmm_plan_create(hnm_ctx* ctx, int64_t N, const int64_
   pl->h_long = new std::vector<int32_t>(lrows);
   pl->mu = new std::mutex();
   // walk rows: every row of more than SPMM_SHORT entries (col << 10 must fit 32 bits)
-  pl->walk = SPMM_WALK && SPMM_GROUPED && N <= (int64_t)1 << 22;
+  pl->walk = SPMM_WALK && SPMM_GROUPED && N <= (int64_t)1 << 22 && rp[0] == 0;
   if (pl->walk) {
-    std::vector<int32_t> wr;
-    std::vector<int64_t> wp{0};
+    std::vector<int32_t> wr, sr;
+    int64_t wn = 0;
     for (int64_t r = 0; r < N; ++r) {
       const int64_t L = rp[r + 1] - rp[r];
-      if (L <= SPMM_SHORT) continue;
+      if (L <= SPMM_SHORT) {
+        sr.push_back((int32_t)r);
+        continue;
+      }
       wr.push_back((int32_t)r);
-      wp.push_back(wp.back() + L);
+      wn += L;
     }
     pl->n_walk = (int64_t)wr.size();
-    pl->walk_nnz = wp.back();
+    pl->walk_nnz = wn;
     // pieces of at most cap entries: half a group's share of a big graph's walk (so the
     // longest list is ~2x the mean), never below 512
     pl->walk_cap = std::max<int64_t>(512, hnm_cdiv(pl->walk_nnz, 2 * WALK_GROUPS_TARGET));
     pl->h_walk_rows = new std::vector<int32_t>(wr);
-    pl->h_walk_ptr = new std::vector<int64_t>(wp);
-    if (pl->n_walk == 0) {
-      pl->walk = 0;
-    } else if (hipMalloc((void**)&pl->walk_rows, pl->n_walk * 4) != hipSuccess ||
-               hipMalloc((void**)&pl->walk_ptr, (pl->n_walk + 1) * 8) != hipSuccess) {
-      hnm_spmm_plan_destroy(pl);
-      hnm_set_error("spmm_plan: hipMalloc failed");
-      return HNM_ENOMEM;
-    } else {
-      HNM_HIP_CHECK(hipMemcpy(pl->walk_rows, wr.data(), pl->n_walk * 4, hipMemcpyHostToDevice));
-      HNM_HIP_CHECK(hipMemcpy(pl->walk_ptr, wp.data(), (pl->n_walk + 1) * 8, hipMemcpyHostToDevice));
-    }
+    pl->h_short_rows = new std::vector<int32_t>(sr);
+    pl->h_rowptr = new std::vector<int64_t>(std::move(rp));
+    pl->swalk = SPMM_SWALK && !sr.empty();
   }
   if (pl->n_long > 0) {
     if (hipMalloc((void**)&pl->long_rows, pl->n_long * 4) != hipSuccess) {
@@ -1204,6 +1436,14 @@ extern "C" hnm_status hnm_spmm_plan_create(hnm_ctx* ctx, int64_t N, const int64_
   return HNM_OK;
 }
 
+extern "C" hnm_status hnm_spmm_plan_prepare(hnm_ctx* ctx, hnm_spmm_plan* plan, const int32_t* col,
+                                            const float* val, int d) {
+  HNM_REQUIRE(ctx && plan && col && val, HNM_EINVAL, "spmm_plan_prepare: NULL argument");
+  HNM_REQUIRE(d == 0 || spmm_d_ok(d), HNM_EUNSUPPORTED,
+              "spmm_plan_prepare: d must be 0 or one of 4, 8, 16, 32, 64, 128, 256 (got %d)", d);
+  return walk_get(ctx, plan, col, val, d, nullptr, nullptr);
+}
+
 extern "C" hnm_status hnm_spmm_plan_destroy(hnm_spmm_plan* pl) {
   if (!pl) return HNM_OK;
   if (pl->heavy_rows) (void)hipFree(pl->heavy_rows);
@@ -1213,14 +1453,14 @@ extern "C" hnm_status hnm_spmm_plan_destroy(hnm_spmm_plan* pl) {
   if (pl->seg_end) (void)hipFree(pl->seg_end);
   if (pl->long_rows) (void)hipFree(pl->long_rows);
   for (WalkSched* w : pl->sched) walk_sched_free(w);
-  if (pl->walk_rows) (void)hipFree(pl->walk_rows);
-  if (pl->walk_ptr) (void)hipFree(pl->walk_ptr);
-  if (pl->wcol) (void)hipFree(pl->wcol);
-  if (pl->wval) (void)hipFree(pl->wval);
+  for (ShortSched* w : pl->ssched) short_sched_free(w);
+  if (pl->scol) (void)hipFree(pl->scol);
+  if (pl->sval) (void)hipFree(pl->sval);
   delete pl->h_walk_rows;
-  delete pl->h_walk_ptr;
-  delete pl->h_wcol;
-  delete pl->h_wval;
+  delete pl->h_short_rows;
+  delete pl->h_rowptr;
+  delete pl->h_scol;
+  delete pl->h_sval;
   delete pl->mu;
   delete pl->h_long;
   delete pl->h_heavy;
@@ -1237,11 +1477,16 @@ static hnm_status spmm_launch(hnm_ctx* ctx, const hnm_spmm_plan* pl, int64_t N,
   const int64_t heavy = has_heavy ? HEAVY : INT64_MAX;
   // the live roofline times whole-graph layers only (row-range calls do less work)
   const bool timed = r0 == 0 && r1 == N;
+  if (pl) {
+    hnm_status s = walk_get(ctx, pl, col, val, 0, nullptr, nullptr);  // binding check
+    if (s) return s;
+  }
   if (pl && pl->walk) {
-    // walk rows (> SPMM_SHORT entries) by the user-ordered walk on the side stream, short rows
-    // by the grouped kernel on the ctx stream, concurrently (disjoint output rows)
-    const WalkSched* ws;
-    hnm_status s = walk_get(ctx, pl, rowptr, col, val, d, &ws);
+    // short rows (<= SPMM_SHORT entries) by the short walk, then the rows of more entries by the
+    // user-ordered walk (+ the split rows' finish), one stream, disjoint output rows
+    const WalkSched* ws = nullptr;
+    const ShortSched* ss = nullptr;
+    hnm_status s = walk_get(ctx, pl, col, val, d, &ws, &ss);
     if (s) return s;
     const std::vector<int32_t>& wr = *pl->h_walk_rows;
     const bool any = std::lower_bound(wr.begin(), wr.end(), (int32_t)std::min<int64_t>(r0, INT32_MAX)) !=
@@ -1257,13 +1502,27 @@ static hnm_status spmm_launch(hnm_ctx* ctx, const hnm_spmm_plan* pl, int64_t N,
     const bool fork = any && SPMM_WALK_MODE == 0;
     hipStream_t wst = fork ? ctx->side : ctx->stream;
     auto short_rows = [&]() -> hnm_status {
-      if (r1 > r0) {
-        hipLaunchKernelGGL(spmm_mixed_kernel<LPR>,
-                           dim3((unsigned)hnm_cdiv(r1 - r0, 4 * (64 / LPR))), dim3(256), 0,
-                           ctx->stream, r0, r1, pl->long_rows, (int64_t)0, (int64_t)0, (int64_t)0,
-                           rowptr, col, val, X, d, ep);
-        HNM_LAUNCH_CHECK();
+      if (r1 <= r0) return HNM_OK;
+      if (ss) {
+        // blocks whose rows meet [r0, r1) (blocks are in ascending row order)
+        const int64_t b0 = std::lower_bound(ss->last.begin(), ss->last.end(),
+                                            (int32_t)std::min<int64_t>(r0, INT32_MAX)) - ss->last.begin();
+        const int64_t b1 = std::lower_bound(ss->first.begin(), ss->first.end(),
+                                            (int32_t)std::min<int64_t>(r1, INT32_MAX)) - ss->first.begin();
+        if (b1 > b0) {
+          const unsigned grid = (unsigned)std::min<int64_t>(b1 - b0, ss->nwg);
+          hipLaunchKernelGGL(spmm_swalk_kernel<LPR>, dim3(grid), dim3(WALK_THREADS), 0, ctx->stream,
+                             ss->gptr, ss->ent, ss->wt, ss->srow, ss->nslot, ss->S, X, d, ep, r0, r1,
+                             b0, b1);
+          HNM_LAUNCH_CHECK();
+        }
+        return HNM_OK;
       }
+      hipLaunchKernelGGL(spmm_mixed_kernel<LPR>,
+                         dim3((unsigned)hnm_cdiv(r1 - r0, 4 * (64 / LPR))), dim3(256), 0,
+                         ctx->stream, r0, r1, pl->long_rows, (int64_t)0, (int64_t)0, (int64_t)0,
+                         rowptr, col, val, X, d, ep);
+      HNM_LAUNCH_CHECK();
       return HNM_OK;
     };
     if (SPMM_WALK_MODE == 2 && (s = short_rows())) return s;
@@ -1389,11 +1648,11 @@ extern "C" hnm_status hnm_spmm_csr_f32(hnm_ctx* ctx, const hnm_spmm_plan* plan, 
 template <int LPR>
 static hnm_status combine_launch(hnm_ctx* ctx, const int64_t* rows, int64_t n, int64_t N,
                                  const int64_t* rowptr, const int32_t* col, const float* val,
-                                 int d, const CombineLayers& cl, const WalkRows& wk, float* out) {
-  const int64_t rows_per_block = SPMM_GROUPED ? 4 * (64 / LPR) : 4;
+                                 int d, const CombineLayers& cl, const CombineOrder& co, float* out) {
+  const int64_t rows_per_block = SPMM_GROUPED && co.mode != 0 ? 4 * (64 / LPR) : 4;
   hipLaunchKernelGGL(spmm_rows_combine_kernel<LPR>, dim3((unsigned)hnm_cdiv(n, rows_per_block)),
                      dim3(256), 0,
-                     ctx->stream, rows, n, N, rowptr, col, val, d, cl, wk, out, ctx->err_dev);
+                     ctx->stream, rows, n, N, rowptr, col, val, d, cl, co, out, ctx->err_dev);
   HNM_LAUNCH_CHECK();
   return HNM_OK;
 }
@@ -1407,17 +1666,20 @@ extern "C" hnm_status hnm_spmm_rows_combine_f32(hnm_ctx* ctx, const hnm_spmm_pla
   HNM_REQUIRE(ctx && rowptr && col && val && layers && alphas && ((rows && out) || n == 0),
               HNM_EINVAL, "spmm_rows_combine: NULL argument");
   HNM_REQUIRE(!plan || plan->N == N, HNM_EINVAL, "spmm_rows_combine: plan built for a different graph");
-  WalkRows wk{};
-  if (plan && plan->walk && n > 0) {
-    hnm_spmm_plan* pl = const_cast<hnm_spmm_plan*>(plan);
-    {
-      std::lock_guard<std::mutex> lk(*pl->mu);
-      hnm_status s = walk_prepare(ctx, pl, rowptr, col, val);
-      if (s) return s;
-    }
-    wk = WalkRows{pl->walk_rows, pl->walk_ptr, pl->wcol, pl->wval, pl->n_walk, pl->walk_cap};
-  }
   HNM_REQUIRE(L >= 1 && L <= 8, HNM_EUNSUPPORTED, "spmm_rows_combine: 1 <= L <= 8");
+  CombineOrder co{};
+  co.mode = plan ? 1 : 0;
+  if (plan) {
+    hnm_status s = walk_get(ctx, plan, col, val, 0, nullptr, nullptr);
+    if (s) return s;
+    if (plan->walk) {
+      co.mode = 2;
+      co.short_sorted = plan->swalk;
+      co.scol = plan->scol;
+      co.sval = plan->sval;
+      co.cap = plan->walk_cap;
+    }
+  }
   CombineLayers cl;
   cl.L = L;
   for (int l = 0; l < L; ++l) {
@@ -1428,5 +1690,5 @@ extern "C" hnm_status hnm_spmm_rows_combine_f32(hnm_ctx* ctx, const hnm_spmm_pla
   for (int l = 0; l <= L; ++l) cl.a[l] = alphas[l];
   if (n <= 0) return HNM_OK;
   HNM_REQUIRE((uintptr_t)out % 16 == 0, HNM_EINVAL, "spmm_rows_combine: out not 16-B aligned");
-  HNM_SPMM_DISPATCH(combine_launch, ctx, rows, n, N, rowptr, col, val, d, cl, wk, out)
+  HNM_SPMM_DISPATCH(combine_launch, ctx, rows, n, N, rowptr, col, val, d, cl, co, out)
 }

@@ -578,7 +578,13 @@ __device__ __forceinline__ void wd_split_relu2(wf2 z, wh2& hi, unsigned& alo) {
   asm("v_fma_mixlo_f16 %0, %1, -1.0, %2 op_sel_hi:[1,0,0]\n\t"
       "v_fma_mixhi_f16 %0, %1, -1.0, %3 op_sel:[1,0,0] op_sel_hi:[1,0,0]"
       : "=&v"(d) : "v"(hub), "v"(z.x), "v"(z.y));
-  if (WD_LO_EXACT) {
+  if (WD_LO_EXACT == 2) {
+    // |x_lo| of x = relu(z) exactly, one packed min: z < 0 has x_hi = 0 and x_lo = 0; z >= 0
+    // has |f16(z - x_hi)| <= x_hi (half an ulp of x_hi when it is normal, 0 or 2^-24 <= x_hi
+    // when subnormal, and x_lo = 0 when x_hi = 0), so min(|d|, x_hi) is |x_lo| in every case
+    alo = __builtin_bit_cast(unsigned, __builtin_elementwise_min(
+                                           __builtin_bit_cast(wh2, d & 0x7fff7fffu), hi));
+  } else if (WD_LO_EXACT) {
     // halves whose z < 0 (sign bit of the unclamped hi) have x = relu(z) = 0, hence x_lo = 0:
     // clear them together with the sign bits (|x_lo| exact instead of over-estimated)
     const unsigned neg = ((hub >> 15) & 0x00010001u) * 0xffffu;

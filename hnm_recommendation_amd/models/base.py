@@ -27,8 +27,46 @@ class RecModule(nn.Module):
         info = inspect.getargvalues(frame)
         self.hparams = {k: info.locals[k] for k in info.args if k != "self"}
 
-    def log(self, *args, **kwargs):  # Lightning no-op (training is out of scope)
-        pass
+    def log(self, name, value, *args, **kwargs):
+        """LightningModule.log stand-in: the last value per name lands in `logged_metrics`
+        (what a Trainer's callback_metrics would hold)."""
+        if not hasattr(self, "logged_metrics"):
+            self.logged_metrics = {}
+        self.logged_metrics[name] = value
+
+    # ------------------------------------------------------ Lightning evaluation hooks
+    # The reference's offline-evaluation stack (`trainer.validate` / `trainer.test(ckpt_path=
+    # "best")`, scripts/train.py:252): validation_step -> predict_all_items -> torch.topk ->
+    # metrics.update, then on_*_epoch_end logs metrics.compute() and resets (neural_cf.py:235-272,
+    # lightgcn.py:267-294, wide_deep.py:314-342, matrix_factorization.py:158-185).  Here the
+    # dense score matrix + torch.topk is the fused top-K (`recommend_with_scores`, same
+    # (score desc, item asc) order), so a step never materialises the [B, num_items] scores.
+    def _validation_topk(self, batch):
+        return self.recommend_with_scores(batch["user_ids"], k=self.top_k)[1]
+
+    def validation_step(self, batch, batch_idx):
+        """batch: {'user_ids': [B], 'ground_truth': [B, T] item ids (negative = padding) or a
+        list of id lists}."""
+        self._check_top_k()  # torch.topk(scores, self.top_k) raises for top_k > num_items
+        with torch.no_grad():
+            top = self._validation_topk(batch)
+        self.metrics.update(top, batch["ground_truth"])
+
+    def _epoch_end(self, prefix, **kw):
+        metrics = self.metrics.compute()
+        self.metrics.reset()
+        for name, value in metrics.items():
+            self.log(f"{prefix}_{name}", value, **kw)
+        return metrics
+
+    def on_validation_epoch_end(self):
+        return self._epoch_end("val", prog_bar=True)
+
+    def test_step(self, batch, batch_idx):
+        self.validation_step(batch, batch_idx)
+
+    def on_test_epoch_end(self):
+        return self._epoch_end("test")
 
     # ------------------------------------------------------------------ helpers
     @property

@@ -54,6 +54,20 @@ class NormalizedGraph:
         _lib.check(_lib.fn("hnm_spmm_plan_create")(c, num_nodes, _lib.ptr(self.rowptr),
                                                    C.byref(plan)), "hnm_spmm_plan_create")
         self.plan = plan
+        self.prepared = set()
+        # bind the plan to this CSR's col / val (a walk plan sorts a copy of every row once)
+        self.prepare(0)
+
+    def prepare(self, d: int):
+        """One-time plan work for embedding width d (hnm_spmm_plan_prepare: the walk schedules;
+        d = 0 binds the plan to col / val only), so no SpMM call does host work or syncs."""
+        if d in self.prepared:
+            return
+        c = _lib.ctx(self.device)
+        _lib.check(_lib.fn("hnm_spmm_plan_prepare")(c, self.plan, _lib.ptr(self.col),
+                                                    _lib.ptr(self.val), int(d)),
+                   "hnm_spmm_plan_prepare")
+        self.prepared.add(d)
 
     def spmm(self, X: torch.Tensor, Y: Optional[torch.Tensor], alpha: float,
              acc: Optional[torch.Tensor], acc_in: bool = True, beta: float = 0.0,
@@ -158,6 +172,8 @@ class LightGCN(RecModule):
         if g is None:
             g = NormalizedGraph(self.graph.edge_index, self.graph.edge_weight, self.num_nodes, dev)
             self.graph.built[dev] = g
+        if self.embedding_dim in (4, 8, 16, 32, 64, 128, 256):
+            g.prepare(self.embedding_dim)
         return g
 
     # ------------------------------------------------------------------ propagation

@@ -7,9 +7,16 @@ scoring methods run on the HIP library:
 * `predict_all_items(user_ids)` (`:143-208`)      -> hnm_ncf_scores_f32 (dense [B, I])
 * `recommend(user_ids, filter_items)` (`:300-326`) -> hnm_ncf_topk_f32 (fused pair-MLP +
   filter + top-K; never materializes [B, I])
+
+Those fused kernels take the reference's default two-layer tower (mlp_dims of length 3 with
+h1 <= 128, h2 <= 32, mf <= 128).  Any other tower `_build_mlp` accepts (`:75-90`: one
+Linear -> ReLU per consecutive pair of mlp_dims, e.g. [64, 32] or [128, 64, 32, 16]) runs the
+exact fp32 deep-tower kernel (hnm_ncf_deep_scores_f32): pair scores for forward, dense rows
+for predict_all_items, and dense rows in user chunks + the row top-k kernel for recommend.
 """
 from __future__ import annotations
 
+import ctypes as C
 from typing import Dict, List, Optional
 
 import torch
@@ -73,17 +80,61 @@ class NeuralCF(RecModule):
         nn.init.zeros_(self.prediction_layer.bias)
 
     # ------------------------------------------------------------------ HIP plumbing
+    def _linears(self):
+        return [m for m in self.mlp_layers if isinstance(m, nn.Linear)]
+
+    def _fused(self) -> bool:
+        """Whether the fused (certified) kernels take this tower: two Linear layers within
+        their register budget -- the reference default [128, 64, 32] with mf 64."""
+        lin = self._linears()
+        return (len(lin) == 2 and lin[0].out_features <= 128 and lin[1].out_features <= 32
+                and 1 <= self.mf_dim <= 128)
+
+    def _deep_weights(self):
+        """(hnm_ncf_deep_weights, tensors it points into) for towers of any depth."""
+        lin = self._linears()
+        if not 1 <= len(lin) <= 8:
+            raise ValueError(f"NeuralCF: 1..8 MLP layers supported, got mlp_dims={self.mlp_dims}")
+        keep = [f32c(p) for p in (self.gmf_user_embedding.weight, self.gmf_item_embedding.weight,
+                                  self.mlp_user_embedding.weight, self.mlp_item_embedding.weight)]
+        ws = [f32c(m.weight) for m in lin]
+        bs = [f32c(m.bias) for m in lin]
+        wp, bp = f32c(self.prediction_layer.weight).reshape(-1), f32c(self.prediction_layer.bias)
+        keep += ws + bs + [wp, bp]
+        _lib.require_gpu(*keep)
+        w = _lib.NcfDeepWeights()
+        w.gmf_user, w.gmf_item, w.mlp_user, w.mlp_item = (t.data_ptr() for t in keep[:4])
+        for j, (a, b) in enumerate(zip(ws, bs)):
+            w.w[j], w.b[j] = a.data_ptr(), b.data_ptr()
+        w.wp, w.bp = wp.data_ptr(), bp.data_ptr()
+        w.num_users, w.num_items, w.mf, w.nl = self.num_users, self.num_items, self.mf_dim, len(lin)
+        dims = [lin[0].in_features] + [m.out_features for m in lin]
+        for j, v in enumerate(dims):
+            w.dims[j] = v
+        return w, keep
+
+    def _deep_scores(self, u, items=None, out=None):
+        w, keep = self._deep_weights()
+        B = u.numel()
+        if out is None:
+            out = torch.empty(B, self.num_items if items is None else 1, dtype=torch.float32,
+                              device=u.device)
+        c = _lib.ctx(u.device)
+        _lib.check(_lib.fn("hnm_ncf_deep_scores_f32")(
+            c, C.byref(w), _lib.ptr(u), B, _lib.ptr(items), _lib.ptr(out),
+            out.stride(0) if items is None else 1), "hnm_ncf_deep_scores_f32")
+        return out
+
     def _weights(self):
         """(hnm_ncf_weights, tensors it points into).  When every parameter already is a
         contiguous fp32 GPU tensor the struct points at the parameters themselves and is reused
         while their storages are unchanged (keyed on the data pointers: the kernels read the
         values at call time, so in-place updates need no rebuild)."""
-        lin = [m for m in self.mlp_layers if isinstance(m, nn.Linear)]
-        if len(lin) != 2:
+        if not self._fused():
             raise ValueError(
-                "the fused NeuralCF kernel covers the reference's two-layer MLP tower "
-                f"(mlp_dims of length 3, e.g. [128, 64, 32]); got mlp_dims={self.mlp_dims}")
-        l1, l2 = lin
+                "the fused NeuralCF kernels cover the reference's two-layer MLP tower "
+                f"(h1 <= 128, h2 <= 32); mlp_dims={self.mlp_dims} runs the deep-tower path")
+        l1, l2 = self._linears()
         params = (self.gmf_user_embedding.weight, self.gmf_item_embedding.weight,
                   self.mlp_user_embedding.weight, self.mlp_item_embedding.weight,
                   l1.weight, l1.bias, l2.weight, l2.bias, self.prediction_layer.weight,
@@ -105,9 +156,15 @@ class NeuralCF(RecModule):
     # ------------------------------------------------------------------ reference API
     def forward(self, user_ids: torch.Tensor, item_ids: torch.Tensor) -> torch.Tensor:
         """Pairwise scores (`neural_cf.py:112-141`); `.squeeze()` semantics kept."""
-        w, keep = self._weights()
         u, hu = self._ids(user_ids, self.num_users)
         i, hi = self._ids(item_ids, self.num_items, "item_ids")
+        if u.numel() != i.numel():
+            raise ValueError("user_ids and item_ids must have the same length")
+        if not self._fused():
+            out = self._deep_scores(u, i).reshape(-1)
+            self._check(u.device, hu, hi)
+            return out.squeeze()
+        w, keep = self._weights()
         out = torch.empty(u.numel(), dtype=torch.float32, device=u.device)
         c = _lib.ctx(u.device)
         _lib.check(_lib.fn("hnm_ncf_pair_scores_f32")(c, w, _lib.ptr(u), _lib.ptr(i), u.numel(),
@@ -117,8 +174,12 @@ class NeuralCF(RecModule):
 
     def predict_all_items(self, user_ids: torch.Tensor) -> torch.Tensor:
         """Dense scores [B, num_items] (`neural_cf.py:143-208`)."""
-        w, keep = self._weights()
         u, hu = self._ids(user_ids, self.num_users)
+        if not self._fused():
+            out = self._deep_scores(u)
+            self._check(u.device, hu)
+            return out
+        w, keep = self._weights()
         out = torch.empty(u.numel(), self.num_items, dtype=torch.float32, device=u.device)
         c = _lib.ctx(u.device)
         _lib.check(_lib.fn("hnm_ncf_scores_f32")(c, w, _lib.ptr(u), u.numel(), _lib.ptr(out),
@@ -131,12 +192,14 @@ class NeuralCF(RecModule):
                               k: Optional[int] = None):
         """(scores [B, k], items [B, k]) sorted by score desc, item asc."""
         k = self.top_k if k is None else k
-        w, keep = self._weights()
         u, hu = self._ids(user_ids, self.num_users)
         mptr, midx = filter_csr(u, filter_items, self.num_items, u.device)
         kk = min(k, self.num_items)
         if kk <= 0:
             return empty_topk(k, u)
+        if not self._fused():
+            return self._deep_topk(u, hu, kk, mptr, midx)
+        w, keep = self._weights()
         if kk > 64:  # serve path k up to 100 (serve.py:56): dense + row top-k kernel
             scores = self.predict_all_items(u)
             return dense_topk(scores, kk, mptr, midx)
@@ -146,6 +209,23 @@ class NeuralCF(RecModule):
         _lib.check(_lib.fn("hnm_ncf_topk_f32")(c, w, _lib.ptr(u), u.numel(), _lib.ptr(mptr),
                                                _lib.ptr(midx), kk, _lib.ptr(out_v),
                                                _lib.ptr(out_i)), "hnm_ncf_topk_f32")
+        self._check(u.device, hu)
+        return out_v, out_i
+
+    def _deep_topk(self, u, hu, k, mptr, midx):
+        """Deep towers: dense rows for a chunk of users (<= 256 MB of scores) + the row top-k
+        kernel with the chunk's slice of the CSR mask (absolute offsets into mask_idx)."""
+        B = u.numel()
+        out_v = torch.empty(B, k, dtype=torch.float32, device=u.device)
+        out_i = torch.empty(B, k, dtype=torch.int64, device=u.device)
+        step = max(1, min(B, (1 << 26) // max(self.num_items, 1)))
+        buf = torch.empty(step, self.num_items, dtype=torch.float32, device=u.device)
+        for b0 in range(0, B, step):
+            b1 = min(B, b0 + step)
+            sc = self._deep_scores(u[b0:b1], out=buf[: b1 - b0])
+            v, i = dense_topk(sc, k, None if mptr is None else mptr[b0:b1 + 1], midx)
+            out_v[b0:b1] = v
+            out_i[b0:b1] = i
         self._check(u.device, hu)
         return out_v, out_i
 

@@ -264,6 +264,12 @@ class WideDeep(RecModule):
         self._check(u.device, hu)
         return out_v, out_i
 
+    def _validation_topk(self, batch):
+        """`predict_all_items(user_ids, user_features)` + torch.topk of the reference's
+        validation_step (wide_deep.py:314-332), as the fused top-K."""
+        return self.recommend_with_scores(batch["user_ids"], batch.get("user_features"),
+                                          k=self.top_k)[1]
+
     def recommend(self, user_ids, user_features=None,
                   filter_items: Optional[Dict[int, set]] = None):
         """Top-`top_k` item ids per user (`wide_deep.py:405-435`)."""

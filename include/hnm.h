@@ -213,6 +213,35 @@ hnm_status hnm_ncf_pair_scores_f32(hnm_ctx* ctx, const hnm_ncf_weights* w,
                                    const int64_t* user_ids, const int64_t* item_ids,
                                    int64_t n, float* out);
 
+/* NeuralCF with an MLP tower of any depth (neural_cf.py:75-90: one Linear -> ReLU per
+ * consecutive pair of mlp_dims, any length >= 2), exact fp32 -- the path for towers the fused
+ * kernels above do not cover (they take the default two-layer tower).  w[l] / b[l] =
+ * mlp_layers.{3l}.weight [dims[l+1], dims[l]] / bias; dims[0] = 2 x the MLP embedding width;
+ * widths dims[1..nl] <= 512, nl <= 8.
+ * item_ids NULL: dense scores out[b * ldo + i] for every item (ldo >= num_items, B < 65536:
+ * predict_all_items; recommend = these + hnm_topk_rows_f32).  item_ids set: pair scores
+ * out[n] = s(user_ids[n], item_ids[n]), n < B (forward).  Out-of-range ids flag HNM_EOOB
+ * (hnm_ctx_check) and score NaN. */
+typedef struct {
+  const float* gmf_user;   /* [num_users, mf] */
+  const float* gmf_item;   /* [num_items, mf] */
+  const float* mlp_user;   /* [num_users, dims[0] / 2] */
+  const float* mlp_item;   /* [num_items, dims[0] / 2] */
+  const float* w[8];
+  const float* b[8];
+  const float* wp;         /* [mf + dims[nl]] prediction_layer.weight */
+  const float* bp;         /* [1] */
+  int64_t num_users;
+  int64_t num_items;
+  int32_t mf;
+  int32_t nl;              /* Linear layers = len(mlp_dims) - 1 */
+  int32_t dims[9];
+} hnm_ncf_deep_weights;
+
+hnm_status hnm_ncf_deep_scores_f32(hnm_ctx* ctx, const hnm_ncf_deep_weights* w,
+                                   const int64_t* user_ids, int64_t B, const int64_t* item_ids,
+                                   float* out, int64_t ldo);
+
 /* ---- a9 + a10: Wide&Deep ------------------------------------------------------------
  * Reference layout (wide_deep.py:92-134): deep tower Linear -> ReLU -> BatchNorm1d (eval:
  * running stats, eps) per layer; final_layer over [wide (one-hot u, one-hot i, wide user
@@ -343,15 +372,33 @@ hnm_status hnm_csr_build_norm(hnm_ctx* ctx, const int64_t* edge_index, const flo
 /* ---- a6: LightGCN.forward propagation -----------------------------------------------
  * Y = A_hat X (graph @ all_embeddings, lightgcn.py:152), with the layer combine fused:
  * acc_out = acc_in + alpha * Y (lightgcn.py:156-158).  Y and acc_out may be NULL.
- * d in {4, 8, 16, 32, 64, 128, 256}.  With a plan, rows of more than 128 entries (the item
- * rows: ~300 neighbours each, power-law up to ~1e6) are summed by the user-ordered walk: the
- * row's entries sorted by (col, CSR position) and cut into pieces of at most `cap` entries
- * (piece j = sorted entries j, j + n, ...), each piece one fp32 fma chain, several pieces
- * summed in 256/(d/4) interleaved slices and a fixed pairwise tree -- deterministic; the
- * first call per d builds the walk schedule (host, one-time).
- * Without a plan: one wave per row (deterministic, slower on power-law rows). */
+ * d in {4, 8, 16, 32, 64, 128, 256}.  With a plan on a graph of N <= 2^22 nodes (the "walk
+ * plan"; rowptr[0] == 0): every row's entries are summed in (col, CSR position) order -- rows
+ * of at most 128 entries (the user rows) as one fp32 fma chain each by the column-ordered short
+ * walk; longer rows (the item rows: ~300 neighbours each, power-law up to ~1e6) by the
+ * user-ordered walk: cut into pieces of at most `cap` entries (piece j = sorted entries
+ * j, j + n, ...), each piece one fp32 fma chain, several pieces summed in 256/(d/4)
+ * interleaved slices and a fixed pairwise tree -- deterministic.  Larger graphs: short rows one
+ * 16-lane group each, long rows one wave, rows over 2,048 entries in 2,048-entry segments + a
+ * fixed tree, all in CSR order.  Without a plan: one wave per row, CSR order (deterministic,
+ * slower on power-law rows).
+ * BINDING: a plan is bound to the col / val pointers of its first prepare / SpMM /
+ * rows_combine call and snapshots their values then (a walk plan keeps a sorted copy and
+ * per-d schedules); a later call with other col / val pointers fails with HNM_EINVAL, and
+ * values changed in place behind the same pointers are NOT seen -- create a new plan.
+ * PREPARATION: binding and the first use of each d do one-time host work that synchronizes the
+ * ctx stream (a D2H copy of col / val, host sorts, synchronous uploads of ~8 B per entry per
+ * schedule; seconds on the 65M-entry H&M graph) and cannot be captured in a hipGraph: call
+ * hnm_spmm_plan_prepare(ctx, plan, col, val, d) up front (d = 0: bind only).  After it every
+ * SpMM / rows_combine call is asynchronous; an SpMM over split rows needs n_part * d * 4 bytes
+ * of ctx workspace (a few MB; hnm_ctx_reserve covers it).
+ * ROW RANGES: a range call launches only the short-walk blocks holding rows of the range, but
+ * the whole long-row walk whenever one of its rows is in the range (outputs restricted to the
+ * range): chunking [0, N) into many ranges repeats the item half's gathers per chunk. */
 hnm_status hnm_spmm_plan_create(hnm_ctx* ctx, int64_t N, const int64_t* rowptr,
                                 hnm_spmm_plan** out);
+hnm_status hnm_spmm_plan_prepare(hnm_ctx* ctx, hnm_spmm_plan* plan, const int32_t* col,
+                                 const float* val, int d);
 hnm_status hnm_spmm_plan_destroy(hnm_spmm_plan* plan);
 hnm_status hnm_spmm_csr_f32(hnm_ctx* ctx, const hnm_spmm_plan* plan, int64_t N,
                             const int64_t* rowptr, const int32_t* col, const float* val,
@@ -371,8 +418,8 @@ hnm_status hnm_spmm_csr_range_f32(hnm_ctx* ctx, const hnm_spmm_plan* plan, int64
  * (host): out[b] = sum_l alphas[l] E_l[rows[b]] with E_L[r] = (A_hat E_{L-1})[r] computed
  * for the listed rows only -- the last layer of LightGCN.forward restricted to the users a
  * recommend() call reads (lightgcn.py:197-199).  Same operations and order as the fused
- * combine of hnm_spmm_csr_f32 with the same plan (bitwise equal, long rows included: they are
- * summed in the plan's walk order; plan NULL: the plan-less SpMM's order).  An id out of
+ * combine of hnm_spmm_csr_f32 with the same plan (bitwise equal: every row is summed in the
+ * order that plan's SpMM uses for it; plan NULL: the plan-less SpMM's order).  An id out of
  * range flags HNM_EOOB and writes NaN.  1 <= L <= 8. */
 hnm_status hnm_spmm_rows_combine_f32(hnm_ctx* ctx, const hnm_spmm_plan* plan, int64_t N,
                                      const int64_t* rowptr,

@@ -5,7 +5,7 @@ GPU box):
 
     PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py [small] [full]
 
-(`small`: the small-shape fixtures; `full`: the full-catalogue I = 105,542 fixtures --
+(`small`: the small-shape fixtures; `deep`: NeuralCF towers of other depths; `full`: the full-catalogue I = 105,542 fixtures --
 `full_fast` without Wide&Deep, `full_widedeep` Wide&Deep only, ~20 s per user.)
 
 The reference `src.models` is imported read-only with the four stubs of SURVEY.md §8(c)
@@ -170,6 +170,32 @@ def gen_ncf(models):
     save("ncf_config1.npz", U=U1, I=I1, K=12, seed=0, user_ids=users1, topk=r1,
          topk_scores=top_vals, row_sums=d1.astype(np.float64).sum(1),
          kth_gap=np.sort(d1, 1)[:, -12] - np.sort(d1, 1)[:, -13])
+
+
+def gen_ncf_deep(models):
+    """NeuralCF towers other than the default two layers (`_build_mlp`, neural_cf.py:75-90,
+    any len(mlp_dims) >= 2): one fixture per tower."""
+    U, I, B, K = 300, 500, 40, 12
+    for tag, dims, mf in (("d4", [128, 64, 32, 16], 64), ("d2", [64, 32], 32),
+                          ("wide", [256, 128, 64], 64)):
+        sd = syn.ncf_state_dict(U, I, mf, tuple(dims), seed=11, bias_scale=0.05, emb_scale=8.0)
+        m = load(models.NeuralCF(num_users=U, num_items=I, mf_dim=mf, mlp_dims=dims, top_k=K), sd)
+        users = tagged_users(U, B, seed=12)
+        fdict = syn.filter_dict(users, I, per_user=23, seed=13)
+        with torch.no_grad():
+            ut = torch.from_numpy(users)
+            dense = m.predict_all_items(ut).numpy()
+            rec = m.recommend(ut).numpy()
+            rec_f = m.recommend(ut, filter_items=fdict).numpy()
+            pu = torch.from_numpy(syn.user_batch(U, 50, seed=14))
+            pi = torch.from_numpy(syn.user_batch(I, 50, seed=15))
+            pair = m(pu, pi).numpy()
+        fk, fp, fi = dict_to_arrays(fdict)
+        save(f"ncf_deep_{tag}.npz", U=U, I=I, K=K, mf_dim=mf, mlp_dims=np.array(dims),
+             user_ids=users, dense=dense, topk=rec, topk_filtered=rec_f,
+             filter_keys=fk, filter_ptr=fp, filter_idx=fi,
+             pair_users=pu.numpy(), pair_items=pi.numpy(), pair_scores=pair,
+             **with_prefix("sd/", sd))
 
 
 def gen_lightgcn(models):
@@ -467,6 +493,8 @@ if __name__ == "__main__":
     which = sys.argv[1:] or ["small"]
     if "edges" in which:
         gen_widedeep_edges(models)
+    if "deep" in which:
+        gen_ncf_deep(models)
     if "small" in which:
         gen_ncf(models)
         gen_lightgcn(models)

@@ -225,3 +225,85 @@ def test_lightning_checkpoint_fixture_serves_on_gpu():
     assert len(one["recommendations"]) == 5
     with pytest.raises(ValueError):
         srv.get_recommendations(3, model_name="neural_cf", num_items=101)  # serve.py:56 le=100
+
+
+def _hook_model(name):
+    """(module, golden) for the Lightning-hook test, built like the golden tests build them."""
+    from hnm_recommendation_amd import LightGCN, WideDeep
+    if name == "ncf":
+        g = load_golden("ncf_small.npz")
+        m = NeuralCF(int(g["U"]), int(g["I"]), top_k=int(g["K"]))
+    elif name == "mf":
+        g = load_golden("mf_small.npz")
+        m = MatrixFactorization(int(g["U"]), int(g["I"]), top_k=int(g["K"]), sparse=False)
+    elif name == "lightgcn":
+        g = load_golden("lightgcn_d64.npz")
+        m = LightGCN(int(g["U"]), int(g["I"]), embedding_dim=int(g["d"]), num_layers=3,
+                     top_k=int(g["K"]))
+        m.set_graph(torch.from_numpy(g["edge_index"]))
+    elif name == "widedeep_feat":
+        g = load_golden("widedeep_feat.npz")
+        m = WideDeep(int(g["U"]), int(g["I"]), num_user_features=int(g["F"]), embedding_dim=16,
+                     deep_layers=[64, 32], top_k=int(g["K"]))
+    else:
+        g = load_golden("widedeep_small.npz")
+        m = WideDeep(int(g["U"]), int(g["I"]), embedding_dim=64, deep_layers=[512, 256, 128],
+                     top_k=int(g["K"]))
+    m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in g["sd"].items()})
+    return m.to(DEV).eval(), g
+
+
+@pytest.mark.parametrize("name", ["ncf", "mf", "lightgcn", "widedeep", "widedeep_feat"])
+def test_lightning_eval_hooks(name):
+    """validation_step / on_validation_epoch_end / test_step / on_test_epoch_end on the four
+    mirrors (neural_cf.py:235-272, lightgcn.py:267-294, wide_deep.py:314-342,
+    matrix_factorization.py:158-185) over {'user_ids', 'ground_truth'} batches (truth padded
+    with -1, some users with none): the logged val_* / test_* values equal the reference's
+    formulas (oracle.user_metrics, float64) over the module's top-K -- itself checked against
+    the REFERENCE's own dense scores (golden) -- MAP and Precision over every row, Recall and
+    NDCG over rows with truth."""
+    m, g = _hook_model(name)
+    K, I = int(g["K"]), int(g["I"])
+    users = np.asarray(g["user_ids"])
+    rng = np.random.Generator(np.random.PCG64(7))
+    T = 20
+    truth = np.full((len(users), T), -1, np.int64)
+    for r in range(len(users)):
+        n = int(rng.integers(0, T + 1)) if r % 5 else 0
+        truth[r, :n] = rng.integers(0, I, n)
+    # half the truth rows hold an item of the reference's own top-K, so hits are frequent
+    ref_top = O.topk(g["dense"], K)[1]
+    truth[1::2, 0] = ref_top[1::2, 3]
+    feats = g["user_features"] if "user_features" in g else None
+    halves = [slice(0, len(users) // 2), slice(len(users) // 2, len(users))]
+    for hook, end, prefix in ((m.validation_step, m.on_validation_epoch_end, "val"),
+                              (m.test_step, m.on_test_epoch_end, "test")):
+        for j, sl in enumerate(halves):
+            batch = {"user_ids": torch.from_numpy(users[sl]).to(DEV),
+                     "ground_truth": torch.from_numpy(truth[sl]).to(DEV)}
+            if feats is not None:
+                batch["user_features"] = torch.from_numpy(feats[sl]).to(DEV)
+            hook(batch, j)
+        end()
+        got = {k: float(m.logged_metrics[f"{prefix}_{k}"])
+               for k in ("map_at_k", "recall_at_k", "precision_at_k", "ndcg_at_k")}
+        uid = torch.from_numpy(users).to(DEV)
+        ours = (m.recommend(uid) if feats is None else
+                m.recommend(uid, torch.from_numpy(feats).to(DEV))).cpu().numpy()
+        assert_topk_equivalent(ours, g["dense"], K, what=f"{name} hook top-K")
+        rows = [O.user_metrics(ours[r].tolist(), set(int(x) for x in truth[r] if x >= 0), K)
+                for r in range(len(users))]
+        a = np.asarray(rows)
+        has = np.array([(truth[r] >= 0).any() for r in range(len(users))])
+        want = {"map_at_k": a[:, 0].mean(), "recall_at_k": a[has, 1].mean(),
+                "precision_at_k": a[:, 2].mean(), "ndcg_at_k": a[has, 3].mean()}
+        for k in want:
+            np.testing.assert_allclose(got[k], want[k], rtol=1e-12, err_msg=f"{name} {prefix} {k}")
+        assert got["map_at_k"] > 0
+    # metrics were reset at each epoch end
+    assert m.metrics._n_all == 0
+    if name == "ncf":
+        m.top_k = I + 1
+        with pytest.raises(RuntimeError):
+            m.validation_step({"user_ids": torch.from_numpy(users[:2]).to(DEV),
+                               "ground_truth": torch.from_numpy(truth[:2]).to(DEV)}, 0)

@@ -47,6 +47,49 @@ def test_ncf_golden():
     assert_scores_close(pair, g["pair_scores"], "ncf pair")
 
 
+@pytest.mark.parametrize("name", ["ncf_deep_d4.npz", "ncf_deep_d2.npz", "ncf_deep_wide.npz"])
+def test_ncf_deep_tower_golden(name):
+    """Towers other than the fused two-layer one ([128,64,32,16], [64,32] with mf 32,
+    [256,128,64]: hnm_ncf_deep_scores_f32) against the reference's own outputs: dense scores,
+    top-K (with and without the history filter, k = 12 and 100), pair forward; out-of-range
+    ids raise IndexError."""
+    g = load_golden(name)
+    U, I, K = int(g["U"]), int(g["I"]), int(g["K"])
+    m = to_module(NeuralCF(U, I, mf_dim=int(g["mf_dim"]), mlp_dims=[int(x) for x in g["mlp_dims"]],
+                           top_k=K), g["sd"])
+    assert not m._fused()
+    users = t(g["user_ids"])
+    dense = m.predict_all_items(users).cpu().numpy()
+    assert_scores_close(dense, g["dense"], name)
+    v, rec = m.recommend_with_scores(users)
+    assert_topk_equivalent(rec.cpu().numpy(), g["dense"], K, what=name)
+    np.testing.assert_array_equal(v.cpu().numpy(), np.take_along_axis(dense, rec.cpu().numpy(), 1))
+    f = filter_from_arrays(g["filter_keys"], g["filter_ptr"], g["filter_idx"])
+    masked = O.apply_filter(g["dense"], g["user_ids"], f)
+    assert_topk_equivalent(m.recommend(users, filter_items=f).cpu().numpy(), masked, K)
+    _, r100 = m.recommend_with_scores(users, filter_items=f, k=100)
+    assert_topk_equivalent(r100.cpu().numpy(), masked, 100)
+    pair = m(t(g["pair_users"]), t(g["pair_items"])).cpu().numpy()
+    assert_scores_close(pair, g["pair_scores"], name + " pair")
+    with pytest.raises(IndexError):
+        m.recommend(torch.tensor([0, U], device=DEV))
+    with pytest.raises(IndexError):
+        m(torch.tensor([0, 1], device=DEV), torch.tensor([0, I], device=DEV))
+
+
+def test_ncf_deep_tower_chunked_full_catalogue():
+    """A deep tower over the full H&M catalogue with more users than one dense chunk
+    (recommend = dense rows per user chunk + the row top-k kernel) against the oracle."""
+    U, I = 3000, syn.HM_ITEMS
+    sd = syn.ncf_state_dict(U, I, 64, (128, 64, 32, 16), seed=21, bias_scale=0.05, emb_scale=8.0)
+    m = to_module(NeuralCF(U, I, mlp_dims=[128, 64, 32, 16]), sd)
+    users = syn.user_batch(U, 700, seed=3)
+    _, rec = m.recommend_with_scores(t(users))
+    rows = [0, 1, 636, 699]
+    ref = O.ncf_predict_all_items(sd, users[rows])
+    assert_topk_equivalent(rec.cpu().numpy()[rows], ref, 12, what="deep full catalogue")
+
+
 def test_ncf_config1_golden():
     """BASELINE configs[0] shape (10k x 5k), reference init distributions."""
     g = load_golden("ncf_config1.npz")

@@ -1,0 +1,148 @@
+"""LightGCN SpMM plans through the C ABI (graph.hip): the short-row walk, the plan's binding to
+its col / val, and rows_combine's summation order with and without a plan
+(reference: lightgcn.py:136-164, `graph @ all_embeddings` per layer)."""
+import ctypes as C
+
+import numpy as np
+import pytest
+import torch
+
+from hnm_recommendation_amd import LightGCN, _lib
+from hnm_recommendation_amd import synthetic as syn
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _graph(U, I, edges, d):
+    m = LightGCN(U, I, d)
+    m.set_graph(torch.from_numpy(edges))
+    m = m.to(DEV)
+    return m, m._device_graph()
+
+
+def _dense_ref(g, x):
+    import scipy.sparse as sp
+    rp, col, val = (a.cpu().numpy() for a in (g.rowptr, g.col, g.val))
+    N = len(rp) - 1
+    A = sp.csr_matrix((val.astype(np.float64), col, rp), shape=(N, N))
+    xd = x.double().cpu().numpy()
+    return A @ xd, abs(A) @ np.abs(xd)
+
+
+def _spmm_raw(g, plan, x, y):
+    c = _lib.ctx(x.device)
+    return _lib.fn("hnm_spmm_csr_f32")(c, plan, g.num_nodes, _lib.ptr(g.rowptr), _lib.ptr(g.col),
+                                       _lib.ptr(g.val), _lib.ptr(x), x.shape[1], _lib.ptr(y), 0.0,
+                                       None, None)
+
+
+def _combine_raw(g, plan, rows, layers, alphas, out, val=None):
+    c = _lib.ctx(rows.device)
+    L = len(layers)
+    ptrs = (C.c_void_p * L)(*[t.data_ptr() for t in layers])
+    al = (C.c_float * (L + 1))(*[float(a) for a in alphas])
+    return _lib.fn("hnm_spmm_rows_combine_f32")(
+        c, plan, g.num_nodes, _lib.ptr(g.rowptr), _lib.ptr(g.col),
+        _lib.ptr(g.val if val is None else val), _lib.ptr(rows), rows.numel(), layers[0].shape[1],
+        ptrs, al, L, _lib.ptr(out))
+
+
+@pytest.mark.parametrize("d", [4, 64, 128, 256])
+def test_spmm_short_walk_rows(d):
+    """Rows of at most 128 entries (every user row here, plus the tail items) go through the
+    column-ordered short walk (spmm_swalk_kernel): blocks of up to S consecutive rows with LDS
+    accumulators.  Rows at the 127 / 128 / 129 boundary, duplicate edges, users with no edge
+    (self-loop only), enough rows for several blocks per workgroup at d = 64.  Checked against
+    A_hat X in float64 (1e-5 of sum |a||x|), run-to-run bitwise, and row-range calls (the users
+    only; a window in the middle) bitwise equal to the whole-graph call with the rest untouched."""
+    U, I = 200_000 if d == 64 else 60_000, 3_000
+    rng = np.random.default_rng(11)
+    base = syn.bipartite_edge_index(U, I, 4 * U, seed=5)
+    gone = np.arange(5, 40)  # users 5..39 lose their random edges
+    base = base[:, ~(np.isin(base[0], gone) | np.isin(base[1], gone))]
+    dup = base[:, :3000]
+    fix = []
+    for u, n in ((5, 126), (6, 127), (7, 128), (8, 129)):
+        it = rng.choice(np.arange(1, I), size=n, replace=False) + U
+        fix.append(np.stack([np.full(n, u), it]))
+    one = np.concatenate([dup] + fix, axis=1)
+    edges = np.concatenate([base, one, one[::-1]], axis=1)
+    m, g = _graph(U, I, edges, d)
+    N = U + I
+    x = torch.randn(N, d, generator=torch.Generator().manual_seed(2)).to(DEV)
+    y1, y2 = torch.empty_like(x), torch.empty_like(x)
+    g.spmm(x, y1, 0.0, None)
+    g.spmm(x, y2, 0.0, None)
+    ya = torch.zeros_like(x)
+    g.spmm(x, ya, 0.0, None, rows=(0, U))
+    mid = (U // 3, U // 3 + 5_000)
+    yb = torch.zeros_like(x)
+    g.spmm(x, yb, 0.0, None, rows=mid)
+    torch.cuda.synchronize()
+    assert torch.equal(y1, y2)
+    assert torch.equal(ya[:U], y1[:U]) and not ya[U:].any()
+    assert torch.equal(yb[mid[0]:mid[1]], y1[mid[0]:mid[1]])
+    assert not yb[:mid[0]].any() and not yb[mid[1]:].any()
+    rp = g.rowptr.cpu().numpy()
+    L = np.diff(rp)
+    assert (L[:U] <= 128).sum() >= U - 10 and (L[10:40] == 1).all()
+    assert [int(v) for v in L[5:9]] == [127, 128, 129, 130]
+    ref, mag = _dense_ref(g, x)
+    err = np.abs(y1.double().cpu().numpy() - ref)
+    assert (err <= 1e-5 * mag + 1e-30).all(), float((err / (mag + 1e-30)).max())
+    # rows_combine sums the short rows in the walk's order: bitwise equal to the layer kernel
+    rows = torch.tensor([0, 5, 6, 7, 8, 12, U - 1, U, N - 1, 7], dtype=torch.int64, device=DEV)
+    out = torch.empty(rows.numel(), d, device=DEV)
+    assert _combine_raw(g, g.plan, rows, [x], [0.0, 1.0], out) == 0
+    torch.cuda.synchronize()
+    assert torch.equal(out, y1[rows])
+
+
+def test_plan_null_rows_combine_matches_plan_null_spmm():
+    """hnm.h: rows_combine with plan NULL sums every row in the plan-less SpMM's order (one wave
+    per row, CSR order), so the two agree bit for bit -- short, long and >2,048-entry rows."""
+    U, I, d = 3_000, 20_000, 64
+    rng = np.random.default_rng(3)
+    base = syn.bipartite_edge_index(U, I, 40_000, seed=4)
+    extra = []
+    for u, n in ((0, 100), (1, 500), (2, 3_000)):
+        it = rng.choice(I, size=n, replace=False) + U
+        extra.append(np.stack([np.full(n, u), it]))
+    e = np.concatenate(extra, axis=1)
+    edges = np.concatenate([base, e, e[::-1]], axis=1)
+    m, g = _graph(U, I, edges, d)
+    N = U + I
+    x = torch.randn(N, d, generator=torch.Generator().manual_seed(5)).to(DEV)
+    y = torch.empty_like(x)
+    assert _spmm_raw(g, None, x, y) == 0
+    rows = torch.tensor([0, 1, 2, 3, U - 1, U, U + 1, N - 1], dtype=torch.int64, device=DEV)
+    out = torch.empty(rows.numel(), d, device=DEV)
+    assert _combine_raw(g, None, rows, [x], [0.0, 1.0], out) == 0
+    torch.cuda.synchronize()
+    assert torch.equal(out, y[rows])
+    ref, mag = _dense_ref(g, x)
+    assert (np.abs(y.double().cpu().numpy() - ref) <= 1e-5 * mag + 1e-30).all()
+
+
+def test_plan_bound_to_its_values():
+    """A plan snapshots the col / val of its first use: a call with another val array is
+    refused (HNM_EINVAL) instead of silently mixing stale and new values (hnm.h BINDING)."""
+    U, I, d = 2_000, 1_000, 64
+    edges = syn.bipartite_edge_index(U, I, 10_000, seed=1)
+    m, g = _graph(U, I, edges, d)
+    x = torch.randn(U + I, d, generator=torch.Generator().manual_seed(1)).to(DEV)
+    y = torch.empty_like(x)
+    val2 = g.val.clone()
+    c = _lib.ctx(x.device)
+    st = _lib.fn("hnm_spmm_csr_f32")(c, g.plan, g.num_nodes, _lib.ptr(g.rowptr), _lib.ptr(g.col),
+                                     _lib.ptr(val2), _lib.ptr(x), d, _lib.ptr(y), 0.0, None, None)
+    assert st == _lib.HNM_EINVAL
+    rows = torch.arange(4, dtype=torch.int64, device=DEV)
+    out = torch.empty(4, d, device=DEV)
+    assert _combine_raw(g, g.plan, rows, [x], [0.0, 1.0], out, val=val2) == _lib.HNM_EINVAL
+    # the bound arrays still work, and prepare for an unsupported d is refused
+    assert _spmm_raw(g, g.plan, x, y) == 0
+    st = _lib.fn("hnm_spmm_plan_prepare")(c, g.plan, _lib.ptr(g.col), _lib.ptr(g.val), 48)
+    assert st == _lib.HNM_EUNSUPPORTED
+    torch.cuda.synchronize()

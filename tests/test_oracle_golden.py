@@ -25,6 +25,20 @@ def test_ncf_small_matches_reference():
     assert_scores_close(pair, g["pair_scores"], "ncf pair")
 
 
+@pytest.mark.parametrize("name", ["ncf_deep_d4.npz", "ncf_deep_d2.npz", "ncf_deep_wide.npz"])
+def test_ncf_deep_towers_match_reference(name):
+    """NeuralCF towers of other depths (neural_cf.py:75-90): [128,64,32,16], [64,32] (mf 32),
+    [256,128,64] -- the oracle's layer loop against the reference's own outputs."""
+    g = load_golden(name)
+    dense = O.ncf_predict_all_items(g["sd"], g["user_ids"])
+    assert_scores_close(dense, g["dense"], name)
+    assert_topk_equivalent(g["topk"], dense, int(g["K"]))
+    f = filter_from_arrays(g["filter_keys"], g["filter_ptr"], g["filter_idx"])
+    assert_topk_equivalent(g["topk_filtered"], O.apply_filter(dense, g["user_ids"], f), int(g["K"]))
+    pair = O.ncf_forward(g["sd"], g["pair_users"], g["pair_items"])
+    assert_scores_close(pair, g["pair_scores"], name + " pair")
+
+
 def test_ncf_config1_matches_reference():
     """BASELINE configs[0]: 10k users x 5k items, weights regenerated from seed 0."""
     g = load_golden("ncf_config1.npz")
