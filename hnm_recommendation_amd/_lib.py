@@ -309,7 +309,8 @@ def set_prefilter(device, on=True):
 def prefilter_stats(device, reset=False):
     """(rows scored, candidates re-scored in fp32, rows that took the exact fallback) summed
     over every thread's ctx on `device`; counted only while HNM_OPT_STATS is on
-    (set_option(dev, HNM_OPT_STATS, 1))."""
+    (set_option(dev, HNM_OPT_STATS, 1)).  Each read syncs the device; calls other threads issue
+    meanwhile may be counted before or after a reset (exact when they are idle)."""
     ctx(device)
     tot = [0, 0, 0]
     for c in _device_ctxs(_dev_index(device)):

@@ -100,7 +100,10 @@ extern "C" hnm_status hnm_ctx_set_option(hnm_ctx* ctx, int option, int64_t value
 
 extern "C" hnm_status hnm_ctx_prefilter_stats(hnm_ctx* ctx, int64_t* out, int reset) {
   HNM_REQUIRE(ctx && out, HNM_EINVAL, "ctx/out is NULL");
-  HNM_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+  // device-wide sync: never reads ctx->stream, which the ctx's owning thread may be switching
+  // (this entry is called across threads: the Python layer sums every thread's ctx)
+  HNM_HIP_CHECK(hipSetDevice(ctx->device));
+  HNM_HIP_CHECK(hipDeviceSynchronize());
   unsigned long long v[3];
   HNM_HIP_CHECK(hipMemcpy(v, ctx->stats_dev, sizeof(v), hipMemcpyDeviceToHost));
   for (int i = 0; i < 3; ++i) out[i] = (int64_t)v[i];

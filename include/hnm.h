@@ -74,9 +74,11 @@ hnm_status hnm_ctx_abort_pending(hnm_ctx* ctx);
 enum { HNM_OPT_PREFILTER = 1,
        HNM_OPT_STATS = 3       /* 1: count pre-filter candidates / fallback rows (diagnostics) */ };
 hnm_status hnm_ctx_set_option(hnm_ctx* ctx, int option, int64_t value);
-/* Pre-filter counters since the last reset (syncs; counted only while HNM_OPT_STATS is 1):
- * out[0] rows scored, out[1] candidates re-scored in fp32, out[2] rows that took the exact
- * fallback scan. */
+/* Pre-filter counters since the last reset (counted only while HNM_OPT_STATS is 1): out[0]
+ * rows scored, out[1] candidates re-scored in fp32, out[2] rows that took the exact fallback
+ * scan.  Synchronizes the whole DEVICE (not the ctx stream), so it may be called on a ctx
+ * another thread owns; counts of calls that thread issues while this runs may land before or
+ * after a reset (totals are exact for threads that are idle meanwhile). */
 hnm_status hnm_ctx_prefilter_stats(hnm_ctx* ctx, int64_t* out, int reset);
 /* Dominant-kernel timer: while on, calls record HIP events on the ctx stream around their
  * main kernel; `mask` selects the class: 1 = the scoring / scan kernel of every top-K or

@@ -7,9 +7,10 @@ The reference goldens (tests/golden/lightgcn_*.npz) pin `oracle/torch_cpu.lightg
 that CPU propagation runs on the full graph and is compared with the HIP SpMM path on
 sampled rows:
 
-* 48 random users, the 4 highest-degree users, and 16 item rows above the SpMM's
-  HEAVY = 2048 entries (segment + finish kernels on the side stream) -- including the 4
-  most popular items and the 4 shortest heavy rows -- within 1e-4 of the row scale;
+* 48 random users and the 4 highest-degree users (short rows: the column-ordered short walk,
+  spmm_swalk_kernel), and 16 item rows of more than 2,048 entries (the user-ordered walk,
+  split into pieces summed by spmm_walk_finish_kernel) -- including the 4 most popular items
+  and the 4 shortest of those rows -- within 1e-4 of the row scale;
 * the top-12 of every sampled user against the CPU's dense F_U[u] @ F_I^T scores
   (identical sets up to near-ties at the 12th, scores within 1e-4);
 * `propagate_for` (what recommend() and the bench step run) bit-identical to forward().

@@ -385,8 +385,9 @@ def test_row_topk_small_batch_split(B, k):
 @pytest.mark.parametrize("alpha,d", [(None, 64), (0.5, 128)])
 def test_lightgcn_propagate_for_equals_forward(alpha, d):
     """The batch-restricted propagation (last layer on item rows + the listed users only)
-    returns exactly forward()'s rows, bit for bit, on the full H&M graph (power-law item
-    rows on the segmented path, duplicate and out-of-batch users)."""
+    returns exactly forward()'s rows, bit for bit, on the full H&M graph (short user rows in
+    the short walk's sorted order, power-law item rows in the walk's piece order, duplicate
+    and out-of-batch users)."""
     U, I, E = syn.HM_USERS, syn.HM_ITEMS, syn.HM_INTERACTIONS
     m = LightGCN(U, I, d, alpha=alpha)
     m.set_graph(torch.from_numpy(syn.bipartite_edge_index(U, I, E, seed=2)))
@@ -401,9 +402,10 @@ def test_lightgcn_propagate_for_equals_forward(alpha, d):
 
 
 def test_lightgcn_propagation_on_other_streams_bitwise():
-    """The SpMM forks its heavy rows onto the ctx's side stream and joins back: forward() on
-    a non-default torch stream, and again on the default one after it, returns the default
-    stream's tables bit for bit (full H&M graph: the segmented heavy-row path is live)."""
+    """forward() on a non-default torch stream, and again on the default one after it, returns
+    the default stream's tables bit for bit (full H&M graph: both walks and the split-row
+    finish run on the ctx stream, which follows torch's current stream; the ctx switches
+    streams by an event, so the second call waits for the first's kernels)."""
     U, I, E = syn.HM_USERS, syn.HM_ITEMS, syn.HM_INTERACTIONS
     m = LightGCN(U, I, 64)
     m.set_graph(torch.from_numpy(syn.bipartite_edge_index(U, I, E, seed=2)))
@@ -498,9 +500,9 @@ def test_spmm_walk_rows(d):
 
 @pytest.mark.parametrize("d", [64, 128])
 def test_lightgcn_propagate_for_heavy_user_rows_bitwise(d):
-    """Listed users whose rows exceed the SpMM's HEAVY = 2048 entries (segmented path in
-    forward(): SEG-long partials + the finish kernel's slice tree) come back from
-    propagate_for bit-identical to forward(): rows_combine sums them in the plan's order.
+    """Listed users whose rows exceed 128 / 2,048 entries (the user-ordered walk in forward():
+    split into pieces, partials + the finish kernel's slice tree) come back from propagate_for
+    bit-identical to forward(): rows_combine sums them in the plan's order.
     Row lengths include the self-loop: 2047 edges -> 2048 entries (light), 2048 -> 2049
     (heavy, one extra segment), 5000, 40000 (20 segments: more than the 16 / 8 slices)."""
     U, I = 3000, 50_000

@@ -4,7 +4,10 @@
 set -uo pipefail
 OUT=gpurun_out/$1; K=$2; shift 2
 mkdir -p $OUT
-if [ "$K" != "-" ]; then
+if [ "$K" = "all" ]; then
+  timeout -k 10 1000 python -u -m pytest tests -v -m gpu --timeout 300 --timeout-method thread > $OUT/tests.out 2>&1
+  echo "tests rc=$?"; grep -E "FAILED|ERROR" $OUT/tests.out | head -30; tail -3 $OUT/tests.out
+elif [ "$K" != "-" ]; then
   timeout -k 10 900 python -u -m pytest tests -x -v -m gpu -k "$K" --timeout 300 --timeout-method thread > $OUT/tests.out 2>&1 || { echo "tests failed"; grep -E "FAILED|Error|error" $OUT/tests.out | head -20; tail -40 $OUT/tests.out; exit 1; }
   tail -3 $OUT/tests.out
 fi
