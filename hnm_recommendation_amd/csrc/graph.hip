@@ -63,8 +63,12 @@
 #ifndef WALK_WIN
 #define WALK_WIN 16
 #endif
+#ifndef WALK_LDS_F4
 #define WALK_LDS_F4 9216        // 144 KiB of float4 row accumulators per workgroup
+#endif
+#ifndef WALK_GROUPS_TARGET
 #define WALK_GROUPS_TARGET 16384  // total LPR-lane groups of a big graph's walk (all d)
+#endif
 // Round 4: the short rows (<= SPMM_SHORT entries: every user row) by a column-ordered walk too
 // (spmm_swalk_kernel): blocks of consecutive rows hold their accumulators in LDS and every
 // lane group walks its rows' entries merged in column order, so the chip's gathers move through
@@ -72,13 +76,45 @@
 #ifndef SPMM_SWALK
 #define SPMM_SWALK 1
 #endif
+// SPMM_SWALK 2: the short rows one lane group each, their entries in (col, position) order,
+// the most gathered rows of X (by count over the short rows' entries) held in LDS for the whole
+// launch (spmm_short_hot_kernel); 1: the column-ordered short walk; 0: CSR order (round 3)
+#ifndef SHORT_HOT_F4
+#define SHORT_HOT_F4 10112     // 158 KiB of hot rows per workgroup (one 1024-thread group / CU)
+#endif
+#ifndef SHORT_HOT_WG
+#define SHORT_HOT_WG 1         // workgroups per CU (SHORT_HOT_F4 x 16 B x SHORT_HOT_WG <= 160 KiB)
+#endif
 // column windows of the short walk (1: none; a barrier after each window otherwise)
 #ifndef SWALK_WIN
 #define SWALK_WIN 1
 #endif
-// persistent short-walk workgroups per CU
+// persistent short-walk workgroups per CU, their threads and LDS accumulators (float4)
 #ifndef SWALK_WG_PER_CU
-#define SWALK_WG_PER_CU 1
+#define SWALK_WG_PER_CU 2
+#endif
+#ifndef SWALK_THREADS
+#define SWALK_THREADS 512
+#endif
+#ifndef SWALK_LDS_F4
+#define SWALK_LDS_F4 4608
+#endif
+// entries per list step (gathers in flight per lane group) and the records' prefetch a step
+// ahead (0: loaded at the step, right before their gathers)
+#ifndef SWALK_STEP
+#define SWALK_STEP 8
+#endif
+#ifndef SWALK_PF
+#define SWALK_PF 1
+#endif
+// bipartite graphs: the short rows of the side that gathers the larger table join the walk
+#ifndef SPMM_SIDE_WALK
+#define SPMM_SIDE_WALK 1
+#endif
+// with the short walk off: 1 = one short row per lane group (spmm_mixed_kernel), 2 = two rows
+// per group with interleaved loads (spmm_short2_kernel)
+#ifndef SPMM_SHORT_ILP
+#define SPMM_SHORT_ILP 1
 #endif
 
 struct WalkSched;
@@ -120,6 +156,7 @@ struct hnm_spmm_plan {
   std::mutex* mu;       // lazy preparation (first call with col/val, first call per d)
   WalkSched* sched[7];  // per d = 4 << i
   ShortSched* ssched[7];
+  struct HotSched* hsched[7];
 };
 
 // ------------------------------------------------------------------ CSR build kernels
@@ -437,6 +474,94 @@ __device__ __forceinline__ float4 row_sum_grouped(const int32_t* __restrict__ co
   return acc;
 }
 
+// Two short rows per lane group with their loads interleaved (8 gathers in flight per group
+// instead of 4); each row is still one fma chain over its entries in order, bitwise
+// row_sum_grouped's value (SPMM_SHORT_ILP = 2 with the short walk off).
+template <int LPR>
+__device__ __forceinline__ void row_sum_grouped2(const int32_t* __restrict__ col,
+                                                 const float* __restrict__ val,
+                                                 const float* __restrict__ X, int d, int64_t pa,
+                                                 int64_t ea, int64_t pb, int64_t eb, int sub,
+                                                 float4& ya, float4& yb) {
+  float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a;
+  auto fma4 = [](float4& acc, float w, const float4& x) {
+    acc.x = fmaf(w, x.x, acc.x);
+    acc.y = fmaf(w, x.y, acc.y);
+    acc.z = fmaf(w, x.z, acc.z);
+    acc.w = fmaf(w, x.w, acc.w);
+  };
+  for (; pa + 3 < ea && pb + 3 < eb; pa += 4, pb += 4) {
+    int c[8];
+    float w[8];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      c[u] = col[pa + u];
+      w[u] = val[pa + u];
+      c[4 + u] = col[pb + u];
+      w[4 + u] = val[pb + u];
+    }
+    float4 x[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) x[u] = *reinterpret_cast<const float4*>(X + (int64_t)c[u] * d + 4 * sub);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) fma4(a, w[u], x[u]);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) fma4(b, w[4 + u], x[4 + u]);
+  }
+  auto tail = [&](float4& acc, int64_t p, int64_t e) {
+    for (; p + 3 < e; p += 4) {
+      int c[4];
+      float w[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        c[u] = col[p + u];
+        w[u] = val[p + u];
+      }
+      float4 x[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) x[u] = *reinterpret_cast<const float4*>(X + (int64_t)c[u] * d + 4 * sub);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) fma4(acc, w[u], x[u]);
+    }
+    for (; p < e; ++p) {
+      const float4 x = *reinterpret_cast<const float4*>(X + (int64_t)col[p] * d + 4 * sub);
+      fma4(acc, val[p], x);
+    }
+  };
+  tail(a, pa, ea);
+  tail(b, pb, eb);
+  ya = a;
+  yb = b;
+}
+
+template <int LPR>
+__global__ __launch_bounds__(256) void spmm_short2_kernel(int64_t r0, int64_t r1,
+                                                          const int64_t* __restrict__ rowptr,
+                                                          const int32_t* __restrict__ col,
+                                                          const float* __restrict__ val,
+                                                          const float* __restrict__ X, int d,
+                                                          SpmmEpi ep) {
+  constexpr int RPW = 64 / LPR;
+  const int lane = threadIdx.x & 63, sub = lane % LPR;
+  const int64_t ra = r0 + ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 2 * RPW + lane / LPR;
+  const int64_t rb = ra + RPW;
+  int64_t sa = 0, ea = 0, sb = 0, eb = 0;
+  if (ra < r1) {
+    sa = rowptr[ra];
+    ea = rowptr[ra + 1];
+    if (ea - sa > SPMM_SHORT) ea = sa;  // walk row: not ours
+  }
+  if (rb < r1) {
+    sb = rowptr[rb];
+    eb = rowptr[rb + 1];
+    if (eb - sb > SPMM_SHORT) eb = sb;
+  }
+  float4 ya, yb;
+  row_sum_grouped2<LPR>(col, val, X, d, sa, ea, sb, eb, sub, ya, yb);
+  if (ra < r1 && rowptr[ra + 1] - rowptr[ra] <= SPMM_SHORT) spmm_epilogue(ra, d, sub, ya, X, ep);
+  if (rb < r1 && rowptr[rb + 1] - rowptr[rb] <= SPMM_SHORT) spmm_epilogue(rb, d, sub, yb, X, ep);
+}
+
 // One launch for the light rows of [r0, r1): blocks [0, nlb) take the long rows listed in
 // long_rows[l0, l1) (one wave per row, the light kernel's order; first, so the longest work
 // starts first), the other blocks the short rows (one LPR-lane group per row), skipping rows
@@ -619,54 +744,182 @@ __global__ __launch_bounds__(WALK_THREADS) void spmm_walk_kernel(
 // Order: row r's value is one fma chain from 0 over its entries sorted by (col, CSR position)
 // -- rows_combine repeats it over the plan's sorted copy (row_sum_grouped on scol / sval).
 template <int LPR>
-__global__ __launch_bounds__(WALK_THREADS) void spmm_swalk_kernel(
+__global__ __launch_bounds__(SWALK_THREADS) void spmm_swalk_kernel(
     const int64_t* __restrict__ gptr, const uint32_t* __restrict__ ent,
     const float* __restrict__ wt, const int32_t* __restrict__ srow,
     const int32_t* __restrict__ nslot, int S, const float* __restrict__ X, int d, SpmmEpi ep,
     int64_t r0, int64_t r1, int64_t b0, int64_t b1) {
-  constexpr int NG = WALK_THREADS / LPR;
+  constexpr int NG = SWALK_THREADS / LPR;
   constexpr int K = SWALK_WIN > 1 ? SWALK_WIN : 1;
-  __shared__ float4 acc[WALK_LDS_F4];
+  constexpr int ST = SWALK_STEP;
+  __shared__ float4 acc[SWALK_LDS_F4];
   const int tid = threadIdx.x, g = tid / LPR, sub = tid % LPR;
-  for (int i = tid; i < WALK_LDS_F4; i += WALK_THREADS) acc[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int i = tid; i < SWALK_LDS_F4; i += SWALK_THREADS) acc[i] = make_float4(0.f, 0.f, 0.f, 0.f);
   __syncthreads();
+  auto consume = [&](const uint32_t* c, const float* w) {
+    float4 x[ST];
+#pragma unroll
+    for (int u = 0; u < ST; ++u)
+      x[u] = *reinterpret_cast<const float4*>(X + (int64_t)(c[u] >> 10) * d + 4 * sub);
+#pragma unroll
+    for (int u = 0; u < ST; ++u) {  // list order: a slot's entries stay one fma chain
+      float4* a = &acc[(c[u] & 1023u) * LPR + sub];
+      float4 v = *a;
+      v.x = fmaf(w[u], x[u].x, v.x);
+      v.y = fmaf(w[u], x[u].y, v.y);
+      v.z = fmaf(w[u], x[u].z, v.z);
+      v.w = fmaf(w[u], x[u].w, v.w);
+      *a = v;
+    }
+  };
   for (int64_t b = b0 + blockIdx.x; b < b1; b += gridDim.x) {
     for (int k = 0; k < K; ++k) {
       int64_t p = gptr[(b * NG + g) * K + k];
-      const int64_t e = gptr[(b * NG + g) * K + k + 1];
-      for (; p + 3 < e; p += 4) {  // lists are padded to multiples of 4
-        uint32_t c[4];
-        float w[4];
+      const int64_t e = gptr[(b * NG + g) * K + k + 1];  // lists are padded to multiples of ST
+      if (SWALK_PF) {
+        uint32_t c[ST], cn[ST];
+        float w[ST], wn[ST];
+        if (p < e) {
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          c[u] = ent[p + u];
-          w[u] = wt[p + u];
+          for (int u = 0; u < ST; ++u) {
+            cn[u] = ent[p + u];
+            wn[u] = wt[p + u];
+          }
         }
-        float4 x[4];
+        for (; p < e; p += ST) {
 #pragma unroll
-        for (int u = 0; u < 4; ++u)
-          x[u] = *reinterpret_cast<const float4*>(X + (int64_t)(c[u] >> 10) * d + 4 * sub);
+          for (int u = 0; u < ST; ++u) {
+            c[u] = cn[u];
+            w[u] = wn[u];
+          }
+          if (p + ST < e) {
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {  // list order: a slot's entries stay one fma chain
-          float4* a = &acc[(c[u] & 1023u) * LPR + sub];
-          float4 v = *a;
-          v.x = fmaf(w[u], x[u].x, v.x);
-          v.y = fmaf(w[u], x[u].y, v.y);
-          v.z = fmaf(w[u], x[u].z, v.z);
-          v.w = fmaf(w[u], x[u].w, v.w);
-          *a = v;
+            for (int u = 0; u < ST; ++u) {
+              cn[u] = ent[p + ST + u];
+              wn[u] = wt[p + ST + u];
+            }
+          }
+          consume(c, w);
+        }
+      } else {
+        for (; p < e; p += ST) {
+          uint32_t c[ST];
+          float w[ST];
+#pragma unroll
+          for (int u = 0; u < ST; ++u) {
+            c[u] = ent[p + u];
+            w[u] = wt[p + u];
+          }
+          consume(c, w);
         }
       }
       if (K > 1) __syncthreads();
     }
     __syncthreads();
     const int ns = nslot[b];
-    for (int i = tid; i < ns * LPR; i += WALK_THREADS) {
+    for (int i = tid; i < ns * LPR; i += SWALK_THREADS) {
       const int64_t r = srow[b * S + i / LPR];
       if (r >= r0 && r < r1) spmm_epilogue(r, d, i % LPR, acc[i], X, ep);
       acc[i] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
     __syncthreads();
+  }
+}
+
+// ------------------------------------------------------------- hot-row short kernel
+// SPMM_SWALK 2.  The short rows (every user row: ~24 entries into the 27 MB item table) gather a
+// power-law table: with H&M's popularity the 600 most gathered item rows take ~40 % of the
+// user half's gathers.  A persistent workgroup per CU copies those H rows of X into LDS once
+// per launch (X is read-only during a layer) and then takes short rows grid-stride, one
+// LPR-lane group per row: each entry is a record ecol = col, or HOT | hot slot for a row held
+// in LDS, and val, in the row's (col, CSR position) order -- one fma chain from 0, the value
+// rows_combine computes from the sorted copy (row_sum_grouped on scol / sval).
+#define SPMM_HOT_BIT 0x80000000u
+template <int LPR, bool BUF>
+__global__ __launch_bounds__(1024) void spmm_short_hot_kernel(
+    const int32_t* __restrict__ rows, const uint2* __restrict__ span, int64_t q0, int64_t q1,
+    const uint32_t* __restrict__ ecol, const float* __restrict__ sval,
+    const int32_t* __restrict__ hot_rows, int H, const float* __restrict__ X, int xbytes, int d,
+    SpmmEpi ep, int64_t r0, int64_t r1) {
+  constexpr int NGB = 1024 / LPR;
+  __shared__ float4 hot[SHORT_HOT_F4];
+  const int tid = threadIdx.x, g = tid / LPR, sub = tid % LPR;
+  // hot rows into LDS, 8 rows' loads in flight per thread (a serial loop waits per row)
+  for (int i0 = 0; i0 < H * LPR; i0 += 8 * 1024) {
+    int64_t src[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int i = i0 + u * 1024 + tid;
+      src[u] = i < H * LPR ? (int64_t)hot_rows[i / LPR] * d + 4 * (i % LPR) : -1;
+    }
+    float4 v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      v[u] = src[u] >= 0 ? *reinterpret_cast<const float4*>(X + src[u]) : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int i = i0 + u * 1024 + tid;
+      if (i < H * LPR) hot[i] = v[u];
+    }
+  }
+  __syncthreads();
+  // every entry issues one buffer load of X (a hot entry's offset is out of range: the load
+  // returns 0 without touching memory) and one LDS read of the hot rows (hot slot 0 for a cold
+  // entry), then selects -- no divergent branch, and no generic (flat) loads the compiler would
+  // otherwise form from a select of the two pointers (flat loads wait on both counters)
+  const __amdgpu_buffer_rsrc_t xr =
+      __builtin_amdgcn_make_buffer_rsrc((void*)X, 0, BUF ? xbytes : 0, 0x00020000);
+  auto fetch = [&](uint32_t c) -> float4 {
+    if (!BUF)  // X past a buffer resource's 2 GB range: no hot rows (H = 0), plain gathers
+      return *reinterpret_cast<const float4*>(X + (int64_t)c * d + 4 * sub);
+    const bool h = (c & SPMM_HOT_BIT) != 0;
+    const int off = h ? (int)0x80000000 : (int)(c * (uint32_t)d * 4u + 16u * sub);
+    const float4 xg = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0));
+    const float4 xl = hot[(h ? (c & ~SPMM_HOT_BIT) : 0u) * LPR + sub];
+    return h ? xl : xg;
+  };
+  const int64_t qs = (int64_t)gridDim.x * NGB;
+  int64_t q = q0 + (int64_t)blockIdx.x * NGB + g;
+  // the next row's id and entry span load while this row's entries are gathered (span = the
+  // row's [start, end) in the CSR, precomputed: no dependent rowptr load per row)
+  int64_t nr = q < q1 ? rows[q] : 0;
+  uint2 nsp = q < q1 ? span[q] : make_uint2(0u, 0u);
+  for (; q < q1; q += qs) {
+    const int64_t r = nr, s = nsp.x, e = nsp.y;
+    if (q + qs < q1) {
+      nr = rows[q + qs];
+      nsp = span[q + qs];
+    }
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    int64_t p = s;
+    for (; p + 3 < e; p += 4) {
+      uint32_t c[4];
+      float w[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        c[u] = ecol[p + u];
+        w[u] = sval[p + u];
+      }
+      float4 x[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) x[u] = fetch(c[u]);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        acc.x = fmaf(w[u], x[u].x, acc.x);
+        acc.y = fmaf(w[u], x[u].y, acc.y);
+        acc.z = fmaf(w[u], x[u].z, acc.z);
+        acc.w = fmaf(w[u], x[u].w, acc.w);
+      }
+    }
+    for (; p < e; ++p) {
+      const float w = sval[p];
+      const float4 x = fetch(ecol[p]);
+      acc.x = fmaf(w, x.x, acc.x);
+      acc.y = fmaf(w, x.y, acc.y);
+      acc.z = fmaf(w, x.z, acc.z);
+      acc.w = fmaf(w, x.w, acc.w);
+    }
+    if (r >= r0 && r < r1) spmm_epilogue(r, d, sub, acc, X, ep);
   }
 }
 
@@ -1001,6 +1254,57 @@ static hnm_status upload(T** dst, const T* src, size_t n) {
   return HNM_OK;
 }
 
+// A bipartite graph stored with contiguous sides -- rows [0, S) connected only to [S, N) and
+// back, self-loops aside (the reference's user / item layout, lightgcn.py:81-112) -- has one
+// side whose rows all gather the OTHER side's table.  The short walk suits the side that gathers
+// the smaller table (users: the 27 MB item table at d = 64); the short rows of the side that
+// gathers the larger table (the tail items, < 129 entries into the 351 MB user table) join the
+// user-ordered walk instead, where their gathers ride the same column sweep as the long item
+// rows.  A short row is one piece there, so its value is the same sorted-order fma chain
+// either way (rows_combine is unchanged).  Called once at binding, before any schedule.
+static void plan_bipartite_sides(hnm_spmm_plan* pl) {
+  const std::vector<int64_t>& rp = *pl->h_rowptr;
+  const std::vector<int32_t>& hc = *pl->h_scol;
+  const int64_t N = pl->N;
+  // S = row 0's smallest neighbour other than itself
+  int64_t S = -1;
+  for (int64_t q = rp[0]; q < rp[1]; ++q)
+    if (hc[q] != 0) {
+      S = hc[q];
+      break;
+    }
+  if (S <= 0 || S >= N) return;
+  std::vector<char> ok((size_t)hnm_cdiv(N, 4096), 1);
+  parallel_for((int64_t)ok.size(), [&](int64_t ch) {
+    const int64_t r1 = std::min<int64_t>(N, (ch + 1) * 4096);
+    for (int64_t r = ch * 4096; r < r1 && ok[ch]; ++r)
+      for (int64_t q = rp[r]; q < rp[r + 1]; ++q) {
+        const int64_t c = hc[q];
+        if (c != r && ((r < S) == (c < S))) {
+          ok[ch] = 0;
+          break;
+        }
+      }
+  });
+  for (char v : ok)
+    if (!v) return;
+  // the side whose neighbours form the larger table moves its short rows into the walk
+  const bool upper = S > N - S;  // rows [S, N) gather the S-row table
+  const int64_t lo = upper ? S : 0, hi = upper ? N : S;
+  std::vector<int32_t>& sr = *pl->h_short_rows;
+  std::vector<int32_t>& wr = *pl->h_walk_rows;
+  std::vector<int32_t> keep, moved;
+  for (int32_t r : sr) (r >= lo && r < hi && rp[r + 1] > rp[r] ? moved : keep).push_back(r);
+  if (moved.empty() || keep.empty()) return;
+  std::vector<int32_t> merged((size_t)(wr.size() + moved.size()));
+  std::merge(wr.begin(), wr.end(), moved.begin(), moved.end(), merged.begin());
+  for (int32_t r : moved) pl->walk_nnz += rp[r + 1] - rp[r];
+  wr.swap(merged);
+  sr.swap(keep);
+  pl->n_walk = (int64_t)wr.size();
+  pl->walk_cap = std::max<int64_t>(512, hnm_cdiv(pl->walk_nnz, 2 * WALK_GROUPS_TARGET));
+}
+
 // Binds the plan to col / val on first use.  A walk plan then copies the CSR to the host,
 // stable-sorts every row's entries by column (the walks' summation order: (col, CSR position))
 // and uploads the sorted copy (rows_combine repeats the walks' order from it).  Later calls
@@ -1043,6 +1347,7 @@ static hnm_status plan_bind(hnm_ctx* ctx, hnm_spmm_plan* pl, const int32_t* col,
     hnm_status st;
     if ((st = upload(&pl->scol, hc.data(), (size_t)T)) || (st = upload(&pl->sval, hv.data(), (size_t)T)))
       return st;
+    if (SPMM_SIDE_WALK && pl->swalk) plan_bipartite_sides(pl);
   }
   pl->bound_col = col;
   pl->bound_val = val;
@@ -1189,8 +1494,8 @@ static hnm_status walk_build(hnm_spmm_plan* pl, int d, WalkSched** out) {
 // spare slot S.  The placement only moves rows between lanes; each row's chain order is its
 // sorted entries' order.
 static hnm_status swalk_build(hnm_spmm_plan* pl, int d, ShortSched** out) {
-  const int lpr = d / 4, ng = WALK_THREADS / lpr;
-  const int S = std::min(1022, WALK_LDS_F4 / lpr - 1);
+  const int lpr = d / 4, ng = SWALK_THREADS / lpr;
+  const int S = std::min(1022, SWALK_LDS_F4 / lpr - 1);
   const std::vector<int64_t>& rp = *pl->h_rowptr;
   const std::vector<int32_t>& sr = *pl->h_short_rows;
   const std::vector<int32_t>& hc = *pl->h_scol;
@@ -1258,7 +1563,8 @@ static hnm_status swalk_build(hnm_spmm_plan* pl, int d, ShortSched** out) {
     }
   });
   std::vector<int64_t> gptr((size_t)(nb * ng * K + 1), 0);
-  for (int64_t i = 0; i < nb * ng * K; ++i) gptr[i + 1] = gptr[i] + hnm_cdiv(wcnt[i], 4) * 4;
+  for (int64_t i = 0; i < nb * ng * K; ++i)
+    gptr[i + 1] = gptr[i] + hnm_cdiv(wcnt[i], SWALK_STEP) * SWALK_STEP;
   const int64_t Tp = gptr.back();
   std::vector<uint32_t> ent((size_t)Tp, (uint32_t)S);
   std::vector<float> wt((size_t)Tp, 0.f);
@@ -1319,6 +1625,75 @@ static hnm_status swalk_build(hnm_spmm_plan* pl, int d, ShortSched** out) {
   return HNM_OK;
 }
 
+// hot-row short kernel (SPMM_SWALK 2): per d the H most gathered rows and the records
+struct HotSched {
+  int H;
+  int32_t* hot_rows;   // [H]
+  uint32_t* ecol;      // [nnz] CSR layout, short rows only: col or HOT | slot, sorted order
+  int32_t* rows;       // [n_short] the short rows, ascending
+  uint2* span;         // [n_short] each short row's [start, end) in the CSR (nnz < 2^32)
+  int64_t n;
+};
+
+static void hot_sched_free(HotSched* h) {
+  if (!h) return;
+  (void)hipFree(h->hot_rows);
+  (void)hipFree(h->ecol);
+  (void)hipFree(h->rows);
+  (void)hipFree(h->span);
+  delete h;
+}
+
+static hnm_status hot_build(hnm_spmm_plan* pl, int d, HotSched** out) {
+  const int lpr = d / 4;
+  const std::vector<int64_t>& rp = *pl->h_rowptr;
+  const std::vector<int32_t>& sr = *pl->h_short_rows;
+  const std::vector<int32_t>& hc = *pl->h_scol;
+  const int64_t N = pl->N;
+  // hot rows are read through a buffer resource over X: 32-bit byte offsets
+  const int Hmax = N * d * 4 <= (int64_t)INT32_MAX - 16 ? SHORT_HOT_F4 / lpr : 0;
+  std::vector<int64_t> cnt((size_t)N, 0);
+  for (int32_t r : sr)
+    for (int64_t q = rp[r]; q < rp[r + 1]; ++q) ++cnt[hc[q]];
+  std::vector<int32_t> order;
+  for (int64_t c = 0; c < N; ++c)
+    if (cnt[c] > 1) order.push_back((int32_t)c);
+  const int H = (int)std::min<int64_t>(Hmax, (int64_t)order.size());
+  std::partial_sort(order.begin(), order.begin() + H, order.end(),
+                    [&](int32_t a, int32_t b) { return cnt[a] > cnt[b] || (cnt[a] == cnt[b] && a < b); });
+  order.resize((size_t)H);
+  std::sort(order.begin(), order.end());  // hot slots in column order
+  std::vector<int32_t> slot((size_t)N, -1);
+  for (int i = 0; i < H; ++i) slot[order[i]] = i;
+  std::vector<uint32_t> ecol((size_t)pl->nnz, 0u);
+  parallel_for((int64_t)sr.size(), [&](int64_t i) {
+    const int32_t r = sr[i];
+    for (int64_t q = rp[r]; q < rp[r + 1]; ++q) {
+      const int32_t c = hc[q];
+      ecol[q] = slot[c] >= 0 ? (SPMM_HOT_BIT | (uint32_t)slot[c]) : (uint32_t)c;
+    }
+  });
+  std::vector<uint2> span(sr.size());
+  for (size_t i = 0; i < sr.size(); ++i) span[i] = make_uint2((unsigned)rp[sr[i]], (unsigned)rp[sr[i] + 1]);
+  HotSched* h = new HotSched();
+  h->H = H;
+  h->n = (int64_t)sr.size();
+  h->hot_rows = nullptr;
+  h->ecol = nullptr;
+  h->rows = nullptr;
+  h->span = nullptr;
+  hnm_status st;
+  if ((st = upload(&h->hot_rows, order.data(), order.size())) ||
+      (st = upload(&h->ecol, ecol.data(), ecol.size())) ||
+      (st = upload(&h->rows, sr.data(), sr.size())) ||
+      (st = upload(&h->span, span.data(), span.size()))) {
+    hot_sched_free(h);
+    return st;
+  }
+  *out = h;
+  return HNM_OK;
+}
+
 static int walk_index(int d) {
   int i = 0;
   while ((4 << i) < d) ++i;
@@ -1334,7 +1709,7 @@ static bool spmm_d_ok(int d) {
 // Binding + the walk schedules for d, built on first use (one-time, host work with stream syncs).
 static hnm_status walk_get(hnm_ctx* ctx, const hnm_spmm_plan* cpl, const int32_t* col,
                            const float* val, int d, const WalkSched** out,
-                           const ShortSched** sout) {
+                           const ShortSched** sout, const HotSched** hout = nullptr) {
   hnm_spmm_plan* pl = const_cast<hnm_spmm_plan*>(cpl);
   std::lock_guard<std::mutex> lk(*pl->mu);
   hnm_status s = plan_bind(ctx, pl, col, val);
@@ -1342,9 +1717,11 @@ static hnm_status walk_get(hnm_ctx* ctx, const hnm_spmm_plan* cpl, const int32_t
   if (!pl->walk || d <= 0) return HNM_OK;
   const int i = walk_index(d);
   if (!pl->sched[i] && (s = walk_build(pl, d, &pl->sched[i]))) return s;
-  if (pl->swalk && !pl->ssched[i] && (s = swalk_build(pl, d, &pl->ssched[i]))) return s;
+  if (pl->swalk == 1 && !pl->ssched[i] && (s = swalk_build(pl, d, &pl->ssched[i]))) return s;
+  if (pl->swalk == 2 && !pl->hsched[i] && (s = hot_build(pl, d, &pl->hsched[i]))) return s;
   if (out) *out = pl->sched[i];
   if (sout) *sout = pl->ssched[i];
+  if (hout) *hout = pl->hsched[i];
   return HNM_OK;
 }
 
@@ -1385,7 +1762,8 @@ extern "C" hnm_status hnm_spmm_plan_create(hnm_ctx* ctx, int64_t N, const int64_
   pl->h_long = new std::vector<int32_t>(lrows);
   pl->mu = new std::mutex();
   // walk rows: every row of more than SPMM_SHORT entries (col << 10 must fit 32 bits)
-  pl->walk = SPMM_WALK && SPMM_GROUPED && N <= (int64_t)1 << 22 && rp[0] == 0;
+  pl->walk = SPMM_WALK && SPMM_GROUPED && N <= (int64_t)1 << 22 && rp[0] == 0 &&
+             rp[N] < ((int64_t)1 << 32);
   if (pl->walk) {
     std::vector<int32_t> wr, sr;
     int64_t wn = 0;
@@ -1406,7 +1784,7 @@ extern "C" hnm_status hnm_spmm_plan_create(hnm_ctx* ctx, int64_t N, const int64_
     pl->h_walk_rows = new std::vector<int32_t>(wr);
     pl->h_short_rows = new std::vector<int32_t>(sr);
     pl->h_rowptr = new std::vector<int64_t>(std::move(rp));
-    pl->swalk = SPMM_SWALK && !sr.empty();
+    pl->swalk = sr.empty() ? 0 : SPMM_SWALK;
   }
   if (pl->n_long > 0) {
     if (hipMalloc((void**)&pl->long_rows, pl->n_long * 4) != hipSuccess) {
@@ -1454,6 +1832,7 @@ extern "C" hnm_status hnm_spmm_plan_destroy(hnm_spmm_plan* pl) {
   if (pl->long_rows) (void)hipFree(pl->long_rows);
   for (WalkSched* w : pl->sched) walk_sched_free(w);
   for (ShortSched* w : pl->ssched) short_sched_free(w);
+  for (HotSched* w : pl->hsched) hot_sched_free(w);
   if (pl->scol) (void)hipFree(pl->scol);
   if (pl->sval) (void)hipFree(pl->sval);
   delete pl->h_walk_rows;
@@ -1486,7 +1865,8 @@ static hnm_status spmm_launch(hnm_ctx* ctx, const hnm_spmm_plan* pl, int64_t N,
     // user-ordered walk (+ the split rows' finish), one stream, disjoint output rows
     const WalkSched* ws = nullptr;
     const ShortSched* ss = nullptr;
-    hnm_status s = walk_get(ctx, pl, col, val, d, &ws, &ss);
+    const HotSched* hs = nullptr;
+    hnm_status s = walk_get(ctx, pl, col, val, d, &ws, &ss, &hs);
     if (s) return s;
     const std::vector<int32_t>& wr = *pl->h_walk_rows;
     const bool any = std::lower_bound(wr.begin(), wr.end(), (int32_t)std::min<int64_t>(r0, INT32_MAX)) !=
@@ -1503,6 +1883,25 @@ static hnm_status spmm_launch(hnm_ctx* ctx, const hnm_spmm_plan* pl, int64_t N,
     hipStream_t wst = fork ? ctx->side : ctx->stream;
     auto short_rows = [&]() -> hnm_status {
       if (r1 <= r0) return HNM_OK;
+      if (hs) {
+        const std::vector<int32_t>& sr = *pl->h_short_rows;
+        const int64_t q0 = std::lower_bound(sr.begin(), sr.end(), (int32_t)std::min<int64_t>(r0, INT32_MAX)) - sr.begin();
+        const int64_t q1 = std::lower_bound(sr.begin(), sr.end(), (int32_t)std::min<int64_t>(r1, INT32_MAX)) - sr.begin();
+        if (q1 > q0) {
+          const unsigned grid = (unsigned)std::min<int64_t>(hnm_cdiv(q1 - q0, 1024 / LPR),
+                                                            (int64_t)ctx->num_cus * SHORT_HOT_WG);
+          if (hs->H > 0)
+            hipLaunchKernelGGL((spmm_short_hot_kernel<LPR, true>), dim3(grid), dim3(1024), 0,
+                               ctx->stream, hs->rows, hs->span, q0, q1, hs->ecol, pl->sval,
+                               hs->hot_rows, hs->H, X, (int)(N * d * 4), d, ep, r0, r1);
+          else
+            hipLaunchKernelGGL((spmm_short_hot_kernel<LPR, false>), dim3(grid), dim3(1024), 0,
+                               ctx->stream, hs->rows, hs->span, q0, q1, hs->ecol, pl->sval,
+                               hs->hot_rows, 0, X, 0, d, ep, r0, r1);
+          HNM_LAUNCH_CHECK();
+        }
+        return HNM_OK;
+      }
       if (ss) {
         // blocks whose rows meet [r0, r1) (blocks are in ascending row order)
         const int64_t b0 = std::lower_bound(ss->last.begin(), ss->last.end(),
@@ -1511,17 +1910,23 @@ static hnm_status spmm_launch(hnm_ctx* ctx, const hnm_spmm_plan* pl, int64_t N,
                                             (int32_t)std::min<int64_t>(r1, INT32_MAX)) - ss->first.begin();
         if (b1 > b0) {
           const unsigned grid = (unsigned)std::min<int64_t>(b1 - b0, ss->nwg);
-          hipLaunchKernelGGL(spmm_swalk_kernel<LPR>, dim3(grid), dim3(WALK_THREADS), 0, ctx->stream,
+          hipLaunchKernelGGL(spmm_swalk_kernel<LPR>, dim3(grid), dim3(SWALK_THREADS), 0, ctx->stream,
                              ss->gptr, ss->ent, ss->wt, ss->srow, ss->nslot, ss->S, X, d, ep, r0, r1,
                              b0, b1);
           HNM_LAUNCH_CHECK();
         }
         return HNM_OK;
       }
-      hipLaunchKernelGGL(spmm_mixed_kernel<LPR>,
-                         dim3((unsigned)hnm_cdiv(r1 - r0, 4 * (64 / LPR))), dim3(256), 0,
-                         ctx->stream, r0, r1, pl->long_rows, (int64_t)0, (int64_t)0, (int64_t)0,
-                         rowptr, col, val, X, d, ep);
+      if (SPMM_SHORT_ILP == 2) {
+        hipLaunchKernelGGL(spmm_short2_kernel<LPR>,
+                           dim3((unsigned)hnm_cdiv(r1 - r0, 8 * (64 / LPR))), dim3(256), 0,
+                           ctx->stream, r0, r1, rowptr, col, val, X, d, ep);
+      } else {
+        hipLaunchKernelGGL(spmm_mixed_kernel<LPR>,
+                           dim3((unsigned)hnm_cdiv(r1 - r0, 4 * (64 / LPR))), dim3(256), 0,
+                           ctx->stream, r0, r1, pl->long_rows, (int64_t)0, (int64_t)0, (int64_t)0,
+                           rowptr, col, val, X, d, ep);
+      }
       HNM_LAUNCH_CHECK();
       return HNM_OK;
     };
@@ -1674,7 +2079,7 @@ extern "C" hnm_status hnm_spmm_rows_combine_f32(hnm_ctx* ctx, const hnm_spmm_pla
     if (s) return s;
     if (plan->walk) {
       co.mode = 2;
-      co.short_sorted = plan->swalk;
+      co.short_sorted = plan->swalk != 0;
       co.scol = plan->scol;
       co.sval = plan->sval;
       co.cap = plan->walk_cap;

@@ -146,3 +146,33 @@ def test_plan_bound_to_its_values():
     st = _lib.fn("hnm_spmm_plan_prepare")(c, g.plan, _lib.ptr(g.col), _lib.ptr(g.val), 48)
     assert st == _lib.HNM_EUNSUPPORTED
     torch.cuda.synchronize()
+
+
+def test_legacy_plan_above_walk_limit():
+    """Graphs of more than 2^22 nodes (the walks pack col << 10 into 32 bits) take the
+    round-2 classes: short rows one 16-lane group each, long rows one wave, rows over 2,048
+    entries in SEG-long segments + the finish tree, all in CSR order.  Checked at that size
+    against A_hat X in float64 (1e-5 of sum |a||x|), and propagate_for bitwise equal to
+    forward() there (rows_combine repeats each class's order: mode 1)."""
+    U, I, d = (1 << 22) + 3000, 4000, 16
+    base = syn.bipartite_edge_index(U, I, 2_000_000, seed=9)
+    hub = np.stack([np.arange(0, U, 997), np.zeros(len(range(0, U, 997)), np.int64) + U])
+    edges = np.concatenate([base, hub, hub[::-1]], axis=1)   # item 0: > 4,000 entries (heavy)
+    m = LightGCN(U, I, d)
+    m.set_graph(torch.from_numpy(edges))
+    m = m.to(DEV)
+    g = m._device_graph()
+    rp = g.rowptr.cpu().numpy()
+    L = np.diff(rp)
+    assert L.max() > 2048 and ((L > 128) & (L <= 2048)).any()
+    x = torch.randn(U + I, d, generator=torch.Generator().manual_seed(3)).to(DEV)
+    y = torch.empty_like(x)
+    g.spmm(x, y, 0.0, None)
+    torch.cuda.synchronize()
+    ref, mag = _dense_ref(g, x)
+    err = np.abs(y.double().cpu().numpy() - ref)
+    assert (err <= 1e-5 * mag + 1e-30).all(), float((err / (mag + 1e-30)).max())
+    users = torch.tensor([0, 997, 5, U - 1, 1 << 21], dtype=torch.int64, device=DEV)
+    fb, fi_b = m.propagate_for(users)
+    fu, fi = m.forward()
+    assert torch.equal(fi_b, fi) and torch.equal(fb, fu[users])
