@@ -163,7 +163,7 @@ def build_workload(name, rank, world, device, batch, exact=False, weights="init"
             world).recommend)(m.propagate(g))
         info["_full_step"] = full_step
         ret = dict(step=rec.recommend, per_launch=per_launch, bound="hbm",
-                   kernel="spmm layer (spmm_mixed short rows + spmm_walk rows + walk finish), whole-graph layers",
+                   kernel="spmm layer (spmm_swalk_kernel short rows + spmm_walk_kernel long rows + spmm_walk_finish_kernel), whole-graph layers",
                    timing=_lib.TIME_SPMM, gathered=g.nnz * d * 4.0)
         return ret, info, ("lightgcn", (sd, edges, d))
     elif name == "widedeep":

@@ -72,18 +72,13 @@
 // Round 4: the short rows (<= SPMM_SHORT entries: every user row) by a column-ordered walk too
 // (spmm_swalk_kernel): blocks of consecutive rows hold their accumulators in LDS and every
 // lane group walks its rows' entries merged in column order, so the chip's gathers move through
-// the item table together and an XCD's L2 serves them instead of the Infinity Cache.
+// the item table together (L2 hit rate 0.52 -> 0.64).  1 = on, 0 = one row per lane group in CSR
+// order (round 3).  Measured alternatives (A/B on one box, d = 64 layer, `git show a7c47dc`):
+// the mixed kernel with two rows per group interleaved 1.72 ms, the short rows one group each
+// with the ~600 most gathered item rows held in LDS (~40 % of the user half's gathers) 1.46-1.65
+// ms, vs 1.36 ms for this walk with 2 workgroups per CU, records a step ahead, 8 gathers a step.
 #ifndef SPMM_SWALK
 #define SPMM_SWALK 1
-#endif
-// SPMM_SWALK 2: the short rows one lane group each, their entries in (col, position) order,
-// the most gathered rows of X (by count over the short rows' entries) held in LDS for the whole
-// launch (spmm_short_hot_kernel); 1: the column-ordered short walk; 0: CSR order (round 3)
-#ifndef SHORT_HOT_F4
-#define SHORT_HOT_F4 10112     // 158 KiB of hot rows per workgroup (one 1024-thread group / CU)
-#endif
-#ifndef SHORT_HOT_WG
-#define SHORT_HOT_WG 1         // workgroups per CU (SHORT_HOT_F4 x 16 B x SHORT_HOT_WG <= 160 KiB)
 #endif
 // column windows of the short walk (1: none; a barrier after each window otherwise)
 #ifndef SWALK_WIN
@@ -110,11 +105,6 @@
 // bipartite graphs: the short rows of the side that gathers the larger table join the walk
 #ifndef SPMM_SIDE_WALK
 #define SPMM_SIDE_WALK 1
-#endif
-// with the short walk off: 1 = one short row per lane group (spmm_mixed_kernel), 2 = two rows
-// per group with interleaved loads (spmm_short2_kernel)
-#ifndef SPMM_SHORT_ILP
-#define SPMM_SHORT_ILP 1
 #endif
 
 struct WalkSched;
@@ -156,7 +146,6 @@ struct hnm_spmm_plan {
   std::mutex* mu;       // lazy preparation (first call with col/val, first call per d)
   WalkSched* sched[7];  // per d = 4 << i
   ShortSched* ssched[7];
-  struct HotSched* hsched[7];
 };
 
 // ------------------------------------------------------------------ CSR build kernels
@@ -474,94 +463,6 @@ __device__ __forceinline__ float4 row_sum_grouped(const int32_t* __restrict__ co
   return acc;
 }
 
-// Two short rows per lane group with their loads interleaved (8 gathers in flight per group
-// instead of 4); each row is still one fma chain over its entries in order, bitwise
-// row_sum_grouped's value (SPMM_SHORT_ILP = 2 with the short walk off).
-template <int LPR>
-__device__ __forceinline__ void row_sum_grouped2(const int32_t* __restrict__ col,
-                                                 const float* __restrict__ val,
-                                                 const float* __restrict__ X, int d, int64_t pa,
-                                                 int64_t ea, int64_t pb, int64_t eb, int sub,
-                                                 float4& ya, float4& yb) {
-  float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a;
-  auto fma4 = [](float4& acc, float w, const float4& x) {
-    acc.x = fmaf(w, x.x, acc.x);
-    acc.y = fmaf(w, x.y, acc.y);
-    acc.z = fmaf(w, x.z, acc.z);
-    acc.w = fmaf(w, x.w, acc.w);
-  };
-  for (; pa + 3 < ea && pb + 3 < eb; pa += 4, pb += 4) {
-    int c[8];
-    float w[8];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      c[u] = col[pa + u];
-      w[u] = val[pa + u];
-      c[4 + u] = col[pb + u];
-      w[4 + u] = val[pb + u];
-    }
-    float4 x[8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) x[u] = *reinterpret_cast<const float4*>(X + (int64_t)c[u] * d + 4 * sub);
-#pragma unroll
-    for (int u = 0; u < 4; ++u) fma4(a, w[u], x[u]);
-#pragma unroll
-    for (int u = 0; u < 4; ++u) fma4(b, w[4 + u], x[4 + u]);
-  }
-  auto tail = [&](float4& acc, int64_t p, int64_t e) {
-    for (; p + 3 < e; p += 4) {
-      int c[4];
-      float w[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        c[u] = col[p + u];
-        w[u] = val[p + u];
-      }
-      float4 x[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) x[u] = *reinterpret_cast<const float4*>(X + (int64_t)c[u] * d + 4 * sub);
-#pragma unroll
-      for (int u = 0; u < 4; ++u) fma4(acc, w[u], x[u]);
-    }
-    for (; p < e; ++p) {
-      const float4 x = *reinterpret_cast<const float4*>(X + (int64_t)col[p] * d + 4 * sub);
-      fma4(acc, val[p], x);
-    }
-  };
-  tail(a, pa, ea);
-  tail(b, pb, eb);
-  ya = a;
-  yb = b;
-}
-
-template <int LPR>
-__global__ __launch_bounds__(256) void spmm_short2_kernel(int64_t r0, int64_t r1,
-                                                          const int64_t* __restrict__ rowptr,
-                                                          const int32_t* __restrict__ col,
-                                                          const float* __restrict__ val,
-                                                          const float* __restrict__ X, int d,
-                                                          SpmmEpi ep) {
-  constexpr int RPW = 64 / LPR;
-  const int lane = threadIdx.x & 63, sub = lane % LPR;
-  const int64_t ra = r0 + ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 2 * RPW + lane / LPR;
-  const int64_t rb = ra + RPW;
-  int64_t sa = 0, ea = 0, sb = 0, eb = 0;
-  if (ra < r1) {
-    sa = rowptr[ra];
-    ea = rowptr[ra + 1];
-    if (ea - sa > SPMM_SHORT) ea = sa;  // walk row: not ours
-  }
-  if (rb < r1) {
-    sb = rowptr[rb];
-    eb = rowptr[rb + 1];
-    if (eb - sb > SPMM_SHORT) eb = sb;
-  }
-  float4 ya, yb;
-  row_sum_grouped2<LPR>(col, val, X, d, sa, ea, sb, eb, sub, ya, yb);
-  if (ra < r1 && rowptr[ra + 1] - rowptr[ra] <= SPMM_SHORT) spmm_epilogue(ra, d, sub, ya, X, ep);
-  if (rb < r1 && rowptr[rb + 1] - rowptr[rb] <= SPMM_SHORT) spmm_epilogue(rb, d, sub, yb, X, ep);
-}
-
 // One launch for the light rows of [r0, r1): blocks [0, nlb) take the long rows listed in
 // long_rows[l0, l1) (one wave per row, the light kernel's order; first, so the longest work
 // starts first), the other blocks the short rows (one LPR-lane group per row), skipping rows
@@ -823,103 +724,6 @@ __global__ __launch_bounds__(SWALK_THREADS) void spmm_swalk_kernel(
       acc[i] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
     __syncthreads();
-  }
-}
-
-// ------------------------------------------------------------- hot-row short kernel
-// SPMM_SWALK 2.  The short rows (every user row: ~24 entries into the 27 MB item table) gather a
-// power-law table: with H&M's popularity the 600 most gathered item rows take ~40 % of the
-// user half's gathers.  A persistent workgroup per CU copies those H rows of X into LDS once
-// per launch (X is read-only during a layer) and then takes short rows grid-stride, one
-// LPR-lane group per row: each entry is a record ecol = col, or HOT | hot slot for a row held
-// in LDS, and val, in the row's (col, CSR position) order -- one fma chain from 0, the value
-// rows_combine computes from the sorted copy (row_sum_grouped on scol / sval).
-#define SPMM_HOT_BIT 0x80000000u
-template <int LPR, bool BUF>
-__global__ __launch_bounds__(1024) void spmm_short_hot_kernel(
-    const int32_t* __restrict__ rows, const uint2* __restrict__ span, int64_t q0, int64_t q1,
-    const uint32_t* __restrict__ ecol, const float* __restrict__ sval,
-    const int32_t* __restrict__ hot_rows, int H, const float* __restrict__ X, int xbytes, int d,
-    SpmmEpi ep, int64_t r0, int64_t r1) {
-  constexpr int NGB = 1024 / LPR;
-  __shared__ float4 hot[SHORT_HOT_F4];
-  const int tid = threadIdx.x, g = tid / LPR, sub = tid % LPR;
-  // hot rows into LDS, 8 rows' loads in flight per thread (a serial loop waits per row)
-  for (int i0 = 0; i0 < H * LPR; i0 += 8 * 1024) {
-    int64_t src[8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int i = i0 + u * 1024 + tid;
-      src[u] = i < H * LPR ? (int64_t)hot_rows[i / LPR] * d + 4 * (i % LPR) : -1;
-    }
-    float4 v[8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u)
-      v[u] = src[u] >= 0 ? *reinterpret_cast<const float4*>(X + src[u]) : make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int i = i0 + u * 1024 + tid;
-      if (i < H * LPR) hot[i] = v[u];
-    }
-  }
-  __syncthreads();
-  // every entry issues one buffer load of X (a hot entry's offset is out of range: the load
-  // returns 0 without touching memory) and one LDS read of the hot rows (hot slot 0 for a cold
-  // entry), then selects -- no divergent branch, and no generic (flat) loads the compiler would
-  // otherwise form from a select of the two pointers (flat loads wait on both counters)
-  const __amdgpu_buffer_rsrc_t xr =
-      __builtin_amdgcn_make_buffer_rsrc((void*)X, 0, BUF ? xbytes : 0, 0x00020000);
-  auto fetch = [&](uint32_t c) -> float4 {
-    if (!BUF)  // X past a buffer resource's 2 GB range: no hot rows (H = 0), plain gathers
-      return *reinterpret_cast<const float4*>(X + (int64_t)c * d + 4 * sub);
-    const bool h = (c & SPMM_HOT_BIT) != 0;
-    const int off = h ? (int)0x80000000 : (int)(c * (uint32_t)d * 4u + 16u * sub);
-    const float4 xg = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0));
-    const float4 xl = hot[(h ? (c & ~SPMM_HOT_BIT) : 0u) * LPR + sub];
-    return h ? xl : xg;
-  };
-  const int64_t qs = (int64_t)gridDim.x * NGB;
-  int64_t q = q0 + (int64_t)blockIdx.x * NGB + g;
-  // the next row's id and entry span load while this row's entries are gathered (span = the
-  // row's [start, end) in the CSR, precomputed: no dependent rowptr load per row)
-  int64_t nr = q < q1 ? rows[q] : 0;
-  uint2 nsp = q < q1 ? span[q] : make_uint2(0u, 0u);
-  for (; q < q1; q += qs) {
-    const int64_t r = nr, s = nsp.x, e = nsp.y;
-    if (q + qs < q1) {
-      nr = rows[q + qs];
-      nsp = span[q + qs];
-    }
-    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-    int64_t p = s;
-    for (; p + 3 < e; p += 4) {
-      uint32_t c[4];
-      float w[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        c[u] = ecol[p + u];
-        w[u] = sval[p + u];
-      }
-      float4 x[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) x[u] = fetch(c[u]);
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        acc.x = fmaf(w[u], x[u].x, acc.x);
-        acc.y = fmaf(w[u], x[u].y, acc.y);
-        acc.z = fmaf(w[u], x[u].z, acc.z);
-        acc.w = fmaf(w[u], x[u].w, acc.w);
-      }
-    }
-    for (; p < e; ++p) {
-      const float w = sval[p];
-      const float4 x = fetch(ecol[p]);
-      acc.x = fmaf(w, x.x, acc.x);
-      acc.y = fmaf(w, x.y, acc.y);
-      acc.z = fmaf(w, x.z, acc.z);
-      acc.w = fmaf(w, x.w, acc.w);
-    }
-    if (r >= r0 && r < r1) spmm_epilogue(r, d, sub, acc, X, ep);
   }
 }
 
@@ -1625,75 +1429,6 @@ static hnm_status swalk_build(hnm_spmm_plan* pl, int d, ShortSched** out) {
   return HNM_OK;
 }
 
-// hot-row short kernel (SPMM_SWALK 2): per d the H most gathered rows and the records
-struct HotSched {
-  int H;
-  int32_t* hot_rows;   // [H]
-  uint32_t* ecol;      // [nnz] CSR layout, short rows only: col or HOT | slot, sorted order
-  int32_t* rows;       // [n_short] the short rows, ascending
-  uint2* span;         // [n_short] each short row's [start, end) in the CSR (nnz < 2^32)
-  int64_t n;
-};
-
-static void hot_sched_free(HotSched* h) {
-  if (!h) return;
-  (void)hipFree(h->hot_rows);
-  (void)hipFree(h->ecol);
-  (void)hipFree(h->rows);
-  (void)hipFree(h->span);
-  delete h;
-}
-
-static hnm_status hot_build(hnm_spmm_plan* pl, int d, HotSched** out) {
-  const int lpr = d / 4;
-  const std::vector<int64_t>& rp = *pl->h_rowptr;
-  const std::vector<int32_t>& sr = *pl->h_short_rows;
-  const std::vector<int32_t>& hc = *pl->h_scol;
-  const int64_t N = pl->N;
-  // hot rows are read through a buffer resource over X: 32-bit byte offsets
-  const int Hmax = N * d * 4 <= (int64_t)INT32_MAX - 16 ? SHORT_HOT_F4 / lpr : 0;
-  std::vector<int64_t> cnt((size_t)N, 0);
-  for (int32_t r : sr)
-    for (int64_t q = rp[r]; q < rp[r + 1]; ++q) ++cnt[hc[q]];
-  std::vector<int32_t> order;
-  for (int64_t c = 0; c < N; ++c)
-    if (cnt[c] > 1) order.push_back((int32_t)c);
-  const int H = (int)std::min<int64_t>(Hmax, (int64_t)order.size());
-  std::partial_sort(order.begin(), order.begin() + H, order.end(),
-                    [&](int32_t a, int32_t b) { return cnt[a] > cnt[b] || (cnt[a] == cnt[b] && a < b); });
-  order.resize((size_t)H);
-  std::sort(order.begin(), order.end());  // hot slots in column order
-  std::vector<int32_t> slot((size_t)N, -1);
-  for (int i = 0; i < H; ++i) slot[order[i]] = i;
-  std::vector<uint32_t> ecol((size_t)pl->nnz, 0u);
-  parallel_for((int64_t)sr.size(), [&](int64_t i) {
-    const int32_t r = sr[i];
-    for (int64_t q = rp[r]; q < rp[r + 1]; ++q) {
-      const int32_t c = hc[q];
-      ecol[q] = slot[c] >= 0 ? (SPMM_HOT_BIT | (uint32_t)slot[c]) : (uint32_t)c;
-    }
-  });
-  std::vector<uint2> span(sr.size());
-  for (size_t i = 0; i < sr.size(); ++i) span[i] = make_uint2((unsigned)rp[sr[i]], (unsigned)rp[sr[i] + 1]);
-  HotSched* h = new HotSched();
-  h->H = H;
-  h->n = (int64_t)sr.size();
-  h->hot_rows = nullptr;
-  h->ecol = nullptr;
-  h->rows = nullptr;
-  h->span = nullptr;
-  hnm_status st;
-  if ((st = upload(&h->hot_rows, order.data(), order.size())) ||
-      (st = upload(&h->ecol, ecol.data(), ecol.size())) ||
-      (st = upload(&h->rows, sr.data(), sr.size())) ||
-      (st = upload(&h->span, span.data(), span.size()))) {
-    hot_sched_free(h);
-    return st;
-  }
-  *out = h;
-  return HNM_OK;
-}
-
 static int walk_index(int d) {
   int i = 0;
   while ((4 << i) < d) ++i;
@@ -1709,7 +1444,7 @@ static bool spmm_d_ok(int d) {
 // Binding + the walk schedules for d, built on first use (one-time, host work with stream syncs).
 static hnm_status walk_get(hnm_ctx* ctx, const hnm_spmm_plan* cpl, const int32_t* col,
                            const float* val, int d, const WalkSched** out,
-                           const ShortSched** sout, const HotSched** hout = nullptr) {
+                           const ShortSched** sout) {
   hnm_spmm_plan* pl = const_cast<hnm_spmm_plan*>(cpl);
   std::lock_guard<std::mutex> lk(*pl->mu);
   hnm_status s = plan_bind(ctx, pl, col, val);
@@ -1717,11 +1452,9 @@ static hnm_status walk_get(hnm_ctx* ctx, const hnm_spmm_plan* cpl, const int32_t
   if (!pl->walk || d <= 0) return HNM_OK;
   const int i = walk_index(d);
   if (!pl->sched[i] && (s = walk_build(pl, d, &pl->sched[i]))) return s;
-  if (pl->swalk == 1 && !pl->ssched[i] && (s = swalk_build(pl, d, &pl->ssched[i]))) return s;
-  if (pl->swalk == 2 && !pl->hsched[i] && (s = hot_build(pl, d, &pl->hsched[i]))) return s;
+  if (pl->swalk && !pl->ssched[i] && (s = swalk_build(pl, d, &pl->ssched[i]))) return s;
   if (out) *out = pl->sched[i];
   if (sout) *sout = pl->ssched[i];
-  if (hout) *hout = pl->hsched[i];
   return HNM_OK;
 }
 
@@ -1784,7 +1517,7 @@ extern "C" hnm_status hnm_spmm_plan_create(hnm_ctx* ctx, int64_t N, const int64_
     pl->h_walk_rows = new std::vector<int32_t>(wr);
     pl->h_short_rows = new std::vector<int32_t>(sr);
     pl->h_rowptr = new std::vector<int64_t>(std::move(rp));
-    pl->swalk = sr.empty() ? 0 : SPMM_SWALK;
+    pl->swalk = SPMM_SWALK && !sr.empty();
   }
   if (pl->n_long > 0) {
     if (hipMalloc((void**)&pl->long_rows, pl->n_long * 4) != hipSuccess) {
@@ -1832,7 +1565,6 @@ extern "C" hnm_status hnm_spmm_plan_destroy(hnm_spmm_plan* pl) {
   if (pl->long_rows) (void)hipFree(pl->long_rows);
   for (WalkSched* w : pl->sched) walk_sched_free(w);
   for (ShortSched* w : pl->ssched) short_sched_free(w);
-  for (HotSched* w : pl->hsched) hot_sched_free(w);
   if (pl->scol) (void)hipFree(pl->scol);
   if (pl->sval) (void)hipFree(pl->sval);
   delete pl->h_walk_rows;
@@ -1865,8 +1597,7 @@ static hnm_status spmm_launch(hnm_ctx* ctx, const hnm_spmm_plan* pl, int64_t N,
     // user-ordered walk (+ the split rows' finish), one stream, disjoint output rows
     const WalkSched* ws = nullptr;
     const ShortSched* ss = nullptr;
-    const HotSched* hs = nullptr;
-    hnm_status s = walk_get(ctx, pl, col, val, d, &ws, &ss, &hs);
+    hnm_status s = walk_get(ctx, pl, col, val, d, &ws, &ss);
     if (s) return s;
     const std::vector<int32_t>& wr = *pl->h_walk_rows;
     const bool any = std::lower_bound(wr.begin(), wr.end(), (int32_t)std::min<int64_t>(r0, INT32_MAX)) !=
@@ -1883,25 +1614,6 @@ static hnm_status spmm_launch(hnm_ctx* ctx, const hnm_spmm_plan* pl, int64_t N,
     hipStream_t wst = fork ? ctx->side : ctx->stream;
     auto short_rows = [&]() -> hnm_status {
       if (r1 <= r0) return HNM_OK;
-      if (hs) {
-        const std::vector<int32_t>& sr = *pl->h_short_rows;
-        const int64_t q0 = std::lower_bound(sr.begin(), sr.end(), (int32_t)std::min<int64_t>(r0, INT32_MAX)) - sr.begin();
-        const int64_t q1 = std::lower_bound(sr.begin(), sr.end(), (int32_t)std::min<int64_t>(r1, INT32_MAX)) - sr.begin();
-        if (q1 > q0) {
-          const unsigned grid = (unsigned)std::min<int64_t>(hnm_cdiv(q1 - q0, 1024 / LPR),
-                                                            (int64_t)ctx->num_cus * SHORT_HOT_WG);
-          if (hs->H > 0)
-            hipLaunchKernelGGL((spmm_short_hot_kernel<LPR, true>), dim3(grid), dim3(1024), 0,
-                               ctx->stream, hs->rows, hs->span, q0, q1, hs->ecol, pl->sval,
-                               hs->hot_rows, hs->H, X, (int)(N * d * 4), d, ep, r0, r1);
-          else
-            hipLaunchKernelGGL((spmm_short_hot_kernel<LPR, false>), dim3(grid), dim3(1024), 0,
-                               ctx->stream, hs->rows, hs->span, q0, q1, hs->ecol, pl->sval,
-                               hs->hot_rows, 0, X, 0, d, ep, r0, r1);
-          HNM_LAUNCH_CHECK();
-        }
-        return HNM_OK;
-      }
       if (ss) {
         // blocks whose rows meet [r0, r1) (blocks are in ascending row order)
         const int64_t b0 = std::lower_bound(ss->last.begin(), ss->last.end(),
@@ -1917,16 +1629,10 @@ static hnm_status spmm_launch(hnm_ctx* ctx, const hnm_spmm_plan* pl, int64_t N,
         }
         return HNM_OK;
       }
-      if (SPMM_SHORT_ILP == 2) {
-        hipLaunchKernelGGL(spmm_short2_kernel<LPR>,
-                           dim3((unsigned)hnm_cdiv(r1 - r0, 8 * (64 / LPR))), dim3(256), 0,
-                           ctx->stream, r0, r1, rowptr, col, val, X, d, ep);
-      } else {
-        hipLaunchKernelGGL(spmm_mixed_kernel<LPR>,
-                           dim3((unsigned)hnm_cdiv(r1 - r0, 4 * (64 / LPR))), dim3(256), 0,
-                           ctx->stream, r0, r1, pl->long_rows, (int64_t)0, (int64_t)0, (int64_t)0,
-                           rowptr, col, val, X, d, ep);
-      }
+      hipLaunchKernelGGL(spmm_mixed_kernel<LPR>,
+                         dim3((unsigned)hnm_cdiv(r1 - r0, 4 * (64 / LPR))), dim3(256), 0,
+                         ctx->stream, r0, r1, pl->long_rows, (int64_t)0, (int64_t)0, (int64_t)0,
+                         rowptr, col, val, X, d, ep);
       HNM_LAUNCH_CHECK();
       return HNM_OK;
     };
@@ -2079,7 +1785,7 @@ extern "C" hnm_status hnm_spmm_rows_combine_f32(hnm_ctx* ctx, const hnm_spmm_pla
     if (s) return s;
     if (plan->walk) {
       co.mode = 2;
-      co.short_sorted = plan->swalk != 0;
+      co.short_sorted = plan->swalk;
       co.scol = plan->scol;
       co.sval = plan->sval;
       co.cap = plan->walk_cap;

@@ -1,7 +1,7 @@
 #!/bin/bash
 # rocprofv3 kernel stats of `bench.py --workload <w> --profile-only` for variant libraries, and
 # FETCH_SIZE / TCC hit-miss passes for the first variant.
-#   bash tools/r4_prof_ab.sh <tag> <workload> variants...
+#   bash tools/gpu_prof_ab.sh <tag> <workload> variants...
 set -uo pipefail
 TAG=$1; W=$2; shift 2
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}

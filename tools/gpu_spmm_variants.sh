@@ -2,7 +2,7 @@
 # SpMM variant sweep: tools/spmm_halves.py (per-half times, sampled forward() rows dumped) per
 # variant library at d=64 (and d=128 for the variants after "--"), then a bitwise comparison of
 # the dumps against the first variant of each summation-order family.
-#   bash tools/r4_spmm_var.sh <tag> v1 v2 ... [-- w1 w2 ...]
+#   bash tools/gpu_spmm_variants.sh <tag> v1 v2 ... [-- w1 w2 ...]
 set -uo pipefail
 TAG=$1; shift
 OUT=gpurun_out/$TAG; mkdir -p $OUT
