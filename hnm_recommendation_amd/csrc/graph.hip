@@ -1070,28 +1070,34 @@ static void plan_bipartite_sides(hnm_spmm_plan* pl) {
   const std::vector<int64_t>& rp = *pl->h_rowptr;
   const std::vector<int32_t>& hc = *pl->h_scol;
   const int64_t N = pl->N;
-  // S = row 0's smallest neighbour other than itself
-  int64_t S = -1;
-  for (int64_t q = rp[0]; q < rp[1]; ++q)
-    if (hc[q] != 0) {
-      S = hc[q];
+  // per row the smallest / largest neighbour other than itself (entries are column-sorted);
+  // a split S is valid when every row below it only reaches [S, N) and every row from it on
+  // only reaches [0, S): prefix min of the minima >= S and suffix max of the maxima < S
+  std::vector<int64_t> mn((size_t)N), mx((size_t)N);
+  parallel_for(hnm_cdiv(N, 4096), [&](int64_t ch) {
+    const int64_t r1 = std::min<int64_t>(N, (ch + 1) * 4096);
+    for (int64_t r = ch * 4096; r < r1; ++r) {
+      int64_t lo = N, hi = -1;
+      for (int64_t q = rp[r]; q < rp[r + 1]; ++q)
+        if (hc[q] != r) {
+          lo = std::min<int64_t>(lo, hc[q]);
+          hi = std::max<int64_t>(hi, hc[q]);
+        }
+      mn[r] = lo;
+      mx[r] = hi;
+    }
+  });
+  std::vector<int64_t> smax((size_t)N + 1, -1);
+  for (int64_t r = N - 1; r >= 0; --r) smax[r] = std::max(smax[r + 1], mx[r]);
+  int64_t S = -1, pmin = N;
+  for (int64_t c = 1; c < N; ++c) {
+    pmin = std::min(pmin, mn[c - 1]);
+    if (pmin >= c && smax[c] < c && pmin < N && smax[c] >= 0) {
+      S = c;
       break;
     }
-  if (S <= 0 || S >= N) return;
-  std::vector<char> ok((size_t)hnm_cdiv(N, 4096), 1);
-  parallel_for((int64_t)ok.size(), [&](int64_t ch) {
-    const int64_t r1 = std::min<int64_t>(N, (ch + 1) * 4096);
-    for (int64_t r = ch * 4096; r < r1 && ok[ch]; ++r)
-      for (int64_t q = rp[r]; q < rp[r + 1]; ++q) {
-        const int64_t c = hc[q];
-        if (c != r && ((r < S) == (c < S))) {
-          ok[ch] = 0;
-          break;
-        }
-      }
-  });
-  for (char v : ok)
-    if (!v) return;
+  }
+  if (S <= 0) return;
   // the side whose neighbours form the larger table moves its short rows into the walk
   const bool upper = S > N - S;  // rows [S, N) gather the S-row table
   const int64_t lo = upper ? S : 0, hi = upper ? N : S;
