@@ -63,6 +63,13 @@
 #ifndef WALK_WIN
 #define WALK_WIN 16
 #endif
+// entries per walk step and the records' prefetch a step ahead (as SWALK_STEP / SWALK_PF)
+#ifndef WALK_STEP
+#define WALK_STEP 4
+#endif
+#ifndef WALK_PF
+#define WALK_PF 0
+#endif
 #ifndef WALK_LDS_F4
 #define WALK_LDS_F4 9216        // 144 KiB of float4 row accumulators per workgroup
 #endif
@@ -579,33 +586,64 @@ __global__ __launch_bounds__(WALK_THREADS) void spmm_walk_kernel(
   const int ns = nslot[blockIdx.x];
   for (int i = tid; i < ns * LPR; i += WALK_THREADS) acc[i] = make_float4(0.f, 0.f, 0.f, 0.f);
   __syncthreads();
-  // 4 entries per step (2: 1.741 ms per d=64 layer, 4: 1.694, 8: 1.848; records prefetched a
-  // step ahead as 16-B vectors with 8 or 16 gathers in flight: 1.812 / 1.823)
+  // WALK_STEP entries per step (round 3, unprefetched: 2: 1.741 ms per d=64 layer, 4: 1.694,
+  // 8: 1.848); WALK_PF: the next step's records loaded before this step's gathers
   constexpr int K = WALK_WIN > 1 ? WALK_WIN : 1;
+  constexpr int ST = WALK_STEP;
+  auto consume = [&](const uint32_t* c, const float* w) {
+    float4 x[ST];
+#pragma unroll
+    for (int u = 0; u < ST; ++u)
+      x[u] = *reinterpret_cast<const float4*>(X + (int64_t)(c[u] >> 10) * d + 4 * sub);
+#pragma unroll
+    for (int u = 0; u < ST; ++u) {  // in list order: a slot's entries stay one fma chain
+      float4* a = &acc[(c[u] & 1023u) * LPR + sub];
+      float4 v = *a;
+      v.x = fmaf(w[u], x[u].x, v.x);
+      v.y = fmaf(w[u], x[u].y, v.y);
+      v.z = fmaf(w[u], x[u].z, v.z);
+      v.w = fmaf(w[u], x[u].w, v.w);
+      *a = v;
+    }
+  };
   for (int k = 0; k < K; ++k) {
     int64_t p = gptr[((int64_t)blockIdx.x * NG + g) * K + k];
     const int64_t e = gptr[((int64_t)blockIdx.x * NG + g) * K + k + 1];
-    for (; p + 3 < e; p += 4) {
-      uint32_t c[4];
-      float w[4];
+    if (WALK_PF) {
+      uint32_t c[ST], cn[ST];
+      float w[ST], wn[ST];
+      if (p + ST - 1 < e) {
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        c[u] = ent[p + u];
-        w[u] = wt[p + u];
+        for (int u = 0; u < ST; ++u) {
+          cn[u] = ent[p + u];
+          wn[u] = wt[p + u];
+        }
       }
-      float4 x[4];
+      for (; p + ST - 1 < e; p += ST) {
 #pragma unroll
-      for (int u = 0; u < 4; ++u)
-        x[u] = *reinterpret_cast<const float4*>(X + (int64_t)(c[u] >> 10) * d + 4 * sub);
+        for (int u = 0; u < ST; ++u) {
+          c[u] = cn[u];
+          w[u] = wn[u];
+        }
+        if (p + 2 * ST - 1 < e) {
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {  // in list order: a slot's entries stay one fma chain
-        float4* a = &acc[(c[u] & 1023u) * LPR + sub];
-        float4 v = *a;
-        v.x = fmaf(w[u], x[u].x, v.x);
-        v.y = fmaf(w[u], x[u].y, v.y);
-        v.z = fmaf(w[u], x[u].z, v.z);
-        v.w = fmaf(w[u], x[u].w, v.w);
-        *a = v;
+          for (int u = 0; u < ST; ++u) {
+            cn[u] = ent[p + ST + u];
+            wn[u] = wt[p + ST + u];
+          }
+        }
+        consume(c, w);
+      }
+    } else {
+      for (; p + ST - 1 < e; p += ST) {
+        uint32_t c[ST];
+        float w[ST];
+#pragma unroll
+        for (int u = 0; u < ST; ++u) {
+          c[u] = ent[p + u];
+          w[u] = wt[p + u];
+        }
+        consume(c, w);
       }
     }
     for (; p < e; ++p) {
@@ -1248,7 +1286,7 @@ static hnm_status walk_build(hnm_spmm_plan* pl, int d, WalkSched** out) {
   });
   std::vector<int64_t> gptr((size_t)(nwg * ng * K + 1), 0);
   for (int64_t i = 0; i < nwg * ng * K; ++i)
-    gptr[i + 1] = gptr[i] + (K > 1 ? hnm_cdiv(wcnt[i], 4) * 4 : wcnt[i]);
+    gptr[i + 1] = gptr[i] + (K > 1 ? hnm_cdiv(wcnt[i], WALK_STEP) * WALK_STEP : wcnt[i]);
   const int64_t Tp = gptr.back();
   std::vector<uint32_t> ent((size_t)Tp, (uint32_t)maxloc);  // padding: col 0, spare slot, 0.0
   std::vector<float> wt((size_t)Tp, 0.f);
