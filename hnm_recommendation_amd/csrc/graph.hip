@@ -63,7 +63,11 @@
 #ifndef WALK_WIN
 #define WALK_WIN 16
 #endif
-// entries per walk step and the records' prefetch a step ahead (as SWALK_STEP / SWALK_PF)
+// entries per walk step and the records' prefetch a step ahead (as SWALK_STEP / SWALK_PF).
+// Round 4 A/B on the final tree (whole-graph layer, d=64 / d=128): 4 entries 1.308 / 2.676 ms,
+// 4 + prefetch 1.415 / 2.920, 8 entries 1.435 / 3.017, 8 + prefetch 1.448 / 3.090 -- unlike the
+// short walk, the long-row walk's 16 windows (barriers) already overlap its record loads.
+// SPMM_WALK_MODE on the same box: 2 (default) 1.308 / 2.676, 1 1.308 / 2.678, 0 1.318 / 2.928.
 #ifndef WALK_STEP
 #define WALK_STEP 4
 #endif

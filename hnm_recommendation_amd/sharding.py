@@ -294,10 +294,17 @@ class lightgcn_shard_topk:
         self.model, self.lo, self.hi, self.k = model, lo, hi, k
         self.history = history
         self._dot = None
+        self._rows = None
 
     def _scorer(self, user_ids):
         fb, fi = self.model.propagate_for(user_ids)
-        rows = torch.arange(user_ids.numel(), dtype=torch.int64, device=user_ids.device)
+        n, dev = user_ids.numel(), user_ids.device
+        if self._rows is None or self._rows.numel() < n or self._rows.device != dev:
+            # kept across calls (one launch less a call); completed before any stream reads it
+            self._rows = torch.arange(n, dtype=torch.int64, device=dev)
+            if dev.type == "cuda":
+                torch.cuda.current_stream(dev).synchronize()
+        rows = self._rows[:n]
         dot = dot_shard_topk(fb, fi, self.lo, self.hi, self.k, self.history)
         dot.mask_users = user_ids.to(torch.int64).contiguous()   # history keyed by user id
         return dot, rows
