@@ -46,11 +46,29 @@ constexpr int64_t DCERT_SAMPLE = DCERT_SAMPLE_N;
 #endif  // sampled items: stride max(8, I / this)
 constexpr float DCERT_RHO = 0.00146484375f;  // 3 u16 = 3 * 2^-11
 constexpr int DCERT_MAX_NP = 64;
-#ifndef DOT_WG64
-#define DOT_WG64 3
+
+// user blocks of 32 per scan wave (each item fragment feeds NB MFMAs), per DP.  Round 4 A/B
+// (MF d=64 step / THRESH scan, one box): NB = 1 0.1827 / 0.0835 ms, NB = 2 at 2 workgroups per
+// CU 0.1845 / 0.0866 (half the LDS fragment reads did not pay for the lost occupancy), the
+// sample pass at NB = 2 0.2011 (its running max then costs 3 instructions a value); round 3's
+// 64-bit tile addressing 0.1872 / 0.0886
+#ifndef DOT_NB64
+#define DOT_NB64 1
 #endif
-// scan occupancy (workgroups per CU): two sub-tiles in flight need up to 168 VGPRs
-__host__ __device__ constexpr int dcert_wg_per_cu(int DP) { return DP > 64 ? 3 : DOT_WG64; }
+#ifndef DOT_NB128
+#define DOT_NB128 1
+#endif
+enum { DSCAN_DENSE = 0, DSCAN_THRESH = 1, DSCAN_SAMPLE = 2 };  // scan modes (below)
+#ifndef DOT_NB64S  // the sample pass (its running max at NB = 2 costs 3 instructions a value)
+#define DOT_NB64S 1
+#endif
+__host__ __device__ constexpr int dscan_nb(int DP, int MODE) {
+  return DP > 64 ? DOT_NB128 : (MODE == DSCAN_SAMPLE ? DOT_NB64S : DOT_NB64);
+}
+__host__ __device__ constexpr int dscan_users(int DP, int MODE) { return 128 * dscan_nb(DP, MODE); }
+// scan occupancy (workgroups per CU): NB = 1, two sub-tiles in flight, fits 3 in 168 VGPRs;
+// NB = 2 (two user blocks' A operands and thresholds) needs ~230: 2
+__host__ __device__ constexpr int dcert_wg_per_cu(int NB) { return NB == 2 ? 2 : 3; }
 
 enum { DM_U, DM_I, DM_NI, DM_IB, DM_N };
 
@@ -97,10 +115,10 @@ struct DotCertShape {
   int capp;
 };
 
-Partition xcd_partition(int64_t I, int64_t ublocks, int num_cus, int DP) {
+Partition xcd_partition(int64_t I, int64_t ublocks, int num_cus, int NB) {
   // ~dcert_wg_per_cu workgroups per CU, NP a multiple of 8 (XCD-aware), <= DCERT_MAX_NP
   int64_t np = std::max<int64_t>(
-      1, (int64_t)dcert_wg_per_cu(DP) * num_cus / std::max<int64_t>(ublocks, 1));
+      1, (int64_t)dcert_wg_per_cu(NB) * num_cus / std::max<int64_t>(ublocks, 1));
   np = std::min<int64_t>(np, std::max<int64_t>(1, hnm_cdiv(I, 4 * TILE)));
   np = std::min<int64_t>(np, DCERT_MAX_NP);
   if (np >= 8) np = np / 8 * 8;
@@ -113,8 +131,10 @@ DotCertShape dcert_shape(int64_t B, int64_t I, int d, int K, int num_cus) {
   sh.DP = d <= 64 ? 64 : 128;
   sh.stride = std::max<int64_t>(DCERT_MIN_STRIDE, I / DCERT_SAMPLE);  // sample <= 1/stride of the items
   sh.Ns = hnm_cdiv(I, sh.stride);
-  sh.part = xcd_partition(I, hnm_cdiv(B, 128), num_cus, sh.DP);
-  sh.spart = xcd_partition(sh.Ns, hnm_cdiv(B, 128), num_cus, sh.DP);
+  sh.part = xcd_partition(I, hnm_cdiv(B, dscan_users(sh.DP, DSCAN_THRESH)), num_cus,
+                          dscan_nb(sh.DP, DSCAN_THRESH));
+  sh.spart = xcd_partition(sh.Ns, hnm_cdiv(B, dscan_users(sh.DP, DSCAN_SAMPLE)), num_cus,
+                           dscan_nb(sh.DP, DSCAN_SAMPLE));
   const int64_t total = std::min<int64_t>(8192, std::max<int64_t>(256, 8 * (int64_t)K * sh.stride));
   sh.capp = (int)std::max<int64_t>(32, std::min<int64_t>(total, hnm_cdiv(4 * total, sh.part.np)));
   return sh;
@@ -306,13 +326,13 @@ __global__ __launch_bounds__(256) void dcert_convert_kernel(DotArgs a, int DP,
 // lane) running max of the scaled approx over the strided sample (masked items excluded)
 // -> dense[b][p * 32 + j]; the K-th best of those maxima is a lower bound of the sample's
 // K-th best.  THRESH: append approx >= tau_b to the (user, partition) segment.
-enum { DSCAN_DENSE = 0, DSCAN_THRESH = 1, DSCAN_SAMPLE = 2 };
 
 struct DScanArgs {
   const _Float16* U16;  // [B, DP]
   const _Float16* I16;  // [Itot, DP]
   const float* ibs;     // [Itot] item bias, scaled (BIAS)
   int64_t B, I, istride, ipp;
+  int64_t itab;         // rows of the I16 / ibs tables (buffer-load extents)
   int NP;
   const int64_t* mptr;
   const int32_t* midx;
@@ -328,95 +348,113 @@ __device__ __forceinline__ f32x16 mfma16(h8 a, h8 b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
 }
 
-// A wave holds 32 users' f16 rows as the MFMA A operand; TI-item tiles of I16 (128 items at
-// DP = 64, 64 at DP = 128) stream through LDS, double-buffered with one barrier per tile, so a
-// wave has SUB = TI / 32 sub-tiles of MFMA + test work per barrier and the next tile's loads
-// (LD 16-B chunks per thread) a whole tile of work to land.  acc[r] = approx dot of user row
-// mfma32_row(r, h) with item lane j of the sub-tile.  THRESH: one v_cmp per score straight
-// into a ballot (SGPR pair), OR-reduced on the scalar unit; only a sub-tile with a pass
-// re-ballots its rows and appends.
+// A wave holds NB blocks of 32 users' f16 rows as MFMA A operands; TI-item tiles of I16 (128
+// items at DP = 64, 64 at DP = 128) stream through LDS, double-buffered with one barrier per
+// tile (LD 16-B chunks per thread: a whole tile of work for the prefetch to land).  Every step
+// runs two independent MFMA chains: NB = 1 two sub-tiles of one user block, NB = 2 one sub-tile
+// of two user blocks -- each item fragment read from LDS then feeds two MFMAs, which halves the
+// LDS traffic per MFMA (round 4: at NB = 1 the 12 waves of a CU read 192 KB of fragments per
+// tile, as many LDS cycles as the tile's matrix-pipe cycles, and the scan ran at ~0.5 of the
+// random-data MFMA rate).  acc[r] = approx dot of user row 32 nb + mfma32_row(r, h) with item
+// lane j of the sub-tile.  THRESH: a lane's 16 rows reduced by one max tree and one ballot per
+// chain; only a chain with a pass forms its row bits and appends.
 // MASK (compile-time): a filter CSR is present.  Its per-row cursor loads are the only global
 // loads inside the tile loop; in a kernel without them the waitcnt pass never has to assume a
 // pending load there (which otherwise costs vmcnt(0) -- the tile prefetch too -- per step).
-template <int DP, int MODE, bool BIAS, bool MASK>
-__global__ __launch_bounds__(256, dcert_wg_per_cu(DP)) void dot16_scan_kernel(DScanArgs A) {
+// Item tiles are fetched by buffer loads (SGPR tile offsets, one per-thread VGPR offset; the
+// 64-bit per-chunk addresses of round 3 cost ~38 VALU a tile): rows past the partition end
+// hold the next partition's items (finite; every consumer tests n < part_end), past the table
+// end the buffer reads zeros (the host keeps itab * DP * 2 < 2^31: dot_cert_eligible).
+template <int DP, int MODE, bool BIAS, bool MASK, int NB>
+__global__ __launch_bounds__(256, dcert_wg_per_cu(NB)) void dot16_scan_kernel(DScanArgs A) {
   constexpr int KS = DP / 16;     // f16 MFMA k-steps
   constexpr int RS = DP + 8;      // LDS row stride (halfs): conflict-free b128 reads
   constexpr int CH = DP / 8;      // 16-B chunks per item row
-#ifndef DOT_TI
   constexpr int TI = DP <= 64 ? 128 : 64;  // items per LDS tile
-#else
-  constexpr int TI = DOT_TI;
-#endif
   constexpr int SUB = TI / TILE;
   constexpr int LD = TI * CH / 256;  // chunks per thread per tile (4)
+  constexpr int UW = 32 * NB;        // users per wave
+  constexpr int NTS = NB == 1 ? 2 : 1;  // sub-tiles per step: two MFMA chains
+  constexpr int NC = NTS * NB;  // MFMA chains per step
   __shared__ __attribute__((aligned(16))) _Float16 vs[2][TI * RS];
   __shared__ float ibl[2][BIAS ? TI : 1];  // the tile's scaled item biases
-  __shared__ int lcnt[4][MODE == DSCAN_THRESH ? 32 : 1];  // THRESH: appends per (wave, user row)
+  __shared__ int lcnt[4][MODE == DSCAN_THRESH ? UW : 1];  // THRESH: appends per (wave, user row)
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5, j = lane & 31;
   const int p = blockIdx.x;
-  const int64_t b0 = (int64_t)blockIdx.y * 128 + wave * 32;
-  const int nu = (int)std::max<int64_t>(0, std::min<int64_t>(32, A.B - b0));
+  const int64_t b0 = (int64_t)blockIdx.y * 4 * UW + wave * UW;
+  const int nu = (int)std::max<int64_t>(0, std::min<int64_t>(UW, A.B - b0));
   const int64_t part_start = (int64_t)p * A.ipp;
   const int64_t part_end = std::min<int64_t>(A.I, part_start + A.ipp);
   const int64_t S = MODE == DSCAN_SAMPLE ? A.istride : 1;  // the strided sample is the only S > 1 pass
 
-  h8 a[KS];
+  h8 a[NB][KS];
 #pragma unroll
-  for (int s = 0; s < KS; ++s) {
-    h8 z = {};
-    a[s] = j < nu ? *reinterpret_cast<const h8*>(A.U16 + (b0 + j) * DP + 16 * s + 8 * h) : z;
-  }
+  for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      h8 z = {};
+      a[nb][s] = 32 * nb + j < nu
+                     ? *reinterpret_cast<const h8*>(A.U16 + (b0 + 32 * nb + j) * DP + 16 * s + 8 * h)
+                     : z;
+    }
   // THRESH: minus the threshold of accumulator row r's user -- the MFMA chain's initial value,
   // so the accumulator ends as approx - tau (-inf for rows past the batch: never passes).  The
   // extra fp32 rounding of the chain by |tau| (a few 2^-24 of the score scale) is inside the
   // 2^-18 guard dcert_tau_kernel leaves.
   // (loads unconditional at a clamped row, then a select: a load inside the branch would be
   // waited for right there, 16 serial round trips)
-  f32x16 ntv;
+  f32x16 ntv[NB];
 #pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const int64_t b = b0 + mfma32_row(r, h);
-    if (MODE == DSCAN_THRESH) {
-      const float tb = A.tau[std::min<int64_t>(b, A.B - 1)];
-      ntv[r] = b < A.B ? -tb : -__builtin_inff();
-    } else {
-      ntv[r] = -__builtin_inff();
+  for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int64_t b = b0 + 32 * nb + mfma32_row(r, h);
+      if (MODE == DSCAN_THRESH) {
+        const float tb = A.tau[std::min<int64_t>(b, A.B - 1)];
+        ntv[nb][r] = b < A.B ? -tb : -__builtin_inff();
+      } else {
+        ntv[nb][r] = -__builtin_inff();
+      }
     }
-  }
-  if (MODE == DSCAN_THRESH && lane < 32) lcnt[wave][lane] = 0;
-  float rmax[MODE == DSCAN_SAMPLE ? 16 : 1];  // SAMPLE: running max per C row
+  if (MODE == DSCAN_THRESH && lane < UW) lcnt[wave][lane] = 0;
+  constexpr int NR = MODE == DSCAN_SAMPLE ? 16 * NB : 1;
+  float rmax[NR];  // SAMPLE: running max per C row (block nb: rmax[16 nb + r])
 #pragma unroll
-  for (int r = 0; r < (MODE == DSCAN_SAMPLE ? 16 : 1); ++r) rmax[r] = -__builtin_inff();
+  for (int r = 0; r < NR; ++r) rmax[r] = -__builtin_inff();
   int nm = INT_BIG;
   int64_t mpos = 0, mend = 0;
   constexpr bool masked = MODE != DSCAN_DENSE && MASK;
-  if (masked && lane < nu) {
+  if (masked && lane < nu) {  // lane u follows user b0 + u (UW <= 64)
     const int64_t lo = A.mptr[b0 + lane], hi = A.mptr[b0 + lane + 1];
     mpos = mask_lower_bound(A.midx, lo, hi, (int)(part_start * S));
     mend = hi;
     nm = mpos < mend ? A.midx[mpos] : INT_BIG;
   }
   int32_t* seg = MODE == DSCAN_THRESH ? A.buf + (b0 * A.NP + p) * (int64_t)A.capp : nullptr;
-  const int segstride = A.NP * A.capp;  // row r's segment at r * segstride (< 2^31 / 32)
+  const int segstride = A.NP * A.capp;  // row r's segment at r * segstride (< 2^31 / 64)
   // Appends are queued in two registers per lane and stored once per tile, after the tile's
   // prefetch has landed: vmcnt waits are in order, so a store inside the tile would make the
   // next wait (at the first MFMA after it) also wait for the prefetch issued before it
+  // (round 4 A/B: direct stores with one ballot per row, 0.105 vs 0.089 ms)
   int qo0 = -1, qo1 = -1, qi0 = 0, qi1 = 0;
 
   const int64_t ntiles = part_end > part_start ? hnm_cdiv(part_end - part_start, TI) : 0;
   h8 st[LD];
   float nib = 0.f;  // thread tid < TI: the bias of tile item tid
+  const __amdgpu_buffer_rsrc_t irs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)A.I16, 0, (int)(A.itab * DP * 2), 0x00020000);
+  const __amdgpu_buffer_rsrc_t brs = __builtin_amdgcn_make_buffer_rsrc(
+      BIAS ? (void*)A.ibs : (void*)A.I16, 0, BIAS ? (int)(A.itab * 4) : 0, 0x00020000);
+  const int vrow = (int)((tid / CH) * S * DP * 2 + (tid % CH) * 16);  // this thread's chunk
+  const int qstride = (int)((256 / CH) * S * DP * 2);                 // next q: 256 / CH rows on
   auto fetch = [&](int64_t base) {
+    const int soff = (int)(base * S * DP * 2);
 #pragma unroll
-    for (int q = 0; q < LD; ++q) {
-      const int f = tid + 256 * q, row = f / CH, c = f % CH;
-      const int64_t n = base + row;
-      h8 z = {};
-      st[q] = n < part_end ? *reinterpret_cast<const h8*>(A.I16 + n * S * DP + 8 * c) : z;
-    }
-    if (BIAS && tid < TI) nib = A.ibs[std::min<int64_t>(base + tid, part_end - 1) * S];
+    for (int q = 0; q < LD; ++q)
+      st[q] = __builtin_bit_cast(h8, __builtin_amdgcn_raw_buffer_load_b128(irs, vrow, soff + q * qstride, 0));
+    if (BIAS && tid < TI)
+      nib = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(brs, (int)(tid * S * 4), (int)(base * S * 4), 0));
   };
   auto stash = [&](int bf) {
 #pragma unroll
@@ -444,11 +482,11 @@ __global__ __launch_bounds__(256, dcert_wg_per_cu(DP)) void dot16_scan_kernel(DS
     // just before the barrier (a store round trip per tile)
     fetch(t + 1 < ntiles ? tbase + TI : tbase);
     if (nu > 0) {
-      // filtered (user, item) pairs of the sub-tile at base -> -inf (rare path)
-      auto apply_mask = [&](f32x16& sc, int64_t base, int64_t n) {
+      // filtered (user, item) pairs of block nb's sub-tile at base -> -inf (rare path)
+      auto apply_mask = [&](f32x16& sc, int nb, int64_t base, int64_t n) {
         const int64_t tile_end = std::min<int64_t>(base + TILE, part_end);
         const int64_t real_end = (tile_end - 1) * S + 1;  // real ids of this tile are < real_end
-        uint64_t mm = __ballot(lane < 32 && nm < real_end) & 0xffffffffull;
+        uint64_t mm = __ballot(lane >= 32 * nb && lane < 32 * nb + 32 && nm < real_end);
         while (mm) {
           const int uu = __builtin_ctzll(mm);
           mm &= mm - 1;
@@ -458,7 +496,7 @@ __global__ __launch_bounds__(256, dcert_wg_per_cu(DP)) void dot16_scan_kernel(DS
             if (tgt % S == 0) {
 #pragma unroll
               for (int r = 0; r < 16; ++r)
-                if (mfma32_row(r, h) == uu && n == tgt / S) sc[r] = -__builtin_inff();
+                if (mfma32_row(r, h) == (uu & 31) && n == tgt / S) sc[r] = -__builtin_inff();
             }
             if (lane == uu) {
               ++mpos;
@@ -475,7 +513,7 @@ __global__ __launch_bounds__(256, dcert_wg_per_cu(DP)) void dot16_scan_kernel(DS
       // passing lanes by the rows' owner lanes: 0.094 vs 0.107 ms (the walk alone 0.027 ms of
       // it), and a per-quarter test (4 maxima, 4 ballots): 4-6 % slower
       // (tools/dot_scan_timing.hip, profiles/r2_dot_scan_timing.txt).
-      auto thresh = [&](const f32x16& acc, float ib, int64_t base, bool ivalid) {
+      auto thresh = [&](const f32x16& acc, int nb, float ib, int64_t base, bool ivalid) {
         float lm = acc[0];
 #pragma unroll
         for (int r = 1; r < 16; ++r) lm = fmaxf(lm, acc[r]);
@@ -488,7 +526,7 @@ __global__ __launch_bounds__(256, dcert_wg_per_cu(DP)) void dot16_scan_kernel(DS
         while (rb) {  // divergent: usually one pass in one lane
           const int r = __builtin_ctz(rb);
           rb &= rb - 1;
-          const int row = (r & 3) + 8 * (r >> 2) + 4 * h;  // mfma32_row(r, h)
+          const int row = 32 * nb + (r & 3) + 8 * (r >> 2) + 4 * h;  // 32 nb + mfma32_row(r, h)
           const int slot = atomicAdd(&lcnt[wave][row], 1);
           if (slot < A.capp) {
             const int off = row * segstride + slot;
@@ -504,59 +542,76 @@ __global__ __launch_bounds__(256, dcert_wg_per_cu(DP)) void dot16_scan_kernel(DS
           }
         }
       };
-      // two sub-tiles per step: both MFMA chains are issued before either is tested, so one
-      // chain's latency runs under the other's MFMAs and the first test
 #pragma unroll 1
-      for (int u = 0; u < SUB; u += 2) {
-        const int64_t baseA = tbase + TILE * u, baseB = baseA + TILE;
+      for (int u = 0; u < SUB; u += NTS) {
+        const int64_t baseA = tbase + TILE * u;
         if (baseA >= part_end) break;  // uniform: partial last tile
-        const bool hasB = baseB < part_end;
-        f32x16 accA = MODE == DSCAN_THRESH ? ntv : f32x16{}, accB = accA;
+        const bool hasB = NTS == 1 || baseA + TILE < part_end;
+        // chain c: user block c % NB, sub-tile u + c / NB
+        f32x16 acc[NC];
 #pragma unroll
-        for (int s = 0; s < KS; ++s) {
-          accA = mfma16(a[s], *reinterpret_cast<const h8*>(&vs[cur][(TILE * u + j) * RS + 16 * s + 8 * h]), accA);
-          accB = mfma16(a[s], *reinterpret_cast<const h8*>(&vs[cur][(TILE * (u + 1) + j) * RS + 16 * s + 8 * h]), accB);
-        }
-        if (MODE == DSCAN_SAMPLE && hasB && baseB + TILE <= part_end) {
-          // both sub-tiles fully inside the partition (uniform): per row one v_max3 over the
-          // pair.  No NaN handling needed: a non-finite table entry marks the whole call bad
-          // (dcert_scales_kernel, NaN-propagating maxima) and every row takes the exact path
-          if (masked) {
-            apply_mask(accA, baseA, baseA + j);
-            apply_mask(accB, baseB, baseB + j);
+        for (int c = 0; c < NC; ++c) acc[c] = MODE == DSCAN_THRESH ? ntv[c % NB] : f32x16{};
+#pragma unroll
+        for (int s = 0; s < KS; ++s)
+#pragma unroll
+          for (int t = 0; t < NTS; ++t) {
+            const h8 bf = *reinterpret_cast<const h8*>(&vs[cur][(TILE * (u + t) + j) * RS + 16 * s + 8 * h]);
+#pragma unroll
+            for (int nb = 0; nb < NB; ++nb) acc[t * NB + nb] = mfma16(a[nb][s], bf, acc[t * NB + nb]);
           }
+        if (MODE == DSCAN_SAMPLE && hasB && baseA + NTS * TILE <= part_end) {
+          // the step's sub-tiles fully inside the partition (uniform).  No NaN handling needed:
+          // a non-finite table entry marks the whole call bad (dcert_scales_kernel,
+          // NaN-propagating maxima) and every row takes the exact path.  NB = 1: one v_max3 per
+          // row and sub-tile pair; NB = 2: one v_med3(x, m, +inf) = max per row and block (an
+          // fmaxf would first canonicalize the MFMA result: 3 instructions)
           const float ibA = BIAS ? ibl[cur][TILE * u + j] : 0.f;
-          const float ibB = BIAS ? ibl[cur][TILE * (u + 1) + j] : 0.f;
+          const float ibB = BIAS && NTS == 2 ? ibl[cur][TILE * (u + 1) + j] : 0.f;
 #pragma unroll
-          for (int r = 0; r < 16; ++r)
-            rmax[r] = fmaxf(rmax[r], fmaxf(BIAS ? accA[r] + ibA : accA[r], BIAS ? accB[r] + ibB : accB[r]));
+          for (int c = 0; c < NC; ++c)
+            if (masked) apply_mask(acc[c], c % NB, baseA + TILE * (c / NB), baseA + TILE * (c / NB) + j);
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            if constexpr (NB == 1) {
+              rmax[r] = fmaxf(rmax[r], fmaxf(BIAS ? acc[0][r] + ibA : acc[0][r], BIAS ? acc[1][r] + ibB : acc[1][r]));
+            } else {
+#pragma unroll
+              for (int nb = 0; nb < NB; ++nb)
+                rmax[16 * nb + r] = __builtin_amdgcn_fmed3f(BIAS ? acc[nb][r] + ibA : acc[nb][r],
+                                                            rmax[16 * nb + r], __builtin_inff());
+            }
+          }
           continue;
         }
 #pragma unroll
-        for (int v = 0; v < 2; ++v) {
-          if (v == 1 && !hasB) break;
-          const int64_t base = v ? baseB : baseA;
+        for (int c = 0; c < NC; ++c) {
+          const int t = c / NB, nb = c % NB;
+          if (t == 1 && !hasB) break;
+          const int sub = u + t;
+          const int64_t base = tbase + TILE * sub;
           const int64_t n = base + j;
           const bool ivalid = n < part_end;
-          f32x16 acc = v ? accB : accA;
-          const float ib = BIAS ? ibl[cur][TILE * (u + v) + j] : 0.f;
-          if (masked) apply_mask(acc, base, n);
+          f32x16 sc = acc[c];
+          const float ib = BIAS ? ibl[cur][TILE * sub + j] : 0.f;
+          if (masked) apply_mask(sc, nb, base, n);
           if (MODE == DSCAN_THRESH) {
-            thresh(acc, ib, base, ivalid);
+            thresh(sc, nb, ib, base, ivalid);
             continue;
           }
 #pragma unroll
-          for (int r = 0; r < 16; ++r) acc[r] = BIAS ? acc[r] + ib : acc[r];
+          for (int r = 0; r < 16; ++r) sc[r] = BIAS ? sc[r] + ib : sc[r];
           if (MODE == DSCAN_DENSE) {
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
-              const int64_t b = b0 + mfma32_row(r, h);
-              if (ivalid && b < A.B) A.dense[b * A.ldo + n] = acc[r];
+              const int64_t b = b0 + 32 * nb + mfma32_row(r, h);
+              if (ivalid && b < A.B) A.dense[b * A.ldo + n] = sc[r];
             }
           } else {  // SAMPLE
 #pragma unroll
-            for (int r = 0; r < 16; ++r)
-              if (ivalid) rmax[r] = (acc[r] > rmax[r] || acc[r] != acc[r]) ? acc[r] : rmax[r];  // NaN sticks
+            for (int r = 0; r < 16; ++r) {
+              float& m = rmax[16 * nb + r];
+              if (ivalid) m = (sc[r] > m || sc[r] != sc[r]) ? sc[r] : m;  // NaN sticks
+            }
           }
         }
       }
@@ -572,10 +627,12 @@ __global__ __launch_bounds__(256, dcert_wg_per_cu(DP)) void dot16_scan_kernel(DS
   if (MODE == DSCAN_THRESH && lane < nu) A.cnt[(b0 + lane) * A.NP + p] = lcnt[wave][lane];
   if (MODE == DSCAN_SAMPLE) {
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int64_t b = b0 + mfma32_row(r, h);
-      if (b < A.B) A.dense[b * A.ldo + p * 32 + j] = rmax[r];
-    }
+    for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int64_t b = b0 + 32 * nb + mfma32_row(r, h);
+        if (b < A.B) A.dense[b * A.ldo + p * 32 + j] = rmax[16 * nb + r];
+      }
   }
 }
 
@@ -772,11 +829,11 @@ template <int MODE>
 void launch_dscan(hnm_ctx* ctx, dim3 grid, const DScanArgs& s, int DP, bool bias) {
 #define HNM_DS2(DPV, BV)                                                                      \
   if (s.mptr && MODE != DSCAN_DENSE)                                                          \
-    hipLaunchKernelGGL((dot16_scan_kernel<DPV, MODE, BV, MODE != DSCAN_DENSE>), grid,         \
-                       dim3(256), 0, ctx->stream, s);                                         \
+    hipLaunchKernelGGL((dot16_scan_kernel<DPV, MODE, BV, MODE != DSCAN_DENSE, dscan_nb(DPV, MODE)>), \
+                       grid, dim3(256), 0, ctx->stream, s);                                   \
   else                                                                                        \
-    hipLaunchKernelGGL((dot16_scan_kernel<DPV, MODE, BV, false>), grid, dim3(256), 0,         \
-                       ctx->stream, s);
+    hipLaunchKernelGGL((dot16_scan_kernel<DPV, MODE, BV, false, dscan_nb(DPV, MODE)>), grid,        \
+                       dim3(256), 0, ctx->stream, s);
 #define HNM_DS(DPV)    \
   if (bias) {          \
     HNM_DS2(DPV, true) \
@@ -799,13 +856,16 @@ DScanArgs dscan_args(const DotCertWs& x, const DotArgs& a) {
   s.ibs = x.ibs;
   s.B = a.B;
   s.istride = 1;
+  s.itab = a.I;
   return s;
 }
 
 }  // namespace
 
 bool dot_cert_eligible(int d, int64_t I, int K) {
-  return d <= 128 && K <= 64 && I >= DCERT_MIN_ITEMS && I >= 64 * (int64_t)K;
+  // buffer-load extents: the f16 table's bytes < 2^31 (16.7M items at d <= 64, 8.3M at 128)
+  return d <= 128 && K <= 64 && I >= DCERT_MIN_ITEMS && I >= 64 * (int64_t)K &&
+         I * (d <= 64 ? 64 : 128) * 2 < ((int64_t)1 << 31);
 }
 
 size_t dot_cert_bytes(int64_t B, int64_t I, int d, int K, int num_cus) {
@@ -820,7 +880,7 @@ hnm_status dot_cert_begin(hnm_ctx* ctx, const DotArgs& a, bool bias, void* scrat
   dcert_carve((char*)scratch, a.B, a.I, a.d, a.K, ctx->num_cus, &x);
   hnm_status st = dcert_prepare(ctx, a, sh, x);
   if (st) return st;
-  const int64_t ublocks = hnm_cdiv(a.B, 128);
+  const int64_t ublocks = hnm_cdiv(a.B, dscan_users(sh.DP, DSCAN_SAMPLE));
   DScanArgs s = dscan_args(x, a);
   s.I = sh.Ns;
   s.istride = sh.stride;
@@ -849,7 +909,7 @@ hnm_status dot_cert_finish(hnm_ctx* ctx, const DotArgs& a, bool bias, void* scra
   const DotCertShape sh = dcert_shape(a.B, a.I, a.d, a.K, ctx->num_cus);
   DotCertWs x;
   dcert_carve((char*)scratch, a.B, a.I, a.d, a.K, ctx->num_cus, &x);
-  const int64_t ublocks = hnm_cdiv(a.B, 128);
+  const int64_t ublocks = hnm_cdiv(a.B, dscan_users(sh.DP, DSCAN_THRESH));
   hipLaunchKernelGGL(dcert_tau_kernel, dim3((unsigned)hnm_cdiv(a.B, 256)), dim3(256), 0,
                      ctx->stream, lb ? lb : x.lb, x.Nu, x.ubr, x.prm, a.B, x.tau, x.flag);
   HNM_LAUNCH_CHECK();
@@ -907,10 +967,11 @@ hnm_status dot_cert_debug(hnm_ctx* ctx, const DotArgs& a, bool bias, void* scrat
   s.I = a.I;
   s.dense = approx;
   s.ldo = lda;
-  const Partition ps = xcd_partition(a.I, hnm_cdiv(a.B, 128), ctx->num_cus, sh.DP);
+  const int64_t ublocks = hnm_cdiv(a.B, dscan_users(sh.DP, DSCAN_DENSE));
+  const Partition ps = xcd_partition(a.I, ublocks, ctx->num_cus, dscan_nb(sh.DP, DSCAN_DENSE));
   s.ipp = ps.ipp;
   s.NP = ps.np;
-  launch_dscan<DSCAN_DENSE>(ctx, dim3((unsigned)ps.np, (unsigned)hnm_cdiv(a.B, 128)), s, sh.DP,
+  launch_dscan<DSCAN_DENSE>(ctx, dim3((unsigned)ps.np, (unsigned)ublocks), s, sh.DP,
                             bias);
   HNM_LAUNCH_CHECK();
   hipLaunchKernelGGL(dcert_debug_out_kernel, dim3((unsigned)hnm_cdiv(a.B * a.I, 256)), dim3(256),

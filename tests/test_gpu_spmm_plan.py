@@ -176,3 +176,75 @@ def test_legacy_plan_above_walk_limit():
     fb, fi_b = m.propagate_for(users)
     fu, fi = m.forward()
     assert torch.equal(fi_b, fi) and torch.equal(fb, fu[users])
+
+
+def _raw_graph(N, r, c, v):
+    """Device CSR (rowptr int64, col int32, val fp32; entries in (row, col) order) + a plan."""
+    import scipy.sparse as sp
+    from types import SimpleNamespace
+    A = sp.csr_matrix((v.astype(np.float32), (r, c)), shape=(N, N))  # duplicates summed
+    A.sort_indices()
+    g = SimpleNamespace(num_nodes=N,
+                        rowptr=torch.from_numpy(A.indptr.astype(np.int64)).to(DEV),
+                        col=torch.from_numpy(A.indices.astype(np.int32)).to(DEV),
+                        val=torch.from_numpy(A.data.astype(np.float32)).to(DEV))
+    plan = C.c_void_p()
+    c = _lib.ctx(g.rowptr.device)
+    _lib.check(_lib.fn("hnm_spmm_plan_create")(c, N, _lib.ptr(g.rowptr), C.byref(plan)), "plan")
+    return g, plan
+
+
+@pytest.mark.parametrize("kind", ["small_side_gathers_large", "not_bipartite", "isolated_edges"])
+def test_spmm_bipartite_side_routing(kind):
+    """The plan's bipartite-side detection (graph.hip plan_bipartite_sides) on graphs unlike the
+    H&M layout: a 3,000-row side whose rows (long AND short) gather a 200,000-row table, so that
+    side's short rows join the user-ordered walk; the same graph with two same-side edges (no
+    split exists: nothing may move); and isolated rows (self-loop only) on both sides of the
+    split.  Every case against A X in float64 (1e-5 of sum |a||x|), run-to-run bitwise, a
+    row-range call over the small side bitwise equal to the whole call, and rows_combine over
+    moved, walked, short and isolated rows bitwise equal to the layer kernel."""
+    S, I, d = 3_000, 200_000, 64
+    N = S + I
+    rng = np.random.default_rng(21)
+    deg = rng.integers(130, 400, S)
+    deg[::7] = rng.integers(1, 129, len(deg[::7]))       # short rows on the small side
+    if kind == "isolated_edges":
+        deg[-5:] = 0                                     # last rows below the split: no edge
+    u = np.repeat(np.arange(S), deg)
+    it = S + rng.integers(0, I, u.size)
+    if kind == "isolated_edges":
+        it = np.where(it < S + 5, it + 5, it)            # first rows above it: no edge
+    r = np.concatenate([u, it])
+    c = np.concatenate([it, u])
+    if kind == "not_bipartite":
+        r = np.concatenate([r, [0, 1, S + 7, S + 9]])
+        c = np.concatenate([c, [1, 0, S + 9, S + 7]])
+    loops = np.arange(0, N, 3)                            # self-loops on a third of the rows
+    r = np.concatenate([r, loops])
+    c = np.concatenate([c, loops])
+    v = rng.uniform(0.01, 1.0, r.size)
+    g, plan = _raw_graph(N, r, c, v)
+    try:
+        x = torch.randn(N, d, generator=torch.Generator().manual_seed(8)).to(DEV)
+        y1, y2, ya = torch.empty_like(x), torch.empty_like(x), torch.zeros_like(x)
+        assert _spmm_raw(g, plan, x, y1) == 0
+        assert _spmm_raw(g, plan, x, y2) == 0
+        cx = _lib.ctx(x.device)
+        assert _lib.fn("hnm_spmm_csr_range_f32")(
+            cx, plan, N, _lib.ptr(g.rowptr), _lib.ptr(g.col), _lib.ptr(g.val), _lib.ptr(x), d,
+            _lib.ptr(ya), 0.0, None, None, 0.0, 0, S, 0) == 0
+        torch.cuda.synchronize()
+        assert torch.equal(y1, y2)
+        assert torch.equal(ya[:S], y1[:S]) and not ya[S:].any()
+        ref, mag = _dense_ref(g, x)
+        err = np.abs(y1.double().cpu().numpy() - ref)
+        assert (err <= 1e-5 * mag + 1e-30).all(), float((err / (mag + 1e-30)).max())
+        short_small = np.flatnonzero(deg < 129)[:6]
+        rows = torch.tensor(list(short_small) + [1, 2, S - 1, S - 5, S, S + 4, S + 11, N - 1],
+                            dtype=torch.int64, device=DEV)
+        out = torch.empty(rows.numel(), d, device=DEV)
+        assert _combine_raw(g, plan, rows, [x], [0.0, 1.0], out) == 0
+        torch.cuda.synchronize()
+        assert torch.equal(out, y1[rows])
+    finally:
+        _lib.fn("hnm_spmm_plan_destroy")(plan)
