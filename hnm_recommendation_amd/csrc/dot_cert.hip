@@ -68,7 +68,10 @@ __host__ __device__ constexpr int dscan_nb(int DP, int MODE) {
 __host__ __device__ constexpr int dscan_users(int DP, int MODE) { return 128 * dscan_nb(DP, MODE); }
 // scan occupancy (workgroups per CU): NB = 1, two sub-tiles in flight, fits 3 in 168 VGPRs;
 // NB = 2 (two user blocks' A operands and thresholds) needs ~230: 2
-__host__ __device__ constexpr int dcert_wg_per_cu(int NB) { return NB == 2 ? 2 : 3; }
+#ifndef DOT_WG1
+#define DOT_WG1 3
+#endif
+__host__ __device__ constexpr int dcert_wg_per_cu(int NB) { return NB == 2 ? 2 : DOT_WG1; }
 
 enum { DM_U, DM_I, DM_NI, DM_IB, DM_N };
 
@@ -249,12 +252,22 @@ __global__ __launch_bounds__(256) void dcert_scales_kernel(DParams* prm, int DP,
   __shared__ float pm[4][4];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   float mi = 0.f, mn = 0.f, mb = 0.f, mu = 0.f;  // items: max|i|, max||i||, max|ib|; users: max|u|
-  for (int blk = tid; blk < item_blocks + user_blocks; blk += 256) {
-    const float* v = part + blk * 4;
-    if (blk < item_blocks) {
-      mi = nmax(mi, v[0]); mn = nmax(mn, v[1]); mb = nmax(mb, v[2]);
-    } else {
-      mu = nmax(mu, v[0]);
+  // partials in batches of 8 per thread, every load of a batch issued before the first use
+  // (this single block is latency: one L2 round trip per batch instead of one per partial)
+  const int nblk = item_blocks + user_blocks;
+  for (int b0 = 0; b0 < nblk; b0 += 8 * 256) {
+    float4 v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+      v[k] = *reinterpret_cast<const float4*>(part + 4 * std::min(b0 + 256 * k + tid, nblk - 1));
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int blk = b0 + 256 * k + tid;
+      if (blk < item_blocks) {
+        mi = nmax(mi, v[k].x); mn = nmax(mn, v[k].y); mb = nmax(mb, v[k].z);
+      } else if (blk < nblk) {
+        mu = nmax(mu, v[k].x);
+      }
     }
   }
   mi = wave_max(mi); mn = wave_max(mn); mb = wave_max(mb); mu = wave_max(mu);
@@ -370,7 +383,10 @@ __global__ __launch_bounds__(256, dcert_wg_per_cu(NB)) void dot16_scan_kernel(DS
   constexpr int KS = DP / 16;     // f16 MFMA k-steps
   constexpr int RS = DP + 8;      // LDS row stride (halfs): conflict-free b128 reads
   constexpr int CH = DP / 8;      // 16-B chunks per item row
-  constexpr int TI = DP <= 64 ? 128 : 64;  // items per LDS tile
+#ifndef DOT_TI
+#define DOT_TI 0
+#endif
+  constexpr int TI = DOT_TI > 0 ? DOT_TI : (DP <= 64 ? 128 : 64);  // items per LDS tile
   constexpr int SUB = TI / TILE;
   constexpr int LD = TI * CH / 256;  // chunks per thread per tile (4)
   constexpr int UW = 32 * NB;        // users per wave
@@ -512,7 +528,9 @@ __global__ __launch_bounds__(256, dcert_wg_per_cu(NB)) void dot16_scan_kernel(DS
       // row (ds_add_rtn), the store queued.  Measured against a scalar-unit walk of the
       // passing lanes by the rows' owner lanes: 0.094 vs 0.107 ms (the walk alone 0.027 ms of
       // it), and a per-quarter test (4 maxima, 4 ballots): 4-6 % slower
-      // (tools/dot_scan_timing.hip, profiles/r2_dot_scan_timing.txt).
+      // (tools/dot_scan_timing.hip, profiles/r2_dot_scan_timing.txt).  Round 4 on the MF step:
+      // row bits formed only for the 4-row groups with a pass (group maxima as the max tree)
+      // 0.092 vs 0.083 ms; one ballot per row with direct stores 0.105 vs 0.089 ms.
       auto thresh = [&](const f32x16& acc, int nb, float ib, int64_t base, bool ivalid) {
         float lm = acc[0];
 #pragma unroll

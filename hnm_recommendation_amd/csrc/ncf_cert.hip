@@ -211,12 +211,22 @@ __global__ __launch_bounds__(256) void cert_scales_kernel(const float* __restric
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   {  // per-block partial maxima of cert_stats_kernel: items Q G B D, users P WG
     float q = 0.f, g = 0.f, bb = 0.f, dd = 0.f, pp = 0.f, wg = 0.f;
-    for (int blk = tid; blk < item_blocks + user_blocks; blk += 256) {
-      const float* v = part + blk * 4;
-      if (blk < item_blocks) {
-        q = nmax(q, v[0]); g = nmax(g, v[1]); bb = nmax(bb, v[2]); dd = nmax(dd, v[3]);
-      } else {
-        pp = nmax(pp, v[0]); wg = nmax(wg, v[1]);
+    // partials in batches of 8 per thread: every load of a batch issued before the first use
+    // (one L2 round trip per batch instead of one per partial: this single block is latency)
+    const int nblk = item_blocks + user_blocks;
+    for (int b0 = 0; b0 < nblk; b0 += 8 * 256) {
+      float4 v[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+        v[k] = *reinterpret_cast<const float4*>(part + 4 * std::min(b0 + 256 * k + tid, nblk - 1));
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int blk = b0 + 256 * k + tid;
+        if (blk < item_blocks) {
+          q = nmax(q, v[k].x); g = nmax(g, v[k].y); bb = nmax(bb, v[k].z); dd = nmax(dd, v[k].w);
+        } else if (blk < nblk) {
+          pp = nmax(pp, v[k].x); wg = nmax(wg, v[k].y);
+        }
       }
     }
     q = wave_max(q); g = wave_max(g); bb = wave_max(bb); dd = wave_max(dd);
