@@ -68,6 +68,8 @@ __host__ __device__ constexpr int dscan_nb(int DP, int MODE) {
 __host__ __device__ constexpr int dscan_users(int DP, int MODE) { return 128 * dscan_nb(DP, MODE); }
 // scan occupancy (workgroups per CU): NB = 1, two sub-tiles in flight, fits 3 in 168 VGPRs;
 // NB = 2 (two user blocks' A operands and thresholds) needs ~230: 2
+// Round 4 A/B (MF step / THRESH scan): 3 workgroups per CU 0.1805 / 0.0832 ms, 2 per CU
+// 0.1911 / 0.0953; 64-item tiles 0.1804 / 0.0859; 256-item tiles at 2 per CU 0.1899 / 0.0923
 #ifndef DOT_WG1
 #define DOT_WG1 3
 #endif
