@@ -843,6 +843,12 @@ __global__ __launch_bounds__(256) void cert_champion_kernel(const float* __restr
 // (score desc, item asc) top-K.  Candidates sit in NP per-partition segments; a row with a
 // flagged bound, an overflowing segment or fewer than K candidates is queued for the
 // fallback.
+// k steps per LDS operand round trip in the layer-2 chain (round 4, rescore kernel under
+// rocprofv3: 1 step 67.3 us, 2 steps 65.8-66.3, 4 steps 64.8 -- the operand waits are not what
+// bounds it; the candidates' G / Q row gathers are)
+#ifndef RESCORE_STEP
+#define RESCORE_STEP 4
+#endif
 #ifndef RESCORE_ABL  // timing ablations (tools only; wrong results): 1 no top-K, 2 fixed items,
                      // 4 at most 64 candidates a row
 #define RESCORE_ABL 0
@@ -985,11 +991,12 @@ __global__ __launch_bounds__(256, 3) void ncf_rescore_kernel(
       acc[4 * r4] = bb.x; acc[4 * r4 + 1] = bb.y; acc[4 * r4 + 2] = bb.z; acc[4 * r4 + 3] = bb.w;
       wmr[4 * r4] = ww.x; wmr[4 * r4 + 1] = ww.y; wmr[4 * r4 + 2] = ww.z; wmr[4 * r4 + 3] = ww.w;
     }
+    typedef __attribute__((address_space(3))) const float* lds_ptr;
+#if RESCORE_STEP == 1
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
       // both reads issued right before their MFMA (hoisted by the compiler, they would hold
       // 64 VGPRs again and spill); operands are LDS byte offsets (address-space-3 pointers)
-      typedef __attribute__((address_space(3))) const float* lds_ptr;
       float w2v, pv;
       asm volatile("ds_read_b32 %0, %2\n\tds_read_b32 %1, %3\n\ts_waitcnt lgkmcnt(0)"
                    : "=&v"(w2v), "=&v"(pv)
@@ -997,6 +1004,43 @@ __global__ __launch_bounds__(256, 3) void ncf_rescore_kernel(
                      "v"((unsigned)(uintptr_t)(lds_ptr)&pl[wave][h * KS + s]));
       acc = mfma32x32x2(w2v, fmaxf(pv + q[s], 0.f), acc);
     }
+#elif RESCORE_STEP == 4
+    // four k steps' operands per LDS round trip
+#pragma unroll
+    for (int s = 0; s < KS; s += 4) {
+      float w[4], pv[4];
+      asm volatile("ds_read_b32 %0, %8\n\tds_read_b32 %1, %9\n\tds_read_b32 %2, %10\n\t"
+                   "ds_read_b32 %3, %11\n\tds_read_b32 %4, %12\n\tds_read_b32 %5, %13\n\t"
+                   "ds_read_b32 %6, %14\n\tds_read_b32 %7, %15\n\ts_waitcnt lgkmcnt(0)"
+                   : "=&v"(w[0]), "=&v"(w[1]), "=&v"(w[2]), "=&v"(w[3]),
+                     "=&v"(pv[0]), "=&v"(pv[1]), "=&v"(pv[2]), "=&v"(pv[3])
+                   : "v"((unsigned)(uintptr_t)(lds_ptr)&w2l[s * 64 + lane]),
+                     "v"((unsigned)(uintptr_t)(lds_ptr)&w2l[(s + 1) * 64 + lane]),
+                     "v"((unsigned)(uintptr_t)(lds_ptr)&w2l[(s + 2) * 64 + lane]),
+                     "v"((unsigned)(uintptr_t)(lds_ptr)&w2l[(s + 3) * 64 + lane]),
+                     "v"((unsigned)(uintptr_t)(lds_ptr)&pl[wave][h * KS + s]),
+                     "v"((unsigned)(uintptr_t)(lds_ptr)&pl[wave][h * KS + s + 1]),
+                     "v"((unsigned)(uintptr_t)(lds_ptr)&pl[wave][h * KS + s + 2]),
+                     "v"((unsigned)(uintptr_t)(lds_ptr)&pl[wave][h * KS + s + 3]));
+#pragma unroll
+      for (int e = 0; e < 4; ++e) acc = mfma32x32x2(w[e], fmaxf(pv[e] + q[s + e], 0.f), acc);
+    }
+#else
+    // two k steps' operands per LDS round trip (one wait per two MFMAs)
+#pragma unroll
+    for (int s = 0; s < KS; s += 2) {
+      float w0, w1, p0, p1;
+      asm volatile("ds_read_b32 %0, %4\n\tds_read_b32 %1, %5\n\tds_read_b32 %2, %6\n\t"
+                   "ds_read_b32 %3, %7\n\ts_waitcnt lgkmcnt(0)"
+                   : "=&v"(w0), "=&v"(w1), "=&v"(p0), "=&v"(p1)
+                   : "v"((unsigned)(uintptr_t)(lds_ptr)&w2l[s * 64 + lane]),
+                     "v"((unsigned)(uintptr_t)(lds_ptr)&w2l[(s + 1) * 64 + lane]),
+                     "v"((unsigned)(uintptr_t)(lds_ptr)&pl[wave][h * KS + s]),
+                     "v"((unsigned)(uintptr_t)(lds_ptr)&pl[wave][h * KS + s + 1]));
+      acc = mfma32x32x2(w0, fmaxf(p0 + q[s], 0.f), acc);
+      acc = mfma32x32x2(w1, fmaxf(p1 + q[s + 1], 0.f), acc);
+    }
+#endif
     float m4[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int r = 0; r < 16; ++r) m4[r & 3] = fmaf(fmaxf(acc[r], 0.f), wmr[r], m4[r & 3]);
