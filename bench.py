@@ -180,7 +180,9 @@ def build_workload(name, rank, world, device, batch, exact=False, weights="init"
         sd = syn.mf_state_dict(U, I, 64, seed=0)
         m = load(MatrixFactorization(U, I, sparse=False), sd, device)
         local = S.dot_shard_topk(m.user_embeddings.weight.detach(), m.item_embeddings.weight.detach(),
-                                 lo, hi, K)
+                                 lo, hi, K, user_bias=m.user_bias.weight.detach(),
+                                 item_bias=m.item_bias.weight.detach(),
+                                 const_bias=m.global_bias.detach())
         per_launch = 2.0 * 64 * batch * world * (hi - lo)
         info["_module"] = m
         info.update({"model": "MatrixFactorization", "embedding_dim": 64})

@@ -195,7 +195,8 @@ class ncf_shard_topk:
 
 
 class dot_shard_topk:
-    """Fused dot score + top-K (LightGCN / MF without biases) over item rows [lo, hi).
+    """Fused dot score + top-K (LightGCN; MF with its user / item / global biases) over item
+    rows [lo, hi).
 
     Called directly: one hnm_dot_topk_f32.  `begin` / `finish`: the two phases of
     hnm_dot_topk_begin_f32 / _finish_f32 around a cross-shard bound exchange.  `history`
@@ -204,18 +205,23 @@ class dot_shard_topk:
     per-call user rows)."""
 
     def __init__(self, user_tab: torch.Tensor, item_tab: torch.Tensor, lo: int, hi: int, k: int,
-                 history=None):
+                 history=None, user_bias=None, item_bias=None, const_bias=None):
         self.user_tab, self.shard, self.k = user_tab, item_tab[lo:hi], k
         self.lo, self.hi, self.n = lo, hi, hi - lo
         self.history = history
+        # MatrixFactorization's score terms (matrix_factorization.py:108-131): [U], [I] (the
+        # shard's slice is used), [1]; None = absent
+        self.ub = None if user_bias is None else user_bias.reshape(-1).contiguous()
+        self.ib = None if item_bias is None else item_bias.reshape(-1)[lo:hi].contiguous()
+        self.cb = None if const_bias is None else const_bias.reshape(-1).contiguous()
         self.mask_users = None   # ids the history is keyed by, when the table rows differ
         self._open = None
 
     def _common(self, u, mask=(None, None)):
         ut, sh = self.user_tab, self.shard
         return (_lib.ptr(ut), ut.shape[0], ut.stride(0), _lib.ptr(u), u.numel(), _lib.ptr(sh),
-                self.n, sh.stride(0), ut.shape[1], None, None, None, _lib.ptr(mask[0]),
-                _lib.ptr(mask[1]))
+                self.n, sh.stride(0), ut.shape[1], _lib.ptr(self.ub), _lib.ptr(self.ib),
+                _lib.ptr(self.cb), _lib.ptr(mask[0]), _lib.ptr(mask[1]))
 
     def _mask(self, u):
         return _mask(self.history, u if self.mask_users is None else self.mask_users,

@@ -193,3 +193,30 @@ def test_ncf_eight_way_rank_shape_certified_equals_exact():
     for v, i in ((v1, i1), (v2, i2)):
         assert torch.equal(i, ei)
         assert torch.equal(v.view(torch.int32), ev.view(torch.int32))
+
+
+def test_mf_shard_scorer_with_biases():
+    """The per-shard dot scorer with MatrixFactorization's user / item / global biases
+    (matrix_factorization.py:108-131; what bench.py's `mf` step runs): each shard's top-K
+    (certified path) equals the exact dense scores of that item slice, ordered (score desc,
+    item asc), bit for bit -- the whole catalogue and a middle shard of three."""
+    from hnm_recommendation_amd import MatrixFactorization
+    U2, I2 = 5000, 30000
+    sd = syn.mf_state_dict(U2, I2, 64, seed=4, bias_scale=0.05)
+    m = MatrixFactorization(U2, I2, sparse=False)
+    m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in sd.items()})
+    m = m.to("cuda:0").eval()
+    users = torch.from_numpy(syn.user_batch(U2, 257, seed=8)).cuda()
+    dense = m.predict_all_items(users).cpu().numpy()
+    for lo, hi in ((0, I2), S.shard_range(I2, 1, 3)):
+        sc = S.dot_shard_topk(m.user_embeddings.weight.detach(), m.item_embeddings.weight.detach(),
+                              lo, hi, K, user_bias=m.user_bias.weight.detach(),
+                              item_bias=m.item_bias.weight.detach(),
+                              const_bias=m.global_bias.detach())
+        v, i = sc(users)
+        v, i = v.cpu().numpy(), i.cpu().numpy()
+        for r in range(users.numel()):
+            s = dense[r, lo:hi]
+            order = np.lexsort((np.arange(hi - lo), -s))[:K]
+            assert np.array_equal(i[r], order), r
+            assert np.array_equal(v[r].view(np.uint32), s[order].view(np.uint32)), r
