@@ -1,5 +1,5 @@
 set -uo pipefail
-ROOT=$(pwd); OUT=$ROOT/gpurun_out/r4j; mkdir -p $OUT
+ROOT=$(pwd); OUT=$ROOT/gpurun_out/${TAG:-r4j}; mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
 for w in lightgcn lightgcn128; do
   echo "== prof $w $(date +%T)"
