@@ -113,6 +113,16 @@
 #ifndef SWALK_PF
 #define SWALK_PF 1
 #endif
+// Round 4, measured and dropped: aligning the workgroups of an XCD -- a bounded wait (per-XCD
+// progress counters, atomics at agent scope) before each short-walk round until all but 1/8 of
+// the XCD's workgroups finished the previous one, and the same before each of the long-row
+// walk's column windows -- so their gathers share one window of the table in that L2: d=64
+// layer 1.304 -> 1.586 ms (short walk aligned), 1.430 (walk windows), 1.699 (both); d=128
+// 2.672 -> 3.235 / 2.680 / 3.237 ms.  The waits cost more than the L2 locality returns.
+// (tools/gather_probe.hip: uniformly random 256-B rows gather at 8.4-8.6 TB/s from a 27 MB
+// table and 7.0-7.3 TB/s from 351 MB whatever the loads in flight, 23 TB/s from an
+// L2-resident 4 MB one; the two walks' 12.8 TB/s lies between: their column order already
+// serves ~62 % of the gathered bytes from L2.)
 // bipartite graphs: the short rows of the side that gathers the larger table join the walk
 #ifndef SPMM_SIDE_WALK
 #define SPMM_SIDE_WALK 1

@@ -1,13 +1,15 @@
-// Random 256-B row-gather bandwidth vs table size on MI355X: does a table that fits the
-// 256 MB Infinity Cache gather faster than one that spills to HBM?  (Premise check for
-// user-range blocking of the LightGCN SpMM item rows.)
+// Random 256-B row-gather bandwidth vs table size and loads in flight on MI355X: the
+// ceiling the LightGCN SpMM's gathers run against (user half: 27 MB item table, item half:
+// 351 MB user table at d = 64).  Round 1 measured U = 1 only (one load in flight per 16-lane
+// group); round 4 adds U = 2 / 4 / 8 independent loads per group per step.
 // Build: hipcc --offload-arch=gfx950 -O3 tools/gather_probe.hip -o build/gather_probe
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
 
-// wave per output row, 16 lanes x float4 per gathered row, 4 rows in flight per wave
-__global__ __launch_bounds__(256) void gather_sum(const float* __restrict__ X, int64_t rows,
+// wave per output row, 16 lanes x float4 per gathered row, 4 groups x U rows in flight per wave
+template <int U>
+__global__ __launch_bounds__(256) void gather_sum(const float* __restrict__ X,
                                                   const int32_t* __restrict__ idx, int64_t nnz_per_out,
                                                   int64_t nout, float* __restrict__ out) {
   const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -15,11 +17,34 @@ __global__ __launch_bounds__(256) void gather_sum(const float* __restrict__ X, i
   const int lane = threadIdx.x & 63, grp = lane >> 4, sub = lane & 15;
   float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
   const int32_t* ir = idx + r * nnz_per_out;
-  for (int64_t p = grp; p < nnz_per_out; p += 4) {
-    const float4 x = *reinterpret_cast<const float4*>(X + (int64_t)ir[p] * 64 + 4 * sub);
-    acc.x += x.x; acc.y += x.y; acc.z += x.z; acc.w += x.w;
+  for (int64_t p = grp * U; p < nnz_per_out; p += 4 * U) {  // nnz_per_out % (4 U) == 0
+    float4 x[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      x[u] = *reinterpret_cast<const float4*>(X + (int64_t)ir[p + u] * 64 + 4 * sub);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      acc.x += x[u].x; acc.y += x[u].y; acc.z += x[u].z; acc.w += x[u].w;
+    }
   }
   if (lane < 16) *reinterpret_cast<float4*>(out + r * 64 + 4 * sub) = acc;
+}
+
+template <int U>
+static float run(const float* X, const int32_t* idx, int64_t per, int64_t nout, float* out,
+                 hipEvent_t e0, hipEvent_t e1) {
+  float best = 1e30f;
+  for (int rep = 0; rep < 4; ++rep) {
+    (void)hipEventRecord(e0);
+    hipLaunchKernelGGL(gather_sum<U>, dim3((unsigned)(nout / 4)), dim3(256), 0, 0, X, idx, per,
+                       nout, out);
+    (void)hipEventRecord(e1);
+    (void)hipEventSynchronize(e1);
+    float ms;
+    (void)hipEventElapsedTime(&ms, e0, e1);
+    if (rep > 0 && ms < best) best = ms;
+  }
+  return best;
 }
 
 int main() {
@@ -36,27 +61,21 @@ int main() {
   hipEvent_t e0, e1;
   (void)hipEventCreate(&e0);
   (void)hipEventCreate(&e1);
-  for (int64_t rows : {16384L, 65536L, 262144L, 524288L, 786432L, 1048576L, 1400000L}) {
+  for (int64_t rows : {16384L, 65536L, 105542L, 262144L, 524288L, 1048576L, 1371980L}) {
     uint64_t s = 88172645463325252ull;
     for (int64_t k = 0; k < nout * per; ++k) {
       s ^= s << 13; s ^= s >> 7; s ^= s << 17;
       h[k] = (int32_t)(s % (uint64_t)rows);
     }
     (void)hipMemcpy(idx, h, nout * per * 4, hipMemcpyHostToDevice);
-    float best = 1e30f;
-    for (int rep = 0; rep < 4; ++rep) {
-      (void)hipEventRecord(e0);
-      hipLaunchKernelGGL(gather_sum, dim3((unsigned)(nout / 4)), dim3(256), 0, 0, X, rows, idx, per,
-                         nout, out);
-      (void)hipEventRecord(e1);
-      (void)hipEventSynchronize(e1);
-      float ms;
-      (void)hipEventElapsedTime(&ms, e0, e1);
-      if (rep > 0 && ms < best) best = ms;
-    }
     const double bytes = (double)nout * per * 256;
-    printf("table %7.1f MB: %.3f ms, gather %.2f TB/s\n", rows * 256.0 / 1e6, best,
-           bytes / (best * 1e-3) / 1e12);
+    const float t1 = run<1>(X, idx, per, nout, out, e0, e1);
+    const float t2 = run<2>(X, idx, per, nout, out, e0, e1);
+    const float t4 = run<4>(X, idx, per, nout, out, e0, e1);
+    const float t8 = run<8>(X, idx, per, nout, out, e0, e1);
+    printf("table %7.1f MB: gather TB/s  U=1 %.2f  U=2 %.2f  U=4 %.2f  U=8 %.2f\n",
+           rows * 256.0 / 1e6, bytes / (t1 * 1e-3) / 1e12, bytes / (t2 * 1e-3) / 1e12,
+           bytes / (t4 * 1e-3) / 1e12, bytes / (t8 * 1e-3) / 1e12);
   }
   return 0;
 }
