@@ -52,8 +52,13 @@ FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: fp32 matrix (= vector) pe
 # x 2.4 GHz (MI355X_MICROARCH.md "Peak BF16/FP16 MFMA ~2.5 PF dense")
 F16_MFMA_PEAK_TFLOPS = 2516.6
 HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md: HBM3E spec peak
-L2_GATHER_TBPS = 17.8           # MI355X_MICROARCH.md "Indexed rows": rows shared via the XCD L2
-MALL_GATHER_TBPS = 8.6          # same table: 38 MB uniformly random rows (Infinity Cache)
+# random 256-B row gathers measured on MI355X (tools/gather_probe.hip, profiles/r4x_gather_probe.txt,
+# 4 loads in flight per 16-lane group): an L2-resident 4 MB table 23.0 TB/s -- the ceiling of a
+# gather with perfect L2 locality; uniformly random rows of the LightGCN tables themselves:
+# 27 MB (the item table at d=64) 8.5 TB/s, 351 MB (the user table) 7.1 TB/s
+L2_GATHER_TBPS = 23.0
+ITEM_TABLE_GATHER_TBPS = 8.5
+USER_TABLE_GATHER_TBPS = 7.1
 K = 12
 
 
@@ -444,7 +449,7 @@ def compact_line(line):
                                               "algorithmic_per_launch", "traffic")}}
     if r.get("gather_ceiling"):
         out["roofline"]["gather_ceiling"] = {k: r["gather_ceiling"].get(k)
-                                             for k in ("bytes", "ms", "frac")}
+                                             for k in ("bytes", "ms", "frac", "vs_uniform_random")}
     for k in ("cpu_baseline", "exact_fp32", "filtered", "serving_cached_propagation",
               "pipelined_3_streams", "full_propagation_step"):
         if line.get(k):
@@ -635,16 +640,19 @@ def main():
             "source": "tools/mfma_shape_probe.hip, profiles/r2_mfma_shape_probe.txt"}
     if wl.get("gathered"):
         # gather-aware ceiling beside the algorithmic one: every CSR entry gathers one whole
-        # d-float row; MI355X_MICROARCH.md "Indexed rows": 16.8-18.8 TB/s from an XCD's L2,
-        # 8.6 TB/s for a uniformly random table in the Infinity Cache
+        # d-float row (half of them from each table); measured 256-B row-gather rates above:
+        # `frac` against perfect L2 locality, `vs_uniform_random` against the same gathers in
+        # random order (what the walks' column order buys)
         gb = wl["gathered"]
         ach = gb / (avg_kernel_ms * 1e-3) / 1e12
+        uni = gb / ((gb / 2) / ITEM_TABLE_GATHER_TBPS + (gb / 2) / USER_TABLE_GATHER_TBPS) / 1e12
         line["roofline"]["gather_ceiling"] = {
             "bytes": gb, "achieved_TBps": round(ach, 3),
-            "l2_rate_TBps": L2_GATHER_TBPS, "infinity_cache_rate_TBps": MALL_GATHER_TBPS,
+            "l2_rate_TBps": L2_GATHER_TBPS, "uniform_random_TBps": round(uni, 3),
             "ms": round(gb / (L2_GATHER_TBPS * 1e12) * 1e3, 4),
             "frac": round(ach / L2_GATHER_TBPS, 4),
-            "frac_of_infinity_cache_rate": round(ach / MALL_GATHER_TBPS, 4)}
+            "vs_uniform_random": round(ach / uni, 4),
+            "source": "tools/gather_probe.hip, profiles/r4x_gather_probe.txt"}
     if "_serving" in info and rank == 0 and world == 1 and not args.profile_only:
         # serving rate with the propagation computed once (weights unchanged between calls);
         # reported beside `value`, never as it
