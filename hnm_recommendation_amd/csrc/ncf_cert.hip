@@ -563,7 +563,7 @@ __global__ __launch_bounds__(256, HNM_SCAN_OCC) void ncf16_scan_kernel(ScanArgs 
   const int32_t* const sidx = MODE == SCAN_SAMPLE ? A.sidx : nullptr;
   // 32-bit element offsets from the (uniform) table bases: the loads take an SGPR base and a
   // VGPR offset, so no 64-bit per-lane addresses stay live across the tile loop (I * 64 <
-  // 2^31 is checked by the host)
+  // 2^31: ncf_cert_eligible)
   auto fetch = [&](int64_t base) {
     const int srow = srow_of(), sc = sc_of();
     const int n = (int)(base + srow);
@@ -1205,8 +1205,10 @@ ScanArgs scan_args(const CertWs& x, int64_t B) {
 }  // namespace
 
 bool ncf_cert_eligible(const hnm_ncf_weights* w, int K) {
+  // the scan addresses Q16 / G16 by 32-bit element offsets (item * 64 < 2^31: 33.5M items)
   return w->h1 <= 64 && w->mf <= 64 && w->h2 <= 32 && K <= 64 &&
-         w->num_items >= CERT_MIN_ITEMS && w->num_items >= 64 * (int64_t)K;
+         w->num_items >= CERT_MIN_ITEMS && w->num_items >= 64 * (int64_t)K &&
+         w->num_items * 64 < ((int64_t)1 << 31);
 }
 
 int ncf_cert_wg(const hnm_ctx* ctx) {

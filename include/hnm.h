@@ -70,7 +70,10 @@ hnm_status hnm_ctx_num_cus(hnm_ctx* ctx, int* out);
 hnm_status hnm_ctx_abort_pending(hnm_ctx* ctx);
 /* Options.  HNM_OPT_PREFILTER (default 1): NCF and dot-product top-K scan the catalogue
  * with the certified f16 pre-filter and re-score the surviving candidates in exact fp32
- * (results identical to the fp32 scan); 0 = exact fp32 scan of every item. */
+ * (results identical to the fp32 scan); 0 = exact fp32 scan of every item.  Calls outside
+ * the pre-filter's range take the exact scan whatever the option: fewer than 8,192 items or
+ * than 64 k, k > 64, the dot path with d > 128 or with an f16 item copy of 2 GiB or more
+ * (16.7M items at d <= 64, 8.3M at d <= 128), NCF layer widths beyond 64 / 32 or 33.5M items. */
 enum { HNM_OPT_PREFILTER = 1,
        HNM_OPT_STATS = 3       /* 1: count pre-filter candidates / fallback rows (diagnostics) */ };
 hnm_status hnm_ctx_set_option(hnm_ctx* ctx, int option, int64_t value);
