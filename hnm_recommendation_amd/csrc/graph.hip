@@ -123,6 +123,13 @@
 // table and 7.0-7.3 TB/s from 351 MB whatever the loads in flight, 23 TB/s from an
 // L2-resident 4 MB one; the two walks' 12.8 TB/s lies between: their column order already
 // serves ~62 % of the gathered bytes from L2.)
+// Also measured and dropped (round 4): the long-row walk split by XCD column ranges -- every
+// walk row of > SPMM_SHORT entries cut at 8 column bounds (equal shares of entries), range x's
+// pieces on workgroups of XCD x with their windows inside range x, rows_combine repeating the
+// range pieces -- bitwise-consistent (32 SpMM / LightGCN GPU tests green) but the walk ran 668
+// -> 1,155 us a launch: ~4x the pieces for the same 575 LDS slots a workgroup (d = 64) means
+// ~4x the workgroups, each a whole window sweep for a quarter of the entries, and every item
+// row then takes the partial + finish path (finish 12 -> 42 us).
 // bipartite graphs: the short rows of the side that gathers the larger table join the walk
 #ifndef SPMM_SIDE_WALK
 #define SPMM_SIDE_WALK 1
