@@ -437,6 +437,20 @@ def run_child(argv, timeout):
     return json.loads(lines[-1])
 
 
+def gather_ceiling(gathered_bytes, avg_kernel_ms):
+    """The SpMM layer's gathered rows (half from each table) against the measured 256-B
+    row-gather rates: perfect L2 locality (`frac`) and the same gathers in uniformly random
+    order (`vs_uniform_random`: what the walks' column order buys)."""
+    ach = gathered_bytes / (avg_kernel_ms * 1e-3) / 1e12                      # TB/s
+    uni = 1.0 / (0.5 / ITEM_TABLE_GATHER_TBPS + 0.5 / USER_TABLE_GATHER_TBPS)  # TB/s
+    return {"bytes": gathered_bytes, "achieved_TBps": round(ach, 3),
+            "l2_rate_TBps": L2_GATHER_TBPS, "uniform_random_TBps": round(uni, 3),
+            "ms": round(gathered_bytes / (L2_GATHER_TBPS * 1e12) * 1e3, 4),
+            "frac": round(ach / L2_GATHER_TBPS, 4),
+            "vs_uniform_random": round(ach / uni, 4),
+            "source": "tools/gather_probe.hip, profiles/r4x_gather_probe.txt"}
+
+
 def compact_line(line):
     """The fields of a workload's line that the headline line repeats under `other_configs`
     (its full line is printed on its own stdout line before the headline): small enough that
@@ -643,16 +657,7 @@ def main():
         # d-float row (half of them from each table); measured 256-B row-gather rates above:
         # `frac` against perfect L2 locality, `vs_uniform_random` against the same gathers in
         # random order (what the walks' column order buys)
-        gb = wl["gathered"]
-        ach = gb / (avg_kernel_ms * 1e-3) / 1e12
-        uni = gb / ((gb / 2) / ITEM_TABLE_GATHER_TBPS + (gb / 2) / USER_TABLE_GATHER_TBPS) / 1e12
-        line["roofline"]["gather_ceiling"] = {
-            "bytes": gb, "achieved_TBps": round(ach, 3),
-            "l2_rate_TBps": L2_GATHER_TBPS, "uniform_random_TBps": round(uni, 3),
-            "ms": round(gb / (L2_GATHER_TBPS * 1e12) * 1e3, 4),
-            "frac": round(ach / L2_GATHER_TBPS, 4),
-            "vs_uniform_random": round(ach / uni, 4),
-            "source": "tools/gather_probe.hip, profiles/r4x_gather_probe.txt"}
+        line["roofline"]["gather_ceiling"] = gather_ceiling(wl["gathered"], avg_kernel_ms)
     if "_serving" in info and rank == 0 and world == 1 and not args.profile_only:
         # serving rate with the propagation computed once (weights unchanged between calls);
         # reported beside `value`, never as it

@@ -49,3 +49,14 @@ def test_recorded_headline_fits_the_tail():
         assert len(json.dumps(head)) < 7000, f
         assert {"lightgcn", "widedeep", "lightgcn128", "mf"} <= set(head["other_configs"])
         assert "gather_ceiling" in head["other_configs"]["lightgcn"]["roofline"]
+
+
+def test_gather_ceiling_units():
+    """16.65 GB of 256-B rows in 1.30 ms = 12.8 TB/s: 0.56 of the 23 TB/s L2-resident rate and
+    ~1.65x the 7.74 TB/s of the same gathers in uniformly random order."""
+    g = bench.gather_ceiling(16.65e9, 1.30)
+    assert abs(g["achieved_TBps"] - 12.81) < 0.01
+    assert abs(g["uniform_random_TBps"] - 7.738) < 0.01
+    assert abs(g["frac"] - 12.81 / 23.0) < 0.001
+    assert 1.6 < g["vs_uniform_random"] < 1.7
+    assert abs(g["ms"] - 0.7239) < 0.001
