@@ -849,6 +849,14 @@ __global__ __launch_bounds__(256) void cert_champion_kernel(const float* __restr
 #ifndef RESCORE_STEP
 #define RESCORE_STEP 4
 #endif
+// persistent re-scoring workgroups per CU looping over rows (0 = one workgroup per 4 rows).
+// Round 4, per-rank step of the sharded NCF (tools/rank_shape_probe.py, the all_reduced
+// bounds): W = 1 2.172 -> 2.147 ms, W = 8 (32,768 rows of ~1/8 the candidates) 2.381 -> 2.284
+// ms at 3 per CU (6 per CU: 2.151 / 2.315) -- the W2 fragments are staged into LDS once per
+// workgroup instead of once per 4 rows
+#ifndef RESCORE_PERSIST
+#define RESCORE_PERSIST 3
+#endif
 #ifndef RESCORE_ABL  // timing ablations (tools only; wrong results): 1 no top-K, 2 fixed items,
                      // 4 at most 64 candidates a row
 #define RESCORE_ABL 0
@@ -870,9 +878,6 @@ __global__ __launch_bounds__(256, 3) void ncf_rescore_kernel(
   __shared__ float w2l[KS * 64];
   __shared__ __attribute__((aligned(16))) float pl[4][64];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5, j = lane & 31;
-  const int64_t b = (int64_t)blockIdx.x * 4 + wave;
-  const bool live = b < B;
-  int c = 0;
   if (tid < 32) {
     b2l[tid] = tid < h2 ? b2[tid] : 0.f;
     wml[tid] = tid < h2 ? wm[tid] : 0.f;
@@ -881,6 +886,18 @@ __global__ __launch_bounds__(256, 3) void ncf_rescore_kernel(
     const int s = e >> 6, jj = e & 31, k = 2 * s + ((e >> 5) & 1);
     w2l[e] = (jj < h2 && k < h1) ? W2[jj * h1 + k] : 0.f;
   }
+#if RESCORE_PERSIST
+  // persistent: the workgroup's shared operands loaded once, then each wave takes rows
+  // b, b + 4 * gridDim.x, ... (its per-row LDS arrays are its own: no workgroup barrier inside)
+  __syncthreads();
+  for (int64_t b = (int64_t)blockIdx.x * 4 + wave; b < B; b += (int64_t)gridDim.x * 4) {
+  const bool live = true;
+  int c = 0;
+#else
+  const int64_t b = (int64_t)blockIdx.x * 4 + wave;
+  const bool live = b < B;
+  int c = 0;
+#endif
   if (live) {
     wgs[wave][lane] = t.WGu[b * 64 + lane];  // pair-permuted wp*g_u
     pl[wave][lane] = t.Pu[b * 64 + lane];
@@ -897,8 +914,14 @@ __global__ __launch_bounds__(256, 3) void ncf_rescore_kernel(
     if (lane == 0) pref[wave][0] = 0;
     if (lane < NP) pref[wave][lane + 1] = incl;
   }
+#if RESCORE_PERSIST
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // this wave's LDS writes, then its reads
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#else
   __syncthreads();
   if (!live) return;
+#endif
 #if RESCORE_ABL & 4
   const int n = std::min(hnm_readlane_i(incl, 63), 64);
 #else
@@ -915,7 +938,11 @@ __global__ __launch_bounds__(256, 3) void ncf_rescore_kernel(
         if (b == 0) atomicAdd(&stats[0], (unsigned long long)B);
       }
     }
+#if RESCORE_PERSIST
+    continue;
+#else
     return;
+#endif
   }
   if (stats && lane == 0) {
     atomicAdd(&stats[1], (unsigned long long)n);
@@ -1057,6 +1084,9 @@ __global__ __launch_bounds__(256, 3) void ncf_rescore_kernel(
   if (abl_sink == 1234.5f) oi[b * K] = 0;
 #endif
   L.store(ov ? ov + b * K : nullptr, oi + b * K, K);
+#if RESCORE_PERSIST
+  }
+#endif
 }
 
 // scaled -> real units, for the diagnostics entry point
@@ -1301,7 +1331,9 @@ hnm_status ncf_cert_finish(hnm_ctx* ctx, const hnm_ncf_weights* w, const NcfTabs
   hnm_timer_end(ctx, HNM_TIME_SCORE);
   HNM_LAUNCH_CHECK();
   // exact fp32 re-scoring + top-K of the candidates; unusable rows -> queue
-  hipLaunchKernelGGL(ncf_rescore_kernel, dim3((unsigned)hnm_cdiv(B, 4)), dim3(256), 0, ctx->stream,
+  const int64_t rgrid = RESCORE_PERSIST ? std::min<int64_t>(hnm_cdiv(B, 4), (int64_t)RESCORE_PERSIST * ctx->num_cus)
+                                        : hnm_cdiv(B, 4);
+  hipLaunchKernelGGL(ncf_rescore_kernel, dim3((unsigned)rgrid), dim3(256), 0, ctx->stream,
                      t, w->mf, w->w2, w->h1, w->h2, w->b2, w->wp + w->mf, w->bp, B, x.flag, x.cnt,
                      x.buf, sh.part.np, sh.capp, K, short_ok, ov, oi, x.ovf_rows, x.ovf_cnt,
                      ctx->stats_on ? ctx->stats_dev : nullptr);
