@@ -788,6 +788,8 @@ extern "C" hnm_status hnm_dot_prefilter_debug_f32(hnm_ctx* ctx, const float* use
   hnm_status st = dot_validate(ctx, user_tab, num_users, ldu, user_ids, B, item_tab, num_items, ldi, d);
   if (st) return st;
   HNM_REQUIRE(approx && bound && lda >= num_items, HNM_EINVAL, "dot_prefilter_debug: bad output");
+  HNM_REQUIRE(num_items * (d <= 64 ? 64 : 128) * 2 < ((int64_t)1 << 31), HNM_EUNSUPPORTED,
+              "dot_prefilter_debug: the scan's f16 item copy must stay below 2 GiB");
   if (B <= 0) return HNM_OK;
   const bool bias = user_bias || item_bias || const_bias;
   DotArgs a = dot_args(ctx, user_tab, num_users, ldu, user_ids, B, item_tab, num_items, ldi, d,
