@@ -812,8 +812,9 @@ extern "C" hnm_status hnm_ncf_prefilter_debug_f32(hnm_ctx* ctx, const hnm_ncf_we
   if (st) return st;
   HNM_REQUIRE(ctx && user_ids && approx && bound && lda >= w->num_items, HNM_EINVAL,
               "ncf_prefilter_debug: bad argument");
-  HNM_REQUIRE(w->h1 <= 64 && w->mf <= 64, HNM_EUNSUPPORTED,
-              "ncf_prefilter_debug: the f16 pre-filter covers h1 <= 64, mf <= 64");
+  HNM_REQUIRE(w->h1 <= 64 && w->mf <= 64 && w->num_items * 64 < ((int64_t)1 << 31),
+              HNM_EUNSUPPORTED,
+              "ncf_prefilter_debug: the f16 pre-filter covers h1 <= 64, mf <= 64, < 2^25 items");
   if (B <= 0) return HNM_OK;
   NcfCall c;
   st = ncf_tables(ctx, w, user_ids, B, ncf_cert_bytes(B, w->num_items, 1, ctx->num_cus, ncf_cert_wg(ctx)), &c);
