@@ -19,6 +19,7 @@ K, B = 12, 4096
 U, I = syn.HM_USERS, syn.HM_ITEMS
 w = sys.argv[1] if len(sys.argv) > 1 else "ncf"
 WS = [int(x) for x in sys.argv[2].split(",")] if len(sys.argv) > 2 else [1, 2, 4, 8]
+IDEAL = len(sys.argv) > 3 and sys.argv[3] == "ideal"  # ncf only
 dev = torch.device("cuda", 0)
 if w == "ncf":
     sd = syn.ncf_state_dict(U, I, 64, (128, 64, 32), seed=0)
@@ -54,6 +55,10 @@ for W in WS:
         for o in others:
             lb = torch.maximum(lb, o.begin(u))
             o.abort()
+        if IDEAL:  # the single-GPU bound (the whole catalogue's sample): an exchange's best case
+            full = S.ncf_shard_topk(m, 0, I, K) if w == "ncf" else None
+            lb = torch.maximum(lb, full.begin(u))
+            full.abort()
         lbmax.append(lb)
 
     def step(s):
