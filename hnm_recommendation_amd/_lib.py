@@ -91,6 +91,8 @@ _SIGS = {
                                 _p, _p, _p]),
     "hnm_ncf_topk_f32": (_i32, [_p, C.POINTER(NcfWeights), _p, _i64, _p, _p, C.c_int, _p, _p]),
     "hnm_ncf_topk_begin_f32": (_i32, [_p, C.POINTER(NcfWeights), _p, _i64, _p, _p, C.c_int, _p]),
+    "hnm_ncf_topk_begin_lists_f32": (_i32, [_p, C.POINTER(NcfWeights), _p, _i64, _p, _p, C.c_int,
+                                            _p]),
     "hnm_ncf_topk_finish_f32": (_i32, [_p, C.POINTER(NcfWeights), _p, _i64, _p, _p, C.c_int, _p,
                                        C.c_int, _p, _p]),
     "hnm_ncf_scores_f32": (_i32, [_p, C.POINTER(NcfWeights), _p, _i64, _p, _i64]),

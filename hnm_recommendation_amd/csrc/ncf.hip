@@ -744,14 +744,13 @@ extern "C" hnm_status hnm_ncf_topk_f32(hnm_ctx* ctx, const hnm_ncf_weights* w,
 // finish scans with them.  Rows may then keep fewer than K entries (short_ok), padded with
 // (-inf, -1); the merge across shards completes them.  Exact mode (pre-filter off or not
 // eligible): begin writes -inf, finish runs the exact fused scan.
-extern "C" hnm_status hnm_ncf_topk_begin_f32(hnm_ctx* ctx, const hnm_ncf_weights* w,
-                                             const int64_t* user_ids, int64_t B,
-                                             const int64_t* mask_ptr, const int32_t* mask_idx,
-                                             int k, float* lower_bound) {
+static hnm_status ncf_topk_begin(hnm_ctx* ctx, const hnm_ncf_weights* w, const int64_t* user_ids,
+                                 int64_t B, const int64_t* mask_ptr, const int32_t* mask_idx,
+                                 int k, float* lower_bound, float* lists) {
   hnm_status st = ncf_check(w);
   if (st) return st;
-  HNM_REQUIRE(ctx && ((user_ids && lower_bound) || B == 0) && k >= 1 && k <= 64, HNM_EINVAL,
-              "ncf_topk_begin: bad argument");
+  HNM_REQUIRE(ctx && ((user_ids && (lower_bound || lists)) || B == 0) && k >= 1 && k <= 64,
+              HNM_EINVAL, "ncf_topk_begin: bad argument");
   HNM_REQUIRE(!ctx->pend.kind, HNM_EINVAL, "ncf_topk_begin: a two-phase call is already open");
   if (B <= 0) return HNM_OK;
   const bool big = w->h1 > 64 || w->mf > 64;
@@ -761,15 +760,32 @@ extern "C" hnm_status hnm_ncf_topk_begin_f32(hnm_ctx* ctx, const hnm_ncf_weights
     st = ncf_tables(ctx, w, user_ids, B,
                     ncf_cert_bytes(B, w->num_items, k, ctx->num_cus, ncf_cert_wg(ctx)), &c);
     if (st) return st;
-    st = ncf_cert_begin(ctx, w, c.t, B, mask_ptr, mask_idx, k, c.extra, lower_bound);
+    st = ncf_cert_begin(ctx, w, c.t, B, mask_ptr, mask_idx, k, c.extra, lower_bound, lists);
     if (st) return st;
   } else {
-    st = hnm_fill_f32(ctx, lower_bound, B, -__builtin_inff());
-    if (st) return st;
+    if (lower_bound && (st = hnm_fill_f32(ctx, lower_bound, B, -__builtin_inff()))) return st;
+    if (lists && (st = hnm_fill_f32(ctx, lists, B * k, -__builtin_inff()))) return st;
   }
   ctx->pend = {cert ? HNM_PEND_NCF_CERT : HNM_PEND_NCF_EXACT, B, w->num_items, k, user_ids,
                w->mlp_item};
   return HNM_OK;
+}
+
+extern "C" hnm_status hnm_ncf_topk_begin_f32(hnm_ctx* ctx, const hnm_ncf_weights* w,
+                                             const int64_t* user_ids, int64_t B,
+                                             const int64_t* mask_ptr, const int32_t* mask_idx,
+                                             int k, float* lower_bound) {
+  HNM_REQUIRE(lower_bound || B == 0, HNM_EINVAL, "ncf_topk_begin: lower_bound is NULL");
+  return ncf_topk_begin(ctx, w, user_ids, B, mask_ptr, mask_idx, k, lower_bound, nullptr);
+}
+
+extern "C" hnm_status hnm_ncf_topk_begin_lists_f32(hnm_ctx* ctx, const hnm_ncf_weights* w,
+                                                   const int64_t* user_ids, int64_t B,
+                                                   const int64_t* mask_ptr,
+                                                   const int32_t* mask_idx, int k,
+                                                   float* lower_lists) {
+  HNM_REQUIRE(lower_lists || B == 0, HNM_EINVAL, "ncf_topk_begin_lists: lower_lists is NULL");
+  return ncf_topk_begin(ctx, w, user_ids, B, mask_ptr, mask_idx, k, nullptr, lower_lists);
 }
 
 extern "C" hnm_status hnm_ncf_topk_finish_f32(hnm_ctx* ctx, const hnm_ncf_weights* w,

@@ -778,6 +778,23 @@ __global__ __launch_bounds__(256) void cert_bound_kernel(const float* __restrict
   lb[b] = (!prm->bad && __builtin_isfinite(l) && __builtin_isfinite(e)) ? l : -__builtin_inff();
 }
 
+// Per (row, r < K): the certified lower bound of the exact score of the sample's r-th best
+// item (real units, as cert_bound_kernel for the K-th), for an exchange of whole lists across
+// item shards: the K-th best of the union of every shard's lists bounds the global K-th.
+__global__ __launch_bounds__(256) void cert_bound_lists_kernel(const float* __restrict__ kth,
+                                                               int K,
+                                                               const float* __restrict__ Eu,
+                                                               const CertParams* __restrict__ prm,
+                                                               const float* __restrict__ bp,
+                                                               int64_t B, float* __restrict__ lists) {
+  const int64_t x = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (x >= B * K) return;
+  const float unit = prm->unit, e = Eu[x / K];
+  float l = (kth[x] - e) / unit + bp[0];
+  l -= fabsf(l) * 4.76837158203125e-07f;  // 2^-21
+  lists[x] = (!prm->bad && __builtin_isfinite(l) && __builtin_isfinite(e)) ? l : -__builtin_inff();
+}
+
 // Per row: the scan threshold in this call's scaled units from a lower bound L of the exact
 // K-th (real units): an item can be in the top-K only if exact >= L, i.e. approx + e_i >=
 // (L - bp) unit - Eu; minus a guard for the fp32 rounding of the test quantities (2^-18 of
@@ -1254,7 +1271,7 @@ size_t ncf_cert_bytes(int64_t B, int64_t I, int K, int num_cus, int wg) {
 // certified lower bound of the exact K-th best score (real units) into lb[B].
 hnm_status ncf_cert_begin(hnm_ctx* ctx, const hnm_ncf_weights* w, const NcfTabs& t, int64_t B,
                           const int64_t* mptr, const int32_t* midx, int K, void* scratch,
-                          float* lb) {
+                          float* lb, float* lists) {
   const int64_t I = w->num_items;
   const int wg = ncf_cert_wg(ctx);
   const CertShape sh = cert_shape(B, I, K, ctx->num_cus, wg);
@@ -1297,6 +1314,11 @@ hnm_status ncf_cert_begin(hnm_ctx* ctx, const hnm_ncf_weights* w, const NcfTabs&
   hipLaunchKernelGGL(cert_bound_kernel, dim3((unsigned)hnm_cdiv(B, 256)), dim3(256), 0,
                      ctx->stream, x.kthv, K, x.Au, x.prm, w->bp, B, lb ? lb : x.lb, x.Eu);
   HNM_LAUNCH_CHECK();
+  if (lists) {
+    hipLaunchKernelGGL(cert_bound_lists_kernel, dim3((unsigned)hnm_cdiv(B * K, 256)), dim3(256), 0,
+                       ctx->stream, x.kthv, K, x.Eu, x.prm, w->bp, B, lists);
+    HNM_LAUNCH_CHECK();
+  }
   return HNM_OK;
 }
 

@@ -30,9 +30,10 @@ hnm_status ncf_cert_topk(hnm_ctx* ctx, const hnm_ncf_weights* w, const NcfTabs& 
 // The two phases of ncf_cert_topk: begin writes each row's certified lower bound of the
 // exact K-th best score (real units) to lb (nullptr: kept in the scratch); finish takes any
 // lower bounds (e.g. the max over item shards) and completes the top-K.
+// lists (nullable): each row's K best certified sample lower bounds [B, K], real units.
 hnm_status ncf_cert_begin(hnm_ctx* ctx, const hnm_ncf_weights* w, const NcfTabs& t, int64_t B,
                           const int64_t* mptr, const int32_t* midx, int K, void* scratch,
-                          float* lb);
+                          float* lb, float* lists = nullptr);
 hnm_status ncf_cert_finish(hnm_ctx* ctx, const hnm_ncf_weights* w, const NcfTabs& t, int64_t B,
                            const int64_t* mptr, const int32_t* midx, int K, void* scratch,
                            const float* lb, int short_ok, float* ov, int64_t* oi);

@@ -432,12 +432,17 @@ __global__ __launch_bounds__(256) void sample_kth_kernel(const float* __restrict
   // K-th largest of the 64 x 4 survivors (a multiset: the value is unique whatever the tie
   // order): K rounds of popping the wave maximum off its lane's sorted list (NaN never
   // enters a list; -inf once the survivors run out)
+  // The r-th popped value (r < K) lands in out[b * K + r]: the row's K largest survivors,
+  // descending -- each a lower bound of the sample's r-th best, on distinct columns (items).
+  const bool anynan = __ballot(nan) != 0;
   float kv = -__builtin_inff();
-  for (int r = 0; r < K; ++r) {
+  int r = 0;
+  for (; r < K; ++r) {
     float m = t0;
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
     kv = m;
+    if (lane == 0 && r < K - 1) out[b * K + r] = anynan ? __builtin_nanf("") : m;
     if (m == -__builtin_inff()) break;  // wave-uniform
     const int w = __builtin_ctzll(__ballot(t0 == m));
     if (lane == w) {
@@ -447,7 +452,9 @@ __global__ __launch_bounds__(256) void sample_kth_kernel(const float* __restrict
       t3 = -__builtin_inff();
     }
   }
-  if (lane == 0) out[b * K + (K - 1)] = __ballot(nan) ? __builtin_nanf("") : kv;
+  for (++r; r < K - 1; ++r)
+    if (lane == 0) out[b * K + r] = anynan ? __builtin_nanf("") : -__builtin_inff();
+  if (lane == 0) out[b * K + (K - 1)] = anynan ? __builtin_nanf("") : kv;
 }
 
 // ------------------------------------------------------------------ host side

@@ -75,7 +75,23 @@ class ItemShardedRecommender:
         all_ids = torch.empty(G * B, dtype=ids.dtype, device=ids.device)
         dist.all_gather_into_tensor(all_ids, ids, group=self.group)
         all_ids = all_ids.to(dev)
-        if hasattr(self.local_topk, "begin"):
+        if hasattr(self.local_topk, "begin_lists"):
+            # every shard's k best sample lower bounds per user, all_gathered: the k-th best of
+            # their union is a lower bound of the user's GLOBAL k-th best (G*B*k*4 bytes)
+            try:
+                lists = stage(self.local_topk.begin_lists(all_ids).contiguous())
+                rows, kk = lists.shape
+                allv = torch.empty((G * rows, kk), dtype=lists.dtype, device=lists.device)
+                dist.all_gather_into_tensor(allv, lists, group=self.group)
+                merged = allv.to(dev).view(G, rows, kk).permute(1, 0, 2).reshape(rows, G * kk)
+                lb = torch.topk(merged, k, dim=1).values[:, k - 1].contiguous()
+            except BaseException:
+                abort = getattr(self.local_topk, "abort", None)
+                if abort is not None:
+                    abort()
+                raise
+            v, i = self.local_topk.finish(all_ids, lb)
+        elif hasattr(self.local_topk, "begin"):
             # two-phase local scorer: global lower bounds of each user's k-th best score
             try:
                 lb = stage(self.local_topk.begin(all_ids).contiguous())
@@ -176,6 +192,23 @@ class ncf_shard_topk:
                    "hnm_ncf_topk_begin_f32")
         self._open = (w, keep, u, kk, mp, mi)  # finish must pass the same ids / tables / mask
         return lb
+
+    def begin_lists(self, user_ids: torch.Tensor) -> torch.Tensor:
+        """begin with each row's k best certified sample lower bounds [B, k] (distinct items,
+        real units, descending, -inf padded) instead of one bound: the k-th best of the union
+        over the item shards bounds the GLOBAL k-th (hnm_ncf_topk_begin_lists_f32)."""
+        w, keep, u, kk = self._args(user_ids)
+        mp, mi = _mask(self.history, u, self.lo, self.hi)
+        out = torch.empty(u.numel(), kk, dtype=torch.float32, device=u.device)
+        _lib.check(_lib.fn("hnm_ncf_topk_begin_lists_f32")(
+            _lib.ctx(u.device), w, _lib.ptr(u), u.numel(), _lib.ptr(mp), _lib.ptr(mi), kk,
+            _lib.ptr(out)), "hnm_ncf_topk_begin_lists_f32")
+        self._open = (w, keep, u, kk, mp, mi)
+        if kk == self.k:
+            return out
+        lists = torch.full((u.numel(), self.k), float("-inf"), dtype=torch.float32, device=u.device)
+        lists[:, :kk] = out  # a shard of fewer than k items: equal all_gather shapes
+        return lists
 
     def abort(self):
         if self._open is not None:

@@ -200,6 +200,16 @@ hnm_status hnm_ncf_topk_f32(hnm_ctx* ctx, const hnm_ncf_weights* w, const int64_
 hnm_status hnm_ncf_topk_begin_f32(hnm_ctx* ctx, const hnm_ncf_weights* w,
                                   const int64_t* user_ids, int64_t B, const int64_t* mask_ptr,
                                   const int32_t* mask_idx, int k, float* lower_bound);
+/* As hnm_ncf_topk_begin_f32, but for each row the k best certified lower bounds of the
+ * sample's items, lower_lists[B, k] (real units, descending, -inf padded; all -inf when
+ * unknown): bounds of k DISTINCT items' exact scores, so the k-th best of the union of every
+ * item shard's lists is a lower bound of the row's global k-th best -- as tight as a
+ * single-device call's -- where the max of the shards' single bounds is only each shard's own
+ * k-th.  finish then takes that merged bound. */
+hnm_status hnm_ncf_topk_begin_lists_f32(hnm_ctx* ctx, const hnm_ncf_weights* w,
+                                        const int64_t* user_ids, int64_t B,
+                                        const int64_t* mask_ptr, const int32_t* mask_idx, int k,
+                                        float* lower_lists);
 hnm_status hnm_ncf_topk_finish_f32(hnm_ctx* ctx, const hnm_ncf_weights* w,
                                    const int64_t* user_ids, int64_t B, const int64_t* mask_ptr,
                                    const int32_t* mask_idx, int k, const float* lower_bound,

@@ -1,12 +1,13 @@
 """GPU: the multi-GPU exchange branch of `ItemShardedRecommender` through a REAL RCCL
 process group (backend "nccl" = RCCL on ROCm) -- a 1-rank group on the box's one GPU, with
 `exchange=True` forcing the collective path.  This executes, on device tensors, exactly the
-calls the 8-GPU run makes (sharding.py: `all_gather_into_tensor` of user ids,
-`all_reduce(MAX)` of the certified bounds, `all_to_all_single` of packed candidates) plus the
-HIP merge, and checks the result bit for bit against single-GPU `recommend_with_scores` for
-NCF (two-phase certified), the dot scorer on LightGCN d=128 propagated tables (two-phase
-certified) and Wide&Deep (one-shot certified).  An exception injected into the bound
-all_reduce must abort the open two-phase call so the next recommend on the same ctx works.
+calls the 8-GPU run makes (sharding.py: `all_gather_into_tensor` of user ids, of NCF's
+certified bound lists / `all_reduce(MAX)` of the dot scorer's bounds, `all_to_all_single` of
+packed candidates) plus the HIP merge, and checks the result bit for bit against single-GPU
+`recommend_with_scores` for NCF (two-phase certified), the dot scorer on LightGCN d=128
+propagated tables (two-phase certified) and Wide&Deep (one-shot certified).  An exception
+injected into either bound exchange must abort the open two-phase call so the next recommend
+on the same ctx works.
 
 The group runs in a spawned child (RCCL state stays out of the pytest process); any
 assertion in the child fails `mp.spawn`.
@@ -71,21 +72,24 @@ def _rccl_worker(rank, port):
         _same(frec.recommend(users), m.recommend_with_scores(users, filter_items=hist_d),
               "ncf rccl exchange, filtered")
 
-        # injected failure inside the exchange: the open two-phase call is aborted, the
-        # error propagates, and the same thread's ctx serves the next call
-        real = dist.all_reduce
+        # injected failure inside the exchange (NCF: the bound lists' all_gather, the call after
+        # the user ids'): the open two-phase call is aborted, the error propagates, and the
+        # same thread's ctx serves the next call
+        real = dist.all_gather_into_tensor
         calls = {"n": 0}
 
         def failing(*a, **kw):
             calls["n"] += 1
-            raise RuntimeError("injected all_reduce failure")
-        S.dist.all_reduce = failing
+            if calls["n"] == 2:
+                raise RuntimeError("injected all_gather failure")
+            return real(*a, **kw)
+        S.dist.all_gather_into_tensor = failing
         try:
             with pytest.raises(RuntimeError, match="injected"):
                 rec.recommend(users)
         finally:
-            S.dist.all_reduce = real
-        assert calls["n"] == 1 and sc._open is None
+            S.dist.all_gather_into_tensor = real
+        assert calls["n"] == 2 and sc._open is None
         _same(rec.recommend(users), ref, "ncf rccl exchange after abort")
         _same(m.recommend_with_scores(users), ref, "ncf single-GPU after abort")
 
@@ -99,6 +103,19 @@ def _rccl_worker(rank, port):
         drec = S.ItemShardedRecommender(S.dot_shard_topk(fu, fi, 0, I, K), S.hip_merge, K, 0,
                                         exchange=True)
         _same(drec.recommend(lusers), lg.recommend_with_scores(lusers), "lightgcn128 rccl")
+        # the dot scorer's exchange is the bound all_reduce(MAX): a failure there aborts too
+        real_ar = dist.all_reduce
+
+        def failing_ar(*a, **kw):
+            raise RuntimeError("injected all_reduce failure")
+        S.dist.all_reduce = failing_ar
+        try:
+            with pytest.raises(RuntimeError, match="injected"):
+                drec.recommend(lusers)
+        finally:
+            S.dist.all_reduce = real_ar
+        assert drec.local_topk._open is None
+        _same(drec.recommend(lusers), lg.recommend_with_scores(lusers), "lightgcn128 after abort")
         # the per-call-propagation scorer (what bench.py's LightGCN step runs)
         prec = S.ItemShardedRecommender(S.lightgcn_shard_topk(lg, 0, I, K), S.hip_merge, K, 0,
                                         exchange=True)

@@ -220,3 +220,44 @@ def test_mf_shard_scorer_with_biases():
             order = np.lexsort((np.arange(hi - lo), -s))[:K]
             assert np.array_equal(i[r], order), r
             assert np.array_equal(v[r].view(np.uint32), s[order].view(np.uint32)), r
+
+
+def test_ncf_bound_lists():
+    """hnm_ncf_topk_begin_lists_f32: each row's k certified sample lower bounds, descending;
+    the r-th is <= the row's exact r-th best score over the shard, and the k-th equals
+    begin's single bound bitwise.  Then the sharded protocol in one process: 4 shards' lists
+    merged (k-th of the union) and every shard finished with that bound (short rows allowed)
+    -> the merged top-k equals the single-GPU top-k bit for bit, and the merged bound is at
+    least the max of the shards' single bounds (the all_reduce protocol's)."""
+    m = _model()
+    users = torch.from_numpy(syn.user_batch(U, 333, seed=12)).cuda()
+    sc = S.ncf_shard_topk(m, 0, I, K)
+    lists = sc.begin_lists(users)
+    sc.abort()
+    lb = sc.begin(users)
+    sc.abort()
+    assert lists.shape == (users.numel(), K)
+    assert torch.equal(lists[:, K - 1].view(torch.int32), lb.view(torch.int32))
+    assert (lists[:, :-1] >= lists[:, 1:]).all()
+    exact = torch.sort(m.predict_all_items(users), dim=1, descending=True).values[:, :K]
+    assert (lists <= exact).all()
+    G = 4
+    shards = [S.ncf_shard_topk(m, *S.shard_range(I, r, G), K) for r in range(G)]
+    allv, singles = [], []
+    for s in shards:
+        allv.append(s.begin_lists(users))
+        s.abort()
+        singles.append(s.begin(users))
+        s.abort()
+    merged = torch.topk(torch.cat(allv, dim=1), K, dim=1).values[:, K - 1]
+    assert (merged >= torch.stack(singles).amax(0)).all()
+    vs, ids = [], []
+    for r, s in enumerate(shards):
+        s.begin_lists(users)
+        v, i = s.finish(users, merged)
+        lo = S.shard_range(I, r, G)[0]
+        vs.append(v)
+        ids.append(torch.where(i >= 0, i + lo, i))
+    gv, gi = S.hip_merge(torch.stack(vs), torch.stack(ids), K)
+    v1, i1 = m.recommend_with_scores(users, k=K)
+    assert torch.equal(gi, i1) and torch.equal(gv.view(torch.int32), v1.view(torch.int32))

@@ -71,13 +71,21 @@ def _worker(rank, world, port, q):
             keep = v >= lb[:, None]
             return torch.where(keep, v, torch.tensor(-np.inf)), torch.where(keep, i, torch.tensor(-1))
 
+    class TwoPhaseLists(TwoPhase):
+        """NCF's protocol: begin_lists -> each row's k best lower bounds of distinct shard
+        items (here: the shard's exact top-K values), all_gathered; the k-th best of the
+        union is the bound finish filters with."""
+        def begin_lists(self, all_ids):
+            return local_topk(all_ids)[0].clone()
+
     users = torch.from_numpy(syn.user_batch(U, B, seed=10 + rank))
     out = []
-    for scorer in (local_topk, TwoPhase()):
+    for scorer in (local_topk, TwoPhase(), TwoPhaseLists()):
         rec = S.ItemShardedRecommender(scorer, _np_merge, K, lo, rank, world)
         v, i = rec.recommend(users)
         out.append((v.numpy(), i.numpy()))
-    assert np.array_equal(out[0][1], out[1][1]) and np.array_equal(out[0][0], out[1][0])
+    for o in out[1:]:
+        assert np.array_equal(out[0][1], o[1]) and np.array_equal(out[0][0], o[0])
     q.put((rank, users.numpy(), out[1][0], out[1][1]))
     dist.barrier()
     dist.destroy_process_group()
