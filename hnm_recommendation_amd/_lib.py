@@ -81,6 +81,8 @@ _SIGS = {
                                 _p, _p, _p, C.c_int, _p, _p]),
     "hnm_dot_topk_begin_f32": (_i32, [_p, _p, _i64, _i64, _p, _i64, _p, _i64, _i64, C.c_int, _p,
                                       _p, _p, _p, _p, C.c_int, _p]),
+    "hnm_dot_topk_begin_lists_f32": (_i32, [_p, _p, _i64, _i64, _p, _i64, _p, _i64, _i64, C.c_int,
+                                            _p, _p, _p, _p, _p, C.c_int, _p]),
     "hnm_dot_topk_finish_f32": (_i32, [_p, _p, _i64, _i64, _p, _i64, _p, _i64, _i64, C.c_int, _p,
                                        _p, _p, _p, _p, C.c_int, _p, C.c_int, _p, _p]),
     "hnm_dot_prefilter_debug_f32": (_i32, [_p, _p, _i64, _i64, _p, _i64, _p, _i64, _i64, C.c_int,

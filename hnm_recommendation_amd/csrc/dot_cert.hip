@@ -679,6 +679,26 @@ __global__ __launch_bounds__(256) void dcert_bound_kernel(const float* __restric
   lb[b] = (!prm->bad && __builtin_isfinite(l) && __builtin_isfinite(E)) ? l : -__builtin_inff();
 }
 
+// Per (row, r < K): the certified lower bound of the exact score of the sample's r-th best
+// item (real units, as dcert_bound_kernel for the K-th; the sample's columns are distinct
+// items), for an exchange of whole lists across item shards: the K-th best of the union of
+// every shard's lists bounds the global K-th.  Runs after dcert_bound_kernel (reads its E).
+__global__ __launch_bounds__(256) void dcert_bound_lists_kernel(const float* __restrict__ kth,
+                                                                int K,
+                                                                const float* __restrict__ Eds,
+                                                                const float* __restrict__ ubr,
+                                                                const DParams* __restrict__ prm,
+                                                                int64_t B,
+                                                                float* __restrict__ lists) {
+  const int64_t x = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (x >= B * K) return;
+  const int64_t b = x / K;
+  const float E = Eds[b];  // E / s
+  float l = kth[x] / prm->s - E + ubr[b];
+  l -= fabsf(l) * 4.76837158203125e-07f;  // 2^-21
+  lists[x] = (!prm->bad && __builtin_isfinite(l) && __builtin_isfinite(E)) ? l : -__builtin_inff();
+}
+
 // Per row: the scan threshold (scaled units) from a lower bound L of the exact K-th: an item
 // can be in the top-K only if exact >= L, i.e. approx >= (L - ubr) s - E; minus the guard for
 // the fp32 rounding of the test quantities (2^-18 of the row's score scale, 2^-20 relative).
@@ -894,7 +914,8 @@ size_t dot_cert_bytes(int64_t B, int64_t I, int d, int K, int num_cus) {
 
 // Phase 1: bound statistics, f16 copies, the sample pass and every row's certified lower
 // bound of its exact K-th best score (real units) into lb (nullptr: kept in the scratch).
-hnm_status dot_cert_begin(hnm_ctx* ctx, const DotArgs& a, bool bias, void* scratch, float* lb) {
+hnm_status dot_cert_begin(hnm_ctx* ctx, const DotArgs& a, bool bias, void* scratch, float* lb,
+                          float* lists) {
   const DotCertShape sh = dcert_shape(a.B, a.I, a.d, a.K, ctx->num_cus);
   DotCertWs x;
   dcert_carve((char*)scratch, a.B, a.I, a.d, a.K, ctx->num_cus, &x);
@@ -919,6 +940,11 @@ hnm_status dot_cert_begin(hnm_ctx* ctx, const DotArgs& a, bool bias, void* scrat
   hipLaunchKernelGGL(dcert_bound_kernel, dim3((unsigned)hnm_cdiv(a.B, 256)), dim3(256), 0,
                      ctx->stream, x.kthv, a.K, x.Nu, x.ubr, x.prm, a.B, lb ? lb : x.lb, x.E);
   HNM_LAUNCH_CHECK();
+  if (lists) {
+    hipLaunchKernelGGL(dcert_bound_lists_kernel, dim3((unsigned)hnm_cdiv(a.B * a.K, 256)), dim3(256),
+                       0, ctx->stream, x.kthv, a.K, x.E, x.ubr, x.prm, a.B, lists);
+    HNM_LAUNCH_CHECK();
+  }
   return HNM_OK;
 }
 

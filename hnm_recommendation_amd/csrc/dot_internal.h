@@ -50,7 +50,8 @@ size_t dot_cert_bytes(int64_t B, int64_t I, int d, int K, int num_cus);
 hnm_status dot_cert_topk(hnm_ctx* ctx, const DotArgs& a, bool bias, void* scratch, float* ov,
                          int64_t* oi);
 // The two phases of dot_cert_topk (see ncf_cert_begin / ncf_cert_finish).
-hnm_status dot_cert_begin(hnm_ctx* ctx, const DotArgs& a, bool bias, void* scratch, float* lb);
+hnm_status dot_cert_begin(hnm_ctx* ctx, const DotArgs& a, bool bias, void* scratch, float* lb,
+                          float* lists = nullptr);
 hnm_status dot_cert_finish(hnm_ctx* ctx, const DotArgs& a, bool bias, void* scratch,
                            const float* lb, int short_ok, float* ov, int64_t* oi);
 // Diagnostics: approx[b, i] = the f16 scan's score (biases included), bound[b] = the row's

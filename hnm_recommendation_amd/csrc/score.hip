@@ -654,18 +654,19 @@ extern "C" hnm_status hnm_dot_topk_f32(hnm_ctx* ctx, const float* user_tab, int6
   return dot_list_pass(ctx, af, bias, cv, ci, out_val, out_idx);
 }
 
-// Two-phase hnm_dot_topk_f32 for item-sharded serving (see hnm_ncf_topk_begin_f32).
-extern "C" hnm_status hnm_dot_topk_begin_f32(hnm_ctx* ctx, const float* user_tab,
-                                             int64_t num_users, int64_t ldu,
-                                             const int64_t* user_ids, int64_t B,
-                                             const float* item_tab, int64_t num_items,
-                                             int64_t ldi, int d, const float* user_bias,
-                                             const float* item_bias, const float* const_bias,
-                                             const int64_t* mask_ptr, const int32_t* mask_idx,
-                                             int k, float* lower_bound) {
+// Two-phase hnm_dot_topk_f32 for item-sharded serving (see hnm_ncf_topk_begin_f32): one
+// lower bound per row (lower_bound) or the row's k best sample lower bounds (lists, [B, k]).
+static hnm_status dot_topk_begin(hnm_ctx* ctx, const float* user_tab, int64_t num_users,
+                                 int64_t ldu, const int64_t* user_ids, int64_t B,
+                                 const float* item_tab, int64_t num_items, int64_t ldi, int d,
+                                 const float* user_bias, const float* item_bias,
+                                 const float* const_bias, const int64_t* mask_ptr,
+                                 const int32_t* mask_idx, int k, float* lower_bound,
+                                 float* lists) {
   hnm_status st = dot_validate(ctx, user_tab, num_users, ldu, user_ids, B, item_tab, num_items, ldi, d);
   if (st) return st;
-  HNM_REQUIRE(k >= 1 && k <= 64 && (lower_bound || B == 0), HNM_EINVAL, "dot_topk_begin: bad argument");
+  HNM_REQUIRE(k >= 1 && k <= 64 && (lower_bound || lists || B == 0), HNM_EINVAL,
+              "dot_topk_begin: bad argument");
   HNM_REQUIRE(!ctx->pend.kind, HNM_EINVAL, "dot_topk_begin: a two-phase call is already open");
   if (B <= 0) return HNM_OK;
   const bool cert = ctx->prefilter && dot_cert_eligible(d, num_items, k);
@@ -676,14 +677,44 @@ extern "C" hnm_status hnm_dot_topk_begin_f32(hnm_ctx* ctx, const float* user_tab
     void* w;
     st = hnm_workspace(ctx, dot_cert_bytes(B, num_items, d, k, ctx->num_cus), &w);
     if (st) return st;
-    st = dot_cert_begin(ctx, a, bias, w, lower_bound);
+    st = dot_cert_begin(ctx, a, bias, w, lower_bound, lists);
     if (st) return st;
   } else {
-    st = hnm_fill_f32(ctx, lower_bound, B, -__builtin_inff());
-    if (st) return st;
+    if (lower_bound && (st = hnm_fill_f32(ctx, lower_bound, B, -__builtin_inff()))) return st;
+    if (lists && (st = hnm_fill_f32(ctx, lists, B * k, -__builtin_inff()))) return st;
   }
   ctx->pend = {cert ? HNM_PEND_DOT_CERT : HNM_PEND_DOT_EXACT, B, num_items, k, user_ids, item_tab};
   return HNM_OK;
+}
+
+extern "C" hnm_status hnm_dot_topk_begin_f32(hnm_ctx* ctx, const float* user_tab,
+                                             int64_t num_users, int64_t ldu,
+                                             const int64_t* user_ids, int64_t B,
+                                             const float* item_tab, int64_t num_items,
+                                             int64_t ldi, int d, const float* user_bias,
+                                             const float* item_bias, const float* const_bias,
+                                             const int64_t* mask_ptr, const int32_t* mask_idx,
+                                             int k, float* lower_bound) {
+  HNM_REQUIRE(lower_bound || B == 0, HNM_EINVAL, "dot_topk_begin: lower_bound is NULL");
+  return dot_topk_begin(ctx, user_tab, num_users, ldu, user_ids, B, item_tab, num_items, ldi, d,
+                        user_bias, item_bias, const_bias, mask_ptr, mask_idx, k, lower_bound,
+                        nullptr);
+}
+
+extern "C" hnm_status hnm_dot_topk_begin_lists_f32(hnm_ctx* ctx, const float* user_tab,
+                                                   int64_t num_users, int64_t ldu,
+                                                   const int64_t* user_ids, int64_t B,
+                                                   const float* item_tab, int64_t num_items,
+                                                   int64_t ldi, int d, const float* user_bias,
+                                                   const float* item_bias,
+                                                   const float* const_bias,
+                                                   const int64_t* mask_ptr,
+                                                   const int32_t* mask_idx, int k,
+                                                   float* lower_lists) {
+  HNM_REQUIRE(lower_lists || B == 0, HNM_EINVAL, "dot_topk_begin_lists: lower_lists is NULL");
+  return dot_topk_begin(ctx, user_tab, num_users, ldu, user_ids, B, item_tab, num_items, ldi, d,
+                        user_bias, item_bias, const_bias, mask_ptr, mask_idx, k, nullptr,
+                        lower_lists);
 }
 
 extern "C" hnm_status hnm_dot_topk_finish_f32(hnm_ctx* ctx, const float* user_tab,

@@ -204,11 +204,7 @@ class ncf_shard_topk:
             _lib.ctx(u.device), w, _lib.ptr(u), u.numel(), _lib.ptr(mp), _lib.ptr(mi), kk,
             _lib.ptr(out)), "hnm_ncf_topk_begin_lists_f32")
         self._open = (w, keep, u, kk, mp, mi)
-        if kk == self.k:
-            return out
-        lists = torch.full((u.numel(), self.k), float("-inf"), dtype=torch.float32, device=u.device)
-        lists[:, :kk] = out  # a shard of fewer than k items: equal all_gather shapes
-        return lists
+        return _pad_lists(out, self.k)
 
     def abort(self):
         if self._open is not None:
@@ -225,6 +221,15 @@ class ncf_shard_topk:
                                                       1, _lib.ptr(out_v), _lib.ptr(out_i)),
                    "hnm_ncf_topk_finish_f32")
         return _pad(out_v, out_i, self.k)
+
+
+def _pad_lists(out: torch.Tensor, k: int) -> torch.Tensor:
+    """Bound lists of a shard of fewer than k items, -inf padded to k (equal all_gather shapes)."""
+    if out.shape[1] == k:
+        return out
+    lists = torch.full((out.shape[0], k), float("-inf"), dtype=torch.float32, device=out.device)
+    lists[:, :out.shape[1]] = out
+    return lists
 
 
 class dot_shard_topk:
@@ -282,6 +287,19 @@ class dot_shard_topk:
                                                      _lib.ptr(lb)), "hnm_dot_topk_begin_f32")
         self._open = (u, kk, mask)  # finish must pass the same ids and mask
         return lb
+
+    def begin_lists(self, user_ids: torch.Tensor) -> torch.Tensor:
+        """begin with each row's k best certified sample lower bounds [B, k]
+        (hnm_dot_topk_begin_lists_f32; see ncf_shard_topk.begin_lists)."""
+        u = user_ids.to(torch.int64).contiguous()
+        kk = min(self.k, self.n)
+        mask = self._mask(u)
+        out = torch.empty(u.numel(), kk, dtype=torch.float32, device=u.device)
+        _lib.check(_lib.fn("hnm_dot_topk_begin_lists_f32")(
+            _lib.ctx(u.device), *self._common(u, mask), kk, _lib.ptr(out)),
+            "hnm_dot_topk_begin_lists_f32")
+        self._open = (u, kk, mask)
+        return _pad_lists(out, self.k)
 
     def abort(self):
         if self._open is not None:
@@ -356,6 +374,11 @@ class lightgcn_shard_topk:
         dot, rows = self._scorer(user_ids)
         self._dot = (dot, rows)
         return dot.begin(rows)
+
+    def begin_lists(self, user_ids: torch.Tensor) -> torch.Tensor:
+        dot, rows = self._scorer(user_ids)
+        self._dot = (dot, rows)
+        return dot.begin_lists(rows)
 
     def abort(self):
         if self._dot is not None:

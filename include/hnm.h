@@ -132,6 +132,15 @@ hnm_status hnm_dot_topk_begin_f32(hnm_ctx* ctx, const float* user_tab, int64_t n
                                   const float* user_bias, const float* item_bias,
                                   const float* const_bias, const int64_t* mask_ptr,
                                   const int32_t* mask_idx, int k, float* lower_bound);
+/* The begin phase with each row's k best certified sample lower bounds [B, k] (distinct
+ * items, real units, descending, -inf padded; as hnm_ncf_topk_begin_lists_f32): the caller
+ * all-gathers them over the item shards and passes the k-th best of the union to finish. */
+hnm_status hnm_dot_topk_begin_lists_f32(hnm_ctx* ctx, const float* user_tab, int64_t num_users,
+                                        int64_t ldu, const int64_t* user_ids, int64_t B,
+                                        const float* item_tab, int64_t num_items, int64_t ldi,
+                                        int d, const float* user_bias, const float* item_bias,
+                                        const float* const_bias, const int64_t* mask_ptr,
+                                        const int32_t* mask_idx, int k, float* lower_lists);
 hnm_status hnm_dot_topk_finish_f32(hnm_ctx* ctx, const float* user_tab, int64_t num_users,
                                    int64_t ldu, const int64_t* user_ids, int64_t B,
                                    const float* item_tab, int64_t num_items, int64_t ldi, int d,

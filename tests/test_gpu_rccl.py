@@ -1,9 +1,8 @@
 """GPU: the multi-GPU exchange branch of `ItemShardedRecommender` through a REAL RCCL
 process group (backend "nccl" = RCCL on ROCm) -- a 1-rank group on the box's one GPU, with
 `exchange=True` forcing the collective path.  This executes, on device tensors, exactly the
-calls the 8-GPU run makes (sharding.py: `all_gather_into_tensor` of user ids, of NCF's
-certified bound lists / `all_reduce(MAX)` of the dot scorer's bounds, `all_to_all_single` of
-packed candidates) plus the HIP merge, and checks the result bit for bit against single-GPU
+calls the 8-GPU run makes (sharding.py: `all_gather_into_tensor` of user ids and of the
+certified bound lists, `all_to_all_single` of packed candidates) plus the HIP merge, and checks the result bit for bit against single-GPU
 `recommend_with_scores` for NCF (two-phase certified), the dot scorer on LightGCN d=128
 propagated tables (two-phase certified) and Wide&Deep (one-shot certified).  An exception
 injected into either bound exchange must abort the open two-phase call so the next recommend
@@ -103,18 +102,15 @@ def _rccl_worker(rank, port):
         drec = S.ItemShardedRecommender(S.dot_shard_topk(fu, fi, 0, I, K), S.hip_merge, K, 0,
                                         exchange=True)
         _same(drec.recommend(lusers), lg.recommend_with_scores(lusers), "lightgcn128 rccl")
-        # the dot scorer's exchange is the bound all_reduce(MAX): a failure there aborts too
-        real_ar = dist.all_reduce
-
-        def failing_ar(*a, **kw):
-            raise RuntimeError("injected all_reduce failure")
-        S.dist.all_reduce = failing_ar
+        # the dot scorer's bound lists exchange: a failure there aborts too
+        calls["n"] = 0
+        S.dist.all_gather_into_tensor = failing
         try:
             with pytest.raises(RuntimeError, match="injected"):
                 drec.recommend(lusers)
         finally:
-            S.dist.all_reduce = real_ar
-        assert drec.local_topk._open is None
+            S.dist.all_gather_into_tensor = real
+        assert calls["n"] == 2 and drec.local_topk._open is None
         _same(drec.recommend(lusers), lg.recommend_with_scores(lusers), "lightgcn128 after abort")
         # the per-call-propagation scorer (what bench.py's LightGCN step runs)
         prec = S.ItemShardedRecommender(S.lightgcn_shard_topk(lg, 0, I, K), S.hip_merge, K, 0,

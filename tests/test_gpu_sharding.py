@@ -261,3 +261,53 @@ def test_ncf_bound_lists():
     gv, gi = S.hip_merge(torch.stack(vs), torch.stack(ids), K)
     v1, i1 = m.recommend_with_scores(users, k=K)
     assert torch.equal(gi, i1) and torch.equal(gv.view(torch.int32), v1.view(torch.int32))
+
+
+def test_dot_bound_lists():
+    """hnm_dot_topk_begin_lists_f32 on MF with biases: descending certified lists, the r-th
+    <= the row's exact r-th best score, the k-th equal to begin's single bound bitwise; 3
+    shards' lists merged and every shard finished with the merged bound -> the merged top-k
+    equals the exact dense top-k (score desc, item asc) bit for bit."""
+    from hnm_recommendation_amd import MatrixFactorization
+    U2, I2, G = 5000, 30000, 3
+    sd = syn.mf_state_dict(U2, I2, 64, seed=5, bias_scale=0.05)
+    m = MatrixFactorization(U2, I2, sparse=False)
+    m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in sd.items()})
+    m = m.to("cuda:0").eval()
+    users = torch.from_numpy(syn.user_batch(U2, 301, seed=9)).cuda()
+
+    def scorer(lo, hi):
+        return S.dot_shard_topk(m.user_embeddings.weight.detach(), m.item_embeddings.weight.detach(),
+                                lo, hi, K, user_bias=m.user_bias.weight.detach(),
+                                item_bias=m.item_bias.weight.detach(),
+                                const_bias=m.global_bias.detach())
+    dense = m.predict_all_items(users)
+    sc = scorer(0, I2)
+    lists = sc.begin_lists(users)
+    sc.abort()
+    lb = sc.begin(users)
+    sc.abort()
+    assert lists.shape == (users.numel(), K)
+    assert torch.equal(lists[:, K - 1].view(torch.int32), lb.view(torch.int32))
+    assert (lists[:, :-1] >= lists[:, 1:]).all()
+    assert (lists <= torch.sort(dense, dim=1, descending=True).values[:, :K]).all()
+    assert torch.isfinite(lists).all()
+    shards = [scorer(*S.shard_range(I2, r, G)) for r in range(G)]
+    allv = []
+    for s_ in shards:
+        allv.append(s_.begin_lists(users))
+        s_.abort()
+    merged = torch.topk(torch.cat(allv, dim=1), K, dim=1).values[:, K - 1].contiguous()
+    vs, ids = [], []
+    for r, s_ in enumerate(shards):
+        s_.begin_lists(users)
+        v, i = s_.finish(users, merged)
+        lo = S.shard_range(I2, r, G)[0]
+        vs.append(v)
+        ids.append(torch.where(i >= 0, i + lo, i))
+    gv, gi = S.hip_merge(torch.stack(vs), torch.stack(ids), K)
+    gv, gi, dn = gv.cpu().numpy(), gi.cpu().numpy(), dense.cpu().numpy()
+    for r in range(users.numel()):
+        order = np.lexsort((np.arange(I2), -dn[r]))[:K]
+        assert np.array_equal(gi[r], order), r
+        assert np.array_equal(gv[r].view(np.uint32), dn[r][order].view(np.uint32)), r

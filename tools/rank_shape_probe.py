@@ -52,7 +52,12 @@ for W in WS:
             m.user_embeddings.weight.detach(), m.item_embeddings.weight.detach(), olo, ohi, K,
             user_bias=m.user_bias.weight.detach(), item_bias=m.item_bias.weight.detach(),
             const_bias=m.global_bias.detach()))
-    full = S.ncf_shard_topk(m, 0, I, K) if (w == "ncf" and "ideal" in MODES) else None
+    full = None
+    if "ideal" in MODES:
+        full = S.ncf_shard_topk(m, 0, I, K) if w == "ncf" else S.dot_shard_topk(
+            m.user_embeddings.weight.detach(), m.item_embeddings.weight.detach(), 0, I, K,
+            user_bias=m.user_bias.weight.detach(), item_bias=m.item_bias.weight.detach(),
+            const_bias=m.global_bias.detach())
     bounds = {}
     for mode in MODES:
         bounds[mode] = []
