@@ -125,6 +125,7 @@ def build_workload(name, rank, world, device, batch, exact=False, weights="init"
         info["_filtered"] = lambda hist: S.ItemShardedRecommender(
             S.ncf_shard_topk(m, lo, hi, K, hist), S.hip_merge, K, lo, rank, world).recommend
         info["_module"] = m
+        info["_user_sharded"] = lambda: S.ncf_shard_topk(m, 0, I, K)
         per_launch = 4352.0 * batch * world * (hi - lo)   # 4,352 FLOP / pair
         info.update({"model": "NeuralCF", "mf_dim": 64, "mlp_dims": [128, 64, 32], "weights": weights,
                      "scan": "exact fp32" if exact else
@@ -167,6 +168,7 @@ def build_workload(name, rank, world, device, batch, exact=False, weights="init"
             S.dot_shard_topk(F[:U], F[U:], lo, hi, K), S.hip_merge, K, lo, rank,
             world).recommend)(m.propagate(g))
         info["_full_step"] = full_step
+        info["_user_sharded"] = lambda: S.lightgcn_shard_topk(m, 0, I, K)
         ret = dict(step=rec.recommend, per_launch=per_launch, bound="hbm",
                    kernel="spmm layer (spmm_swalk_kernel short rows + spmm_walk_kernel long rows + spmm_walk_finish_kernel), whole-graph layers",
                    timing=_lib.TIME_SPMM, gathered=g.nnz * d * 4.0)
@@ -175,6 +177,7 @@ def build_workload(name, rank, world, device, batch, exact=False, weights="init"
         sd = syn.widedeep_state_dict(U, I, 64, (512, 256, 128), seed=0)
         m = load(WideDeep(U, I), sd, device)
         local = S.widedeep_shard_topk(m, lo, hi, K)
+        info["_user_sharded"] = lambda: S.widedeep_shard_topk(m, 0, I, K)
         per_launch = 328450.0 * batch * world * (hi - lo)   # 328,450 FLOP / pair
         info.update({"model": "WideDeep", "embedding_dim": 64, "deep_layers": [512, 256, 128]})
         bound, kernel = "mfma", ("widedeep_score_kernel" if exact else "wdc_scan_kernel")
@@ -190,6 +193,10 @@ def build_workload(name, rank, world, device, batch, exact=False, weights="init"
                                  const_bias=m.global_bias.detach())
         per_launch = 2.0 * 64 * batch * world * (hi - lo)
         info["_module"] = m
+        info["_user_sharded"] = lambda: S.dot_shard_topk(
+            m.user_embeddings.weight.detach(), m.item_embeddings.weight.detach(), 0, I, K,
+            user_bias=m.user_bias.weight.detach(), item_bias=m.item_bias.weight.detach(),
+            const_bias=m.global_bias.detach())
         info.update({"model": "MatrixFactorization", "embedding_dim": 64})
         bound, kernel = "mfma", ("dot_score_kernel" if exact else "dot16_scan_kernel")
         cpu = ("mf", sd)
@@ -735,6 +742,20 @@ def main():
                         "recommend() calls on independent batches; what a threaded server gets"}
         except Exception as e:  # reported, never fatal
             log(f"pipelined leg failed: {e!r}")
+    if world > 1 and "_user_sharded" in info and not args.profile_only:
+        # SURVEY §8(e)'s comparison layout: every rank holds the whole catalogue and scores
+        # only its own B users (no collective); the same batches, clock and max over ranks
+        try:
+            us = info["_user_sharded"]()
+            urate = timed_rate(us, batches, min(args.steps, 20), world, B)
+            line["user_sharded_layout"] = {
+                "value": round(urate, 2), "unit": "users/s", "vs_value": round(urate / value, 4),
+                "note": "replicated item tables, each rank its own 4,096 users over all items, no "
+                        "exchange: SURVEY §8(e)'s upper-bound layout, reported beside the "
+                        "item-sharded `value`"}
+            del us
+        except Exception as e:  # reported, never fatal
+            log(f"user-sharded leg failed: {e!r}")
     if "_full_step" in info and not args.profile_only:
         full = info["_full_step"]
         full(batches[0])
