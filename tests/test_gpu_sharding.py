@@ -162,8 +162,8 @@ def test_lightgcn128_full_shape_two_rank_sharding(tmp_path):
 # ------------------------------------------------------------------ N = 8 per-rank shape
 # What one rank runs in the driver's 8-GPU scaling bench (bench.py --gpus 8, NCF default):
 # the all-gathered 8 x 4,096 users against its 1/8 item shard of the full catalogue.  One
-# process, no collective: the two-phase call with the rank's own bounds (an all_reduce(MAX)
-# over 8 ranks only raises them) and the one-shot call must both equal the exact fp32 scan
+# process, no collective: the two-phase call with the rank's own bounds (the exchanged
+# bound of 8 ranks only raises them) and the one-shot call must both equal the exact fp32 scan
 # of the shard bit for bit, with no fallback rows.
 def test_ncf_eight_way_rank_shape_certified_equals_exact():
     from hnm_recommendation_amd import _lib
@@ -311,3 +311,56 @@ def test_dot_bound_lists():
         order = np.lexsort((np.arange(I2), -dn[r]))[:K]
         assert np.array_equal(gi[r], order), r
         assert np.array_equal(gv[r].view(np.uint32), dn[r][order].view(np.uint32)), r
+
+
+def test_bound_lists_exact_mode_and_tiny_shard():
+    """Bound lists where no certified bound exists: a shard of 10 items (< K, exact path: -inf
+    lists padded to K) beside a certified 8,990-item shard, and the whole protocol with the
+    pre-filter off (every list -inf, finish = the exact scan) -> the merged top-k equals the
+    exact dense top-k bit for bit in both."""
+    from hnm_recommendation_amd import MatrixFactorization, _lib
+    U2, I2, cut = 2000, 9000, 8990
+    sd = syn.mf_state_dict(U2, I2, 64, seed=6, bias_scale=0.05)
+    m = MatrixFactorization(U2, I2, sparse=False)
+    m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in sd.items()})
+    m = m.to("cuda:0").eval()
+    users = torch.from_numpy(syn.user_batch(U2, 130, seed=3)).cuda()
+    dn = m.predict_all_items(users).cpu().numpy()
+
+    def scorer(lo, hi):
+        return S.dot_shard_topk(m.user_embeddings.weight.detach(), m.item_embeddings.weight.detach(),
+                                lo, hi, K, user_bias=m.user_bias.weight.detach(),
+                                item_bias=m.item_bias.weight.detach(),
+                                const_bias=m.global_bias.detach())
+
+    def protocol():
+        shards = [(0, cut), (cut, I2)]
+        scs = [scorer(lo, hi) for lo, hi in shards]
+        allv = []
+        for sc in scs:
+            allv.append(sc.begin_lists(users))
+            sc.abort()
+        merged = torch.topk(torch.cat(allv, dim=1), K, dim=1).values[:, K - 1].contiguous()
+        vs, ids = [], []
+        for (lo, _), sc in zip(shards, scs):
+            sc.begin_lists(users)
+            v, i = sc.finish(users, merged)
+            vs.append(v)
+            ids.append(torch.where(i >= 0, i + lo, i))
+        gv, gi = S.hip_merge(torch.stack(vs), torch.stack(ids), K)
+        gv, gi = gv.cpu().numpy(), gi.cpu().numpy()
+        for r in range(users.numel()):
+            order = np.lexsort((np.arange(I2), -dn[r]))[:K]
+            assert np.array_equal(gi[r], order), r
+            assert np.array_equal(gv[r].view(np.uint32), dn[r][order].view(np.uint32)), r
+        return allv
+
+    allv = protocol()
+    assert allv[1].shape == (users.numel(), K) and torch.isneginf(allv[1]).all()
+    assert torch.isfinite(allv[0]).all()
+    _lib.set_prefilter(users.device, False)
+    try:
+        allv = protocol()
+    finally:
+        _lib.set_prefilter(users.device, True)
+    assert all(torch.isneginf(a).all() for a in allv)
