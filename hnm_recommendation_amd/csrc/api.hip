@@ -501,6 +501,60 @@ hnm_status hnm_topk_merge_rows(hnm_ctx* ctx, const float* cv, const int32_t* ci,
   return launch_merge<int32_t>(ctx, cv, ci, B, G, gstride, bstride, kc, k, ov, oi, rows, nrows);
 }
 
+// ------------------------------------------------------------------ k-th of bound lists
+// One thread per row: a G-way merge of the row's G descending lists (heads and positions in
+// registers, G a template constant), k pops; the k-th popped value (-inf past the union).
+// The item-shard exchange's bound: ~96 values a row at G = 8, k = 12 (the wave-per-row top-K
+// merge above spends ~86 us on 32k such rows; this reads each value at most once).
+template <int G>
+__global__ __launch_bounds__(256) void lists_kth_kernel(const float* __restrict__ L, int64_t B,
+                                                        int kc, int k, float* __restrict__ out) {
+  const int64_t b = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (b >= B) return;
+  const float* row = L + b * kc;
+  const int64_t gs = B * kc;
+  float head[G];
+  int pos[G];
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    pos[g] = 0;
+    head[g] = row[g * gs];
+  }
+  float v = -__builtin_inff();
+  for (int r = 0; r < k; ++r) {
+    int best = 0;
+#pragma unroll
+    for (int g = 1; g < G; ++g)
+      if (head[g] > head[best]) best = g;
+#pragma unroll
+    for (int g = 0; g < G; ++g)
+      if (g == best) {
+        v = head[g];
+        ++pos[g];
+        head[g] = pos[g] < kc ? row[g * gs + pos[g]] : -__builtin_inff();
+      }
+  }
+  out[b] = v;
+}
+
+extern "C" hnm_status hnm_topk_lists_kth_f32(hnm_ctx* ctx, const float* lists, int64_t B,
+                                             int64_t G, int kc, int k, float* out) {
+  HNM_REQUIRE(ctx && ((lists && out) || B == 0), HNM_EINVAL, "lists_kth: NULL argument");
+  HNM_REQUIRE(G >= 1 && G <= 16 && kc >= 1 && k >= 1 && k <= kc * G, HNM_EINVAL,
+              "lists_kth: 1 <= G <= 16, 1 <= k <= G * kc");
+  if (B <= 0) return HNM_OK;
+  const dim3 grid((unsigned)hnm_cdiv(B, 256));
+  switch (G) {
+#define HNM_KTH(g) \
+  case g: hipLaunchKernelGGL(lists_kth_kernel<g>, grid, dim3(256), 0, ctx->stream, lists, B, kc, k, out); break;
+    HNM_KTH(1) HNM_KTH(2) HNM_KTH(3) HNM_KTH(4) HNM_KTH(5) HNM_KTH(6) HNM_KTH(7) HNM_KTH(8)
+    HNM_KTH(9) HNM_KTH(10) HNM_KTH(11) HNM_KTH(12) HNM_KTH(13) HNM_KTH(14) HNM_KTH(15) HNM_KTH(16)
+#undef HNM_KTH
+  }
+  HNM_LAUNCH_CHECK();
+  return HNM_OK;
+}
+
 extern "C" hnm_status hnm_topk_merge_f32(hnm_ctx* ctx, const float* cand_val,
                                          const int64_t* cand_idx, int64_t B, int64_t G,
                                          int64_t gstride, int64_t bstride, int kc, int k,

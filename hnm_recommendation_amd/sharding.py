@@ -8,10 +8,10 @@ The reference has no distributed code; this is the MI355X design:
   B*8 bytes per rank) gives every rank the G*B users of the step;
 * each rank runs the fused score + top-K kernel over its item shard for all G*B users
   (per-GPU work is the single-GPU work: weak scaling).  With the certified pre-filter the
-  local scorer runs in two phases: `begin` gives every user's certified lower bound of the
-  k-th best score over the rank's items -- a lower bound of the GLOBAL k-th too -- one
-  `all_reduce(MAX)` of those G*B floats gives every rank the best bound of all shards, and
-  `finish` keeps only items that can be in the global top-k (candidates per user stay
+  local scorer runs in two phases: `begin_lists` gives every user's k best certified sample
+  lower bounds over the rank's items (distinct items), one `all_gather` of those G*B*k floats
+  and the k-th best of their union give every rank a lower bound of the GLOBAL k-th (a scorer
+  with a single-bound `begin` gets the `all_reduce(MAX)` of those), and `finish` keeps only items that can be in the global top-k (candidates per user stay
   ~constant as G grows instead of G x; rows may come back short, padded with -inf / -1);
 * one `all_to_all` returns to every rank the G candidate lists (k score bits + global
   item ids, packed as int32 pairs) of ITS users (B*k*8 bytes per rank pair: latency-bound
@@ -44,7 +44,7 @@ def shard_range(num_items: int, rank: int, world: int) -> Tuple[int, int]:
 class ItemShardedRecommender:
     def __init__(self, local_topk: LocalTopK, merge: Merge, k: int, item_offset: int,
                  rank: int = 0, world: int = 1, group=None, exchange: Optional[bool] = None):
-        """exchange: run the collective path (all_gather, bound all_reduce, all_to_all,
+        """exchange: run the collective path (all_gather, bound exchange, all_to_all,
         merge) -- the default whenever world > 1; True forces it at world == 1 as well
         (a 1-rank process group: the RCCL calls of the multi-GPU path on one GPU)."""
         self.local_topk = local_topk
@@ -83,8 +83,7 @@ class ItemShardedRecommender:
                 rows, kk = lists.shape
                 allv = torch.empty((G * rows, kk), dtype=lists.dtype, device=lists.device)
                 dist.all_gather_into_tensor(allv, lists, group=self.group)
-                merged = allv.to(dev).view(G, rows, kk).permute(1, 0, 2).reshape(rows, G * kk)
-                lb = torch.topk(merged, k, dim=1).values[:, k - 1].contiguous()
+                lb = _kth_of_lists(allv.to(dev).view(G, rows, kk), k)
             except BaseException:
                 abort = getattr(self.local_topk, "abort", None)
                 if abort is not None:
@@ -118,6 +117,20 @@ class ItemShardedRecommender:
 
 
 # ------------------------------------------------------------------ HIP wiring
+def _kth_of_lists(allv: torch.Tensor, k: int) -> torch.Tensor:
+    """[G, B, kc] bound lists (each row descending) -> [B] the k-th best of each row's union.
+    On the GPU one thread per row merges the G lists (hnm_topk_lists_kth_f32); host tensors
+    (the CPU tests' scorers) and G > 16 use torch.topk over the concatenation."""
+    G, B, kc = allv.shape
+    if not allv.is_cuda or G > 16:
+        return torch.topk(allv.permute(1, 0, 2).reshape(B, G * kc), k, dim=1).values[:, k - 1].contiguous()
+    allv = allv.contiguous()
+    out = torch.empty(B, dtype=torch.float32, device=allv.device)
+    _lib.check(_lib.fn("hnm_topk_lists_kth_f32")(_lib.ctx(allv.device), _lib.ptr(allv), B, G, kc,
+                                                 k, _lib.ptr(out)), "hnm_topk_lists_kth_f32")
+    return out
+
+
 def _pad(v, i, k):
     """Keep k candidate columns on every rank (equal all_to_all splits) for tiny shards."""
     if v.shape[1] == k:

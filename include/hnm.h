@@ -355,6 +355,13 @@ hnm_status hnm_topk_merge_f32(hnm_ctx* ctx, const float* cand_val, const int64_t
                               int64_t B, int64_t G, int64_t gstride, int64_t bstride,
                               int kc, int k, float* out_val, int64_t* out_idx);
 
+/* The item-shard bound exchange's merge: lists[g*B*kc + b*kc + j] (g < G <= 16, j < kc), each
+ * row of each list in descending order (hnm_{ncf,dot}_topk_begin_lists_f32's output,
+ * all-gathered); out[b] = the k-th best value of row b's union of the G lists (k <= G*kc).
+ * New (the reference has no multi-GPU path): sharding.py's exchange calls it. */
+hnm_status hnm_topk_lists_kth_f32(hnm_ctx* ctx, const float* lists, int64_t B, int64_t G,
+                                  int kc, int k, float* out);
+
 /* Diagnostics of the certified split-f16 pre-filter of hnm_widedeep_topk_f32 (no reference
  * counterpart): approx[b, i] = the scan's score, bound[b, i] = its certified error bound;
  * |approx - exact| <= bound for every pair (tests check it on the full catalogue). */

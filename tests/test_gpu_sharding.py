@@ -364,3 +364,17 @@ def test_bound_lists_exact_mode_and_tiny_shard():
     finally:
         _lib.set_prefilter(users.device, True)
     assert all(torch.isneginf(a).all() for a in allv)
+
+
+def test_kth_of_lists_matches_torch_topk():
+    """The exchange's k-th best of G descending bound lists (hnm_topk_lists_kth_f32) equals
+    torch.topk over their concatenation bit for bit, with -inf tails, ties, G = 1 and 16."""
+    g = torch.Generator().manual_seed(5)
+    for G, B, kk in ((8, 1000, K), (1, 77, K), (3, 513, 64), (16, 300, 5)):
+        v = torch.randn(G, B, kk, generator=g)
+        v[v < -1.2] = float("-inf")                     # short rows' padding
+        v[:, ::7, :] = torch.round(v[:, ::7, :] * 4) / 4  # ties across shards
+        v = torch.sort(v, dim=2, descending=True).values.cuda()
+        got = S._kth_of_lists(v, kk)
+        ref = torch.topk(v.permute(1, 0, 2).reshape(B, G * kk), kk, dim=1).values[:, kk - 1]
+        assert torch.equal(got.view(torch.int32), ref.view(torch.int32)), (G, B, kk)
