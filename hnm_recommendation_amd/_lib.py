@@ -81,6 +81,8 @@ _SIGS = {
                                 _p, _p, _p, C.c_int, _p, _p]),
     "hnm_dot_topk_begin_f32": (_i32, [_p, _p, _i64, _i64, _p, _i64, _p, _i64, _i64, C.c_int, _p,
                                       _p, _p, _p, _p, C.c_int, _p]),
+    "hnm_pack_candidates_i32": (_i32, [_p, _p, _p, _i64, _i64, _p]),
+    "hnm_topk_merge_sorted_pairs_i32": (_i32, [_p, _p, _i64, _i64, C.c_int, C.c_int, _p, _p]),
     "hnm_topk_lists_kth_f32": (_i32, [_p, _p, _i64, _i64, C.c_int, C.c_int, _p]),
     "hnm_dot_topk_begin_lists_f32": (_i32, [_p, _p, _i64, _i64, _p, _i64, _p, _i64, _i64, C.c_int,
                                             _p, _p, _p, _p, _p, C.c_int, _p]),

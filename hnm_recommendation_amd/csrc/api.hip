@@ -555,6 +555,91 @@ extern "C" hnm_status hnm_topk_lists_kth_f32(hnm_ctx* ctx, const float* lists, i
   return HNM_OK;
 }
 
+// ------------------------------------------------------------------ exchange candidates
+// The item-shard exchange's candidate lists travel as int32 pairs (score bits, global item
+// id): one all_to_all.  pack: shard-local ids + offset (-1 stays -1) next to the score bits.
+__global__ __launch_bounds__(256) void pack_pairs_kernel(const float* __restrict__ v,
+                                                         const int64_t* __restrict__ idx,
+                                                         int64_t n, int64_t offset,
+                                                         int2* __restrict__ out) {
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (e >= n) return;
+  const int64_t i = idx[e];
+  out[e] = make_int2(__float_as_int(v[e]), i >= 0 ? (int)(i + offset) : (int)i);
+}
+
+extern "C" hnm_status hnm_pack_candidates_i32(hnm_ctx* ctx, const float* val, const int64_t* idx,
+                                              int64_t n, int64_t offset, int32_t* pairs) {
+  HNM_REQUIRE(ctx && ((val && idx && pairs) || n <= 0), HNM_EINVAL, "pack_candidates: NULL argument");
+  HNM_REQUIRE(((uintptr_t)pairs & 7) == 0, HNM_EINVAL, "pack_candidates: pairs must be 8-byte aligned");
+  if (n <= 0) return HNM_OK;
+  hipLaunchKernelGGL(pack_pairs_kernel, dim3((unsigned)hnm_cdiv(n, 256)), dim3(256), 0, ctx->stream,
+                     val, idx, n, offset, (int2*)pairs);
+  HNM_LAUNCH_CHECK();
+  return HNM_OK;
+}
+
+// merge: one thread per row, a G-way merge of G lists each sorted in the top-K order (score
+// desc, id asc; empty slots = id < 0 at the tail), k pops -> the same [B, k] as
+// topk_merge_kernel over the same candidates (empty slots out as (-inf, -1)).
+template <int G>
+__global__ __launch_bounds__(256) void merge_sorted_pairs_kernel(const int2* __restrict__ P,
+                                                                 int64_t B, int kc, int k,
+                                                                 float* __restrict__ ov,
+                                                                 int64_t* __restrict__ oi) {
+  const int64_t b = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (b >= B) return;
+  const int2* row = P + b * kc;
+  const int64_t gs = B * kc;
+  float hv[G];
+  int hi[G], pos[G];
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    pos[g] = 0;
+    const int2 e = row[g * gs];
+    hv[g] = e.y >= 0 ? __int_as_float(e.x) : -__builtin_inff();
+    hi[g] = e.y >= 0 ? e.y : HNM_SENTINEL_IDX;
+  }
+  for (int r = 0; r < k; ++r) {
+    int best = 0;
+#pragma unroll
+    for (int g = 1; g < G; ++g)
+      if (hnm_better(hv[g], hi[g], hv[best], hi[best])) best = g;
+#pragma unroll
+    for (int g = 0; g < G; ++g)
+      if (g == best) {
+        ov[b * k + r] = hv[g];
+        oi[b * k + r] = hi[g] == HNM_SENTINEL_IDX ? -1 : hi[g];
+        ++pos[g];
+        const int2 e = pos[g] < kc ? row[g * gs + pos[g]] : make_int2(0, -1);
+        hv[g] = e.y >= 0 ? __int_as_float(e.x) : -__builtin_inff();
+        hi[g] = e.y >= 0 ? e.y : HNM_SENTINEL_IDX;
+      }
+  }
+}
+
+extern "C" hnm_status hnm_topk_merge_sorted_pairs_i32(hnm_ctx* ctx, const int32_t* pairs,
+                                                      int64_t B, int64_t G, int kc, int k,
+                                                      float* out_val, int64_t* out_idx) {
+  HNM_REQUIRE(ctx && ((pairs && out_val && out_idx) || B == 0), HNM_EINVAL,
+              "merge_sorted_pairs: NULL argument");
+  HNM_REQUIRE(G >= 1 && G <= 16 && kc >= 1 && k >= 1 && k <= 128, HNM_EINVAL,
+              "merge_sorted_pairs: 1 <= G <= 16, kc >= 1, 1 <= k <= 128");
+  HNM_REQUIRE(((uintptr_t)pairs & 7) == 0, HNM_EINVAL, "merge_sorted_pairs: pairs must be 8-byte aligned");
+  if (B <= 0) return HNM_OK;
+  const dim3 grid((unsigned)hnm_cdiv(B, 256));
+  const int2* P = (const int2*)pairs;
+  switch (G) {
+#define HNM_MSP(g) \
+  case g: hipLaunchKernelGGL(merge_sorted_pairs_kernel<g>, grid, dim3(256), 0, ctx->stream, P, B, kc, k, out_val, out_idx); break;
+    HNM_MSP(1) HNM_MSP(2) HNM_MSP(3) HNM_MSP(4) HNM_MSP(5) HNM_MSP(6) HNM_MSP(7) HNM_MSP(8)
+    HNM_MSP(9) HNM_MSP(10) HNM_MSP(11) HNM_MSP(12) HNM_MSP(13) HNM_MSP(14) HNM_MSP(15) HNM_MSP(16)
+#undef HNM_MSP
+  }
+  HNM_LAUNCH_CHECK();
+  return HNM_OK;
+}
+
 extern "C" hnm_status hnm_topk_merge_f32(hnm_ctx* ctx, const float* cand_val,
                                          const int64_t* cand_idx, int64_t B, int64_t G,
                                          int64_t gstride, int64_t bstride, int kc, int k,

@@ -103,14 +103,20 @@ class ItemShardedRecommender:
             v, i = self.local_topk.finish(all_ids, lb.to(dev))  # [G*B, k], shard-local ids
         else:
             v, i = self.local_topk(all_ids)  # [G*B, k], shard-local ids
-        i = torch.where(i >= 0, i + self.item_offset, i)
         # ONE exchange: (score bits, global item id) packed as int32 pairs -- item ids are
         # < 2^31 -- so values and ids travel in a single all_to_all (B*k*8 bytes per pair)
-        packed = torch.stack([v.contiguous().view(torch.int32), i.to(torch.int32)], dim=-1)
-        packed = stage(packed.reshape(-1))
+        pm = getattr(self.merge, "packed", None)   # (pack, merge) HIP kernels on device
+        if pm is not None and v.is_cuda:
+            packed = stage(pm[0](v, i, self.item_offset).reshape(-1))
+        else:
+            i = torch.where(i >= 0, i + self.item_offset, i)
+            packed = torch.stack([v.contiguous().view(torch.int32), i.to(torch.int32)], dim=-1)
+            packed = stage(packed.reshape(-1))
         recv = torch.empty_like(packed)
         dist.all_to_all_single(recv, packed, group=self.group)
         recv = recv.to(dev).view(G, B, k, 2)
+        if pm is not None and recv.is_cuda:
+            return pm[1](recv, k)
         rv = recv.view(torch.float32)[..., 0].contiguous()
         ri = recv[..., 1].to(torch.int64)
         return self.merge(rv, ri, k)
@@ -152,6 +158,34 @@ def hip_merge(cand_v: torch.Tensor, cand_i: torch.Tensor, k: int):
                                              kc, kc, k, _lib.ptr(out_v), _lib.ptr(out_i)),
                "hnm_topk_merge_f32")
     return out_v, out_i
+
+
+def _pack_pairs(v: torch.Tensor, i: torch.Tensor, offset: int) -> torch.Tensor:
+    """[R, k] scores + shard-local ids -> [R, k, 2] int32 (score bits, global id; -1 stays)."""
+    v, i = v.contiguous(), i.to(torch.int64).contiguous()
+    out = torch.empty(v.shape + (2,), dtype=torch.int32, device=v.device)
+    _lib.check(_lib.fn("hnm_pack_candidates_i32")(_lib.ctx(v.device), _lib.ptr(v), _lib.ptr(i),
+                                                  v.numel(), offset, _lib.ptr(out)),
+               "hnm_pack_candidates_i32")
+    return out
+
+
+def _merge_pairs(recv: torch.Tensor, k: int):
+    """[G, B, kc, 2] received pairs, each list in top-K order -> [B, k] (scores, global ids)."""
+    G, B, kc, _ = recv.shape
+    if G > 16:
+        rv = recv.view(torch.float32)[..., 0].contiguous()
+        return hip_merge(rv, recv[..., 1].to(torch.int64), k)
+    recv = recv.contiguous()
+    out_v = torch.empty(B, k, dtype=torch.float32, device=recv.device)
+    out_i = torch.empty(B, k, dtype=torch.int64, device=recv.device)
+    _lib.check(_lib.fn("hnm_topk_merge_sorted_pairs_i32")(
+        _lib.ctx(recv.device), _lib.ptr(recv), B, G, kc, k, _lib.ptr(out_v), _lib.ptr(out_i)),
+        "hnm_topk_merge_sorted_pairs_i32")
+    return out_v, out_i
+
+
+hip_merge.packed = (_pack_pairs, _merge_pairs)
 
 
 def _mask(history, u, lo, hi):

@@ -355,6 +355,17 @@ hnm_status hnm_topk_merge_f32(hnm_ctx* ctx, const float* cand_val, const int64_t
                               int64_t B, int64_t G, int64_t gstride, int64_t bstride,
                               int kc, int k, float* out_val, int64_t* out_idx);
 
+/* The item-shard exchange's candidate lists as int32 pairs (one all_to_all): pairs[2e] = the
+ * bits of val[e], pairs[2e+1] = idx[e] + offset (idx < 0 stays; global ids < 2^31); pairs
+ * 8-byte aligned. */
+hnm_status hnm_pack_candidates_i32(hnm_ctx* ctx, const float* val, const int64_t* idx, int64_t n,
+                                   int64_t offset, int32_t* pairs);
+/* Merge of received pairs [G][B][kc][2] (G <= 16), each list sorted in the top-K order (score
+ * desc, id asc; id < 0 = empty, at the tail) -> out [B, k] sorted, empty slots (-inf, -1):
+ * the same result as hnm_topk_merge_f32 over the unpacked candidates. */
+hnm_status hnm_topk_merge_sorted_pairs_i32(hnm_ctx* ctx, const int32_t* pairs, int64_t B,
+                                           int64_t G, int kc, int k, float* out_val,
+                                           int64_t* out_idx);
 /* The item-shard bound exchange's merge: lists[g*B*kc + b*kc + j] (g < G <= 16, j < kc), each
  * row of each list in descending order (hnm_{ncf,dot}_topk_begin_lists_f32's output,
  * all-gathered); out[b] = the k-th best value of row b's union of the G lists (k <= G*kc).

@@ -378,3 +378,31 @@ def test_kth_of_lists_matches_torch_topk():
         got = S._kth_of_lists(v, kk)
         ref = torch.topk(v.permute(1, 0, 2).reshape(B, G * kk), kk, dim=1).values[:, kk - 1]
         assert torch.equal(got.view(torch.int32), ref.view(torch.int32)), (G, B, kk)
+
+
+def test_packed_pairs_merge_matches_hip_merge():
+    """The exchange's pack (score bits + global id) and G-way merge of sorted lists equal the
+    unpacked candidates through hnm_topk_merge_f32 bit for bit: ties across shards (id
+    order), short lists padded (-inf, -1), G = 1, 8 and 16, k below / equal / above kc."""
+    g = torch.Generator().manual_seed(9)
+    for G, B, kc, k in ((8, 700, K, K), (1, 50, K, K), (16, 129, 5, 12), (3, 64, 20, 7)):
+        vs, ids, offs = [], [], []
+        for s in range(G):
+            n = 40
+            sc = torch.round(torch.randn(B, n, generator=g) * 3) / 3   # many ties
+            order = torch.argsort(-sc, dim=1, stable=True)[:, :kc]      # (score desc, id asc)
+            v = torch.gather(sc, 1, order)
+            i = order.clone()
+            short = torch.rand(B, generator=g) < 0.2                    # short rows
+            v[short, kc // 2:] = float("-inf")
+            i[short, kc // 2:] = -1
+            vs.append(v)
+            ids.append(i)
+            offs.append(s * n)
+        packed = torch.stack([S._pack_pairs(v.cuda(), i.cuda(), o) for v, i, o in zip(vs, ids, offs)])
+        got_v, got_i = S._merge_pairs(packed, k)
+        rv = torch.stack(vs).cuda()
+        ri = torch.stack([torch.where(i >= 0, i + o, i) for i, o in zip(ids, offs)]).cuda()
+        ref_v, ref_i = S.hip_merge(rv, ri, k)
+        assert torch.equal(got_i, ref_i), (G, B, kc, k)
+        assert torch.equal(got_v.view(torch.int32), ref_v.view(torch.int32)), (G, B, kc, k)
