@@ -60,6 +60,9 @@ L2_GATHER_TBPS = 23.0
 ITEM_TABLE_GATHER_TBPS = 8.5
 USER_TABLE_GATHER_TBPS = 7.1
 K = 12
+# trained-like weight sets (synthetic.stress_state_dict; the certified bounds' stress cases of
+# tests/test_gpu_bound_stress.py): embedding rows at norms 50-200 / Student-t(3) weights and biases
+STRESS_WEIGHTS = ("norms", "student_t")
 
 
 def log(*a):
@@ -118,8 +121,11 @@ def build_workload(name, rank, world, device, batch, exact=False, weights="init"
     lo, hi = S.shard_range(I, rank, world)
     info = {}
     if name == "ncf":
-        kw = dict(bias_scale=0.05, emb_scale=20.0) if weights == "personal" else {}
+        kw = (dict(bias_scale=0.05, emb_scale=20.0) if weights == "personal" else
+              dict(bias_scale=0.05) if weights in STRESS_WEIGHTS else {})
         sd = syn.ncf_state_dict(U, I, 64, (128, 64, 32), seed=0, **kw)
+        if weights in STRESS_WEIGHTS:
+            sd = syn.stress_state_dict(sd, weights, syn.NCF_EMB_KEYS, "mlp_item_embedding.weight")
         m = load(NeuralCF(U, I), sd, device)
         local = S.ncf_shard_topk(m, lo, hi, K)
         info["_filtered"] = lambda hist: S.ItemShardedRecommender(
@@ -185,7 +191,12 @@ def build_workload(name, rank, world, device, batch, exact=False, weights="init"
                         "certified f16 (layers 2 and 3: one W_hi.x_hi MFMA pass each; weight and activation residuals bounded exactly, the layer-2 bound terms on the matrix pipe) pre-filter + exact fp32 re-scoring")
         cpu = ("widedeep", None)
     elif name == "mf":
-        sd = syn.mf_state_dict(U, I, 64, seed=0)
+        if weights == "personal":
+            raise SystemExit("--weights personal: NCF only (MF's init best items are already "
+                             "user-specific)")
+        sd = syn.mf_state_dict(U, I, 64, seed=0, bias_scale=0.05 if weights in STRESS_WEIGHTS else 0.0)
+        if weights in STRESS_WEIGHTS:
+            sd = syn.stress_state_dict(sd, weights, syn.MF_EMB_KEYS, "item_embeddings.weight")
         m = load(MatrixFactorization(U, I, sparse=False), sd, device)
         local = S.dot_shard_topk(m.user_embeddings.weight.detach(), m.item_embeddings.weight.detach(),
                                  lo, hi, K, user_bias=m.user_bias.weight.detach(),
@@ -197,7 +208,7 @@ def build_workload(name, rank, world, device, batch, exact=False, weights="init"
             m.user_embeddings.weight.detach(), m.item_embeddings.weight.detach(), 0, I, K,
             user_bias=m.user_bias.weight.detach(), item_bias=m.item_bias.weight.detach(),
             const_bias=m.global_bias.detach())
-        info.update({"model": "MatrixFactorization", "embedding_dim": 64})
+        info.update({"model": "MatrixFactorization", "embedding_dim": 64, "weights": weights})
         bound, kernel = "mfma", ("dot_score_kernel" if exact else "dot16_scan_kernel")
         cpu = ("mf", sd)
     else:
@@ -500,6 +511,24 @@ def run_extras(args):
             line["config"]["baseline_config"] = what
             full[w] = line
             out[w] = compact_line(line)
+    # pruning robustness: the certified NCF / MF steps on weights less
+    # favourable to the pruning than the init -- NCF "personal" (user-specific best items) and
+    # the trained-like stress sets; step time, candidates re-scored per row, fallback rows
+    rob = {}
+    for w, ws in (("ncf", ("personal", "norms", "student_t")), ("mf", ("norms", "student_t"))):
+        for wt in ws:
+            line = run_child(["--workload", w, "--weights", wt, "--steps", str(args.steps),
+                              "--warmup", str(args.warmup), "--profile-only"], 600)
+            log(f"robustness {w} {wt} done")
+            if line is not None:
+                pf = line.get("prefilter") or {}
+                rob.setdefault(w, {})[wt] = {
+                    "value": line["value"], "ms_per_step": line["ms_per_step"],
+                    "candidates_per_row": pf.get("candidates_per_row"),
+                    "fallback_rows": pf.get("fallback_rows"),
+                    "strided_sample_rows": pf.get("strided_sample_rows"),
+                    "scan_ms": (line.get("roofline") or {}).get("avg_kernel_ms")}
+    out["pruning_robustness"] = rob
     for w in ("ncf", "lightgcn"):
         line = run_child(["--latency", "--workload", w, "--steps", "200", "--no-extras"], 600)
         log(f"serve latency {w} done")
@@ -521,9 +550,11 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--latency", action="store_true",
                     help="serve-path B=1 latency (p50/p99) instead of the throughput line")
-    ap.add_argument("--weights", default="init", choices=["init", "personal"],
+    ap.add_argument("--weights", default="init", choices=["init", "personal", *STRESS_WEIGHTS],
                     help="init: reference init distributions; personal: NCF weights whose "
-                         "best items are user-specific (emb_scale 20, biases)")
+                         "best items are user-specific (emb_scale 20, biases); norms / "
+                         "student_t: trained-like weights (NCF, MF: embedding rows at norms "
+                         "50-200 / Student-t(3) weights and biases)")
     ap.add_argument("--exact", action="store_true",
                     help="exact fp32 scan of every item instead of the certified f16 pre-filter")
     ap.add_argument("--profile-only", action="store_true",
@@ -576,7 +607,8 @@ def main():
     _lib.set_option(device, _lib.HNM_OPT_STATS, 1)
     step(batches[0])
     _lib.set_option(device, _lib.HNM_OPT_STATS, 0)
-    pf_rows, pf_cands, pf_fallback = _lib.prefilter_stats(device, reset=True)
+    pf_rows, pf_cands, pf_fallback, pf_sampled = _lib.prefilter_stats(device, reset=True,
+                                                                      extended=True)
     exact_rate = None
     if args.profile_only:
         args.no_extras = args.no_cpu_baseline = True
@@ -633,7 +665,9 @@ def main():
         "vs_baseline": None,
         "dtype": ("f32" if args.exact or not (f16 or bound == "hbm") else
                   "f16+f32"),
-        "data": "synthetic (PCG64 weights with reference init distributions; H&M shape)",
+        "data": ("synthetic (PCG64 weights with reference init distributions; H&M shape)"
+                 if args.weights == "init" else
+                 f"synthetic (PCG64 weights, '{args.weights}' set: bench.py --weights; H&M shape)"),
         "config": {"workload": f"{args.workload}: BASELINE configs[1] NeuralCF dim=64, full H&M "
                                f"shape, batch={B} users/rank, K=12" if args.workload == "ncf"
                    else args.workload,
@@ -775,6 +809,7 @@ def main():
     if pf_rows:
         line["prefilter"] = {"rows": pf_rows, "candidates_per_row": round(
             pf_cands / max(pf_rows - pf_fallback, 1), 1), "fallback_rows": pf_fallback,
+            "strided_sample_rows": pf_sampled,
             "outputs": "bit-identical to the exact fp32 scan (tests/test_gpu_prefilter.py)"}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:

@@ -74,6 +74,7 @@ _SIGS = {
     "hnm_ctx_timing": (_i32, [_p, C.POINTER(C.c_double), C.POINTER(_i64)]),
     "hnm_ctx_set_option": (_i32, [_p, C.c_int, _i64]),
     "hnm_ctx_prefilter_stats": (_i32, [_p, C.POINTER(_i64), C.c_int]),
+    "hnm_ctx_prefilter_stats_ex": (_i32, [_p, C.POINTER(_i64), C.c_int, C.c_int]),
     "hnm_gather_rows_f32": (_i32, [_p, _p, _i64, _i64, C.c_int, _p, _i64, _p, _i64]),
     "hnm_linear_rows_f32": (_i32, [_p, _p, _i64, _p, _i64, _i64, C.c_int, _p, _i64, _p,
                                    C.c_int, _p, _i64, C.c_int]),
@@ -313,17 +314,20 @@ def set_prefilter(device, on=True):
     set_option(device, HNM_OPT_PREFILTER, int(bool(on)))
 
 
-def prefilter_stats(device, reset=False):
+def prefilter_stats(device, reset=False, extended=False):
     """(rows scored, candidates re-scored in fp32, rows that took the exact fallback) summed
     over every thread's ctx on `device`; counted only while HNM_OPT_STATS is on
-    (set_option(dev, HNM_OPT_STATS, 1)).  Each read syncs the device; calls other threads issue
-    meanwhile may be counted before or after a reset (exact when they are idle)."""
+    (set_option(dev, HNM_OPT_STATS, 1)).  extended: a 4th count, rows whose bound also used
+    the gated per-user strided sample (NeuralCF).  Each read syncs the device; calls other
+    threads issue meanwhile may be counted before or after a reset (exact when they are idle)."""
     ctx(device)
-    tot = [0, 0, 0]
+    n = 4 if extended else 3
+    tot = [0] * n
     for c in _device_ctxs(_dev_index(device)):
-        out = (_i64 * 3)()
-        check(fn("hnm_ctx_prefilter_stats")(c.handle, out, int(reset)), "hnm_ctx_prefilter_stats")
-        for j in range(3):
+        out = (_i64 * n)()
+        check(fn("hnm_ctx_prefilter_stats_ex")(c.handle, out, n, int(reset)),
+              "hnm_ctx_prefilter_stats_ex")
+        for j in range(n):
             tot[j] += int(out[j])
     return tuple(tot)
 

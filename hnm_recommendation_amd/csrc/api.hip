@@ -99,14 +99,26 @@ extern "C" hnm_status hnm_ctx_set_option(hnm_ctx* ctx, int option, int64_t value
 }
 
 extern "C" hnm_status hnm_ctx_prefilter_stats(hnm_ctx* ctx, int64_t* out, int reset) {
+  return hnm_ctx_prefilter_stats_ex(ctx, out, 3, reset);
+}
+
+extern "C" hnm_status hnm_ctx_prefilter_stats_ex(hnm_ctx* ctx, int64_t* out, int n, int reset) {
   HNM_REQUIRE(ctx && out, HNM_EINVAL, "ctx/out is NULL");
+  HNM_REQUIRE(n >= 1 && n <= HNM_STATS_N, HNM_EINVAL, "prefilter_stats: 1 <= n <= %d", HNM_STATS_N);
   // device-wide sync: never reads ctx->stream, which the ctx's owning thread may be switching
-  // (this entry is called across threads: the Python layer sums every thread's ctx)
+  // (this entry is called across threads: the Python layer sums every thread's ctx).  The
+  // calling thread's current device is restored on every exit path.
+  int prev = -1;
+  HNM_HIP_CHECK(hipGetDevice(&prev));
+  struct Restore {
+    int dev;
+    ~Restore() { (void)hipSetDevice(dev); }
+  } restore{prev};
   HNM_HIP_CHECK(hipSetDevice(ctx->device));
   HNM_HIP_CHECK(hipDeviceSynchronize());
-  unsigned long long v[3];
+  unsigned long long v[HNM_STATS_N];
   HNM_HIP_CHECK(hipMemcpy(v, ctx->stats_dev, sizeof(v), hipMemcpyDeviceToHost));
-  for (int i = 0; i < 3; ++i) out[i] = (int64_t)v[i];
+  for (int i = 0; i < n; ++i) out[i] = (int64_t)v[i];
   if (reset) HNM_HIP_CHECK(hipMemset(ctx->stats_dev, 0, sizeof(v)));
   return HNM_OK;
 }
@@ -444,9 +456,15 @@ __global__ __launch_bounds__(256) void topk_merge_kernel(const float* __restrict
                                                          float* __restrict__ ov,
                                                          int64_t* __restrict__ oi,
                                                          const int32_t* __restrict__ rows,
-                                                         const int32_t* __restrict__ nrows) {
+                                                         const int32_t* __restrict__ nrows,
+                                                         int64_t dyn_items, int dyn_cus) {
   const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (b >= (nrows ? (int64_t)*nrows : B)) return;
+  const int64_t nb = nrows ? (int64_t)*nrows : B;
+  if (b >= nb) return;
+  if (dyn_cus > 0) {  // row-list candidates: np partitions per row, as the launch chose them
+    kc *= choose_partition(dyn_items, hnm_cdiv(nb, 128), dyn_cus).np;
+    bstride = kc;
+  }
   const int64_t ob = rows ? (int64_t)rows[b] : b;
   const int lane = threadIdx.x & 63;
   WaveTopK<NS> L;
@@ -476,14 +494,14 @@ template <typename IdxT>
 hnm_status launch_merge(hnm_ctx* ctx, const float* cv, const IdxT* ci, int64_t B, int64_t G,
                         int64_t gstride, int64_t bstride, int kc, int k, float* ov,
                         int64_t* oi, const int32_t* rows = nullptr,
-                        const int32_t* nrows = nullptr) {
+                        const int32_t* nrows = nullptr, int64_t dyn_items = 0, int dyn_cus = 0) {
   dim3 grid((unsigned)hnm_cdiv(B, 4));
   if (k <= 64)
     hipLaunchKernelGGL((topk_merge_kernel<1, IdxT>), grid, dim3(256), 0, ctx->stream, cv, ci,
-                       B, G, gstride, bstride, kc, k, ov, oi, rows, nrows);
+                       B, G, gstride, bstride, kc, k, ov, oi, rows, nrows, dyn_items, dyn_cus);
   else
     hipLaunchKernelGGL((topk_merge_kernel<2, IdxT>), grid, dim3(256), 0, ctx->stream, cv, ci,
-                       B, G, gstride, bstride, kc, k, ov, oi, rows, nrows);
+                       B, G, gstride, bstride, kc, k, ov, oi, rows, nrows, dyn_items, dyn_cus);
   HNM_LAUNCH_CHECK();
   return HNM_OK;
 }
@@ -497,8 +515,9 @@ hnm_status hnm_topk_merge_i32(hnm_ctx* ctx, const float* cv, const int32_t* ci, 
 hnm_status hnm_topk_merge_rows(hnm_ctx* ctx, const float* cv, const int32_t* ci, int64_t B,
                                int64_t G, int64_t gstride, int64_t bstride, int kc, int k,
                                float* ov, int64_t* oi, const int32_t* rows,
-                               const int32_t* nrows) {
-  return launch_merge<int32_t>(ctx, cv, ci, B, G, gstride, bstride, kc, k, ov, oi, rows, nrows);
+                               const int32_t* nrows, int64_t dyn_items, int dyn_cus) {
+  return launch_merge<int32_t>(ctx, cv, ci, B, G, gstride, bstride, kc, k, ov, oi, rows, nrows,
+                               dyn_items, dyn_cus);
 }
 
 // ------------------------------------------------------------------ k-th of bound lists

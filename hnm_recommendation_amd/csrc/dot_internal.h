@@ -31,6 +31,7 @@ struct DotArgs {
   int cap;
   const int32_t* rows;     // optional: launch row b serves request row rows[b] ...
   const int32_t* nrows;    // ... for b < *nrows (device count)
+  int dyn_cus;             // LIST with rows: > 0 = partitions follow *nrows (list_rows_np)
   unsigned* err;
 };
 

@@ -18,6 +18,7 @@
 
 #include <algorithm>
 #include <cstring>
+#include <memory>
 #include <mutex>
 #include <queue>
 #include <thread>
@@ -1193,10 +1194,12 @@ static hnm_status plan_bind(hnm_ctx* ctx, hnm_spmm_plan* pl, const int32_t* col,
     HNM_HIP_CHECK(hipMemcpyAsync(c0.data(), col, T * 4, hipMemcpyDeviceToHost, ctx->stream));
     HNM_HIP_CHECK(hipMemcpyAsync(v0.data(), val, T * 4, hipMemcpyDeviceToHost, ctx->stream));
     HNM_HIP_CHECK(hipStreamSynchronize(ctx->stream));
-    pl->h_scol = new std::vector<int32_t>((size_t)T);
-    pl->h_sval = new std::vector<float>((size_t)T);
-    std::vector<int32_t>& hc = *pl->h_scol;
-    std::vector<float>& hv = *pl->h_sval;
+    // all-or-nothing: the host copies and device uploads are installed in the plan only when
+    // every step succeeded, so a failed bind leaves the plan unbound and a retry starts clean
+    std::unique_ptr<std::vector<int32_t>> hcp(new std::vector<int32_t>((size_t)T));
+    std::unique_ptr<std::vector<float>> hvp(new std::vector<float>((size_t)T));
+    std::vector<int32_t>& hc = *hcp;
+    std::vector<float>& hv = *hvp;
     const int64_t nchunk = hnm_cdiv(pl->N, 4096);
     parallel_for(nchunk, [&](int64_t ch) {
       std::vector<int32_t> ix;
@@ -1213,9 +1216,18 @@ static hnm_status plan_bind(hnm_ctx* ctx, hnm_spmm_plan* pl, const int32_t* col,
         }
       }
     });
-    hnm_status st;
-    if ((st = upload(&pl->scol, hc.data(), (size_t)T)) || (st = upload(&pl->sval, hv.data(), (size_t)T)))
+    int32_t* dcol = nullptr;
+    float* dval = nullptr;
+    hnm_status st = upload(&dcol, hc.data(), (size_t)T);
+    if (!st) st = upload(&dval, hv.data(), (size_t)T);
+    if (st) {
+      if (dcol) (void)hipFree(dcol);
       return st;
+    }
+    pl->scol = dcol;
+    pl->sval = dval;
+    pl->h_scol = hcp.release();
+    pl->h_sval = hvp.release();
     if (SPMM_SIDE_WALK && pl->swalk) plan_bipartite_sides(pl);
   }
   pl->bound_col = col;

@@ -28,7 +28,8 @@ struct hnm_ctx {
   hipEvent_t* ev0;
   hipEvent_t* ev1;
   int prefilter;                   // HNM_OPT_PREFILTER (default 1)
-  unsigned long long* stats_dev;   // pre-filter counters: rows, candidates, fallback rows
+  unsigned long long* stats_dev;   // pre-filter counters: rows, candidates, fallback rows,
+                                   // rows whose bound used the gated strided sample
   int stats_on;                    // HNM_OPT_STATS (default 0: counting costs same-address atomics)
   // open two-phase top-K call (hnm_*_topk_begin_f32 ... hnm_*_topk_finish_f32): the
   // workspace holds the begin phase's tables until the matching finish, so every other
@@ -41,6 +42,7 @@ struct hnm_ctx {
     const void* items;      // the item table the begin phase read
   } pend;
 };
+#define HNM_STATS_N 4  // pre-filter counters (hnm_ctx_prefilter_stats_ex)
 #define HNM_PEND_NCF_CERT 1
 #define HNM_PEND_NCF_EXACT 2
 #define HNM_PEND_DOT_CERT 3
@@ -101,15 +103,41 @@ struct Partition {
   int np;
   int64_t ipp;
 };
-static inline Partition choose_partition(int64_t I, int64_t ublocks, int num_cus,
-                                         int64_t tile = 32, int wg_per_cu = 2) {
-  const int64_t want = std::max<int64_t>(
-      1, (int64_t)wg_per_cu * num_cus / std::max<int64_t>(ublocks, 1));
-  const int64_t maxp = std::max<int64_t>(1, hnm_cdiv(I, 4 * tile));
-  int64_t np = std::min(want, maxp);
+__host__ __device__ static inline Partition choose_partition(int64_t I, int64_t ublocks,
+                                                             int num_cus, int64_t tile = 32,
+                                                             int wg_per_cu = 2) {
+  int64_t want = (int64_t)wg_per_cu * num_cus / (ublocks > 1 ? ublocks : 1);
+  if (want < 1) want = 1;
+  int64_t maxp = hnm_cdiv(I, 4 * tile);
+  if (maxp < 1) maxp = 1;
+  int64_t np = want < maxp ? want : maxp;
   int64_t ipp = hnm_cdiv(hnm_cdiv(I, np), tile) * tile;
   np = hnm_cdiv(I, ipp);
   return {(int)np, ipp};
+}
+
+// Row-list launches -- the certified paths' exact fallback, whose queued rows are known only
+// on the device (rows[0, *nrows)): the grid is (cdiv(B, 128), list_rows_np(I, num_cus)) and
+// each workgroup derives the partition actually used from *nrows, choose_partition(I,
+// cdiv(nrows, 128), num_cus), so that a handful of queued rows still spreads over the whole
+// chip (workgroups past it exit at once).  Candidates of list row b sit at [b][p][K] with row
+// stride np * K; the merge derives np the same way (topk_merge_kernel's dyn_cus).
+static inline int list_rows_np(int64_t I, int num_cus) {
+  return choose_partition(I, 1, num_cus).np;
+}
+// candidate slots (rows x partitions) a row-list launch over <= B queued rows can write
+static inline int64_t list_rows_slots(int64_t B, int64_t I, int num_cus) {
+  int64_t best = 0;
+  // rows * np(rows) peaks at the largest row count of each user-block count
+  for (int64_t nb = 1; nb <= hnm_cdiv(B, 128); ++nb) {
+    const int64_t n = std::min<int64_t>(B, nb * 128);
+    best = std::max<int64_t>(best, n * choose_partition(I, nb, num_cus).np);
+    if (choose_partition(I, nb, num_cus).np == 1) {
+      best = std::max<int64_t>(best, B);
+      break;
+    }
+  }
+  return best;
 }
 
 // torch.topk over a dense [B, I] score matrix whose column c is item c * istride, with the
@@ -117,11 +145,23 @@ static inline Partition choose_partition(int64_t I, int64_t ublocks, int num_cus
 hnm_status hnm_topk_rows_strided(hnm_ctx* ctx, const float* s, int64_t ld, int64_t B, int64_t I,
                                  const int64_t* mptr, const int32_t* midx, int K, float* ov,
                                  int64_t* oi, int64_t istride);
-// Lower bound of the K-th best value of each sample row (score.hip sample_kth_kernel),
-// written at out[b * K + K - 1].
+// Per sample row (score.hip sample_kth_kernel): out is [B, K], slot r = a lower bound of the
+// row's (r+1)-th best value (the row's K best sampled survivors in descending order), -inf past
+// the survivors; every slot NaN when the row holds a NaN.  All K slots are written (the
+// bound-lists kernels read them), so callers must allocate B * K floats.  gate (optional,
+// device): *gate == 0 skips the launch's work (a sample pass that was gated off).
 hnm_status hnm_sample_kth(hnm_ctx* ctx, const float* s, int64_t ld, int64_t B, int64_t Ns,
                           const int64_t* mptr, const int32_t* midx, int K, int64_t grp,
-                          int64_t period, const int32_t* sidx, float* out);
+                          int64_t period, const int32_t* sidx, float* out,
+                          const int* gate = nullptr);
+
+// Top-k merge of kc candidates per row (G groups), one wave per row (api.hip).  rows/nrows: list
+// row b is output row rows[b], b < *nrows.  dyn_cus > 0: a row-list launch's candidates, whose
+// partition count np follows *nrows (list_rows_np): kc and bstride are then np * kc.
+hnm_status hnm_topk_merge_rows(hnm_ctx* ctx, const float* cv, const int32_t* ci, int64_t B,
+                               int64_t G, int64_t gstride, int64_t bstride, int kc, int k,
+                               float* ov, int64_t* oi, const int32_t* rows,
+                               const int32_t* nrows, int64_t dyn_items = 0, int dyn_cus = 0);
 
 // p[0, n) = v on the ctx stream
 hnm_status hnm_fill_f32(hnm_ctx* ctx, float* p, int64_t n, float v);

@@ -26,10 +26,6 @@
 hnm_status hnm_topk_merge_i32(hnm_ctx* ctx, const float* cv, const int32_t* ci, int64_t B,
                               int64_t G, int64_t gstride, int64_t bstride, int kc, int k,
                               float* ov, int64_t* oi);
-hnm_status hnm_topk_merge_rows(hnm_ctx* ctx, const float* cv, const int32_t* ci, int64_t B,
-                               int64_t G, int64_t gstride, int64_t bstride, int kc, int k,
-                               float* ov, int64_t* oi, const int32_t* rows,
-                               const int32_t* nrows);
 
 // ------------------------------------------------------------------ 32-user kernel
 // ABL: ablation bits for tools/ncf_ablation.hip only (0 in the library): 1 = no top-K,
@@ -45,9 +41,10 @@ __global__ __launch_bounds__(256, 2) void ncf32_kernel(
     int64_t ipp, const int64_t* __restrict__ mptr, const int32_t* __restrict__ midx, int K,
     float* __restrict__ cand_v, int32_t* __restrict__ cand_i, int NP,
     float* __restrict__ dense, int64_t ldo, const int32_t* __restrict__ rows,
-    const int32_t* __restrict__ nrows) {
+    const int32_t* __restrict__ nrows, int dyn_cus) {
   // rows != nullptr: batch row b is request row rows[b], b < *nrows (device-side list of
-  // the rows the certified path queued); candidates stay at the compact index b.
+  // the rows the certified path queued); candidates stay at the compact index b.  dyn_cus > 0:
+  // the item partitions follow *nrows (hnm_internal.h list_rows_np; grid.y is the maximum).
   constexpr int KS = 32;          // MFMA k-steps of layer 2 (h1 <= 64) and of GMF (mf <= 64)
   constexpr int RS = 68;          // LDS row stride (floats): conflict-free b128 reads
   constexpr int NU = 128;         // users per workgroup
@@ -61,10 +58,16 @@ __global__ __launch_bounds__(256, 2) void ncf32_kernel(
   const int64_t ublk = (int64_t)blockIdx.x * NU;
   if (rows) B = *nrows;
   if (ublk >= B) return;  // whole workgroup: before any barrier
+  if (rows && dyn_cus > 0) {
+    const Partition dp = choose_partition(I, hnm_cdiv(B, NU), dyn_cus);
+    NP = dp.np;
+    ipp = dp.ipp;
+  }
+  const int p = blockIdx.y;
+  if (p >= NP) return;  // whole workgroup (dynamic row-list partitions)
   auto R = [&](int64_t b) -> int64_t { return rows ? (int64_t)rows[b] : b; };
   const int64_t u0 = ublk + wave * 32;  // first user of this wave
   const int nu = (int)std::max<int64_t>(0, std::min<int64_t>(32, B - u0));
-  const int p = blockIdx.y;
   const int64_t part_start = (int64_t)p * ipp;
   const int64_t part_end = std::min<int64_t>(I, part_start + ipp);
   float* lv_s = lists + wave * 32 * K;
@@ -580,11 +583,13 @@ template <bool DENSE>
 static void launch_ncf32(hnm_ctx* ctx, dim3 grid, const NcfTabs& t, const hnm_ncf_weights* w,
                          int64_t B, int64_t ipp, const int64_t* mptr, const int32_t* midx, int K,
                          float* cv, int32_t* ci, int NP, float* dense, int64_t ldo,
-                         const int32_t* rows = nullptr, const int32_t* nrows = nullptr) {
+                         const int32_t* rows = nullptr, const int32_t* nrows = nullptr,
+                         int dyn_cus = 0) {
   const size_t lds = DENSE ? 0 : (size_t)4 * 32 * K * 8;
   hipLaunchKernelGGL((ncf32_kernel<DENSE>), grid, dim3(256), lds, ctx->stream, t.Pu, t.WGu, t.Qi,
                      t.G, t.ldg, w->mf, w->w2, w->h1, w->h2, w->b2, w->wp + w->mf, w->bp, B,
-                     w->num_items, ipp, mptr, midx, K, cv, ci, NP, dense, ldo, rows, nrows);
+                     w->num_items, ipp, mptr, midx, K, cv, ci, NP, dense, ldo, rows, nrows,
+                     dyn_cus);
 }
 
 template <int WU, int H1P, int MFH, bool DENSE>
@@ -598,19 +603,22 @@ static void launch_ncf(hnm_ctx* ctx, dim3 grid, const NcfTabs& t, const hnm_ncf_
 
 size_t ncf_list_bytes(int64_t B, int64_t I, int K, int num_cus) {
   const Partition part = choose_partition(I, hnm_cdiv(B, 128), num_cus);
-  return hnm_align((size_t)B * part.np * K * 4);
+  const int64_t slots = std::max<int64_t>(B * part.np, list_rows_slots(B, I, num_cus));
+  return hnm_align((size_t)slots * K * 4);
 }
 
 hnm_status ncf_list_rows(hnm_ctx* ctx, const hnm_ncf_weights* w, const NcfTabs& t, int64_t B,
                          const int64_t* mptr, const int32_t* midx, int K, const int32_t* rows,
                          const int32_t* nrows, float* cv, int32_t* ci, float* ov, int64_t* oi) {
+  // the queued rows are known only on the device: the widest grid, the partitions used
+  // derived from *nrows in the kernel and the merge (hnm_internal.h list_rows_np)
   const int64_t ublocks = hnm_cdiv(B, 128);
-  const Partition part = choose_partition(w->num_items, ublocks, ctx->num_cus);
-  launch_ncf32<false>(ctx, dim3((unsigned)ublocks, (unsigned)part.np), t, w, B, part.ipp, mptr,
-                      midx, K, cv, ci, part.np, nullptr, 0, rows, nrows);
+  const int npmax = list_rows_np(w->num_items, ctx->num_cus);
+  launch_ncf32<false>(ctx, dim3((unsigned)ublocks, (unsigned)npmax), t, w, B, 0, mptr, midx, K,
+                      cv, ci, npmax, nullptr, 0, rows, nrows, ctx->num_cus);
   HNM_LAUNCH_CHECK();
-  return hnm_topk_merge_rows(ctx, cv, ci, B, 1, 0, (int64_t)part.np * K, part.np * K, K, ov, oi,
-                             rows, nrows);
+  return hnm_topk_merge_rows(ctx, cv, ci, B, 1, 0, K, K, K, ov, oi, rows, nrows, w->num_items,
+                             ctx->num_cus);
 }
 
 // Per-call tables: P_u, wp*g_u (users), Q_i (items), the GMF item table (padded copy when
@@ -733,8 +741,19 @@ extern "C" hnm_status hnm_ncf_topk_f32(hnm_ctx* ctx, const hnm_ncf_weights* w,
                                        const int64_t* mask_ptr, const int32_t* mask_idx, int k,
                                        float* out_val, int64_t* out_idx) {
   HNM_REQUIRE(k >= 1 && k <= 64 && (out_idx || B == 0), HNM_EINVAL, "ncf_topk: fused path needs 1 <= k <= 64");
-  return ncf_common<false>(ctx, w, user_ids, B, mask_ptr, mask_idx, k, out_val, out_idx,
-                           nullptr, 0);
+  // very large batches in chunks of rows: the certified path's per-row scratch (samples,
+  // candidate segments) stays bounded; the mask CSR holds absolute offsets, so a chunk reads
+  // its rows' slice of mask_ptr as is
+  constexpr int64_t CHUNK = 32768;
+  for (int64_t b0 = 0; b0 < B || b0 == 0; b0 += CHUNK) {
+    const int64_t nb = std::min<int64_t>(CHUNK, B - b0);
+    hnm_status st = ncf_common<false>(ctx, w, user_ids ? user_ids + b0 : nullptr, nb,
+                                      mask_ptr ? mask_ptr + b0 : nullptr, mask_idx, k,
+                                      out_val ? out_val + b0 * k : nullptr,
+                                      out_idx ? out_idx + b0 * k : nullptr, nullptr, 0);
+    if (st || B <= 0) return st;
+  }
+  return HNM_OK;
 }
 
 // Two-phase fused top-K for item-sharded serving (sharding.py): begin computes the per-call

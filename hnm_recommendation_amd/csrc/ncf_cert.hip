@@ -41,10 +41,6 @@
 typedef _Float16 h8 __attribute__((ext_vector_type(8)));
 typedef _Float16 h2 __attribute__((ext_vector_type(2)));
 
-hnm_status hnm_topk_merge_rows(hnm_ctx* ctx, const float* cv, const int32_t* ci, int64_t B,
-                               int64_t G, int64_t gstride, int64_t bstride, int kc, int k,
-                               float* ov, int64_t* oi, const int32_t* rows,
-                               const int32_t* nrows);
 
 namespace {
 
@@ -54,6 +50,22 @@ constexpr int CERT_MAX_NP = 64;           // item partitions (candidate segments
 constexpr int CERT_PROXY_USERS = 8;       // batch rows that pick the champion sample
 constexpr int64_t CERT_CHAMPIONS = 2048;  // champion sample size (item groups), at most
 constexpr int64_t CERT_GROUP_MIN = 48;    // items per champion group, at least
+// Gated per-user strided sample (round 5).  The champion sample is tight when the rows' best
+// items are shared (init weights at the H&M shape: ~70 candidates a row) and degrades to a
+// ~1/52 random sample when they are user-specific (trained-like weights: 600+ candidates and
+// overflowing segments).  A sample pass over one 32-item tile in CERT_STRIDE for every row gives
+// a second lower bound (the larger of the two is used) at ~1/CERT_STRIDE of the scan's cost.
+// Whether it pays is predicted on the proxy rows, whose every item the proxy pass scored:
+// cert_gate_kth_kernel takes each proxy's K-th over its LEAVE-ONE-OUT champions (picked by the
+// other proxies: what a non-proxy row sees) and over the strided tiles; cert_gate_count_kernel
+// counts, per proxy, the items the main scan would append under each bound (approx + e_i >=
+// tau, tau = kv - 2 Eu: cert_tau_kernel); the pass runs when it saves more than CERT_GATE_GAIN
+// candidates a row on average -- re-scoring ~250 candidates costs about what the 1/8 pass does
+// (bench step: 65 us for 4,096 x 70 candidates against 1/8 of a 1.85 ms scan).  Gated off, the
+// pass and its K-th exit at launch.
+constexpr int CERT_STRIDE = 8;
+constexpr int64_t CERT_GATE_GAIN = 250;
+constexpr int CERT_GATE_CHUNKS = 64;  // workgroups per proxy row of the count kernel
 #ifndef HNM_SCAN_OCC
 #define HNM_SCAN_OCC 3
 #endif
@@ -433,6 +445,7 @@ struct ScanArgs {
   float* dense;      // [B, ldo]
   float* dense2;     // [B, ldo] (DEBUG)
   int64_t ldo;
+  const int* gate;   // SAMPLE: *gate == 0 -> the launch does nothing (gated strided sample)
 };
 
 __device__ __forceinline__ f32x16 mfma16(h8 a, h8 b, f32x16 c) {
@@ -462,6 +475,7 @@ __global__ __launch_bounds__(256, HNM_SCAN_OCC) void ncf16_scan_kernel(ScanArgs 
   constexpr int RS = 72;   // LDS row stride in halfs (144 B): conflict-free b128 reads
   constexpr int NU = 128;  // users per workgroup
   constexpr bool FOLD = MODE == SCAN_THRESH || MODE == SCAN_SAMPLE;
+  if (MODE == SCAN_SAMPLE && A.gate && *A.gate == 0) return;  // whole grid: gated off
   __shared__ __attribute__((aligned(16))) _Float16 qs[2][TILE * RS];  // double-buffered tiles
   __shared__ __attribute__((aligned(16))) _Float16 gs[2][TILE * RS];
   __shared__ __attribute__((aligned(16))) _Float16 ps[NU * 64];
@@ -761,7 +775,19 @@ __global__ __launch_bounds__(256, HNM_SCAN_OCC) void ncf16_scan_kernel(ScanArgs 
 // relative 2^-21 covers the fp32 rounding of the subtraction and of + bp).  Rows with an
 // unusable bound get L = -inf.  Any lower bound works downstream -- e.g. the max of the
 // item shards' L over the ranks of a node (hnm_ncf_topk_begin_f32 / _finish_f32).
-__global__ __launch_bounds__(256) void cert_bound_kernel(const float* __restrict__ kth, int K,
+// The larger of two samples' lower bounds (kth2 used when *gate: the strided sample ran); a NaN
+// in either (a row with a NaN score) stays NaN.
+__device__ __forceinline__ float kth_pick(const float* kth, const float* kth2, const int* gate,
+                                          int64_t x) {
+  const float a = kth[x];
+  if (!gate || *gate == 0) return a;
+  const float c = kth2[x];
+  return (a != a || c != c) ? __builtin_nanf("") : fmaxf(a, c);
+}
+
+__global__ __launch_bounds__(256) void cert_bound_kernel(const float* __restrict__ kth,
+                                                         const float* __restrict__ kth2,
+                                                         const int* __restrict__ gate, int K,
                                                          const float* __restrict__ Au,
                                                          const CertParams* __restrict__ prm,
                                                          const float* __restrict__ bp, int64_t B,
@@ -773,7 +799,7 @@ __global__ __launch_bounds__(256) void cert_bound_kernel(const float* __restrict
   const float e = unit * (CERT_RHO * (prm->c0 + Au[b]) + prm->absb);
   if (Eu) Eu[b] = e;
   if (!kth) return;
-  float l = (kth[b * K + (K - 1)] - e) / unit + bp[0];
+  float l = (kth_pick(kth, kth2, gate, b * K + (K - 1)) - e) / unit + bp[0];
   l -= fabsf(l) * 4.76837158203125e-07f;  // 2^-21
   lb[b] = (!prm->bad && __builtin_isfinite(l) && __builtin_isfinite(e)) ? l : -__builtin_inff();
 }
@@ -782,6 +808,8 @@ __global__ __launch_bounds__(256) void cert_bound_kernel(const float* __restrict
 // item (real units, as cert_bound_kernel for the K-th), for an exchange of whole lists across
 // item shards: the K-th best of the union of every shard's lists bounds the global K-th.
 __global__ __launch_bounds__(256) void cert_bound_lists_kernel(const float* __restrict__ kth,
+                                                               const float* __restrict__ kth2,
+                                                               const int* __restrict__ gate,
                                                                int K,
                                                                const float* __restrict__ Eu,
                                                                const CertParams* __restrict__ prm,
@@ -790,7 +818,9 @@ __global__ __launch_bounds__(256) void cert_bound_lists_kernel(const float* __re
   const int64_t x = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (x >= B * K) return;
   const float unit = prm->unit, e = Eu[x / K];
-  float l = (kth[x] - e) / unit + bp[0];
+  // slot r of either sample's list lower-bounds the row's (r+1)-th best item of this shard,
+  // so the larger of the two does too (the lists exchange needs exactly that per slot)
+  float l = (kth_pick(kth, kth2, gate, x) - e) / unit + bp[0];
   l -= fabsf(l) * 4.76837158203125e-07f;  // 2^-21
   lists[x] = (!prm->bad && __builtin_isfinite(l) && __builtin_isfinite(e)) ? l : -__builtin_inff();
 }
@@ -823,22 +853,47 @@ __global__ __launch_bounds__(256) void cert_tau_kernel(const float* __restrict__
 // best mean (approx - e_i) over the proxy rows (the first users of the batch) -- a
 // popularity-like sample in increasing item order.  Any item subset gives a valid lower
 // bound of a row's K-th; this one tends to hold the rows' best items.  One wave per group.
+// sloo (optional): also each proxy row r's leave-one-out champions, by the mean over the OTHER
+// rows, at sloo[r * nch + g] (cert_gate_kernel's quality check).
 __global__ __launch_bounds__(256) void cert_champion_kernel(const float* __restrict__ pd,
                                                             int64_t ld, int np_rows, int64_t I,
                                                             int64_t gsz, int64_t nch,
-                                                            int32_t* __restrict__ sidx) {
+                                                            int32_t* __restrict__ sidx,
+                                                            int32_t* __restrict__ sloo) {
   const int64_t g = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (g >= nch) return;
   const int lane = threadIdx.x & 63;
   const int64_t i0 = g * gsz, i1 = std::min<int64_t>(I, i0 + gsz);
   float best = -__builtin_inff();
   int64_t bi = i0;
+  float lbest[CERT_PROXY_USERS];
+  int64_t lbi[CERT_PROXY_USERS];
+#pragma unroll
+  for (int r = 0; r < CERT_PROXY_USERS; ++r) {
+    lbest[r] = -__builtin_inff();
+    lbi[r] = i0;
+  }
   for (int64_t i = i0 + lane; i < i1; i += 64) {
+    float v[CERT_PROXY_USERS];
     float m = 0.f;
-    for (int r = 0; r < np_rows; ++r) m += pd[r * ld + i];
+#pragma unroll
+    for (int r = 0; r < CERT_PROXY_USERS; ++r) {
+      v[r] = r < np_rows ? pd[r * ld + i] : 0.f;
+      if (r < np_rows) m += v[r];
+    }
     if (m > best) {  // NaN never wins; the lane's items are visited in increasing order
       best = m;
       bi = i;
+    }
+    if (sloo) {
+#pragma unroll
+      for (int r = 0; r < CERT_PROXY_USERS; ++r) {
+        const float mr = m - v[r];
+        if (mr > lbest[r]) {
+          lbest[r] = mr;
+          lbi[r] = i;
+        }
+      }
     }
   }
 #pragma unroll
@@ -851,6 +906,134 @@ __global__ __launch_bounds__(256) void cert_champion_kernel(const float* __restr
     }
   }
   if (lane == 0) sidx[g] = (int32_t)bi;
+  if (!sloo) return;
+#pragma unroll
+  for (int r = 0; r < CERT_PROXY_USERS; ++r) {
+    float b = lbest[r];
+    int64_t x = lbi[r];
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+      const float ob = __shfl_xor(b, o);
+      const int64_t oi = __shfl_xor(x, o);
+      if (ob > b || (ob == b && oi < x)) {
+        b = ob;
+        x = oi;
+      }
+    }
+    if (lane == 0 && r < np_rows) sloo[r * nch + g] = (int32_t)x;
+  }
+}
+
+// Lane top-4 insert and the K-th of a wave's lists by K pops (sample_kth_kernel's scheme: a
+// lower bound of the K-th best of the values offered; -inf when fewer).
+struct Top4 {
+  float t0 = -__builtin_inff(), t1 = -__builtin_inff(), t2 = -__builtin_inff(),
+        t3 = -__builtin_inff();
+  __device__ void offer(float x) {
+    if (x > t3) {
+      const float a = fminf(x, t2), c2 = fmaxf(x, t2);
+      t3 = a;
+      t2 = fminf(c2, t1);
+      const float c1 = fmaxf(c2, t1);
+      t1 = fminf(c1, t0);
+      t0 = fmaxf(c1, t0);
+    }
+  }
+  __device__ float kth(int K, int lane) {
+    float kv = -__builtin_inff();
+    for (int r = 0; r < K; ++r) {
+      float m = t0;
+#pragma unroll
+      for (int o = 32; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+      kv = m;
+      if (m == -__builtin_inff()) break;  // wave-uniform
+      const int wl = __builtin_ctzll(__ballot(t0 == m));
+      if (lane == wl) {
+        t0 = t1;
+        t1 = t2;
+        t2 = t3;
+        t3 = -__builtin_inff();
+      }
+    }
+    return kv;
+  }
+};
+
+// Gate, step 1 (one workgroup, wave r = proxy row r): kv[2r] = the K-th of the row's
+// (approx - e_i) over its leave-one-out champions, kv[2r + 1] = the larger of that and the K-th
+// over the strided tiles; zeroes the count kernel's counters; writes the strided sample's item
+// map (tiles 0, S, 2S, ... of 32 items: sidx2[0, ns)).
+__global__ __launch_bounds__(512) void cert_gate_kth_kernel(const float* __restrict__ pd,
+                                                            int64_t ld, int np_rows,
+                                                            const int32_t* __restrict__ sloo,
+                                                            int64_t nch, int K, int64_t ns,
+                                                            int32_t* __restrict__ sidx2,
+                                                            float* __restrict__ kv,
+                                                            unsigned long long* __restrict__ cnt) {
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  for (int64_t n = threadIdx.x; n < ns; n += 512)
+    sidx2[n] = (int32_t)((n >> 5) * (32 * CERT_STRIDE) + (n & 31));
+  if (threadIdx.x < 4) cnt[threadIdx.x] = 0;
+  if (w >= np_rows) return;
+  const float* row = pd + w * ld;
+  const int32_t* sl = sloo + w * nch;
+  Top4 c, t;
+  for (int64_t q = lane; q < nch; q += 64) c.offer(row[sl[q]]);
+  for (int64_t n = lane; n < ns; n += 64) t.offer(row[(n >> 5) * (32 * CERT_STRIDE) + (n & 31)]);
+  const float kc = c.kth(K, lane), ks = t.kth(K, lane);
+  if (lane == 0) {
+    kv[2 * w] = kc;
+    kv[2 * w + 1] = fmaxf(kc, ks);
+  }
+}
+
+// Gate, step 2 (grid CERT_GATE_CHUNKS x proxy rows): per proxy row the items the main scan would
+// append under each bound of step 1, summed into cnt[0] / cnt[1]; the last workgroup to finish
+// writes *gate = 1 when the strided sample saves more than CERT_GATE_GAIN candidates a row.
+__global__ __launch_bounds__(256) void cert_gate_count_kernel(
+    const float* __restrict__ pd, int64_t ld, int np_rows, int64_t I,
+    const float* __restrict__ kv, const float* __restrict__ Bs, const float* __restrict__ Di,
+    const float* __restrict__ Cs, const float* __restrict__ Au, const CertParams* __restrict__ prm,
+    unsigned long long* __restrict__ cnt, int* __restrict__ gate, int64_t B,
+    unsigned long long* __restrict__ stats) {
+  __shared__ int part[2][4];
+  const int r = blockIdx.y, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t chunk = hnm_cdiv(I, gridDim.x);
+  const int64_t i0 = (int64_t)blockIdx.x * chunk, i1 = std::min<int64_t>(I, i0 + chunk);
+  const float eu2 = 2.f * prm->unit * (CERT_RHO * (prm->c0 + Au[r]) + prm->absb);
+  const float tc = kv[2 * r] - eu2, ts = kv[2 * r + 1] - eu2, cr = Cs[r];
+  const float* row = pd + r * ld;
+  int nc = 0, nsv = 0;
+  for (int64_t i = i0 + threadIdx.x; i < i1; i += 256) {
+    const float ub = row[i] + 2.f * fmaf(cr, Di[i], Bs[i]);  // approx + e_i
+    nc += ub >= tc;
+    nsv += ub >= ts;
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    nc += __shfl_xor(nc, o);
+    nsv += __shfl_xor(nsv, o);
+  }
+  if (lane == 0) {
+    part[0][w] = nc;
+    part[1][w] = nsv;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    atomicAdd(&cnt[0], (unsigned long long)(part[0][0] + part[0][1] + part[0][2] + part[0][3]));
+    atomicAdd(&cnt[1], (unsigned long long)(part[1][0] + part[1][1] + part[1][2] + part[1][3]));
+    __threadfence();
+    const unsigned long long ticket = atomicAdd(&cnt[2], 1ull);
+    if (ticket == (unsigned long long)gridDim.x * gridDim.y - 1) {  // every count is in
+      __threadfence();
+      const unsigned long long c0 = atomicAdd(&cnt[0], 0ull), c1 = atomicAdd(&cnt[1], 0ull);
+      const int on = (np_rows >= 4 && !prm->bad &&
+                      c0 > c1 + (unsigned long long)(CERT_GATE_GAIN * np_rows)) ? 1 : 0;
+      *gate = on;
+      cnt[3] = c0;  // (diagnostics: the proxies' predicted candidates, champion bound alone)
+      if (on && stats) atomicAdd(&stats[3], (unsigned long long)B);
+    }
+  }
 }
 
 // ------------------------------------------------------------------ exact re-scoring
@@ -1121,6 +1304,13 @@ struct CertWs {
   float *Au, *Cu, *Bi, *Di, *tau, *Eu, *b2s, *kthv, *lb, *pdense, *cdense, *part;
   float *Bs, *Cs;  // Bi, Cu in the scan's test units (cert_convert_kernel)
   int32_t* sidx;  // champion items
+  int32_t* sloo;  // [CERT_PROXY_USERS, nch] leave-one-out champions (gate)
+  int32_t* sidx2; // [ns] strided sample items
+  float* sdense;  // [B, ns] strided sample values (gated)
+  float* kth2;    // [B, K] its K best
+  int* gate;
+  float* gkv;     // [2 * CERT_PROXY_USERS] gate: the proxies' bounds
+  unsigned long long* gcnt;  // [4] gate counters
   int64_t* kthi;
   int *cnt, *flag;
   int32_t *buf, *ovf_cnt, *ovf_rows;
@@ -1142,6 +1332,7 @@ Partition scan_partition(int64_t I, int64_t ublocks, int num_cus, int wg) {
 
 struct CertShape {
   int64_t nch, gsz;  // champion sample: nch groups of gsz items
+  int64_t ns;        // strided sample: items of tiles 0, S, 2S, ... (CERT_STRIDE)
   Partition part;    // of the main scan
   int capp;          // candidate slots per (row, partition)
 };
@@ -1150,6 +1341,8 @@ CertShape cert_shape(int64_t B, int64_t I, int K, int num_cus, int wg) {
   CertShape sh;
   sh.gsz = std::max<int64_t>(CERT_GROUP_MIN, hnm_cdiv(I, CERT_CHAMPIONS));
   sh.nch = hnm_cdiv(I, sh.gsz);
+  const int64_t nst = hnm_cdiv(hnm_cdiv(I, TILE), CERT_STRIDE);  // sampled tiles
+  sh.ns = (nst - 1) * TILE + std::min<int64_t>(TILE, I - (nst - 1) * CERT_STRIDE * TILE);
   sh.part = scan_partition(I, hnm_cdiv(B, 128), num_cus, wg);
   // a row's candidates: items within the bound's margin of the champion sample's K-th --
   // at worst (no shared best items) the K-th of a 1/gsz sample, ~K * gsz items; each
@@ -1185,6 +1378,13 @@ size_t cert_carve(char* base, int64_t B, int64_t I, int K, int num_cus, int wg, 
   x.pdense = (float*)take((size_t)CERT_PROXY_USERS * I * 4);
   x.cdense = (float*)take((size_t)B * sh.nch * 4);
   x.sidx = (int32_t*)take((size_t)sh.nch * 4);
+  x.sloo = (int32_t*)take((size_t)CERT_PROXY_USERS * sh.nch * 4);
+  x.sidx2 = (int32_t*)take((size_t)sh.ns * 4);
+  x.sdense = (float*)take((size_t)B * sh.ns * 4);
+  x.kth2 = (float*)take((size_t)B * K * 4);
+  x.gate = (int*)take(4);
+  x.gkv = (float*)take(2 * CERT_PROXY_USERS * 4);
+  x.gcnt = (unsigned long long*)take(4 * 8);
   x.kthi = (int64_t*)take((size_t)B * K * 8);
   x.cnt = (int*)take((size_t)B * sh.part.np * 4);
   x.flag = (int*)take(B * 4);
@@ -1295,7 +1495,18 @@ hnm_status ncf_cert_begin(hnm_ctx* ctx, const hnm_ncf_weights* w, const NcfTabs&
   launch_scan<SCAN_SAMPLE>(ctx, dim3((unsigned)a.NP, 1), a);
   HNM_LAUNCH_CHECK();
   hipLaunchKernelGGL(cert_champion_kernel, dim3((unsigned)hnm_cdiv(sh.nch, 4)), dim3(256), 0,
-                     ctx->stream, x.pdense, I, (int)bp, I, sh.gsz, sh.nch, x.sidx);
+                     ctx->stream, x.pdense, I, (int)bp, I, sh.gsz, sh.nch, x.sidx, x.sloo);
+  HNM_LAUNCH_CHECK();
+  hipLaunchKernelGGL(cert_gate_kth_kernel, dim3(1), dim3(512), 0, ctx->stream, x.pdense, I,
+                     (int)bp, x.sloo, sh.nch, K, sh.ns, x.sidx2, x.gkv, x.gcnt);
+  HNM_LAUNCH_CHECK();
+  if (bp >= 4) {
+    hipLaunchKernelGGL(cert_gate_count_kernel, dim3(CERT_GATE_CHUNKS, (unsigned)bp), dim3(256), 0,
+                       ctx->stream, x.pdense, I, (int)bp, I, x.gkv, x.Bs, x.Di, x.Cs, x.Au, x.prm,
+                       x.gcnt, x.gate, B, ctx->stats_on ? ctx->stats_dev : nullptr);
+  } else {
+    HNM_HIP_CHECK(hipMemsetAsync(x.gate, 0, 4, ctx->stream));
+  }
   HNM_LAUNCH_CHECK();
   ScanArgs c = scan_args(x, B);
   c.I = sh.nch;
@@ -1311,12 +1522,27 @@ hnm_status ncf_cert_begin(hnm_ctx* ctx, const hnm_ncf_weights* w, const NcfTabs&
   HNM_LAUNCH_CHECK();
   st = hnm_sample_kth(ctx, x.cdense, sh.nch, B, sh.nch, mptr, midx, K, 1, 1, x.sidx, x.kthv);
   if (st) return st;
+  // gated strided sample: every row against one tile in CERT_STRIDE (exits when gated off)
+  ScanArgs g2 = scan_args(x, B);
+  g2.I = sh.ns;
+  g2.sidx = x.sidx2;
+  g2.dense = x.sdense;
+  g2.ldo = sh.ns;
+  g2.gate = x.gate;
+  const Partition p2 = scan_partition(sh.ns, ublocks, ctx->num_cus, wg);
+  g2.ipp = p2.ipp;
+  g2.NP = p2.np;
+  launch_scan<SCAN_SAMPLE>(ctx, dim3((unsigned)p2.np, (unsigned)ublocks), g2);
+  HNM_LAUNCH_CHECK();
+  st = hnm_sample_kth(ctx, x.sdense, sh.ns, B, sh.ns, mptr, midx, K, 1, 1, x.sidx2, x.kth2, x.gate);
+  if (st) return st;
   hipLaunchKernelGGL(cert_bound_kernel, dim3((unsigned)hnm_cdiv(B, 256)), dim3(256), 0,
-                     ctx->stream, x.kthv, K, x.Au, x.prm, w->bp, B, lb ? lb : x.lb, x.Eu);
+                     ctx->stream, x.kthv, x.kth2, x.gate, K, x.Au, x.prm, w->bp, B, lb ? lb : x.lb,
+                     x.Eu);
   HNM_LAUNCH_CHECK();
   if (lists) {
     hipLaunchKernelGGL(cert_bound_lists_kernel, dim3((unsigned)hnm_cdiv(B * K, 256)), dim3(256), 0,
-                       ctx->stream, x.kthv, K, x.Eu, x.prm, w->bp, B, lists);
+                       ctx->stream, x.kthv, x.kth2, x.gate, K, x.Eu, x.prm, w->bp, B, lists);
     HNM_LAUNCH_CHECK();
   }
   return HNM_OK;
@@ -1380,7 +1606,7 @@ hnm_status ncf_cert_debug(hnm_ctx* ctx, const hnm_ncf_weights* w, const NcfTabs&
   hnm_status st = cert_prepare(ctx, w, t, B, x);
   if (st) return st;
   hipLaunchKernelGGL(cert_bound_kernel, dim3((unsigned)hnm_cdiv(B, 256)), dim3(256), 0, ctx->stream,
-                     nullptr, 1, x.Au, x.prm, w->bp, B, nullptr, x.Eu);
+                     nullptr, nullptr, nullptr, 1, x.Au, x.prm, w->bp, B, nullptr, x.Eu);
   HNM_LAUNCH_CHECK();
   ScanArgs a = scan_args(x, B);
   a.I = I;

@@ -175,11 +175,21 @@ extern "C" hnm_status hnm_ncf_deep_scores_f32(hnm_ctx* ctx, const hnm_ncf_deep_w
     hipLaunchKernelGGL(kern, grid, dim3(256), lds, ctx->stream, a, maxw, ctx->err_dev);
   };
   if (dense) {
-    HNM_REQUIRE(B < 65536, HNM_EUNSUPPORTED, "ncf_deep: dense calls take < 65536 users");
-    const dim3 g((unsigned)hnm_cdiv(w->num_items, TP), (unsigned)B);
-    if (TP == 64) launch(ncf_deep_kernel<64, true>, g);
-    else if (TP == 32) launch(ncf_deep_kernel<32, true>, g);
-    else launch(ncf_deep_kernel<16, true>, g);
+    // grid.y = the chunk's users (< 65536 per launch): any B
+    const DeepArgs all = a;
+    for (int64_t b0 = 0; b0 < B; b0 += 65535) {
+      const int64_t nb = std::min<int64_t>(65535, B - b0);
+      a = all;
+      a.P = all.P + b0 * d1;
+      a.uids = all.uids + b0;
+      a.out = all.out + b0 * ldo;
+      a.B = nb;
+      const dim3 g((unsigned)hnm_cdiv(w->num_items, TP), (unsigned)nb);
+      if (TP == 64) launch(ncf_deep_kernel<64, true>, g);
+      else if (TP == 32) launch(ncf_deep_kernel<32, true>, g);
+      else launch(ncf_deep_kernel<16, true>, g);
+      HNM_LAUNCH_CHECK();
+    }
   } else {
     const dim3 g((unsigned)hnm_cdiv(B, TP));
     if (TP == 64) launch(ncf_deep_kernel<64, false>, g);

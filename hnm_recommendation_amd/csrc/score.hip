@@ -48,9 +48,17 @@ __global__ __launch_bounds__(256, (MODE == DOT_LIST || DP > 64) ? 2 : 4) void do
   const int64_t Bl = A.nrows ? (int64_t)*A.nrows : A.B;  // rows of this launch
   const int64_t b0 = (int64_t)blockIdx.x * 128 + wave * 32;
   if ((int64_t)blockIdx.x * 128 >= Bl) return;  // whole workgroup idle (fallback launches)
+  int64_t ipp = A.ipp;
+  int NP = A.NP;
+  if (A.rows && A.dyn_cus > 0) {  // row-list launch: partitions follow *nrows (list_rows_np)
+    const Partition dp = choose_partition(A.I, hnm_cdiv(Bl, 128), A.dyn_cus);
+    ipp = dp.ipp;
+    NP = dp.np;
+  }
   const int p = blockIdx.y;
-  const int64_t part_start = (int64_t)p * A.ipp;
-  const int64_t part_end = std::min<int64_t>(A.I, part_start + A.ipp);
+  if (p >= NP) return;  // whole workgroup
+  const int64_t part_start = (int64_t)p * ipp;
+  const int64_t part_end = std::min<int64_t>(A.I, part_start + ipp);
   const int64_t K = A.K;
   auto req = [&](int64_t b) -> int64_t { return A.rows ? (int64_t)A.rows[b] : b; };
 
@@ -247,7 +255,7 @@ __global__ __launch_bounds__(256, (MODE == DOT_LIST || DP > 64) ? 2 : 4) void do
     for (int i = 0; i < 32; ++i) {
       const int64_t b = b0 + i;
       if (b < Bl && lane < K) {
-        const int64_t o = (b * A.NP + p) * K + lane;
+        const int64_t o = (b * NP + p) * K + lane;
         A.cand_v[o] = lv[i];
         A.cand_i[o] = li[i] == HNM_SENTINEL_IDX ? -1 : li[i];
       }
@@ -379,9 +387,11 @@ __global__ __launch_bounds__(256) void sample_kth_kernel(const float* __restrict
                                                          const int32_t* __restrict__ midx, int K,
                                                          int64_t grp, int64_t period,
                                                          const int32_t* __restrict__ sidx,
-                                                         float* __restrict__ out) {
+                                                         float* __restrict__ out,
+                                                         const int* __restrict__ gate) {
   const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (b >= B) return;
+  if (gate && *gate == 0) return;  // a gated sample (ncf_cert.hip) that did not run
   const int lane = threadIdx.x & 63;
   float t0 = -__builtin_inff(), t1 = t0, t2 = t0, t3 = t0;
   bool nan = false;
@@ -460,11 +470,11 @@ __global__ __launch_bounds__(256) void sample_kth_kernel(const float* __restrict
 // ------------------------------------------------------------------ host side
 hnm_status hnm_sample_kth(hnm_ctx* ctx, const float* s, int64_t ld, int64_t B, int64_t Ns,
                           const int64_t* mptr, const int32_t* midx, int K, int64_t grp,
-                          int64_t period, const int32_t* sidx, float* out) {
+                          int64_t period, const int32_t* sidx, float* out, const int* gate) {
   HNM_REQUIRE(K >= 1 && K <= 64, HNM_EINVAL, "sample_kth: 1 <= K <= 64");
   HNM_REQUIRE(grp >= 1 && period >= grp, HNM_EINVAL, "sample_kth: 1 <= grp <= period");
   hipLaunchKernelGGL(sample_kth_kernel, dim3((unsigned)hnm_cdiv(B, 4)), dim3(256), 0, ctx->stream,
-                     s, ld, B, Ns, mptr, midx, K, grp, period, sidx, out);
+                     s, ld, B, Ns, mptr, midx, K, grp, period, sidx, out, gate);
   HNM_LAUNCH_CHECK();
   return HNM_OK;
 }
@@ -479,10 +489,6 @@ hnm_status hnm_topk_rows_strided(hnm_ctx* ctx, const float* s, int64_t ld, int64
   return HNM_OK;
 }
 
-hnm_status hnm_topk_merge_rows(hnm_ctx* ctx, const float* cv, const int32_t* ci, int64_t B,
-                               int64_t G, int64_t gstride, int64_t bstride, int kc, int k,
-                               float* ov, int64_t* oi, const int32_t* rows,
-                               const int32_t* nrows);
 
 template <int MODE>
 static void launch_dot(hnm_ctx* ctx, dim3 grid, const DotArgs& a, bool bias) {
@@ -534,11 +540,23 @@ DotArgs dot_args(hnm_ctx* ctx, const float* ut, int64_t U, int64_t ldu, const in
 hnm_status dot_list_pass(hnm_ctx* ctx, DotArgs a, bool bias, float* cv, int32_t* ci,
                                 float* ov, int64_t* oi) {
   const int64_t ublocks = hnm_cdiv(a.B, 128);
+  a.cand_v = cv;
+  a.cand_i = ci;
+  if (a.rows) {
+    // the queued rows are known only on the device: the widest grid, the partitions used
+    // derived from *nrows in the kernel and the merge (hnm_internal.h list_rows_np)
+    const int npmax = list_rows_np(a.I, ctx->num_cus);
+    a.ipp = 0;
+    a.NP = npmax;
+    a.dyn_cus = ctx->num_cus;
+    launch_dot<DOT_LIST>(ctx, dim3((unsigned)ublocks, (unsigned)npmax), a, bias);
+    HNM_LAUNCH_CHECK();
+    return hnm_topk_merge_rows(ctx, cv, ci, a.B, 1, 0, a.K, a.K, a.K, ov, oi, a.rows, a.nrows,
+                               a.I, ctx->num_cus);
+  }
   Partition part = choose_partition(a.I, ublocks, ctx->num_cus);
   a.ipp = part.ipp;
   a.NP = part.np;
-  a.cand_v = cv;
-  a.cand_i = ci;
   launch_dot<DOT_LIST>(ctx, dim3((unsigned)ublocks, (unsigned)part.np), a, bias);
   HNM_LAUNCH_CHECK();
   return hnm_topk_merge_rows(ctx, cv, ci, a.B, 1, 0, (int64_t)part.np * a.K, part.np * a.K, a.K,
@@ -547,7 +565,8 @@ hnm_status dot_list_pass(hnm_ctx* ctx, DotArgs a, bool bias, float* cv, int32_t*
 
 size_t list_cand_bytes(int64_t B, int64_t I, int K, int num_cus) {
   Partition part = choose_partition(I, hnm_cdiv(B, 128), num_cus);
-  return hnm_align((size_t)B * part.np * K * 4);
+  const int64_t slots = std::max<int64_t>(B * part.np, list_rows_slots(B, I, num_cus));
+  return hnm_align((size_t)slots * K * 4);
 }
 
 extern "C" hnm_status hnm_dot_topk_f32(hnm_ctx* ctx, const float* user_tab, int64_t num_users,

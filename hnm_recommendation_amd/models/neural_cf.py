@@ -218,7 +218,7 @@ class NeuralCF(RecModule):
         B = u.numel()
         out_v = torch.empty(B, k, dtype=torch.float32, device=u.device)
         out_i = torch.empty(B, k, dtype=torch.int64, device=u.device)
-        step = max(1, min(B, (1 << 26) // max(self.num_items, 1)))
+        step = max(1, min(B, 65535, (1 << 26) // max(self.num_items, 1)))
         buf = torch.empty(step, self.num_items, dtype=torch.float32, device=u.device)
         for b0 in range(0, B, step):
             b1 = min(B, b0 + step)

@@ -132,6 +132,63 @@ def widedeep_state_dict(num_users, num_items, embedding_dim=64, deep_layers=(512
     return sd
 
 
+def _t3(rng, shape, spread):
+    """Student-t(3) scaled to `spread` (t3's std is sqrt(3))."""
+    return (rng.standard_t(3, size=shape) * (spread / np.sqrt(3.0))).astype(np.float32)
+
+
+def _row_norms(rng, a, lo=50.0, hi=200.0):
+    n = np.linalg.norm(a, axis=1, keepdims=True)
+    n[n == 0] = 1.0
+    return (a / n * rng.uniform(lo, hi, (a.shape[0], 1))).astype(np.float32)
+
+
+def stress_state_dict(sd, kind, emb_keys, item_key, seed=0):
+    """Weights unlike the init -- what trained models look like (the certified pre-filters'
+    stress cases, tests/test_gpu_bound_stress.py, and bench.py --weights):
+
+    norms      every embedding row of `emb_keys` rescaled to a norm uniform in [50, 200];
+    student_t  every float weight (embeddings, Linear weights AND biases; BatchNorm statistics
+               and affine kept) Student-t(nu = 3) at the original spread (heavy tailed);
+    bn         (W&D) BatchNorm running_var down to 1e-4, |gamma| up to 10;
+    big / huge one item row of `item_key` at 1e6 / 1e13.
+    Returns a new dict (the input is not modified)."""
+    rng = _rng(1000 + seed)
+    sd = {k: (v.copy() if isinstance(v, np.ndarray) else v) for k, v in sd.items()}
+    if kind == "norms":
+        for k in emb_keys:
+            sd[k] = _row_norms(rng, sd[k])
+    elif kind == "student_t":
+        for k, v in sd.items():
+            if not isinstance(v, np.ndarray) or v.dtype != np.float32 or "running" in k:
+                continue
+            if k.startswith("deep_network") and v.ndim == 1 and int(k.split(".")[1]) % 4 == 2:
+                continue  # BatchNorm affine: kept (the "bn" kind stresses it)
+            spread = float(v.std()) if v.std() > 0 else 0.05
+            sd[k] = _t3(rng, v.shape, spread)
+    elif kind == "big":
+        sd[item_key][77] = np.float32(1e6) * np.sign(sd[item_key][77] + 1e-30)
+    elif kind == "huge":
+        sd[item_key][77] = np.float32(1e13) * np.sign(sd[item_key][77] + 1e-30)
+    elif kind == "bn":
+        for k in list(sd):
+            if k.endswith("running_var"):
+                n = sd[k].size
+                sd[k] = (10.0 ** rng.uniform(-4, 0, n)).astype(np.float32)
+                g = k.replace("running_var", "weight")
+                sd[g] = (rng.choice([-1.0, 1.0], n) * rng.uniform(0.1, 10.0, n)).astype(np.float32)
+                sd[k.replace("running_var", "bias")] = rng.uniform(-1, 1, n).astype(np.float32)
+                sd[k.replace("running_var", "running_mean")] = rng.uniform(-0.5, 0.5, n).astype(np.float32)
+    else:
+        raise ValueError(kind)
+    return sd
+
+
+NCF_EMB_KEYS = ("gmf_user_embedding.weight", "gmf_item_embedding.weight",
+                "mlp_user_embedding.weight", "mlp_item_embedding.weight")
+MF_EMB_KEYS = ("user_embeddings.weight", "item_embeddings.weight")
+
+
 def user_batch(num_users, batch, seed=1, distinct=True):
     """B user ids drawn uniformly from [0, U) (distinct when B <= U)."""
     rng = _rng(seed)

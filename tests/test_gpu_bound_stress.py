@@ -36,47 +36,8 @@ DEV = "cuda"
 I_FULL = syn.HM_ITEMS
 
 
-def _t3(rng, shape, spread):
-    """Student-t(3) scaled to `spread` (t3's std is sqrt(3))."""
-    return (rng.standard_t(3, size=shape) * (spread / np.sqrt(3.0))).astype(np.float32)
-
-
-def _row_norms(rng, a, lo=50.0, hi=200.0):
-    n = np.linalg.norm(a, axis=1, keepdims=True)
-    n[n == 0] = 1.0
-    return (a / n * rng.uniform(lo, hi, (a.shape[0], 1))).astype(np.float32)
-
-
 def stress(sd, kind, emb_keys, item_key, seed):
-    rng = np.random.Generator(np.random.PCG64(1000 + seed))
-    sd = {k: (v.copy() if isinstance(v, np.ndarray) else v) for k, v in sd.items()}
-    if kind == "norms":
-        for k in emb_keys:
-            sd[k] = _row_norms(rng, sd[k])
-    elif kind == "student_t":
-        for k, v in sd.items():
-            if not isinstance(v, np.ndarray) or v.dtype != np.float32 or "running" in k:
-                continue
-            if k.startswith("deep_network") and v.ndim == 1 and int(k.split(".")[1]) % 4 == 2:
-                continue  # BatchNorm affine: kept (the "bn" kind stresses it)
-            spread = float(v.std()) if v.std() > 0 else 0.05
-            sd[k] = _t3(rng, v.shape, spread)
-    elif kind == "big":
-        sd[item_key][77] = np.float32(1e6) * np.sign(sd[item_key][77] + 1e-30)
-    elif kind == "huge":
-        sd[item_key][77] = np.float32(1e13) * np.sign(sd[item_key][77] + 1e-30)
-    elif kind == "bn":
-        for k in list(sd):
-            if k.endswith("running_var"):
-                n = sd[k].size
-                sd[k] = (10.0 ** rng.uniform(-4, 0, n)).astype(np.float32)
-                g = k.replace("running_var", "weight")
-                sd[g] = (rng.choice([-1.0, 1.0], n) * rng.uniform(0.1, 10.0, n)).astype(np.float32)
-                sd[k.replace("running_var", "bias")] = rng.uniform(-1, 1, n).astype(np.float32)
-                sd[k.replace("running_var", "running_mean")] = rng.uniform(-0.5, 0.5, n).astype(np.float32)
-    else:
-        raise ValueError(kind)
-    return sd
+    return syn.stress_state_dict(sd, kind, emb_keys, item_key, seed)
 
 
 def _check_bitwise(ex, pf, stats, B, kind, what, I=I_FULL):
@@ -200,3 +161,45 @@ def test_wd_topk_stress_bitwise(kind):
     users = torch.from_numpy(syn.user_batch(m.num_users, B, seed=9)).to(DEV)
     ex, pf, stats = topk_both(m, users)
     _check_bitwise(ex, pf, stats, B, kind, "W&D")
+
+
+@pytest.mark.parametrize("kind", ["init", "personal", "norms", "student_t"])
+def test_ncf_strided_sample_gate(kind):
+    """The certified NCF path's gated per-user strided sample (ncf_cert.hip CERT_STRIDE, round
+    5): whether it runs is predicted on the proxy rows (candidates saved vs. the pass's cost);
+    either way the top-K is bitwise the exact scan's (rows whose segments overflow take the
+    exact fallback, now spread over the whole chip), and the count of rows that used it is
+    all-or-nothing per call.  At U = 60,000 the init weights' user embeddings are 5x larger
+    than at the H&M shape (xavier bounds scale with 1/sqrt(U)).  Measured (round 5, B = 512):
+    init 1,158 candidates a row, bound-limited (the gate correctly predicts no saving: off);
+    personal 413 and norms 106 with the pass on (norms: 598 + overflow rows before it at the
+    H&M shape)."""
+    U, B = 60_000, 512
+    if kind == "init":
+        sd = syn.ncf_state_dict(U, I_FULL, 64, (128, 64, 32), seed=3)
+    elif kind == "personal":
+        sd = syn.ncf_state_dict(U, I_FULL, 64, (128, 64, 32), seed=3, bias_scale=0.05,
+                                emb_scale=20.0)
+    else:
+        sd = syn.ncf_state_dict(U, I_FULL, 64, (128, 64, 32), seed=3, bias_scale=0.05)
+        sd = stress(sd, kind, NCF_EMB, "mlp_item_embedding.weight", 3)
+    m = to_module(NeuralCF(U, I_FULL), sd)
+    users = torch.from_numpy(syn.user_batch(U, B, seed=11)).to(DEV)
+    dev = users.device
+    _lib.set_prefilter(dev, False)
+    try:
+        ev, ei = m.recommend_with_scores(users)
+    finally:
+        _lib.set_prefilter(dev, True)
+    _lib.prefilter_stats(dev, reset=True)
+    _lib.set_option(dev, _lib.HNM_OPT_STATS, 1)
+    try:
+        pv, pi = m.recommend_with_scores(users)
+    finally:
+        _lib.set_option(dev, _lib.HNM_OPT_STATS, 0)
+    rows, cands, fallback, sampled = _lib.prefilter_stats(dev, reset=True, extended=True)
+    print(f"NCF {kind}: candidates/row {cands / max(rows - fallback, 1):.1f}, fallback {fallback}, "
+          f"strided-sample rows {sampled}")
+    assert torch.equal(ei, pi) and torch.equal(ev.view(torch.int32), pv.view(torch.int32))
+    assert rows == B
+    assert sampled in (0, B)

@@ -119,3 +119,19 @@ def test_failed_exchange_aborts_two_phase_call(model):
     assert _bits(model.recommend_with_scores(users))[0].equal(ref[0])
     v, i = sc(users)
     assert torch.equal(i.cpu(), ref[0])
+
+
+def test_prefilter_stats_keeps_current_device():
+    """hnm_ctx_prefilter_stats switches to the ctx's device to read its counters and restores
+    the caller's current device on exit: a diagnostics read of another GPU must not
+    move this thread's later allocations / launches.  Needs 2 GPUs for the cross-device case;
+    the same-device read is checked everywhere."""
+    torch.cuda.set_device(0)
+    _lib.prefilter_stats(torch.device("cuda", 0))
+    assert torch.cuda.current_device() == 0
+    if torch.cuda.device_count() < 2:
+        pytest.skip("cross-device read needs 2 GPUs")
+    _lib.prefilter_stats(torch.device("cuda", 1))
+    assert torch.cuda.current_device() == 0
+    x = torch.empty(4, device="cuda")
+    assert x.device.index == 0

@@ -90,6 +90,27 @@ def test_ncf_deep_tower_chunked_full_catalogue():
     assert_topk_equivalent(rec.cpu().numpy()[rows], ref, 12, what="deep full catalogue")
 
 
+def test_ncf_deep_tower_over_65535_users():
+    """B > 65,535 users with a tiny catalogue: the dense deep-tower launch is cut
+    into < 65,536-user grids inside the C entry and recommend's chunks are capped the same way;
+    rows on either side of the cut equal the same users scored in a small call (bitwise) and
+    the oracle."""
+    U, I, B = 80_000, 40, 70_000
+    sd = syn.ncf_state_dict(U, I, 64, (128, 64, 32, 16), seed=5, bias_scale=0.05, emb_scale=8.0)
+    m = to_module(NeuralCF(U, I, mlp_dims=[128, 64, 32, 16], top_k=12), sd)
+    users = syn.user_batch(U, B, seed=8)
+    dense = m.predict_all_items(t(users))
+    v, rec = m.recommend_with_scores(t(users))
+    rows = [0, 65534, 65535, 65536, B - 1]
+    small = m.predict_all_items(t(users[rows]))
+    assert torch.equal(dense[rows].view(torch.int32), small.view(torch.int32))
+    ref = O.ncf_predict_all_items(sd, users[rows])
+    assert_scores_close(small.cpu().numpy(), ref, "deep B > 65535")
+    assert_topk_equivalent(rec.cpu().numpy()[rows], ref, 12, what="deep B > 65535 top-k")
+    np.testing.assert_array_equal(v.cpu().numpy(),
+                                  np.take_along_axis(dense.cpu().numpy(), rec.cpu().numpy(), 1))
+
+
 def test_ncf_config1_golden():
     """BASELINE configs[0] shape (10k x 5k), reference init distributions."""
     g = load_golden("ncf_config1.npz")

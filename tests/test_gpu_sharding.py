@@ -41,6 +41,9 @@ def _worker(rank, world, port, out_dir):
         m = _model()
         lo, hi = S.shard_range(I, rank, world)
         users = torch.from_numpy(syn.user_batch(U, B, seed=50 + rank)).cuda()
+        # both scorers run the bound-lists exchange (begin_lists -> all_gather -> k-th of the
+        # union -> finish) and the packed pair all_to_all + sorted merge
+        assert hasattr(S.ncf_shard_topk, "begin_lists") and hasattr(S.dot_shard_topk, "begin_lists")
         ncf = S.ItemShardedRecommender(S.ncf_shard_topk(m, lo, hi, K), S.hip_merge, K, lo, rank, world)
         v, i = ncf.recommend(users)
         gu = m.gmf_user_embedding.weight.detach().contiguous()
