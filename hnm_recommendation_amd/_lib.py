@@ -318,10 +318,11 @@ def prefilter_stats(device, reset=False, extended=False):
     """(rows scored, candidates re-scored in fp32, rows that took the exact fallback) summed
     over every thread's ctx on `device`; counted only while HNM_OPT_STATS is on
     (set_option(dev, HNM_OPT_STATS, 1)).  extended: a 4th count, rows whose bound also used
-    the gated per-user strided sample (NeuralCF).  Each read syncs the device; calls other
+    the gated per-user strided sample (NeuralCF); extended="gate" adds the last NCF call's
+    gate inputs (its proxies' predicted candidates without / with the strided sample).  Each read syncs the device; calls other
     threads issue meanwhile may be counted before or after a reset (exact when they are idle)."""
     ctx(device)
-    n = 4 if extended else 3
+    n = (6 if extended == "gate" else 4) if extended else 3
     tot = [0] * n
     for c in _device_ctxs(_dev_index(device)):
         out = (_i64 * n)()

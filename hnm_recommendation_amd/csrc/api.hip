@@ -470,22 +470,29 @@ __global__ __launch_bounds__(256) void topk_merge_kernel(const float* __restrict
   WaveTopK<NS> L;
   L.init();
   const int64_t n = G * (int64_t)kc;
-  for (int64_t base = 0; base < n; base += 64) {
-    const int64_t j = base + lane;
-    float v = -__builtin_inff();
-    int idx = HNM_SENTINEL_IDX;
-    bool ok = false;
-    if (j < n) {
-      const int64_t g = j / kc, q = j % kc;
-      const int64_t off = g * gstride + b * bstride + q;
-      const IdxT ii = ci[off];
-      if (ii >= 0) {
-        v = cv[off];
-        idx = (int)ii;
-        ok = true;
+  // 4 chunks of 64 candidates per round, every load issued before the first offer (one load
+  // round trip per chunk made a row-list merge of ~5.6k candidates a row latency-bound)
+  constexpr int U = 4;
+  for (int64_t base = 0; base < n; base += 64 * U) {
+    IdxT ii[U];
+    float vv[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t j = base + 64 * u + lane;
+      ii[u] = -1;
+      vv[u] = -__builtin_inff();
+      if (j < n) {
+        const int64_t g = j / kc, q = j % kc;
+        const int64_t off = g * gstride + b * bstride + q;
+        ii[u] = ci[off];
+        vv[u] = cv[off];
       }
     }
-    L.offer(v, idx, ok, k);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const bool ok = ii[u] >= 0;
+      L.offer(ok ? vv[u] : -__builtin_inff(), ok ? (int)ii[u] : HNM_SENTINEL_IDX, ok, k);
+    }
   }
   L.store(ov ? ov + ob * k : nullptr, oi + ob * k, k);
 }

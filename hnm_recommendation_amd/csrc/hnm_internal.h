@@ -29,7 +29,8 @@ struct hnm_ctx {
   hipEvent_t* ev1;
   int prefilter;                   // HNM_OPT_PREFILTER (default 1)
   unsigned long long* stats_dev;   // pre-filter counters: rows, candidates, fallback rows,
-                                   // rows whose bound used the gated strided sample
+                                   // rows whose bound used the gated strided sample, and
+                                   // (last NCF call) the gate's predicted proxy candidates
   int stats_on;                    // HNM_OPT_STATS (default 0: counting costs same-address atomics)
   // open two-phase top-K call (hnm_*_topk_begin_f32 ... hnm_*_topk_finish_f32): the
   // workspace holds the begin phase's tables until the matching finish, so every other
@@ -42,7 +43,7 @@ struct hnm_ctx {
     const void* items;      // the item table the begin phase read
   } pend;
 };
-#define HNM_STATS_N 4  // pre-filter counters (hnm_ctx_prefilter_stats_ex)
+#define HNM_STATS_N 6  // pre-filter counters (hnm_ctx_prefilter_stats_ex)
 #define HNM_PEND_NCF_CERT 1
 #define HNM_PEND_NCF_EXACT 2
 #define HNM_PEND_DOT_CERT 3
@@ -117,13 +118,25 @@ __host__ __device__ static inline Partition choose_partition(int64_t I, int64_t 
 }
 
 // Row-list launches -- the certified paths' exact fallback, whose queued rows are known only
-// on the device (rows[0, *nrows)): the grid is (cdiv(B, 128), list_rows_np(I, num_cus)) and
-// each workgroup derives the partition actually used from *nrows, choose_partition(I,
-// cdiv(nrows, 128), num_cus), so that a handful of queued rows still spreads over the whole
-// chip (workgroups past it exit at once).  Candidates of list row b sit at [b][p][K] with row
-// stride np * K; the merge derives np the same way (topk_merge_kernel's dyn_cus).
-static inline int list_rows_np(int64_t I, int num_cus) {
-  return choose_partition(I, 1, num_cus).np;
+// on the device (rows[0, *nrows)): a FLAT grid of list_rows_grid(B, I, num_cus) workgroups;
+// each derives the partition actually used from *nrows, np = choose_partition(I, nb =
+// cdiv(nrows, 128), num_cus).np, and takes (user block w / np, item partition w % np) for
+// w < nb * np (the rest exit), so that a handful of queued rows still spreads over the whole
+// chip.  (A (blocks, partitions) grid sized for the worst case launched ~15k mostly empty
+// workgroups of 78 KB LDS: 12.5 ms of dispatch for 19 queued rows, round 5.)  Candidates of list
+// row b sit at [b][p][K] with row stride np * K; the merge derives np the same way
+// (topk_merge_kernel's dyn_cus).
+static inline int64_t list_rows_grid(int64_t B, int64_t I, int num_cus) {
+  int64_t best = 1;
+  for (int64_t nb = 1; nb <= hnm_cdiv(B, 128); ++nb) {
+    const int np = choose_partition(I, nb, num_cus).np;
+    best = std::max<int64_t>(best, nb * np);
+    if (np == 1) {
+      best = std::max<int64_t>(best, hnm_cdiv(B, 128));
+      break;
+    }
+  }
+  return best;
 }
 // candidate slots (rows x partitions) a row-list launch over <= B queued rows can write
 static inline int64_t list_rows_slots(int64_t B, int64_t I, int num_cus) {

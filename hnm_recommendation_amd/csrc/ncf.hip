@@ -55,16 +55,20 @@ __global__ __launch_bounds__(256, 2) void ncf32_kernel(
   extern __shared__ __attribute__((aligned(16))) float lists[];  // [4][32][K] v, then i
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5, j = lane & 31;
-  const int64_t ublk = (int64_t)blockIdx.x * NU;
+  int64_t ublk = (int64_t)blockIdx.x * NU;
+  int p = blockIdx.y;
   if (rows) B = *nrows;
-  if (ublk >= B) return;  // whole workgroup: before any barrier
-  if (rows && dyn_cus > 0) {
-    const Partition dp = choose_partition(I, hnm_cdiv(B, NU), dyn_cus);
+  if (rows && dyn_cus > 0) {  // flat grid: (user block, partition) from *nrows (list_rows_grid)
+    const int64_t nb = hnm_cdiv(B, NU);
+    const Partition dp = choose_partition(I, nb, dyn_cus);
     NP = dp.np;
     ipp = dp.ipp;
+    const int64_t w = blockIdx.x;
+    if (w >= nb * NP) return;  // whole workgroup: before any barrier
+    ublk = w / NP * NU;
+    p = (int)(w % NP);
   }
-  const int p = blockIdx.y;
-  if (p >= NP) return;  // whole workgroup (dynamic row-list partitions)
+  if (ublk >= B || p >= NP) return;  // whole workgroup: before any barrier
   auto R = [&](int64_t b) -> int64_t { return rows ? (int64_t)rows[b] : b; };
   const int64_t u0 = ublk + wave * 32;  // first user of this wave
   const int nu = (int)std::max<int64_t>(0, std::min<int64_t>(32, B - u0));
@@ -612,10 +616,9 @@ hnm_status ncf_list_rows(hnm_ctx* ctx, const hnm_ncf_weights* w, const NcfTabs& 
                          const int32_t* nrows, float* cv, int32_t* ci, float* ov, int64_t* oi) {
   // the queued rows are known only on the device: the widest grid, the partitions used
   // derived from *nrows in the kernel and the merge (hnm_internal.h list_rows_np)
-  const int64_t ublocks = hnm_cdiv(B, 128);
-  const int npmax = list_rows_np(w->num_items, ctx->num_cus);
-  launch_ncf32<false>(ctx, dim3((unsigned)ublocks, (unsigned)npmax), t, w, B, 0, mptr, midx, K,
-                      cv, ci, npmax, nullptr, 0, rows, nrows, ctx->num_cus);
+  const int64_t grid = list_rows_grid(B, w->num_items, ctx->num_cus);
+  launch_ncf32<false>(ctx, dim3((unsigned)grid, 1), t, w, B, 0, mptr, midx, K, cv, ci, 1, nullptr,
+                      0, rows, nrows, ctx->num_cus);
   HNM_LAUNCH_CHECK();
   return hnm_topk_merge_rows(ctx, cv, ci, B, 1, 0, K, K, K, ov, oi, rows, nrows, w->num_items,
                              ctx->num_cus);

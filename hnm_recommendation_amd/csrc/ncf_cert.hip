@@ -959,31 +959,87 @@ struct Top4 {
   }
 };
 
-// Gate, step 1 (one workgroup, wave r = proxy row r): kv[2r] = the K-th of the row's
-// (approx - e_i) over its leave-one-out champions, kv[2r + 1] = the larger of that and the K-th
-// over the strided tiles; zeroes the count kernel's counters; writes the strided sample's item
-// map (tiles 0, S, 2S, ... of 32 items: sidx2[0, ns)).
-__global__ __launch_bounds__(512) void cert_gate_kth_kernel(const float* __restrict__ pd,
+// Gate, step 1 (one workgroup of 256 threads per proxy row r): kv[2r] = a lower bound of the
+// K-th of the row's (approx - e_i) over its leave-one-out champions, kv[2r + 1] = the larger of
+// that and the same over the strided tiles (lane top-4 lists, each wave's K pops, then the
+// K-th of the 4 waves' lists; loads issued 8 at a time: the rows sit in L2, the latency of
+// one dependent load per iteration would cost ~0.1 ms).  Workgroup 0 also zeroes the count
+// kernel's counters and writes the strided sample's item map (tiles 0, S, 2S, ... of 32 items:
+// sidx2[0, ns)).
+__global__ __launch_bounds__(256) void cert_gate_kth_kernel(const float* __restrict__ pd,
                                                             int64_t ld, int np_rows,
                                                             const int32_t* __restrict__ sloo,
                                                             int64_t nch, int K, int64_t ns,
                                                             int32_t* __restrict__ sidx2,
                                                             float* __restrict__ kv,
                                                             unsigned long long* __restrict__ cnt) {
-  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  for (int64_t n = threadIdx.x; n < ns; n += 512)
-    sidx2[n] = (int32_t)((n >> 5) * (32 * CERT_STRIDE) + (n & 31));
-  if (threadIdx.x < 4) cnt[threadIdx.x] = 0;
-  if (w >= np_rows) return;
-  const float* row = pd + w * ld;
-  const int32_t* sl = sloo + w * nch;
+  __shared__ float wl[2][4][64];
+  const int r = blockIdx.x, tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+  if (r == 0) {
+    for (int64_t n = tid; n < ns; n += 256)
+      sidx2[n] = (int32_t)((n >> 5) * (32 * CERT_STRIDE) + (n & 31));
+    if (tid < 4) cnt[tid] = 0;
+  }
+  const float* row = pd + r * ld;
+  const int32_t* sl = sloo + r * nch;
   Top4 c, t;
-  for (int64_t q = lane; q < nch; q += 64) c.offer(row[sl[q]]);
-  for (int64_t n = lane; n < ns; n += 64) t.offer(row[(n >> 5) * (32 * CERT_STRIDE) + (n & 31)]);
-  const float kc = c.kth(K, lane), ks = t.kth(K, lane);
-  if (lane == 0) {
-    kv[2 * w] = kc;
-    kv[2 * w + 1] = fmaxf(kc, ks);
+  constexpr int U = 8;
+  for (int64_t q0 = 0; q0 < nch; q0 += 256 * U) {
+    int32_t ix[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t q = q0 + u * 256 + tid;
+      ix[u] = q < nch ? sl[q] : -1;
+    }
+    float v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = ix[u] >= 0 ? row[ix[u]] : -__builtin_inff();
+#pragma unroll
+    for (int u = 0; u < U; ++u) c.offer(v[u]);
+  }
+  for (int64_t n0 = 0; n0 < ns; n0 += 256 * U) {
+    float v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t n = n0 + u * 256 + tid;
+      v[u] = n < ns ? row[(n >> 5) * (32 * CERT_STRIDE) + (n & 31)] : -__builtin_inff();
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) t.offer(v[u]);
+  }
+  // each wave's K best survivors (descending) -> LDS; then wave 0 takes the K-th of the 4 K
+  for (int i = 0; i < 2; ++i) {
+    Top4& L = i ? t : c;
+    for (int q = 0; q < K; ++q) {
+      float m = L.t0;
+#pragma unroll
+      for (int o = 32; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+      if (lane == 0) wl[i][w][q] = m;
+      if (m == -__builtin_inff()) {
+        for (int z = q + 1 + lane; z < K; z += 64) wl[i][w][z] = -__builtin_inff();
+        break;  // wave-uniform
+      }
+      const int wk = __builtin_ctzll(__ballot(L.t0 == m));
+      if (lane == wk) {
+        L.t0 = L.t1;
+        L.t1 = L.t2;
+        L.t2 = L.t3;
+        L.t3 = -__builtin_inff();
+      }
+    }
+  }
+  __syncthreads();
+  if (w == 0) {
+    float res[2];
+    for (int i = 0; i < 2; ++i) {
+      Top4 M;
+      for (int z = lane; z < 4 * K; z += 64) M.offer(wl[i][z / K][z % K]);
+      res[i] = M.kth(K, lane);
+    }
+    if (lane == 0) {
+      kv[2 * r] = res[0];
+      kv[2 * r + 1] = fmaxf(res[0], res[1]);
+    }
   }
 }
 
@@ -1030,8 +1086,12 @@ __global__ __launch_bounds__(256) void cert_gate_count_kernel(
       const int on = (np_rows >= 4 && !prm->bad &&
                       c0 > c1 + (unsigned long long)(CERT_GATE_GAIN * np_rows)) ? 1 : 0;
       *gate = on;
-      cnt[3] = c0;  // (diagnostics: the proxies' predicted candidates, champion bound alone)
-      if (on && stats) atomicAdd(&stats[3], (unsigned long long)B);
+      if (stats) {
+        if (on) atomicAdd(&stats[3], (unsigned long long)B);
+        // diagnostics (last call): the proxies' predicted candidates under each bound
+        stats[4] = c0;
+        stats[5] = c1;
+      }
     }
   }
 }
@@ -1497,8 +1557,8 @@ hnm_status ncf_cert_begin(hnm_ctx* ctx, const hnm_ncf_weights* w, const NcfTabs&
   hipLaunchKernelGGL(cert_champion_kernel, dim3((unsigned)hnm_cdiv(sh.nch, 4)), dim3(256), 0,
                      ctx->stream, x.pdense, I, (int)bp, I, sh.gsz, sh.nch, x.sidx, x.sloo);
   HNM_LAUNCH_CHECK();
-  hipLaunchKernelGGL(cert_gate_kth_kernel, dim3(1), dim3(512), 0, ctx->stream, x.pdense, I,
-                     (int)bp, x.sloo, sh.nch, K, sh.ns, x.sidx2, x.gkv, x.gcnt);
+  hipLaunchKernelGGL(cert_gate_kth_kernel, dim3((unsigned)bp), dim3(256), 0, ctx->stream,
+                     x.pdense, I, (int)bp, x.sloo, sh.nch, K, sh.ns, x.sidx2, x.gkv, x.gcnt);
   HNM_LAUNCH_CHECK();
   if (bp >= 4) {
     hipLaunchKernelGGL(cert_gate_count_kernel, dim3(CERT_GATE_CHUNKS, (unsigned)bp), dim3(256), 0,

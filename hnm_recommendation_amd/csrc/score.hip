@@ -46,17 +46,22 @@ __global__ __launch_bounds__(256, (MODE == DOT_LIST || DP > 64) ? 2 : 4) void do
   const int h = lane >> 5;
   const int j = lane & 31;
   const int64_t Bl = A.nrows ? (int64_t)*A.nrows : A.B;  // rows of this launch
-  const int64_t b0 = (int64_t)blockIdx.x * 128 + wave * 32;
-  if ((int64_t)blockIdx.x * 128 >= Bl) return;  // whole workgroup idle (fallback launches)
+  int64_t ublk = (int64_t)blockIdx.x * 128;
   int64_t ipp = A.ipp;
   int NP = A.NP;
-  if (A.rows && A.dyn_cus > 0) {  // row-list launch: partitions follow *nrows (list_rows_np)
-    const Partition dp = choose_partition(A.I, hnm_cdiv(Bl, 128), A.dyn_cus);
+  int p = blockIdx.y;
+  if (A.rows && A.dyn_cus > 0) {  // flat grid: (user block, partition) from *nrows
+    const int64_t nb = hnm_cdiv(Bl, 128);
+    const Partition dp = choose_partition(A.I, nb, A.dyn_cus);
     ipp = dp.ipp;
     NP = dp.np;
+    const int64_t w = blockIdx.x;
+    if (w >= nb * NP) return;  // whole workgroup
+    ublk = w / NP * 128;
+    p = (int)(w % NP);
   }
-  const int p = blockIdx.y;
-  if (p >= NP) return;  // whole workgroup
+  if (ublk >= Bl || p >= NP) return;  // whole workgroup idle (fallback launches)
+  const int64_t b0 = ublk + wave * 32;
   const int64_t part_start = (int64_t)p * ipp;
   const int64_t part_end = std::min<int64_t>(A.I, part_start + ipp);
   const int64_t K = A.K;
@@ -545,11 +550,10 @@ hnm_status dot_list_pass(hnm_ctx* ctx, DotArgs a, bool bias, float* cv, int32_t*
   if (a.rows) {
     // the queued rows are known only on the device: the widest grid, the partitions used
     // derived from *nrows in the kernel and the merge (hnm_internal.h list_rows_np)
-    const int npmax = list_rows_np(a.I, ctx->num_cus);
     a.ipp = 0;
-    a.NP = npmax;
+    a.NP = 1;
     a.dyn_cus = ctx->num_cus;
-    launch_dot<DOT_LIST>(ctx, dim3((unsigned)ublocks, (unsigned)npmax), a, bias);
+    launch_dot<DOT_LIST>(ctx, dim3((unsigned)list_rows_grid(a.B, a.I, ctx->num_cus), 1), a, bias);
     HNM_LAUNCH_CHECK();
     return hnm_topk_merge_rows(ctx, cv, ci, a.B, 1, 0, a.K, a.K, a.K, ov, oi, a.rows, a.nrows,
                                a.I, ctx->num_cus);

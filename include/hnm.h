@@ -83,8 +83,10 @@ hnm_status hnm_ctx_set_option(hnm_ctx* ctx, int option, int64_t value);
  * another thread owns; counts of calls that thread issues while this runs may land before or
  * after a reset (totals are exact for threads that are idle meanwhile). */
 hnm_status hnm_ctx_prefilter_stats(hnm_ctx* ctx, int64_t* out, int reset);
-/* The same counters, the first n of 4: out[3] = rows whose bound also used the per-user strided
- * sample (NeuralCF: gated on when the champion sample is poor for the call's weights). */
+/* The same counters, the first n of 6: out[3] = rows whose bound also used the per-user strided
+ * sample (NeuralCF: gated on when it is predicted to save re-scoring); out[4] / out[5] = the
+ * last NeuralCF call's gate inputs: candidates its proxy rows would re-score with the champion
+ * bound alone / with the strided sample's bound too (diagnostics). */
 hnm_status hnm_ctx_prefilter_stats_ex(hnm_ctx* ctx, int64_t* out, int n, int reset);
 /* Dominant-kernel timer: while on, calls record HIP events on the ctx stream around their
  * main kernel; `mask` selects the class: 1 = the scoring / scan kernel of every top-K or
