@@ -37,13 +37,8 @@ constexpr int64_t DCERT_MIN_ITEMS = 8192;
 // candidates a row, scan 0.105 ms; stride 4 -> 55, 0.096 ms; stride 2 -> 28, 0.087 ms -- the
 // step is the same for 4 and 2 (the sample pass grows by what the scan saves), 10 % shorter
 // than stride 8 once the sample pass's max runs as one v_max3 per row and sub-tile pair.
-#ifndef DCERT_SAMPLE_N
-#define DCERT_SAMPLE_N 52771
-#endif
-constexpr int64_t DCERT_SAMPLE = DCERT_SAMPLE_N;
-#ifndef DCERT_MIN_STRIDE
-#define DCERT_MIN_STRIDE 2
-#endif  // sampled items: stride max(8, I / this)
+constexpr int64_t DCERT_SAMPLE = 52771;  // sampled items: stride max(DCERT_MIN_STRIDE, I / this)
+constexpr int64_t DCERT_MIN_STRIDE = 2;
 constexpr float DCERT_RHO = 0.00146484375f;  // 3 u16 = 3 * 2^-11
 constexpr int DCERT_MAX_NP = 64;
 
@@ -52,28 +47,15 @@ constexpr int DCERT_MAX_NP = 64;
 // CU 0.1845 / 0.0866 (half the LDS fragment reads did not pay for the lost occupancy), the
 // sample pass at NB = 2 0.2011 (its running max then costs 3 instructions a value); round 3's
 // 64-bit tile addressing 0.1872 / 0.0886
-#ifndef DOT_NB64
-#define DOT_NB64 1
-#endif
-#ifndef DOT_NB128
-#define DOT_NB128 1
-#endif
 enum { DSCAN_DENSE = 0, DSCAN_THRESH = 1, DSCAN_SAMPLE = 2 };  // scan modes (below)
-#ifndef DOT_NB64S  // the sample pass (its running max at NB = 2 costs 3 instructions a value)
-#define DOT_NB64S 1
-#endif
-__host__ __device__ constexpr int dscan_nb(int DP, int MODE) {
-  return DP > 64 ? DOT_NB128 : (MODE == DSCAN_SAMPLE ? DOT_NB64S : DOT_NB64);
-}
+// (the kernel keeps its NB template parameter; every product launch uses NB = 1)
+__host__ __device__ constexpr int dscan_nb(int DP, int MODE) { return 1; }
 __host__ __device__ constexpr int dscan_users(int DP, int MODE) { return 128 * dscan_nb(DP, MODE); }
 // scan occupancy (workgroups per CU): NB = 1, two sub-tiles in flight, fits 3 in 168 VGPRs;
 // NB = 2 (two user blocks' A operands and thresholds) needs ~230: 2
 // Round 4 A/B (MF step / THRESH scan): 3 workgroups per CU 0.1805 / 0.0832 ms, 2 per CU
 // 0.1911 / 0.0953; 64-item tiles 0.1804 / 0.0859; 256-item tiles at 2 per CU 0.1899 / 0.0923
-#ifndef DOT_WG1
-#define DOT_WG1 3
-#endif
-__host__ __device__ constexpr int dcert_wg_per_cu(int NB) { return NB == 2 ? 2 : DOT_WG1; }
+__host__ __device__ constexpr int dcert_wg_per_cu(int NB) { return NB == 2 ? 2 : 3; }
 
 enum { DM_U, DM_I, DM_NI, DM_IB, DM_N };
 
@@ -385,10 +367,7 @@ __global__ __launch_bounds__(256, dcert_wg_per_cu(NB)) void dot16_scan_kernel(DS
   constexpr int KS = DP / 16;     // f16 MFMA k-steps
   constexpr int RS = DP + 8;      // LDS row stride (halfs): conflict-free b128 reads
   constexpr int CH = DP / 8;      // 16-B chunks per item row
-#ifndef DOT_TI
-#define DOT_TI 0
-#endif
-  constexpr int TI = DOT_TI > 0 ? DOT_TI : (DP <= 64 ? 128 : 64);  // items per LDS tile
+  constexpr int TI = DP <= 64 ? 128 : 64;  // items per LDS tile
   constexpr int SUB = TI / TILE;
   constexpr int LD = TI * CH / 256;  // chunks per thread per tile (4)
   constexpr int UW = 32 * NB;        // users per wave

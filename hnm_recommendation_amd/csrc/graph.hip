@@ -27,93 +27,41 @@
 #include "hnm_device.h"
 #include "hnm_internal.h"
 
-#ifndef HEAVY
-#define HEAVY 2048
-#endif
-#ifndef SEG
-#define SEG 2048
-#endif
+// Fixed design constants (round 5: the measured-and-dropped A/B switches of rounds 2-4 --
+// walk launch order / side stream, record prefetch in the long-row walk, column windows in the
+// short walk, the CSR-order short rows, ... -- are gone; DESIGN.md §4 keeps their numbers).
+//
 // Row classes by entry count L (self-loop included), decided per row so that every kernel that
 // sums a row (the layer kernels, rows_combine) uses the same order:
 //   short  L <= SPMM_SHORT           one LPR-lane group per row, 64 / LPR rows per wave
 //   long   SPMM_SHORT < L <= HEAVY   one wave per row (4 neighbour groups + a fixed tree)
 //   heavy  L > HEAVY                 SEG-long segments + a finish kernel
-// SPMM_SHORT 0 puts every light row in the long class (the round-2 kernel).
-#ifndef SPMM_SHORT
+// Graphs of up to 2^22 nodes (every BASELINE graph) run the two walks below instead: short rows
+// by the column-ordered short walk, the others by the user-ordered walk; the classes above
+// remain the plan-less path and the path of larger graphs (both tested).
+#define HEAVY 2048
+#define SEG 2048
 #define SPMM_SHORT 128
-#endif
-#define SPMM_GROUPED (SPMM_SHORT > 0)
-#ifndef SPMM_SIDE_STREAM  // heavy-row segments on the ctx's side stream, beside the light kernel
-#define SPMM_SIDE_STREAM 1
-#endif
-// Round 3: rows of more than SPMM_SHORT entries (the item half of the bipartite graph) by the
-// user-ordered walk (spmm_walk_kernel, below) instead of the long / heavy classes.
-#ifndef SPMM_WALK
-#define SPMM_WALK 1
-#endif
-// 0: walk on the side stream beside the short rows; 1: walk then short rows; 2: short then walk
-// (measured, d=64 layer: 1.725 / 1.700 / 1.689 ms; 0 with a normal-priority side stream 1.732)
-#ifndef SPMM_WALK_MODE
-#define SPMM_WALK_MODE 2
-#endif
+// the long-row walk: 1024-thread workgroups (one per CU), 144 KiB of float4 row accumulators,
+// lists cut at WALK_WIN column windows with a workgroup barrier after each (d=64 layer: no
+// windows 1.635 ms, 4: 1.499, 8: 1.448, 16: 1.431-1.451, 32: 1.474), WALK_STEP entries a step
+// (round 4, whole-graph layer d=64 / d=128: 4 entries 1.308 / 2.676 ms, 4 + records prefetched a
+// step ahead 1.415 / 2.920, 8 entries 1.435 / 3.017), pieces cut for ~WALK_GROUPS_TARGET groups
 #define WALK_THREADS 1024
-// Column windows: each group's list is cut at WALK_WIN column bounds and the workgroup's groups
-// meet at a barrier after every window, so a CU's 64 lists stay inside one window of X (without
-// it a short list runs ahead of a long one through the table).  d=64 layer: no windows 1.635 ms,
-// 4: 1.499, 8: 1.448, 16: 1.431-1.451, 32: 1.474, 64: 1.508 (per-window imbalance grows).
-#ifndef WALK_WIN
 #define WALK_WIN 16
-#endif
-// entries per walk step and the records' prefetch a step ahead (as SWALK_STEP / SWALK_PF).
-// Round 4 A/B on the final tree (whole-graph layer, d=64 / d=128): 4 entries 1.308 / 2.676 ms,
-// 4 + prefetch 1.415 / 2.920, 8 entries 1.435 / 3.017, 8 + prefetch 1.448 / 3.090 -- unlike the
-// short walk, the long-row walk's 16 windows (barriers) already overlap its record loads.
-// SPMM_WALK_MODE on the same box: 2 (default) 1.308 / 2.676, 1 1.308 / 2.678, 0 1.318 / 2.928.
-#ifndef WALK_STEP
 #define WALK_STEP 4
-#endif
-#ifndef WALK_PF
-#define WALK_PF 0
-#endif
-#ifndef WALK_LDS_F4
-#define WALK_LDS_F4 9216        // 144 KiB of float4 row accumulators per workgroup
-#endif
-#ifndef WALK_GROUPS_TARGET
-#define WALK_GROUPS_TARGET 16384  // total LPR-lane groups of a big graph's walk (all d)
-#endif
-// Round 4: the short rows (<= SPMM_SHORT entries: every user row) by a column-ordered walk too
-// (spmm_swalk_kernel): blocks of consecutive rows hold their accumulators in LDS and every
-// lane group walks its rows' entries merged in column order, so the chip's gathers move through
-// the item table together (L2 hit rate 0.52 -> 0.64).  1 = on, 0 = one row per lane group in CSR
-// order (round 3).  Measured alternatives (A/B on one box, d = 64 layer, `git show a7c47dc`):
-// the mixed kernel with two rows per group interleaved 1.72 ms, the short rows one group each
-// with the ~600 most gathered item rows held in LDS (~40 % of the user half's gathers) 1.46-1.65
-// ms, vs 1.36 ms for this walk with 2 workgroups per CU, records a step ahead, 8 gathers a step.
-#ifndef SPMM_SWALK
-#define SPMM_SWALK 1
-#endif
-// column windows of the short walk (1: none; a barrier after each window otherwise)
-#ifndef SWALK_WIN
-#define SWALK_WIN 1
-#endif
-// persistent short-walk workgroups per CU, their threads and LDS accumulators (float4)
-#ifndef SWALK_WG_PER_CU
+#define WALK_LDS_F4 9216
+#define WALK_GROUPS_TARGET 16384
+// the short walk (round 4): 2 persistent 512-thread workgroups per CU, 72 KiB of float4 row
+// accumulators each, 8 entries a step with the records loaded a step ahead.  Measured and
+// dropped (A/B on one box, d = 64 layer, `git show a7c47dc`): the short rows one lane group
+// each in CSR order 1.44 ms, two rows per group interleaved 1.72 ms, the ~600 most gathered item
+// rows held in LDS 1.46-1.65 ms, column windows with barriers 1.537 / 1.602 ms (4 / 8 windows),
+// vs 1.305 ms for this walk.
 #define SWALK_WG_PER_CU 2
-#endif
-#ifndef SWALK_THREADS
 #define SWALK_THREADS 512
-#endif
-#ifndef SWALK_LDS_F4
 #define SWALK_LDS_F4 4608
-#endif
-// entries per list step (gathers in flight per lane group) and the records' prefetch a step
-// ahead (0: loaded at the step, right before their gathers)
-#ifndef SWALK_STEP
 #define SWALK_STEP 8
-#endif
-#ifndef SWALK_PF
-#define SWALK_PF 1
-#endif
 // Round 4, measured and dropped: aligning the workgroups of an XCD -- a bounded wait (per-XCD
 // progress counters, atomics at agent scope) before each short-walk round until all but 1/8 of
 // the XCD's workgroups finished the previous one, and the same before each of the long-row
@@ -123,18 +71,12 @@
 // (tools/gather_probe.hip: uniformly random 256-B rows gather at 8.4-8.6 TB/s from a 27 MB
 // table and 7.0-7.3 TB/s from 351 MB whatever the loads in flight, 23 TB/s from an
 // L2-resident 4 MB one; the two walks' 12.8 TB/s lies between: their column order already
-// serves ~62 % of the gathered bytes from L2.)
-// Also measured and dropped (round 4): the long-row walk split by XCD column ranges -- every
-// walk row of > SPMM_SHORT entries cut at 8 column bounds (equal shares of entries), range x's
-// pieces on workgroups of XCD x with their windows inside range x, rows_combine repeating the
-// range pieces -- bitwise-consistent (32 SpMM / LightGCN GPU tests green) but the walk ran 668
-// -> 1,155 us a launch: ~4x the pieces for the same 575 LDS slots a workgroup (d = 64) means
-// ~4x the workgroups, each a whole window sweep for a quarter of the entries, and every item
-// row then takes the partial + finish path (finish 12 -> 42 us).
-// bipartite graphs: the short rows of the side that gathers the larger table join the walk
-#ifndef SPMM_SIDE_WALK
-#define SPMM_SIDE_WALK 1
-#endif
+// serves ~62 % of the gathered bytes from L2.  Round 5, tools/granule_probe.hip: gathers of
+// column slices -- 32 / 64 / 128-B granules from slice tables of 3.4 / 6.8 / 13.5 MB -- run at
+// 4.3 / 5.3 / 8.8 TB/s, below the walks' rate: slicing the item table per XCD cannot pay.)
+// Also measured and dropped (round 4): the long-row walk split by XCD column ranges (668 ->
+// 1,155 us a launch: ~4x the pieces for the same LDS slots), and the walk on the side stream
+// beside the short rows (1.318 / 2.928 ms vs 1.308 / 2.676).
 
 struct WalkSched;
 struct ShortSched;
@@ -156,9 +98,9 @@ struct hnm_spmm_plan {
   int64_t* seg_end;     // [n_seg]
   std::vector<int32_t>* h_heavy;  // host copies (row-range launches)
   std::vector<int64_t>* h_seg_ptr;
-  // user-ordered walk of the rows of more than SPMM_SHORT entries (SPMM_WALK)
+  // user-ordered walk of the rows of more than SPMM_SHORT entries
   int walk;
-  int swalk;            // short rows by the column-ordered short walk (SPMM_SWALK)
+  int swalk;            // short rows by the column-ordered short walk
   int64_t walk_cap;     // entries per piece: a row of L entries is cut into cdiv(L, cap) pieces
   int64_t n_walk, walk_nnz;
   std::vector<int32_t>* h_walk_rows;  // ascending
@@ -608,9 +550,8 @@ __global__ __launch_bounds__(WALK_THREADS) void spmm_walk_kernel(
   const int ns = nslot[blockIdx.x];
   for (int i = tid; i < ns * LPR; i += WALK_THREADS) acc[i] = make_float4(0.f, 0.f, 0.f, 0.f);
   __syncthreads();
-  // WALK_STEP entries per step (round 3, unprefetched: 2: 1.741 ms per d=64 layer, 4: 1.694,
-  // 8: 1.848); WALK_PF: the next step's records loaded before this step's gathers
-  constexpr int K = WALK_WIN > 1 ? WALK_WIN : 1;
+  // WALK_STEP entries per step (round 3: 2: 1.741 ms per d=64 layer, 4: 1.694, 8: 1.848)
+  constexpr int K = WALK_WIN;
   constexpr int ST = WALK_STEP;
   auto consume = [&](const uint32_t* c, const float* w) {
     float4 x[ST];
@@ -631,42 +572,15 @@ __global__ __launch_bounds__(WALK_THREADS) void spmm_walk_kernel(
   for (int k = 0; k < K; ++k) {
     int64_t p = gptr[((int64_t)blockIdx.x * NG + g) * K + k];
     const int64_t e = gptr[((int64_t)blockIdx.x * NG + g) * K + k + 1];
-    if (WALK_PF) {
-      uint32_t c[ST], cn[ST];
-      float w[ST], wn[ST];
-      if (p + ST - 1 < e) {
+    for (; p + ST - 1 < e; p += ST) {
+      uint32_t c[ST];
+      float w[ST];
 #pragma unroll
-        for (int u = 0; u < ST; ++u) {
-          cn[u] = ent[p + u];
-          wn[u] = wt[p + u];
-        }
+      for (int u = 0; u < ST; ++u) {
+        c[u] = ent[p + u];
+        w[u] = wt[p + u];
       }
-      for (; p + ST - 1 < e; p += ST) {
-#pragma unroll
-        for (int u = 0; u < ST; ++u) {
-          c[u] = cn[u];
-          w[u] = wn[u];
-        }
-        if (p + 2 * ST - 1 < e) {
-#pragma unroll
-          for (int u = 0; u < ST; ++u) {
-            cn[u] = ent[p + ST + u];
-            wn[u] = wt[p + ST + u];
-          }
-        }
-        consume(c, w);
-      }
-    } else {
-      for (; p + ST - 1 < e; p += ST) {
-        uint32_t c[ST];
-        float w[ST];
-#pragma unroll
-        for (int u = 0; u < ST; ++u) {
-          c[u] = ent[p + u];
-          w[u] = wt[p + u];
-        }
-        consume(c, w);
-      }
+      consume(c, w);
     }
     for (; p < e; ++p) {
       const uint32_t c = ent[p];
@@ -711,7 +625,6 @@ __global__ __launch_bounds__(SWALK_THREADS) void spmm_swalk_kernel(
     const int32_t* __restrict__ nslot, int S, const float* __restrict__ X, int d, SpmmEpi ep,
     int64_t r0, int64_t r1, int64_t b0, int64_t b1) {
   constexpr int NG = SWALK_THREADS / LPR;
-  constexpr int K = SWALK_WIN > 1 ? SWALK_WIN : 1;
   constexpr int ST = SWALK_STEP;
   __shared__ float4 acc[SWALK_LDS_F4];
   const int tid = threadIdx.x, g = tid / LPR, sub = tid % LPR;
@@ -734,47 +647,32 @@ __global__ __launch_bounds__(SWALK_THREADS) void spmm_swalk_kernel(
     }
   };
   for (int64_t b = b0 + blockIdx.x; b < b1; b += gridDim.x) {
-    for (int k = 0; k < K; ++k) {
-      int64_t p = gptr[(b * NG + g) * K + k];
-      const int64_t e = gptr[(b * NG + g) * K + k + 1];  // lists are padded to multiples of ST
-      if (SWALK_PF) {
-        uint32_t c[ST], cn[ST];
-        float w[ST], wn[ST];
-        if (p < e) {
+    int64_t p = gptr[b * NG + g];
+    const int64_t e = gptr[b * NG + g + 1];  // lists are padded to multiples of ST
+    // the next step's records are loaded before this step's gathers
+    uint32_t c[ST], cn[ST];
+    float w[ST], wn[ST];
+    if (p < e) {
 #pragma unroll
-          for (int u = 0; u < ST; ++u) {
-            cn[u] = ent[p + u];
-            wn[u] = wt[p + u];
-          }
-        }
-        for (; p < e; p += ST) {
+      for (int u = 0; u < ST; ++u) {
+        cn[u] = ent[p + u];
+        wn[u] = wt[p + u];
+      }
+    }
+    for (; p < e; p += ST) {
 #pragma unroll
-          for (int u = 0; u < ST; ++u) {
-            c[u] = cn[u];
-            w[u] = wn[u];
-          }
-          if (p + ST < e) {
+      for (int u = 0; u < ST; ++u) {
+        c[u] = cn[u];
+        w[u] = wn[u];
+      }
+      if (p + ST < e) {
 #pragma unroll
-            for (int u = 0; u < ST; ++u) {
-              cn[u] = ent[p + ST + u];
-              wn[u] = wt[p + ST + u];
-            }
-          }
-          consume(c, w);
-        }
-      } else {
-        for (; p < e; p += ST) {
-          uint32_t c[ST];
-          float w[ST];
-#pragma unroll
-          for (int u = 0; u < ST; ++u) {
-            c[u] = ent[p + u];
-            w[u] = wt[p + u];
-          }
-          consume(c, w);
+        for (int u = 0; u < ST; ++u) {
+          cn[u] = ent[p + ST + u];
+          wn[u] = wt[p + ST + u];
         }
       }
-      if (K > 1) __syncthreads();
+      consume(c, w);
     }
     __syncthreads();
     const int ns = nslot[b];
@@ -985,7 +883,7 @@ __global__ __launch_bounds__(256) void spmm_rows_combine_kernel(
   __shared__ float4 slices[4][256];
   const int lane = threadIdx.x & 63;
   const float* Xl = cl.E[cl.L - 1];
-  if (!SPMM_GROUPED || co.mode == 0) {
+  if (co.mode == 0) {
     const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (b >= n) return;
     const int64_t r = rows[b];
@@ -1077,7 +975,7 @@ static void walk_sched_free(WalkSched* w) {
 struct ShortSched {
   int lpr, ng, S, nwg;
   int64_t nb;
-  int64_t* gptr;     // [nb * ng * K + 1] (K = SWALK_WIN)
+  int64_t* gptr;     // [nb * ng + 1]
   uint32_t* ent;     // col << 10 | slot (slot S: padding, weight 0)
   float* wt;
   int32_t* srow;     // [nb * S] row of each slot
@@ -1228,7 +1126,7 @@ static hnm_status plan_bind(hnm_ctx* ctx, hnm_spmm_plan* pl, const int32_t* col,
     pl->sval = dval;
     pl->h_scol = hcp.release();
     pl->h_sval = hvp.release();
-    if (SPMM_SIDE_WALK && pl->swalk) plan_bipartite_sides(pl);
+    if (pl->swalk) plan_bipartite_sides(pl);
   }
   pl->bound_col = col;
   pl->bound_val = val;
@@ -1370,9 +1268,8 @@ static hnm_status walk_build(hnm_spmm_plan* pl, int d, WalkSched** out) {
 // Short-walk schedule for d: the short rows cut into nb blocks of consecutive rows at equal
 // shares of their entries (at most S rows a block; nb a multiple of the persistent grid once the
 // graph fills it), each block's rows dealt to its ng lane groups (longest first, least-loaded
-// group), each group's rows' entries merged by column, cut at SWALK_WIN column bounds (quantiles
-// of all short entries' columns) and padded to multiples of 4 with weight-0 entries into the
-// spare slot S.  The placement only moves rows between lanes; each row's chain order is its
+// group), each group's rows' entries merged by column and padded to multiples of SWALK_STEP with
+// weight-0 entries into the spare slot S.  The placement only moves rows between lanes; each row's chain order is its
 // sorted entries' order.
 static hnm_status swalk_build(hnm_spmm_plan* pl, int d, ShortSched** out) {
   const int lpr = d / 4, ng = SWALK_THREADS / lpr;
@@ -1402,25 +1299,8 @@ static hnm_status swalk_build(hnm_spmm_plan* pl, int d, ShortSched** out) {
     if (i >= ns) break;
     nb += nb >= nwg_full ? nwg_full : 1;  // the last block overflowed S rows
   }
-  constexpr int K = SWALK_WIN > 1 ? SWALK_WIN : 1;
-  // column bounds of the windows: quantiles of every short entry's column
-  std::vector<int32_t> cb;
-  if (K > 1 && total > 0) {
-    std::vector<int64_t> hist((size_t)pl->N + 1, 0);
-    for (int64_t i = 0; i < ns; ++i)
-      for (int64_t q = rp[sr[i]]; q < rp[sr[i] + 1]; ++q) ++hist[hc[q]];
-    int64_t c = 0, acc = 0;
-    for (int k = 1; k < K; ++k) {
-      const int64_t want = total * k / K;
-      while (c < pl->N && acc + hist[c] <= want) acc += hist[c++];
-      cb.push_back((int32_t)c);  // window k starts at column cb[k - 1]
-    }
-  }
-  auto win = [&](int32_t c) {
-    return (int)(std::upper_bound(cb.begin(), cb.end(), c) - cb.begin());
-  };
   std::vector<int32_t> srow((size_t)(nb * S), -1), nslot((size_t)nb, 0);
-  std::vector<int64_t> wcnt((size_t)(nb * ng * K), 0);
+  std::vector<int64_t> wcnt((size_t)(nb * ng), 0);
   std::vector<std::vector<std::vector<int32_t>>> gslot((size_t)nb);  // per block, per group: slots
   parallel_for(nb, [&](int64_t b) {
     const int64_t i0 = bstart[b], n = bstart[b + 1] - i0;
@@ -1440,11 +1320,11 @@ static hnm_status swalk_build(hnm_spmm_plan* pl, int d, ShortSched** out) {
       gslot[b][g].push_back(s);
       gl[g] += cum[i0 + s + 1] - cum[i0 + s];
       const int32_t r = sr[i0 + s];
-      for (int64_t q = rp[r]; q < rp[r + 1]; ++q) ++wcnt[(b * ng + g) * K + win(hc[q])];
+      wcnt[b * ng + g] += rp[r + 1] - rp[r];
     }
   });
-  std::vector<int64_t> gptr((size_t)(nb * ng * K + 1), 0);
-  for (int64_t i = 0; i < nb * ng * K; ++i)
+  std::vector<int64_t> gptr((size_t)(nb * ng + 1), 0);
+  for (int64_t i = 0; i < nb * ng; ++i)
     gptr[i + 1] = gptr[i] + hnm_cdiv(wcnt[i], SWALK_STEP) * SWALK_STEP;
   const int64_t Tp = gptr.back();
   std::vector<uint32_t> ent((size_t)Tp, (uint32_t)S);
@@ -1463,18 +1343,15 @@ static hnm_status swalk_build(hnm_spmm_plan* pl, int d, ShortSched** out) {
       }
       std::stable_sort(Lst.begin(), Lst.end(),
                        [](const auto& x, const auto& y) { return (x.first >> 10) < (y.first >> 10); });
-      size_t i = 0;
-      for (int k = 0; k < K; ++k) {
-        int64_t o = gptr[(b * ng + g) * K + k];
-        const int64_t e = gptr[(b * ng + g) * K + k + 1];
-        uint32_t pad = (uint32_t)S;
-        for (; i < Lst.size() && win((int32_t)(Lst[i].first >> 10)) == k; ++i) {
-          ent[o] = (uint32_t)Lst[i].first;
-          wt[o++] = Lst[i].second;
-          pad = (uint32_t)((Lst[i].first >> 10) << 10) | (uint32_t)S;  // re-gather a cached row
-        }
-        for (; o < e; ++o) ent[o] = pad;
+      int64_t o = gptr[b * ng + g];
+      const int64_t e = gptr[b * ng + g + 1];
+      uint32_t pad = (uint32_t)S;
+      for (size_t i = 0; i < Lst.size(); ++i) {
+        ent[o] = (uint32_t)Lst[i].first;
+        wt[o++] = Lst[i].second;
+        pad = (uint32_t)((Lst[i].first >> 10) << 10) | (uint32_t)S;  // re-gather a cached row
       }
+      for (; o < e; ++o) ent[o] = pad;
     }
   });
   ShortSched* ws = new ShortSched();
@@ -1547,7 +1424,7 @@ extern "C" hnm_status hnm_spmm_plan_create(hnm_ctx* ctx, int64_t N, const int64_
   for (int64_t r = 0; r < N; ++r) {
     const int64_t s = rp[r], e = rp[r + 1];
     HNM_REQUIRE(e >= s, HNM_EINVAL, "spmm_plan: rowptr decreases at row %lld", (long long)r);
-    if (SPMM_GROUPED && e - s > SPMM_SHORT && e - s <= HEAVY) lrows.push_back((int32_t)r);
+    if (e - s > SPMM_SHORT && e - s <= HEAVY) lrows.push_back((int32_t)r);
     if (e - s <= HEAVY) continue;
     const int32_t hi = (int32_t)hrows.size();
     hrows.push_back((int32_t)r);
@@ -1572,7 +1449,7 @@ extern "C" hnm_status hnm_spmm_plan_create(hnm_ctx* ctx, int64_t N, const int64_
   pl->h_long = new std::vector<int32_t>(lrows);
   pl->mu = new std::mutex();
   // walk rows: every row of more than SPMM_SHORT entries (col << 10 must fit 32 bits)
-  pl->walk = SPMM_WALK && SPMM_GROUPED && N <= (int64_t)1 << 22 && rp[0] == 0 &&
+  pl->walk = N <= (int64_t)1 << 22 && rp[0] == 0 &&
              rp[N] < ((int64_t)1 << 32);
   if (pl->walk) {
     std::vector<int32_t> wr, sr;
@@ -1594,7 +1471,7 @@ extern "C" hnm_status hnm_spmm_plan_create(hnm_ctx* ctx, int64_t N, const int64_
     pl->h_walk_rows = new std::vector<int32_t>(wr);
     pl->h_short_rows = new std::vector<int32_t>(sr);
     pl->h_rowptr = new std::vector<int64_t>(std::move(rp));
-    pl->swalk = SPMM_SWALK && !sr.empty();
+    pl->swalk = !sr.empty();
   }
   if (pl->n_long > 0) {
     if (hipMalloc((void**)&pl->long_rows, pl->n_long * 4) != hipSuccess) {
@@ -1687,8 +1564,6 @@ static hnm_status spmm_launch(hnm_ctx* ctx, const hnm_spmm_plan* pl, int64_t N,
       partial = (float*)w;
     }
     if (timed) hnm_timer_begin(ctx, HNM_TIME_SPMM);
-    const bool fork = any && SPMM_WALK_MODE == 0;
-    hipStream_t wst = fork ? ctx->side : ctx->stream;
     auto short_rows = [&]() -> hnm_status {
       if (r1 <= r0) return HNM_OK;
       if (ss) {
@@ -1713,25 +1588,18 @@ static hnm_status spmm_launch(hnm_ctx* ctx, const hnm_spmm_plan* pl, int64_t N,
       HNM_LAUNCH_CHECK();
       return HNM_OK;
     };
-    if (SPMM_WALK_MODE == 2 && (s = short_rows())) return s;
-    if (fork) {
-      HNM_HIP_CHECK(hipEventRecord(ctx->side_in, ctx->stream));
-      HNM_HIP_CHECK(hipStreamWaitEvent(ctx->side, ctx->side_in, 0));
-    }
+    if ((s = short_rows())) return s;
     if (any) {
       hipLaunchKernelGGL(spmm_walk_kernel<LPR>, dim3((unsigned)ws->nwg), dim3(WALK_THREADS), 0,
-                         wst, ws->gptr, ws->ent, ws->wt, ws->slot_out, ws->nslot, ws->maxloc,
+                         ctx->stream, ws->gptr, ws->ent, ws->wt, ws->slot_out, ws->nslot, ws->maxloc,
                          X, d, partial, ep, r0, r1);
       HNM_LAUNCH_CHECK();
       if (ws->n_split > 0) {
         hipLaunchKernelGGL(spmm_walk_finish_kernel, dim3((unsigned)ws->n_split), dim3(256), 0,
-                           wst, ws->split_rows, ws->split_ptr, partial, X, d, ep, r0, r1);
+                           ctx->stream, ws->split_rows, ws->split_ptr, partial, X, d, ep, r0, r1);
         HNM_LAUNCH_CHECK();
       }
     }
-    if (fork) HNM_HIP_CHECK(hipEventRecord(ctx->side_out, ctx->side));
-    if (SPMM_WALK_MODE != 2 && (s = short_rows())) return s;
-    if (fork) HNM_HIP_CHECK(hipStreamWaitEvent(ctx->stream, ctx->side_out, 0));
     if (timed) hnm_timer_end(ctx, HNM_TIME_SPMM);
     return HNM_OK;
   }
@@ -1751,12 +1619,9 @@ static hnm_status spmm_launch(hnm_ctx* ctx, const hnm_spmm_plan* pl, int64_t N,
       hnm_status s = hnm_workspace(ctx, (size_t)(sg1 - sg0) * d * 4, &w);
       if (s) return s;
       float* partial = (float*)w;
-      hipStream_t hs = ctx->stream;
-      if (SPMM_SIDE_STREAM) {
-        HNM_HIP_CHECK(hipEventRecord(ctx->side_in, ctx->stream));
-        HNM_HIP_CHECK(hipStreamWaitEvent(ctx->side, ctx->side_in, 0));
-        hs = ctx->side;
-      }
+      HNM_HIP_CHECK(hipEventRecord(ctx->side_in, ctx->stream));
+      HNM_HIP_CHECK(hipStreamWaitEvent(ctx->side, ctx->side_in, 0));
+      const hipStream_t hs = ctx->side;
       hipLaunchKernelGGL(spmm_segment_kernel<LPR>, dim3((unsigned)hnm_cdiv(sg1 - sg0, 4)),
                          dim3(256), 0, hs, sg0, sg1, pl->seg_start, pl->seg_end, col, val,
                          X, d, partial);
@@ -1764,14 +1629,12 @@ static hnm_status spmm_launch(hnm_ctx* ctx, const hnm_spmm_plan* pl, int64_t N,
       hipLaunchKernelGGL(spmm_finish_kernel, dim3((unsigned)(h1 - h0)), dim3(256), 0, hs,
                          h0, pl->heavy_rows, pl->seg_ptr, sg0, partial, X, d, ep);
       HNM_LAUNCH_CHECK();
-      if (SPMM_SIDE_STREAM) {
-        HNM_HIP_CHECK(hipEventRecord(ctx->side_out, ctx->side));
-        forked = true;
-      }
+      HNM_HIP_CHECK(hipEventRecord(ctx->side_out, ctx->side));
+      forked = true;
     }
   }
   if (r1 > r0) {
-    if (SPMM_GROUPED && pl) {
+    if (pl) {
       // long rows inside [r0, r1) (ascending list) + every short row of the range
       const std::vector<int32_t>& lv = *pl->h_long;
       const int64_t l0 = std::lower_bound(lv.begin(), lv.end(), (int32_t)std::min<int64_t>(r0, INT32_MAX)) - lv.begin();
@@ -1837,7 +1700,7 @@ template <int LPR>
 static hnm_status combine_launch(hnm_ctx* ctx, const int64_t* rows, int64_t n, int64_t N,
                                  const int64_t* rowptr, const int32_t* col, const float* val,
                                  int d, const CombineLayers& cl, const CombineOrder& co, float* out) {
-  const int64_t rows_per_block = SPMM_GROUPED && co.mode != 0 ? 4 * (64 / LPR) : 4;
+  const int64_t rows_per_block = co.mode != 0 ? 4 * (64 / LPR) : 4;
   hipLaunchKernelGGL(spmm_rows_combine_kernel<LPR>, dim3((unsigned)hnm_cdiv(n, rows_per_block)),
                      dim3(256), 0,
                      ctx->stream, rows, n, N, rowptr, col, val, d, cl, co, out, ctx->err_dev);

@@ -28,9 +28,7 @@ hnm_status hnm_topk_merge_i32(hnm_ctx* ctx, const float* cv, const int32_t* ci, 
                               float* ov, int64_t* oi);
 
 // ------------------------------------------------------------------ 32-user kernel
-// ABL: ablation bits for tools/ncf_ablation.hip only (0 in the library): 1 = no top-K,
-// 2 = no ReLU.w epilogue, 4 = no GMF chain, 8 = no tile staging, 16 = no P reads.
-template <bool DENSE, int ABL = 0>
+template <bool DENSE>
 __global__ __launch_bounds__(256, 2) void ncf32_kernel(
     const float* __restrict__ Pu,   // [B, 64]  pair-permuted  W1u m_u + b1
     const float* __restrict__ WGu,  // [B, 64]  pair-permuted  wp_gmf * g_u
@@ -127,10 +125,10 @@ __global__ __launch_bounds__(256, 2) void ncf32_kernel(
   const int64_t ntiles = part_end > part_start ? hnm_cdiv(part_end - part_start, TILE) : 0;
   for (int64_t t = 0; t < ntiles; ++t) {
     const int64_t base = part_start + t * TILE;
-    if (!(ABL & 32)) __syncthreads();  // every wave is done with the previous tile
+    __syncthreads();  // every wave is done with the previous tile
     // stage Q (already pair-permuted) and G (pair-permuted here) for items base..base+31
 #pragma unroll
-    for (int q = 0; q < ((ABL & 8) ? 0 : 2); ++q) {
+    for (int q = 0; q < 2; ++q) {
       const int f = tid + 256 * q;
       const int row = f >> 4, c = f & 15;
       const int64_t item = base + row;
@@ -142,11 +140,11 @@ __global__ __launch_bounds__(256, 2) void ncf32_kernel(
       *reinterpret_cast<float2*>(&gs[row * RS + 2 * c]) = make_float2(g.x, g.z);
       *reinterpret_cast<float2*>(&gs[row * RS + KS + 2 * c]) = make_float2(g.y, g.w);
     }
-    if (!(ABL & 32)) __syncthreads();
+    __syncthreads();
     if (nu == 0) continue;
 
     // GMF of the wave's 32 users x 32 items: one MFMA chain, parked in LDS
-    if (!(ABL & 4)) {
+    {
       f32x16 gacc = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
       const float* grow = &gs[j * RS + h * KS];
 #pragma unroll
@@ -204,7 +202,7 @@ __global__ __launch_bounds__(256, 2) void ncf32_kernel(
 #pragma unroll
       for (int s4 = 0; s4 < KS / 4; ++s4) {
         float4 na = pa, nb = pb;
-        if (s4 + 1 < KS / 4 && !(ABL & 16)) {
+        if (s4 + 1 < KS / 4) {
           na = *reinterpret_cast<const float4*>(prA + 4 * (s4 + 1));
           nb = *reinterpret_cast<const float4*>(prB + 4 * (s4 + 1));
         }
@@ -224,15 +222,10 @@ __global__ __launch_bounds__(256, 2) void ncf32_kernel(
         const int u = side ? uB : uA;
         if (side && uB == uA) break;
         const f32x16& acc = side ? accB : accA;
-        float mlp = 0.f;
-        if (ABL & 2) {
-          mlp = acc[0] + acc[15];
-        } else {
-          float m4[4] = {0.f, 0.f, 0.f, 0.f};  // 4 short chains instead of one 16-deep
+        float m4[4] = {0.f, 0.f, 0.f, 0.f};  // 4 short chains instead of one 16-deep
 #pragma unroll
-          for (int r = 0; r < 16; ++r) m4[r & 3] = fmaf(fmaxf(acc[r], 0.f), wmr[r], m4[r & 3]);
-          mlp = (m4[0] + m4[1]) + (m4[2] + m4[3]);
-        }
+        for (int r = 0; r < 16; ++r) m4[r & 3] = fmaf(fmaxf(acc[r], 0.f), wmr[r], m4[r & 3]);
+        const float mlp = (m4[0] + m4[1]) + (m4[2] + m4[3]);
         const float gm = side ? gmB : gmA;
         const float tot = hnm_sum_halves(mlp + (h == 0 ? gm : 0.f));
         float score = tot + bpv;
@@ -240,9 +233,7 @@ __global__ __launch_bounds__(256, 2) void ncf32_kernel(
           const unsigned bits = (unsigned)hnm_readlane_i((int)mbits, u);
           if ((bits >> j) & 1u) score = -__builtin_inff();
         }
-        if (ABL & 1) {
-          tvv += score;
-        } else if (DENSE) {
+        if (DENSE) {
           if (ivalid) dense[(u0 + u) * ldo + item] = score;
         } else {
           const float thv = hnm_readlane_f(tvv, u);
@@ -265,8 +256,7 @@ __global__ __launch_bounds__(256, 2) void ncf32_kernel(
       }
     }
   }
-  if (ABL & 1) cand_v[blockIdx.x * 256 + tid] = tvv;
-  if (!DENSE && !(ABL & 1)) {
+  if (!DENSE) {
     for (int e = lane; e < nu * K; e += 64) {
       const int u = e / K, s = e % K;
       const int64_t o = ((u0 + u) * NP + p) * K + s;

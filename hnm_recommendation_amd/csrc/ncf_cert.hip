@@ -66,10 +66,9 @@ constexpr int64_t CERT_GROUP_MIN = 48;    // items per champion group, at least
 constexpr int CERT_STRIDE = 8;
 constexpr int64_t CERT_GATE_GAIN = 250;
 constexpr int CERT_GATE_CHUNKS = 64;  // workgroups per proxy row of the count kernel
-#ifndef HNM_SCAN_OCC
+// scan workgroups per CU (LDS 51.7 KB each; the scan's 168 VGPRs fit three waves per SIMD)
 #define HNM_SCAN_OCC 3
-#endif
-constexpr int CERT_WG_PER_CU = HNM_SCAN_OCC;  // scan workgroups per CU (LDS 51.7 KB each)
+constexpr int CERT_WG_PER_CU = HNM_SCAN_OCC;
 
 enum { CM_P, CM_Q, CM_WG, CM_G, CM_B, CM_D, CM_N };
 
@@ -1103,24 +1102,14 @@ __global__ __launch_bounds__(256) void cert_gate_count_kernel(
 // (score desc, item asc) top-K.  Candidates sit in NP per-partition segments; a row with a
 // flagged bound, an overflowing segment or fewer than K candidates is queued for the
 // fallback.
-// k steps per LDS operand round trip in the layer-2 chain (round 4, rescore kernel under
-// rocprofv3: 1 step 67.3 us, 2 steps 65.8-66.3, 4 steps 64.8 -- the operand waits are not what
-// bounds it; the candidates' G / Q row gathers are)
-#ifndef RESCORE_STEP
-#define RESCORE_STEP 4
-#endif
-// persistent re-scoring workgroups per CU looping over rows (0 = one workgroup per 4 rows).
-// Round 4, per-rank step of the sharded NCF (tools/rank_shape_probe.py, the all_reduced
-// bounds): W = 1 2.172 -> 2.147 ms, W = 8 (32,768 rows of ~1/8 the candidates) 2.381 -> 2.284
-// ms at 3 per CU (6 per CU: 2.151 / 2.315) -- the W2 fragments are staged into LDS once per
-// workgroup instead of once per 4 rows
-#ifndef RESCORE_PERSIST
+// Four k steps' LDS operands per round trip in the layer-2 chain (round 4, under rocprofv3:
+// 1 step 67.3 us, 2 steps 65.8-66.3, 4 steps 64.8 -- the operand waits are not what bounds it;
+// the candidates' G / Q row gathers are).  RESCORE_PERSIST persistent workgroups per CU loop
+// over rows (round 4, per-rank step of the sharded NCF, tools/rank_shape_probe.py: W = 1 2.172
+// -> 2.147 ms, W = 8 (32,768 rows of ~1/8 the candidates) 2.381 -> 2.284 ms at 3 per CU, 6 per
+// CU 2.151 / 2.315, against one workgroup per 4 rows): the W2 fragments are staged into LDS once
+// per workgroup instead of once per 4 rows.
 #define RESCORE_PERSIST 3
-#endif
-#ifndef RESCORE_ABL  // timing ablations (tools only; wrong results): 1 no top-K, 2 fixed items,
-                     // 4 at most 64 candidates a row
-#define RESCORE_ABL 0
-#endif
 __global__ __launch_bounds__(256, 3) void ncf_rescore_kernel(
     NcfTabs t, int mf, const float* __restrict__ W2, int h1, int h2, const float* __restrict__ b2,
     const float* __restrict__ wm, const float* __restrict__ bp, int64_t B,
@@ -1146,18 +1135,12 @@ __global__ __launch_bounds__(256, 3) void ncf_rescore_kernel(
     const int s = e >> 6, jj = e & 31, k = 2 * s + ((e >> 5) & 1);
     w2l[e] = (jj < h2 && k < h1) ? W2[jj * h1 + k] : 0.f;
   }
-#if RESCORE_PERSIST
   // persistent: the workgroup's shared operands loaded once, then each wave takes rows
   // b, b + 4 * gridDim.x, ... (its per-row LDS arrays are its own: no workgroup barrier inside)
   __syncthreads();
   for (int64_t b = (int64_t)blockIdx.x * 4 + wave; b < B; b += (int64_t)gridDim.x * 4) {
   const bool live = true;
   int c = 0;
-#else
-  const int64_t b = (int64_t)blockIdx.x * 4 + wave;
-  const bool live = b < B;
-  int c = 0;
-#endif
   if (live) {
     wgs[wave][lane] = t.WGu[b * 64 + lane];  // pair-permuted wp*g_u
     pl[wave][lane] = t.Pu[b * 64 + lane];
@@ -1174,19 +1157,10 @@ __global__ __launch_bounds__(256, 3) void ncf_rescore_kernel(
     if (lane == 0) pref[wave][0] = 0;
     if (lane < NP) pref[wave][lane + 1] = incl;
   }
-#if RESCORE_PERSIST
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // this wave's LDS writes, then its reads
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#else
-  __syncthreads();
-  if (!live) return;
-#endif
-#if RESCORE_ABL & 4
-  const int n = std::min(hnm_readlane_i(incl, 63), 64);
-#else
   const int n = hnm_readlane_i(incl, 63);
-#endif
   const bool over = __ballot(c > capp) != 0;
   // fewer than K candidates: the row's bound came from another item shard (short_ok: the
   // merge across shards completes the list) or the threshold is unusable -> fallback
@@ -1198,11 +1172,7 @@ __global__ __launch_bounds__(256, 3) void ncf_rescore_kernel(
         if (b == 0) atomicAdd(&stats[0], (unsigned long long)B);
       }
     }
-#if RESCORE_PERSIST
     continue;
-#else
-    return;
-#endif
   }
   if (stats && lane == 0) {
     atomicAdd(&stats[1], (unsigned long long)n);
@@ -1211,8 +1181,6 @@ __global__ __launch_bounds__(256, 3) void ncf_rescore_kernel(
   const float bpv = bp[0];
   WaveTopK<1> L;
   L.init();
-  float abl_sink = 0.f;
-  (void)abl_sink;
   const int32_t* rowbuf = buf + b * (int64_t)NP * capp;
   // candidate g's item (0 past the row's n): segment = last p with pref[p] <= g
   auto cand = [&](int g) {
@@ -1236,9 +1204,6 @@ __global__ __launch_bounds__(256, 3) void ncf_rescore_kernel(
     const bool ok = g < n;
     int item = item_next;
     item_next = cand(g + 32);
-#if RESCORE_ABL & 2
-    item = j;
-#endif
     // GMF: fma chain in the f32 MFMA's order (k = 2s, then 2s + 1) over all 64 k (zero
     // beyond mf, as the fp32 kernel's padded operands); loads in two batches of 8 float4
     // issued together (a runtime-bounded loop would wait on each load)
@@ -1279,19 +1244,6 @@ __global__ __launch_bounds__(256, 3) void ncf_rescore_kernel(
       wmr[4 * r4] = ww.x; wmr[4 * r4 + 1] = ww.y; wmr[4 * r4 + 2] = ww.z; wmr[4 * r4 + 3] = ww.w;
     }
     typedef __attribute__((address_space(3))) const float* lds_ptr;
-#if RESCORE_STEP == 1
-#pragma unroll
-    for (int s = 0; s < KS; ++s) {
-      // both reads issued right before their MFMA (hoisted by the compiler, they would hold
-      // 64 VGPRs again and spill); operands are LDS byte offsets (address-space-3 pointers)
-      float w2v, pv;
-      asm volatile("ds_read_b32 %0, %2\n\tds_read_b32 %1, %3\n\ts_waitcnt lgkmcnt(0)"
-                   : "=&v"(w2v), "=&v"(pv)
-                   : "v"((unsigned)(uintptr_t)(lds_ptr)&w2l[s * 64 + lane]),
-                     "v"((unsigned)(uintptr_t)(lds_ptr)&pl[wave][h * KS + s]));
-      acc = mfma32x32x2(w2v, fmaxf(pv + q[s], 0.f), acc);
-    }
-#elif RESCORE_STEP == 4
     // four k steps' operands per LDS round trip
 #pragma unroll
     for (int s = 0; s < KS; s += 4) {
@@ -1312,41 +1264,16 @@ __global__ __launch_bounds__(256, 3) void ncf_rescore_kernel(
 #pragma unroll
       for (int e = 0; e < 4; ++e) acc = mfma32x32x2(w[e], fmaxf(pv[e] + q[s + e], 0.f), acc);
     }
-#else
-    // two k steps' operands per LDS round trip (one wait per two MFMAs)
-#pragma unroll
-    for (int s = 0; s < KS; s += 2) {
-      float w0, w1, p0, p1;
-      asm volatile("ds_read_b32 %0, %4\n\tds_read_b32 %1, %5\n\tds_read_b32 %2, %6\n\t"
-                   "ds_read_b32 %3, %7\n\ts_waitcnt lgkmcnt(0)"
-                   : "=&v"(w0), "=&v"(w1), "=&v"(p0), "=&v"(p1)
-                   : "v"((unsigned)(uintptr_t)(lds_ptr)&w2l[s * 64 + lane]),
-                     "v"((unsigned)(uintptr_t)(lds_ptr)&w2l[(s + 1) * 64 + lane]),
-                     "v"((unsigned)(uintptr_t)(lds_ptr)&pl[wave][h * KS + s]),
-                     "v"((unsigned)(uintptr_t)(lds_ptr)&pl[wave][h * KS + s + 1]));
-      acc = mfma32x32x2(w0, fmaxf(p0 + q[s], 0.f), acc);
-      acc = mfma32x32x2(w1, fmaxf(p1 + q[s + 1], 0.f), acc);
-    }
-#endif
     float m4[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int r = 0; r < 16; ++r) m4[r & 3] = fmaf(fmaxf(acc[r], 0.f), wmr[r], m4[r & 3]);
     const float mlp = (m4[0] + m4[1]) + (m4[2] + m4[3]);
     const float tot = hnm_sum_halves(mlp + (h == 0 ? gm : 0.f));
     const float score = tot + bpv;
-#if RESCORE_ABL & 1
-    abl_sink = fmaxf(abl_sink, score);
-#else
     L.offer(score, item, ok && h == 0, K);
-#endif
   }
-#if RESCORE_ABL & 1
-  if (abl_sink == 1234.5f) oi[b * K] = 0;
-#endif
   L.store(ov ? ov + b * K : nullptr, oi + b * K, K);
-#if RESCORE_PERSIST
   }
-#endif
 }
 
 // scaled -> real units, for the diagnostics entry point
@@ -1639,8 +1566,7 @@ hnm_status ncf_cert_finish(hnm_ctx* ctx, const hnm_ncf_weights* w, const NcfTabs
   hnm_timer_end(ctx, HNM_TIME_SCORE);
   HNM_LAUNCH_CHECK();
   // exact fp32 re-scoring + top-K of the candidates; unusable rows -> queue
-  const int64_t rgrid = RESCORE_PERSIST ? std::min<int64_t>(hnm_cdiv(B, 4), (int64_t)RESCORE_PERSIST * ctx->num_cus)
-                                        : hnm_cdiv(B, 4);
+  const int64_t rgrid = std::min<int64_t>(hnm_cdiv(B, 4), (int64_t)RESCORE_PERSIST * ctx->num_cus);
   hipLaunchKernelGGL(ncf_rescore_kernel, dim3((unsigned)rgrid), dim3(256), 0, ctx->stream,
                      t, w->mf, w->w2, w->h1, w->h2, w->b2, w->wp + w->mf, w->bp, B, x.flag, x.cnt,
                      x.buf, sh.part.np, sh.capp, K, short_ok, ov, oi, x.ovf_rows, x.ovf_cnt,

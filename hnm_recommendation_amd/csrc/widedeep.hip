@@ -464,12 +464,10 @@ typedef _Float16 wh8 __attribute__((ext_vector_type(8)));
 // (WD_BOUND_MFMA below) and packed operand formation: 232 ms (1,145 candidates a row; their
 // exact fp32 re-scoring ~14 ms) vs 2 passes 262-267 ms (393) -- W&D 15.1 k -> 16.5 k users/s
 // (profiles/r3g_widedeep_ab.txt).
-#ifndef WD_SPLIT_PASSES
-#define WD_SPLIT_PASSES 1  // layer 2
-#endif
-#ifndef WD_SPLIT_PASSES3
-#define WD_SPLIT_PASSES3 1  // layer 3: W_hi x_hi only (both residuals bounded)
-#endif
+// The product (round 5: the alternatives above and below are gone from the source; git
+// history and DESIGN.md §4 keep them): layer 2 and layer 3 one W_hi x_hi pass each, the
+// layer-2 bound terms on the matrix pipe, the k loop in register-set pairs with the weight
+// fragments two steps ahead, the accumulators pinned by asm.
 // One-pass layer 2 (WD_SPLIT_PASSES = 1) with the bound's layer-2 terms on the matrix pipe: per k
 // step and user two v_mfma_f32_16x16x32_f16 whose A rows 0 / 1 carry sb v1 (B = x_hi) and
 // sb (v1 + 1.001 v1o / g1) (B = |x_lo|) for the items c / c + 16 of the 32x32 operand layout,
@@ -477,18 +475,8 @@ typedef _Float16 wh8 __attribute__((ext_vector_type(8)));
 //   g1 v1.x + 1.001 v1o.|x - x_hi|  <=  g1 (v1.x_hi + (v1 + 1.001 v1o / g1).|x_lo|)
 // (x = x_hi + x_lo exactly, |x_lo| rounded to f16 costs 2^-10 relative, in the A rows).  This
 // replaces the 16 VALU fmas per user and k step that bound the VALU-bound one-pass kernel.
-#ifndef WD_BOUND_MFMA
-#define WD_BOUND_MFMA 1
-#endif
-#ifndef WD_LO_EXACT  // |x_lo| := 0 where z < 0 (exact) instead of |f16(z - f16(z))|
-#define WD_LO_EXACT 0
-#endif
-#ifndef WD_PAIRS  // one-pass k loop in register-set pairs (0: one step per iteration + copies)
-#define WD_PAIRS 1
-#endif
-#ifndef WD_PREFETCH  // one-pass k loop: weight fragments this many k steps ahead (2 or 3)
-#define WD_PREFETCH 2
-#endif
+// (Measured and dropped, round 3: |x_lo| := 0 where z < 0 -- 789 instead of 1,145 candidates
+// a row but a 5.7 ms slower scan, the same step; weight fragments three steps ahead.)
 
 // one 16-B fragment per lane from a buffer: a uniform byte offset (SGPR) + lane * 16, so a
 // fragment costs one scalar add instead of a 64-bit per-lane address (8 of those held across
@@ -518,15 +506,7 @@ __device__ __forceinline__ f32x16 wd_mfma16(wh8 a, wh8 b, f32x16 c) {
 // B operand a VALU instruction may just have written; an accumulate chain (C = the previous
 // MFMA's D, same shape) needs none; the results -> any other reader: the s_nop fences after
 // each loop.
-#ifndef WD_ASM_ACC
-#define WD_ASM_ACC 1
-#endif
-#ifndef WD_ASM_L3  // layer 3's MFMAs as asm (0: builtins)
-#define WD_ASM_L3 1
-#endif
-#ifndef WD_ASM_BOUND  // (0: the bound MFMAs as builtins: measured 128 accumulator moves a step)
-#define WD_ASM_BOUND 1
-#endif
+// (As builtins the bound MFMAs cost 128 accumulator moves a step, measured.)
 template <bool NOP>
 __device__ __forceinline__ void wd_mfma16x_accv(f32x4& c, const wh8& a, const wh8& b) {
   if (NOP)
@@ -578,20 +558,7 @@ __device__ __forceinline__ void wd_split_relu2(wf2 z, wh2& hi, unsigned& alo) {
   asm("v_fma_mixlo_f16 %0, %1, -1.0, %2 op_sel_hi:[1,0,0]\n\t"
       "v_fma_mixhi_f16 %0, %1, -1.0, %3 op_sel:[1,0,0] op_sel_hi:[1,0,0]"
       : "=&v"(d) : "v"(hub), "v"(z.x), "v"(z.y));
-  if (WD_LO_EXACT == 2) {
-    // |x_lo| of x = relu(z) exactly, one packed min: z < 0 has x_hi = 0 and x_lo = 0; z >= 0
-    // has |f16(z - x_hi)| <= x_hi (half an ulp of x_hi when it is normal, 0 or 2^-24 <= x_hi
-    // when subnormal, and x_lo = 0 when x_hi = 0), so min(|d|, x_hi) is |x_lo| in every case
-    alo = __builtin_bit_cast(unsigned, __builtin_elementwise_min(
-                                           __builtin_bit_cast(wh2, d & 0x7fff7fffu), hi));
-  } else if (WD_LO_EXACT) {
-    // halves whose z < 0 (sign bit of the unclamped hi) have x = relu(z) = 0, hence x_lo = 0:
-    // clear them together with the sign bits (|x_lo| exact instead of over-estimated)
-    const unsigned neg = ((hub >> 15) & 0x00010001u) * 0xffffu;
-    alo = d & ~(neg | 0x80008000u);
-  } else {
-    alo = d & 0x7fff7fffu;
-  }
+  alo = d & 0x7fff7fffu;
 }
 
 // Split 8 fp32 values into f16 hi / lo halves: hi = f16(x), lo = f16(x - hi) (RNE; the
@@ -772,8 +739,8 @@ __global__ __launch_bounds__(256) void wdc_params_kernel(hnm_widedeep_weights w,
   for (float sc : {s1, sw2, s2, sw3}) bad |= !(sc >= 1e-25f && sc <= 1e25f);
   // b2' in x2 units
   for (int jx = tid; jx < n2; jx += 256) b2s[jx] = p.b2p[jx] * s2;
-  if ((WD_SPLIT_PASSES < 3 || WD_SPLIT_PASSES3 < 3) && !bad) {
-    // the dropped W_lo x_hi passes (see WD_SPLIT_PASSES): v1 += (|R2|^T v2) / g1 and, with a
+  if (!bad) {
+    // the dropped W_lo x_hi passes: v1 += (|R2|^T v2) / g1 and, with a
     // third layer, v2 += (|R3|^T v3) / g2, R = W' - f16(W' sw) / sw exactly as wdc_convert_kernel
     // rounds it; 1 + 2^-10 covers |x_hi| <= (1 + 2^-11)|x| and the fp32 sums.  Each thread
     // updates the entries it wrote above (same t / jx mapping).
@@ -784,8 +751,8 @@ __global__ __launch_bounds__(256) void wdc_params_kernel(hnm_widedeep_weights w,
     // one pass on layer 3 also drops W_hi x_lo: |x_lo| <= 2^-11 |x| (RNE), i.e. v2 += 2^-11 v2 /
     // g2; a one-pass layer 2 bounds its x_lo term per pair instead (scan: v1o . |x - x_hi|)
     const float xl1 = 0.f;
-    const float xl3 = WD_SPLIT_PASSES3 == 1 ? 4.8828125e-4f : 0.f;
-    for (int t = tid; t < K1P && WD_SPLIT_PASSES < 3; t += 256) {
+    const float xl3 = 4.8828125e-4f;
+    for (int t = tid; t < K1P; t += 256) {
       const int k = wd_korig(t, K1P);
       if (k >= l1) continue;
       float r = 0.f;
@@ -796,7 +763,7 @@ __global__ __launch_bounds__(256) void wdc_params_kernel(hnm_widedeep_weights w,
       }
       v1[t] = v1[t] * (1.f + fr * xl1 / g1c) + fr * (r / sw2) / g1c;
     }
-    if (p.OB > 0 && WD_SPLIT_PASSES3 < 3) {
+    if (p.OB > 0) {
       for (int jx = tid; jx < l2; jx += 256) {
         float r = 0.f;
         for (int m = 0; m < l3; ++m) {
@@ -808,11 +775,11 @@ __global__ __launch_bounds__(256) void wdc_params_kernel(hnm_widedeep_weights w,
       }
     }
   }
-  // scale of the bound A rows (WD_BOUND_MFMA): max over k of v1 + (1.001 / g1) v1o, the larger row
+  // scale of the bound A rows: max over k of v1 + (1.001 / g1) v1o, the larger row
   __shared__ float ared[4];
   __syncthreads();  // every thread's v1 / v1o entries are written
   float amax = 0.f;
-  if (WD_SPLIT_PASSES == 1 && WD_BOUND_MFMA) {
+  {
     const float g1c = (2.125f * K1P + 22.f) * 5.9604645e-08f;
     for (int t = tid; t < K1P; t += 256) amax = wd_nmax(amax, v1[t] + (1.0009765625f / g1c) * v1o[t]);
   }
@@ -973,12 +940,8 @@ struct WdScanArgs {
 
 #define WDC_THRESH 0
 #define WDC_DEBUG 1
-#ifndef WDC_VPM
 #define WDC_VPM 4  // VALU instructions scheduled per MFMA in the k loop's interleave
-#endif
-#ifndef WDC_G2
-#define WDC_G2 8  // layer-2 row blocks per pass over k (the x operands are formed once per pass)
-#endif
+#define WDC_G2 8   // layer-2 row blocks per pass over k (the x operands are formed once per pass)
 #ifndef WD_STAMPS  // diagnostic builds only: per-phase s_memtime cycle sums (tools/wd_stamps.py)
 #define WD_STAMPS 0
 #endif
@@ -992,40 +955,33 @@ extern "C" int hnm_debug_wd_stamps_reset() {
   return (int)hipMemcpyToSymbol(HIP_SYMBOL(wd_stamp_acc), z, sizeof(z));
 }
 #endif
-#ifndef WDC_INTERLEAVE
-#define WDC_INTERLEAVE 1  // sched_group_barrier interleave of the k loop (0: compiler order)
-#endif
 
 // Block = 4 waves x UPW users each (rows blockIdx.x * 4 UPW + wave * UPW + v) x item
 // partition blockIdx.y; the Q tile (32 items, fp32) is shared through LDS.  Per tile a wave
-// runs layer 2 as WD_SPLIT_PASSES x RB2 x K1P/16 f16 MFMAs per user (G2 row blocks per pass
+// runs layer 2 as RB2 x K1P/16 f16 MFMAs per user (one W_hi x_hi pass; G2 row blocks per pass
 // over k, the next layer fed from the accumulators as each pass completes), layer 3 as
-// WD_SPLIT_PASSES3 x OB x 2 RB2, then the bound.  UPW = 2: every weight fragment loaded from
+// OB x 2 RB2, then the bound.  UPW = 2: every weight fragment loaded from
 // L2 feeds two users' MFMAs -- the fragment stream is what bounds the one-user variant
 // (tools/wd_ablation.sh: no weight loads = -19% time).  Round 3 product: G2 = RB2 = 8, one
 // pass over k (the x operands, most of the k loop's vector work, formed once per tile instead
 // of once per pass: 217 -> 160-164 ms), layer 2's 256 accumulators in the AGPR file, layer 3
 // after all of layer 2 (ASMACC below).
-template <int RB2, int OB, int G2, int MODE, int UPW, int ABL = 0>
+template <int RB2, int OB, int G2, int MODE, int UPW>
 __global__ __launch_bounds__(256, UPW == 1 ? 2 : 1) void wdc_scan_kernel(WdScanArgs A) {
   constexpr int NOB = OB > 0 ? OB : 1;
   constexpr int NL = OB > 0 ? OB : RB2;
   constexpr int NU = 4 * UPW;  // users per block
-  constexpr bool BM = WD_SPLIT_PASSES == 1 && WD_BOUND_MFMA;
-  constexpr bool ASMACC = BM && WD_ASM_ACC && G2 == RB2 && WD_PAIRS;
+  constexpr bool ASMACC = G2 == RB2;  // accumulators pinned by asm (the 8 x 4 product shape)
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int K1P = A.K1P, KB = K1P / 16, QRS = K1P + 4;
   float* qs = smem;               // [32][QRS]
   float* ps = qs + 32 * QRS;      // [NU][K1P]
-  float* v1s = ps + NU * K1P;     // [K1P]
-  float* b2l = v1s + K1P;         // [RB2*32]
+  float* b2l = ps + NU * K1P;     // [RB2*32]
   float* v2l = b2l + RB2 * 32;    // [RB2*32]
   float* b3l = v2l + RB2 * 32;    // [NOB*32]
   float* wdl = b3l + NOB * 32;    // [NL*32]
-  float* v0s = wdl + NL * 32;     // [K1P] zeros (the bound row of passes > 0)
-  float* v1os = v0s + K1P;        // [K1P] v1o (one-pass layer 2: the per-pair x_lo term)
   // qs / qn (offset qn_off): the Q tile being scored and the next one, filled during its k loop
-  const int qn_off = (int)(v1os + K1P - smem);
+  const int qn_off = (int)(wdl + NL * 32 - smem);
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5, j = lane & 31;
   const __amdgpu_buffer_rsrc_t w2rs =
@@ -1039,13 +995,8 @@ __global__ __launch_bounds__(256, UPW == 1 ? 2 : 1) void wdc_scan_kernel(WdScanA
   const int64_t part_start = (int64_t)p * A.ipp;
   const int64_t part_end = std::min<int64_t>(A.I, part_start + A.ipp);
   // P and Q are staged pre-scaled by s1 (a power of two: relu(s1 p + s1 q) = s1 relu(p + q)
-  // exactly), v1 by 1 / s1, so the k loop forms the f16 operands without a multiply
+  // exactly), so the k loop forms the f16 operands without a multiply
   const float s1 = A.prm->s1, inv_s1 = 1.f / s1;
-  for (int e = tid; e < K1P; e += 256) {
-    v1s[e] = A.v1[e] * inv_s1;
-    v0s[e] = 0.f;
-    v1os[e] = WD_SPLIT_PASSES == 1 ? A.v1o[e] * inv_s1 : 0.f;
-  }
   for (int e = tid; e < NU * K1P / 4; e += 256) {
     const int r = e / (K1P / 4), c = e % (K1P / 4);
     float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -1104,7 +1055,6 @@ __global__ __launch_bounds__(256, UPW == 1 ? 2 : 1) void wdc_scan_kernel(WdScanA
   const int qrow_t = tid >> 3, qcol_t = tid & 7;
   const int qvoff = (qrow_t * K1P + qcol_t) * 4;
   auto qrsrc = [&](int64_t nb) {  // the tile at nb: its rows inside the partition
-    if (ABL & 2) nb = part_start;  // ablation: every tile's copy reads the first (cache-hot) tile
     const int64_t rows = std::max<int64_t>(0, std::min<int64_t>(WD_TILE, part_end - nb));
     const float* src = A.Qi + std::min<int64_t>(nb, part_end - 1) * K1P;
     return __builtin_amdgcn_make_buffer_rsrc((void*)src, 0, (int)(rows * K1P * 4), 0x00020000);
@@ -1134,10 +1084,10 @@ __global__ __launch_bounds__(256, UPW == 1 ? 2 : 1) void wdc_scan_kernel(WdScanA
 
     const float* qrow = smem + cur_off + j * QRS + 8 * h;
     f32x16 acc3[UPW][NOB];
-    float fin[UPW], bx1[UPW], bx2[UPW], bx3[UPW], bxl[UPW];
+    float fin[UPW], bx2[UPW], bx3[UPW];
 #pragma unroll
-    for (int v = 0; v < UPW; ++v) fin[v] = bx1[v] = bx2[v] = bx3[v] = bxl[v] = 0.f;
-    // the bound's layer-2 terms on the matrix pipe (WD_BOUND_MFMA): 16x16 accumulators, rows 0 / 1
+    for (int v = 0; v < UPW; ++v) fin[v] = bx2[v] = bx3[v] = 0.f;
+    // the bound's layer-2 terms on the matrix pipe: 16x16 accumulators, rows 0 / 1
     // of lanes 0-15 = items c / c + 16
     f32x4 accb[UPW];
 #pragma unroll
@@ -1146,7 +1096,7 @@ __global__ __launch_bounds__(256, UPW == 1 ? 2 : 1) void wdc_scan_kernel(WdScanA
     // the x_hi rows, pass 1 the |x_lo| rows (one 16x16x32 MFMA per user and k step each); NG = 1
     // both.  One loop body for every pass: duplicating it for the passes spilled 300+ registers
     constexpr int NG2 = RB2 / G2;
-    static_assert(!BM || NG2 <= 2, "bound MFMA split assumes at most two row-block passes");
+    static_assert(NG2 <= 2, "bound MFMA split assumes at most two row-block passes");
 #pragma unroll 1
     for (int g = 0; g < NG2; ++g) {
       f32x16 acc2[UPW][G2];
@@ -1160,30 +1110,21 @@ __global__ __launch_bounds__(256, UPW == 1 ? 2 : 1) void wdc_scan_kernel(WdScanA
       // SIMD issues ~5 VALU per 32-cycle MFMA gap nearly for free (MI355X_MICROARCH.md,
       // cycle constants), so a step costs its MFMAs instead of VALU + MFMA.  hi weight
       // fragments are prefetched one step ahead, lo fragments at the top of their step (first
-      // used 2 G2 UPW MFMAs later).  v1 . x1 accumulates in pass 0 only: later passes and the
-      // tail step read the zero row v0s, so the loop body stays branch-free for the scheduler.
-      const float* v1p = g == 0 ? v1s : v0s;
-      const float* vop = g == 0 ? v1os : v0s;
+      // used 2 G2 UPW MFMAs later).
       auto frag = [&](int gi, int kk, int hl) {
-        const int q = (ABL & 1) ? gi * 2 : ((g * G2 + gi) * KB + kk) * 2;
+        const int q = ((g * G2 + gi) * KB + kk) * 2;
         return wd_frag(w2rs, lane, (q + hl) * 1024);
       };
-      auto form = [&](int kk, const float* vrow, const float* vorow, wh8* oh, wh8* ol) {
+      // x_hi and |x_lo| of step kk (the layer-2 MFMAs' and the bound MFMAs' B operands), packed
+      auto form = [&](int kk, wh8* oh, wh8* ol) {
         const float4 q0 = *reinterpret_cast<const float4*>(qrow + 16 * kk);
         const float4 q1 = *reinterpret_cast<const float4*>(qrow + 16 * kk + 4);
-        const float4 va = *reinterpret_cast<const float4*>(vrow + 16 * kk + 8 * h);
-        const float4 vb = *reinterpret_cast<const float4*>(vrow + 16 * kk + 8 * h + 4);
-        float4 oa = {}, ob = {};
-        if (WD_SPLIT_PASSES == 1) {
-          oa = *reinterpret_cast<const float4*>(vorow + 16 * kk + 8 * h);
-          ob = *reinterpret_cast<const float4*>(vorow + 16 * kk + 8 * h + 4);
-        }
 #pragma unroll
         for (int v = 0; v < UPW; ++v) {
           const float* prow = ps + (wave * UPW + v) * K1P + 8 * h + 16 * kk;
           const float4 p0 = *reinterpret_cast<const float4*>(prow);
           const float4 p1 = *reinterpret_cast<const float4*>(prow + 4);
-          if constexpr (BM) {  // x_hi and |x_lo| (the bound MFMAs' B operands), packed
+          {
             const wf2 s2v = {s1, s1};
             const wf2 zq[4] = {{q0.x, q0.y}, {q0.z, q0.w}, {q1.x, q1.y}, {q1.z, q1.w}};
             const wf2 zp[4] = {{p0.x, p0.y}, {p0.z, p0.w}, {p1.x, p1.y}, {p1.z, p1.w}};
@@ -1198,99 +1139,10 @@ __global__ __launch_bounds__(256, UPW == 1 ? 2 : 1) void wdc_scan_kernel(WdScanA
               ol[v][2 * e] = lo2[0];
               ol[v][2 * e + 1] = lo2[1];
             }
-            continue;
-          }
-          // x1 * s1 (P pre-scaled, Q scaled here)
-          float x[8] = {fmaxf(fmaf(q0.x, s1, p0.x), 0.f), fmaxf(fmaf(q0.y, s1, p0.y), 0.f),
-                        fmaxf(fmaf(q0.z, s1, p0.z), 0.f), fmaxf(fmaf(q0.w, s1, p0.w), 0.f),
-                        fmaxf(fmaf(q1.x, s1, p1.x), 0.f), fmaxf(fmaf(q1.y, s1, p1.y), 0.f),
-                        fmaxf(fmaf(q1.z, s1, p1.z), 0.f), fmaxf(fmaf(q1.w, s1, p1.w), 0.f)};
-          float bb = bx1[v];
-          bb = fmaf(va.x, x[0], bb); bb = fmaf(va.y, x[1], bb);
-          bb = fmaf(va.z, x[2], bb); bb = fmaf(va.w, x[3], bb);
-          bb = fmaf(vb.x, x[4], bb); bb = fmaf(vb.y, x[5], bb);
-          bb = fmaf(vb.z, x[6], bb); bb = fmaf(vb.w, x[7], bb);
-          bx1[v] = bb;
-          if (WD_SPLIT_PASSES == 1) {
-            // layer 2 runs W_hi x_hi only: its x_lo term, v1o . |x - f32(x_hi)| (exact residual)
-            const float vo[8] = {oa.x, oa.y, oa.z, oa.w, ob.x, ob.y, ob.z, ob.w};
-            float bl = bxl[v];
-#pragma unroll
-            for (int e = 0; e < 8; ++e) {
-              const _Float16 hv = (_Float16)x[e];
-              oh[v][e] = hv;
-              bl = fmaf(vo[e], fabsf(x[e] - (float)hv), bl);
-            }
-            bxl[v] = bl;
-          } else {
-            wd_split8(x, oh[v], ol[v]);
           }
         }
       };
-      // one k step: MFMAs on the (ah, xh, xl) set while the other set is loaded / formed for
-      // step kb + 1
-      auto step = [&](int kb, const wfr (&ah)[G2], wfr (&an)[G2], const wh8 (&xh)[UPW],
-                      const wh8 (&xl)[UPW], wh8 (&nxh)[UPW], wh8 (&nxl)[UPW], const wfr (&bc)[2],
-                      wfr (&bn)[2]) {
-        const bool more = kb + 1 < KB;
-        const int kn = more ? kb + 1 : kb;
-        wfr al[G2];
-#pragma unroll
-        for (int gi = 0; gi < G2; ++gi) {
-          an[gi] = frag(gi, kn, 0);
-          if (WD_SPLIT_PASSES == 3) al[gi] = frag(gi, kb, 1);
-        }
-        if constexpr (BM) {
-          bn[0] = wd_frag(wbrs, lane, (int)(((NG2 == 1 ? 0 : g) * KB + kn)) * 1024);
-          if (NG2 == 1) bn[1] = wd_frag(wbrs, lane, (int)((KB + kn)) * 1024);
-        }
-#pragma unroll
-        for (int gi = 0; gi < G2; ++gi)
-#pragma unroll
-          for (int v = 0; v < UPW; ++v) acc2[v][gi] = wd_mfma16(wd_h(ah[gi]), xh[v], acc2[v][gi]);
-#pragma unroll
-        for (int gi = 0; gi < G2; ++gi)
-#pragma unroll
-          for (int v = 0; v < UPW; ++v)
-            if (WD_SPLIT_PASSES >= 2) acc2[v][gi] = wd_mfma16(wd_h(ah[gi]), xl[v], acc2[v][gi]);
-        if (WD_SPLIT_PASSES == 3) {
-#pragma unroll
-          for (int gi = 0; gi < G2; ++gi)
-#pragma unroll
-            for (int v = 0; v < UPW; ++v) acc2[v][gi] = wd_mfma16(wd_h(al[gi]), xh[v], acc2[v][gi]);
-        }
-        if constexpr (BM) {
-#pragma unroll
-          for (int v = 0; v < UPW; ++v) {
-            if (NG2 == 1) {
-              accb[v] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wd_h(bc[0]), xh[v], accb[v], 0, 0, 0);
-              accb[v] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wd_h(bc[1]), xl[v], accb[v], 0, 0, 0);
-            } else {
-              const wh8 bop = g == 0 ? xh[v] : xl[v];
-              accb[v] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wd_h(bc[0]), bop, accb[v], 0, 0, 0);
-            }
-          }
-        }
-        form(kn, more ? v1p : v0s, more ? vop : v0s, nxh, nxl);
-        // next tile's copy: write the slice loaded last step, load the next one
-#pragma unroll
-        for (int e = 0; e < QPS; ++e) {
-          const int c = 8 * ((g * KB + kb) * QPS + e);
-          qdst[c] = qv[e];
-          qv[e] = qload(qrs, c + 8 * QPS);
-        }
-        if (WDC_INTERLEAVE) {
-          // the next step's LDS reads first, then one MFMA + 4 VALU at a time (2+1 passes:
-          // 268-272 ms; 2, 3, 5, 6, 8 VALU per MFMA 305-315 ms, compiler order 331 ms)
-          __builtin_amdgcn_sched_group_barrier(0x100, 4 + 2 * UPW, 0);
-#pragma unroll
-          for (int i = 0; i < WD_SPLIT_PASSES * G2 * UPW + (BM ? (3 - NG2) * UPW : 0); ++i) {
-            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-            __builtin_amdgcn_sched_group_barrier(0x002, WDC_VPM, 0);
-          }
-        }
-      };
-      // BM: the weight and bound fragments of step kb + 2 are loaded into the registers step kb's
+      // the weight and bound fragments of step kb + 2 are loaded into the registers step kb's
       // MFMAs have just read -- a two-step prefetch distance with two register sets (the
       // one-pass step is half as long as a two-pass one, so one step ahead left its MFMAs
       // waiting on L2)
@@ -1298,7 +1150,7 @@ __global__ __launch_bounds__(256, UPW == 1 ? 2 : 1) void wdc_scan_kernel(WdScanA
                        wh8 (&nxh)[UPW], wh8 (&nxl)[UPW], wfr (&bq)[2]) {
         const bool more = kb + 1 < KB;
         const int kn = more ? kb + 1 : kb;
-        const int kf = kb + WD_PREFETCH < KB ? kb + WD_PREFETCH : KB - 1;
+        const int kf = kb + 2 < KB ? kb + 2 : KB - 1;
 #pragma unroll
         for (int gi = 0; gi < G2; ++gi)
 #pragma unroll
@@ -1307,7 +1159,7 @@ __global__ __launch_bounds__(256, UPW == 1 ? 2 : 1) void wdc_scan_kernel(WdScanA
           }
 #pragma unroll
         for (int v = 0; v < UPW; ++v) {
-          if constexpr (ASMACC && WD_ASM_BOUND && NG2 == 1) {
+          if constexpr (ASMACC && NG2 == 1) {
             wd_mfma16x_accv<true>(accb[v], wd_h(bq[0]), xh[v]);
             wd_mfma16x_accv<true>(accb[v], wd_h(bq[1]), xl[v]);
           } else if (NG2 == 1) {
@@ -1322,87 +1174,48 @@ __global__ __launch_bounds__(256, UPW == 1 ? 2 : 1) void wdc_scan_kernel(WdScanA
         for (int gi = 0; gi < G2; ++gi) a[gi] = frag(gi, kf, 0);
         bq[0] = wd_frag(wbrs, lane, (int)(((NG2 == 1 ? 0 : g) * KB + kf)) * 1024);
         if (NG2 == 1) bq[1] = wd_frag(wbrs, lane, (int)((KB + kf)) * 1024);
-        form(kn, v0s, v0s, nxh, nxl);
+        form(kn, nxh, nxl);
 #pragma unroll
         for (int e = 0; e < QPS; ++e) {
           const int c = 8 * ((g * KB + kb) * QPS + e);
           qdst[c] = qv[e];
           qv[e] = qload(qrs, c + 8 * QPS);
         }
-        if (WDC_INTERLEAVE) {
-          __builtin_amdgcn_sched_group_barrier(0x100, 4 + 2 * UPW, 0);
+        // the next step's LDS reads first, then one MFMA + WDC_VPM VALU at a time (2+1 passes:
+        // 268-272 ms; 2, 3, 5, 6, 8 VALU per MFMA 305-315 ms, compiler order 331 ms)
+        __builtin_amdgcn_sched_group_barrier(0x100, 4 + 2 * UPW, 0);
 #pragma unroll
-          for (int i = 0; i < G2 * UPW + (3 - NG2) * UPW; ++i) {
-            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-            __builtin_amdgcn_sched_group_barrier(0x002, WDC_VPM, 0);
-          }
+        for (int i = 0; i < G2 * UPW + (3 - NG2) * UPW; ++i) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x002, WDC_VPM, 0);
         }
       };
       wfr fa[G2], fb[G2], ba[2], bb[2];
       wh8 xha[UPW], xla[UPW], xhb[UPW], xlb[UPW];
-      form(0, v1p, vop, xha, xla);
+      form(0, xha, xla);
 #pragma unroll
       for (int gi = 0; gi < G2; ++gi) fa[gi] = frag(gi, 0, 0);
-      wfr fc[G2], bc3[2];  // third fragment set (WD_PREFETCH 3)
-      if constexpr (BM) {
-        const int k1 = KB > 1 ? 1 : 0, k2 = KB > 2 ? 2 : KB - 1;
+      {
+        const int k1 = KB > 1 ? 1 : 0;
 #pragma unroll
-        for (int gi = 0; gi < G2; ++gi) {
-          fb[gi] = frag(gi, k1, 0);
-          if (WD_PREFETCH == 3) fc[gi] = frag(gi, k2, 0);
-        }
+        for (int gi = 0; gi < G2; ++gi) fb[gi] = frag(gi, k1, 0);
         const int bo = (NG2 == 1 ? 0 : g) * KB;
         ba[0] = wd_frag(wbrs, lane, (int)(bo) * 1024);
         bb[0] = wd_frag(wbrs, lane, (int)((bo + k1)) * 1024);
-        if (WD_PREFETCH == 3) bc3[0] = wd_frag(wbrs, lane, (int)((bo + k2)) * 1024);
         if (NG2 == 1) {
           ba[1] = wd_frag(wbrs, lane, (int)(KB) * 1024);
           bb[1] = wd_frag(wbrs, lane, (int)((KB + k1)) * 1024);
-          if (WD_PREFETCH == 3) bc3[1] = wd_frag(wbrs, lane, (int)((KB + k2)) * 1024);
         }
       }
-      if constexpr (BM && WD_PAIRS) {
+      {
         // steps in pairs with the two register sets swapped (the one-pass kernel is issue-bound:
-        // the copies of the copy form below were 28 v_mov per step; the 2-pass kernel was
-        // MFMA-bound and measured 266 vs 261 ms the other way round)
+        // copying one set into the other was 28 v_mov per step)
         int kb = 0;
-        if (WD_PREFETCH == 3) {
-          // three fragment sets x two operand sets: six steps per iteration, guarded tail
-          for (; kb + 5 < KB; kb += 6) {
-            stepd(kb, fa, xha, xla, xhb, xlb, ba);
-            stepd(kb + 1, fb, xhb, xlb, xha, xla, bb);
-            stepd(kb + 2, fc, xha, xla, xhb, xlb, bc3);
-            stepd(kb + 3, fa, xhb, xlb, xha, xla, ba);
-            stepd(kb + 4, fb, xha, xla, xhb, xlb, bb);
-            stepd(kb + 5, fc, xhb, xlb, xha, xla, bc3);
-          }
-          if (kb < KB) stepd(kb, fa, xha, xla, xhb, xlb, ba);
-          if (kb + 1 < KB) stepd(kb + 1, fb, xhb, xlb, xha, xla, bb);
-          if (kb + 2 < KB) stepd(kb + 2, fc, xha, xla, xhb, xlb, bc3);
-          if (kb + 3 < KB) stepd(kb + 3, fa, xhb, xlb, xha, xla, ba);
-          if (kb + 4 < KB) stepd(kb + 4, fb, xha, xla, xhb, xlb, bb);
-        } else {
-          for (; kb + 1 < KB; kb += 2) {
-            stepd(kb, fa, xha, xla, xhb, xlb, ba);
-            stepd(kb + 1, fb, xhb, xlb, xha, xla, bb);
-          }
-          if (kb < KB) stepd(kb, fa, xha, xla, xhb, xlb, ba);
+        for (; kb + 1 < KB; kb += 2) {
+          stepd(kb, fa, xha, xla, xhb, xlb, ba);
+          stepd(kb + 1, fb, xhb, xlb, xha, xla, bb);
         }
-      } else {
-        for (int kb = 0; kb < KB; ++kb) {
-          step(kb, fa, fb, xha, xla, xhb, xlb, ba, bb);
-#pragma unroll
-          for (int gi = 0; gi < G2; ++gi) fa[gi] = fb[gi];
-          if constexpr (BM) {
-            ba[0] = bb[0];
-            ba[1] = bb[1];
-          }
-#pragma unroll
-          for (int v = 0; v < UPW; ++v) {
-            xha[v] = xhb[v];
-            xla[v] = xlb[v];
-          }
-        }
+        if (kb < KB) stepd(kb, fa, xha, xla, xhb, xlb, ba);
       }
       if constexpr (ASMACC) {
         // the last MFMAs' results -> any reader: 8-pass XDL, 12+ wait states; the fence names
@@ -1430,7 +1243,7 @@ __global__ __launch_bounds__(256, UPW == 1 ? 2 : 1) void wdc_scan_kernel(WdScanA
       // kept in 8 registers per row block and user, its bound term summed), then layer 3 -- so
       // layer 3's accumulators take the registers of layer 2's, which are all dead by then
       // (one phase per row block kept both sets live and spilled).
-      if constexpr (G2 == RB2 && OB > 0 && WD_SPLIT_PASSES3 == 1) {
+      if constexpr (G2 == RB2 && OB > 0) {
         // in halves of RH row blocks: x2 of the half's blocks (their f16 B operands, their
         // bound terms), then their layer-3 MFMAs -- layer 3's accumulators take the registers of
         // the first half's layer-2 ones (all 256 accumulator registers hold layer 2 until then)
@@ -1449,7 +1262,7 @@ __global__ __launch_bounds__(256, UPW == 1 ? 2 : 1) void wdc_scan_kernel(WdScanA
         auto w3load = [&](int kb3) {
 #pragma unroll
           for (int ob = 0; ob < NOB; ++ob) {
-            const int q = (ABL & 8) ? ob * 2 : (ob * 2 * RB2 + kb3) * 2;
+            const int q = (ob * 2 * RB2 + kb3) * 2;
             w3b[kb3 % (W3D + 1)][ob] = wd_frag(w3rs, lane, q * 1024);
           }
         };
@@ -1501,7 +1314,7 @@ __global__ __launch_bounds__(256, UPW == 1 ? 2 : 1) void wdc_scan_kernel(WdScanA
               for (int ob = 0; ob < NOB; ++ob)
 #pragma unroll
                 for (int v = 0; v < UPW; ++v) {
-                  if constexpr (ASMACC && WD_ASM_L3) {
+                  if constexpr (ASMACC) {
                     if (first) {
                       if (ob == 0) wd_mfma_acc0<true>(acc3[v][ob], wd_h(bh[ob]), yh_h[v][rr][half2]);
                       else wd_mfma_acc0<false>(acc3[v][ob], wd_h(bh[ob]), yh_h[v][rr][half2]);
@@ -1564,12 +1377,11 @@ __global__ __launch_bounds__(256, UPW == 1 ? 2 : 1) void wdc_scan_kernel(WdScanA
 #pragma unroll
             for (int v = 0; v < UPW; ++v) wd_split8(&y[v][8 * half2], yh[v], yl[v]);
             const int kb3 = 2 * rb + half2;
-            wh8 bh[NOB], bl[NOB];
+            wh8 bh[NOB];
 #pragma unroll
             for (int ob = 0; ob < NOB; ++ob) {
-              const int q = (ABL & 8) ? ob * 2 : (ob * 2 * RB2 + kb3) * 2;
+              const int q = (ob * 2 * RB2 + kb3) * 2;
               bh[ob] = wd_h(wd_frag(w3rs, lane, q * 1024));
-              if (WD_SPLIT_PASSES3 == 3) bl[ob] = wd_h(wd_frag(w3rs, lane, (q + 1) * 1024));
             }
             // G2 = RB2: the chain starts at the first row block with C = 0 (an inline constant),
             // so acc3 becomes live only as acc2's registers are consumed
@@ -1580,17 +1392,7 @@ __global__ __launch_bounds__(256, UPW == 1 ? 2 : 1) void wdc_scan_kernel(WdScanA
 #pragma unroll
               for (int v = 0; v < UPW; ++v)
                 acc3[v][ob] = wd_mfma16(bh[ob], yh[v], first ? zero16 : acc3[v][ob]);
-#pragma unroll
-            for (int ob = 0; ob < NOB; ++ob)
-#pragma unroll
-              for (int v = 0; v < UPW; ++v)
-                if (WD_SPLIT_PASSES3 >= 2) acc3[v][ob] = wd_mfma16(bh[ob], yl[v], acc3[v][ob]);
-            if (WD_SPLIT_PASSES3 == 3) {
-#pragma unroll
-              for (int ob = 0; ob < NOB; ++ob)
-#pragma unroll
-                for (int v = 0; v < UPW; ++v) acc3[v][ob] = wd_mfma16(bl[ob], yh[v], acc3[v][ob]);
-            }
+
           }
         }
       }
@@ -1626,17 +1428,11 @@ __global__ __launch_bounds__(256, UPW == 1 ? 2 : 1) void wdc_scan_kernel(WdScanA
         fin[v] *= inv_s2;
       }
       const float fv = hnm_sum_halves(fin[v]);
-      float b1, bl1;
-      if constexpr (BM) {
-        // item j's row of the bound accumulators: lane j (< 16) row 0, lane j - 16 row 1
-        const float d0 = __shfl(accb[v][0], lane & 15), d1 = __shfl(accb[v][1], lane & 15);
-        b1 = ((lane & 31) < 16 ? d0 : d1) * (A.prm->inv_sb * inv_s1);
-        bl1 = 0.f;  // inside b1 (A rows of the |x_lo| operand)
-      } else {
-        b1 = hnm_sum_halves(bx1[v]);
-        // one-pass layer 2's x_lo term (x 1 + 2^-10: |W_hi| <= (1 + 2^-11)|W'| and the sums)
-        bl1 = WD_SPLIT_PASSES == 1 ? 1.0009765625f * hnm_sum_halves(bxl[v]) : 0.f;
-      }
+      // item j's row of the bound accumulators: lane j (< 16) row 0, lane j - 16 row 1; the
+      // layer-2 x_lo term is inside (the A rows of the |x_lo| operand)
+      const float d0 = __shfl(accb[v][0], lane & 15), d1 = __shfl(accb[v][1], lane & 15);
+      const float b1 = ((lane & 31) < 16 ? d0 : d1) * (A.prm->inv_sb * inv_s1);
+      const float bl1 = 0.f;
       const float b2 = hnm_sum_halves(bx2[v]);
       const float b3 = hnm_sum_halves(bx3[v]);
       const float score = fv + cub[v] + wi;
@@ -2017,7 +1813,7 @@ static hnm_status wd_exact(hnm_ctx* ctx, const hnm_widedeep_weights* w, const Wd
 }
 
 // ------------------------------------------------------------------ certified path host
-#define WDC_CAP (WD_SPLIT_PASSES == 1 ? 4096 : 1024)  // appended candidates per (user, partition) segment
+#define WDC_CAP 4096  // appended candidates per (user, partition) segment
 
 static bool wdc_instantiated(int RB2, int OB) {
   return (RB2 == 8 && OB == 4) || (RB2 == 4 && OB == 2) || (RB2 == 2 && OB == 1) ||
@@ -2113,21 +1909,17 @@ static hnm_status wdc_prepare(hnm_ctx* ctx, const hnm_widedeep_weights* w, const
                      WDC_STAT_BLOCKS, c.v1, c.v2, c.b2s, c.prm, c.v1o);
   hipLaunchKernelGGL(wdc_convert_kernel, dim3(256), dim3(256), 0, s, *w, S.pr, c.prm, c.W2hl,
                      c.W3hl);
-  if (WD_SPLIT_PASSES == 1 && WD_BOUND_MFMA)
-    hipLaunchKernelGGL(wdc_boundfrag_kernel, dim3((unsigned)hnm_cdiv(S.K1P / 16 * 2 * 64, 256)),
+  hipLaunchKernelGGL(wdc_boundfrag_kernel, dim3((unsigned)hnm_cdiv(S.K1P / 16 * 2 * 64, 256)),
                        dim3(256), 0, s, c.prm, c.v1, c.v1o, S.K1P, c.WBf);
   HNM_LAUNCH_CHECK();
   return HNM_OK;
 }
 
-#ifndef WDC_ABL  // timing ablations (wrong scores; tools only): 1 W2 / 8 W3 fragments from one
-#define WDC_ABL 0  // address
-#endif
-template <int RB2, int OB, int MODE, int ABL = WDC_ABL>
+template <int RB2, int OB, int MODE>
 static void wdc_launch_scan(hnm_ctx* ctx, dim3 grid, size_t lds, const WdScanArgs& a) {
   constexpr int G2 = RB2 < WDC_G2 ? RB2 : WDC_G2;
   constexpr int UPW = RB2 == 8 && OB == 4 ? 2 : 1;  // = wdc_upw
-  auto kern = wdc_scan_kernel<RB2, OB, G2, MODE, UPW, ABL>;
+  auto kern = wdc_scan_kernel<RB2, OB, G2, MODE, UPW>;
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   hipLaunchKernelGGL(kern, grid, dim3(256), lds, ctx->stream, a);
 }
@@ -2176,7 +1968,7 @@ static hnm_status wdc_scan(hnm_ctx* ctx, const hnm_widedeep_weights* w, const Wd
   a.lda = lda;
   const int upb = 4 * wdc_upw(pr);
   const size_t lds =
-      (size_t)(2 * 32 * (S.K1P + 4) + (upb + 3) * S.K1P + 2 * pr.RB2 * 32 + NOB * 32 + NL * 32) * 4;
+      (size_t)(2 * 32 * (S.K1P + 4) + upb * S.K1P + 2 * pr.RB2 * 32 + NOB * 32 + NL * 32) * 4;
   dim3 grid((unsigned)hnm_cdiv(B, upb), (unsigned)c.np);
   if (mode == WDC_THRESH) hnm_timer_begin(ctx, HNM_TIME_SCORE);
 #define WDC_CASE(R, O)                                                        \
