@@ -515,10 +515,13 @@ def run_extras(args):
     # favourable to the pruning than the init -- NCF "personal" (user-specific best items) and
     # the trained-like stress sets; step time, candidates re-scored per row, fallback rows
     rob = {}
-    for w, ws in (("ncf", ("personal", "norms", "student_t")), ("mf", ("norms", "student_t"))):
+    for w, ws in (("ncf", ("personal", "norms", "student_t", "norms+strided")),
+                  ("mf", ("norms", "student_t"))):
         for wt in ws:
-            line = run_child(["--workload", w, "--weights", wt, "--steps", str(args.steps),
-                              "--warmup", str(args.warmup), "--profile-only"], 600)
+            wname, _, opt = wt.partition("+")
+            line = run_child(["--workload", w, "--weights", wname, "--steps", str(args.steps),
+                              "--warmup", str(args.warmup), "--profile-only"]
+                             + (["--" + opt] if opt else []), 600)
             log(f"robustness {w} {wt} done")
             if line is not None:
                 pf = line.get("prefilter") or {}
@@ -555,6 +558,10 @@ def main():
                          "best items are user-specific (emb_scale 20, biases); norms / "
                          "student_t: trained-like weights (NCF, MF: embedding rows at norms "
                          "50-200 / Student-t(3) weights and biases)")
+    ap.add_argument("--strided", action="store_true",
+                    help="NCF: HNM_OPT_STRIDED=1, the gated per-user strided sample beside the "
+                         "champion sample (pays off on weights whose best items are "
+                         "user-specific; costs ~2 %% of the init-weight step)")
     ap.add_argument("--exact", action="store_true",
                     help="exact fp32 scan of every item instead of the certified f16 pre-filter")
     ap.add_argument("--profile-only", action="store_true",
@@ -576,8 +583,12 @@ def main():
     t_setup = time.perf_counter()
     if args.exact:
         _lib.set_prefilter(device, False)
+    if args.strided:
+        _lib.set_option(device, _lib.HNM_OPT_STRIDED, 1)
     wl, info, cpu = build_workload(args.workload, rank, world, device, B, args.exact,
                                    args.weights)
+    if args.strided:
+        info["strided_sample"] = True
     step, per_launch, bound, kernel = wl["step"], wl["per_launch"], wl["bound"], wl["kernel"]
     # resident user batches: rank-specific, distinct ids
     nb = 4

@@ -297,6 +297,7 @@ def kernel_timing(device):
 
 HNM_OPT_PREFILTER = 1
 HNM_OPT_STATS = 3
+HNM_OPT_STRIDED = 4
 
 
 def set_option(device, option, value):

@@ -29,6 +29,7 @@ extern "C" hnm_status hnm_ctx_create(int device, hnm_ctx** out) {
   if (hipGetDeviceProperties(&prop, device) == hipSuccess) c->num_cus = prop.multiProcessorCount;
   if (c->num_cus <= 0) c->num_cus = 256;
   c->prefilter = 1;
+  c->strided = 0;
   if (hipMalloc((void**)&c->err_dev, 64) != hipSuccess) {
     free(c);
     hnm_set_error("hnm_ctx_create: hipMalloc of the error word failed");
@@ -91,6 +92,9 @@ extern "C" hnm_status hnm_ctx_set_option(hnm_ctx* ctx, int option, int64_t value
       return HNM_OK;
     case HNM_OPT_STATS:
       ctx->stats_on = value != 0;
+      return HNM_OK;
+    case HNM_OPT_STRIDED:
+      ctx->strided = value != 0;
       return HNM_OK;
     default:
       hnm_set_error("hnm_ctx_set_option: unknown option %d", option);

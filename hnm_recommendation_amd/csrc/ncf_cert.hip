@@ -56,16 +56,18 @@ constexpr int64_t CERT_GROUP_MIN = 48;    // items per champion group, at least
 // overflowing segments).  A sample pass over one 32-item tile in CERT_STRIDE for every row gives
 // a second lower bound (the larger of the two is used) at ~1/CERT_STRIDE of the scan's cost.
 // Whether it pays is predicted on the proxy rows, whose every item the proxy pass scored:
-// cert_gate_kth_kernel takes each proxy's K-th over its LEAVE-ONE-OUT champions (picked by the
-// other proxies: what a non-proxy row sees) and over the strided tiles; cert_gate_count_kernel
-// counts, per proxy, the items the main scan would append under each bound (approx + e_i >=
-// tau, tau = kv - 2 Eu: cert_tau_kernel); the pass runs when it saves more than CERT_GATE_GAIN
+// cert_gate_kernel takes each proxy's K-th over its LEAVE-ONE-OUT champions (picked by the
+// other proxies: what a non-proxy row sees) and over the strided tiles, and counts, per proxy,
+// the items the main scan would append under each bound (approx + e_i >= tau, tau = kv - 2 Eu:
+// cert_tau_kernel); the pass runs when it saves more than CERT_GATE_GAIN
 // candidates a row on average -- re-scoring ~250 candidates costs about what the 1/8 pass does
 // (bench step: 65 us for 4,096 x 70 candidates against 1/8 of a 1.85 ms scan).  Gated off, the
 // pass and its K-th exit at launch.
+// Opt-in (HNM_OPT_STRIDED = 1; round 5, A/B on one box: init weights 2.002 -> 2.046 ms a step,
+// the gate and the gated-off launches; "norms" weights 3.683 -> 3.092 ms).
 constexpr int CERT_STRIDE = 8;
-constexpr int64_t CERT_GATE_GAIN = 250;
-constexpr int CERT_GATE_CHUNKS = 64;  // workgroups per proxy row of the count kernel
+constexpr int64_t CERT_GATE_GAIN = 150;  // (the proxies under-predict the saving: 235 predicted
+                                         // for 468 measured on "norms" batch 1)
 // scan workgroups per CU (LDS 51.7 KB each; the scan's 168 VGPRs fit three waves per SIMD)
 #define HNM_SCAN_OCC 3
 constexpr int CERT_WG_PER_CU = HNM_SCAN_OCC;
@@ -858,7 +860,15 @@ __global__ __launch_bounds__(256) void cert_champion_kernel(const float* __restr
                                                             int64_t ld, int np_rows, int64_t I,
                                                             int64_t gsz, int64_t nch,
                                                             int32_t* __restrict__ sidx,
-                                                            int32_t* __restrict__ sloo) {
+                                                            int32_t* __restrict__ sloo,
+                                                            int64_t ns, int32_t* __restrict__ sidx2,
+                                                            unsigned long long* __restrict__ gcnt) {
+  // the gate's inputs: its counters zeroed, the strided sample's item map (tiles 0, S, 2S, ...
+  // of 32 items: sidx2[0, ns)) -- both read only by later launches
+  if (gcnt && blockIdx.x == 0 && threadIdx.x < 4) gcnt[threadIdx.x] = 0;
+  if (sidx2)
+    for (int64_t n = (int64_t)blockIdx.x * 256 + threadIdx.x; n < ns; n += (int64_t)gridDim.x * 256)
+      sidx2[n] = (int32_t)((n >> 5) * (32 * CERT_STRIDE) + (n & 31));
   const int64_t g = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (g >= nch) return;
   const int lane = threadIdx.x & 63;
@@ -958,56 +968,55 @@ struct Top4 {
   }
 };
 
-// Gate, step 1 (one workgroup of 256 threads per proxy row r): kv[2r] = a lower bound of the
-// K-th of the row's (approx - e_i) over its leave-one-out champions, kv[2r + 1] = the larger of
-// that and the same over the strided tiles (lane top-4 lists, each wave's K pops, then the
-// K-th of the 4 waves' lists; loads issued 8 at a time: the rows sit in L2, the latency of
-// one dependent load per iteration would cost ~0.1 ms).  Workgroup 0 also zeroes the count
-// kernel's counters and writes the strided sample's item map (tiles 0, S, 2S, ... of 32 items:
-// sidx2[0, ns)).
-__global__ __launch_bounds__(256) void cert_gate_kth_kernel(const float* __restrict__ pd,
-                                                            int64_t ld, int np_rows,
-                                                            const int32_t* __restrict__ sloo,
-                                                            int64_t nch, int K, int64_t ns,
-                                                            int32_t* __restrict__ sidx2,
-                                                            float* __restrict__ kv,
-                                                            unsigned long long* __restrict__ cnt) {
-  __shared__ float wl[2][4][64];
+// The gate (one 1,024-thread workgroup per proxy row r).  Two lower bounds of the row's K-th best
+// (approx - e_i): kc over its leave-one-out champions, ks over the strided sample's items (lane
+// top-4 lists, each wave's K pops, the K-th of the 16 waves' lists); then, over the strided items
+// -- a uniform 1/CERT_STRIDE sample of the catalogue, already in registers -- the count of those
+// the main scan would append with the champion bound alone (approx + e_i >= kc - 2 Eu) and with
+// the strided sample's bound too, times CERT_STRIDE.  The last workgroup writes *gate = 1 when
+// the pass is predicted to save more than CERT_GATE_GAIN candidates a row.  Every load is issued
+// in one of three batches (the proxy rows were just written: each dependent round trip costs
+// microseconds).  Round 5, earlier forms: a kth kernel + a full-catalogue count kernel 25 + 24
+// us, one fused kernel counting the whole catalogue 32 us a call.
+constexpr int GATE_SPT = 16;  // strided items per thread (16,384 per row: I <= 524,288 fully)
+__global__ __launch_bounds__(1024) void cert_gate_kernel(
+    const float* __restrict__ pd, int64_t ld, int np_rows, const int32_t* __restrict__ sloo,
+    int64_t nch, int K, int64_t ns, const float* __restrict__ Bs, const float* __restrict__ Di,
+    const float* __restrict__ Cs, const float* __restrict__ Au, const CertParams* __restrict__ prm,
+    unsigned long long* __restrict__ cnt, int* __restrict__ gate, int64_t B,
+    unsigned long long* __restrict__ stats) {
+  constexpr int NW = 16;
+  __shared__ float wl[2][NW][64];
+  __shared__ float kvs[2];
+  __shared__ int part[2][NW];
   const int r = blockIdx.x, tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
-  if (r == 0) {
-    for (int64_t n = tid; n < ns; n += 256)
-      sidx2[n] = (int32_t)((n >> 5) * (32 * CERT_STRIDE) + (n & 31));
-    if (tid < 4) cnt[tid] = 0;
-  }
   const float* row = pd + r * ld;
   const int32_t* sl = sloo + r * nch;
+  // the strided sample: thread tid takes its items n = tid + 1024 u (u < GATE_SPT); with more
+  // than 16,384 sampled items the rest are left out (a lower bound / a sample of the count)
+  const int64_t nsg = std::min<int64_t>(ns, 1024 * GATE_SPT);
+  int32_t ix[4];
+  float v[GATE_SPT], bsv[GATE_SPT], dv[GATE_SPT];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int64_t q = u * 1024 + tid;
+    ix[u] = q < nch ? sl[q] : -1;  // nch <= CERT_CHAMPIONS (<= 4,096 loaded)
+  }
+#pragma unroll
+  for (int u = 0; u < GATE_SPT; ++u) {
+    const int64_t n = u * 1024 + tid;
+    const int64_t it = (n >> 5) * (32 * CERT_STRIDE) + (n & 31);
+    const bool ok = n < nsg;
+    v[u] = ok ? row[it] : -__builtin_inff();
+    bsv[u] = ok ? Bs[it] : 0.f;
+    dv[u] = ok ? Di[it] : 0.f;
+  }
   Top4 c, t;
-  constexpr int U = 8;
-  for (int64_t q0 = 0; q0 < nch; q0 += 256 * U) {
-    int32_t ix[U];
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int64_t q = q0 + u * 256 + tid;
-      ix[u] = q < nch ? sl[q] : -1;
-    }
-    float v[U];
+  for (int u = 0; u < 4; ++u) c.offer(ix[u] >= 0 ? row[ix[u]] : -__builtin_inff());
 #pragma unroll
-    for (int u = 0; u < U; ++u) v[u] = ix[u] >= 0 ? row[ix[u]] : -__builtin_inff();
-#pragma unroll
-    for (int u = 0; u < U; ++u) c.offer(v[u]);
-  }
-  for (int64_t n0 = 0; n0 < ns; n0 += 256 * U) {
-    float v[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int64_t n = n0 + u * 256 + tid;
-      v[u] = n < ns ? row[(n >> 5) * (32 * CERT_STRIDE) + (n & 31)] : -__builtin_inff();
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) t.offer(v[u]);
-  }
-  // each wave's K best survivors (descending) -> LDS; then wave 0 takes the K-th of the 4 K
-  for (int i = 0; i < 2; ++i) {
+  for (int u = 0; u < GATE_SPT; ++u) t.offer(v[u]);
+  for (int i = 0; i < 2; ++i) {  // each wave's K best survivors, descending
     Top4& L = i ? t : c;
     for (int q = 0; q < K; ++q) {
       float m = L.t0;
@@ -1028,39 +1037,20 @@ __global__ __launch_bounds__(256) void cert_gate_kth_kernel(const float* __restr
     }
   }
   __syncthreads();
-  if (w == 0) {
-    float res[2];
-    for (int i = 0; i < 2; ++i) {
-      Top4 M;
-      for (int z = lane; z < 4 * K; z += 64) M.offer(wl[i][z / K][z % K]);
-      res[i] = M.kth(K, lane);
-    }
-    if (lane == 0) {
-      kv[2 * r] = res[0];
-      kv[2 * r + 1] = fmaxf(res[0], res[1]);
-    }
+  if (w < 2) {  // wave i: the K-th of the 16 waves' lists (exact for K <= 16: at most 4 values a
+                // lane; a lower bound of it beyond, as good for a prediction)
+    Top4 M;
+    for (int z = lane; z < NW * K; z += 64) M.offer(wl[w][z / K][z % K]);
+    const float kv = M.kth(K, lane);
+    if (lane == 0) kvs[w] = kv;
   }
-}
-
-// Gate, step 2 (grid CERT_GATE_CHUNKS x proxy rows): per proxy row the items the main scan would
-// append under each bound of step 1, summed into cnt[0] / cnt[1]; the last workgroup to finish
-// writes *gate = 1 when the strided sample saves more than CERT_GATE_GAIN candidates a row.
-__global__ __launch_bounds__(256) void cert_gate_count_kernel(
-    const float* __restrict__ pd, int64_t ld, int np_rows, int64_t I,
-    const float* __restrict__ kv, const float* __restrict__ Bs, const float* __restrict__ Di,
-    const float* __restrict__ Cs, const float* __restrict__ Au, const CertParams* __restrict__ prm,
-    unsigned long long* __restrict__ cnt, int* __restrict__ gate, int64_t B,
-    unsigned long long* __restrict__ stats) {
-  __shared__ int part[2][4];
-  const int r = blockIdx.y, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int64_t chunk = hnm_cdiv(I, gridDim.x);
-  const int64_t i0 = (int64_t)blockIdx.x * chunk, i1 = std::min<int64_t>(I, i0 + chunk);
+  __syncthreads();
   const float eu2 = 2.f * prm->unit * (CERT_RHO * (prm->c0 + Au[r]) + prm->absb);
-  const float tc = kv[2 * r] - eu2, ts = kv[2 * r + 1] - eu2, cr = Cs[r];
-  const float* row = pd + r * ld;
+  const float tc = kvs[0] - eu2, ts = fmaxf(kvs[0], kvs[1]) - eu2, cr = Cs[r];
   int nc = 0, nsv = 0;
-  for (int64_t i = i0 + threadIdx.x; i < i1; i += 256) {
-    const float ub = row[i] + 2.f * fmaf(cr, Di[i], Bs[i]);  // approx + e_i
+#pragma unroll
+  for (int u = 0; u < GATE_SPT; ++u) {
+    const float ub = v[u] + 2.f * fmaf(cr, dv[u], bsv[u]);  // approx + e_i
     nc += ub >= tc;
     nsv += ub >= ts;
   }
@@ -1074,12 +1064,19 @@ __global__ __launch_bounds__(256) void cert_gate_count_kernel(
     part[1][w] = nsv;
   }
   __syncthreads();
-  if (threadIdx.x == 0) {
-    atomicAdd(&cnt[0], (unsigned long long)(part[0][0] + part[0][1] + part[0][2] + part[0][3]));
-    atomicAdd(&cnt[1], (unsigned long long)(part[1][0] + part[1][1] + part[1][2] + part[1][3]));
+  if (tid == 0) {
+    unsigned long long s0 = 0, s1 = 0;
+    for (int q = 0; q < NW; ++q) {
+      s0 += (unsigned)part[0][q];
+      s1 += (unsigned)part[1][q];
+    }
+    // scaled to the catalogue: the sampled share of the items
+    const double scale = (double)ns / (double)std::max<int64_t>(nsg, 1) * CERT_STRIDE;
+    atomicAdd(&cnt[0], (unsigned long long)(s0 * scale));
+    atomicAdd(&cnt[1], (unsigned long long)(s1 * scale));
     __threadfence();
     const unsigned long long ticket = atomicAdd(&cnt[2], 1ull);
-    if (ticket == (unsigned long long)gridDim.x * gridDim.y - 1) {  // every count is in
+    if (ticket == (unsigned long long)gridDim.x - 1) {  // every count is in
       __threadfence();
       const unsigned long long c0 = atomicAdd(&cnt[0], 0ull), c1 = atomicAdd(&cnt[1], 0ull);
       const int on = (np_rows >= 4 && !prm->bad &&
@@ -1296,7 +1293,6 @@ struct CertWs {
   float* sdense;  // [B, ns] strided sample values (gated)
   float* kth2;    // [B, K] its K best
   int* gate;
-  float* gkv;     // [2 * CERT_PROXY_USERS] gate: the proxies' bounds
   unsigned long long* gcnt;  // [4] gate counters
   int64_t* kthi;
   int *cnt, *flag;
@@ -1370,7 +1366,6 @@ size_t cert_carve(char* base, int64_t B, int64_t I, int K, int num_cus, int wg, 
   x.sdense = (float*)take((size_t)B * sh.ns * 4);
   x.kth2 = (float*)take((size_t)B * K * 4);
   x.gate = (int*)take(4);
-  x.gkv = (float*)take(2 * CERT_PROXY_USERS * 4);
   x.gcnt = (unsigned long long*)take(4 * 8);
   x.kthi = (int64_t*)take((size_t)B * K * 8);
   x.cnt = (int*)take((size_t)B * sh.part.np * 4);
@@ -1471,6 +1466,7 @@ hnm_status ncf_cert_begin(hnm_ctx* ctx, const hnm_ncf_weights* w, const NcfTabs&
   // nch groups -> every row's K-th best approx - e over those items -> L (a lower bound of
   // the exact K-th for any item subset; this one tends to hold the rows' best items)
   const int64_t bp = std::min<int64_t>(CERT_PROXY_USERS, B);
+  const bool strided = ctx->strided != 0;  // HNM_OPT_STRIDED: the gated strided sample may run
   ScanArgs a = scan_args(x, bp);
   a.I = I;
   a.dense = x.pdense;
@@ -1482,19 +1478,25 @@ hnm_status ncf_cert_begin(hnm_ctx* ctx, const hnm_ncf_weights* w, const NcfTabs&
   launch_scan<SCAN_SAMPLE>(ctx, dim3((unsigned)a.NP, 1), a);
   HNM_LAUNCH_CHECK();
   hipLaunchKernelGGL(cert_champion_kernel, dim3((unsigned)hnm_cdiv(sh.nch, 4)), dim3(256), 0,
-                     ctx->stream, x.pdense, I, (int)bp, I, sh.gsz, sh.nch, x.sidx, x.sloo);
+                     ctx->stream, x.pdense, I, (int)bp, I, sh.gsz, sh.nch, x.sidx,
+                     strided ? x.sloo : nullptr, sh.ns, strided ? x.sidx2 : nullptr,
+                     strided ? x.gcnt : nullptr);
   HNM_LAUNCH_CHECK();
-  hipLaunchKernelGGL(cert_gate_kth_kernel, dim3((unsigned)bp), dim3(256), 0, ctx->stream,
-                     x.pdense, I, (int)bp, x.sloo, sh.nch, K, sh.ns, x.sidx2, x.gkv, x.gcnt);
-  HNM_LAUNCH_CHECK();
-  if (bp >= 4) {
-    hipLaunchKernelGGL(cert_gate_count_kernel, dim3(CERT_GATE_CHUNKS, (unsigned)bp), dim3(256), 0,
-                       ctx->stream, x.pdense, I, (int)bp, I, x.gkv, x.Bs, x.Di, x.Cs, x.Au, x.prm,
-                       x.gcnt, x.gate, B, ctx->stats_on ? ctx->stats_dev : nullptr);
-  } else {
+  // the gate (8 workgroups, latency-bound: ~22 us) runs on the ctx's side stream beside the
+  // champion pass of every row below (independent: both read the proxy rows and the champions);
+  // the ctx stream joins before the strided pass reads the gate
+  const bool gated = strided && bp >= 4;
+  if (gated) {
+    HNM_HIP_CHECK(hipEventRecord(ctx->side_in, ctx->stream));
+    HNM_HIP_CHECK(hipStreamWaitEvent(ctx->side, ctx->side_in, 0));
+    hipLaunchKernelGGL(cert_gate_kernel, dim3((unsigned)bp), dim3(1024), 0, ctx->side,
+                       x.pdense, I, (int)bp, x.sloo, sh.nch, K, sh.ns, x.Bs, x.Di, x.Cs, x.Au,
+                       x.prm, x.gcnt, x.gate, B, ctx->stats_on ? ctx->stats_dev : nullptr);
+    HNM_LAUNCH_CHECK();
+    HNM_HIP_CHECK(hipEventRecord(ctx->side_out, ctx->side));
+  } else if (strided) {
     HNM_HIP_CHECK(hipMemsetAsync(x.gate, 0, 4, ctx->stream));
   }
-  HNM_LAUNCH_CHECK();
   ScanArgs c = scan_args(x, B);
   c.I = sh.nch;
   c.sidx = x.sidx;
@@ -1506,6 +1508,7 @@ hnm_status ncf_cert_begin(hnm_ctx* ctx, const hnm_ncf_weights* w, const NcfTabs&
   c.ipp = hnm_cdiv(hnm_cdiv(sh.nch, npc), TILE) * TILE;
   c.NP = (int)hnm_cdiv(sh.nch, c.ipp);
   launch_scan<SCAN_SAMPLE>(ctx, dim3((unsigned)c.NP, (unsigned)ublocks), c);
+  if (gated) HNM_HIP_CHECK(hipStreamWaitEvent(ctx->stream, ctx->side_out, 0));  // join
   HNM_LAUNCH_CHECK();
   st = hnm_sample_kth(ctx, x.cdense, sh.nch, B, sh.nch, mptr, midx, K, 1, 1, x.sidx, x.kthv);
   if (st) return st;
@@ -1519,17 +1522,20 @@ hnm_status ncf_cert_begin(hnm_ctx* ctx, const hnm_ncf_weights* w, const NcfTabs&
   const Partition p2 = scan_partition(sh.ns, ublocks, ctx->num_cus, wg);
   g2.ipp = p2.ipp;
   g2.NP = p2.np;
-  launch_scan<SCAN_SAMPLE>(ctx, dim3((unsigned)p2.np, (unsigned)ublocks), g2);
-  HNM_LAUNCH_CHECK();
-  st = hnm_sample_kth(ctx, x.sdense, sh.ns, B, sh.ns, mptr, midx, K, 1, 1, x.sidx2, x.kth2, x.gate);
-  if (st) return st;
+  if (strided) {
+    launch_scan<SCAN_SAMPLE>(ctx, dim3((unsigned)p2.np, (unsigned)ublocks), g2);
+    HNM_LAUNCH_CHECK();
+    st = hnm_sample_kth(ctx, x.sdense, sh.ns, B, sh.ns, mptr, midx, K, 1, 1, x.sidx2, x.kth2, x.gate);
+    if (st) return st;
+  }
+  const int* gp = strided ? x.gate : nullptr;
   hipLaunchKernelGGL(cert_bound_kernel, dim3((unsigned)hnm_cdiv(B, 256)), dim3(256), 0,
-                     ctx->stream, x.kthv, x.kth2, x.gate, K, x.Au, x.prm, w->bp, B, lb ? lb : x.lb,
+                     ctx->stream, x.kthv, x.kth2, gp, K, x.Au, x.prm, w->bp, B, lb ? lb : x.lb,
                      x.Eu);
   HNM_LAUNCH_CHECK();
   if (lists) {
     hipLaunchKernelGGL(cert_bound_lists_kernel, dim3((unsigned)hnm_cdiv(B * K, 256)), dim3(256), 0,
-                       ctx->stream, x.kthv, x.kth2, x.gate, K, x.Eu, x.prm, w->bp, B, lists);
+                       ctx->stream, x.kthv, x.kth2, gp, K, x.Eu, x.prm, w->bp, B, lists);
     HNM_LAUNCH_CHECK();
   }
   return HNM_OK;

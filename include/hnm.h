@@ -75,7 +75,12 @@ hnm_status hnm_ctx_abort_pending(hnm_ctx* ctx);
  * than 64 k, k > 64, the dot path with d > 128 or with an f16 item copy of 2 GiB or more
  * (16.7M items at d <= 64, 8.3M at d <= 128), NCF layer widths beyond 64 / 32 or 33.5M items. */
 enum { HNM_OPT_PREFILTER = 1,
-       HNM_OPT_STATS = 3       /* 1: count pre-filter candidates / fallback rows (diagnostics) */ };
+       HNM_OPT_STATS = 3,      /* 1: count pre-filter candidates / fallback rows (diagnostics) */
+       HNM_OPT_STRIDED = 4     /* NeuralCF certified top-K: 1 = the gated per-user strided
+                                  sample may run (weights whose best items are user-specific:
+                                  bench "norms" 3.68 -> 3.09 ms a step); 0 (default) = the
+                                  champion sample alone (the gate costs ~2 % of the init-weight
+                                  step) */ };
 hnm_status hnm_ctx_set_option(hnm_ctx* ctx, int option, int64_t value);
 /* Pre-filter counters since the last reset (counted only while HNM_OPT_STATS is 1): out[0]
  * rows scored, out[1] candidates re-scored in fp32, out[2] rows that took the exact fallback

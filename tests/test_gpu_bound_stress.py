@@ -166,7 +166,7 @@ def test_wd_topk_stress_bitwise(kind):
 @pytest.mark.parametrize("kind", ["init", "personal", "norms", "student_t"])
 def test_ncf_strided_sample_gate(kind):
     """The certified NCF path's gated per-user strided sample (ncf_cert.hip CERT_STRIDE, round
-    5): whether it runs is predicted on the proxy rows (candidates saved vs. the pass's cost);
+    5; opt-in, HNM_OPT_STRIDED = 1): whether it runs is predicted on the proxy rows (candidates saved vs. the pass's cost);
     either way the top-K is bitwise the exact scan's (rows whose segments overflow take the
     exact fallback, now spread over the whole chip), and the count of rows that used it is
     all-or-nothing per call.  At U = 60,000 the init weights' user embeddings are 5x larger
@@ -193,10 +193,12 @@ def test_ncf_strided_sample_gate(kind):
         _lib.set_prefilter(dev, True)
     _lib.prefilter_stats(dev, reset=True)
     _lib.set_option(dev, _lib.HNM_OPT_STATS, 1)
+    _lib.set_option(dev, _lib.HNM_OPT_STRIDED, 1)  # opt-in (default 0)
     try:
         pv, pi = m.recommend_with_scores(users)
     finally:
         _lib.set_option(dev, _lib.HNM_OPT_STATS, 0)
+        _lib.set_option(dev, _lib.HNM_OPT_STRIDED, 0)
     rows, cands, fallback, sampled = _lib.prefilter_stats(dev, reset=True, extended=True)
     print(f"NCF {kind}: candidates/row {cands / max(rows - fallback, 1):.1f}, fallback {fallback}, "
           f"strided-sample rows {sampled}")

@@ -1,7 +1,7 @@
 """Per-batch pre-filter statistics of the certified NCF step on bench.py's weight sets (rows,
 candidates re-scored per row, exact-fallback rows, rows with the strided sample) and the
 step time of each batch: which batches of a weight set leave the certified path, and why.
-    python tools/robust_probe.py [weights ...]"""
+    python tools/robust_probe.py [--strided] [weights ...]"""
 import sys
 import time
 
@@ -14,7 +14,11 @@ from hnm_recommendation_amd import synthetic as syn  # noqa: E402
 
 dev = torch.device("cuda", 0)
 torch.cuda.set_device(0)
-for wt in sys.argv[1:] or ["init", "personal", "norms", "student_t"]:
+args = sys.argv[1:]
+if "--strided" in args:
+    args.remove("--strided")
+    _lib.set_option(dev, _lib.HNM_OPT_STRIDED, 1)
+for wt in args or ["init", "personal", "norms", "student_t"]:
     wl, info, _ = build_workload("ncf", 0, 1, dev, 4096, False, wt)
     step = wl["step"]
     batches = [torch.from_numpy(syn.user_batch(syn.HM_USERS, 4096, seed=100 + j)).to(dev)
