@@ -41,6 +41,7 @@ constexpr int64_t DCERT_SAMPLE = 52771;  // sampled items: stride max(DCERT_MIN_
 constexpr int64_t DCERT_MIN_STRIDE = 2;
 constexpr float DCERT_RHO = 0.00146484375f;  // 3 u16 = 3 * 2^-11
 constexpr int DCERT_MAX_NP = 64;
+constexpr int DCERT_USER_BLOCKS = 2048;  // dcert_stats_kernel user blocks (4 waves x 4 rows), at most
 
 // user blocks of 32 per scan wave (each item fragment feeds NB MFMAs), per DP.  Round 4 A/B
 // (MF d=64 step / THRESH scan, one box): NB = 1 0.1827 / 0.0835 ms, NB = 2 at 2 workgroups per
@@ -138,7 +139,7 @@ size_t dcert_carve(char* base, int64_t B, int64_t I, int d, int K, int num_cus, 
   DotCertWs x;
   x.prm = (DParams*)take(sizeof(DParams));
   x.Nu = (float*)take(B * 4);
-  x.part = (float*)take(4 * 4 * (2048 + 512));
+  x.part = (float*)take(4 * 4 * (2048 + DCERT_USER_BLOCKS));
   x.Ni = (float*)take(I * 4);
   x.ubr = (float*)take(B * 4);
   x.ibs = (float*)take(I * 4);
@@ -195,21 +196,28 @@ __global__ __launch_bounds__(256) void dcert_stats_kernel(DotArgs a, float* __re
         }
       }
     }
-  } else {  // m0 = max|u_k|
+  } else {  // m0 = max|u_k|; LPU lanes x float4 per request row (the a1 gather fused), 64 / LPU
+            // rows per wave step (a wave per row was a serial latency chain per wave at the
+            // 8 x 4,096 rows of an 8-rank item-sharded step)
+    const int LPU = a.d <= 64 ? 16 : 32, upw = 64 / LPU;
+    const int sub = lane / LPU, l = lane % LPU;
     const int ub = (int)blockIdx.x - item_blocks;
-    for (int64_t b = (int64_t)ub * 4 + wave; b < a.B; b += (int64_t)user_blocks * 4) {
-      const int64_t uid = a.uids[b];
+    for (int64_t b0 = ((int64_t)ub * 4 + wave) * upw; b0 < a.B;
+         b0 += (int64_t)user_blocks * 4 * upw) {
+      const int64_t b = b0 + sub;
+      const bool live = b < a.B;
+      const int64_t uid = live ? a.uids[b] : 0;
       const bool ok = uid >= 0 && uid < a.num_users;
-      if (!ok && lane == 0) hnm_flag(a.err, HNM_ERR_OOB);
-      const float* row = a.ut + (ok ? uid : 0) * a.ldu;
-      const float v0 = lane < a.d ? row[lane] : 0.f;
-      const float v1 = lane + 64 < a.d ? row[lane + 64] : 0.f;
-      m0 = nmax(m0, nmax(fabsf(v0), fabsf(v1)));
-      const float n = sqrtf(wave_sum(v0 * v0 + v1 * v1));
-      if (lane == 0) {
-        Nu[b] = n;
-        const float v = (a.ubias && ok) ? a.ubias[uid] : 0.f;
-        ubr[b] = v + (a.cbias ? a.cbias[0] : 0.f);  // the exact kernel's ub[r]
+      if (live && !ok && l == 0) hnm_flag(a.err, HNM_ERR_OOB);
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (live && ok && 4 * l < a.d) v = *reinterpret_cast<const float4*>(a.ut + uid * a.ldu + 4 * l);
+      m0 = nmax(m0, nmax(nmax(fabsf(v.x), fabsf(v.y)), nmax(fabsf(v.z), fabsf(v.w))));
+      float q = v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+      for (int o = LPU / 2; o >= 1; o >>= 1) q += __shfl_xor(q, o);
+      if (live && l == 0) {
+        Nu[b] = sqrtf(q);
+        const float bv = (a.ubias && ok) ? a.ubias[uid] : 0.f;
+        ubr[b] = bv + (a.cbias ? a.cbias[0] : 0.f);  // the exact kernel's ub[r]
       }
     }
   }
@@ -793,7 +801,22 @@ __global__ __launch_bounds__(256, 4) void dcert_rescore_kernel(
   float v0 = -__builtin_inff(), v1 = -__builtin_inff();
   int i0 = HNM_SENTINEL_IDX, i1 = HNM_SENTINEL_IDX;
   bool nan = false;
-  for (int c0 = 0; c0 < n; c0 += 128 - K) {
+  if (n <= 64) {
+    // one round: lane l re-scores candidate l, one sort of the first 16 / 32 / 64 lanes (the
+    // same total order as the 128-slot rounds, so the same output; the item-sharded step's
+    // ranks see a few candidates a row over 8x the rows, where the 128-slot sort dominated)
+    if (lane < n) {
+      i0 = cand(lane);
+      v0 = score(i0);
+    }
+    nan = v0 != v0;
+    if (__ballot(nan) == 0) {
+      if (n <= 16) hnm_sort_lanes<16>(v0, i0);
+      else if (n <= 32) hnm_sort_lanes<32>(v0, i0);
+      else hnm_sort_lanes<64>(v0, i0);
+    }
+  }
+  for (int c0 = 0; n > 64 && c0 < n; c0 += 128 - K) {
     const int g0 = c0 + lane - K, g1 = c0 + 64 + lane - K;  // candidate of slot lane / lane+64
     if (lane >= K) {
       const bool ok = g0 < n;
@@ -830,7 +853,7 @@ __global__ void dcert_debug_out_kernel(float* __restrict__ ap, int64_t lda, int6
 hnm_status dcert_prepare(hnm_ctx* ctx, const DotArgs& a, const DotCertShape& sh,
                          const DotCertWs& x) {
   const int ib = (int)std::min<int64_t>(2048, hnm_cdiv(a.I, 16));
-  const int ub = (int)std::min<int64_t>(512, hnm_cdiv(a.B, 4));
+  const int ub = (int)std::min<int64_t>(DCERT_USER_BLOCKS, hnm_cdiv(a.B, 4 * (a.d <= 64 ? 4 : 2)));
   hipLaunchKernelGGL(dcert_stats_kernel, dim3(ib + ub), dim3(256), 0, ctx->stream, a, x.part,
                      x.Nu, x.Ni, x.ubr, ib, ub);
   HNM_LAUNCH_CHECK();

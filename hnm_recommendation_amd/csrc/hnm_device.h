@@ -116,10 +116,102 @@ struct WaveTopK {
   }
 };
 
+// x of lane (lane ^ J), J a power of two < 64, without LDS: DPP quad permutes (J = 1, 2), row
+// rotates (J = 4, 8: row_ror:n reads lane (i - n) mod 16 of the row) and the gfx950 row / half
+// swaps (J = 16, 32) -- 1-3 VALU instead of a ds_bpermute round trip (~100+ cycles of latency
+// on a dependent chain such as a sort network or a reduction).
+template <int J>
+__device__ __forceinline__ int hnm_xor_lane(int x) {
+  static_assert(J == 1 || J == 2 || J == 4 || J == 8 || J == 16 || J == 32, "J");
+  if constexpr (J == 1) {
+    return __builtin_amdgcn_update_dpp(0, x, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
+  } else if constexpr (J == 2) {
+    return __builtin_amdgcn_update_dpp(0, x, 0x4E, 0xF, 0xF, false);  // quad_perm [2,3,0,1]
+  } else if constexpr (J == 4) {
+    const int a = __builtin_amdgcn_update_dpp(0, x, 0x124, 0xF, 0xF, false);  // row_ror:4
+    const int b = __builtin_amdgcn_update_dpp(0, x, 0x12C, 0xF, 0xF, false);  // row_ror:12
+    return (__lane_id() & 4) ? a : b;
+  } else if constexpr (J == 8) {
+    return __builtin_amdgcn_update_dpp(0, x, 0x128, 0xF, 0xF, false);  // row_ror:8
+  } else if constexpr (J == 16) {
+    // (vdst, src) = (x, x): vdst's odd rows <-> src's even rows: r[0] = rows (0,0,2,2),
+    // r[1] = rows (1,1,3,3)
+    const auto r = __builtin_amdgcn_permlane16_swap(x, x, false, false);
+    return (__lane_id() & 16) ? (int)r[0] : (int)r[1];
+  } else {
+    const auto r = __builtin_amdgcn_permlane32_swap(x, x, false, false);  // r[0] = lo, r[1] = hi
+    return (__lane_id() & 32) ? (int)r[0] : (int)r[1];
+  }
+}
+template <int J>
+__device__ __forceinline__ float hnm_xor_lane(float x) {
+  return __int_as_float(hnm_xor_lane<J>(__float_as_int(x)));
+}
+
+// Maximum over each aligned group of G lanes (G = 16, 32, 64) in every lane of the group
+// (fmaxf: a NaN lane is ignored unless all are NaN), by DPP / permlane steps (no LDS).
+template <int G>
+__device__ __forceinline__ float hnm_group_max(float x) {
+  static_assert(G == 16 || G == 32 || G == 64, "G");
+  x = fmaxf(x, hnm_xor_lane<1>(x));
+  x = fmaxf(x, hnm_xor_lane<2>(x));
+  x = fmaxf(x, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x124, 0xF, 0xF,
+                                                          false)));  // quads q, q - 1
+  x = fmaxf(x, hnm_xor_lane<8>(x));  // row max in every lane of the row
+  if constexpr (G >= 32) {
+    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false,
+                                                    false);
+    x = fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));  // rows 2k, 2k + 1
+  }
+  if constexpr (G == 64) {
+    const auto h = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false,
+                                                    false);
+    x = fmaxf(__uint_as_float(h[0]), __uint_as_float(h[1]));
+  }
+  return x;
+}
+__device__ __forceinline__ float hnm_wave_max(float x) { return hnm_group_max<64>(x); }
+
+// One compare-exchange step of a bitonic network across lanes: partner lane ^ J; `up`: this
+// lane's block is ordered best-first ((value desc, index asc), hnm_better).
+template <int J>
+__device__ __forceinline__ void hnm_cx(float& v, int& ix, bool up) {
+  const float pv = hnm_xor_lane<J>(v);
+  const int pi = hnm_xor_lane<J>(ix);
+  const bool lower = (hnm_lane() & J) == 0;
+  const bool pb = hnm_better(pv, pi, v, ix);   // partner ranks before mine
+  const bool take = (lower == up) ? pb : !pb;  // lower slot of an up block keeps the better
+  v = take ? pv : v;
+  ix = take ? pi : ix;
+}
+__device__ __forceinline__ void hnm_cx_rt(int j, float& v, int& ix, bool up) {
+  switch (j) {  // a compile-time constant after unrolling
+    case 1: hnm_cx<1>(v, ix, up); break;
+    case 2: hnm_cx<2>(v, ix, up); break;
+    case 4: hnm_cx<4>(v, ix, up); break;
+    case 8: hnm_cx<8>(v, ix, up); break;
+    case 16: hnm_cx<16>(v, ix, up); break;
+    default: hnm_cx<32>(v, ix, up); break;
+  }
+}
+
+// Bitonic sort of one (value, index) pair per lane over each aligned group of W lanes (W = 16,
+// 32, 64) into (value desc, index asc) order -- lane 0 of the group = best.  Total order on the
+// inputs as hnm_sort128.
+template <int W>
+__device__ __forceinline__ void hnm_sort_lanes(float& v, int& ix) {
+  const int lane = hnm_lane();
+#pragma unroll
+  for (int k = 2; k <= W; k <<= 1)
+#pragma unroll
+    for (int j = k >> 1; j > 0; j >>= 1) hnm_cx_rt(j, v, ix, k == W || (lane & k) == 0);
+}
+
 // Wave-wide bitonic sort of 128 (value, index) pairs, two per lane (slot e = lane + 64 r:
 // (v0, i0) is slot lane, (v1, i1) slot lane + 64), into (value desc, index asc) order --
-// slot 0 = best.  28 compare-exchange steps of one shfl_xor each; no serial inserts.  The
-// order must be total on the inputs: distinct indices, no NaN (callers check).
+// slot 0 = best.  28 compare-exchange steps of one lane exchange each (hnm_xor_lane: DPP /
+// permlane, no LDS); no serial inserts.  The order must be total on the inputs: distinct
+// indices, no NaN (callers check).
 __device__ __forceinline__ void hnm_sort128(float& v0, int& i0, float& v1, int& i1) {
   const int lane = hnm_lane();
 #pragma unroll
@@ -133,19 +225,10 @@ __device__ __forceinline__ void hnm_sort128(float& v0, int& i0, float& v1, int& 
         }
         continue;
       }
-      const bool lower = (lane & j) == 0;
 #pragma unroll
       for (int r = 0; r < 2; ++r) {
-        float& v = r ? v1 : v0;
-        int& ix = r ? i1 : i0;
         const int e = lane + 64 * r;
-        const bool up = (e & k) == 0;       // this block is ordered best-first
-        const float pv = __shfl_xor(v, j);
-        const int pi = __shfl_xor(ix, j);
-        const bool pb = hnm_better(pv, pi, v, ix);  // partner ranks before mine
-        const bool take = (lower == up) ? pb : !pb;  // lower slot of an up block keeps the better
-        v = take ? pv : v;
-        ix = take ? pi : ix;
+        hnm_cx_rt(j, r ? v1 : v0, r ? i1 : i0, (e & k) == 0);  // up: block ordered best-first
       }
     }
   }

@@ -951,9 +951,7 @@ struct Top4 {
   __device__ float kth(int K, int lane) {
     float kv = -__builtin_inff();
     for (int r = 0; r < K; ++r) {
-      float m = t0;
-#pragma unroll
-      for (int o = 32; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+      const float m = hnm_wave_max(t0);
       kv = m;
       if (m == -__builtin_inff()) break;  // wave-uniform
       const int wl = __builtin_ctzll(__ballot(t0 == m));
@@ -1019,9 +1017,7 @@ __global__ __launch_bounds__(1024) void cert_gate_kernel(
   for (int i = 0; i < 2; ++i) {  // each wave's K best survivors, descending
     Top4& L = i ? t : c;
     for (int q = 0; q < K; ++q) {
-      float m = L.t0;
-#pragma unroll
-      for (int o = 32; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+      const float m = hnm_wave_max(L.t0);
       if (lane == 0) wl[i][w][q] = m;
       if (m == -__builtin_inff()) {
         for (int z = q + 1 + lane; z < K; z += 64) wl[i][w][z] = -__builtin_inff();
