@@ -640,7 +640,8 @@ __global__ __launch_bounds__(256) void wdc_params_kernel(hnm_widedeep_weights w,
                                                          float* __restrict__ v2,
                                                          float* __restrict__ b2s,
                                                          WdCertParams* prm,
-                                                         float* __restrict__ v1o) {
+                                                         float* __restrict__ v1o,
+                                                         float* __restrict__ v2o) {
   __shared__ float sv2[256];
   __shared__ float red[8][4];
   __shared__ float bc[8];
@@ -670,6 +671,7 @@ __global__ __launch_bounds__(256) void wdc_params_kernel(hnm_widedeep_weights w,
     }
     sv2[jx] = v;
     v2[jx] = v;
+    v2o[jx] = v;  // before the dropped-pass terms (the re-scoring cascade's three-pass tile)
     sv2b = fmaf(v, fabsf(p.b2p[jx]), sv2b);
   }
   for (int m = tid; m < NOB * 32; m += 256) {
@@ -1502,30 +1504,195 @@ struct WdRescoreArgs {
   int64_t B;
   int NP, K, cap;
   const float* Lk;   // [B, K] merged lower-bound lists (slot K-1 = L_u)
-  const int32_t* segi;
-  const float* segu;
+  int32_t* segi;     // [B, NP * cap] the scan's segments; wdc_collect compacts each row's
+  float* segu;       //   survivors to its front (items, then the refined upper bounds)
+  float* segl;       // [B, NP * cap] the survivors' refined lower bounds
   const int* cnt;
+  int* ns;           // [B] survivors of each row; -1: the row takes the exact kernel
+  int* toff;         // [B + 1] exclusive prefix of the rows' refining tiles (toff[B] = total)
   int32_t* fbrows;   // rows that take the exact kernel
   int* nfb;
   float* ov;
   int64_t* oi;
-  unsigned long long* stats;  // HNM_OPT_STATS: rows, candidates re-scored, fallback rows
+  unsigned long long* stats;  // HNM_OPT_STATS: rows, candidates re-scored in fp32, fallback rows
+  // the refining stage (three-pass split-f16 tile, wd_tile_f16x3)
+  const wh8* W2hl;
+  const wh8* W3hl;
+  const float* v1p;  // [K1P] plain v1 (no dropped-pass terms)
+  const float* v2p;  // [RB2*32] plain v2
+  const float* b2s;  // [RB2*32] b2' s2
 };
 
-// One wave per row: survivors (ub >= L_u) of the row's segments, 32 at a time, through
-// wd_tile_fp32 -- the exact kernel's arithmetic -- into a wave top-K.
-template <int RB2, int OB>
-__global__ __launch_bounds__(256, 1) void wdc_rescore_kernel(WdRescoreArgs R) {
-  __shared__ int stage[4][96];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5, j = lane & 31;
-  const int64_t b = (int64_t)blockIdx.x * 4 + wave;
-  if (b >= R.B) return;  // no block-level barriers below
-  const int K = R.K;
-  const float Lu = R.Lk[b * K + K - 1];
+// Refined certified score of the re-scoring cascade (round 5): one user against the 32 gathered
+// items of a tile (lane (j, h): item j), both layers as three split-f16 MFMA passes
+// (W_hi x_hi + W_hi x_lo + W_lo x_hi; the dropped W_lo x_lo is 2^-22 relative), fp32
+// accumulation -- the configuration the header's g1 / g2 constants were derived for, so the
+// bound there holds with the PLAIN v1 / v2 (the scan's one-pass vectors carry dropped-pass
+// terms): |approx - exact| <= e.  About 3/16 of the fp32 tile's matrix-pipe time.  Layer 2 in
+// RB2 / G2 passes over k of G2 row blocks each (the x operands re-formed per pass), each pass's
+// x2 feeding layer 3 at once: G2 = 4 keeps the tile within 256 registers (two waves a SIMD).
+//   psr: the user's layer-1 row scaled by s1, offset 8 h (LDS); qrow: item j's row + 8 h
+//   (global); v1s / b2l / v2l / b3l / wdl: LDS copies.  Returns (score - cu - wI) in every lane
+//   and the bound's three dot products (real units, summed over the halves).
+template <int RB2, int OB, int G2>
+__device__ __forceinline__ void wd_tile_f16x3(const float* __restrict__ psr,
+                                              const float* __restrict__ qrow, int KB,
+                                              __amdgpu_buffer_rsrc_t w2rs,
+                                              __amdgpu_buffer_rsrc_t w3rs,
+                                              const float* __restrict__ v1s,
+                                              const float* __restrict__ b2l,
+                                              const float* __restrict__ v2l,
+                                              const float* __restrict__ b3l,
+                                              const float* __restrict__ wdl, float s1, float c2,
+                                              float c3, float inv_s2, int lane, int h,
+                                              float& fv, float& b1, float& b2, float& b3) {
+  constexpr int NOB = OB > 0 ? OB : 1;
+  f32x16 acc3[NOB];
+#pragma unroll
+  for (int ob = 0; ob < NOB; ++ob)
+    acc3[ob] = f32x16{0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  float bx1 = 0.f, bx2 = 0.f, fin = 0.f, bx3 = 0.f;
+  auto qload = [&](int kb, float4 (&q)[2]) {
+    q[0] = *reinterpret_cast<const float4*>(qrow + 16 * kb);
+    q[1] = *reinterpret_cast<const float4*>(qrow + 16 * kb + 4);
+  };
+#pragma unroll 1
+  for (int g = 0; g < RB2 / G2; ++g) {
+    f32x16 acc2[G2];
+#pragma unroll
+    for (int gi = 0; gi < G2; ++gi)
+      acc2[gi] = f32x16{0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    // item rows two k steps ahead (gathered rows); each weight fragment is reloaded for step
+    // kb + 1 right after step kb's MFMAs read it (one register set, a whole step of lead)
+    wfr w[G2][2];
+#pragma unroll
+    for (int gi = 0; gi < G2; ++gi)
+#pragma unroll
+      for (int hl = 0; hl < 2; ++hl) w[gi][hl] = wd_frag(w2rs, lane, ((g * G2 + gi) * KB * 2 + hl) * 1024);
+    auto step = [&](int kb, const float4 (&q)[2]) {
+      const float4 p0 = *reinterpret_cast<const float4*>(psr + 16 * kb);
+      const float4 p1 = *reinterpret_cast<const float4*>(psr + 16 * kb + 4);
+      const float pv[8] = {p0.x, p0.y, p0.z, p0.w, p1.x, p1.y, p1.z, p1.w};
+      const float qv[8] = {q[0].x, q[0].y, q[0].z, q[0].w, q[1].x, q[1].y, q[1].z, q[1].w};
+      float x[8];
+#pragma unroll
+      for (int t = 0; t < 8; ++t) x[t] = fmaxf(fmaf(qv[t], s1, pv[t]), 0.f);  // s1 x1 exactly
+      if (g == 0) {  // the layer-2 bound term, once
+        const float4 w0 = *reinterpret_cast<const float4*>(v1s + 16 * kb + 8 * h);
+        const float4 w1 = *reinterpret_cast<const float4*>(v1s + 16 * kb + 8 * h + 4);
+        const float vv[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+#pragma unroll
+        for (int t = 0; t < 8; ++t) bx1 = fmaf(vv[t], x[t], bx1);
+      }
+      wh8 xh, xl;
+      wd_split8(x, xh, xl);
+      const int kn = kb + 1 < KB ? kb + 1 : kb;
+#pragma unroll
+      for (int gi = 0; gi < G2; ++gi) {
+        acc2[gi] = wd_mfma16(wd_h(w[gi][0]), xh, acc2[gi]);
+        acc2[gi] = wd_mfma16(wd_h(w[gi][0]), xl, acc2[gi]);
+        acc2[gi] = wd_mfma16(wd_h(w[gi][1]), xh, acc2[gi]);
+#pragma unroll
+        for (int hl = 0; hl < 2; ++hl)
+          w[gi][hl] = wd_frag(w2rs, lane, (((g * G2 + gi) * KB + kn) * 2 + hl) * 1024);
+      }
+    };
+    {
+      // item rows QD k steps ahead: four register sets in rotation (the gathered rows come from
+      // MALL / HBM; two steps of lead left the MFMAs waiting on them)
+      constexpr int QD = 4;
+      float4 qr[QD][2];
+      auto kc = [&](int k) { return k < KB ? k : KB - 1; };
+#pragma unroll
+      for (int d = 0; d < QD; ++d) qload(kc(d), qr[d]);
+      int kb = 0;
+      for (; kb + QD <= KB; kb += QD) {
+#pragma unroll
+        for (int d = 0; d < QD; ++d) {
+          step(kb + d, qr[d]);
+          qload(kc(kb + d + QD), qr[d]);
+        }
+      }
+#pragma unroll
+      for (int d = 0; d < QD; ++d)
+        if (kb + d < KB) step(kb + d, qr[d]);
+    }
+    // x2 = relu(D2 + b2') in s2 units, its bound term, then its layer-3 passes (or the final
+    // dot of a two-layer tower)
+#pragma unroll
+    for (int gi = 0; gi < G2; ++gi) {
+      const int rb = g * G2 + gi;
+      float y[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = rb * 32 + mfma32_row(r, h);
+        y[r] = fmaxf(fmaf(acc2[gi][r], c2, b2l[row]), 0.f);
+        bx2 = fmaf(v2l[row], y[r], bx2);
+        if (OB == 0) fin = fmaf(y[r], wdl[row], fin);
+      }
+      if constexpr (OB > 0) {
+#pragma unroll
+        for (int half2 = 0; half2 < 2; ++half2) {
+          wh8 yh, yl;
+          wd_split8(&y[8 * half2], yh, yl);
+          const int kb3 = 2 * rb + half2;
+#pragma unroll
+          for (int ob = 0; ob < NOB; ++ob) {
+            const int q = (ob * 2 * RB2 + kb3) * 2;
+            const wh8 bh = wd_h(wd_frag(w3rs, lane, q * 1024));
+            const wh8 bl = wd_h(wd_frag(w3rs, lane, (q + 1) * 1024));
+            acc3[ob] = wd_mfma16(bh, yh, acc3[ob]);
+            acc3[ob] = wd_mfma16(bh, yl, acc3[ob]);
+            acc3[ob] = wd_mfma16(bl, yh, acc3[ob]);
+          }
+        }
+      }
+    }
+  }
+  if constexpr (OB > 0) {
+    float fp[4] = {0.f, 0.f, 0.f, 0.f}, bp[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ob = 0; ob < NOB; ++ob)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int o = ob * 32 + mfma32_row(r, h);
+        const float z = fmaxf(fmaf(acc3[ob][r], c3, b3l[o]), 0.f);
+        fp[r & 3] = fmaf(z, wdl[o], fp[r & 3]);
+        bp[r & 3] = fmaf(fabsf(wdl[o]), z, bp[r & 3]);
+      }
+    fin = (fp[0] + fp[1]) + (fp[2] + fp[3]);
+    bx3 = (bp[0] + bp[1]) + (bp[2] + bp[3]);
+  } else {
+    fin *= inv_s2;
+  }
+  fv = hnm_sum_halves(fin);
+  b1 = hnm_sum_halves(bx1) / s1;
+  b2 = hnm_sum_halves(bx2) * inv_s2;
+  b3 = hnm_sum_halves(bx3);
+}
+
+// The re-scoring cascade (round 5; round 4 sent all ~1,145 scan survivors a row through the
+// fp32 tile: 15.7 ms a batch):
+//   wdc_collect_kernel  one wave per row: fallback rows queued; the row's scan survivors
+//                       (ub >= L_u) compacted to the front of its segment area, their count;
+//   wdc_tiles_kernel    exclusive prefix of the rows' 32-item refining tiles (one block);
+//   wdc_refine_kernel   a fixed grid, each wave a contiguous run of tiles (balanced whatever
+//                       the rows' survivor counts): wd_tile_f16x3 -> refined bounds
+//                       lb2 <= exact <= ub2 per survivor;
+//   wdc_rescore_kernel  one wave per row: L2 = the K-th best lb2 (a lower bound of the row's
+//                       exact K-th best), then the survivors with ub2 >= max(L2, L_u) -- every
+//                       item that can be in the top-K -- through wd_tile_fp32, the exact
+//                       kernel's arithmetic, into a wave top-K: bitwise the exact path's output.
+__global__ __launch_bounds__(256) void wdc_collect_kernel(WdRescoreArgs R) {
+  const int lane = threadIdx.x & 63;
+  const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (b >= R.B) return;
+  const float Lu = R.Lk[b * R.K + R.K - 1];
   bool fb = R.prm->bad || !(Lu > -__builtin_inff());
   for (int p = 0; p < R.NP; ++p) fb |= R.cnt[b * R.NP + p] > R.cap;
   if (fb) {
     if (lane == 0) {
+      R.ns[b] = -1;
       R.fbrows[atomicAdd(R.nfb, 1)] = (int32_t)b;
       if (R.stats) {
         atomicAdd(R.stats + 0, 1ull);
@@ -1534,14 +1701,153 @@ __global__ __launch_bounds__(256, 1) void wdc_rescore_kernel(WdRescoreArgs R) {
     }
     return;
   }
-  int nsurv = 0;
+  // in place: the write position never passes the read position, and a chunk's loads are
+  // issued before its stores
+  const int64_t rowbase = b * R.NP * (int64_t)R.cap;
+  int no = 0;
+  for (int p = 0; p < R.NP; ++p) {
+    const int n = R.cnt[b * R.NP + p];
+    const int64_t base = rowbase + (int64_t)p * R.cap;
+    for (int c0 = 0; c0 < n; c0 += 64) {
+      const int e = c0 + lane;
+      const bool in = e < n;
+      const int32_t it = in ? R.segi[base + e] : 0;
+      const bool ok = in && R.segu[base + e] >= Lu;
+      const uint64_t m = __ballot(ok);
+      if (ok) R.segi[rowbase + no + __popcll(m & ((1ull << lane) - 1))] = it;
+      no += __popcll(m);
+    }
+  }
+  if (lane == 0) R.ns[b] = no;
+}
+
+__global__ __launch_bounds__(1024) void wdc_tiles_kernel(const int* __restrict__ ns, int64_t B,
+                                                         int* __restrict__ toff) {
+  __shared__ int wsum[16];
+  __shared__ int carry;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (tid == 0) carry = 0;
+  __syncthreads();
+  for (int64_t b0 = 0; b0 < B; b0 += 1024) {
+    const int64_t b = b0 + tid;
+    const int t = b < B ? (int)hnm_cdiv(std::max(ns[b], 0), WD_TILE) : 0;
+    int incl = t;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int v = __shfl_up(incl, o);
+      if (lane >= o) incl += v;
+    }
+    if (lane == 63) wsum[wave] = incl;
+    __syncthreads();
+    int before = carry;
+    for (int w = 0; w < wave; ++w) before += wsum[w];
+    if (b < B) toff[b] = before + incl - t;
+    __syncthreads();
+    if (tid == 1023) carry = before + incl;
+    __syncthreads();
+  }
+  if (tid == 0) toff[B] = carry;
+}
+
+template <int RB2, int OB>
+__global__ __launch_bounds__(256, 1) void wdc_refine_kernel(WdRescoreArgs R) {
+  constexpr int NOB = OB > 0 ? OB : 1, NL = OB > 0 ? OB : RB2;
+  constexpr int G2 = RB2;
+  extern __shared__ __attribute__((aligned(16))) float wsm[];
+  const int K1P = R.K1P, KB = K1P / 16;
+  float* const v1s = wsm;                  // [K1P]
+  float* const b2l = v1s + K1P;            // [RB2 * 32]
+  float* const v2l = b2l + RB2 * 32;       // [RB2 * 32]
+  float* const b3l = v2l + RB2 * 32;       // [NOB * 32]
+  float* const wdl = b3l + NOB * 32;       // [NL * 32]
+  float* const psm = wdl + NL * 32;        // [4][K1P] the wave's current user row, scaled by s1
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5, j = lane & 31;
+  for (int e = tid; e < K1P; e += 256) v1s[e] = R.v1p[e];
+  for (int e = tid; e < RB2 * 32; e += 256) {
+    b2l[e] = R.b2s[e];
+    v2l[e] = R.v2p[e];
+  }
+  for (int e = tid; e < NOB * 32; e += 256) b3l[e] = OB > 0 ? R.b3p[e] : 0.f;
+  for (int e = tid; e < NL * 32; e += 256) wdl[e] = R.wdp[e];
+  __syncthreads();  // the only block-level barrier
+  const WdCertParams& P = *R.prm;
+  const float s1 = P.s1, c2 = P.c2, c3 = P.c3, inv_s2 = P.inv_s2;
+  const float g1 = P.g1, g2 = P.g2, g3 = P.g3, g4 = P.g4, cbd = P.cb, absb = P.absb, rho = P.rho;
+  const __amdgpu_buffer_rsrc_t w2rs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)R.W2hl, 0, RB2 * KB * 2 * 1024, 0x00020000);
+  const __amdgpu_buffer_rsrc_t w3rs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)R.W3hl, 0, NOB * 2 * RB2 * 2 * 1024, 0x00020000);
+  // this wave's tiles: a contiguous run of the T tiles (rows in order)
+  const int64_t T = R.toff[R.B];
+  const int64_t nw = (int64_t)gridDim.x * 4, w = (int64_t)blockIdx.x * 4 + wave;
+  const int64_t t0 = T * w / nw, t1 = T * (w + 1) / nw;
+  if (t0 >= t1) return;
+  int64_t lo = 0, hi = R.B;  // the row holding tile t0: last b with toff[b] <= t0
+  while (hi - lo > 1) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (R.toff[mid] <= t0) lo = mid;
+    else hi = mid;
+  }
+  int64_t b = lo, cb = -1;
+  float* const ps = psm + wave * K1P;
+  float cub = 0.f;
+  for (int64_t t = t0; t < t1; ++t) {
+    while (R.toff[b + 1] <= t) ++b;  // rows without tiles are skipped
+    if (b != cb) {
+      __builtin_amdgcn_wave_barrier();
+      for (int e = lane; e < K1P; e += 64) ps[e] = R.Pu[b * K1P + e] * s1;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      cub = R.cu[b];
+      cb = b;
+    }
+    const int k = (int)(t - R.toff[b]);
+    const int nv = std::min(WD_TILE, R.ns[b] - WD_TILE * k);
+    const int64_t at = b * R.NP * (int64_t)R.cap + (int64_t)WD_TILE * k;
+    const bool ivalid = lane < 32 && j < nv;
+    const int it = R.segi[at + (j < nv ? j : 0)];
+    float fv, b1, b2, b3;
+    wd_tile_f16x3<RB2, OB, G2>(ps + 8 * h, R.Qi + (int64_t)it * K1P + 8 * h, KB, w2rs, w3rs, v1s,
+                               b2l, v2l, b3l, wdl, s1, c2, c3, inv_s2, lane, h, fv, b1, b2, b3);
+    const float wi = R.wI[it];
+    const float score = fv + cub + wi;
+    const float e = rho * (g1 * b1 + g2 * b2 + g3 * b3 +
+                           g4 * (fabsf(fv) + fabsf(cub) + fabsf(wi)) + cbd) + absb;
+    if (ivalid) {
+      R.segl[at + j] = score - e;
+      R.segu[at + j] = score + e;
+    }
+  }
+}
+
+template <int RB2, int OB>
+__global__ __launch_bounds__(256, 1) void wdc_rescore_kernel(WdRescoreArgs R) {
+  __shared__ int stage[4][96];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5, j = lane & 31;
+  const int64_t b = (int64_t)blockIdx.x * 4 + wave;
+  if (b >= R.B) return;  // no block-level barriers below
+  const int ns = R.ns[b];
+  if (ns < 0) return;  // queued for the exact kernel by wdc_collect
+  const int K = R.K;
+  const float Lu = R.Lk[b * K + K - 1];
+  const int64_t rowbase = b * R.NP * (int64_t)R.cap;
+  // L2: the K-th best refined lower bound (K distinct items)
+  WaveTopK<1> T2;
+  T2.init();
+  for (int c0 = 0; c0 < ns; c0 += 64) {
+    const int e = c0 + lane;
+    const bool in = e < ns;
+    T2.offer(in ? R.segl[rowbase + e] : -__builtin_inff(), in ? R.segi[rowbase + e] : 0, in, K);
+  }
+  const float thr = fmaxf(T2.thr_v, Lu);
   const int KS1 = R.K1P / 2, S4 = R.K1P / 8;
   const float cub = R.cu[b];
   const float* prow = R.Pu + b * R.K1P + h * KS1;
   int* st = stage[wave];
   WaveTopK<1> T;
   T.init();
-  int ns = 0;
+  int nsurv = 0, nst = 0;
   auto run_tile = [&](int nv) {
     const int it = st[j < nv ? j : 0];
     const float* qrow = R.Qi + (int64_t)it * R.K1P + h * KS1;
@@ -1551,33 +1857,29 @@ __global__ __launch_bounds__(256, 1) void wdc_rescore_kernel(WdRescoreArgs R) {
     const float score = fin + cub + (ivalid ? R.wI[it] : 0.f);
     T.offer(score, it, ivalid, K);
   };
-  for (int p = 0; p < R.NP; ++p) {
-    const int n = R.cnt[b * R.NP + p];
-    const int64_t base = (b * R.NP + p) * (int64_t)R.cap;
-    for (int c0 = 0; c0 < n; c0 += 64) {
-      const int e = c0 + lane;
-      const bool ok = e < n && R.segu[base + e] >= Lu;
-      const uint64_t m = __ballot(ok);
-      if (ok) st[ns + __popcll(m & ((1ull << lane) - 1))] = R.segi[base + e];
-      ns += __popcll(m);
-      nsurv += __popcll(m);
+  for (int c0 = 0; c0 < ns; c0 += 64) {
+    const int e = c0 + lane;
+    const bool ok = e < ns && R.segu[rowbase + e] >= thr;
+    const uint64_t m = __ballot(ok);
+    if (ok) st[nst + __popcll(m & ((1ull << lane) - 1))] = R.segi[rowbase + e];
+    nst += __popcll(m);
+    nsurv += __popcll(m);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    while (nst >= 32) {
+      run_tile(32);
+      const int rest = nst - 32;
+      const int mv = lane < rest ? st[32 + lane] : 0;
+      __builtin_amdgcn_wave_barrier();
+      if (lane < rest) st[lane] = mv;
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      while (ns >= 32) {
-        run_tile(32);
-        const int rest = ns - 32;
-        const int mv = lane < rest ? st[32 + lane] : 0;
-        __builtin_amdgcn_wave_barrier();
-        if (lane < rest) st[lane] = mv;
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        ns = rest;
-      }
+      nst = rest;
     }
   }
-  if (ns > 0) run_tile(ns);
+  if (nst > 0) run_tile(nst);
   T.store(R.ov + b * K, R.oi + b * K, K);
   if (R.stats && lane == 0) {
     atomicAdd(R.stats + 0, 1ull);
@@ -1832,6 +2134,7 @@ struct WdcWs {
   wh8* WBf;
   float* v1;
   float* v1o;
+  float* v2o;
   float* v2;
   float* b2s;
   float* part;
@@ -1842,6 +2145,9 @@ struct WdcWs {
   int32_t* segi;
   float* segu;
   int* cnt;
+  float* segl;
+  int* ns;
+  int* toff;
   int32_t* fbrows;
   int* nfb;
   float* fcv;
@@ -1877,6 +2183,7 @@ static size_t wdc_carve(const hnm_ctx* ctx, const WdPrep& pr, int64_t B, int64_t
   t.v1 = (float*)take((size_t)K1P * 4);
   t.v1o = (float*)take((size_t)K1P * 4);
   t.v2 = (float*)take((size_t)pr.RB2 * 32 * 4);
+  t.v2o = (float*)take((size_t)pr.RB2 * 32 * 4);
   t.b2s = (float*)take((size_t)pr.RB2 * 32 * 4);
   t.part = (float*)take((size_t)WDC_STAT_BLOCKS * 2 * 4);
   t.lbv = (float*)take((size_t)B * np * K * 4);
@@ -1886,6 +2193,9 @@ static size_t wdc_carve(const hnm_ctx* ctx, const WdPrep& pr, int64_t B, int64_t
   t.segi = (int32_t*)take((size_t)B * np * cap * 4);
   t.segu = (float*)take((size_t)B * np * cap * 4);
   t.cnt = (int*)take((size_t)B * np * 4);
+  t.segl = (float*)take((size_t)B * np * cap * 4);
+  t.ns = (int*)take((size_t)B * 4);
+  t.toff = (int*)take((size_t)(B + 1) * 4);
   t.fbrows = (int32_t*)take((size_t)B * 4);
   t.nfb = (int*)take(4);
   t.fcv = (float*)take((size_t)fbn * K * 4);
@@ -1906,7 +2216,7 @@ static hnm_status wdc_prepare(hnm_ctx* ctx, const hnm_widedeep_weights* w, const
   hipLaunchKernelGGL(wdc_stats_kernel, dim3(WDC_STAT_BLOCKS), dim3(256), 0, s, S.Pu,
                      B * S.K1P, S.Qi, I * S.K1P, c.part);
   hipLaunchKernelGGL(wdc_params_kernel, dim3(1), dim3(256), 0, s, *w, S.pr, c.part,
-                     WDC_STAT_BLOCKS, c.v1, c.v2, c.b2s, c.prm, c.v1o);
+                     WDC_STAT_BLOCKS, c.v1, c.v2, c.b2s, c.prm, c.v1o, c.v2o);
   hipLaunchKernelGGL(wdc_convert_kernel, dim3(256), dim3(256), 0, s, *w, S.pr, c.prm, c.W2hl,
                      c.W3hl);
   hipLaunchKernelGGL(wdc_boundfrag_kernel, dim3((unsigned)hnm_cdiv(S.K1P / 16 * 2 * 64, 256)),
@@ -1926,6 +2236,13 @@ static void wdc_launch_scan(hnm_ctx* ctx, dim3 grid, size_t lds, const WdScanArg
 
 template <int RB2, int OB>
 static void wdc_launch_rescore(hnm_ctx* ctx, dim3 grid, const WdRescoreArgs& r) {
+  constexpr int NOB = OB > 0 ? OB : 1, NL = OB > 0 ? OB : RB2;
+  hipLaunchKernelGGL(wdc_collect_kernel, grid, dim3(256), 0, ctx->stream, r);
+  hipLaunchKernelGGL(wdc_tiles_kernel, dim3(1), dim3(1024), 0, ctx->stream, r.ns, r.B, r.toff);
+  const size_t lds = (size_t)(5 * r.K1P + 2 * RB2 * 32 + NOB * 32 + NL * 32) * 4;
+  auto kern = wdc_refine_kernel<RB2, OB>;
+  (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  hipLaunchKernelGGL(kern, dim3(ctx->num_cus), dim3(256), lds, ctx->stream, r);
   hipLaunchKernelGGL((wdc_rescore_kernel<RB2, OB>), grid, dim3(256), 0, ctx->stream, r);
 }
 
@@ -2025,6 +2342,14 @@ static hnm_status wdc_topk(hnm_ctx* ctx, const hnm_widedeep_weights* w, const Wd
   r.ov = ov;
   r.oi = oi;
   r.stats = ctx->stats_on ? ctx->stats_dev : nullptr;
+  r.segl = c.segl;
+  r.ns = c.ns;
+  r.toff = c.toff;
+  r.W2hl = c.W2hl;
+  r.W3hl = c.W3hl;
+  r.v1p = c.v1o;
+  r.v2p = c.v2o;
+  r.b2s = c.b2s;
   dim3 grid((unsigned)hnm_cdiv(B, 4));
 #define WDC_CASE(R, O) \
   if (pr.RB2 == R && pr.OB == O) wdc_launch_rescore<R, O>(ctx, grid, r);
