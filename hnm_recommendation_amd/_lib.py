@@ -127,6 +127,8 @@ _SIGS = {
                                                _i64, _p]),
     "hnm_widedeep_prefilter_debug_f32": (_i32, [_p, C.POINTER(WideDeepWeights), _p, _i64, _p, _p,
                                                 _i64, _p]),
+    "hnm_widedeep_refine_debug_f32": (_i32, [_p, C.POINTER(WideDeepWeights), _p, _i64, _p, _p,
+                                                _i64, _p]),
     "hnm_mask_gather_csr": (_i32, [_p, _p, _p, _i64, _p, _i64, _i64, _i64, _i64, _p, _p]),
     "hnm_rank_metrics_f64": (_i32, [_p, _p, _i64, _i64, _p, C.c_int, _p, _p, _i64, _p, _p, _p,
                                     _p, _p]),

@@ -1521,6 +1521,10 @@ struct WdRescoreArgs {
   const float* v1p;  // [K1P] plain v1 (no dropped-pass terms)
   const float* v2p;  // [RB2*32] plain v2
   const float* b2s;  // [RB2*32] b2' s2
+  int64_t rstride;   // row stride of segi / segu / segl (NP * cap)
+  float* dbg_a;      // hnm_widedeep_refine_debug_f32: refined score / bound per item, [B, lda]
+  float* dbg_e;
+  int64_t lda;
 };
 
 // Refined certified score of the re-scoring cascade (round 5): one user against the 32 gathered
@@ -1618,29 +1622,56 @@ __device__ __forceinline__ void wd_tile_f16x3(const float* __restrict__ psr,
         if (kb + d < KB) step(kb + d, qr[d]);
     }
     // x2 = relu(D2 + b2') in s2 units, its bound term, then its layer-3 passes (or the final
-    // dot of a two-layer tower)
+    // dot of a two-layer tower).  Layer-3 fragments run W3D kb3 steps ahead in a ring of
+    // W3D + 1 register sets (the steps are unrolled: compile-time slots); bias / bound rows are
+    // read as float4 (rows 8 r4 + 4 h + 0..3 of a row block hold registers 4 r4 .. 4 r4 + 3).
+    constexpr int W3D = 2, NK3 = 2 * G2;
+    wfr w3b[W3D + 1][NOB][2];
+    auto w3load = [&](int k3) {  // k3: this pass's kb3 step (2 gi + half2)
+      const int kb3 = 2 * g * G2 + k3;
+#pragma unroll
+      for (int ob = 0; ob < NOB; ++ob)
+#pragma unroll
+        for (int hl = 0; hl < 2; ++hl)
+          w3b[k3 % (W3D + 1)][ob][hl] = wd_frag(w3rs, lane, ((ob * 2 * RB2 + kb3) * 2 + hl) * 1024);
+    };
+    if constexpr (OB > 0) {
+#pragma unroll
+      for (int k3 = 0; k3 < W3D && k3 < NK3; ++k3) w3load(k3);
+    }
 #pragma unroll
     for (int gi = 0; gi < G2; ++gi) {
       const int rb = g * G2 + gi;
       float y[16];
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = rb * 32 + mfma32_row(r, h);
-        y[r] = fmaxf(fmaf(acc2[gi][r], c2, b2l[row]), 0.f);
-        bx2 = fmaf(v2l[row], y[r], bx2);
-        if (OB == 0) fin = fmaf(y[r], wdl[row], fin);
+      for (int r4 = 0; r4 < 4; ++r4) {
+        const float4 bb = *reinterpret_cast<const float4*>(b2l + rb * 32 + 8 * r4 + 4 * h);
+        const float4 vq = *reinterpret_cast<const float4*>(v2l + rb * 32 + 8 * r4 + 4 * h);
+        const float bq[4] = {bb.x, bb.y, bb.z, bb.w}, vv[4] = {vq.x, vq.y, vq.z, vq.w};
+        float wq[4] = {0.f, 0.f, 0.f, 0.f};
+        if (OB == 0) {
+          const float4 w4 = *reinterpret_cast<const float4*>(wdl + rb * 32 + 8 * r4 + 4 * h);
+          wq[0] = w4.x; wq[1] = w4.y; wq[2] = w4.z; wq[3] = w4.w;
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int r = 4 * r4 + e;
+          y[r] = fmaxf(fmaf(acc2[gi][r], c2, bq[e]), 0.f);
+          bx2 = fmaf(vv[e], y[r], bx2);
+          if (OB == 0) fin = fmaf(y[r], wq[e], fin);
+        }
       }
       if constexpr (OB > 0) {
 #pragma unroll
         for (int half2 = 0; half2 < 2; ++half2) {
+          const int k3 = 2 * gi + half2;
+          if (k3 + W3D < NK3) w3load(k3 + W3D);
           wh8 yh, yl;
           wd_split8(&y[8 * half2], yh, yl);
-          const int kb3 = 2 * rb + half2;
 #pragma unroll
           for (int ob = 0; ob < NOB; ++ob) {
-            const int q = (ob * 2 * RB2 + kb3) * 2;
-            const wh8 bh = wd_h(wd_frag(w3rs, lane, q * 1024));
-            const wh8 bl = wd_h(wd_frag(w3rs, lane, (q + 1) * 1024));
+            const wh8 bh = wd_h(w3b[k3 % (W3D + 1)][ob][0]);
+            const wh8 bl = wd_h(w3b[k3 % (W3D + 1)][ob][1]);
             acc3[ob] = wd_mfma16(bh, yh, acc3[ob]);
             acc3[ob] = wd_mfma16(bh, yl, acc3[ob]);
             acc3[ob] = wd_mfma16(bl, yh, acc3[ob]);
@@ -1654,11 +1685,16 @@ __device__ __forceinline__ void wd_tile_f16x3(const float* __restrict__ psr,
 #pragma unroll
     for (int ob = 0; ob < NOB; ++ob)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int o = ob * 32 + mfma32_row(r, h);
-        const float z = fmaxf(fmaf(acc3[ob][r], c3, b3l[o]), 0.f);
-        fp[r & 3] = fmaf(z, wdl[o], fp[r & 3]);
-        bp[r & 3] = fmaf(fabsf(wdl[o]), z, bp[r & 3]);
+      for (int r4 = 0; r4 < 4; ++r4) {
+        const float4 b3 = *reinterpret_cast<const float4*>(b3l + ob * 32 + 8 * r4 + 4 * h);
+        const float4 w4 = *reinterpret_cast<const float4*>(wdl + ob * 32 + 8 * r4 + 4 * h);
+        const float bq[4] = {b3.x, b3.y, b3.z, b3.w}, wq[4] = {w4.x, w4.y, w4.z, w4.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float z = fmaxf(fmaf(acc3[ob][4 * r4 + e], c3, bq[e]), 0.f);
+          fp[e] = fmaf(z, wq[e], fp[e]);
+          bp[e] = fmaf(fabsf(wq[e]), z, bp[e]);
+        }
       }
     fin = (fp[0] + fp[1]) + (fp[2] + fp[3]);
     bx3 = (bp[0] + bp[1]) + (bp[2] + bp[3]);
@@ -1703,7 +1739,7 @@ __global__ __launch_bounds__(256) void wdc_collect_kernel(WdRescoreArgs R) {
   }
   // in place: the write position never passes the read position, and a chunk's loads are
   // issued before its stores
-  const int64_t rowbase = b * R.NP * (int64_t)R.cap;
+  const int64_t rowbase = b * R.rstride;
   int no = 0;
   for (int p = 0; p < R.NP; ++p) {
     const int n = R.cnt[b * R.NP + p];
@@ -1804,7 +1840,7 @@ __global__ __launch_bounds__(256, 1) void wdc_refine_kernel(WdRescoreArgs R) {
     }
     const int k = (int)(t - R.toff[b]);
     const int nv = std::min(WD_TILE, R.ns[b] - WD_TILE * k);
-    const int64_t at = b * R.NP * (int64_t)R.cap + (int64_t)WD_TILE * k;
+    const int64_t at = b * R.rstride + (int64_t)WD_TILE * k;
     const bool ivalid = lane < 32 && j < nv;
     const int it = R.segi[at + (j < nv ? j : 0)];
     float fv, b1, b2, b3;
@@ -1815,8 +1851,13 @@ __global__ __launch_bounds__(256, 1) void wdc_refine_kernel(WdRescoreArgs R) {
     const float e = rho * (g1 * b1 + g2 * b2 + g3 * b3 +
                            g4 * (fabsf(fv) + fabsf(cub) + fabsf(wi)) + cbd) + absb;
     if (ivalid) {
-      R.segl[at + j] = score - e;
-      R.segu[at + j] = score + e;
+      if (R.dbg_a) {
+        R.dbg_a[b * R.lda + it] = score;
+        R.dbg_e[b * R.lda + it] = e;
+      } else {
+        R.segl[at + j] = score - e;
+        R.segu[at + j] = score + e;
+      }
     }
   }
 }
@@ -1831,7 +1872,7 @@ __global__ __launch_bounds__(256, 1) void wdc_rescore_kernel(WdRescoreArgs R) {
   if (ns < 0) return;  // queued for the exact kernel by wdc_collect
   const int K = R.K;
   const float Lu = R.Lk[b * K + K - 1];
-  const int64_t rowbase = b * R.NP * (int64_t)R.cap;
+  const int64_t rowbase = b * R.rstride;
   // L2: the K-th best refined lower bound (K distinct items)
   WaveTopK<1> T2;
   T2.init();
@@ -2235,14 +2276,19 @@ static void wdc_launch_scan(hnm_ctx* ctx, dim3 grid, size_t lds, const WdScanArg
 }
 
 template <int RB2, int OB>
-static void wdc_launch_rescore(hnm_ctx* ctx, dim3 grid, const WdRescoreArgs& r) {
+static void wdc_launch_refine(hnm_ctx* ctx, const WdRescoreArgs& r) {
   constexpr int NOB = OB > 0 ? OB : 1, NL = OB > 0 ? OB : RB2;
-  hipLaunchKernelGGL(wdc_collect_kernel, grid, dim3(256), 0, ctx->stream, r);
   hipLaunchKernelGGL(wdc_tiles_kernel, dim3(1), dim3(1024), 0, ctx->stream, r.ns, r.B, r.toff);
   const size_t lds = (size_t)(5 * r.K1P + 2 * RB2 * 32 + NOB * 32 + NL * 32) * 4;
   auto kern = wdc_refine_kernel<RB2, OB>;
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   hipLaunchKernelGGL(kern, dim3(ctx->num_cus), dim3(256), lds, ctx->stream, r);
+}
+
+template <int RB2, int OB>
+static void wdc_launch_rescore(hnm_ctx* ctx, dim3 grid, const WdRescoreArgs& r) {
+  hipLaunchKernelGGL(wdc_collect_kernel, grid, dim3(256), 0, ctx->stream, r);
+  wdc_launch_refine<RB2, OB>(ctx, r);
   hipLaunchKernelGGL((wdc_rescore_kernel<RB2, OB>), grid, dim3(256), 0, ctx->stream, r);
 }
 
@@ -2343,6 +2389,9 @@ static hnm_status wdc_topk(hnm_ctx* ctx, const hnm_widedeep_weights* w, const Wd
   r.oi = oi;
   r.stats = ctx->stats_on ? ctx->stats_dev : nullptr;
   r.segl = c.segl;
+  r.rstride = c.np * (int64_t)c.cap;
+  r.dbg_a = r.dbg_e = nullptr;
+  r.lda = 0;
   r.ns = c.ns;
   r.toff = c.toff;
   r.W2hl = c.W2hl;
@@ -2446,6 +2495,78 @@ extern "C" hnm_status hnm_widedeep_prefilter_debug_f32(hnm_ctx* ctx,
   st = wdc_prepare(ctx, w, S, B, c);
   if (st) return st;
   return wdc_scan(ctx, w, S, B, nullptr, nullptr, 1, c, WDC_DEBUG, approx, bound, lda);
+}
+
+// every row's item list = the whole catalogue (the refine stage's debug input)
+__global__ void wdc_debug_rows_kernel(int32_t* __restrict__ segi, int* __restrict__ ns, int64_t B,
+                                      int64_t I) {
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (e < B * I) segi[e] = (int32_t)(e % I);
+  if (e < B) ns[e] = (int)I;
+}
+
+extern "C" hnm_status hnm_widedeep_refine_debug_f32(hnm_ctx* ctx, const hnm_widedeep_weights* w,
+                                                    const int64_t* user_ids, int64_t B,
+                                                    const float* user_features, float* approx,
+                                                    int64_t lda, float* bound) {
+  HNM_REQUIRE(ctx && user_ids && approx && bound && w && lda >= w->num_items, HNM_EINVAL,
+              "widedeep_refine_debug: bad argument");
+  WdSetup S;
+  hnm_status st = wd_shape(w, &S.pr);
+  if (st) return st;
+  HNM_REQUIRE(wdc_eligible(ctx, S.pr, w->num_items, 1, true), HNM_EUNSUPPORTED,
+              "widedeep_refine_debug: tower shape not covered by the certified scan");
+  if (B <= 0) return HNM_OK;
+  const int64_t I = w->num_items;
+  HNM_REQUIRE(B * I < ((int64_t)1 << 31), HNM_EINVAL, "widedeep_refine_debug: B * I >= 2^31");
+  const size_t cb = wdc_carve(ctx, S.pr, B, I, 1, nullptr, nullptr);
+  const size_t lb = hnm_align((size_t)B * I * 4) + hnm_align((size_t)B * 4) + hnm_align((size_t)(B + 1) * 4);
+  st = wd_setup(ctx, w, user_ids, B, user_features, cb + lb, &S);
+  if (st) return st;
+  WdcWs c;
+  wdc_carve(ctx, S.pr, B, I, 1, S.extra, &c);
+  st = wdc_prepare(ctx, w, S, B, c);
+  if (st) return st;
+  char* x = (char*)S.extra + cb;
+  int32_t* segi = (int32_t*)x;
+  int* ns = (int*)(x + hnm_align((size_t)B * I * 4));
+  int* toff = (int*)(x + hnm_align((size_t)B * I * 4) + hnm_align((size_t)B * 4));
+  hipLaunchKernelGGL(wdc_debug_rows_kernel, dim3((unsigned)hnm_cdiv(B * I, 256)), dim3(256), 0,
+                     ctx->stream, segi, ns, B, I);
+  const WdPrep& pr = S.pr;
+  WdRescoreArgs r{};
+  r.Pu = S.Pu;
+  r.Qi = S.Qi;
+  r.K1P = S.K1P;
+  r.b3p = pr.b3p;
+  r.wdp = pr.wdp;
+  r.cu = S.cu;
+  r.wI = w->wide_item;
+  r.prm = c.prm;
+  r.B = B;
+  r.segi = segi;
+  r.ns = ns;
+  r.toff = toff;
+  r.W2hl = c.W2hl;
+  r.W3hl = c.W3hl;
+  r.v1p = c.v1o;
+  r.v2p = c.v2o;
+  r.b2s = c.b2s;
+  r.rstride = I;
+  r.dbg_a = approx;
+  r.dbg_e = bound;
+  r.lda = lda;
+#define WDC_CASE(R, O) \
+  if (pr.RB2 == R && pr.OB == O) wdc_launch_refine<R, O>(ctx, r);
+  WDC_CASE(8, 4)
+  WDC_CASE(4, 2)
+  WDC_CASE(2, 1)
+  WDC_CASE(1, 1)
+  WDC_CASE(1, 0)
+  WDC_CASE(2, 0)
+#undef WDC_CASE
+  HNM_LAUNCH_CHECK();
+  return HNM_OK;
 }
 
 extern "C" hnm_status hnm_widedeep_pair_scores_ex_f32(hnm_ctx* ctx, const hnm_widedeep_weights* w,

@@ -390,6 +390,14 @@ hnm_status hnm_widedeep_prefilter_debug_f32(hnm_ctx* ctx, const hnm_widedeep_wei
                                             const int64_t* user_ids, int64_t B,
                                             const float* user_features, float* approx,
                                             int64_t lda, float* bound);
+/* The re-scoring cascade's refining stage (round 5) over the WHOLE catalogue: approx[b*lda + i]
+ * = the three-pass split-f16 score of (user b, item i), bound[b*lda + i] its certified bound
+ * (|approx - exact| <= bound, exact = hnm_widedeep_pair_scores_f32's arithmetic); the top-K path
+ * runs it only on the scan's survivors.  Diagnostics / tests; B * num_items < 2^31. */
+hnm_status hnm_widedeep_refine_debug_f32(hnm_ctx* ctx, const hnm_widedeep_weights* w,
+                                         const int64_t* user_ids, int64_t B,
+                                         const float* user_features, float* approx, int64_t lda,
+                                         float* bound);
 
 /* ---- a11: batch mask from a device-resident history CSR --------------------------------
  * The purchase-history filter (serve.py:350-352; the filter_items loop of every recommend,
