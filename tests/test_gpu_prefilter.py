@@ -212,6 +212,24 @@ def test_dot_prefilter_identical(d, bias, B):
     assert rows == B and fallback == 0
 
 
+@pytest.mark.parametrize("B,I,k", [(32768, 13192, 12), (20000, 8200, 12), (50000, 9000, 40)])
+def test_dot_prefilter_many_rows_small_shard(B, I, k):
+    """An 8-rank item shard's shape on one GPU (round 5): many rows over few items, so the
+    sample K-th pops 2 or 4 rows per wave (sample_kth_kernel<R>, lossless at <= 4 columns a
+    lane) and most rows re-score a handful of candidates in one sorting round
+    (dcert_rescore_kernel's 16 / 32 / 64-lane sort) -- bitwise the exact scan's top-K."""
+    ut, it, b = dot_tables(64, U=60000, I=I, seed=7, bias=True)
+    ids = torch.from_numpy(syn.user_batch(ut.shape[0], B, seed=13)).to(DEV)
+    ub, ib, cb = b
+    (ev, ei), (pv, pi), stats = dot_both(ut, ids, it, k, ub=ub, ib=ib, cb=cb)
+    assert np.array_equal(ei, pi)
+    assert np.array_equal(ev.view(np.uint32), pv.view(np.uint32))
+    rows, cands, fallback = stats
+    print(f"dot B={B} I={I} k={k}: candidates/row {cands / max(rows - fallback, 1):.1f}, "
+          f"fallback {fallback}")
+    assert rows == B
+
+
 def test_dot_prefilter_masks_ties_fallback():
     d, I = 64, 30000
     ut, it, _ = dot_tables(d, U=2000, I=I, seed=5)
