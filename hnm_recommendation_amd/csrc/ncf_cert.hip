@@ -442,6 +442,7 @@ struct ScanArgs {
   const float* tau;  // [B] scaled thresholds (THRESH)
   int* cnt;          // [B, NP] appended counts (THRESH)
   int32_t* buf;      // [B, NP, capp] appended item ids (THRESH)
+  float* segd;       // [B, NP, capp] their test values approx + e_i - tau (THRESH)
   int capp;
   float* dense;      // [B, ldo]
   float* dense2;     // [B, ldo] (DEBUG)
@@ -553,6 +554,14 @@ __global__ __launch_bounds__(256, HNM_SCAN_OCC) void ncf16_scan_kernel(ScanArgs 
     nm = mpos < mend ? A.midx[mpos] : INT_BIG;
   }
   int32_t* seg = MODE == SCAN_THRESH ? A.buf + ((u0 * A.NP) + p) * (int64_t)A.capp : nullptr;
+  // the wave's 32 rows of candidate ids / test values (THRESH): buffer resources over the rows'
+  // segments, partition p's slots at row * segstride + slot (NP * capp * 128 < 2^31: cert_shape)
+  const __amdgpu_buffer_rsrc_t segrs = __builtin_amdgcn_make_buffer_rsrc(
+      MODE == SCAN_THRESH ? (void*)seg : (void*)A.buf, 0,
+      MODE == SCAN_THRESH ? (int)(32 * (int64_t)A.NP * A.capp * 4) : 0, 0x00020000);
+  const __amdgpu_buffer_rsrc_t segdrs = __builtin_amdgcn_make_buffer_rsrc(
+      MODE == SCAN_THRESH ? (void*)(A.segd + ((u0 * A.NP) + p) * (int64_t)A.capp) : (void*)A.buf,
+      0, MODE == SCAN_THRESH ? (int)(32 * (int64_t)A.NP * A.capp * 4) : 0, 0x00020000);
   const int64_t segstride = (int64_t)A.NP * A.capp;  // next user's segment
 
   const int64_t ntiles = part_end > part_start ? hnm_cdiv(part_end - part_start, TILE) : 0;
@@ -629,6 +638,8 @@ __global__ __launch_bounds__(256, HNM_SCAN_OCC) void ncf16_scan_kernel(ScanArgs 
         // folded test term gmf + sgn * e_i - tau (sgn = +1 for the threshold test, -1 for the
         // sample's lower bound)
         constexpr float sgn = MODE == SCAN_THRESH ? 1.f : -1.f;
+        // (measured, round 5: the same stores from one lane base + immediate offsets -- 6 fewer
+        // VGPRs -- scheduled the pair loop's LDS reads differently, +1-2 % scan time)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int row = mfma32_row(r, h);
@@ -729,11 +740,26 @@ __global__ __launch_bounds__(256, HNM_SCAN_OCC) void ncf16_scan_kernel(ScanArgs 
             m &= ~((uint64_t)mba | ((uint64_t)mbb << 32));
           }
           if (m) {
-            const bool pass = (m >> lane) & 1;
-            const unsigned mh = (unsigned)(m >> (32 * h));
+            // lane c < 16 holds d[0..3] = the test values of (a, c), (a, c + 16), (b, c),
+            // (b, c + 16): it appends its passing pairs itself -- the id and, for the
+            // re-scoring's best-first order, the test value -- at the slot the pair's rank in the
+            // pass mask gives (no cross-lane moves; the store addresses are uniform bases)
             const int ca = hnm_readlane_i(ccount, ua), cb = hnm_readlane_i(ccount, ub);
-            const int pos = (h ? cb : ca) + __builtin_popcount(mh & ((1u << j) - 1u));
-            if (pass && pos < A.capp) seg[uh * segstride + pos] = (int32_t)n;
+            if (lane < 16) {
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                const int uu = r >> 1, it = lane + 16 * (r & 1);
+                const unsigned mu = (unsigned)(m >> (32 * uu));
+                const int ps = (uu ? cb : ca) + __builtin_popcount(mu & ((1u << it) - 1u));
+                if (((mu >> it) & 1u) && ps < A.capp) {
+                  // buffer stores: uniform row offset in an SGPR, the slot in one VGPR (the
+                  // tile loop runs at the 168-VGPR limit; 64-bit addresses here spilled)
+                  const int so = (uu ? ub : ua) * (int)segstride * 4;
+                  __builtin_amdgcn_raw_buffer_store_b32((int)(base + it), segrs, ps * 4, so, 0);
+                  __builtin_amdgcn_raw_buffer_store_b32(__float_as_int(d[r]), segdrs, ps * 4, so, 0);
+                }
+              }
+            }
             if (lane == ua) ccount += __builtin_popcount((unsigned)m);
             if (lane == ub && hasb) ccount += __builtin_popcount((unsigned)(m >> 32));
           }
@@ -1103,14 +1129,18 @@ __global__ __launch_bounds__(1024) void cert_gate_kernel(
 // CU 2.151 / 2.315, against one workgroup per 4 rows): the W2 fragments are staged into LDS once
 // per workgroup instead of once per 4 rows.
 #define RESCORE_PERSIST 3
+constexpr int RESCORE_BEST_FIRST = 96;  // rows with more candidates score the best 64 first
 __global__ __launch_bounds__(256, 3) void ncf_rescore_kernel(
     NcfTabs t, int mf, const float* __restrict__ W2, int h1, int h2, const float* __restrict__ b2,
     const float* __restrict__ wm, const float* __restrict__ bp, int64_t B,
     const int* __restrict__ flag, const int* __restrict__ cnt, const int32_t* __restrict__ buf,
+    const float* __restrict__ bufd, const float* __restrict__ tau, const float* __restrict__ Eu,
+    const float* __restrict__ Au, const float* __restrict__ Cu, const CertParams* __restrict__ prm,
     int NP, int capp, int K, int short_ok, float* __restrict__ ov, int64_t* __restrict__ oi,
     int32_t* __restrict__ ovf_rows, int32_t* __restrict__ ovf_cnt,
     unsigned long long* __restrict__ stats) {
   constexpr int KS = 32;
+  __shared__ int stg[4][96];  // best-first: staged candidate ordinals
   __shared__ __attribute__((aligned(16))) float wgs[4][64];
   __shared__ __attribute__((aligned(16))) float b2l[32], wml[32];  // 0 beyond h2
   __shared__ int pref[4][CERT_MAX_NP + 1];
@@ -1167,36 +1197,24 @@ __global__ __launch_bounds__(256, 3) void ncf_rescore_kernel(
     }
     continue;
   }
-  if (stats && lane == 0) {
-    atomicAdd(&stats[1], (unsigned long long)n);
-    if (b == 0) atomicAdd(&stats[0], (unsigned long long)B);
-  }
   const float bpv = bp[0];
   WaveTopK<1> L;
   L.init();
   const int32_t* rowbuf = buf + b * (int64_t)NP * capp;
-  // candidate g's item (0 past the row's n): segment = last p with pref[p] <= g
-  auto cand = [&](int g) {
-    int it = 0;
-    if (g < n) {
-      int lo = 0, hi = NP;
-      while (hi - lo > 1) {
-        const int mid = (lo + hi) >> 1;
-        if (pref[wave][mid] <= g) lo = mid;
-        else hi = mid;
-      }
-      it = rowbuf[(int64_t)lo * capp + (g - pref[wave][lo])];
+  const float* rowd = bufd + b * (int64_t)NP * capp;
+  // candidate g's slot in the row's segments (g < n): segment = last p with pref[p] <= g
+  auto slot = [&](int g) {
+    int lo = 0, hi = NP;
+    while (hi - lo > 1) {
+      const int mid = (lo + hi) >> 1;
+      if (pref[wave][mid] <= g) lo = mid;
+      else hi = mid;
     }
-    return it;
+    return (int64_t)lo * capp + (g - pref[wave][lo]);
   };
-  // the next chunk's candidate id is loaded while this chunk is scored (one dependent
-  // round trip less per chunk); b2 / wm come from LDS (16 + 16 VGPRs freed)
-  int item_next = cand(j);
-  for (int c0 = 0; c0 < n; c0 += 32) {
-    const int g = c0 + j;
-    const bool ok = g < n;
-    int item = item_next;
-    item_next = cand(g + 32);
+  auto cand = [&](int g) { return g < n ? rowbuf[slot(g)] : 0; };
+  // exact fp32 score of lane j's candidate (both halves of the wave), offered to the top-K
+  auto score_item = [&](int item, bool ok) {
     // GMF: fma chain in the f32 MFMA's order (k = 2s, then 2s + 1) over all 64 k (zero
     // beyond mf, as the fp32 kernel's padded operands); loads in two batches of 8 float4
     // issued together (a runtime-bounded loop would wait on each load)
@@ -1264,6 +1282,77 @@ __global__ __launch_bounds__(256, 3) void ncf_rescore_kernel(
     const float tot = hnm_sum_halves(mlp + (h == 0 ? gm : 0.f));
     const float score = tot + bpv;
     L.offer(score, item, ok && h == 0, K);
+  };
+  // Best first (round 5), rows of more than RESCORE_BEST_FIRST candidates: the 64 with the best
+  // scan test values are scored first; their K-th exact score thr lower-bounds the row's K-th,
+  // so a remaining candidate is scored only if it would have passed the scan against thr -- its
+  // test value against the threshold tau2 that cert_tau_kernel derives from thr, with twice that
+  // kernel's guard (the extra rounding of d + tau).  Rows whose scan bound came from a poor
+  // sample (user-specific best items: ~300 candidates a row) drop to about what a perfect
+  // sample would leave (tools/ncf_bound_limit_probe.py).  Shorter rows: every candidate, in
+  // order.  Candidates are staged 32 at a time (one scoring site: the kernel stays at 168 VGPRs).
+  int* st = stg[wave];
+  int ns = 0, nscored = 0;
+  float v63 = 0.f, t2 = 0.f;
+  int i63 = 0;
+  bool usable = false;
+  const float tb = tau[b];
+  const bool bf = n > RESCORE_BEST_FIRST;
+  if (bf) {
+    float tv = -__builtin_inff();
+    int ti = HNM_SENTINEL_IDX;
+    for (int c0 = 0; c0 < n; c0 += 64) {  // the 64 best (test value desc, ordinal asc)
+      const int g = c0 + lane;
+      const float d = g < n ? rowd[slot(g)] : -__builtin_inff();
+      float v1 = d != d ? __builtin_inff() : d;  // a NaN test value is scored first
+      int i1 = g < n ? g : HNM_SENTINEL_IDX;
+      hnm_sort128(tv, ti, v1, i1);
+    }
+    v63 = hnm_readlane_f(tv, 63);
+    i63 = hnm_readlane_i(ti, 63);
+  }
+  for (int phase = bf ? 0 : 2; phase < (bf ? 2 : 3); ++phase) {  // bf: 0, 1; else 2
+    if (phase == 1) {
+      const float thr = L.thr_v;  // 64 >= K items scored: a valid K-th
+      const float unit = prm->unit;
+      const float scale = unit * (prm->c0 + Au[b] + prm->Bmax + Cu[b] * prm->Dmax);
+      t2 = (thr - bpv) * unit - Eu[b] - 2.f * 3.814697265625e-06f * scale;  // 2 x 2^-18
+      t2 -= fabsf(t2) * 1.9073486328125e-06f;                                 // 2 x 2^-20
+      usable = __builtin_isfinite(t2);
+    }
+    for (int c0 = 0; c0 < n; c0 += 64) {
+      const int g = c0 + lane;
+      bool keep = g < n;
+      if (keep && phase < 2) {
+        const float d = rowd[slot(g)];
+        const bool top = !hnm_better(v63, i63, d != d ? __builtin_inff() : d, g);
+        keep = phase == 0 ? top : !top && (!usable || !(d + tb < t2));
+      }
+      const uint64_t m = __ballot(keep);
+      if (keep) st[ns + __popcll(m & ((1ull << lane) - 1))] = g;
+      ns += __popcll(m);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      const bool last = c0 + 64 >= n;
+      while (ns >= 32 || (last && ns > 0)) {
+        const int nv = ns < 32 ? ns : 32;
+        score_item(cand(st[j < nv ? j : 0]), j < nv);
+        nscored += nv;
+        const int rest = ns - nv;
+        const int mv = lane < rest ? st[32 + lane] : 0;
+        __builtin_amdgcn_wave_barrier();
+        if (lane < rest) st[lane] = mv;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        ns = rest;
+      }
+    }
+  }
+  if (stats && lane == 0) {
+    atomicAdd(&stats[1], (unsigned long long)nscored);
+    if (b == 0) atomicAdd(&stats[0], (unsigned long long)B);
   }
   L.store(ov ? ov + b * K : nullptr, oi + b * K, K);
   }
@@ -1293,6 +1382,7 @@ struct CertWs {
   int64_t* kthi;
   int *cnt, *flag;
   int32_t *buf, *ovf_cnt, *ovf_rows;
+  float* bufd;  // the appended candidates' test values
   _Float16 *P16, *WG16, *Q16, *G16, *W2h, *wmh;
   float* cv;
   int32_t* ci;
@@ -1369,6 +1459,7 @@ size_t cert_carve(char* base, int64_t B, int64_t I, int K, int num_cus, int wg, 
   x.ovf_cnt = (int32_t*)take(256);
   x.ovf_rows = (int32_t*)take(B * 4);
   x.buf = (int32_t*)take((size_t)B * sh.part.np * sh.capp * 4);
+  x.bufd = (float*)take((size_t)B * sh.part.np * sh.capp * 4);
   x.P16 = (_Float16*)take((size_t)B * 64 * 2);
   x.WG16 = (_Float16*)take((size_t)B * 64 * 2);
   x.Q16 = (_Float16*)take((size_t)I * 64 * 2);
@@ -1560,6 +1651,7 @@ hnm_status ncf_cert_finish(hnm_ctx* ctx, const hnm_ncf_weights* w, const NcfTabs
   a.tau = x.tau;
   a.cnt = x.cnt;
   a.buf = x.buf;
+  a.segd = x.bufd;
   a.capp = sh.capp;
   a.ipp = sh.part.ipp;
   a.NP = sh.part.np;
@@ -1571,7 +1663,8 @@ hnm_status ncf_cert_finish(hnm_ctx* ctx, const hnm_ncf_weights* w, const NcfTabs
   const int64_t rgrid = std::min<int64_t>(hnm_cdiv(B, 4), (int64_t)RESCORE_PERSIST * ctx->num_cus);
   hipLaunchKernelGGL(ncf_rescore_kernel, dim3((unsigned)rgrid), dim3(256), 0, ctx->stream,
                      t, w->mf, w->w2, w->h1, w->h2, w->b2, w->wp + w->mf, w->bp, B, x.flag, x.cnt,
-                     x.buf, sh.part.np, sh.capp, K, short_ok, ov, oi, x.ovf_rows, x.ovf_cnt,
+                     x.buf, x.bufd, x.tau, x.Eu, x.Au, x.Cu, x.prm, sh.part.np, sh.capp, K,
+                     short_ok, ov, oi, x.ovf_rows, x.ovf_cnt,
                      ctx->stats_on ? ctx->stats_dev : nullptr);
   HNM_LAUNCH_CHECK();
   // exact fp32 scan over all items for the queued rows (device-side row list)
