@@ -1415,8 +1415,12 @@ CertShape cert_shape(int64_t B, int64_t I, int K, int num_cus, int wg) {
   sh.part = scan_partition(I, hnm_cdiv(B, 128), num_cus, wg);
   // a row's candidates: items within the bound's margin of the champion sample's K-th --
   // at worst (no shared best items) the K-th of a 1/gsz sample, ~K * gsz items; each
-  // partition gets 4x its even share of 2x that, >= 64 slots (overflow: fallback row)
-  const int64_t total = std::min<int64_t>(8192, std::max<int64_t>(512, 2 * (int64_t)K * sh.gsz));
+  // partition gets 4x its even share of 8x that, >= 64 slots (overflow: fallback row).
+  // Round 5: 8x (was 2x) -- with the best-first re-scoring a long candidate list costs the
+  // scan's appends and one sort, while an overflowing row costs an exact scan of the whole
+  // catalogue ("norms" trained-like weights: 44 fallback rows -> 0, 3.50 -> 3.24 ms a step;
+  // init weights unchanged: profiles/r6k_ncf_capp_ab.txt)
+  const int64_t total = std::min<int64_t>(8192, std::max<int64_t>(512, 8 * (int64_t)K * sh.gsz));
   sh.capp = (int)std::max<int64_t>(64, std::min<int64_t>(total, hnm_cdiv(4 * total, sh.part.np)));
   return sh;
 }
