@@ -1298,20 +1298,27 @@ __global__ __launch_bounds__(256, 3) void ncf_rescore_kernel(
   bool usable = false;
   const float tb = tau[b];
   const bool bf = n > RESCORE_BEST_FIRST;
+  int ti = HNM_SENTINEL_IDX;
   if (bf) {
     float tv = -__builtin_inff();
-    int ti = HNM_SENTINEL_IDX;
     for (int c0 = 0; c0 < n; c0 += 64) {  // the 64 best (test value desc, ordinal asc)
       const int g = c0 + lane;
       const float d = g < n ? rowd[slot(g)] : -__builtin_inff();
       float v1 = d != d ? __builtin_inff() : d;  // a NaN test value is scored first
       int i1 = g < n ? g : HNM_SENTINEL_IDX;
-      hnm_sort128(tv, ti, v1, i1);
+      // only a chunk holding an entry above the current 64th can change the 64 best
+      const float c63 = hnm_readlane_f(tv, 63);
+      const int c63i = hnm_readlane_i(ti, 63);
+      if (__ballot(hnm_better(v1, i1, c63, c63i))) hnm_sort128(tv, ti, v1, i1);
     }
     v63 = hnm_readlane_f(tv, 63);
     i63 = hnm_readlane_i(ti, 63);
   }
   for (int phase = bf ? 0 : 2; phase < (bf ? 2 : 3); ++phase) {  // bf: 0, 1; else 2
+    if (phase == 0) {  // the 64 best, already in ti (lane = rank)
+      st[lane] = ti;
+      ns = 64;
+    }
     if (phase == 1) {
       const float thr = L.thr_v;  // 64 >= K items scored: a valid K-th
       const float unit = prm->unit;
@@ -1320,21 +1327,23 @@ __global__ __launch_bounds__(256, 3) void ncf_rescore_kernel(
       t2 -= fabsf(t2) * 1.9073486328125e-06f;                                 // 2 x 2^-20
       usable = __builtin_isfinite(t2);
     }
-    for (int c0 = 0; c0 < n; c0 += 64) {
-      const int g = c0 + lane;
-      bool keep = g < n;
-      if (keep && phase < 2) {
-        const float d = rowd[slot(g)];
-        const bool top = !hnm_better(v63, i63, d != d ? __builtin_inff() : d, g);
-        keep = phase == 0 ? top : !top && (!usable || !(d + tb < t2));
+    for (int c0 = 0; c0 < (phase == 0 ? 1 : n); c0 += 64) {
+      if (phase != 0) {
+        const int g = c0 + lane;
+        bool keep = g < n;
+        if (keep && phase == 1) {
+          const float d = rowd[slot(g)];
+          const bool top = !hnm_better(v63, i63, d != d ? __builtin_inff() : d, g);
+          keep = !top && (!usable || !(d + tb < t2));
+        }
+        const uint64_t m = __ballot(keep);
+        if (keep) st[ns + __popcll(m & ((1ull << lane) - 1))] = g;
+        ns += __popcll(m);
       }
-      const uint64_t m = __ballot(keep);
-      if (keep) st[ns + __popcll(m & ((1ull << lane) - 1))] = g;
-      ns += __popcll(m);
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      const bool last = c0 + 64 >= n;
+      const bool last = phase == 0 || c0 + 64 >= n;
       while (ns >= 32 || (last && ns > 0)) {
         const int nv = ns < 32 ? ns : 32;
         score_item(cand(st[j < nv ? j : 0]), j < nv);
