@@ -207,3 +207,30 @@ def test_ncf_strided_sample_gate(kind):
     assert torch.equal(ei, pi) and torch.equal(ev.view(torch.int32), pv.view(torch.int32))
     assert rows == B
     assert sampled in (0, B)
+
+
+@pytest.mark.parametrize("kind", ["personal", "norms"])
+def test_ncf_best_first_rescoring(kind):
+    """Rows whose scan bound came from a poor sample append hundreds of candidates; the
+    re-scoring scores the 64 best (by the scan's test value) first and then only candidates
+    that pass against their exact K-th (ncf_cert.hip ncf_rescore_kernel, round 5).  Bitwise the
+    exact scan's top-K, with far fewer exact re-scores than appended candidates (the bench's
+    weight sets at the H&M shape: personal 306 appended / 64 re-scored a row, norms 598 / 64)."""
+    U, B = syn.HM_USERS, 512
+    if kind == "personal":
+        sd = syn.ncf_state_dict(U, I_FULL, 64, (128, 64, 32), seed=4, bias_scale=0.05,
+                                emb_scale=20.0)
+    else:
+        sd = syn.ncf_state_dict(U, I_FULL, 64, (128, 64, 32), seed=4, bias_scale=0.05)
+        sd = stress(sd, kind, NCF_EMB, "mlp_item_embedding.weight", 4)
+    m = to_module(NeuralCF(U, I_FULL), sd)
+    users = torch.from_numpy(syn.user_batch(U, B, seed=21)).to(DEV)
+    ex, pf, stats = topk_both(m, users)
+    (ev, ei), (pv, pi) = ex, pf
+    assert np.array_equal(ei, pi) and np.array_equal(ev.view(np.uint32), pv.view(np.uint32))
+    rows, cands, fallback = stats
+    per_row = cands / max(rows - fallback, 1)
+    print(f"NCF {kind}: exact re-scores / row {per_row:.1f}, fallback rows {fallback}")
+    assert rows == B
+    assert per_row <= 128, per_row  # 64 + the few that pass against the exact K-th
+
