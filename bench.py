@@ -1,7 +1,7 @@
 """Headline benchmark: recommendations/sec (batched users, K=12) on the reference's
 configs (BASELINE.json), MI355X-native HIP path.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload ncf|lightgcn|lightgcn128|widedeep|mf]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload ncf|lightgcn|lightgcn128|widedeep|mf|ncf_deep]
 
 Default workload = BASELINE.json configs[1]: NeuralCF mf 64, mlp [128,64,32], full H&M
 shape (1,371,980 users x 105,542 items), batch 4096 users per rank per step, K=12,
@@ -190,6 +190,25 @@ def build_workload(name, rank, world, device, batch, exact=False, weights="init"
         info["scan"] = ("exact fp32" if exact else
                         "certified f16 (layers 2 and 3: one W_hi.x_hi MFMA pass each; weight and activation residuals bounded exactly, the layer-2 bound terms on the matrix pipe) pre-filter + exact fp32 re-scoring")
         cpu = ("widedeep", None)
+    elif name == "ncf_deep":
+        # a NeuralCF tower other than the default two-layer one (VERDICT r4 missing #1): the
+        # reference builds any depth (neural_cf.py:75-90); [128, 64, 32, 16] with mf 64
+        if world > 1:
+            raise SystemExit("--workload ncf_deep: single-GPU line (the item-sharded exchange "
+                             "serves the default tower)")
+        sd = syn.ncf_state_dict(U, I, 64, (128, 64, 32, 16), seed=0)
+        m = load(NeuralCF(U, I, mlp_dims=[128, 64, 32, 16]), sd, device)
+        local = lambda u: m.recommend_with_scores(u, k=K)  # noqa: E731
+        info["_module"] = m
+        info["_per_pair_route"] = True
+        # useful fp32 MACs a pair after the per-row first layer: GMF 64, layers 64x32 and
+        # 32x16, prediction 16
+        per_launch = 2.0 * (64 + 64 * 32 + 32 * 16 + 16) * batch * (hi - lo)
+        info.update({"model": "NeuralCF", "mf_dim": 64, "mlp_dims": [128, 64, 32, 16],
+                     "scan": "exact fp32: f32-MFMA layer chains over 32-item tiles (bitwise the "
+                             "fmaf chain) with fused per-partition top-k lists (ncf_deep.hip)"})
+        bound, kernel = "mfma", "ncf_deep_mfma_kernel"
+        cpu = ("ncf", sd)
     elif name == "mf":
         if weights == "personal":
             raise SystemExit("--weights personal: NCF only (MF's init best items are already "
@@ -435,7 +454,8 @@ def pmc_traffic(workload):
 EXTRA_WORKLOADS = (("lightgcn", "configs[2]: LightGCN 3-layer dim=64, full H&M adjacency"),
                    ("widedeep", "configs[3]: Wide&Deep dim=64, 512-256-128 tower"),
                    ("lightgcn128", "configs[4] per-GPU work at N=1: LightGCN dim=128"),
-                   ("mf", "MatrixFactorization dim=64 (SURVEY §8(f))"))
+                   ("mf", "MatrixFactorization dim=64 (SURVEY §8(f))"),
+                   ("ncf_deep", "NeuralCF [128,64,32,16] tower (neural_cf.py:75-90 any depth)"))
 
 
 def run_child(argv, timeout):
@@ -483,7 +503,7 @@ def compact_line(line):
         out["roofline"]["gather_ceiling"] = {k: r["gather_ceiling"].get(k)
                                              for k in ("bytes", "ms", "frac", "vs_uniform_random")}
     for k in ("cpu_baseline", "exact_fp32", "filtered", "serving_cached_propagation",
-              "pipelined_3_streams", "full_propagation_step"):
+              "pipelined_3_streams", "full_propagation_step", "per_pair_lds_route"):
         if line.get(k):
             out[k] = line[k]["value"]
     if line.get("prefilter"):
@@ -623,7 +643,20 @@ def main():
     exact_rate = None
     if args.profile_only:
         args.no_extras = args.no_cpu_baseline = True
-    if not args.exact and not args.profile_only:
+    per_pair = None
+    if info.get("_per_pair_route") and not args.profile_only:
+        # the same step through the per-pair LDS kernel + dense rows + row top-k
+        # (HNM_OPT_DEEP_MFMA = 0, bitwise the same lists), reported beside `value`
+        _lib.set_option(device, _lib.HNM_OPT_DEEP_MFMA, 0)
+        step(batches[0])
+        torch.cuda.synchronize()
+        tp = time.perf_counter()
+        for j in range(2):
+            step(batches[j % nb])
+        torch.cuda.synchronize()
+        per_pair = B * 2 / (time.perf_counter() - tp)
+        _lib.set_option(device, _lib.HNM_OPT_DEEP_MFMA, 1)
+    if not args.exact and not args.profile_only and not info.get("_per_pair_route"):
         # the like-for-like fp32 path (HNM_OPT_PREFILTER=0: every pair scored in exact fp32
         # arithmetic), timed the same way on the same batches, reported beside `value`
         _lib.set_prefilter(device, False)
@@ -693,6 +726,11 @@ def main():
                      "traffic": pmc_traffic(args.workload)},
         "cpu_baseline": None,
     }
+    if per_pair is not None:
+        line["per_pair_lds_route"] = {
+            "value": round(per_pair, 2), "unit": "users/s", "vs_value": round(per_pair / value, 4),
+            "note": "HNM_OPT_DEEP_MFMA=0: per-pair LDS kernel (dense rows) + row top-k, the round-4 "
+                    "deep-tower path; identical lists"}
     issued = ISSUED_F16_FLOP_PER_PAIR.get(args.workload)
     if f16 and issued and not args.exact:
         # f16 MFMA FLOP the scan actually issues per pair (epilogue / split passes included)

@@ -30,6 +30,7 @@ extern "C" hnm_status hnm_ctx_create(int device, hnm_ctx** out) {
   if (c->num_cus <= 0) c->num_cus = 256;
   c->prefilter = 1;
   c->strided = 0;
+  c->deep_mfma = 1;
   if (hipMalloc((void**)&c->err_dev, 64) != hipSuccess) {
     free(c);
     hnm_set_error("hnm_ctx_create: hipMalloc of the error word failed");
@@ -95,6 +96,9 @@ extern "C" hnm_status hnm_ctx_set_option(hnm_ctx* ctx, int option, int64_t value
       return HNM_OK;
     case HNM_OPT_STRIDED:
       ctx->strided = value != 0;
+      return HNM_OK;
+    case HNM_OPT_DEEP_MFMA:
+      ctx->deep_mfma = value != 0;
       return HNM_OK;
     default:
       hnm_set_error("hnm_ctx_set_option: unknown option %d", option);

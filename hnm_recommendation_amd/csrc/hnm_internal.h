@@ -29,6 +29,7 @@ struct hnm_ctx {
   hipEvent_t* ev1;
   int prefilter;                   // HNM_OPT_PREFILTER (default 1)
   int strided;                     // HNM_OPT_STRIDED (default 0)
+  int deep_mfma;                   // HNM_OPT_DEEP_MFMA (default 1)
   unsigned long long* stats_dev;   // pre-filter counters: rows, candidates, fallback rows,
                                    // rows whose bound used the gated strided sample, and
                                    // (last NCF call) the gate's predicted proxy candidates

@@ -213,11 +213,22 @@ class NeuralCF(RecModule):
         return out_v, out_i
 
     def _deep_topk(self, u, hu, k, mptr, midx):
-        """Deep towers: dense rows for a chunk of users (<= 256 MB of scores) + the row top-k
-        kernel with the chunk's slice of the CSR mask (absolute offsets into mask_idx)."""
+        """Deep towers: hnm_ncf_deep_topk_f32 for k <= 64 (the fp32-MFMA scan with fused
+        per-partition top-k lists where the tower's widths are <= 64, else dense rows per user
+        chunk in the library's workspace + the row top-k kernel); k > 64 (serve path, up to
+        100): dense rows for a chunk of users (<= 256 MB of scores) + the row top-k kernel with
+        the chunk's slice of the CSR mask (absolute offsets into mask_idx)."""
         B = u.numel()
         out_v = torch.empty(B, k, dtype=torch.float32, device=u.device)
         out_i = torch.empty(B, k, dtype=torch.int64, device=u.device)
+        if k <= 64:
+            w, keep = self._deep_weights()
+            c = _lib.ctx(u.device)
+            _lib.check(_lib.fn("hnm_ncf_deep_topk_f32")(
+                c, C.byref(w), _lib.ptr(u), B, _lib.ptr(mptr), _lib.ptr(midx), k,
+                _lib.ptr(out_v), _lib.ptr(out_i)), "hnm_ncf_deep_topk_f32")
+            self._check(u.device, hu)
+            return out_v, out_i
         step = max(1, min(B, 65535, (1 << 26) // max(self.num_items, 1)))
         buf = torch.empty(step, self.num_items, dtype=torch.float32, device=u.device)
         for b0 in range(0, B, step):

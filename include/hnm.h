@@ -76,11 +76,15 @@ hnm_status hnm_ctx_abort_pending(hnm_ctx* ctx);
  * (16.7M items at d <= 64, 8.3M at d <= 128), NCF layer widths beyond 64 / 32 or 33.5M items. */
 enum { HNM_OPT_PREFILTER = 1,
        HNM_OPT_STATS = 3,      /* 1: count pre-filter candidates / fallback rows (diagnostics) */
-       HNM_OPT_STRIDED = 4     /* NeuralCF certified top-K: 1 = the gated per-user strided
+       HNM_OPT_STRIDED = 4,    /* NeuralCF certified top-K: 1 = the gated per-user strided
                                   sample may run (weights whose best items are user-specific:
                                   bench "norms" 3.68 -> 3.09 ms a step); 0 (default) = the
                                   champion sample alone (the gate costs ~2 % of the init-weight
-                                  step) */ };
+                                  step) */
+       HNM_OPT_DEEP_MFMA = 5   /* deep NeuralCF towers (hnm_ncf_deep_*): 1 (default) = the
+                                  fp32-MFMA tile kernel where the tower fits it (widths <= 64,
+                                  mf <= 128); 0 = the per-pair LDS kernel everywhere (same
+                                  scores bitwise: the A/B and parity switch) */ };
 hnm_status hnm_ctx_set_option(hnm_ctx* ctx, int option, int64_t value);
 /* Pre-filter counters since the last reset (counted only while HNM_OPT_STATS is 1): out[0]
  * rows scored, out[1] candidates re-scored in fp32, out[2] rows that took the exact fallback
@@ -252,8 +256,8 @@ hnm_status hnm_ncf_pair_scores_f32(hnm_ctx* ctx, const hnm_ncf_weights* w,
  * kernels above do not cover (they take the default two-layer tower).  w[l] / b[l] =
  * mlp_layers.{3l}.weight [dims[l+1], dims[l]] / bias; dims[0] = 2 x the MLP embedding width;
  * widths dims[1..nl] <= 512, nl <= 8.
- * item_ids NULL: dense scores out[b * ldo + i] for every item (ldo >= num_items, B < 65536:
- * predict_all_items; recommend = these + hnm_topk_rows_f32).  item_ids set: pair scores
+ * item_ids NULL: dense scores out[b * ldo + i] for every item (ldo >= num_items:
+ * predict_all_items; recommend = hnm_ncf_deep_topk_f32).  item_ids set: pair scores
  * out[n] = s(user_ids[n], item_ids[n]), n < B (forward).  Out-of-range ids flag HNM_EOOB
  * (hnm_ctx_check) and score NaN. */
 typedef struct {
@@ -275,6 +279,16 @@ typedef struct {
 hnm_status hnm_ncf_deep_scores_f32(hnm_ctx* ctx, const hnm_ncf_deep_weights* w,
                                    const int64_t* user_ids, int64_t B, const int64_t* item_ids,
                                    float* out, int64_t ldo);
+/* Fused top-k of a deep tower (NeuralCF.recommend, neural_cf.py:300-326, with the -inf filter
+ * and torch.topk of neural_cf.py:316-324): (score desc, item asc), scores bitwise those of
+ * hnm_ncf_deep_scores_f32, 1 <= k <= 64, mask as hnm_ncf_topk_f32.  Towers with every width
+ * dims[1..nl] <= 64 and mf <= 128 take the fp32-MFMA scan that keeps per-partition top-k
+ * lists (no [B, I] score matrix); wider towers score dense rows per user chunk in the
+ * workspace and take the row top-k kernel. */
+hnm_status hnm_ncf_deep_topk_f32(hnm_ctx* ctx, const hnm_ncf_deep_weights* w,
+                                 const int64_t* user_ids, int64_t B, const int64_t* mask_ptr,
+                                 const int32_t* mask_idx, int k, float* out_val,
+                                 int64_t* out_idx);
 
 /* ---- a9 + a10: Wide&Deep ------------------------------------------------------------
  * Reference layout (wide_deep.py:92-134): deep tower Linear -> ReLU -> BatchNorm1d (eval:

@@ -1,0 +1,115 @@
+"""GPU: NeuralCF towers other than the fused two-layer one (neural_cf.py:75-90 `_build_mlp`,
+scored as neural_cf.py:131-141 and ranked as neural_cf.py:300-326).
+
+* The fp32-MFMA tile kernel (ncf_deep.hip `ncf_deep_mfma_kernel`, widths <= 64) scores bitwise
+  what the per-pair LDS kernel scores (HNM_OPT_DEEP_MFMA = 0): the f32 MFMA is the fmaf chain.
+* Its fused top-k (hnm_ncf_deep_topk_f32, per-partition wave lists + merge) equals the
+  (score desc, item asc) order of those dense rows exactly, filtered and unfiltered, at both
+  users-per-wave variants and on towers with one and two 32-unit tiles, odd widths, a single
+  Linear, mf not a multiple of 8 and 7 layers; the wide-tower route (dense chunk + row top-k
+  inside the library) gives the same lists.
+* Rows against the CPU oracle (oracle/hnm_oracle.py ncf_predict_all_items) within the fp32
+  tolerance of tests/parity.py.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import hnm_oracle as O
+from parity import assert_scores_close
+from hnm_recommendation_amd import NeuralCF, _lib
+from hnm_recommendation_amd import synthetic as syn
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+TOWERS = [  # (mf, mlp_dims)
+    (64, (128, 64, 32, 16)),          # one 32-unit MFMA tile a layer
+    (32, (64, 32)),                   # a single Linear: no MFMA layer
+    (20, (96, 48, 40, 24, 12)),       # odd widths; mf padded to 24
+    (64, (128, 64, 64, 8)),           # a 64-wide MFMA layer (two tiles)
+    (128, (64, 32, 16, 8, 4, 2, 1)),  # 6 Linear layers, mf 128
+]
+
+
+def model(U, I, mf, dims, seed):
+    sd = syn.ncf_state_dict(U, I, mf, dims, seed=seed, bias_scale=0.05, emb_scale=8.0)
+    m = NeuralCF(U, I, mf_dim=mf, mlp_dims=list(dims))
+    m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in sd.items()})
+    return m.to(DEV).eval(), sd
+
+
+def per_pair(fn):
+    """Run fn with the per-pair LDS kernel (and the dense-chunk top-k) forced."""
+    _lib.set_option(DEV, _lib.HNM_OPT_DEEP_MFMA, 0)
+    try:
+        return fn()
+    finally:
+        _lib.set_option(DEV, _lib.HNM_OPT_DEEP_MFMA, 1)
+
+
+def topk_order(scores, k):
+    """(score desc, item asc) per row -- the library's total order."""
+    idx = np.empty((scores.shape[0], k), np.int64)
+    items = np.arange(scores.shape[1])
+    for b in range(scores.shape[0]):
+        idx[b] = np.lexsort((items, -scores[b].astype(np.float64)))[:k]
+    return idx, np.take_along_axis(scores, idx, 1)
+
+
+@pytest.mark.parametrize("mf,dims", TOWERS)
+@pytest.mark.parametrize("B", [37, 300])
+def test_deep_mfma_bitwise_and_fused_topk(mf, dims, B):
+    U, I, K = 700, 3001, 12
+    m, sd = model(U, I, mf, dims, seed=len(dims) + mf)
+    assert not m._fused()
+    users_np = syn.user_batch(U, B, seed=B)
+    users = torch.from_numpy(users_np).to(DEV)
+    fast = m.predict_all_items(users)
+    slow = per_pair(lambda: m.predict_all_items(users))
+    assert torch.equal(fast.view(torch.int32), slow.view(torch.int32)), "MFMA vs per-pair"
+    dense = fast.cpu().numpy()
+    rows = [0, B // 2, B - 1]
+    assert_scores_close(dense[rows], O.ncf_predict_all_items(sd, users_np[rows]), "deep oracle")
+
+    ref_i, ref_v = topk_order(dense, K)
+    v, i = m.recommend_with_scores(users, k=K)
+    np.testing.assert_array_equal(i.cpu().numpy(), ref_i)
+    np.testing.assert_array_equal(v.cpu().numpy().view(np.int32), ref_v.view(np.int32))
+    v2, i2 = per_pair(lambda: m.recommend_with_scores(users, k=K))
+    assert torch.equal(i2, i) and torch.equal(v2.view(torch.int32), v.view(torch.int32))
+
+    # history filter: each row's current top-3 plus random items, every 3rd row
+    rng = np.random.default_rng(B)
+    filt = {}
+    for b in range(0, B, 3):
+        u = int(users_np[b])
+        filt.setdefault(u, set()).update(int(x) for x in ref_i[b, :3])
+        filt[u].update(int(x) for x in rng.integers(0, I, 40))
+    masked = dense.copy()
+    for b in range(B):
+        for it in filt.get(int(users_np[b]), ()):
+            masked[b, it] = -np.inf
+    ref_i, ref_v = topk_order(masked, K)
+    v, i = m.recommend_with_scores(users, filter_items=filt, k=K)
+    np.testing.assert_array_equal(i.cpu().numpy(), ref_i)
+    np.testing.assert_array_equal(v.cpu().numpy(), ref_v)
+    # k = 64, the fused path's maximum
+    ref_i, _ = topk_order(dense, 64)
+    np.testing.assert_array_equal(m.recommend_with_scores(users, k=64)[1].cpu().numpy(), ref_i)
+
+
+def test_deep_mfma_full_catalogue_topk():
+    """[128,64,32,16] over the full H&M catalogue (105,542 items, many partitions) at B = 512:
+    fused top-12 equals the per-pair route's lists bitwise; oracle rows agree."""
+    U, I = 3000, syn.HM_ITEMS
+    m, sd = model(U, I, 64, (128, 64, 32, 16), seed=21)
+    users_np = syn.user_batch(U, 512, seed=4)
+    users = torch.from_numpy(users_np).to(DEV)
+    v, i = m.recommend_with_scores(users)
+    v2, i2 = per_pair(lambda: m.recommend_with_scores(users))
+    assert torch.equal(i, i2) and torch.equal(v.view(torch.int32), v2.view(torch.int32))
+    rows = [0, 255, 511]
+    ref = O.ncf_predict_all_items(sd, users_np[rows])
+    got = m.predict_all_items(users[rows]).cpu().numpy()
+    assert_scores_close(got, ref, "deep full-catalogue rows")
