@@ -136,6 +136,7 @@ __global__ __launch_bounds__(256) void ncf_deep_kernel(DeepArgs a, int maxw, uns
 #define DM_W 64               // P / Q row width (pair-permuted, zero padded)
 #define DM_QRS (DM_W + 4)     // LDS row stride of the Q tile (b128 reads conflict-free)
 #define DM_WU 4               // users per wave (two MFMA chains at a time)
+#define DM_NU (4 * DM_WU)     // users per workgroup
 
 struct DeepMArgs {
   const float* P;      // [B, 64]
@@ -205,12 +206,11 @@ __global__ __launch_bounds__(256) void deep_pack_kernel(DeepPack pk, float* __re
   } while (0)
 #define DM_ACC(W0, W1, BA, BB) DM_STEP(W0, W1, BA, BB, cA0, cA1, cB0, cB1)
 
-template <int NT, int MFP, bool DENSE, int NW>
-__global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void ncf_deep_mfma_kernel(DeepMArgs a) {
-  constexpr int WU = DM_WU, NU = NW * DM_WU, NTH = 64 * NW;
+template <int NT, int MFP, bool DENSE>
+__global__ __launch_bounds__(256, 2) void ncf_deep_mfma_kernel(DeepMArgs a) {
+  constexpr int WU = DM_WU, NU = DM_NU;
   constexpr int GRS = MFP + 4;       // LDS row stride of the GMF tile
-  constexpr int QF4 = (TILE * DM_W / 4 + NTH - 1) / NTH;  // Q tile float4 a thread
-  constexpr int GF4 = (TILE * MFP / 4 + NTH - 1) / NTH;   // GMF tile float4 a thread
+  constexpr int GF4 = MFP / 32;      // GMF tile float4 a thread (32 rows x MFP / 4)
   extern __shared__ float4 dm_lds4[];
   float* img = (float*)dm_lds4;
   float* qs = img + a.img_n;              // [2][TILE][DM_QRS]
@@ -227,20 +227,20 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void ncf_deep_mfma_kernel
   const int64_t part_start = (int64_t)p * a.ipp;
   const int64_t part_end = std::min<int64_t>(I, part_start + a.ipp);
 
-  for (int e = tid; e < a.img_n / 4; e += NTH) dm_lds4[e] = reinterpret_cast<const float4*>(a.img)[e];
-  for (int e = tid; e < NU * DM_W / 4; e += NTH) {
+  for (int e = tid; e < a.img_n / 4; e += 256) dm_lds4[e] = reinterpret_cast<const float4*>(a.img)[e];
+  for (int e = tid; e < NU * DM_W / 4; e += 256) {
     const int64_t b = ublk + e / (DM_W / 4);
     reinterpret_cast<float4*>(ps)[e] =
         b < B ? reinterpret_cast<const float4*>(a.P + b * DM_W)[e % (DM_W / 4)]
               : make_float4(0.f, 0.f, 0.f, 0.f);
   }
-  for (int e = tid; e < NU * MFP; e += NTH) {
+  for (int e = tid; e < NU * MFP; e += 256) {
     const int c = e % MFP;
     const int64_t b = ublk + e / MFP;
     const int64_t u = b < B ? a.uids[b] : -1;
     us[e] = (u >= 0 && u < a.num_users && c < a.mf) ? a.gu[u * a.mf + c] : 0.f;
   }
-  for (int e = tid; e < MFP + 64; e += NTH)
+  for (int e = tid; e < MFP + 64; e += 256)
     wps[e] = e < a.mf ? a.wp[e] : (e >= MFP && e - MFP < a.dl) ? a.wp[a.mf + e - MFP] : 0.f;
 
   WaveTopK<1> L[WU];
@@ -266,38 +266,34 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void ncf_deep_mfma_kernel
 
   // item tile staging through registers: issued before a tile's compute, written to the other
   // LDS buffer after it
-  float4 qst[QF4], gst[GF4];
+  float4 qst[2], gst[GF4];
   auto load_tile = [&](int64_t base) {
 #pragma unroll
-    for (int q = 0; q < QF4; ++q) {
-      const int f = tid + NTH * q;
+    for (int q = 0; q < 2; ++q) {
+      const int f = tid + 256 * q;
       const int64_t item = base + (f >> 4);
-      qst[q] = (f < TILE * DM_W / 4 && item < part_end)
-                   ? reinterpret_cast<const float4*>(a.Q + item * DM_W)[f & 15]
-                   : make_float4(0.f, 0.f, 0.f, 0.f);
+      qst[q] = item < part_end ? reinterpret_cast<const float4*>(a.Q + item * DM_W)[f & 15]
+                               : make_float4(0.f, 0.f, 0.f, 0.f);
     }
 #pragma unroll
     for (int q = 0; q < GF4; ++q) {
-      const int f = tid + NTH * q;
+      const int f = tid + 256 * q;
       const int64_t item = base + f / (MFP / 4);
-      gst[q] = (f < TILE * MFP / 4 && item < part_end)
-                   ? reinterpret_cast<const float4*>(a.G + item * MFP)[f % (MFP / 4)]
-                   : make_float4(0.f, 0.f, 0.f, 0.f);
+      gst[q] = item < part_end ? reinterpret_cast<const float4*>(a.G + item * MFP)[f % (MFP / 4)]
+                               : make_float4(0.f, 0.f, 0.f, 0.f);
     }
   };
   auto store_tile = [&](int buf) {
 #pragma unroll
-    for (int q = 0; q < QF4; ++q) {
-      const int f = tid + NTH * q;
-      if (f < TILE * DM_W / 4)
-        *reinterpret_cast<float4*>(&qs[(buf * TILE + (f >> 4)) * DM_QRS + 4 * (f & 15)]) = qst[q];
+    for (int q = 0; q < 2; ++q) {
+      const int f = tid + 256 * q;
+      *reinterpret_cast<float4*>(&qs[(buf * TILE + (f >> 4)) * DM_QRS + 4 * (f & 15)]) = qst[q];
     }
 #pragma unroll
     for (int q = 0; q < GF4; ++q) {
-      const int f = tid + NTH * q;
-      if (f < TILE * MFP / 4)
-        *reinterpret_cast<float4*>(&gs[(buf * TILE + f / (MFP / 4)) * GRS + 4 * (f % (MFP / 4))]) =
-            gst[q];
+      const int f = tid + 256 * q;
+      *reinterpret_cast<float4*>(&gs[(buf * TILE + f / (MFP / 4)) * GRS + 4 * (f % (MFP / 4))]) =
+          gst[q];
     }
   };
 
@@ -510,19 +506,12 @@ static hnm_status deep_check(const hnm_ncf_deep_weights* w) {
   return HNM_OK;
 }
 
-#include <stdlib.h>
-static int deep_nw() {  // A/B: HNM_DEEP_NW
-  static const int env = getenv("HNM_DEEP_NW") ? atoi(getenv("HNM_DEEP_NW")) : 4;
-  return env == 12 ? 12 : 4;
-}
-
 // MFMA tile layout of a tower; false when it does not fit (widths > 64, mf > 128, an LDS
 // image beyond a CU's 160 KB)
 struct DeepMLayout {
   DeepPack pk;
   int mfp;     // GMF width padded to 32, 64 or 128
   int nt;      // max 32-unit tiles of an MFMA layer (1 or 2)
-  int nw;      // waves per workgroup (4: two workgroups a CU; 12: one)
   size_t lds;  // dynamic LDS bytes
 };
 static bool deep_mfma_layout(const hnm_ctx* ctx, const hnm_ncf_deep_weights* w, DeepMLayout* o) {
@@ -547,10 +536,8 @@ static bool deep_mfma_layout(const hnm_ctx* ctx, const hnm_ncf_deep_weights* w, 
   }
   pk.img_n = off;
   o->mfp = w->mf <= 32 ? 32 : w->mf <= 64 ? 64 : 128;
-  o->nw = deep_nw();
-  const int nu = o->nw * DM_WU;
-  o->lds = (size_t)4 * (off + 2 * TILE * DM_QRS + 2 * TILE * (o->mfp + 4) + nu * DM_W +
-                        nu * o->mfp + o->mfp + 64);
+  o->lds = (size_t)4 * (off + 2 * TILE * DM_QRS + 2 * TILE * (o->mfp + 4) + DM_NU * DM_W +
+                        DM_NU * o->mfp + o->mfp + 64);
   return o->lds <= 160 * 1024 && off < 65536;
 }
 
@@ -619,20 +606,19 @@ static hnm_status deep_mfma_tables(hnm_ctx* ctx, const hnm_ncf_deep_weights* w,
   return HNM_OK;
 }
 
-template <int NT, int MFP, bool DENSE, int NW>
+template <int NT, int MFP, bool DENSE>
 static hnm_status deep_mfma_launch1(hnm_ctx* ctx, DeepMArgs a, const DeepMLayout& lay) {
-  const int64_t ublocks = hnm_cdiv(a.B, NW * DM_WU);
-  const Partition part = choose_partition(a.num_items, ublocks, ctx->num_cus, TILE, NW == 4 ? 2 : 1);
+  const int64_t ublocks = hnm_cdiv(a.B, DM_NU);
+  const Partition part = choose_partition(a.num_items, ublocks, ctx->num_cus);
   a.ipp = part.ipp;
   a.NP = part.np;
   HNM_REQUIRE(ublocks < ((int64_t)1 << 31), HNM_EUNSUPPORTED, "ncf_deep: batch too large");
   if (lay.lds > 64 * 1024)  // e.g. two 64-wide MFMA layers: one workgroup a CU
-    (void)hipFuncSetAttribute((const void*)ncf_deep_mfma_kernel<NT, MFP, DENSE, NW>,
+    (void)hipFuncSetAttribute((const void*)ncf_deep_mfma_kernel<NT, MFP, DENSE>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lay.lds);
   hnm_timer_begin(ctx, HNM_TIME_SCORE);
-  hipLaunchKernelGGL((ncf_deep_mfma_kernel<NT, MFP, DENSE, NW>),
-                     dim3((unsigned)ublocks, (unsigned)part.np), dim3(64 * NW), lay.lds, ctx->stream,
-                     a);
+  hipLaunchKernelGGL((ncf_deep_mfma_kernel<NT, MFP, DENSE>),
+                     dim3((unsigned)ublocks, (unsigned)part.np), dim3(256), lay.lds, ctx->stream, a);
   hnm_timer_end(ctx, HNM_TIME_SCORE);
   HNM_LAUNCH_CHECK();
   return HNM_OK;
@@ -641,11 +627,10 @@ static hnm_status deep_mfma_launch1(hnm_ctx* ctx, DeepMArgs a, const DeepMLayout
 // NT = 1 when every MFMA layer has <= 32 outputs (one 32-unit tile: half the registers), else 2
 template <bool DENSE>
 static hnm_status deep_mfma_launch(hnm_ctx* ctx, const DeepMArgs& a, const DeepMLayout& lay) {
-#define HNM_DEEP_MFP(NTV)                                                              \
-  if (lay.nw == 12 && lay.mfp == 64) return deep_mfma_launch1<NTV, 64, DENSE, 12>(ctx, a, lay); \
-  return lay.mfp == 32   ? deep_mfma_launch1<NTV, 32, DENSE, 4>(ctx, a, lay)           \
-         : lay.mfp == 64 ? deep_mfma_launch1<NTV, 64, DENSE, 4>(ctx, a, lay)           \
-                         : deep_mfma_launch1<NTV, 128, DENSE, 4>(ctx, a, lay);
+#define HNM_DEEP_MFP(NTV)                                                  \
+  return lay.mfp == 32   ? deep_mfma_launch1<NTV, 32, DENSE>(ctx, a, lay)  \
+         : lay.mfp == 64 ? deep_mfma_launch1<NTV, 64, DENSE>(ctx, a, lay)  \
+                         : deep_mfma_launch1<NTV, 128, DENSE>(ctx, a, lay);
   if (lay.nt > 1) {
     HNM_DEEP_MFP(2)
   }
@@ -777,8 +762,7 @@ static hnm_status deep_topk_chunk(hnm_ctx* ctx, const hnm_ncf_deep_weights* w,
   DeepMLayout lay;
   hnm_status st;
   if (deep_mfma_layout(ctx, w, &lay)) {
-    const Partition part = choose_partition(I, hnm_cdiv(B, lay.nw * DM_WU), ctx->num_cus, TILE,
-                                            lay.nw == 4 ? 2 : 1);
+    const Partition part = choose_partition(I, hnm_cdiv(B, DM_NU), ctx->num_cus);
     const size_t szC = hnm_align((size_t)B * part.np * K * 4);
     DeepMArgs m;
     void* extra;
