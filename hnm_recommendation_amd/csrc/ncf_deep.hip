@@ -149,6 +149,7 @@ struct DeepMArgs {
   const float* bp;
   int64_t num_users, num_items, B, ipp;
   int mf, nl, dl, img_n;
+  int last16;   // the last layer (l = nl - 1 >= 2, <= 16 outputs) on v_mfma_f32_16x16x4f32
   int meta[8];  // MFMA layer l >= 1: A image offset | 4-step groups << 16 | 32-unit tiles << 20
   const int64_t* mptr;
   const int32_t* midx;
@@ -165,7 +166,7 @@ struct DeepPack {
   const float* w[8];
   const float* b[8];
   int dims[9];
-  int nl, img_n;
+  int nl, img_n, last16;
   int ks4[8], nt[8], aoff[8], boff[8];
 };
 
@@ -179,7 +180,19 @@ __global__ __launch_bounds__(256) void deep_pack_kernel(DeepPack pk, float* __re
     while (l + 1 < pk.nl && e >= pk.aoff[l + 1]) ++l;
     const int din = pk.dims[l], dout = pk.dims[l + 1];
     float v = 0.f;
-    if (e < pk.boff[l]) {
+    if (pk.last16 && l == pk.nl - 1) {
+      // 16x16x4 layer: A[m = lane & 15][k = lane >> 4] of step s = 4 * group + (e & 3)
+      // (input units 4s .. 4s + 3); then the bias, 16 plain floats
+      if (e < pk.boff[l]) {
+        const int rel = e - pk.aoff[l];
+        const int lane = (rel >> 2) & 63, s = 4 * (rel >> 8) + (rel & 3);
+        const int m = lane & 15, k = 4 * s + (lane >> 4);
+        if (m < dout && k < din) v = pk.w[l][(int64_t)m * din + k];
+      } else {
+        const int unit = e - pk.boff[l];
+        if (unit < dout) v = pk.b[l][unit];
+      }
+    } else if (e < pk.boff[l]) {
       const int rel = e - pk.aoff[l];
       const int lane = (rel >> 2) & 63, grp = rel >> 8;
       const int t = grp / pk.ks4[l], s = 4 * (grp % pk.ks4[l]) + (rel & 3);
@@ -407,7 +420,7 @@ __global__ __launch_bounds__(256, 2) void ncf_deep_mfma_kernel(DeepMArgs a) {
         };
         epilogue(meta1);
         // layers 3..: B operand of step s = 16t + r is x_t[r] (unit 2s + h), from registers
-        for (int l = 2; l < a.nl; ++l) {
+        for (int l = 2; l < a.nl - a.last16; ++l) {
           const int meta = a.meta[l];
           const int ks4 = (meta >> 16) & 15;
           const bool two = NT > 1 && (meta >> 20) > 1;
@@ -433,6 +446,61 @@ __global__ __launch_bounds__(256, 2) void ncf_deep_mfma_kernel(DeepMArgs a) {
           }
           epilogue(meta);
         }
+        if (a.last16) {
+          // last layer (<= 16 outputs) on v_mfma_f32_16x16x4f32: half the matrix cycles of a
+          // 32-unit tile.  Step s takes input units 4s .. 4s + 3 = registers (2s, 2s + 1) of x
+          // (units 2r + h); a permlane32 then a permlane16 swap turn the register pair into the
+          // B operands of the two 16-item blocks (lane l: item l & 15 of the block, unit
+          // 4s + (l >> 4)).
+          const int meta = a.meta[a.nl - 1];
+          const int g4 = (meta >> 16) & 15;
+          const float* A16 = img + (meta & 0xffff) + 4 * lane;
+          const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+          f32x4 dA0 = z, dA1 = z, dB0 = z, dB1 = z;  // (user, item block)
+#pragma unroll
+          for (int st = 0; st < 8 * NT; ++st) {
+            if (st < 4 * g4) {
+              const float w = A16[256 * (st >> 2) + (st & 3)];
+              const int t = st >> 3, r = (2 * st) & 15;
+              const auto pa = __builtin_amdgcn_permlane32_swap(
+                  __float_as_uint(t ? xA1[r] : xA0[r]), __float_as_uint(t ? xA1[r + 1] : xA0[r + 1]),
+                  false, false);
+              const auto qa = __builtin_amdgcn_permlane16_swap(pa[0], pa[1], false, false);
+              const auto pb = __builtin_amdgcn_permlane32_swap(
+                  __float_as_uint(t ? xB1[r] : xB0[r]), __float_as_uint(t ? xB1[r + 1] : xB0[r + 1]),
+                  false, false);
+              const auto qb = __builtin_amdgcn_permlane16_swap(pb[0], pb[1], false, false);
+              dA0 = __builtin_amdgcn_mfma_f32_16x16x4f32(w, __uint_as_float(qa[0]), dA0, 0, 0, 0);
+              dA1 = __builtin_amdgcn_mfma_f32_16x16x4f32(w, __uint_as_float(qa[1]), dA1, 0, 0, 0);
+              dB0 = __builtin_amdgcn_mfma_f32_16x16x4f32(w, __uint_as_float(qb[0]), dB0, 0, 0, 0);
+              dB1 = __builtin_amdgcn_mfma_f32_16x16x4f32(w, __uint_as_float(qb[1]), dB1, 0, 0, 0);
+            }
+          }
+          // lane l holds units 4 (l >> 4) + i of item (l & 15) of its block; a 4 x 4 transpose
+          // of (block set, 16-lane row) by permlane32 + permlane16 swaps brings all 16 units
+          // of (user h, item l & 31) into lane l, the lane that holds that pair's chain
+          const float* b16 = img + (meta & 0xffff) + g4 * 256;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const auto x02 = __builtin_amdgcn_permlane32_swap(__float_as_uint(dA0[i]),
+                                                              __float_as_uint(dB0[i]), false, false);
+            const auto x13 = __builtin_amdgcn_permlane32_swap(__float_as_uint(dA1[i]),
+                                                              __float_as_uint(dB1[i]), false, false);
+            const auto y01 = __builtin_amdgcn_permlane16_swap(x02[0], x13[0], false, false);
+            const auto y23 = __builtin_amdgcn_permlane16_swap(x02[1], x13[1], false, false);
+            dA0[i] = __uint_as_float(y01[0]);  // unit i
+            dA1[i] = __uint_as_float(y01[1]);  // unit 4 + i
+            dB0[i] = __uint_as_float(y23[0]);  // unit 8 + i
+            dB1[i] = __uint_as_float(y23[1]);  // unit 12 + i
+          }
+#pragma unroll
+          for (int u = 0; u < 16; ++u) {
+            if (u < a.dl) {
+              const float v = (u < 4 ? dA0 : u < 8 ? dA1 : u < 12 ? dB0 : dB1)[u & 3];
+              s = fmaf(wm[u], fmaxf(v + b16[u], 0.f), s);
+            }
+          }
+        } else {
         // MLP terms of the chain: one permlane32 swap of (x_A, x_B) gives every lane of half 0
         // user A's even (r[0]) and odd (r[1]) units, and every lane of half 1 user B's
 #pragma unroll
@@ -448,6 +516,7 @@ __global__ __launch_bounds__(256, 2) void ncf_deep_mfma_kernel(DeepMArgs a) {
               s = fmaf(wm[jj + 1], __uint_as_float(sw[1]), s);  // wm zero past dl: exact
             }
           }
+        }
         }
       }
       float score = s + bpv;
@@ -524,12 +593,20 @@ static bool deep_mfma_layout(const hnm_ctx* ctx, const hnm_ncf_deep_weights* w, 
   for (int l = 0; l <= w->nl; ++l) pk.dims[l] = w->dims[l];
   int off = 0;
   o->nt = 1;
+  pk.last16 = w->nl >= 3 && w->dims[w->nl] <= 16;
   for (int l = 1; l < w->nl; ++l) {
     pk.w[l] = w->w[l];
     pk.b[l] = w->b[l];
+    pk.aoff[l] = off;
+    if (pk.last16 && l == w->nl - 1) {  // 16x16x4 steps of 4 input units, bias 16 floats
+      pk.ks4[l] = (int)hnm_cdiv(hnm_cdiv(w->dims[l], 4), 4);
+      pk.nt[l] = 1;
+      pk.boff[l] = off + pk.ks4[l] * 256;
+      off = pk.boff[l] + 16;
+      continue;
+    }
     pk.ks4[l] = (int)hnm_cdiv(hnm_cdiv(w->dims[l], 2), 4);
     pk.nt[l] = (int)hnm_cdiv(w->dims[l + 1], 32);
-    pk.aoff[l] = off;
     pk.boff[l] = off + pk.nt[l] * pk.ks4[l] * 256;
     off = pk.boff[l] + pk.nt[l] * 32;
     o->nt = std::max(o->nt, pk.nt[l]);
@@ -599,6 +676,7 @@ static hnm_status deep_mfma_tables(hnm_ctx* ctx, const hnm_ncf_deep_weights* w,
   m.nl = w->nl;
   m.dl = w->dims[w->nl];
   m.img_n = lay.pk.img_n;
+  m.last16 = lay.pk.last16;
   for (int l = 1; l < w->nl; ++l)
     m.meta[l] = lay.pk.aoff[l] | lay.pk.ks4[l] << 16 | lay.pk.nt[l] << 20;
   m.K = 1;
