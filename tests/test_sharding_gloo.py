@@ -91,7 +91,7 @@ def _worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2])
+@pytest.mark.parametrize("world", [2, 3, 8])
 def test_item_sharded_recommend_matches_single_process(world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
