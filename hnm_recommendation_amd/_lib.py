@@ -17,7 +17,7 @@ PKG = os.path.dirname(os.path.abspath(__file__))
 # from tools/; the in-tree build is the product and the default)
 LIB_PATH = os.environ.get("HNM_LIB_PATH") or os.path.join(PKG, "libhnm_mi355x.so")
 
-HNM_OK, HNM_EINVAL, HNM_EOOB, HNM_EHIP, HNM_ENOMEM, HNM_EUNSUPPORTED = 0, -1, -2, -3, -4, -5
+HNM_OK, HNM_EINVAL, HNM_EOOB, HNM_EHIP, HNM_ENOMEM, HNM_EUNSUPPORTED, HNM_ECOLL = 0, -1, -2, -3, -4, -5, -6
 
 _p = C.c_void_p
 _i64 = C.c_int64
@@ -108,6 +108,10 @@ _SIGS = {
     "hnm_ncf_pair_scores_f32": (_i32, [_p, C.POINTER(NcfWeights), _p, _p, _i64, _p]),
     "hnm_ncf_prefilter_debug_f32": (_i32, [_p, C.POINTER(NcfWeights), _p, _i64, _p, _i64, _p]),
     "hnm_topk_merge_f32": (_i32, [_p, _p, _p, _i64, _i64, _i64, _i64, C.c_int, C.c_int, _p, _p]),
+    "hnm_rccl_unique_id": (_i32, [_p, _i64]),
+    "hnm_ctx_rccl_init": (_i32, [_p, C.c_int, C.c_int, _p, _i64]),
+    "hnm_ctx_set_rccl_comm": (_i32, [_p, _p]),
+    "hnm_topk_allgather_merge_f32": (_i32, [_p, _p, _p, _i64, C.c_int, _p, _p]),
     "hnm_topk_rows_f32": (_i32, [_p, _p, _i64, _i64, _i64, _p, _p, C.c_int, _p, _p]),
     "hnm_csr_build_norm": (_i32, [_p, _p, _p, _i64, _i64, _p, _p, _p]),
     "hnm_spmm_plan_create": (_i32, [_p, _i64, _p, C.POINTER(_p)]),

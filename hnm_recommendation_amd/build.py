@@ -16,7 +16,7 @@ CSRC = os.path.join(PKG, "csrc")
 BUILD = os.path.join(REPO, "build", "obj")
 LIB = os.path.join(PKG, "libhnm_mi355x.so")
 SOURCES = ["api.hip", "score.hip", "dot_cert.hip", "ncf.hip", "ncf_cert.hip", "ncf_deep.hip", "graph.hip",
-           "widedeep.hip", "eval.hip", "topk_sort.hip"]
+           "widedeep.hip", "eval.hip", "topk_sort.hip", "collective.hip"]
 HEADERS = ["hnm_device.h", "hnm_internal.h", "dot_internal.h", "ncf_internal.h"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-Wall",
@@ -59,7 +59,8 @@ def build_library(force: bool = False, verbose: bool = True) -> str:
         raise RuntimeError("hipcc failed:\n" + "\n".join(errs))
     objs = [o for o, _ in results]
     if force or _mtime(LIB) < max(_mtime(o) for o in objs):
-        cmd = [HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", LIB, *objs]
+        cmd = [HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", LIB, *objs,
+               "-L/opt/rocm/lib", "-lrccl"]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")

@@ -57,6 +57,7 @@ extern "C" hnm_status hnm_ctx_destroy(hnm_ctx* ctx) {
   }
   free(ctx->ev0);
   free(ctx->ev1);
+  hnm_rccl_release(ctx);
   if (ctx->ws) (void)hipFree(ctx->ws);
   if (ctx->err_dev) (void)hipFree(ctx->err_dev);
   (void)hipEventDestroy(ctx->chain_ev);

@@ -30,6 +30,8 @@ struct hnm_ctx {
   int prefilter;                   // HNM_OPT_PREFILTER (default 1)
   int strided;                     // HNM_OPT_STRIDED (default 0)
   int deep_mfma;                   // HNM_OPT_DEEP_MFMA (default 1)
+  void* comm;                      // RCCL communicator (ncclComm_t) of the C-side exchange
+  int comm_owned;                  // 1: created by hnm_ctx_rccl_init, destroyed with the ctx
   unsigned long long* stats_dev;   // pre-filter counters: rows, candidates, fallback rows,
                                    // rows whose bound used the gated strided sample, and
                                    // (last NCF call) the gate's predicted proxy candidates
@@ -58,6 +60,7 @@ void hnm_timer_begin(hnm_ctx* ctx, int cls);
 void hnm_timer_end(hnm_ctx* ctx, int cls);
 
 void hnm_set_error(const char* fmt, ...);
+void hnm_rccl_release(hnm_ctx* ctx);  // collective.hip
 
 #define HNM_HIP_CHECK(expr)                                                        \
   do {                                                                             \

@@ -49,7 +49,8 @@ enum {
   HNM_EOOB = -2,         /* an id was out of range (reported by hnm_ctx_check) */
   HNM_EHIP = -3,         /* HIP runtime error */
   HNM_ENOMEM = -4,       /* workspace allocation failed */
-  HNM_EUNSUPPORTED = -5  /* shape outside what the kernels are built for */
+  HNM_EUNSUPPORTED = -5, /* shape outside what the kernels are built for */
+  HNM_ECOLL = -6         /* RCCL error (hnm_ctx_rccl_init, hnm_topk_allgather_merge_f32) */
 };
 
 typedef struct hnm_ctx hnm_ctx;
@@ -378,6 +379,23 @@ hnm_status hnm_widedeep_pair_scores_ex_f32(hnm_ctx* ctx, const hnm_widedeep_weig
 hnm_status hnm_topk_merge_f32(hnm_ctx* ctx, const float* cand_val, const int64_t* cand_idx,
                               int64_t B, int64_t G, int64_t gstride, int64_t bstride,
                               int kc, int k, float* out_val, int64_t* out_idx);
+
+/* ---- (e) item-sharded exchange from the C ABI, over RCCL (SURVEY §8(b) hnm_topk_allgather_merge)
+ * Every rank scores the SAME B users against its own item shard (global item ids) into [B, k]
+ * lists; hnm_topk_allgather_merge_f32 all-gathers the lists of the communicator's ranks on the
+ * ctx stream and merges them into the global top-k (score desc, item asc), identical on every
+ * rank.  Every rank must call it (B and k equal on all).  The communicator: hnm_rccl_unique_id
+ * on one rank (size >= 128 bytes), the bytes shared by the host, hnm_ctx_rccl_init on every
+ * rank (owned by the ctx); or hnm_ctx_set_rccl_comm with the host's own ncclComm_t (borrowed;
+ * NULL detaches).  The Python mirror's exchange (sharding.py, torch.distributed) adds a
+ * certified bound exchange before the shard scans; this is the single-phase form. */
+hnm_status hnm_rccl_unique_id(void* out, int64_t size);
+hnm_status hnm_ctx_rccl_init(hnm_ctx* ctx, int world, int rank, const void* unique_id,
+                             int64_t size);
+hnm_status hnm_ctx_set_rccl_comm(hnm_ctx* ctx, void* comm);
+hnm_status hnm_topk_allgather_merge_f32(hnm_ctx* ctx, const float* local_val,
+                                        const int64_t* local_idx, int64_t B, int k,
+                                        float* out_val, int64_t* out_idx);
 
 /* The item-shard exchange's candidate lists as int32 pairs (one all_to_all): pairs[2e] = the
  * bits of val[e], pairs[2e+1] = idx[e] + offset (idx < 0 stays; global ids < 2^31); pairs

@@ -132,3 +132,71 @@ def _rccl_worker(rank, port):
 
 def test_rccl_one_rank_exchange_matches_single_gpu():
     mp.spawn(_rccl_worker, args=(_free_port(),), nprocs=1, join=True)
+
+
+def _c_exchange_worker(rank):
+    """hnm_topk_allgather_merge_f32 (the C-ABI exchange, csrc/collective.hip) on a 1-rank RCCL
+    communicator the library creates itself: unsorted lists with ties and empty slots come back
+    as the (score desc, item asc) top-k; the dot top-k of a 3-shard split merged by the library
+    equals the unsharded call; no communicator -> ValueError; B = 0 is a no-op."""
+    import ctypes as C
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    c = _lib.ctx(dev)
+    f = _lib.fn
+    B, k = 300, 12
+    # without a communicator the entry refuses
+    v = torch.zeros(B, k, device=dev)
+    i = torch.zeros(B, k, dtype=torch.int64, device=dev)
+    with pytest.raises(ValueError):
+        _lib.check(f("hnm_topk_allgather_merge_f32")(c, _lib.ptr(v), _lib.ptr(i), B, k,
+                                                     _lib.ptr(v), _lib.ptr(i)), "merge")
+    uid = (C.c_char * 128)()
+    _lib.check(f("hnm_rccl_unique_id")(uid, 128), "unique_id")
+    _lib.check(f("hnm_ctx_rccl_init")(c, 1, 0, uid, 128), "rccl_init")
+    # (1) unsorted lists, ties, empty (-inf, -1) slots
+    g = torch.Generator().manual_seed(3)
+    lv = torch.randint(0, 6, (B, k), generator=g).float().to(dev)
+    li = torch.stack([torch.randperm(1000, generator=g)[:k] for _ in range(B)]).to(dev)
+    lv[:, -2:] = -float("inf")
+    li[:, -2:] = -1
+    ov = torch.empty(B, k, device=dev)
+    oi = torch.empty(B, k, dtype=torch.int64, device=dev)
+    _lib.check(f("hnm_topk_allgather_merge_f32")(c, _lib.ptr(lv), _lib.ptr(li), B, k,
+                                                 _lib.ptr(ov), _lib.ptr(oi)), "merge")
+    torch.cuda.synchronize()
+    ref_i = li.cpu().numpy().copy()
+    ref_v = lv.cpu().numpy().copy()
+    for b in range(B):
+        key = np.lexsort((np.where(ref_i[b] < 0, 1 << 40, ref_i[b]), -ref_v[b].astype(np.float64)))
+        ref_i[b], ref_v[b] = ref_i[b][key], ref_v[b][key]
+    np.testing.assert_array_equal(oi.cpu().numpy(), ref_i)
+    np.testing.assert_array_equal(ov.cpu().numpy(), ref_v)
+    # (2) three item shards of a dot-product model, scored with global ids, merged
+    U, I, d = 5000, 30_001, 64
+    sd = syn.lightgcn_state_dict(U, I, d, seed=4)
+    ut = torch.from_numpy(sd["embeddings.weight"][:U]).to(dev)
+    it = torch.from_numpy(sd["embeddings.weight"][U:]).to(dev)
+    users = torch.from_numpy(syn.user_batch(U, B, seed=2)).to(dev)
+    full = S.dot_shard_topk(ut, it, 0, I, k)(users)
+    parts = []
+    for r in range(3):
+        lo, hi = S.shard_range(I, r, 3)
+        pv, pi = S.dot_shard_topk(ut, it, lo, hi, k)(users)
+        parts.append((pv, torch.where(pi >= 0, pi + lo, pi)))
+    # world 1: the three shards' lists side by side as one rank's k' = 3k candidates
+    cv = torch.cat([p[0] for p in parts], 1).contiguous()
+    ci = torch.cat([p[1] for p in parts], 1).contiguous()
+    mv = torch.empty(B, 3 * k, device=dev)
+    mi = torch.empty(B, 3 * k, dtype=torch.int64, device=dev)
+    _lib.check(f("hnm_topk_allgather_merge_f32")(c, _lib.ptr(cv), _lib.ptr(ci), B, 3 * k,
+                                                 _lib.ptr(mv), _lib.ptr(mi)), "merge shards")
+    _same((mv[:, :k].contiguous(), mi[:, :k].contiguous()), full, "C exchange, 3 shards")
+    # (3) B = 0
+    _lib.check(f("hnm_topk_allgather_merge_f32")(c, None, None, 0, k, None, None), "merge B=0")
+    torch.cuda.synchronize()
+    _lib.check(f("hnm_ctx_set_rccl_comm")(c, None), "detach")
+
+
+def test_c_abi_rccl_exchange_one_rank():
+    mp.spawn(_c_exchange_worker, nprocs=1, join=True)

@@ -16,5 +16,5 @@ objs=()
 for o in "$ROOT"/build/obj/*.o; do
   [ "$(basename "$o" .o)" = "$base" ] && objs+=("$ROOT/tools/bin/obj_$TAG/$base.o") || objs+=("$o")
 done
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$ROOT/tools/bin/libhnm_$TAG.so" "${objs[@]}"
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$ROOT/tools/bin/libhnm_$TAG.so" "${objs[@]}" -L/opt/rocm/lib -lrccl
 echo "built tools/bin/libhnm_$TAG.so"
