@@ -49,6 +49,14 @@ extern "C" hnm_status hnm_ctx_rccl_init(hnm_ctx* ctx, int world, int rank, const
   HNM_REQUIRE(ctx && unique_id && size >= (int64_t)sizeof(ncclUniqueId) && world >= 1 &&
                   rank >= 0 && rank < world,
               HNM_EINVAL, "ctx_rccl_init: bad argument (world %d, rank %d)", world, rank);
+  // RCCL binds the communicator to the current device: the ctx's, for this call only (the
+  // caller's current device is restored on every exit path)
+  int prev = -1;
+  HNM_HIP_CHECK(hipGetDevice(&prev));
+  struct Restore {
+    int dev;
+    ~Restore() { (void)hipSetDevice(dev); }
+  } restore{prev};
   HNM_HIP_CHECK(hipSetDevice(ctx->device));
   ncclUniqueId id;
   memcpy(&id, unique_id, sizeof(id));
