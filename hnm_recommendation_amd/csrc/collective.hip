@@ -97,9 +97,12 @@ extern "C" hnm_status hnm_topk_allgather_merge_f32(hnm_ctx* ctx, const float* lv
   float* av = (float*)ws;
   int64_t* ai = (int64_t*)((char*)ws + szV);
   HNM_RCCL_CHECK(ncclGroupStart());
-  HNM_RCCL_CHECK(ncclAllGather(lval, av, n, ncclFloat32, comm, ctx->stream));
-  HNM_RCCL_CHECK(ncclAllGather(lidx, ai, n, ncclInt64, comm, ctx->stream));
-  HNM_RCCL_CHECK(ncclGroupEnd());
+  // the group is closed on every path, a failed enqueue included
+  const ncclResult_t r0 = ncclAllGather(lval, av, n, ncclFloat32, comm, ctx->stream);
+  const ncclResult_t r1 =
+      r0 == ncclSuccess ? ncclAllGather(lidx, ai, n, ncclInt64, comm, ctx->stream) : r0;
+  const ncclResult_t r2 = ncclGroupEnd();
+  HNM_RCCL_CHECK(r1 != ncclSuccess ? r1 : r2);
   if (B <= 0) return HNM_OK;
   // gathered [world][B][k]: group g = rank g's lists
   return hnm_topk_merge_f32(ctx, av, ai, B, world, (int64_t)n, k, k, k, gval, gidx);
