@@ -25,7 +25,7 @@ step bench_ncf_personal 300 python bench.py --weights personal --no-cpu-baseline
 HNM_DIST_BACKEND=gloo step bench_2rank 400 python bench.py --gpus 2 --workload lightgcn128 --steps 5 --warmup 2
 if [ -n "$PROF" ]; then
   cd /tmp && export TMPDIR=/tmp
-  for w in ncf lightgcn widedeep mf; do
+  for w in ncf lightgcn widedeep mf ncf_deep; do
     extra=""  # the bench defaults, so the averages match the bench line's HIP-event timing
     [ $w = widedeep ] && extra="--steps 3 --warmup 1"
     echo "== prof $w $(date +%T)"
