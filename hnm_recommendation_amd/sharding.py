@@ -26,6 +26,7 @@ kernels (`ncf_shard_topk`, `dot_shard_topk`, `hip_merge`).
 """
 from __future__ import annotations
 
+import ctypes as C
 from typing import Callable, Optional, Tuple
 
 import torch
@@ -200,7 +201,14 @@ class ncf_shard_topk:
 
     Called directly: one hnm_ncf_topk_f32.  `begin` / `finish`: the two phases of
     hnm_ncf_topk_begin_f32 / _finish_f32 around a cross-shard bound exchange.  `history`
-    (a UserHistory): mask each user's history items, gathered on the device per call."""
+    (a UserHistory): mask each user's history items, gathered on the device per call.
+    A model whose tower the fused kernels do not take (any other `mlp_dims`) gets an
+    `ncf_deep_shard_topk` instead."""
+
+    def __new__(cls, model, lo: int, hi: int, k: int, history=None):
+        if cls is ncf_shard_topk and not model._fused():
+            return ncf_deep_shard_topk(model, lo, hi, k, history)
+        return super().__new__(cls)
 
     def __init__(self, model, lo: int, hi: int, k: int, history=None):
         self.model, self.lo, self.hi, self.k = model, lo, hi, k
@@ -267,6 +275,35 @@ class ncf_shard_topk:
                                                       _lib.ptr(mp), _lib.ptr(mi), kk, _lib.ptr(lb),
                                                       1, _lib.ptr(out_v), _lib.ptr(out_i)),
                    "hnm_ncf_topk_finish_f32")
+        return _pad(out_v, out_i, self.k)
+
+
+class ncf_deep_shard_topk:
+    """NeuralCF towers other than the fused two-layer one over item rows [lo, hi):
+    hnm_ncf_deep_topk_f32 on the shard's item tables (fp32-MFMA tile kernel with fused
+    per-partition top-k lists, scores bitwise the unsharded ones).  Single-phase: the exchange
+    merges every shard's k best (no bound exchange), so k <= 64."""
+
+    def __init__(self, model, lo: int, hi: int, k: int, history=None):
+        if k > 64:
+            raise ValueError("ncf_deep_shard_topk: k <= 64 (the fused deep top-k)")
+        self.model, self.lo, self.hi, self.k = model, lo, hi, k
+        self.history = history
+
+    def __call__(self, user_ids: torch.Tensor):
+        w, keep = self.model._deep_weights()
+        w = _lib.NcfDeepWeights.from_buffer_copy(w)
+        w.gmf_item = w.gmf_item + self.lo * self.model.mf_dim * 4
+        w.mlp_item = w.mlp_item + self.lo * (self.model.mlp_dims[0] // 2) * 4
+        w.num_items = self.hi - self.lo
+        u = user_ids.to(torch.int64).contiguous()
+        kk = min(self.k, self.hi - self.lo)
+        mp, mi = _mask(self.history, u, self.lo, self.hi)
+        out_v = torch.empty(u.numel(), kk, dtype=torch.float32, device=u.device)
+        out_i = torch.empty(u.numel(), kk, dtype=torch.int64, device=u.device)
+        _lib.check(_lib.fn("hnm_ncf_deep_topk_f32")(
+            _lib.ctx(u.device), C.byref(w), _lib.ptr(u), u.numel(), _lib.ptr(mp), _lib.ptr(mi),
+            kk, _lib.ptr(out_v), _lib.ptr(out_i)), "hnm_ncf_deep_topk_f32")
         return _pad(out_v, out_i, self.k)
 
 

@@ -7,7 +7,8 @@ scored as neural_cf.py:131-141 and ranked as neural_cf.py:300-326).
   (score desc, item asc) order of those dense rows exactly, filtered and unfiltered, at both
   users-per-wave variants and on towers with one and two 32-unit tiles, odd widths, a single
   Linear, mf not a multiple of 8 and 7 layers; the wide-tower route (dense chunk + row top-k
-  inside the library) gives the same lists.
+  inside the library) gives the same lists; item shards (sharding.ncf_deep_shard_topk) merge to
+  the unsharded lists.
 * Rows against the CPU oracle (oracle/hnm_oracle.py ncf_predict_all_items) within the fp32
   tolerance of tests/parity.py.
 """
@@ -113,3 +114,31 @@ def test_deep_mfma_full_catalogue_topk():
     ref = O.ncf_predict_all_items(sd, users_np[rows])
     got = m.predict_all_items(users[rows]).cpu().numpy()
     assert_scores_close(got, ref, "deep full-catalogue rows")
+
+
+def test_deep_item_shards_merge_to_the_unsharded_topk():
+    """Item-sharded deep towers (sharding.ncf_shard_topk -> ncf_deep_shard_topk on shard tables,
+    ragged shards, with the history filter): the shards' lists merged by hnm_topk_merge_f32 are
+    bitwise the unsharded fused top-k."""
+    from hnm_recommendation_amd import sharding as S
+    from hnm_recommendation_amd import UserHistory
+    U, I, K, B = 900, 7001, 12, 260
+    m, _ = model(U, I, 64, (128, 64, 32, 16), seed=8)
+    users_np = syn.user_batch(U, B, seed=5)
+    users = torch.from_numpy(users_np).to(DEV)
+    rng = np.random.default_rng(2)
+    filt = {int(u): set(int(x) for x in rng.integers(0, I, 30)) for u in users_np[::4]}
+    hist = UserHistory(filt, U, I, torch.device(DEV))
+    for f, h in ((None, None), (filt, hist)):
+        full_v, full_i = m.recommend_with_scores(users, filter_items=f, k=K)
+        vs, is_ = [], []
+        for r in range(3):
+            lo, hi = S.shard_range(I, r, 3)
+            sc = S.ncf_shard_topk(m, lo, hi, K, history=h)
+            assert isinstance(sc, S.ncf_deep_shard_topk)
+            v, i = sc(users)
+            vs.append(v)
+            is_.append(torch.where(i >= 0, i + lo, i))
+        mv, mi = S.hip_merge(torch.stack(vs).contiguous(), torch.stack(is_).contiguous(), K)
+        assert torch.equal(mi, full_i)
+        assert torch.equal(mv.view(torch.int32), full_v.view(torch.int32))
