@@ -708,6 +708,32 @@ __global__ __launch_bounds__(256) void dcert_tau_kernel(const float* __restrict_
   flag[b] = ok ? 0 : 1;
 }
 
+// One-shot calls (dot_cert_topk): dcert_bound_kernel's lower bound and dcert_tau_kernel's
+// threshold in one pass per row -- the same arithmetic, L kept in a register (one launch and one
+// kernel boundary less on the per-call latency chain).
+__global__ __launch_bounds__(256) void dcert_bound_tau_kernel(const float* __restrict__ kth,
+                                                              int K,
+                                                              const float* __restrict__ Nu,
+                                                              const float* __restrict__ ubr,
+                                                              const DParams* __restrict__ prm,
+                                                              int64_t B, float* __restrict__ tau,
+                                                              int* __restrict__ flag) {
+  const int64_t b = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (b >= B) return;
+  const float s = prm->s;
+  const float nimax = __uint_as_float(prm->mx[DM_NI]), ibmax = __uint_as_float(prm->mx[DM_IB]);
+  const float E = s * (DCERT_RHO * Nu[b] * nimax + 2.4e-7f * (fabsf(ubr[b]) + ibmax)) + prm->absb;
+  float l = (kth[b * K + (K - 1)] - E) / s + ubr[b];
+  l -= fabsf(l) * 4.76837158203125e-07f;  // 2^-21
+  if (!(!prm->bad && __builtin_isfinite(l) && __builtin_isfinite(E))) l = -__builtin_inff();
+  const float scale = s * (Nu[b] * nimax + fabsf(ubr[b]) + ibmax);
+  float tv = (l - ubr[b]) * s - E - 3.814697265625e-06f * scale;  // 2^-18
+  tv -= fabsf(tv) * 9.5367431640625e-07f;                          // 2^-20
+  const bool ok = !prm->bad && __builtin_isfinite(tv) && __builtin_isfinite(scale);
+  tau[b] = ok ? tv : __builtin_inff();
+  flag[b] = ok ? 0 : 1;
+}
+
 // ------------------------------------------------------------------ exact re-scoring
 // One wave per user; each lane re-scores one candidate with the sequential fp32 fma chain
 // (k = 0 .. DP-1, zero padding included) the f32 MFMA computes, then (acc + ub) + ib as
@@ -916,8 +942,8 @@ size_t dot_cert_bytes(int64_t B, int64_t I, int d, int K, int num_cus) {
 
 // Phase 1: bound statistics, f16 copies, the sample pass and every row's certified lower
 // bound of its exact K-th best score (real units) into lb (nullptr: kept in the scratch).
-hnm_status dot_cert_begin(hnm_ctx* ctx, const DotArgs& a, bool bias, void* scratch, float* lb,
-                          float* lists) {
+static hnm_status dot_cert_begin_impl(hnm_ctx* ctx, const DotArgs& a, bool bias, void* scratch,
+                                      float* lb, float* lists, bool fused) {
   const DotCertShape sh = dcert_shape(a.B, a.I, a.d, a.K, ctx->num_cus);
   DotCertWs x;
   dcert_carve((char*)scratch, a.B, a.I, a.d, a.K, ctx->num_cus, &x);
@@ -939,6 +965,7 @@ hnm_status dot_cert_begin(hnm_ctx* ctx, const DotArgs& a, bool bias, void* scrat
   st = hnm_sample_kth(ctx, x.sdense, nmax_cols, a.B, nmax_cols, nullptr, nullptr, a.K, 1, 1,
                       nullptr, x.kthv);
   if (st) return st;
+  if (fused) return HNM_OK;  // bound + threshold in dot_cert_finish_impl's first kernel
   hipLaunchKernelGGL(dcert_bound_kernel, dim3((unsigned)hnm_cdiv(a.B, 256)), dim3(256), 0,
                      ctx->stream, x.kthv, a.K, x.Nu, x.ubr, x.prm, a.B, lb ? lb : x.lb, x.E);
   HNM_LAUNCH_CHECK();
@@ -950,16 +977,27 @@ hnm_status dot_cert_begin(hnm_ctx* ctx, const DotArgs& a, bool bias, void* scrat
   return HNM_OK;
 }
 
+hnm_status dot_cert_begin(hnm_ctx* ctx, const DotArgs& a, bool bias, void* scratch, float* lb,
+                          float* lists) {
+  return dot_cert_begin_impl(ctx, a, bias, scratch, lb, lists, false);
+}
+
 // Phase 2: thresholds from lower bounds lb (this call's, or the max over item shards), the
-// main f16 scan, exact re-scoring + top-K, the exact LIST scan for unusable rows.
-hnm_status dot_cert_finish(hnm_ctx* ctx, const DotArgs& a, bool bias, void* scratch,
-                           const float* lb, int short_ok, float* ov, int64_t* oi) {
+// main f16 scan, exact re-scoring + top-K, the exact LIST scan for unusable rows.  fused: the
+// one-shot call, thresholds straight from the sample K-th (dcert_bound_tau_kernel).
+static hnm_status dot_cert_finish_impl(hnm_ctx* ctx, const DotArgs& a, bool bias, void* scratch,
+                                       const float* lb, int short_ok, float* ov, int64_t* oi,
+                                       bool fused) {
   const DotCertShape sh = dcert_shape(a.B, a.I, a.d, a.K, ctx->num_cus);
   DotCertWs x;
   dcert_carve((char*)scratch, a.B, a.I, a.d, a.K, ctx->num_cus, &x);
   const int64_t ublocks = hnm_cdiv(a.B, dscan_users(sh.DP, DSCAN_THRESH));
-  hipLaunchKernelGGL(dcert_tau_kernel, dim3((unsigned)hnm_cdiv(a.B, 256)), dim3(256), 0,
-                     ctx->stream, lb ? lb : x.lb, x.Nu, x.ubr, x.prm, a.B, x.tau, x.flag);
+  if (fused)
+    hipLaunchKernelGGL(dcert_bound_tau_kernel, dim3((unsigned)hnm_cdiv(a.B, 256)), dim3(256), 0,
+                       ctx->stream, x.kthv, a.K, x.Nu, x.ubr, x.prm, a.B, x.tau, x.flag);
+  else
+    hipLaunchKernelGGL(dcert_tau_kernel, dim3((unsigned)hnm_cdiv(a.B, 256)), dim3(256), 0,
+                       ctx->stream, lb ? lb : x.lb, x.Nu, x.ubr, x.prm, a.B, x.tau, x.flag);
   HNM_LAUNCH_CHECK();
   {  // main f16 scan: append approx >= tau_u
     DScanArgs s = dscan_args(x, a);
@@ -997,11 +1035,16 @@ hnm_status dot_cert_finish(hnm_ctx* ctx, const DotArgs& a, bool bias, void* scra
   return dot_list_pass(ctx, af, bias, x.cv, x.ci, ov, oi);
 }
 
+hnm_status dot_cert_finish(hnm_ctx* ctx, const DotArgs& a, bool bias, void* scratch,
+                           const float* lb, int short_ok, float* ov, int64_t* oi) {
+  return dot_cert_finish_impl(ctx, a, bias, scratch, lb, short_ok, ov, oi, false);
+}
+
 hnm_status dot_cert_topk(hnm_ctx* ctx, const DotArgs& a, bool bias, void* scratch, float* ov,
                          int64_t* oi) {
-  hnm_status st = dot_cert_begin(ctx, a, bias, scratch, nullptr);
+  hnm_status st = dot_cert_begin_impl(ctx, a, bias, scratch, nullptr, nullptr, true);
   if (st) return st;
-  return dot_cert_finish(ctx, a, bias, scratch, nullptr, 0, ov, oi);
+  return dot_cert_finish_impl(ctx, a, bias, scratch, nullptr, 0, ov, oi, true);
 }
 
 hnm_status dot_cert_debug(hnm_ctx* ctx, const DotArgs& a, bool bias, void* scratch,
