@@ -389,6 +389,8 @@ def serve_latency(args, device):
     U, I = syn.HM_USERS, syn.HM_ITEMS
     if args.workload == "ncf":
         m = load(NeuralCF(U, I), syn.ncf_state_dict(U, I, 64, (128, 64, 32), seed=0), device)
+        if not os.environ.get("HNM_BENCH_NO_ITEM_CACHE"):
+            m.cache_item_tables()  # what serving.Recommender does with a server's fixed weights
     elif args.workload in ("lightgcn", "lightgcn128"):
         d = 64 if args.workload == "lightgcn" else 128
         m = LightGCN(U, I, embedding_dim=d, num_layers=3)

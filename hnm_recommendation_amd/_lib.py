@@ -30,7 +30,7 @@ class NcfWeights(C.Structure):
     _fields_ = [("gmf_user", _p), ("gmf_item", _p), ("mlp_user", _p), ("mlp_item", _p),
                 ("w1", _p), ("b1", _p), ("w2", _p), ("b2", _p), ("wp", _p), ("bp", _p),
                 ("num_users", _i64), ("num_items", _i64), ("mf", _i32), ("h0", _i32),
-                ("h1", _i32), ("h2", _i32)]
+                ("h1", _i32), ("h2", _i32), ("item_proj", _p)]
 
 
 class NcfDeepWeights(C.Structure):
@@ -102,6 +102,7 @@ _SIGS = {
     "hnm_ncf_topk_finish_f32": (_i32, [_p, C.POINTER(NcfWeights), _p, _i64, _p, _p, C.c_int, _p,
                                        C.c_int, _p, _p]),
     "hnm_ncf_scores_f32": (_i32, [_p, C.POINTER(NcfWeights), _p, _i64, _p, _i64]),
+    "hnm_ncf_item_proj_f32": (_i32, [_p, C.POINTER(NcfWeights), _p]),
     "hnm_ncf_deep_scores_f32": (_i32, [_p, C.POINTER(NcfDeepWeights), _p, _i64, _p, _p, _i64]),
     "hnm_ncf_deep_topk_f32": (_i32, [_p, C.POINTER(NcfDeepWeights), _p, _i64, _p, _p, C.c_int,
                                      _p, _p]),

@@ -630,8 +630,10 @@ static hnm_status ncf_tables(hnm_ctx* ctx, const hnm_ncf_weights* w, const int64
   const int H1P = big ? 128 : 64, GW = big ? 128 : 64;
   const int64_t I = w->num_items;
   const bool gcopy = (big ? w->mf != GW : w->mf % 4 != 0) || ((uintptr_t)w->gmf_item % 16 != 0);
+  const bool qcache = w->item_proj != nullptr;  // the caller's item projection (fixed tables)
   const size_t szP = hnm_align((size_t)B * H1P * 4), szW = hnm_align((size_t)B * GW * 4);
-  const size_t szQ = hnm_align((size_t)I * H1P * 4), szG = gcopy ? hnm_align((size_t)I * GW * 4) : 0;
+  const size_t szQ = qcache ? 0 : hnm_align((size_t)I * H1P * 4);
+  const size_t szG = gcopy ? hnm_align((size_t)I * GW * 4) : 0;
   void* wsp = ctx->ws;
   hnm_status st = HNM_OK;
   if (fill) {
@@ -654,19 +656,21 @@ static hnm_status ncf_tables(hnm_ctx* ctx, const hnm_ncf_weights* w, const int64
     G = Gc;
     ldg = GW;
   }
-  out->t = {Pu, WGu, Qi, G, ldg};
+  out->t = {Pu, WGu, qcache ? w->item_proj : Qi, G, ldg};
   if (!fill) return HNM_OK;
   if (w->h1 < H1P) {
     HNM_HIP_CHECK(hipMemsetAsync(Pu, 0, szP, ctx->stream));
-    HNM_HIP_CHECK(hipMemsetAsync(Qi, 0, szQ, ctx->stream));
+    if (!qcache) HNM_HIP_CHECK(hipMemsetAsync(Qi, 0, szQ, ctx->stream));
   }
   // P_u = W1[:, :h0] m_u + b1 ; Q_i = W1[:, h0:] m_i  (pair-permuted, lane-half order)
   st = hnm_linear_rows_f32(ctx, w->mlp_user, w->h0, ids, w->num_users, B, w->h0, w->w1,
                            2 * w->h0, w->b1, w->h1, Pu, H1P, 1);
   if (st) return st;
-  st = hnm_linear_rows_f32(ctx, w->mlp_item, w->h0, nullptr, I, I, w->h0, w->w1 + w->h0,
-                           2 * w->h0, nullptr, w->h1, Qi, H1P, 1);
-  if (st) return st;
+  if (!qcache) {
+    st = hnm_linear_rows_f32(ctx, w->mlp_item, w->h0, nullptr, I, I, w->h0, w->w1 + w->h0,
+                             2 * w->h0, nullptr, w->h1, Qi, H1P, 1);
+    if (st) return st;
+  }
   hipLaunchKernelGGL(gather_scale_kernel, dim3((unsigned)hnm_cdiv(B, 4)), dim3(256), 0,
                      ctx->stream, w->gmf_user, w->num_users, w->mf, w->mf, ids, B, w->wp, WGu,
                      GW, ctx->err_dev, big ? 0 : 1);
@@ -824,6 +828,17 @@ extern "C" hnm_status hnm_ncf_topk_finish_f32(hnm_ctx* ctx, const hnm_ncf_weight
   if (st) return st;
   return ncf_cert_finish(ctx, w, c.t, B, mask_ptr, mask_idx, k, c.extra, lower_bound,
                          short_ok, out_val, out_idx);
+}
+
+extern "C" hnm_status hnm_ncf_item_proj_f32(hnm_ctx* ctx, const hnm_ncf_weights* w, float* out) {
+  hnm_status st = ncf_check(w);
+  if (st) return st;
+  HNM_REQUIRE(ctx && out, HNM_EINVAL, "ncf_item_proj: NULL argument");
+  const int H1P = (w->h1 > 64 || w->mf > 64) ? 128 : 64;  // ncf_tables' layout
+  const int64_t I = w->num_items;
+  if (w->h1 < H1P) HNM_HIP_CHECK(hipMemsetAsync(out, 0, (size_t)I * H1P * 4, ctx->stream));
+  return hnm_linear_rows_f32(ctx, w->mlp_item, w->h0, nullptr, I, I, w->h0, w->w1 + w->h0,
+                             2 * w->h0, nullptr, w->h1, out, H1P, 1);
 }
 
 extern "C" hnm_status hnm_ncf_scores_f32(hnm_ctx* ctx, const hnm_ncf_weights* w,

@@ -142,6 +142,7 @@ class NeuralCF(RecModule):
         key = tuple(p.data_ptr() for p in params)
         cached = getattr(self, "_wcache", None)
         if cached is not None and cached[0] == key:
+            self._attach_item_proj(cached[1], cached[2])
             return cached[1], cached[2]
         keep = [f32c(p) for p in params]
         keep[8] = keep[8].reshape(-1)
@@ -151,7 +152,36 @@ class NeuralCF(RecModule):
                             l2.out_features)
         if all(t.data_ptr() == p.data_ptr() for t, p in zip(keep, params)):
             self._wcache = (key, w, keep)   # no conversion copies: safe to reuse
+        self._attach_item_proj(w, keep)
         return w, keep
+
+    def cache_item_tables(self, enabled: bool = True) -> "NeuralCF":
+        """Keep the item half of layer 1 (W1[:, h0:] m_i for every item, 27 MB at the H&M
+        catalogue) between calls instead of recomputing it in every recommend call (22 us of
+        kernel time a call: most of a B = 1 request's scoring).  For frozen weights -- a server
+        (`serving.Recommender` turns it on); the cache is keyed on the item table's and W1's
+        storage and torch version counters, so in-place updates through the parameters
+        (optimizer steps, load_state_dict) rebuild it, but writes through `.data` do not."""
+        self._item_cache_on = bool(enabled)
+        if not enabled:
+            self._item_proj = None
+        return self
+
+    def _attach_item_proj(self, w, keep):
+        if not getattr(self, "_item_cache_on", False):
+            w.item_proj = None
+            return
+        mi, w1 = self.mlp_item_embedding.weight, self._linears()[0].weight
+        key = (mi.data_ptr(), mi._version, w1.data_ptr(), w1._version, self.num_items)
+        cached = getattr(self, "_item_proj", None)
+        if cached is None or cached[0] != key:
+            w.item_proj = None
+            h1p = 128 if (w.h1 > 64 or w.mf > 64) else 64
+            proj = torch.empty(self.num_items, h1p, dtype=torch.float32, device=keep[0].device)
+            _lib.check(_lib.fn("hnm_ncf_item_proj_f32")(_lib.ctx(proj.device), C.byref(w),
+                                                        _lib.ptr(proj)), "hnm_ncf_item_proj_f32")
+            cached = self._item_proj = (key, proj)
+        w.item_proj = cached[1].data_ptr()
 
     # ------------------------------------------------------------------ reference API
     def forward(self, user_ids: torch.Tensor, item_ids: torch.Tensor) -> torch.Tensor:

@@ -103,6 +103,8 @@ class Recommender:
 
     def add_model(self, name: str, model, metrics: Optional[Dict[str, float]] = None):
         self.models[name] = model.to(self.device).eval()
+        if isinstance(model, NeuralCF) and model._fused():
+            model.cache_item_tables()  # a server's weights are fixed: keep the item projection
         self.model_metrics[name] = dict(metrics or {})
 
     def load_checkpoints(self, checkpoint_dir: str, graph=None) -> List[str]:

@@ -221,6 +221,8 @@ class ncf_shard_topk:
         mf, h0 = self.model.mf_dim, self.model.mlp_dims[0] // 2
         w.gmf_item = w.gmf_item + self.lo * mf * 4
         w.mlp_item = w.mlp_item + self.lo * h0 * 4
+        if w.item_proj:  # the model's cached item projection: this shard's rows
+            w.item_proj = w.item_proj + self.lo * (128 if (w.h1 > 64 or w.mf > 64) else 64) * 4
         w.num_items = self.hi - self.lo
         u = user_ids.to(torch.int64).contiguous()
         return w, keep, u, min(self.k, self.hi - self.lo)

@@ -208,7 +208,15 @@ typedef struct {
   int32_t h0;
   int32_t h1;
   int32_t h2;
+  /* Optional (NULL: computed per call): the item half of layer 1 for THESE num_items rows,
+   * W1[:, h0:] m_i pair-permuted, [num_items, 64] (h1 <= 64 and mf <= 64) or [num_items, 128],
+   * as hnm_ncf_item_proj_f32 writes it -- for callers whose item tables and W1 stay fixed
+   * between calls (a server); a row shard points at its first row. */
+  const float* item_proj;
 } hnm_ncf_weights;
+
+/* out = the item projection hnm_ncf_weights.item_proj takes (zero padded columns). */
+hnm_status hnm_ncf_item_proj_f32(hnm_ctx* ctx, const hnm_ncf_weights* w, float* out);
 
 hnm_status hnm_ncf_topk_f32(hnm_ctx* ctx, const hnm_ncf_weights* w, const int64_t* user_ids,
                             int64_t B, const int64_t* mask_ptr, const int32_t* mask_idx,

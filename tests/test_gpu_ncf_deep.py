@@ -142,3 +142,4 @@ def test_deep_item_shards_merge_to_the_unsharded_topk():
         mv, mi = S.hip_merge(torch.stack(vs).contiguous(), torch.stack(is_).contiguous(), K)
         assert torch.equal(mi, full_i)
         assert torch.equal(mv.view(torch.int32), full_v.view(torch.int32))
+
