@@ -214,3 +214,18 @@ def test_build_tracks_every_csrc_header():
     from hnm_recommendation_amd import build
     hdrs = {os.path.basename(p) for p in glob.glob(os.path.join(build.CSRC, "*.h"))}
     assert hdrs <= set(build.HEADERS), sorted(hdrs - set(build.HEADERS))
+
+
+def test_ncf_shard_scorer_dispatch():
+    """sharding.ncf_shard_topk gives the fused two-phase scorer for the default tower and
+    ncf_deep_shard_topk (single-phase, k <= 64) for any other tower (no GPU work at
+    construction)."""
+    from hnm_recommendation_amd import NeuralCF
+    from hnm_recommendation_amd import sharding as S
+    fused = S.ncf_shard_topk(NeuralCF(50, 40), 0, 40, 12)
+    assert type(fused) is S.ncf_shard_topk and hasattr(fused, "begin_lists")
+    deep = S.ncf_shard_topk(NeuralCF(50, 40, mlp_dims=[128, 64, 32, 16]), 10, 40, 12)
+    assert type(deep) is S.ncf_deep_shard_topk and not hasattr(deep, "begin_lists")
+    assert (deep.lo, deep.hi, deep.k) == (10, 40, 12)
+    with pytest.raises(ValueError):
+        S.ncf_shard_topk(NeuralCF(50, 40, mlp_dims=[64, 32]), 0, 40, 100)
