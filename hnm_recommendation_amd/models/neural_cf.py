@@ -180,6 +180,8 @@ class NeuralCF(RecModule):
             proj = torch.empty(self.num_items, h1p, dtype=torch.float32, device=keep[0].device)
             _lib.check(_lib.fn("hnm_ncf_item_proj_f32")(_lib.ctx(proj.device), C.byref(w),
                                                         _lib.ptr(proj)), "hnm_ncf_item_proj_f32")
+            # other threads' streams read the cache as soon as it is published: complete it first
+            torch.cuda.current_stream(proj.device).synchronize()
             cached = self._item_proj = (key, proj)
         w.item_proj = cached[1].data_ptr()
 
