@@ -457,10 +457,13 @@ __global__ __launch_bounds__(256, 2) void ncf_deep_mfma_kernel(DeepMArgs a) {
           const float* A16 = img + (meta & 0xffff) + 4 * lane;
           const f32x4 z = {0.f, 0.f, 0.f, 0.f};
           f32x4 dA0 = z, dA1 = z, dB0 = z, dB1 = z;  // (user, item block)
+          float4 w4 = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
           for (int st = 0; st < 8 * NT; ++st) {
             if (st < 4 * g4) {
-              const float w = A16[256 * (st >> 2) + (st & 3)];
+              // one conflict-free ds_read_b128 per 4 steps (lane-contiguous 16 B)
+              if ((st & 3) == 0) w4 = *reinterpret_cast<const float4*>(A16 + 256 * (st >> 2));
+              const float w = (st & 3) == 0 ? w4.x : (st & 3) == 1 ? w4.y : (st & 3) == 2 ? w4.z : w4.w;
               const int t = st >> 3, r = (2 * st) & 15;
               const auto pa = __builtin_amdgcn_permlane32_swap(
                   __float_as_uint(t ? xA1[r] : xA0[r]), __float_as_uint(t ? xA1[r + 1] : xA0[r + 1]),
