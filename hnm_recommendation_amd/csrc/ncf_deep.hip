@@ -220,15 +220,15 @@ __global__ __launch_bounds__(256) void deep_pack_kernel(DeepPack pk, float* __re
 #define DM_ACC(W0, W1, BA, BB) DM_STEP(W0, W1, BA, BB, cA0, cA1, cB0, cB1)
 
 template <int NT, int MFP, bool DENSE>
-__global__ __launch_bounds__(256, 2) void ncf_deep_mfma_kernel(DeepMArgs a) {
+__global__ __launch_bounds__(256, NT == 1 ? 3 : 2) void ncf_deep_mfma_kernel(DeepMArgs a) {
   constexpr int WU = DM_WU, NU = DM_NU;
   constexpr int GRS = MFP + 4;       // LDS row stride of the GMF tile
   constexpr int GF4 = MFP / 32;      // GMF tile float4 a thread (32 rows x MFP / 4)
   extern __shared__ float4 dm_lds4[];
   float* img = (float*)dm_lds4;
-  float* qs = img + a.img_n;              // [2][TILE][DM_QRS]
-  float* gs = qs + 2 * TILE * DM_QRS;     // [2][TILE][GRS]
-  float* ps = gs + 2 * TILE * GRS;        // [NU][DM_W]
+  float* qs = img + a.img_n;              // [TILE][DM_QRS] (one buffer: three workgroups a CU)
+  float* gs = qs + TILE * DM_QRS;         // [TILE][GRS]
+  float* ps = gs + TILE * GRS;            // [NU][DM_W]
   float* us = ps + NU * DM_W;             // [NU][MFP]  g_u rows (zero padded)
   float* wps = us + NU * MFP;             // [MFP + 64] wp: GMF part, MLP part (zero padded)
 
@@ -323,7 +323,7 @@ __global__ __launch_bounds__(256, 2) void ncf_deep_mfma_kernel(DeepMArgs a) {
   const f32x16 zero16 = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f,
                          0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   for (int64_t tt = 0; tt < ntiles; ++tt) {
-    const int buf = (int)(tt & 1);
+    const int buf = 0;
     const int64_t base = part_start + tt * TILE;
     if (tt + 1 < ntiles) load_tile(base + TILE);
     const float* qrow = &qs[(buf * TILE + j) * DM_QRS];
@@ -545,7 +545,10 @@ __global__ __launch_bounds__(256, 2) void ncf_deep_mfma_kernel(DeepMArgs a) {
     }
 
     // tile t + 1 into the other buffer (every wave finished reading it before the last barrier)
-    if (tt + 1 < ntiles) store_tile(buf ^ 1);
+    if (tt + 1 < ntiles) {
+      __syncthreads();
+      store_tile(0);
+    }
     __syncthreads();
   }
 
@@ -616,7 +619,7 @@ static bool deep_mfma_layout(const hnm_ctx* ctx, const hnm_ncf_deep_weights* w, 
   }
   pk.img_n = off;
   o->mfp = w->mf <= 32 ? 32 : w->mf <= 64 ? 64 : 128;
-  o->lds = (size_t)4 * (off + 2 * TILE * DM_QRS + 2 * TILE * (o->mfp + 4) + DM_NU * DM_W +
+  o->lds = (size_t)4 * (off + TILE * DM_QRS + TILE * (o->mfp + 4) + DM_NU * DM_W +
                         DM_NU * o->mfp + o->mfp + 64);
   return o->lds <= 160 * 1024 && off < 65536;
 }
@@ -690,7 +693,7 @@ static hnm_status deep_mfma_tables(hnm_ctx* ctx, const hnm_ncf_deep_weights* w,
 template <int NT, int MFP, bool DENSE>
 static hnm_status deep_mfma_launch1(hnm_ctx* ctx, DeepMArgs a, const DeepMLayout& lay) {
   const int64_t ublocks = hnm_cdiv(a.B, DM_NU);
-  const Partition part = choose_partition(a.num_items, ublocks, ctx->num_cus);
+  const Partition part = choose_partition(a.num_items, ublocks, ctx->num_cus, TILE, NT == 1 ? 3 : 2);
   a.ipp = part.ipp;
   a.NP = part.np;
   HNM_REQUIRE(ublocks < ((int64_t)1 << 31), HNM_EUNSUPPORTED, "ncf_deep: batch too large");
@@ -843,7 +846,7 @@ static hnm_status deep_topk_chunk(hnm_ctx* ctx, const hnm_ncf_deep_weights* w,
   DeepMLayout lay;
   hnm_status st;
   if (deep_mfma_layout(ctx, w, &lay)) {
-    const Partition part = choose_partition(I, hnm_cdiv(B, DM_NU), ctx->num_cus);
+    const Partition part = choose_partition(I, hnm_cdiv(B, DM_NU), ctx->num_cus, TILE, lay.nt == 1 ? 3 : 2);
     const size_t szC = hnm_align((size_t)B * part.np * K * 4);
     DeepMArgs m;
     void* extra;
