@@ -149,8 +149,11 @@ def build_workload(name, rank, world, device, batch, exact=False, weights="init"
         # the reference recomputes the propagation inside every recommend() call
         # (lightgcn.py:197 predict_all_items -> self.forward()): so does the step, restricted
         # to the rows that call reads (LightGCN.propagate_for: outputs identical)
-        rec = S.ItemShardedRecommender(S.lightgcn_shard_topk(m, lo, hi, K), S.hip_merge, K, lo,
-                                       rank, world)
+        # world > 1: the propagation's item rows are sharded too (restricted SpMM plans, one
+        # all_gather of the [I, d] item rows after layers 1 and 2; bitwise the same outputs)
+        ex = S.ItemRowExchange(U, I, rank, world) if world > 1 else None
+        rec = S.ItemShardedRecommender(S.lightgcn_shard_topk(m, lo, hi, K, exchange=ex),
+                                       S.hip_merge, K, lo, rank, world)
 
         def full_step(users):  # whole-graph propagation per call, for comparison
             F = m.propagate(g)
@@ -162,8 +165,24 @@ def build_workload(name, rank, world, device, batch, exact=False, weights="init"
         # X read once, Y written once, item-row accumulators read + written (layers 1..L-1;
         # the restricted last layer is not timed)
         per_launch = g.nnz * 8.0 + (N + 1) * 8.0 + 2.0 * N * d * 4 + 2.0 * I * d * 4
+        gathered = g.nnz * d * 4.0
+        if ex is not None:
+            # a rank's layer 1..L-1: the user rows + its item shard (restricted plan), X read
+            # once, its rows written, its items' accumulators read + written
+            rp = g.rowptr.cpu()
+            kept = int(rp[U]) + int(rp[U + hi]) - int(rp[U + lo])
+            per_launch = (kept * 8.0 + (N + 1) * 8.0 + N * d * 4.0 + (U + hi - lo) * d * 4.0
+                          + 2.0 * (hi - lo) * d * 4)
+            gathered = kept * d * 4.0
+            info["item_row_exchange"] = {
+                "all_gathers_per_step": 2, "bytes_received_per_rank": ex.bytes_per_call(d),
+                "note": "propagation item rows sharded: every rank computes all user rows of "
+                        "layers 1-2 and its own item rows (hnm_spmm_plan_restrict), one "
+                        "all_gather of the [I, d] item rows after each of those layers, the "
+                        "last layer on its own items; roofline prices the rank's restricted layer"}
         info["_filtered"] = lambda hist: S.ItemShardedRecommender(
-            S.lightgcn_shard_topk(m, lo, hi, K, hist), S.hip_merge, K, lo, rank, world).recommend
+            S.lightgcn_shard_topk(m, lo, hi, K, hist, exchange=ex), S.hip_merge, K, lo, rank,
+            world).recommend
         info["_module"] = m
         info.update({"model": "LightGCN", "embedding_dim": d, "num_layers": 3,
                 "interactions": syn.HM_INTERACTIONS, "nnz_with_self_loops": g.nnz,
@@ -177,7 +196,7 @@ def build_workload(name, rank, world, device, batch, exact=False, weights="init"
         info["_user_sharded"] = lambda: S.lightgcn_shard_topk(m, 0, I, K)
         ret = dict(step=rec.recommend, per_launch=per_launch, bound="hbm",
                    kernel="spmm layer (spmm_swalk_kernel short rows + spmm_walk_kernel long rows + spmm_walk_finish_kernel), whole-graph layers",
-                   timing=_lib.TIME_SPMM, gathered=g.nnz * d * 4.0)
+                   timing=_lib.TIME_SPMM, gathered=gathered)
         return ret, info, ("lightgcn", (sd, edges, d))
     elif name == "widedeep":
         sd = syn.widedeep_state_dict(U, I, 64, (512, 256, 128), seed=0)

@@ -112,12 +112,14 @@ _SIGS = {
     "hnm_rccl_unique_id": (_i32, [_p, _i64]),
     "hnm_ctx_rccl_init": (_i32, [_p, C.c_int, C.c_int, _p, _i64]),
     "hnm_ctx_set_rccl_comm": (_i32, [_p, _p]),
+    "hnm_ctx_rccl_abort": (_i32, [_p]),
     "hnm_topk_allgather_merge_f32": (_i32, [_p, _p, _p, _i64, C.c_int, _p, _p]),
     "hnm_topk_rows_f32": (_i32, [_p, _p, _i64, _i64, _i64, _p, _p, C.c_int, _p, _p]),
     "hnm_csr_build_norm": (_i32, [_p, _p, _p, _i64, _i64, _p, _p, _p]),
     "hnm_spmm_plan_create": (_i32, [_p, _i64, _p, C.POINTER(_p)]),
     "hnm_spmm_plan_prepare": (_i32, [_p, _p, _p, _p, C.c_int]),
     "hnm_spmm_plan_destroy": (_i32, [_p]),
+    "hnm_spmm_plan_restrict": (_i32, [_p, _p, C.POINTER(_i64), C.c_int, C.POINTER(_p)]),
     "hnm_spmm_csr_f32": (_i32, [_p, _p, _i64, _p, _p, _p, _p, C.c_int, _p, _f32, _p, _p]),
     "hnm_spmm_csr_range_f32": (_i32, [_p, _p, _i64, _p, _p, _p, _p, C.c_int, _p, _f32, _p, _p,
                                       _f32, _i64, _i64, _i64]),

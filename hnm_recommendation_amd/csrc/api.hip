@@ -20,7 +20,11 @@ extern "C" const char* hnm_last_error(void) { return g_err; }
 
 extern "C" hnm_status hnm_ctx_create(int device, hnm_ctx** out) {
   HNM_REQUIRE(out, HNM_EINVAL, "hnm_ctx_create: out is NULL");
-  HNM_HIP_CHECK(hipSetDevice(device));
+  int ndev = 0;
+  HNM_HIP_CHECK(hipGetDeviceCount(&ndev));
+  HNM_REQUIRE(device >= 0 && device < ndev, HNM_EINVAL, "hnm_ctx_create: no device %d (%d visible)",
+              device, ndev);
+  const HnmDeviceGuard guard(device);  // the caller's current device is restored on return
   hnm_ctx* c = (hnm_ctx*)calloc(1, sizeof(hnm_ctx));
   HNM_REQUIRE(c, HNM_ENOMEM, "hnm_ctx_create: out of host memory");
   c->device = device;
@@ -48,8 +52,8 @@ extern "C" hnm_status hnm_ctx_create(int device, hnm_ctx** out) {
 }
 
 extern "C" hnm_status hnm_ctx_destroy(hnm_ctx* ctx) {
+  HNM_CTX_DEVICE(ctx);
   if (!ctx) return HNM_OK;
-  (void)hipSetDevice(ctx->device);
   (void)hipDeviceSynchronize();
   for (int i = 0; i < ctx->cap; ++i) {
     (void)hipEventDestroy(ctx->ev0[i]);
@@ -69,6 +73,7 @@ extern "C" hnm_status hnm_ctx_destroy(hnm_ctx* ctx) {
 }
 
 extern "C" hnm_status hnm_ctx_set_stream(hnm_ctx* ctx, void* s) {
+  HNM_CTX_DEVICE(ctx);
   HNM_REQUIRE(ctx, HNM_EINVAL, "ctx is NULL");
   const hipStream_t ns = (hipStream_t)s;
   if (ns == ctx->stream) return HNM_OK;
@@ -81,12 +86,14 @@ extern "C" hnm_status hnm_ctx_set_stream(hnm_ctx* ctx, void* s) {
 }
 
 extern "C" hnm_status hnm_ctx_abort_pending(hnm_ctx* ctx) {
+  HNM_CTX_DEVICE(ctx);
   HNM_REQUIRE(ctx, HNM_EINVAL, "ctx is NULL");
   ctx->pend.kind = 0;
   return HNM_OK;
 }
 
 extern "C" hnm_status hnm_ctx_set_option(hnm_ctx* ctx, int option, int64_t value) {
+  HNM_CTX_DEVICE(ctx);
   HNM_REQUIRE(ctx, HNM_EINVAL, "ctx is NULL");
   switch (option) {
     case HNM_OPT_PREFILTER:
@@ -108,10 +115,12 @@ extern "C" hnm_status hnm_ctx_set_option(hnm_ctx* ctx, int option, int64_t value
 }
 
 extern "C" hnm_status hnm_ctx_prefilter_stats(hnm_ctx* ctx, int64_t* out, int reset) {
+  HNM_CTX_DEVICE(ctx);
   return hnm_ctx_prefilter_stats_ex(ctx, out, 3, reset);
 }
 
 extern "C" hnm_status hnm_ctx_prefilter_stats_ex(hnm_ctx* ctx, int64_t* out, int n, int reset) {
+  HNM_CTX_DEVICE(ctx);
   HNM_REQUIRE(ctx && out, HNM_EINVAL, "ctx/out is NULL");
   HNM_REQUIRE(n >= 1 && n <= HNM_STATS_N, HNM_EINVAL, "prefilter_stats: 1 <= n <= %d", HNM_STATS_N);
   // device-wide sync: never reads ctx->stream, which the ctx's owning thread may be switching
@@ -133,6 +142,7 @@ extern "C" hnm_status hnm_ctx_prefilter_stats_ex(hnm_ctx* ctx, int64_t* out, int
 }
 
 extern "C" hnm_status hnm_ctx_num_cus(hnm_ctx* ctx, int* out) {
+  HNM_CTX_DEVICE(ctx);
   HNM_REQUIRE(ctx && out, HNM_EINVAL, "ctx/out is NULL");
   *out = ctx->num_cus;
   return HNM_OK;
@@ -172,6 +182,7 @@ hnm_status hnm_fill_f32(hnm_ctx* ctx, float* p, int64_t n, float v) {
 }
 
 extern "C" hnm_status hnm_ctx_reserve(hnm_ctx* ctx, size_t bytes) {
+  HNM_CTX_DEVICE(ctx);
   HNM_REQUIRE(ctx, HNM_EINVAL, "ctx is NULL");
   void* p;
   return hnm_workspace(ctx, bytes, &p);
@@ -203,6 +214,7 @@ void hnm_timer_end(hnm_ctx* ctx, int cls) {
 }
 
 extern "C" hnm_status hnm_ctx_enable_timing(hnm_ctx* ctx, int on) {
+  HNM_CTX_DEVICE(ctx);
   HNM_REQUIRE(ctx, HNM_EINVAL, "ctx is NULL");
   ctx->timing = on;
   ctx->nev = 0;
@@ -210,6 +222,7 @@ extern "C" hnm_status hnm_ctx_enable_timing(hnm_ctx* ctx, int on) {
 }
 
 extern "C" hnm_status hnm_ctx_timing(hnm_ctx* ctx, double* total_ms, int64_t* launches) {
+  HNM_CTX_DEVICE(ctx);
   HNM_REQUIRE(ctx && total_ms && launches, HNM_EINVAL, "hnm_ctx_timing: NULL argument");
   HNM_HIP_CHECK(hipStreamSynchronize(ctx->stream));
   double t = 0.0;
@@ -225,6 +238,7 @@ extern "C" hnm_status hnm_ctx_timing(hnm_ctx* ctx, double* total_ms, int64_t* la
 }
 
 extern "C" hnm_status hnm_ctx_check(hnm_ctx* ctx) {
+  HNM_CTX_DEVICE(ctx);
   HNM_REQUIRE(ctx, HNM_EINVAL, "ctx is NULL");
   unsigned h = 0;
   HNM_HIP_CHECK(hipMemcpyAsync(&h, ctx->err_dev, sizeof(unsigned), hipMemcpyDeviceToHost,
@@ -275,6 +289,7 @@ __global__ __launch_bounds__(256) void gather_rows_kernel(const float* __restric
 extern "C" hnm_status hnm_gather_rows_f32(hnm_ctx* ctx, const float* table, int64_t rows,
                                           int64_t ld, int d, const int64_t* ids, int64_t n,
                                           float* out, int64_t ldo) {
+  HNM_CTX_DEVICE(ctx);
   HNM_REQUIRE(ctx && table && ((ids && out) || n == 0), HNM_EINVAL, "gather: NULL argument");
   HNM_REQUIRE(d > 0 && ld >= d && ldo >= d && rows > 0, HNM_EINVAL, "gather: bad shape");
   if (n <= 0) return HNM_OK;
@@ -410,6 +425,7 @@ extern "C" hnm_status hnm_linear_rows_f32(hnm_ctx* ctx, const float* X, int64_t 
                                           const int64_t* ids, int64_t x_rows, int64_t M, int K,
                                           const float* W, int64_t ldw, const float* bias, int N,
                                           float* Y, int64_t ldy, int pair_permute) {
+  HNM_CTX_DEVICE(ctx);
   HNM_REQUIRE(ctx && X && W && Y, HNM_EINVAL, "linear_rows: NULL argument");
   HNM_REQUIRE(K > 0 && N > 0 && ldx >= K && ldw >= K && ldy >= N, HNM_EINVAL,
               "linear_rows: bad shape");
@@ -445,6 +461,7 @@ __global__ __launch_bounds__(256) void axpby_kernel(int64_t n, float a, const fl
 
 extern "C" hnm_status hnm_axpby_f32(hnm_ctx* ctx, int64_t n, float alpha, const float* x,
                                     float beta, const float* y, float* out) {
+  HNM_CTX_DEVICE(ctx);
   HNM_REQUIRE(ctx && ((x && out) || n == 0), HNM_EINVAL, "axpby: NULL argument");
   if (n <= 0) return HNM_OK;
   const unsigned grid = (unsigned)std::min<int64_t>(hnm_cdiv(n, 256), 8 * 2048);
@@ -574,6 +591,7 @@ __global__ __launch_bounds__(256) void lists_kth_kernel(const float* __restrict_
 
 extern "C" hnm_status hnm_topk_lists_kth_f32(hnm_ctx* ctx, const float* lists, int64_t B,
                                              int64_t G, int kc, int k, float* out) {
+  HNM_CTX_DEVICE(ctx);
   HNM_REQUIRE(ctx && ((lists && out) || B == 0), HNM_EINVAL, "lists_kth: NULL argument");
   HNM_REQUIRE(G >= 1 && G <= 16 && kc >= 1 && k >= 1 && k <= kc * G, HNM_EINVAL,
               "lists_kth: 1 <= G <= 16, 1 <= k <= G * kc");
@@ -605,6 +623,7 @@ __global__ __launch_bounds__(256) void pack_pairs_kernel(const float* __restrict
 
 extern "C" hnm_status hnm_pack_candidates_i32(hnm_ctx* ctx, const float* val, const int64_t* idx,
                                               int64_t n, int64_t offset, int32_t* pairs) {
+  HNM_CTX_DEVICE(ctx);
   HNM_REQUIRE(ctx && ((val && idx && pairs) || n <= 0), HNM_EINVAL, "pack_candidates: NULL argument");
   HNM_REQUIRE(((uintptr_t)pairs & 7) == 0, HNM_EINVAL, "pack_candidates: pairs must be 8-byte aligned");
   if (n <= 0) return HNM_OK;
@@ -656,6 +675,7 @@ __global__ __launch_bounds__(256) void merge_sorted_pairs_kernel(const int2* __r
 extern "C" hnm_status hnm_topk_merge_sorted_pairs_i32(hnm_ctx* ctx, const int32_t* pairs,
                                                       int64_t B, int64_t G, int kc, int k,
                                                       float* out_val, int64_t* out_idx) {
+  HNM_CTX_DEVICE(ctx);
   HNM_REQUIRE(ctx && ((pairs && out_val && out_idx) || B == 0), HNM_EINVAL,
               "merge_sorted_pairs: NULL argument");
   HNM_REQUIRE(G >= 1 && G <= 16 && kc >= 1 && k >= 1 && k <= 128, HNM_EINVAL,
@@ -679,6 +699,7 @@ extern "C" hnm_status hnm_topk_merge_f32(hnm_ctx* ctx, const float* cand_val,
                                          const int64_t* cand_idx, int64_t B, int64_t G,
                                          int64_t gstride, int64_t bstride, int kc, int k,
                                          float* out_val, int64_t* out_idx) {
+  HNM_CTX_DEVICE(ctx);
   HNM_REQUIRE(ctx && ((cand_val && cand_idx && out_idx) || B == 0), HNM_EINVAL, "merge: NULL argument");
   HNM_REQUIRE(k >= 1 && k <= 128 && kc >= 1 && G >= 1, HNM_EINVAL, "merge: bad k/kc/G");
   if (B <= 0) return HNM_OK;
@@ -726,6 +747,7 @@ extern "C" hnm_status hnm_pair_dot_f32(hnm_ctx* ctx, const float* user_tab, int6
                                        const int64_t* item_ids, int64_t n,
                                        const float* user_bias, const float* item_bias,
                                        const float* const_bias, float* out) {
+  HNM_CTX_DEVICE(ctx);
   HNM_REQUIRE(ctx && user_tab && item_tab && ((user_ids && item_ids && out) || n == 0), HNM_EINVAL,
               "pair_dot: NULL argument");
   HNM_REQUIRE(d >= 1 && ldu >= d && ldi >= d, HNM_EINVAL, "pair_dot: bad shape");
@@ -840,6 +862,7 @@ extern "C" hnm_status hnm_mask_gather_csr(hnm_ctx* ctx, const int64_t* hist_ptr,
                                           const int64_t* user_ids, int64_t B, int64_t item_lo,
                                           int64_t item_hi, int64_t capacity, int64_t* mask_ptr,
                                           int32_t* mask_idx) {
+  HNM_CTX_DEVICE(ctx);
   HNM_REQUIRE(ctx && hist_ptr && (user_ids || B == 0) && mask_ptr && (hist_idx || capacity == 0) &&
                   (mask_idx || capacity == 0),
               HNM_EINVAL, "mask_gather: NULL argument");

@@ -46,18 +46,12 @@ void hnm_rccl_release(hnm_ctx* ctx) {  // hnm_ctx_destroy / a replaced communica
 
 extern "C" hnm_status hnm_ctx_rccl_init(hnm_ctx* ctx, int world, int rank, const void* unique_id,
                                         int64_t size) {
+  HNM_CTX_DEVICE(ctx);
   HNM_REQUIRE(ctx && unique_id && size >= (int64_t)sizeof(ncclUniqueId) && world >= 1 &&
                   rank >= 0 && rank < world,
               HNM_EINVAL, "ctx_rccl_init: bad argument (world %d, rank %d)", world, rank);
   // RCCL binds the communicator to the current device: the ctx's, for this call only (the
-  // caller's current device is restored on every exit path)
-  int prev = -1;
-  HNM_HIP_CHECK(hipGetDevice(&prev));
-  struct Restore {
-    int dev;
-    ~Restore() { (void)hipSetDevice(dev); }
-  } restore{prev};
-  HNM_HIP_CHECK(hipSetDevice(ctx->device));
+  // entry's device guard restores the caller's current device on every exit path)
   ncclUniqueId id;
   memcpy(&id, unique_id, sizeof(id));
   ncclComm_t comm;
@@ -69,15 +63,28 @@ extern "C" hnm_status hnm_ctx_rccl_init(hnm_ctx* ctx, int world, int rank, const
 }
 
 extern "C" hnm_status hnm_ctx_set_rccl_comm(hnm_ctx* ctx, void* comm) {
+  HNM_CTX_DEVICE(ctx);
   HNM_REQUIRE(ctx, HNM_EINVAL, "ctx is NULL");
   hnm_rccl_release(ctx);
   ctx->comm = comm;  // borrowed (NULL detaches)
   return HNM_OK;
 }
 
+extern "C" hnm_status hnm_ctx_rccl_abort(hnm_ctx* ctx) {
+  HNM_CTX_DEVICE(ctx);
+  HNM_REQUIRE(ctx, HNM_EINVAL, "ctx is NULL");
+  // a communicator whose ranks disagree (one rank returned before the collective): abort
+  // releases the peers blocked in it; the ctx no longer has a communicator afterwards
+  if (ctx->comm && ctx->comm_owned) HNM_RCCL_CHECK(ncclCommAbort((ncclComm_t)ctx->comm));
+  ctx->comm = nullptr;
+  ctx->comm_owned = 0;
+  return HNM_OK;
+}
+
 extern "C" hnm_status hnm_topk_allgather_merge_f32(hnm_ctx* ctx, const float* lval,
                                                    const int64_t* lidx, int64_t B, int k,
                                                    float* gval, int64_t* gidx) {
+  HNM_CTX_DEVICE(ctx);
   HNM_REQUIRE(ctx && ((lval && lidx && gidx) || B == 0), HNM_EINVAL,
               "topk_allgather_merge: NULL argument");
   HNM_REQUIRE(ctx->comm, HNM_EINVAL,
@@ -88,7 +95,11 @@ extern "C" hnm_status hnm_topk_allgather_merge_f32(hnm_ctx* ctx, const float* lv
   ncclComm_t comm = (ncclComm_t)ctx->comm;
   int world = 0;
   HNM_RCCL_CHECK(ncclCommCount(comm, &world));
-  // every rank takes part in the collective, B == 0 included (the counts must agree)
+  // every rank takes part in the collective, B == 0 included (the counts must agree).  All local
+  // checks -- the arguments, an open two-phase call, the workspace (the merge after the
+  // collective needs none) -- run before it, so a rank that fails here returns before entering
+  // the collective its peers are blocked in: the host then aborts the communicator on every
+  // rank (hnm_ctx_rccl_abort).
   const size_t n = (size_t)std::max<int64_t>(B, 0) * k;
   const size_t szV = hnm_align(std::max<size_t>(n, 1) * world * 4);
   void* ws;

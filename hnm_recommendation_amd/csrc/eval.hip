@@ -159,6 +159,7 @@ extern "C" hnm_status hnm_rank_metrics_f64(hnm_ctx* ctx, const int64_t* pred, in
                                            int64_t ldt, const uint8_t* truth_mask,
                                            const double* inv_log2, double* per_user,
                                            int64_t* n_true, double* sums) {
+  HNM_CTX_DEVICE(ctx);
   HNM_REQUIRE(ctx && inv_log2, HNM_EINVAL, "rank_metrics: NULL argument");
   HNM_REQUIRE(k >= 1 && k <= 128, HNM_EINVAL, "rank_metrics: 1 <= k <= 128");
   HNM_REQUIRE(B >= 0 && ldp >= 0 && (ldp == 0 || pred || B == 0), HNM_EINVAL,

@@ -117,6 +117,8 @@ struct hnm_spmm_plan {
   std::mutex* mu;       // lazy preparation (first call with col/val, first call per d)
   WalkSched* sched[7];  // per d = 4 << i
   ShortSched* ssched[7];
+  // hnm_spmm_plan_restrict: the row ranges [keep[2j], keep[2j+1]) this plan computes (NULL: all)
+  std::vector<int64_t>* keep;
 };
 
 // ------------------------------------------------------------------ CSR build kernels
@@ -229,6 +231,7 @@ __global__ void csr_norm_kernel(const int32_t* __restrict__ skeys, int64_t E, in
 extern "C" hnm_status hnm_csr_build_norm(hnm_ctx* ctx, const int64_t* edge_index,
                                          const float* edge_weight, int64_t E, int64_t N,
                                          int64_t* rowptr, int32_t* col, float* val) {
+  HNM_CTX_DEVICE(ctx);
   HNM_REQUIRE(ctx && rowptr && col && val && (edge_index || E == 0), HNM_EINVAL,
               "csr_build: NULL argument");
   HNM_REQUIRE(N > 0 && N < 0x7fffffff && E >= 0 && E < 0x7fffffff, HNM_EUNSUPPORTED,
@@ -1414,6 +1417,7 @@ static hnm_status walk_get(hnm_ctx* ctx, const hnm_spmm_plan* cpl, const int32_t
 
 extern "C" hnm_status hnm_spmm_plan_create(hnm_ctx* ctx, int64_t N, const int64_t* rowptr,
                                            hnm_spmm_plan** out) {
+  HNM_CTX_DEVICE(ctx);
   HNM_REQUIRE(ctx && rowptr && out && N > 0, HNM_EINVAL, "spmm_plan: bad argument");
   std::vector<int64_t> rp((size_t)N + 1);
   HNM_HIP_CHECK(hipMemcpyAsync(rp.data(), rowptr, (N + 1) * 8, hipMemcpyDeviceToHost, ctx->stream));
@@ -1503,6 +1507,7 @@ extern "C" hnm_status hnm_spmm_plan_create(hnm_ctx* ctx, int64_t N, const int64_
 
 extern "C" hnm_status hnm_spmm_plan_prepare(hnm_ctx* ctx, hnm_spmm_plan* plan, const int32_t* col,
                                             const float* val, int d) {
+  HNM_CTX_DEVICE(ctx);
   HNM_REQUIRE(ctx && plan && col && val, HNM_EINVAL, "spmm_plan_prepare: NULL argument");
   HNM_REQUIRE(d == 0 || spmm_d_ok(d), HNM_EUNSUPPORTED,
               "spmm_plan_prepare: d must be 0 or one of 4, 8, 16, 32, 64, 128, 256 (got %d)", d);
@@ -1511,6 +1516,7 @@ extern "C" hnm_status hnm_spmm_plan_prepare(hnm_ctx* ctx, hnm_spmm_plan* plan, c
 
 extern "C" hnm_status hnm_spmm_plan_destroy(hnm_spmm_plan* pl) {
   if (!pl) return HNM_OK;
+  const HnmDeviceGuard guard(pl->device);
   if (pl->heavy_rows) (void)hipFree(pl->heavy_rows);
   if (pl->seg_ptr) (void)hipFree(pl->seg_ptr);
   if (pl->seg_hrow) (void)hipFree(pl->seg_hrow);
@@ -1530,21 +1536,140 @@ extern "C" hnm_status hnm_spmm_plan_destroy(hnm_spmm_plan* pl) {
   delete pl->h_long;
   delete pl->h_heavy;
   delete pl->h_seg_ptr;
+  delete pl->keep;
   free(pl);
+  return HNM_OK;
+}
+
+template <typename T>
+static hnm_status dup_device(T** dst, const T* src, int64_t n) {
+  *dst = nullptr;
+  if (!src || n <= 0) return HNM_OK;
+  if (hipMalloc((void**)dst, (size_t)n * sizeof(T)) != hipSuccess) {
+    *dst = nullptr;
+    hnm_set_error("spmm_plan_restrict: hipMalloc of %lld bytes failed", (long long)(n * sizeof(T)));
+    return HNM_ENOMEM;
+  }
+  HNM_HIP_CHECK(hipMemcpy(*dst, src, (size_t)n * sizeof(T), hipMemcpyDeviceToDevice));
+  return HNM_OK;
+}
+
+// Item-sharded propagation: a copy of a bound plan that computes
+// only the rows of `ranges` -- e.g. every user row plus this rank's item rows.  A walk plan keeps
+// the base's piece length (cap), its bipartite routing and its sorted copy, and filters the walk
+// and short-walk row lists, so every kept row is cut into the same pieces and summed in the same
+// order as by the base (bitwise equal rows), while the walks' schedules -- built per d on first
+// use -- hold only the kept rows' entries (work proportional to them).  A plan without the walks
+// runs the kept sub-ranges of each call with its row-class kernels (per-row order independent of
+// the range).
+extern "C" hnm_status hnm_spmm_plan_restrict(hnm_ctx* ctx, const hnm_spmm_plan* base,
+                                             const int64_t* ranges, int n_ranges,
+                                             hnm_spmm_plan** out) {
+  HNM_CTX_DEVICE(ctx);
+  HNM_REQUIRE(ctx && base && out && n_ranges >= 0 && (ranges || n_ranges == 0), HNM_EINVAL,
+              "spmm_plan_restrict: bad argument");
+  HNM_REQUIRE(!base->keep, HNM_EINVAL, "spmm_plan_restrict: the base plan is itself restricted");
+  for (int j = 0; j < n_ranges; ++j)
+    HNM_REQUIRE(ranges[2 * j] >= (j ? ranges[2 * j - 1] : 0) && ranges[2 * j] <= ranges[2 * j + 1] &&
+                    ranges[2 * j + 1] <= base->N,
+                HNM_EINVAL, "spmm_plan_restrict: ranges must be ascending, disjoint, inside [0, N)");
+  hnm_spmm_plan* bp = const_cast<hnm_spmm_plan*>(base);
+  std::lock_guard<std::mutex> lk(*bp->mu);
+  HNM_REQUIRE(bp->bound_col, HNM_EINVAL,
+              "spmm_plan_restrict: bind the base plan first (hnm_spmm_plan_prepare, d = 0)");
+  std::vector<int64_t> kr(ranges, ranges + 2 * n_ranges);
+  auto kept = [&](int64_t r) {
+    // first range whose end is past r
+    int lo = 0, hi = n_ranges;
+    while (lo < hi) {
+      const int m = (lo + hi) / 2;
+      if (kr[2 * m + 1] <= r) lo = m + 1; else hi = m;
+    }
+    return lo < n_ranges && kr[2 * lo] <= r;
+  };
+  hnm_spmm_plan* pl = (hnm_spmm_plan*)calloc(1, sizeof(hnm_spmm_plan));
+  HNM_REQUIRE(pl, HNM_ENOMEM, "spmm_plan_restrict: out of host memory");
+  pl->device = bp->device;
+  pl->num_cus = bp->num_cus;
+  pl->N = bp->N;
+  pl->nnz = bp->nnz;
+  pl->walk = bp->walk;
+  pl->swalk = bp->swalk;
+  pl->walk_cap = bp->walk_cap;
+  pl->bound_col = bp->bound_col;
+  pl->bound_val = bp->bound_val;
+  pl->mu = new std::mutex();
+  pl->keep = new std::vector<int64_t>(kr);
+  hnm_status st = HNM_OK;
+  if (bp->walk) {
+    const std::vector<int64_t>& rp = *bp->h_rowptr;
+    pl->h_rowptr = new std::vector<int64_t>(rp);
+    pl->h_scol = new std::vector<int32_t>(*bp->h_scol);
+    pl->h_sval = new std::vector<float>(*bp->h_sval);
+    pl->h_walk_rows = new std::vector<int32_t>();
+    pl->h_short_rows = new std::vector<int32_t>();
+    for (int32_t r : *bp->h_walk_rows)
+      if (kept(r)) {
+        pl->h_walk_rows->push_back(r);
+        pl->walk_nnz += rp[r + 1] - rp[r];
+      }
+    for (int32_t r : *bp->h_short_rows)
+      if (kept(r)) pl->h_short_rows->push_back(r);
+    pl->n_walk = (int64_t)pl->h_walk_rows->size();
+    pl->h_long = new std::vector<int32_t>();
+    pl->h_heavy = new std::vector<int32_t>();
+    pl->h_seg_ptr = new std::vector<int64_t>(1, 0);
+    if (!(st = dup_device(&pl->scol, bp->scol, bp->nnz))) st = dup_device(&pl->sval, bp->sval, bp->nnz);
+  } else {
+    pl->n_heavy = bp->n_heavy;
+    pl->n_seg = bp->n_seg;
+    pl->n_long = bp->n_long;
+    pl->h_long = new std::vector<int32_t>(*bp->h_long);
+    pl->h_heavy = new std::vector<int32_t>(*bp->h_heavy);
+    pl->h_seg_ptr = new std::vector<int64_t>(*bp->h_seg_ptr);
+    if (!(st = dup_device(&pl->long_rows, bp->long_rows, bp->n_long)) &&
+        !(st = dup_device(&pl->heavy_rows, bp->heavy_rows, bp->n_heavy)) &&
+        !(st = dup_device(&pl->seg_ptr, bp->seg_ptr, bp->n_heavy + 1)) &&
+        !(st = dup_device(&pl->seg_hrow, bp->seg_hrow, bp->n_seg)) &&
+        !(st = dup_device(&pl->seg_start, bp->seg_start, bp->n_seg)))
+      st = dup_device(&pl->seg_end, bp->seg_end, bp->n_seg);
+  }
+  if (st) {
+    hnm_spmm_plan_destroy(pl);
+    return st;
+  }
+  *out = pl;
   return HNM_OK;
 }
 
 template <int LPR>
 static hnm_status spmm_launch(hnm_ctx* ctx, const hnm_spmm_plan* pl, int64_t N,
                               const int64_t* rowptr, const int32_t* col, const float* val,
-                              const float* X, int d, const SpmmEpi& ep, int64_t r0, int64_t r1) {
+                              const float* X, int d, const SpmmEpi& ep, int64_t r0, int64_t r1,
+                              bool timer = true) {
   const bool has_heavy = pl && pl->n_heavy > 0;
   const int64_t heavy = has_heavy ? HEAVY : INT64_MAX;
-  // the live roofline times whole-graph layers only (row-range calls do less work)
-  const bool timed = r0 == 0 && r1 == N;
+  // the live roofline times whole-plan layers only (row-range calls do less work; a restricted
+  // plan's whole layer is timed as such -- bench.py prices its kept rows)
+  const bool timed = timer && r0 == 0 && r1 == N;
   if (pl) {
     hnm_status s = walk_get(ctx, pl, col, val, 0, nullptr, nullptr);  // binding check
     if (s) return s;
+  }
+  if (pl && pl->keep && !pl->walk) {
+    // a restricted plan without the walks: its kept sub-ranges of [r0, r1), one at a time
+    if (timed) hnm_timer_begin(ctx, HNM_TIME_SPMM);
+    const std::vector<int64_t>& kr = *pl->keep;
+    for (size_t j = 0; j + 1 < kr.size(); j += 2) {
+      const int64_t a = std::max(r0, kr[j]), b = std::min(r1, kr[j + 1]);
+      if (a >= b) continue;
+      hnm_spmm_plan unrestricted = *pl;
+      unrestricted.keep = nullptr;
+      hnm_status s = spmm_launch<LPR>(ctx, &unrestricted, N, rowptr, col, val, X, d, ep, a, b, false);
+      if (s) return s;
+    }
+    if (timed) hnm_timer_end(ctx, HNM_TIME_SPMM);
+    return HNM_OK;
   }
   if (pl && pl->walk) {
     // short rows (<= SPMM_SHORT entries) by the short walk, then the rows of more entries by the
@@ -1674,6 +1799,7 @@ extern "C" hnm_status hnm_spmm_csr_range_f32(hnm_ctx* ctx, const hnm_spmm_plan* 
                                              float alpha, const float* acc_in, float* acc_out,
                                              float beta, int64_t row_begin, int64_t row_end,
                                              int64_t acc_row0) {
+  HNM_CTX_DEVICE(ctx);
   HNM_REQUIRE(ctx && rowptr && col && val && X, HNM_EINVAL, "spmm: NULL argument");
   HNM_REQUIRE(!plan || plan->N == N, HNM_EINVAL, "spmm: plan built for a different graph");
   HNM_REQUIRE((uintptr_t)X % 16 == 0 && (!Y || (uintptr_t)Y % 16 == 0) &&
@@ -1692,6 +1818,7 @@ extern "C" hnm_status hnm_spmm_csr_f32(hnm_ctx* ctx, const hnm_spmm_plan* plan, 
                                        const int64_t* rowptr, const int32_t* col,
                                        const float* val, const float* X, int d, float* Y,
                                        float alpha, const float* acc_in, float* acc_out) {
+  HNM_CTX_DEVICE(ctx);
   return hnm_spmm_csr_range_f32(ctx, plan, N, rowptr, col, val, X, d, Y, alpha, acc_in, acc_out,
                                 0.f, 0, N, 0);
 }
@@ -1714,6 +1841,7 @@ extern "C" hnm_status hnm_spmm_rows_combine_f32(hnm_ctx* ctx, const hnm_spmm_pla
                                                 const int64_t* rows, int64_t n, int d,
                                                 const float* const* layers, const float* alphas,
                                                 int L, float* out) {
+  HNM_CTX_DEVICE(ctx);
   HNM_REQUIRE(ctx && rowptr && col && val && layers && alphas && ((rows && out) || n == 0),
               HNM_EINVAL, "spmm_rows_combine: NULL argument");
   HNM_REQUIRE(!plan || plan->N == N, HNM_EINVAL, "spmm_rows_combine: plan built for a different graph");

@@ -45,13 +45,33 @@ struct hnm_ctx {
     int K;
     const void* ids;
     const void* items;      // the item table the begin phase read
+    int flags;              // HNM_PEND_STRIDED: the begin carved the strided sample's scratch
   } pend;
 };
+// Device binding: every entry point that takes a ctx runs on ctx->device --
+// its workspace hipMalloc, events, null stream and launches -- and leaves the calling thread's
+// current device as it found it, so one host thread may drive ctxs of several GPUs.
+struct HnmDeviceGuard {
+  int prev = -1;
+  explicit HnmDeviceGuard(int device) {
+    int cur = -1;
+    if (device >= 0 && hipGetDevice(&cur) == hipSuccess && cur != device &&
+        hipSetDevice(device) == hipSuccess)
+      prev = cur;
+  }
+  ~HnmDeviceGuard() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+  HnmDeviceGuard(const HnmDeviceGuard&) = delete;
+  HnmDeviceGuard& operator=(const HnmDeviceGuard&) = delete;
+};
+#define HNM_CTX_DEVICE(c) const HnmDeviceGuard hnm_device_guard_((c) ? (c)->device : -1)
 #define HNM_STATS_N 6  // pre-filter counters (hnm_ctx_prefilter_stats_ex)
 #define HNM_PEND_NCF_CERT 1
 #define HNM_PEND_NCF_EXACT 2
 #define HNM_PEND_DOT_CERT 3
 #define HNM_PEND_DOT_EXACT 4
+#define HNM_PEND_STRIDED 1  // pend.flags
 
 // dominant-kernel timer classes (hnm_ctx_enable_timing mask)
 #define HNM_TIME_SCORE 1  // the scoring / scan kernel of each top-K or dense call

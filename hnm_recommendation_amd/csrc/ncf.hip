@@ -570,6 +570,10 @@ static hnm_status ncf_check(const hnm_ncf_weights* w) {
                   w->h2 >= 1 && w->h2 <= 32,
               HNM_EUNSUPPORTED, "ncf: needs mf <= 128, h1 <= 128, h2 <= 32 (got %d, %d, %d)",
               w->mf, w->h1, w->h2);
+  // item_proj is read with 16-B loads as the Qi table (a caller that filled the
+  // struct field by field without zeroing it passes garbage here -- refused when misaligned)
+  HNM_REQUIRE((uintptr_t)w->item_proj % 16 == 0, HNM_EINVAL,
+              "ncf: item_proj must be NULL or 16-B aligned (zero the hnm_ncf_weights struct)");
   return HNM_OK;
 }
 
@@ -700,11 +704,13 @@ static hnm_status ncf_common(hnm_ctx* ctx, const hnm_ncf_weights* w, const int64
   const int64_t ublocks = big ? hnm_cdiv(B, 4 * WU) : hnm_cdiv(B, 128);
   const Partition part = choose_partition(I, ublocks, ctx->num_cus);
   const size_t szC = DENSE ? 0 : hnm_align((size_t)B * part.np * K * 4);
-  const size_t extra = cert ? ncf_cert_bytes(B, I, K, ctx->num_cus, ncf_cert_wg(ctx)) : 2 * szC;
+  const bool strided = ctx->strided != 0;
+  const size_t extra =
+      cert ? ncf_cert_bytes(B, I, K, ctx->num_cus, ncf_cert_wg(ctx), strided) : 2 * szC;
   NcfCall c;
   st = ncf_tables(ctx, w, ids, B, extra, &c);
   if (st) return st;
-  if (cert) return ncf_cert_topk(ctx, w, c.t, B, mptr, midx, K, c.extra, ov, oi);
+  if (cert) return ncf_cert_topk(ctx, w, c.t, B, mptr, midx, K, c.extra, strided, ov, oi);
   float* cv = (float*)c.extra;
   int32_t* ci = (int32_t*)((char*)c.extra + szC);
 
@@ -737,6 +743,7 @@ extern "C" hnm_status hnm_ncf_topk_f32(hnm_ctx* ctx, const hnm_ncf_weights* w,
                                        const int64_t* user_ids, int64_t B,
                                        const int64_t* mask_ptr, const int32_t* mask_idx, int k,
                                        float* out_val, int64_t* out_idx) {
+  HNM_CTX_DEVICE(ctx);
   HNM_REQUIRE(k >= 1 && k <= 64 && (out_idx || B == 0), HNM_EINVAL, "ncf_topk: fused path needs 1 <= k <= 64");
   // very large batches in chunks of rows: the certified path's per-row scratch (samples,
   // candidate segments) stays bounded; the mask CSR holds absolute offsets, so a chunk reads
@@ -771,19 +778,23 @@ static hnm_status ncf_topk_begin(hnm_ctx* ctx, const hnm_ncf_weights* w, const i
   if (B <= 0) return HNM_OK;
   const bool big = w->h1 > 64 || w->mf > 64;
   const bool cert = !big && ctx->prefilter && ncf_cert_eligible(w, k);
+  // the scratch layout (with / without the strided sample's) is the begin's, kept for finish
+  const bool strided = ctx->strided != 0;
   if (cert) {
     NcfCall c;
     st = ncf_tables(ctx, w, user_ids, B,
-                    ncf_cert_bytes(B, w->num_items, k, ctx->num_cus, ncf_cert_wg(ctx)), &c);
+                    ncf_cert_bytes(B, w->num_items, k, ctx->num_cus, ncf_cert_wg(ctx), strided),
+                    &c);
     if (st) return st;
-    st = ncf_cert_begin(ctx, w, c.t, B, mask_ptr, mask_idx, k, c.extra, lower_bound, lists);
+    st = ncf_cert_begin(ctx, w, c.t, B, mask_ptr, mask_idx, k, c.extra, strided, lower_bound,
+                        lists);
     if (st) return st;
   } else {
     if (lower_bound && (st = hnm_fill_f32(ctx, lower_bound, B, -__builtin_inff()))) return st;
     if (lists && (st = hnm_fill_f32(ctx, lists, B * k, -__builtin_inff()))) return st;
   }
   ctx->pend = {cert ? HNM_PEND_NCF_CERT : HNM_PEND_NCF_EXACT, B, w->num_items, k, user_ids,
-               w->mlp_item};
+               w->mlp_item, strided ? HNM_PEND_STRIDED : 0};
   return HNM_OK;
 }
 
@@ -791,6 +802,7 @@ extern "C" hnm_status hnm_ncf_topk_begin_f32(hnm_ctx* ctx, const hnm_ncf_weights
                                              const int64_t* user_ids, int64_t B,
                                              const int64_t* mask_ptr, const int32_t* mask_idx,
                                              int k, float* lower_bound) {
+  HNM_CTX_DEVICE(ctx);
   HNM_REQUIRE(lower_bound || B == 0, HNM_EINVAL, "ncf_topk_begin: lower_bound is NULL");
   return ncf_topk_begin(ctx, w, user_ids, B, mask_ptr, mask_idx, k, lower_bound, nullptr);
 }
@@ -800,6 +812,7 @@ extern "C" hnm_status hnm_ncf_topk_begin_lists_f32(hnm_ctx* ctx, const hnm_ncf_w
                                                    const int64_t* mask_ptr,
                                                    const int32_t* mask_idx, int k,
                                                    float* lower_lists) {
+  HNM_CTX_DEVICE(ctx);
   HNM_REQUIRE(lower_lists || B == 0, HNM_EINVAL, "ncf_topk_begin_lists: lower_lists is NULL");
   return ncf_topk_begin(ctx, w, user_ids, B, mask_ptr, mask_idx, k, nullptr, lower_lists);
 }
@@ -809,6 +822,7 @@ extern "C" hnm_status hnm_ncf_topk_finish_f32(hnm_ctx* ctx, const hnm_ncf_weight
                                               const int64_t* mask_ptr, const int32_t* mask_idx,
                                               int k, const float* lower_bound, int short_ok,
                                               float* out_val, int64_t* out_idx) {
+  HNM_CTX_DEVICE(ctx);
   HNM_REQUIRE(ctx && w && (out_idx || B == 0), HNM_EINVAL, "ncf_topk_finish: bad argument");
   if (B <= 0) return HNM_OK;
   const int kind = ctx->pend.kind;
@@ -821,16 +835,18 @@ extern "C" hnm_status hnm_ncf_topk_finish_f32(hnm_ctx* ctx, const hnm_ncf_weight
     return ncf_common<false>(ctx, w, user_ids, B, mask_ptr, mask_idx, k, out_val, out_idx,
                              nullptr, 0);
   HNM_REQUIRE(lower_bound, HNM_EINVAL, "ncf_topk_finish: lower_bound is NULL");
+  const bool strided = (ctx->pend.flags & HNM_PEND_STRIDED) != 0;  // the begin's layout
   NcfCall c;
-  hnm_status st = ncf_tables(ctx, w, user_ids, B,
-                             ncf_cert_bytes(B, w->num_items, k, ctx->num_cus, ncf_cert_wg(ctx)),
-                             &c, false);
+  hnm_status st = ncf_tables(
+      ctx, w, user_ids, B,
+      ncf_cert_bytes(B, w->num_items, k, ctx->num_cus, ncf_cert_wg(ctx), strided), &c, false);
   if (st) return st;
-  return ncf_cert_finish(ctx, w, c.t, B, mask_ptr, mask_idx, k, c.extra, lower_bound,
+  return ncf_cert_finish(ctx, w, c.t, B, mask_ptr, mask_idx, k, c.extra, strided, lower_bound,
                          short_ok, out_val, out_idx);
 }
 
 extern "C" hnm_status hnm_ncf_item_proj_f32(hnm_ctx* ctx, const hnm_ncf_weights* w, float* out) {
+  HNM_CTX_DEVICE(ctx);
   hnm_status st = ncf_check(w);
   if (st) return st;
   HNM_REQUIRE(ctx && out, HNM_EINVAL, "ncf_item_proj: NULL argument");
@@ -844,6 +860,7 @@ extern "C" hnm_status hnm_ncf_item_proj_f32(hnm_ctx* ctx, const hnm_ncf_weights*
 extern "C" hnm_status hnm_ncf_scores_f32(hnm_ctx* ctx, const hnm_ncf_weights* w,
                                          const int64_t* user_ids, int64_t B, float* out,
                                          int64_t ldo) {
+  HNM_CTX_DEVICE(ctx);
   HNM_REQUIRE((out || B == 0) && w && ldo >= w->num_items, HNM_EINVAL, "ncf_scores: bad output");
   return ncf_common<true>(ctx, w, user_ids, B, nullptr, nullptr, 1, nullptr, nullptr, out, ldo);
 }
@@ -851,6 +868,7 @@ extern "C" hnm_status hnm_ncf_scores_f32(hnm_ctx* ctx, const hnm_ncf_weights* w,
 extern "C" hnm_status hnm_ncf_prefilter_debug_f32(hnm_ctx* ctx, const hnm_ncf_weights* w,
                                                   const int64_t* user_ids, int64_t B,
                                                   float* approx, int64_t lda, float* bound) {
+  HNM_CTX_DEVICE(ctx);
   hnm_status st = ncf_check(w);
   if (st) return st;
   HNM_REQUIRE(ctx && user_ids && approx && bound && lda >= w->num_items, HNM_EINVAL,
@@ -860,7 +878,8 @@ extern "C" hnm_status hnm_ncf_prefilter_debug_f32(hnm_ctx* ctx, const hnm_ncf_we
               "ncf_prefilter_debug: the f16 pre-filter covers h1 <= 64, mf <= 64, < 2^25 items");
   if (B <= 0) return HNM_OK;
   NcfCall c;
-  st = ncf_tables(ctx, w, user_ids, B, ncf_cert_bytes(B, w->num_items, 1, ctx->num_cus, ncf_cert_wg(ctx)), &c);
+  st = ncf_tables(ctx, w, user_ids, B,
+                  ncf_cert_bytes(B, w->num_items, 1, ctx->num_cus, ncf_cert_wg(ctx), false), &c);
   if (st) return st;
   return ncf_cert_debug(ctx, w, c.t, B, c.extra, approx, lda, bound);
 }
@@ -868,6 +887,7 @@ extern "C" hnm_status hnm_ncf_prefilter_debug_f32(hnm_ctx* ctx, const hnm_ncf_we
 extern "C" hnm_status hnm_ncf_pair_scores_f32(hnm_ctx* ctx, const hnm_ncf_weights* w,
                                               const int64_t* user_ids, const int64_t* item_ids,
                                               int64_t n, float* out) {
+  HNM_CTX_DEVICE(ctx);
   hnm_status st = ncf_check(w);
   if (st) return st;
   HNM_REQUIRE(ctx && ((user_ids && item_ids && out) || n == 0), HNM_EINVAL, "ncf_pair: NULL argument");

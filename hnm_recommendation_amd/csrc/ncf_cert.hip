@@ -1435,7 +1435,10 @@ CertShape cert_shape(int64_t B, int64_t I, int K, int num_cus, int wg) {
 }
 
 // carve (or size, when base == nullptr) the scratch region
-size_t cert_carve(char* base, int64_t B, int64_t I, int K, int num_cus, int wg, CertWs* w) {
+// strided: carve the gated strided sample's scratch (sloo, sidx2, sdense [B, ns], kth2) -- only
+// for calls that may run it (HNM_OPT_STRIDED; ADVICE r5: ~0.2 GB a B = 4,096 call otherwise)
+size_t cert_carve(char* base, int64_t B, int64_t I, int K, int num_cus, int wg, bool strided,
+                  CertWs* w) {
   const CertShape sh = cert_shape(B, I, K, num_cus, wg);
   size_t off = 0;
   auto take = [&](size_t bytes) {
@@ -1460,10 +1463,10 @@ size_t cert_carve(char* base, int64_t B, int64_t I, int K, int num_cus, int wg, 
   x.pdense = (float*)take((size_t)CERT_PROXY_USERS * I * 4);
   x.cdense = (float*)take((size_t)B * sh.nch * 4);
   x.sidx = (int32_t*)take((size_t)sh.nch * 4);
-  x.sloo = (int32_t*)take((size_t)CERT_PROXY_USERS * sh.nch * 4);
-  x.sidx2 = (int32_t*)take((size_t)sh.ns * 4);
-  x.sdense = (float*)take((size_t)B * sh.ns * 4);
-  x.kth2 = (float*)take((size_t)B * K * 4);
+  x.sloo = strided ? (int32_t*)take((size_t)CERT_PROXY_USERS * sh.nch * 4) : nullptr;
+  x.sidx2 = strided ? (int32_t*)take((size_t)sh.ns * 4) : nullptr;
+  x.sdense = strided ? (float*)take((size_t)B * sh.ns * 4) : nullptr;
+  x.kth2 = strided ? (float*)take((size_t)B * K * 4) : nullptr;
   x.gate = (int*)take(4);
   x.gcnt = (unsigned long long*)take(4 * 8);
   x.kthi = (int64_t*)take((size_t)B * K * 8);
@@ -1545,20 +1548,20 @@ int ncf_cert_wg(const hnm_ctx* ctx) {
   return CERT_WG_PER_CU;
 }
 
-size_t ncf_cert_bytes(int64_t B, int64_t I, int K, int num_cus, int wg) {
-  return cert_carve(nullptr, B, I, K, num_cus, wg, nullptr);
+size_t ncf_cert_bytes(int64_t B, int64_t I, int K, int num_cus, int wg, bool strided) {
+  return cert_carve(nullptr, B, I, K, num_cus, wg, strided, nullptr);
 }
 
 // Phase 1: per-call bound statistics and f16 copies, the champion sample, and every row's
 // certified lower bound of the exact K-th best score (real units) into lb[B].
 hnm_status ncf_cert_begin(hnm_ctx* ctx, const hnm_ncf_weights* w, const NcfTabs& t, int64_t B,
                           const int64_t* mptr, const int32_t* midx, int K, void* scratch,
-                          float* lb, float* lists) {
+                          bool strided, float* lb, float* lists) {
   const int64_t I = w->num_items;
   const int wg = ncf_cert_wg(ctx);
   const CertShape sh = cert_shape(B, I, K, ctx->num_cus, wg);
   CertWs x;
-  cert_carve((char*)scratch, B, I, K, ctx->num_cus, wg, &x);
+  cert_carve((char*)scratch, B, I, K, ctx->num_cus, wg, strided, &x);
   hnm_status st = cert_prepare(ctx, w, t, B, x);
   if (st) return st;
   const int64_t ublocks = hnm_cdiv(B, 128);
@@ -1566,7 +1569,6 @@ hnm_status ncf_cert_begin(hnm_ctx* ctx, const hnm_ncf_weights* w, const NcfTabs&
   // nch groups -> every row's K-th best approx - e over those items -> L (a lower bound of
   // the exact K-th for any item subset; this one tends to hold the rows' best items)
   const int64_t bp = std::min<int64_t>(CERT_PROXY_USERS, B);
-  const bool strided = ctx->strided != 0;  // HNM_OPT_STRIDED: the gated strided sample may run
   ScanArgs a = scan_args(x, bp);
   a.I = I;
   a.dense = x.pdense;
@@ -1646,12 +1648,12 @@ hnm_status ncf_cert_begin(hnm_ctx* ctx, const hnm_ncf_weights* w, const NcfTabs&
 // short_ok: a row may keep fewer than K candidates (its bound came from another shard).
 hnm_status ncf_cert_finish(hnm_ctx* ctx, const hnm_ncf_weights* w, const NcfTabs& t, int64_t B,
                            const int64_t* mptr, const int32_t* midx, int K, void* scratch,
-                           const float* lb, int short_ok, float* ov, int64_t* oi) {
+                           bool strided, const float* lb, int short_ok, float* ov, int64_t* oi) {
   const int64_t I = w->num_items;
   const int wg = ncf_cert_wg(ctx);
   const CertShape sh = cert_shape(B, I, K, ctx->num_cus, wg);
   CertWs x;
-  cert_carve((char*)scratch, B, I, K, ctx->num_cus, wg, &x);
+  cert_carve((char*)scratch, B, I, K, ctx->num_cus, wg, strided, &x);
   const int64_t ublocks = hnm_cdiv(B, 128);
   hipLaunchKernelGGL(cert_tau_kernel, dim3((unsigned)hnm_cdiv(B, 256)), dim3(256), 0,
                      ctx->stream, lb ? lb : x.lb, x.Au, x.Cu, x.Eu, x.prm, w->bp, B, x.tau, x.flag);
@@ -1686,17 +1688,17 @@ hnm_status ncf_cert_finish(hnm_ctx* ctx, const hnm_ncf_weights* w, const NcfTabs
 
 hnm_status ncf_cert_topk(hnm_ctx* ctx, const hnm_ncf_weights* w, const NcfTabs& t, int64_t B,
                          const int64_t* mptr, const int32_t* midx, int K, void* scratch,
-                         float* ov, int64_t* oi) {
-  hnm_status st = ncf_cert_begin(ctx, w, t, B, mptr, midx, K, scratch, nullptr);
+                         bool strided, float* ov, int64_t* oi) {
+  hnm_status st = ncf_cert_begin(ctx, w, t, B, mptr, midx, K, scratch, strided, nullptr);
   if (st) return st;
-  return ncf_cert_finish(ctx, w, t, B, mptr, midx, K, scratch, nullptr, 0, ov, oi);
+  return ncf_cert_finish(ctx, w, t, B, mptr, midx, K, scratch, strided, nullptr, 0, ov, oi);
 }
 
 hnm_status ncf_cert_debug(hnm_ctx* ctx, const hnm_ncf_weights* w, const NcfTabs& t, int64_t B,
                           void* scratch, float* approx, int64_t lda, float* bound) {
   const int64_t I = w->num_items;
   CertWs x;
-  cert_carve((char*)scratch, B, I, 1, ctx->num_cus, ncf_cert_wg(ctx), &x);
+  cert_carve((char*)scratch, B, I, 1, ctx->num_cus, ncf_cert_wg(ctx), false, &x);
   hnm_status st = cert_prepare(ctx, w, t, B, x);
   if (st) return st;
   hipLaunchKernelGGL(cert_bound_kernel, dim3((unsigned)hnm_cdiv(B, 256)), dim3(256), 0, ctx->stream,

@@ -799,6 +799,7 @@ static hnm_status deep_scalar_dense(hnm_ctx* ctx, const hnm_ncf_deep_weights* w,
 extern "C" hnm_status hnm_ncf_deep_scores_f32(hnm_ctx* ctx, const hnm_ncf_deep_weights* w,
                                               const int64_t* user_ids, int64_t B,
                                               const int64_t* item_ids, float* out, int64_t ldo) {
+  HNM_CTX_DEVICE(ctx);
   hnm_status st = deep_check(w);
   if (st) return st;
   HNM_REQUIRE(ctx && ((user_ids && out) || B == 0), HNM_EINVAL, "ncf_deep: NULL argument");
@@ -886,6 +887,7 @@ extern "C" hnm_status hnm_ncf_deep_topk_f32(hnm_ctx* ctx, const hnm_ncf_deep_wei
                                             const int64_t* user_ids, int64_t B,
                                             const int64_t* mask_ptr, const int32_t* mask_idx,
                                             int k, float* out_val, int64_t* out_idx) {
+  HNM_CTX_DEVICE(ctx);
   hnm_status st = deep_check(w);
   if (st) return st;
   HNM_REQUIRE(ctx && ((user_ids && out_idx) || B == 0), HNM_EINVAL, "ncf_deep_topk: NULL argument");

@@ -22,21 +22,23 @@ size_t ncf_list_bytes(int64_t B, int64_t I, int K, int num_cus);
 // Certified pre-filter path (ncf_cert.hip): eligible when h1 <= 64, mf <= 64, K <= 64 and
 // the catalogue is large enough for the sample pass to pay.
 bool ncf_cert_eligible(const hnm_ncf_weights* w, int K);
-size_t ncf_cert_bytes(int64_t B, int64_t I, int K, int num_cus, int wg);
+// strided: the call may run the gated strided sample (HNM_OPT_STRIDED), whose per-row scratch
+// ([B, I / 8] values) is carved only then; begin and finish of one call must agree on it
+size_t ncf_cert_bytes(int64_t B, int64_t I, int K, int num_cus, int wg, bool strided);
 int ncf_cert_wg(const hnm_ctx* ctx);  // scan workgroups per CU of the selected variant
 hnm_status ncf_cert_topk(hnm_ctx* ctx, const hnm_ncf_weights* w, const NcfTabs& t, int64_t B,
                          const int64_t* mptr, const int32_t* midx, int K, void* scratch,
-                         float* ov, int64_t* oi);
+                         bool strided, float* ov, int64_t* oi);
 // The two phases of ncf_cert_topk: begin writes each row's certified lower bound of the
 // exact K-th best score (real units) to lb (nullptr: kept in the scratch); finish takes any
 // lower bounds (e.g. the max over item shards) and completes the top-K.
 // lists (nullable): each row's K best certified sample lower bounds [B, K], real units.
 hnm_status ncf_cert_begin(hnm_ctx* ctx, const hnm_ncf_weights* w, const NcfTabs& t, int64_t B,
                           const int64_t* mptr, const int32_t* midx, int K, void* scratch,
-                          float* lb, float* lists = nullptr);
+                          bool strided, float* lb, float* lists = nullptr);
 hnm_status ncf_cert_finish(hnm_ctx* ctx, const hnm_ncf_weights* w, const NcfTabs& t, int64_t B,
                            const int64_t* mptr, const int32_t* midx, int K, void* scratch,
-                           const float* lb, int short_ok, float* ov, int64_t* oi);
+                           bool strided, const float* lb, int short_ok, float* ov, int64_t* oi);
 // Diagnostics: the pre-filter's approximate scores (real units, bp excluded) for every
 // item and its per-user error bound E_u: |approx + bp - exact| <= E_u is what the path
 // relies on (tests check it on the full catalogue).

@@ -597,6 +597,7 @@ extern "C" hnm_status hnm_dot_topk_f32(hnm_ctx* ctx, const float* user_tab, int6
                                        const float* const_bias, const int64_t* mask_ptr,
                                        const int32_t* mask_idx, int k, float* out_val,
                                        int64_t* out_idx) {
+  HNM_CTX_DEVICE(ctx);
   hnm_status st = dot_validate(ctx, user_tab, num_users, ldu, user_ids, B, item_tab, num_items, ldi, d);
   if (st) return st;
   HNM_REQUIRE(k >= 1 && k <= 64 && (out_idx || B == 0), HNM_EINVAL, "dot_topk: fused path needs 1 <= k <= 64");
@@ -735,6 +736,7 @@ extern "C" hnm_status hnm_dot_topk_begin_f32(hnm_ctx* ctx, const float* user_tab
                                              const float* item_bias, const float* const_bias,
                                              const int64_t* mask_ptr, const int32_t* mask_idx,
                                              int k, float* lower_bound) {
+  HNM_CTX_DEVICE(ctx);
   HNM_REQUIRE(lower_bound || B == 0, HNM_EINVAL, "dot_topk_begin: lower_bound is NULL");
   return dot_topk_begin(ctx, user_tab, num_users, ldu, user_ids, B, item_tab, num_items, ldi, d,
                         user_bias, item_bias, const_bias, mask_ptr, mask_idx, k, lower_bound,
@@ -751,6 +753,7 @@ extern "C" hnm_status hnm_dot_topk_begin_lists_f32(hnm_ctx* ctx, const float* us
                                                    const int64_t* mask_ptr,
                                                    const int32_t* mask_idx, int k,
                                                    float* lower_lists) {
+  HNM_CTX_DEVICE(ctx);
   HNM_REQUIRE(lower_lists || B == 0, HNM_EINVAL, "dot_topk_begin_lists: lower_lists is NULL");
   return dot_topk_begin(ctx, user_tab, num_users, ldu, user_ids, B, item_tab, num_items, ldi, d,
                         user_bias, item_bias, const_bias, mask_ptr, mask_idx, k, nullptr,
@@ -766,6 +769,7 @@ extern "C" hnm_status hnm_dot_topk_finish_f32(hnm_ctx* ctx, const float* user_ta
                                               const int64_t* mask_ptr, const int32_t* mask_idx,
                                               int k, const float* lower_bound, int short_ok,
                                               float* out_val, int64_t* out_idx) {
+  HNM_CTX_DEVICE(ctx);
   HNM_REQUIRE(ctx && (out_idx || B == 0), HNM_EINVAL, "dot_topk_finish: bad argument");
   if (B <= 0) return HNM_OK;
   const int kind = ctx->pend.kind;
@@ -794,6 +798,7 @@ extern "C" hnm_status hnm_dot_scores_f32(hnm_ctx* ctx, const float* user_tab, in
                                          const float* item_tab, int64_t num_items, int64_t ldi,
                                          int d, const float* user_bias, const float* item_bias,
                                          const float* const_bias, float* out, int64_t ldo) {
+  HNM_CTX_DEVICE(ctx);
   hnm_status st = dot_validate(ctx, user_tab, num_users, ldu, user_ids, B, item_tab, num_items, ldi, d);
   if (st) return st;
   HNM_REQUIRE((out || B == 0) && ldo >= num_items, HNM_EINVAL, "dot_scores: bad output");
@@ -818,6 +823,7 @@ extern "C" hnm_status hnm_topk_rows_f32(hnm_ctx* ctx, const float* scores, int64
                                         int64_t I, const int64_t* mask_ptr,
                                         const int32_t* mask_idx, int k, float* out_val,
                                         int64_t* out_idx) {
+  HNM_CTX_DEVICE(ctx);
   HNM_REQUIRE(ctx && ((scores && out_idx) || B == 0), HNM_EINVAL, "topk_rows: NULL argument");
   HNM_REQUIRE(k >= 1 && k <= I && ld >= I, HNM_EINVAL, "topk_rows: bad k/shape");
   HNM_REQUIRE(I < INT_BIG, HNM_EUNSUPPORTED, "topk_rows: too many items");
@@ -863,6 +869,7 @@ extern "C" hnm_status hnm_dot_prefilter_debug_f32(hnm_ctx* ctx, const float* use
                                                   int64_t ldi, int d, const float* user_bias,
                                                   const float* item_bias, const float* const_bias,
                                                   float* approx, int64_t lda, float* bound) {
+  HNM_CTX_DEVICE(ctx);
   hnm_status st = dot_validate(ctx, user_tab, num_users, ldu, user_ids, B, item_tab, num_items, ldi, d);
   if (st) return st;
   HNM_REQUIRE(approx && bound && lda >= num_items, HNM_EINVAL, "dot_prefilter_debug: bad output");

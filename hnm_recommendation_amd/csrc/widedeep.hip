@@ -2430,6 +2430,7 @@ extern "C" hnm_status hnm_widedeep_topk_f32(hnm_ctx* ctx, const hnm_widedeep_wei
                                             const float* user_features, const int64_t* mask_ptr,
                                             const int32_t* mask_idx, int k, float* out_val,
                                             int64_t* out_idx) {
+  HNM_CTX_DEVICE(ctx);
   HNM_REQUIRE(k >= 1 && k <= 64 && (out_idx || B == 0), HNM_EINVAL, "widedeep_topk: fused path needs 1 <= k <= 64");
   HNM_REQUIRE(ctx && (user_ids || B == 0), HNM_EINVAL, "widedeep: NULL argument");
   WdSetup S;
@@ -2460,6 +2461,7 @@ extern "C" hnm_status hnm_widedeep_scores_f32(hnm_ctx* ctx, const hnm_widedeep_w
                                               const int64_t* user_ids, int64_t B,
                                               const float* user_features, float* out,
                                               int64_t ldo) {
+  HNM_CTX_DEVICE(ctx);
   HNM_REQUIRE((out || B == 0) && w && ldo >= w->num_items, HNM_EINVAL, "widedeep_scores: bad output");
   HNM_REQUIRE(ctx && (user_ids || B == 0), HNM_EINVAL, "widedeep: NULL argument");
   WdSetup S;
@@ -2478,6 +2480,7 @@ extern "C" hnm_status hnm_widedeep_prefilter_debug_f32(hnm_ctx* ctx,
                                                        const float* user_features,
                                                        float* approx, int64_t lda,
                                                        float* bound) {
+  HNM_CTX_DEVICE(ctx);
   HNM_REQUIRE(ctx && user_ids && approx && bound && w && lda >= w->num_items, HNM_EINVAL,
               "widedeep_prefilter_debug: bad argument");
   WdSetup S;
@@ -2509,6 +2512,7 @@ extern "C" hnm_status hnm_widedeep_refine_debug_f32(hnm_ctx* ctx, const hnm_wide
                                                     const int64_t* user_ids, int64_t B,
                                                     const float* user_features, float* approx,
                                                     int64_t lda, float* bound) {
+  HNM_CTX_DEVICE(ctx);
   HNM_REQUIRE(ctx && user_ids && approx && bound && w && lda >= w->num_items, HNM_EINVAL,
               "widedeep_refine_debug: bad argument");
   WdSetup S;
@@ -2576,6 +2580,7 @@ extern "C" hnm_status hnm_widedeep_pair_scores_ex_f32(hnm_ctx* ctx, const hnm_wi
                                                       const float* user_features,
                                                       const float* item_features, int64_t n,
                                                       float* out) {
+  HNM_CTX_DEVICE(ctx);
   HNM_REQUIRE(ctx && w && ((user_ids && item_ids && out) || n == 0), HNM_EINVAL, "widedeep_pair: NULL argument");
   HNM_REQUIRE(w->l1 <= 512 && w->l2 <= 512 && w->l3 <= 512 && w->l1_in <= 512, HNM_EUNSUPPORTED,
               "widedeep_pair: widths must be <= 512");
@@ -2645,6 +2650,7 @@ extern "C" hnm_status hnm_widedeep_pair_scores_f32(hnm_ctx* ctx, const hnm_wided
                                                    const int64_t* item_ids,
                                                    const float* user_features, int64_t n,
                                                    float* out) {
+  HNM_CTX_DEVICE(ctx);
   return hnm_widedeep_pair_scores_ex_f32(ctx, w, nullptr, user_ids, item_ids, user_features,
                                          nullptr, n, out);
 }

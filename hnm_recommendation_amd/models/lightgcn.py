@@ -55,30 +55,50 @@ class NormalizedGraph:
                                                    C.byref(plan)), "hnm_spmm_plan_create")
         self.plan = plan
         self.prepared = set()
+        self._restricted: Dict[tuple, C.c_void_p] = {}
         # bind the plan to this CSR's col / val (a walk plan sorts a copy of every row once)
         self.prepare(0)
 
-    def prepare(self, d: int):
+    def prepare(self, d: int, plan=None):
         """One-time plan work for embedding width d (hnm_spmm_plan_prepare: the walk schedules;
         d = 0 binds the plan to col / val only), so no SpMM call does host work or syncs."""
-        if d in self.prepared:
+        key = (d, None if plan is None else plan.value)
+        if key in self.prepared:
             return
         c = _lib.ctx(self.device)
-        _lib.check(_lib.fn("hnm_spmm_plan_prepare")(c, self.plan, _lib.ptr(self.col),
-                                                    _lib.ptr(self.val), int(d)),
+        _lib.check(_lib.fn("hnm_spmm_plan_prepare")(c, self.plan if plan is None else plan,
+                                                    _lib.ptr(self.col), _lib.ptr(self.val), int(d)),
                    "hnm_spmm_plan_prepare")
-        self.prepared.add(d)
+        self.prepared.add(key)
+
+    def restricted(self, ranges, d: int = 0):
+        """A plan that computes only the rows of `ranges` ((begin, end) pairs, ascending), each
+        summed exactly as by the whole-graph plan (hnm_spmm_plan_restrict): one rank's share of
+        the item-sharded propagation.  Built once per ranges (host work), prepared for d."""
+        key = tuple((int(a), int(b)) for a, b in ranges)
+        p = self._restricted.get(key)
+        if p is None:
+            flat = (C.c_int64 * (2 * len(key)))(*[x for r in key for x in r])
+            p = C.c_void_p()
+            _lib.check(_lib.fn("hnm_spmm_plan_restrict")(_lib.ctx(self.device), self.plan, flat,
+                                                         len(key), C.byref(p)),
+                       "hnm_spmm_plan_restrict")
+            self._restricted[key] = p
+        if d:
+            self.prepare(d, p)
+        return p
 
     def spmm(self, X: torch.Tensor, Y: Optional[torch.Tensor], alpha: float,
              acc: Optional[torch.Tensor], acc_in: bool = True, beta: float = 0.0,
-             rows: Optional[Tuple[int, int]] = None, acc_row0: int = 0):
+             rows: Optional[Tuple[int, int]] = None, acc_row0: int = 0, plan=None):
         """Y = A X on rows [r0, r1) (default all);  acc = fma(alpha, Y, acc or beta * X) on
-        rows >= acc_row0, stored from acc_row0 on (either output optional)."""
+        rows >= acc_row0, stored from acc_row0 on (either output optional).  plan: a
+        `restricted` plan (only its rows are computed) instead of the whole-graph one."""
         r0, r1 = (0, self.num_nodes) if rows is None else rows
         c = _lib.ctx(X.device)
         _lib.check(_lib.fn("hnm_spmm_csr_range_f32")(
-            c, self.plan, self.num_nodes, _lib.ptr(self.rowptr), _lib.ptr(self.col),
-            _lib.ptr(self.val), _lib.ptr(X), X.shape[1], _lib.ptr(Y), alpha,
+            c, self.plan if plan is None else plan, self.num_nodes, _lib.ptr(self.rowptr),
+            _lib.ptr(self.col), _lib.ptr(self.val), _lib.ptr(X), X.shape[1], _lib.ptr(Y), alpha,
             _lib.ptr(acc) if acc_in else None, _lib.ptr(acc), beta, r0, r1, acc_row0),
             "hnm_spmm_csr_range_f32")
 
@@ -102,6 +122,8 @@ class NormalizedGraph:
         if plan and _lib._lib is not None:
             try:
                 torch.cuda.synchronize(self.device)
+                for p in getattr(self, "_restricted", {}).values():
+                    _lib.fn("hnm_spmm_plan_destroy")(p)
                 _lib.fn("hnm_spmm_plan_destroy")(plan)
             except Exception:
                 pass
@@ -233,6 +255,37 @@ class LightGCN(RecModule):
                    beta=float(self.alpha[0]), rows=(U, N) if last else None, acc_row0=U)
             if not last:
                 layers.append(nxt)
+        return g.rows_combine(u, layers, self.alpha), acc
+
+    def propagate_for_shard(self, user_ids: torch.Tensor, lo: int, hi: int, exchange,
+                            g: Optional[NormalizedGraph] = None
+                            ) -> Tuple[torch.Tensor, torch.Tensor]:
+        """propagate_for with the item rows sharded over the ranks of a node:
+        (final rows of the listed users [B, d], final rows of THIS rank's items [lo, hi)
+        [hi - lo, d]).  Every rank computes all user rows of layers 1..L-1 (they gather the
+        whole item table) and only its own item rows (a restricted plan: hnm_spmm_plan_restrict),
+        `exchange(Y)` (sharding.ItemRowExchange: one all_gather of the [I, d] item rows) fills
+        the other shards' item rows after each of those layers, and the last layer runs on the
+        rank's items alone.  Rows are summed exactly as by the whole-graph plan, so the outputs
+        are bitwise those of propagate_for / forward()."""
+        from ..sharding import item_sharded_layers
+        g = self._device_graph() if g is None else g
+        U, L, d = self.num_users, self.num_layers, self.embedding_dim
+        if not 0 <= lo <= hi <= self.num_items:
+            raise ValueError(f"item shard [{lo}, {hi}) outside [0, {self.num_items})")
+        if lo == 0 and hi == self.num_items:
+            return self.propagate_for(user_ids, g)
+        u, hu = self._ids(user_ids, U)
+        E0 = f32c(self.embeddings.weight)
+        _lib.require_gpu(E0)
+        if L == 0:
+            return E0[u] * float(self.alpha[0]), E0[U + lo:U + hi] * float(self.alpha[0])
+        plan = g.restricted(((0, U), (U + lo, U + hi)), d)
+
+        def layer(X, Y, alpha, acc, acc_in, beta, last):
+            g.spmm(X, Y, alpha, acc, acc_in=acc_in, beta=beta,
+                   rows=(U + lo, U + hi) if last else None, acc_row0=U + lo, plan=plan)
+        layers, acc = item_sharded_layers(E0, U, L, self.alpha, lo, hi, layer, exchange)
         return g.rows_combine(u, layers, self.alpha), acc
 
     # ------------------------------------------------------------------ scoring

@@ -329,8 +329,13 @@ class dot_shard_topk:
     per-call user rows)."""
 
     def __init__(self, user_tab: torch.Tensor, item_tab: torch.Tensor, lo: int, hi: int, k: int,
-                 history=None, user_bias=None, item_bias=None, const_bias=None):
-        self.user_tab, self.shard, self.k = user_tab, item_tab[lo:hi], k
+                 history=None, user_bias=None, item_bias=None, const_bias=None,
+                 shard_table: bool = False):
+        """shard_table: item_tab holds the shard's rows [lo, hi) only (an item-sharded
+        LightGCN propagation's output) instead of the whole catalogue."""
+        if shard_table and item_tab.shape[0] != hi - lo:
+            raise ValueError(f"shard table of {item_tab.shape[0]} rows for items [{lo}, {hi})")
+        self.user_tab, self.shard, self.k = user_tab, (item_tab if shard_table else item_tab[lo:hi]), k
         self.lo, self.hi, self.n = lo, hi, hi - lo
         self.history = history
         # MatrixFactorization's score terms (matrix_factorization.py:108-131): [U], [I] (the
@@ -427,20 +432,92 @@ def widedeep_shard_topk(model, lo: int, hi: int, k: int, history=None) -> LocalT
     return run
 
 
+def item_sharded_layers(E0: torch.Tensor, num_users: int, num_layers: int, alphas, lo: int,
+                        hi: int, layer, exchange):
+    """The layer loop of the item-sharded LightGCN propagation (`lightgcn.py:136-164`, one rank
+    of a node): every rank computes ALL user rows of layers 1..L-1 (each gathers the whole item
+    table) but only ITS item rows [U+lo, U+hi); after each of those layers `exchange(Y)` fills
+    the other shards' item rows of Y (an all_gather of [I, d]: 54 MB at the H&M shape, d = 128,
+    against the 702 MB user half it would take to shard the users too), and the last layer runs
+    on the rank's item rows alone.  The combine sum_l alpha_l E_l is kept for those rows.
+
+    layer(X, Y, alpha, acc, acc_in, beta, last) computes rows [0, U) and [U+lo, U+hi) of
+    Y = A_hat X (only [U+lo, U+hi) when last; Y None then) with the fused combine into acc
+    (rows U+lo.. stored from 0; acc_in False: beta * X).  Returns (E_0 .. E_{L-1}, acc [hi-lo, d]).
+    The product passes a restricted SpMM plan (LightGCN.propagate_for_shard); the CPU tests
+    pass the oracle's row-restricted SpMM and a gloo exchange."""
+    acc = torch.empty(hi - lo, E0.shape[1], dtype=E0.dtype, device=E0.device)
+    layers = [E0]
+    for li in range(num_layers):
+        last = li == num_layers - 1
+        nxt = None if last else torch.empty_like(E0)
+        layer(layers[-1], nxt, float(alphas[li + 1]), acc, li > 0, float(alphas[0]), last)
+        if not last:
+            exchange(nxt)
+            layers.append(nxt)
+    return layers, acc
+
+
+class ItemRowExchange:
+    """Fills the other shards' item rows of a propagation layer Y [U + I, d]: rank r computed
+    rows U + shard_range(I, r, G); one all_gather_into_tensor of every shard's rows (padded to
+    the largest shard, m rows: G * m * d * 4 bytes received per rank), then one copy per other
+    shard into place.  RCCL moves device tensors; gloo (CPU tests, one-GPU rehearsal) is staged
+    through host memory."""
+
+    def __init__(self, num_users: int, num_items: int, rank: int, world: int, group=None):
+        self.U, self.I, self.rank, self.world, self.group = num_users, num_items, rank, world, group
+        self.ranges = [shard_range(num_items, r, world) for r in range(world)]
+        self.m = max(b - a for a, b in self.ranges)
+        self.calls = 0
+
+    def bytes_per_call(self, d: int, itemsize: int = 4) -> int:
+        return self.world * self.m * d * itemsize
+
+    def __call__(self, Y: torch.Tensor):
+        G, m, U = self.world, self.m, self.U
+        lo, hi = self.ranges[self.rank]
+        d = Y.shape[1]
+        host = dist.get_backend(self.group) == "gloo"
+        own = Y[U + lo:U + hi]
+        if hi - lo == m and not host:
+            send = own                     # contiguous rows: no staging copy
+        else:
+            send = torch.empty(m, d, dtype=Y.dtype, device="cpu" if host else Y.device)
+            send[:hi - lo].copy_(own)
+            if hi - lo < m:
+                send[hi - lo:].zero_()
+        recv = torch.empty(G * m, d, dtype=Y.dtype, device=send.device)
+        dist.all_gather_into_tensor(recv, send, group=self.group)
+        for r, (a, b) in enumerate(self.ranges):
+            if r != self.rank and b > a:
+                Y[U + a:U + b].copy_(recv[r * m:r * m + (b - a)])
+        self.calls += 1
+
+
 class lightgcn_shard_topk:
     """LightGCN recommend() over item rows [lo, hi) with the propagation recomputed per
     call, as the reference does (`lightgcn.py:197` -> `forward()`), restricted to what the
-    call reads: `LightGCN.propagate_for(all users of the step)` (layers 1..L-1 whole graph,
-    the last layer on item rows + these users), then the dot top-K over the shard."""
+    call reads, then the dot top-K over the shard.  exchange None: `LightGCN.propagate_for(all
+    users of the step)` (layers 1..L-1 whole graph, the last layer on item rows + these users),
+    replicated per rank; an `ItemRowExchange`: `LightGCN.propagate_for_shard` -- the item rows
+    of every layer sharded over the ranks, one all_gather of [I, d] after each of layers
+    1..L-1, the last layer on this shard's items only (outputs bitwise the same)."""
 
-    def __init__(self, model, lo: int, hi: int, k: int, history=None):
+    def __init__(self, model, lo: int, hi: int, k: int, history=None, exchange=None):
         self.model, self.lo, self.hi, self.k = model, lo, hi, k
         self.history = history
+        self.exchange = exchange
         self._dot = None
         self._rows = None
 
     def _scorer(self, user_ids):
-        fb, fi = self.model.propagate_for(user_ids)
+        if self.exchange is None:
+            fb, fi = self.model.propagate_for(user_ids)
+            shard = False
+        else:
+            fb, fi = self.model.propagate_for_shard(user_ids, self.lo, self.hi, self.exchange)
+            shard = True
         n, dev = user_ids.numel(), user_ids.device
         if self._rows is None or self._rows.numel() < n or self._rows.device != dev:
             # kept across calls (one launch less a call); completed before any stream reads it
@@ -448,7 +525,7 @@ class lightgcn_shard_topk:
             if dev.type == "cuda":
                 torch.cuda.current_stream(dev).synchronize()
         rows = self._rows[:n]
-        dot = dot_shard_topk(fb, fi, self.lo, self.hi, self.k, self.history)
+        dot = dot_shard_topk(fb, fi, self.lo, self.hi, self.k, self.history, shard_table=shard)
         dot.mask_users = user_ids.to(torch.int64).contiguous()   # history keyed by user id
         return dot, rows
 

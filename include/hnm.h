@@ -22,6 +22,12 @@
  *    it.  A stream handed to hnm_ctx_set_stream must therefore stay alive until the ctx has
  *    been switched away from it (torch's pooled streams always do; a caller-owned
  *    hipStream_t / torch.cuda.ExternalStream must outlive that switch).
+ *  - Device binding: a ctx belongs to the device it was created on.  Every entry that takes
+ *    a ctx switches the calling thread to ctx->device for its duration (workspace allocation,
+ *    events, launches, the null stream when no stream was set) and restores the caller's
+ *    current device before returning; hnm_ctx_create leaves the current device unchanged.  So
+ *    one host thread may drive ctxs of several GPUs; the pointers passed to a call must live on
+ *    that ctx's device, and a stream set with hnm_ctx_set_stream must belong to it.
  *  - Status: 0 on success, negative on error; hnm_last_error() holds a thread-local
  *    message.  No C++ exception crosses the ABI.
  *  - Out-of-range user/item ids never fault: the row is skipped (index -1 / NaN) and the
@@ -208,7 +214,9 @@ typedef struct {
   int32_t h0;
   int32_t h1;
   int32_t h2;
-  /* Optional (NULL: computed per call): the item half of layer 1 for THESE num_items rows,
+  /* Optional (NULL: computed per call; ZERO-INITIALISE the struct so an unset field is NULL --
+   * a non-NULL pointer is used as the table, and one that is not 16-B aligned is refused with
+   * HNM_EINVAL): the item half of layer 1 for THESE num_items rows,
    * W1[:, h0:] m_i pair-permuted, [num_items, 64] (h1 <= 64 and mf <= 64) or [num_items, 128],
    * as hnm_ncf_item_proj_f32 writes it -- for callers whose item tables and W1 stay fixed
    * between calls (a server); a row shard points at its first row. */
@@ -401,6 +409,12 @@ hnm_status hnm_rccl_unique_id(void* out, int64_t size);
 hnm_status hnm_ctx_rccl_init(hnm_ctx* ctx, int world, int rank, const void* unique_id,
                              int64_t size);
 hnm_status hnm_ctx_set_rccl_comm(hnm_ctx* ctx, void* comm);
+/* Abort the ctx's own communicator (ncclCommAbort; a borrowed one is only detached).  When
+ * hnm_topk_allgather_merge_f32 returns an error on one rank (argument check, open two-phase
+ * call, workspace ENOMEM -- all checked before the collective), that rank never entered the
+ * collective its peers are waiting in: the host aborts the communicator on every rank and
+ * creates a new one (hnm_ctx_rccl_init). */
+hnm_status hnm_ctx_rccl_abort(hnm_ctx* ctx);
 hnm_status hnm_topk_allgather_merge_f32(hnm_ctx* ctx, const float* local_val,
                                         const int64_t* local_idx, int64_t B, int k,
                                         float* out_val, int64_t* out_idx);
@@ -500,6 +514,17 @@ hnm_status hnm_spmm_plan_create(hnm_ctx* ctx, int64_t N, const int64_t* rowptr,
 hnm_status hnm_spmm_plan_prepare(hnm_ctx* ctx, hnm_spmm_plan* plan, const int32_t* col,
                                  const float* val, int d);
 hnm_status hnm_spmm_plan_destroy(hnm_spmm_plan* plan);
+/* A row-restricted copy of a BOUND plan (no reference counterpart: the item-sharded LightGCN
+ * propagation of SURVEY §8(e)).  The new plan computes only the rows inside the n_ranges host
+ * ranges [ranges[2j], ranges[2j+1]) (ascending, disjoint, within [0, N)); SpMM calls on it never
+ * write other rows of Y or acc.  Every kept row is summed exactly as the base plan sums it (same
+ * pieces and order: bitwise equal rows), and a walk plan's schedules hold only the kept rows'
+ * entries, so a layer costs what its kept rows cost (one rank: all user rows + its item shard).
+ * The copy is bound to the base's col / val, owns its own sorted copy and schedules (destroy it
+ * separately; its per-d schedules are built on first use / prepare as for any plan);
+ * rows_combine on it equals rows_combine on the base.  The base itself must not be restricted. */
+hnm_status hnm_spmm_plan_restrict(hnm_ctx* ctx, const hnm_spmm_plan* base, const int64_t* ranges,
+                                  int n_ranges, hnm_spmm_plan** out);
 hnm_status hnm_spmm_csr_f32(hnm_ctx* ctx, const hnm_spmm_plan* plan, int64_t N,
                             const int64_t* rowptr, const int32_t* col, const float* val,
                             const float* X, int d, float* Y, float alpha,

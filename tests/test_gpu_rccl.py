@@ -200,3 +200,61 @@ def _c_exchange_worker(rank):
 
 def test_c_abi_rccl_exchange_one_rank():
     mp.spawn(_c_exchange_worker, nprocs=1, join=True)
+
+
+def _device_binding_worker(rank):
+    """hnm.h "Device binding": hnm_ctx_create leaves the caller's current device unchanged (also
+    for a refused device id); with two or more GPUs, a ctx of device 0 driven from a thread whose
+    current device is 1 runs a fused top-k and the C-ABI exchange on device 0 (results equal to
+    the same calls made from device 0) and leaves device 1 current; hnm_ctx_rccl_abort releases
+    the ctx's communicator (the exchange is then refused)."""
+    import ctypes as C
+    f = _lib.fn
+    ndev = torch.cuda.device_count()
+    torch.cuda.set_device(0)
+    h = C.c_void_p()
+    assert f("hnm_ctx_create")(ndev + 3, C.byref(h)) == _lib.HNM_EINVAL
+    assert torch.cuda.current_device() == 0
+    other = 1 if ndev > 1 else 0
+    torch.cuda.set_device(other)
+    _lib.check(f("hnm_ctx_create")(0, C.byref(h)), "ctx_create")
+    assert torch.cuda.current_device() == other
+    dev = torch.device("cuda", 0)
+    U, I, d, B, k = 3000, 20_000, 64, 200, 12
+    sd = syn.lightgcn_state_dict(U, I, d, seed=6)
+    ut = torch.from_numpy(sd["embeddings.weight"][:U]).to(dev)
+    it = torch.from_numpy(sd["embeddings.weight"][U:]).to(dev)
+    users = torch.from_numpy(syn.user_batch(U, B, seed=4)).to(dev)
+    torch.cuda.synchronize(dev)
+    ov = torch.empty(B, k, device=dev)
+    oi = torch.empty(B, k, dtype=torch.int64, device=dev)
+    try:
+        _lib.check(f("hnm_dot_topk_f32")(h, _lib.ptr(ut), U, d, _lib.ptr(users), B, _lib.ptr(it), I, d,
+                                         d, None, None, None, None, None, k, _lib.ptr(ov),
+                                         _lib.ptr(oi)), "dot_topk")
+        assert torch.cuda.current_device() == other
+        uid = (C.c_char * 128)()
+        _lib.check(f("hnm_rccl_unique_id")(uid, 128), "unique_id")
+        _lib.check(f("hnm_ctx_rccl_init")(h, 1, 0, uid, 128), "rccl_init")
+        mv = torch.empty(B, k, device=dev)
+        mi = torch.empty(B, k, dtype=torch.int64, device=dev)
+        _lib.check(f("hnm_topk_allgather_merge_f32")(h, _lib.ptr(ov), _lib.ptr(oi), B, k,
+                                                     _lib.ptr(mv), _lib.ptr(mi)), "merge")
+        assert torch.cuda.current_device() == other
+        _lib.check(f("hnm_ctx_check")(h), "check")
+        torch.cuda.set_device(0)
+        ref = S.dot_shard_topk(ut, it, 0, I, k)(users)
+        _same((ov, oi), ref, "dot top-k from another current device")
+        _same((mv, mi), ref, "C exchange from another current device")
+        _lib.check(f("hnm_ctx_rccl_abort")(h), "rccl_abort")
+        with pytest.raises(ValueError):
+            _lib.check(f("hnm_topk_allgather_merge_f32")(h, _lib.ptr(ov), _lib.ptr(oi), B, k,
+                                                         _lib.ptr(mv), _lib.ptr(mi)), "merge")
+        print(f"device binding checked with {ndev} visible device(s)")
+    finally:
+        f("hnm_ctx_destroy")(h)
+    assert torch.cuda.current_device() == 0
+
+
+def test_c_abi_device_binding():
+    mp.spawn(_device_binding_worker, nprocs=1, join=True)

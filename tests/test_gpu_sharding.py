@@ -97,8 +97,8 @@ def test_two_phase_contract():
 
 
 # ------------------------------------------------------------------ BASELINE configs[4]
-# LightGCN d=128 at the full H&M shape (65M-nnz graph), item table row-sharded, one
-# exchange step -- rehearsed with 2 gloo ranks on one GPU.
+# LightGCN d=128 at the full H&M shape (65M-nnz graph): propagation item rows and the item
+# table row-sharded, the bound and candidate exchanges -- rehearsed with 2 gloo ranks on one GPU.
 LU, LI = syn.HM_USERS, syn.HM_ITEMS
 LB = 512
 
@@ -120,12 +120,15 @@ def _lgcn_worker(rank, world, port, out_dir):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         m = _lightgcn128()
-        fu, fi = m.forward()  # propagation replicated per rank
         lo, hi = S.shard_range(LI, rank, world)
         users = torch.from_numpy(syn.user_batch(LU, LB, seed=70 + rank)).cuda()
-        rec = S.ItemShardedRecommender(S.dot_shard_topk(fu, fi, lo, hi, K), S.hip_merge, K, lo,
-                                       rank, world)
+        # the propagation recomputed per call with its item rows sharded over the ranks
+        # (restricted plans + one all_gather of the [I, d] item rows after layers 1 and 2)
+        ex = S.ItemRowExchange(LU, LI, rank, world)
+        rec = S.ItemShardedRecommender(S.lightgcn_shard_topk(m, lo, hi, K, exchange=ex),
+                                       S.hip_merge, K, lo, rank, world)
         v, i = rec.recommend(users)
+        assert ex.calls == 2
         np.savez(os.path.join(out_dir, f"l{rank}.npz"), users=users.cpu().numpy(),
                  v=v.cpu().numpy(), i=i.cpu().numpy())
     finally:

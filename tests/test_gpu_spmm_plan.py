@@ -248,3 +248,122 @@ def test_spmm_bipartite_side_routing(kind):
         assert torch.equal(out, y1[rows])
     finally:
         _lib.fn("hnm_spmm_plan_destroy")(plan)
+
+
+@pytest.mark.parametrize("d", [64, 128])
+def test_restricted_plan_rows_bitwise(d):
+    """hnm_spmm_plan_restrict (item-sharded propagation): a plan keeping the user
+    rows plus one item shard computes exactly those rows, bitwise equal to the whole-graph plan
+    (same pieces, same order -- split item rows of > cap entries and the tail items the bipartite
+    routing moved into the walk included), and writes nothing else; shards covering the items
+    together reproduce the whole layer; an empty range, ragged shards, the acc epilogue from
+    acc_row0 and rows_combine on the restricted plan agree too; bad ranges are refused."""
+    from hnm_recommendation_amd import sharding as S
+    U, I = 150_000, 5_000
+    edges = syn.bipartite_edge_index(U, I, 900_000, seed=7, zipf=1.1)
+    m, g = _graph(U, I, edges, d)
+    N = U + I
+    L = np.diff(g.rowptr.cpu().numpy())
+    assert L[U:].max() > 2 * 512 and (L[U:] <= 128).any()     # split rows and short items
+    x = torch.randn(N, d, generator=torch.Generator().manual_seed(4)).to(DEV)
+    y = torch.empty_like(x)
+    acc_full = torch.empty(I, d, device=DEV)
+    g.spmm(x, y, 0.7, acc_full, acc_in=False, beta=0.25, acc_row0=U)
+    G = 3
+    cover = torch.full_like(x, float("nan"))
+    for r in range(G):
+        lo, hi = S.shard_range(I, r, G)
+        plan = g.restricted(((0, U), (U + lo, U + hi)), d)
+        yr = torch.full_like(x, float("nan"))
+        acc = torch.empty(hi - lo, d, device=DEV)
+        g.spmm(x, yr, 0.7, acc, acc_in=False, beta=0.25, acc_row0=U + lo, plan=plan)
+        torch.cuda.synchronize()
+        assert torch.equal(yr[:U], y[:U]) and torch.equal(yr[U + lo:U + hi], y[U + lo:U + hi])
+        assert torch.isnan(yr[U:U + lo]).all() and torch.isnan(yr[U + hi:]).all()
+        assert torch.equal(acc, acc_full[lo:hi])
+        # the last layer's form: the shard's item rows only
+        yl = torch.full_like(x, float("nan"))
+        g.spmm(x, yl, 0.0, None, rows=(U + lo, U + hi), plan=plan)
+        torch.cuda.synchronize()
+        assert torch.equal(yl[U + lo:U + hi], y[U + lo:U + hi]) and torch.isnan(yl[:U + lo]).all()
+        cover[U + lo:U + hi] = yr[U + lo:U + hi]
+        rows = torch.tensor([0, U - 1, U + lo, U + hi - 1, N - 1], dtype=torch.int64, device=DEV)
+        out = torch.empty(rows.numel(), d, device=DEV)
+        assert _combine_raw(g, plan, rows, [x], [0.0, 1.0], out) == 0
+        torch.cuda.synchronize()
+        assert torch.equal(out, y[rows])
+    assert torch.equal(cover[U:], y[U:])
+    # an item-only plan with an empty range beside it
+    plan = g.restricted(((U, U), (U + 10, U + 4000)), d)
+    ye = torch.full_like(x, float("nan"))
+    g.spmm(x, ye, 0.0, None, plan=plan)
+    torch.cuda.synchronize()
+    assert torch.equal(ye[U + 10:U + 4000], y[U + 10:U + 4000])
+    assert torch.isnan(ye[:U + 10]).all() and torch.isnan(ye[U + 4000:]).all()
+    c = _lib.ctx(x.device)
+    p = C.c_void_p()
+    for bad in ((5, 3), (0, N + 1), (10, 20, 15, 30)):
+        flat = (C.c_int64 * len(bad))(*bad)
+        assert _lib.fn("hnm_spmm_plan_restrict")(c, g.plan, flat, len(bad) // 2, C.byref(p)) == _lib.HNM_EINVAL
+    flat = (C.c_int64 * 2)(0, U)
+    assert _lib.fn("hnm_spmm_plan_restrict")(c, plan, flat, 1, C.byref(p)) == _lib.HNM_EINVAL
+
+
+def test_restricted_legacy_plan():
+    """A restricted plan without the walks (> 2^22 nodes): the kept sub-ranges by the row-class
+    kernels, bitwise the whole-graph rows, other rows untouched."""
+    U, I, d = (1 << 22) + 3000, 4000, 16
+    base = syn.bipartite_edge_index(U, I, 2_000_000, seed=9)
+    hub = np.stack([np.arange(0, U, 997), np.zeros(len(range(0, U, 997)), np.int64) + U])
+    edges = np.concatenate([base, hub, hub[::-1]], axis=1)
+    m, g = _graph(U, I, edges, d)
+    x = torch.randn(U + I, d, generator=torch.Generator().manual_seed(3)).to(DEV)
+    y = torch.empty_like(x)
+    g.spmm(x, y, 0.0, None)
+    plan = g.restricted(((1000, 50_000), (U, U + 1500)), d)
+    yr = torch.full_like(x, float("nan"))
+    g.spmm(x, yr, 0.0, None, plan=plan)
+    torch.cuda.synchronize()
+    assert torch.equal(yr[1000:50_000], y[1000:50_000]) and torch.equal(yr[U:U + 1500], y[U:U + 1500])
+    assert torch.isnan(yr[:1000]).all() and torch.isnan(yr[50_000:U]).all() and torch.isnan(yr[U + 1500:]).all()
+
+
+def test_item_sharded_propagation_full_shape():
+    """LightGCN.propagate_for_shard at the full H&M shape (configs[2]/[4] graph, d = 64): each of
+    8 emulated ranks runs the product method with its restricted plan, and its exchange hands it
+    the other shards' item rows from a whole-graph reference run (what the all_gather delivers)
+    after checking the rows the rank computed itself -- every user row and its item shard of
+    layers 1 and 2 -- bit for bit.  The rank's final item rows and the batch users' final rows
+    equal propagate_for's (= forward()'s) bitwise."""
+    from hnm_recommendation_amd import sharding as S
+    U, I, d, G = syn.HM_USERS, syn.HM_ITEMS, 64, 8
+    edges = syn.bipartite_edge_index(U, I, syn.HM_INTERACTIONS, seed=2)
+    m = LightGCN(U, I, embedding_dim=d, num_layers=3)
+    m.set_graph(torch.from_numpy(edges))
+    del edges
+    sd = syn.lightgcn_state_dict(U, I, d, seed=0)
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
+    m = m.to(DEV).eval()
+    g = m._device_graph()
+    E0 = m.embeddings.weight.detach()
+    ref = [E0]
+    for _ in range(2):
+        y = torch.empty_like(E0)
+        g.spmm(ref[-1], y, 0.0, None)
+        ref.append(y)
+    users = torch.from_numpy(syn.user_batch(U, 4096, seed=5)).to(DEV)
+    fb_ref, fi_ref = m.propagate_for(users)
+    for r in (0, 3, G - 1):
+        lo, hi = S.shard_range(I, r, G)
+        seen = []
+
+        def exchange(Y, lo=lo, hi=hi, seen=seen):
+            want = ref[len(seen) + 1]
+            seen.append(torch.equal(Y[:U], want[:U]) and torch.equal(Y[U + lo:U + hi], want[U + lo:U + hi]))
+            Y[U:U + lo] = want[U:U + lo]
+            Y[U + hi:] = want[U + hi:]
+        fb, fi = m.propagate_for_shard(users, lo, hi, exchange)
+        torch.cuda.synchronize()
+        assert seen == [True, True], (r, seen)
+        assert torch.equal(fi, fi_ref[lo:hi]), r
+        assert torch.equal(fb, fb_ref), r

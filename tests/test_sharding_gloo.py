@@ -192,3 +192,91 @@ def test_exchange_requires_process_group():
         pytest.skip("a process group is live in this process")
     with pytest.raises(RuntimeError, match="process group"):
         S.ItemShardedRecommender(lambda u: u, _np_merge, K, 0, exchange=True)
+
+
+# ------------------------------------------------------------------ item-sharded propagation
+# configs[4]'s LightGCN propagation with the item rows sharded (sharding.item_sharded_layers +
+# ItemRowExchange): each rank computes every user row and its own item rows of each layer, one
+# gloo all_gather fills the other shards' item rows, the last layer runs on the rank's items.
+# The SpMM here is the oracle's COO sum restricted to the kept rows (np.add.at keeps each row's
+# entry order, so a row's value does not depend on which other rows are computed -- as the
+# restricted HIP plan guarantees); the sharded outputs must equal the unsharded run bit for bit.
+PU, PI, PD, PL = 230, 173, 8, 3
+
+
+def _prop_graph():
+    ei = syn.bipartite_edge_index(PU, PI, 1500, seed=4)
+    return O.lightgcn_set_graph(ei, None, PU + PI)
+
+
+def _prop_layer(graph, kept_rows):
+    row, col, val = graph
+
+    def layer(X, Y, alpha, acc, acc_in, beta, last):
+        keep = kept_rows(last)
+        sel = np.isin(row, keep)
+        y = np.zeros((X.shape[0], X.shape[1]), np.float32)
+        np.add.at(y, row[sel], X.numpy()[col[sel]] * val[sel][:, None])
+        y = torch.from_numpy(y)
+        if Y is not None:
+            Y[keep] = y[keep]
+        items = keep[keep >= PU]
+        a0 = items.min() if items.size else PU
+        base = acc[items - a0] if acc_in else beta * X[items]
+        acc[items - a0] = base + alpha * y[items]
+    return layer
+
+
+def _prop_run(rank, world, exchange):
+    graph = _prop_graph()
+    lo, hi = S.shard_range(PI, rank, world)
+    E0 = torch.from_numpy(np.random.default_rng(3).standard_normal((PU + PI, PD)).astype(np.float32))
+    own = np.arange(PU + lo, PU + hi)
+    layer = _prop_layer(graph, lambda last: own if last else np.concatenate([np.arange(PU), own]))
+    alphas = O.lightgcn_alphas(PL)
+    layers, acc = S.item_sharded_layers(E0, PU, PL, alphas, lo, hi, layer, exchange)
+    # the batch users' final rows from the layer inputs (what rows_combine computes)
+    row, col, val = graph
+    last = np.zeros((PU + PI, PD), np.float32)
+    np.add.at(last, row, layers[-1].numpy()[col] * val[:, None])
+    users = np.arange(0, PU, 7)
+    fu = sum(np.float32(a) * t.numpy()[users] for a, t in zip(alphas, layers)) + np.float32(alphas[-1]) * last[users]
+    return [t.numpy()[PU:].copy() for t in layers[1:]], acc.numpy(), fu
+
+
+def _prop_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        ex = S.ItemRowExchange(PU, PI, rank, world)
+        layers, acc, fu = _prop_run(rank, world, ex)
+        assert ex.calls == PL - 1
+        q.put((rank, layers, acc, fu))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3, 8])
+def test_item_sharded_propagation_matches_unsharded(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_prop_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = [q.get(timeout=300) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    ref_layers, ref_acc, ref_fu = _prop_run(0, 1, lambda Y: None)
+    # and the unsharded run against the oracle's forward (different combine order: tolerance)
+    fu_o, fi_o = O.lightgcn_forward(
+        np.random.default_rng(3).standard_normal((PU + PI, PD)).astype(np.float32), _prop_graph(), PU, PL)
+    np.testing.assert_allclose(ref_acc, fi_o, rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(ref_fu, fu_o[::7], rtol=1e-5, atol=1e-6)
+    for rank, layers, acc, fu in results:
+        lo, hi = S.shard_range(PI, rank, world)
+        for got, ref in zip(layers, ref_layers):   # every item row after the exchange
+            assert np.array_equal(got.view(np.uint32), ref.view(np.uint32)), f"rank {rank}"
+        assert np.array_equal(acc.view(np.uint32), ref_acc[lo:hi].view(np.uint32)), f"rank {rank}"
+        assert np.array_equal(fu.view(np.uint32), ref_fu.view(np.uint32)), f"rank {rank}"
