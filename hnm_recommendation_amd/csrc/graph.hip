@@ -1163,6 +1163,12 @@ static hnm_status walk_build(hnm_spmm_plan* pl, int d, WalkSched** out) {
   int64_t nwg = std::max<int64_t>(1, std::min<int64_t>(hnm_cdiv(WALK_GROUPS_TARGET, ng),
                                                         hnm_cdiv(T, (int64_t)ng * 256)));
   while ((int64_t)pcs.size() > nwg * maxloc * 7 / 8) nwg *= 2;
+  // a walk of a few entries a group (a restricted plan's item shard: ~260 entries a group at
+  // d = 128 for 1/8 of the H&M items) is bound by the per-window latency, not by its gathers:
+  // one round of workgroups (one per CU) instead of a second partial round, when the slots hold
+  // every piece (placement only moves pieces between lanes; every result is unchanged)
+  const int64_t cus = std::max(1, pl->num_cus);
+  if (nwg > cus && (int64_t)pcs.size() <= cus * maxloc * 7 / 8 && T <= cus * ng * 1024) nwg = cus;
   std::vector<std::vector<int32_t>> wgp((size_t)nwg);
   {
     using E = std::pair<int64_t, int64_t>;

@@ -11,8 +11,11 @@ scoring methods run on the HIP library:
 Those fused kernels take the reference's default two-layer tower (mlp_dims of length 3 with
 h1 <= 128, h2 <= 32, mf <= 128).  Any other tower `_build_mlp` accepts (`:75-90`: one
 Linear -> ReLU per consecutive pair of mlp_dims, e.g. [64, 32] or [128, 64, 32, 16]) runs the
-exact fp32 deep-tower kernel (hnm_ncf_deep_scores_f32): pair scores for forward, dense rows
-for predict_all_items, and dense rows in user chunks + the row top-k kernel for recommend.
+exact fp32 deep-tower kernels: pair scores for forward and dense rows for predict_all_items
+(hnm_ncf_deep_scores_f32), and for recommend with k <= 64 the fused deep top-k
+(hnm_ncf_deep_topk_f32: f32-MFMA layer chains over item tiles with per-partition top-k lists for
+towers of widths <= 64, dense chunks + the row top-k inside the C entry for wider ones); k > 64
+takes dense rows + the row top-k kernel.
 """
 from __future__ import annotations
 
@@ -164,8 +167,20 @@ class NeuralCF(RecModule):
         (optimizer steps, load_state_dict) rebuild it, but writes through `.data` do not."""
         self._item_cache_on = bool(enabled)
         if not enabled:
-            self._item_proj = None
+            cached = getattr(self, "_wcache", None)
+            if cached is not None:
+                cached[1].item_proj = None      # the cached struct no longer points into it
+            self._release_item_proj()
         return self
+
+    def _release_item_proj(self):
+        """Drop the cached projection once no stream can still read it: kernels of other
+        threads' streams (or an open two-phase shard call) may hold its address, and the
+        caching allocator would hand the block out again on the allocating stream alone."""
+        old = getattr(self, "_item_proj", None)
+        self._item_proj = None
+        if old is not None:
+            torch.cuda.synchronize(old[1].device)
 
     def _attach_item_proj(self, w, keep):
         if not getattr(self, "_item_cache_on", False):
@@ -175,6 +190,8 @@ class NeuralCF(RecModule):
         key = (mi.data_ptr(), mi._version, w1.data_ptr(), w1._version, self.num_items)
         cached = getattr(self, "_item_proj", None)
         if cached is None or cached[0] != key:
+            if cached is not None:
+                self._release_item_proj()
             w.item_proj = None
             h1p = 128 if (w.h1 > 64 or w.mf > 64) else 64
             proj = torch.empty(self.num_items, h1p, dtype=torch.float32, device=keep[0].device)
