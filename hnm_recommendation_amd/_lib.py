@@ -106,6 +106,8 @@ _SIGS = {
     "hnm_ncf_deep_scores_f32": (_i32, [_p, C.POINTER(NcfDeepWeights), _p, _i64, _p, _p, _i64]),
     "hnm_ncf_deep_topk_f32": (_i32, [_p, C.POINTER(NcfDeepWeights), _p, _i64, _p, _p, C.c_int,
                                      _p, _p]),
+    "hnm_ncf_deep_prefilter_debug_f32": (_i32, [_p, C.POINTER(NcfDeepWeights), _p, _i64, _p,
+                                                _i64, _p]),
     "hnm_ncf_pair_scores_f32": (_i32, [_p, C.POINTER(NcfWeights), _p, _p, _i64, _p]),
     "hnm_ncf_prefilter_debug_f32": (_i32, [_p, C.POINTER(NcfWeights), _p, _i64, _p, _i64, _p]),
     "hnm_topk_merge_f32": (_i32, [_p, _p, _p, _i64, _i64, _i64, _i64, C.c_int, C.c_int, _p, _p]),

@@ -884,6 +884,69 @@ extern "C" hnm_status hnm_ncf_prefilter_debug_f32(hnm_ctx* ctx, const hnm_ncf_we
   return ncf_cert_debug(ctx, w, c.t, B, c.extra, approx, lda, bound);
 }
 
+// ------------------------------------------------------------------ deep towers, certified
+// A deep tower [2 h0, h1, h2, h3] seen as the two-layer tower's tables (layers 1 and 2) plus its
+// third layer (CertDeep): the certified f16 scan with the layer-3 epilogue and the exact deep
+// re-scoring (ncf_cert.hip).
+static void deep_view(const hnm_ncf_deep_weights* dw, const int64_t* ids, hnm_ncf_weights* w,
+                      CertDeep* dp) {
+  *w = hnm_ncf_weights{};
+  w->gmf_user = dw->gmf_user;
+  w->gmf_item = dw->gmf_item;
+  w->mlp_user = dw->mlp_user;
+  w->mlp_item = dw->mlp_item;
+  w->w1 = dw->w[0];
+  w->b1 = dw->b[0];
+  w->w2 = dw->w[1];
+  w->b2 = dw->b[1];
+  w->wp = dw->wp;  // [mf + h3]: only its GMF part is read through this view
+  w->bp = dw->bp;
+  w->num_users = dw->num_users;
+  w->num_items = dw->num_items;
+  w->mf = dw->mf;
+  w->h0 = dw->dims[0] / 2;
+  w->h1 = dw->dims[1];
+  w->h2 = dw->dims[2];
+  *dp = CertDeep{dw->w[2], dw->b[2], dw->wp + dw->mf, dw->dims[3], dw->gmf_user, dw->gmf_item,
+                 dw->wp, ids};
+}
+
+bool ncf_deep_cert_eligible(const hnm_ncf_deep_weights* dw, int K) {
+  if (dw->nl != 3 || dw->dims[1] > 64 || dw->dims[2] > 32 || dw->dims[3] > 16 || dw->mf > 64 ||
+      dw->mf % 4 != 0 || (uintptr_t)dw->gmf_item % 16 != 0)
+    return false;
+  hnm_ncf_weights w;
+  CertDeep dp;
+  deep_view(dw, nullptr, &w, &dp);
+  return ncf_cert_eligible(&w, K);
+}
+
+hnm_status ncf_deep_cert(hnm_ctx* ctx, const hnm_ncf_deep_weights* dw, const int64_t* ids,
+                         int64_t B, const int64_t* mptr, const int32_t* midx, int K, float* ov,
+                         int64_t* oi, int32_t** ovf_rows, int32_t** ovf_cnt, bool* pruned) {
+  hnm_ncf_weights w;
+  CertDeep dp;
+  deep_view(dw, ids, &w, &dp);
+  NcfCall c;
+  hnm_status st = ncf_tables(
+      ctx, &w, ids, B, ncf_cert_bytes(B, w.num_items, K, ctx->num_cus, ncf_cert_wg(ctx), false), &c);
+  if (st) return st;
+  return ncf_deep_cert_topk(ctx, &w, dp, c.t, B, mptr, midx, K, c.extra, ov, oi, ovf_rows, ovf_cnt,
+                            pruned);
+}
+
+hnm_status ncf_deep_cert_debug(hnm_ctx* ctx, const hnm_ncf_deep_weights* dw, const int64_t* ids,
+                               int64_t B, float* approx, int64_t lda, float* bound) {
+  hnm_ncf_weights w;
+  CertDeep dp;
+  deep_view(dw, ids, &w, &dp);
+  NcfCall c;
+  hnm_status st = ncf_tables(
+      ctx, &w, ids, B, ncf_cert_bytes(B, w.num_items, 1, ctx->num_cus, ncf_cert_wg(ctx), false), &c);
+  if (st) return st;
+  return ncf_cert_debug(ctx, &w, c.t, B, c.extra, approx, lda, bound, &dp);
+}
+
 extern "C" hnm_status hnm_ncf_pair_scores_f32(hnm_ctx* ctx, const hnm_ncf_weights* w,
                                               const int64_t* user_ids, const int64_t* item_ids,
                                               int64_t n, float* out) {

@@ -39,6 +39,7 @@
 #include "ncf_internal.h"
 
 typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+typedef _Float16 h4 __attribute__((ext_vector_type(4)));
 typedef _Float16 h2 __attribute__((ext_vector_type(2)));
 
 
@@ -46,6 +47,10 @@ namespace {
 
 constexpr int64_t CERT_MIN_ITEMS = 8192;  // below this the exact LIST kernel is cheaper
 constexpr float CERT_RHO = 0.0029296875f; // 6 u16 = 3 * 2^-10
+// Deep towers [2 h0, h1, h2, h3] (round 6): the same scan with a third layer; the bound keeps
+// its separable form with v = |wp3|^T |W3| |W2| and a factor 7.03 u < 8 u = 2^-8 (derivation at
+// cert_deep_scales below)
+constexpr float CERT_RHO_DEEP = 0.00390625f;
 constexpr int CERT_MAX_NP = 64;           // item partitions (candidate segments per row)
 constexpr int CERT_PROXY_USERS = 8;       // batch rows that pick the champion sample
 constexpr int64_t CERT_CHAMPIONS = 2048;  // champion sample size (item groups), at most
@@ -77,7 +82,9 @@ enum { CM_P, CM_Q, CM_WG, CM_G, CM_B, CM_D, CM_N };
 struct CertParams {
   unsigned mx[CM_N];  // float bits of non-negative maxima (reduced from per-block partials)
   float s1, sw, sm, sgu, sgi;
+  float s3;           // deep towers: the layer-3 weight scale (1 otherwise)
   float unit, cg;     // scaled score unit; GMF accumulator -> score unit
+  float rho;          // the bound's relative factor (CERT_RHO; deep towers CERT_RHO_DEEP)
   float c0, absb, Bmax, Dmax;
   int bad;            // bound not usable: every row takes the exact fallback
 };
@@ -218,7 +225,7 @@ __global__ __launch_bounds__(256) void cert_scales_kernel(const float* __restric
                                                           CertParams* prm,
                                                           const float* __restrict__ part,
                                                           int item_blocks, int user_blocks,
-                                                          int* __restrict__ ovf_cnt) {
+                                                          int* __restrict__ ovf_cnt, CertDeep dp) {
   __shared__ float red[7][4];
   __shared__ float pm[4][6];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -329,25 +336,65 @@ __global__ __launch_bounds__(256) void cert_scales_kernel(const float* __restric
   // below 1, so the [0, 1] clamp of the f32 -> f16 convert is an exact ReLU
   const float hmax = (s1 * mb2 + 0.51f * mrow) * 1.01f;
   const float sw = hmax > 0.f ? pow2_below_inv(hmax) : 1.f;
-  const float sm = mwm > 0.f ? pow2_below_inv(mwm) : 1.f;
+  float sm = mwm > 0.f ? pow2_below_inv(mwm) : 1.f;
   const float sgu = mWG > 0.f ? pow2_below_inv(mWG) : 1.f;
   const float sgi = mG > 0.f ? pow2_below_inv(mG) : 1.f;
-  const float unit = s1 * sw * sm;
-  const float cg = unit / (sgu * sgi);
-  bad |= !(unit >= 1e-30f && unit <= 1e30f && cg >= 1e-30f && cg <= 1e30f);
   const float phi = 2.98023224e-08f;  // 2^-25: half the f16 subnormal spacing
   const float rmax = mb2 + 64.f * mW * zmax;
-  const float absb = 16.f * phi *
-                         (3.f * vsum / s1 + 64.f * swm * zmax / sw + swm / (s1 * sw) +
-                          32.f * rmax / sm + 64.f * mG / sgu + 64.f * mWG / sgi) +
-                     2.4e-7f * fabsf(bp[0]);
+  float s3 = 1.f, rho = CERT_RHO;
+  // the per-rounding absolute slack terms (real units, x 16 phi below): layer-1 operands and
+  // sum, W2 rounding, relu(H) rounding, GMF operands -- and the last weights' rounding
+  float abst = 3.f * vsum / s1 + 64.f * swm * zmax / sw + swm / (s1 * sw) + 64.f * mG / sgu +
+               64.f * mWG / sgi;
+  if (dp.W3) {
+    // Deep tower (round 6).  `wm` is u = |wp3|^T |W3| here, so vsum = sum_k v_k, swm = sum_l u_l
+    // and c0 = u . |b2| with v = |wp3|^T |W3| |W2| (the stats kernel's A_u / B_i).  Error of the
+    // scan against the exact chain, u = 2^-11: layer-2 output dH_l <= 3.02u sum_k |W2_lk| z_k as
+    // before; y~ = f16(relu(H~)) adds u R_l (R_l = |b2_l| + sum_k |W2_lk| z_k >= |H_l|); the f16
+    // W3 and layer-3 accumulation give dH3_m <= sum_l |W3_ml| ((1 + u) dH_l + 2u R_l); z~ =
+    // f16(relu(H3~)) adds u R3_m (R3_m = |b3_m| + sum_l |W3_ml| R_l) and the f16 wp3 another u
+    // R3_m: |err| <= u (7.03 (A_u + B_i) + 4 c0 + 2 cb3) + 2.01u C_u D_i + O(u^2) <= 8u (c0 + cb3
+    // + A_u + B_i + C_u D_i) (fp32 accumulation ~2^-22 relative, inside the margin); absolute
+    // slack for f16 subnormals per rounding site, each through the weights after it.
+    float mW3 = 0.f, mrow3 = 0.f, mb3 = 0.f, mwp = 0.f, swp = 0.f, cb3 = 0.f;
+    for (int m = 0; m < dp.h3; ++m) {
+      float rs = 0.f;
+      for (int l = 0; l < h2; ++l) {
+        const float a = fabsf(dp.W3[m * h2 + l]);
+        mW3 = nmax(mW3, a);
+        rs += a;
+      }
+      mrow3 = nmax(mrow3, rs);
+      mb3 = nmax(mb3, fabsf(dp.b3[m]));
+      mwp = nmax(mwp, fabsf(dp.wp3[m]));
+      swp += fabsf(dp.wp3[m]);
+      cb3 += fabsf(dp.wp3[m]) * fabsf(dp.b3[m]);
+    }
+    for (float m : {mW3, mrow3, mb3, mwp, swp, cb3}) bad |= !(m <= lim);
+    // relu(H~) <= 1 after the clamp, so |H3~| <= s3 (s1 sw |b3| + sum_l |W3_ml|) <= 1
+    const float hmax3 = (s1 * sw * mb3 + mrow3) * 1.01f;
+    s3 = hmax3 > 0.f ? pow2_below_inv(hmax3) : 1.f;
+    sm = mwp > 0.f ? pow2_below_inv(mwp) : 1.f;
+    const float r3max = mb3 + (float)h2 * mW3 * rmax;
+    c0 += cb3;
+    abst += 32.f * swp * rmax / s3 + swp / (s1 * sw * s3) + 16.f * r3max / sm;
+    rho = CERT_RHO_DEEP;
+  } else {
+    abst += 32.f * rmax / sm;  // wm rounding
+  }
+  const float unit = s1 * sw * s3 * sm;
+  const float cg = unit / (sgu * sgi);
+  bad |= !(unit >= 1e-30f && unit <= 1e30f && cg >= 1e-30f && cg <= 1e30f);
+  const float absb = 16.f * phi * abst + 2.4e-7f * fabsf(bp[0]);
   prm->s1 = s1;
   prm->sw = sw;
   prm->sm = sm;
+  prm->s3 = s3;
   prm->sgu = sgu;
   prm->sgi = sgi;
   prm->unit = unit;
   prm->cg = cg;
+  prm->rho = rho;
   prm->c0 = c0;
   prm->absb = absb;
   prm->Bmax = Bmax;
@@ -363,14 +410,15 @@ __global__ __launch_bounds__(256) void cert_convert_kernel(
     _Float16* __restrict__ G16, const float* __restrict__ W2, int h1, int h2,
     const float* __restrict__ b2, const float* __restrict__ wm, _Float16* __restrict__ W2h,
     _Float16* __restrict__ wmh, float* __restrict__ b2s, const float* __restrict__ Bi,
-    const float* __restrict__ Cu, float* __restrict__ Bs, float* __restrict__ Cs) {
+    const float* __restrict__ Cu, float* __restrict__ Bs, float* __restrict__ Cs, CertDeep dp,
+    _Float16* __restrict__ W3h, _Float16* __restrict__ wph, float* __restrict__ b3s) {
   const float s1 = prm->s1, sgu = prm->sgu, sgi = prm->sgi;
-  // the scan's bound terms in test units (CERT_RHO * unit * B_i, ... * C_u): the same fp32
+  // the scan's bound terms in test units (rho * unit * B_i, ... * C_u): the same fp32
   // products the scan formed itself before, computed once here so the scan keeps no scale
   // factor live across its tile loop
   const int64_t nthreads = (int64_t)gridDim.x * 256;
   const int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  const float ru = CERT_RHO * prm->unit;
+  const float ru = prm->rho * prm->unit;
   for (int64_t e = g; e < I; e += nthreads) Bs[e] = ru * Bi[e];
   for (int64_t e = g; e < B; e += nthreads) Cs[e] = ru * Cu[e];
   // items: 16 chunks of 4 per row
@@ -405,10 +453,33 @@ __global__ __launch_bounds__(256) void cert_convert_kernel(
     }
     if (threadIdx.x < 32) {
       const int j = threadIdx.x;
-      wmh[j] = (_Float16)(j < h2 ? wm[j] * sm : 0.f);
+      wmh[j] = (_Float16)(j < h2 && !dp.W3 ? wm[j] * sm : 0.f);
       b2s[j] = j < h2 ? b2[j] * s1 * sw : 0.f;
     }
+    if (dp.W3) {  // layer 3 (unit m, hidden l) x s3, its bias x s1 sw s3, wp3 x sm
+      const float s3 = prm->s3;
+      for (int e = threadIdx.x; e < 16 * 32; e += 256) {
+        const int m = e >> 5, l = e & 31;
+        W3h[e] = (_Float16)((m < dp.h3 && l < h2) ? dp.W3[m * h2 + l] * s3 : 0.f);
+      }
+      if (threadIdx.x < 16) {
+        const int m = threadIdx.x;
+        wph[m] = (_Float16)(m < dp.h3 ? dp.wp3[m] * sm : 0.f);
+        b3s[m] = m < dp.h3 ? dp.b3[m] * s1 * sw * s3 : 0.f;
+      }
+    }
   }
+}
+
+// Deep towers: u_l = sum_m |wp3_m| |W3_ml| (l < h2), the weights the bound statistics take in
+// place of the two-layer tower's |wm| (v = |wp3|^T |W3| |W2|)
+__global__ __launch_bounds__(64) void cert_deep_u_kernel(CertDeep dp, int h2, float* __restrict__ u) {
+  const int l = threadIdx.x;
+  if (l >= 32) return;
+  float v = 0.f;
+  if (l < h2)
+    for (int m = 0; m < dp.h3; ++m) v += fabsf(dp.wp3[m]) * fabsf(dp.W3[m * h2 + l]);
+  u[l] = v;
 }
 
 // ------------------------------------------------------------------ f16 scan kernel
@@ -426,9 +497,12 @@ struct ScanArgs {
   const _Float16* W2h;   // [32, 64]
   const _Float16* wmh;   // [32]
   const float* b2s;      // [32]
-  const float* Bi;       // [Itot] per-item bound terms (x CERT_RHO * unit: test units)
+  const _Float16* W3h;   // DEEP: [16, 32] layer-3 weights x s3 (unit, hidden)
+  const _Float16* wph;   // DEEP: [16] prediction weights of the layer-3 units x sm
+  const float* b3s;      // DEEP: [16] layer-3 bias x s1 sw s3
+  const float* Bi;       // [Itot] per-item bound terms (x rho * unit: test units)
   const float* Di;
-  const float* Cu;       // [B] per-user bound terms (x CERT_RHO * unit)
+  const float* Cu;       // [B] per-user bound terms (x rho * unit)
   const float* Eu;       // [B] user-constant part of the bound, scaled (DEBUG)
   const CertParams* prm;
   int64_t B;
@@ -472,11 +546,22 @@ __device__ __forceinline__ f32x16 mfma16(h8 a, h8 b, f32x16 c) {
 // profiles/r2_ncf_scan_variants.txt); splitting it (user a on the matrix pipe, user b by packed
 // dots) measured 2.03 vs 1.88 ms (round 3, profiles/r3c_ncf_epilogue_ab.txt): the VALU side is
 // the binding one.  DEBUG keeps a VALU epilogue (packed dots + swap).
-template <int MODE>
-__global__ __launch_bounds__(256, HNM_SCAN_OCC) void ncf16_scan_kernel(ScanArgs A) {
+// DEEP (round 6, towers [2 h0, h1 <= 64, h2 <= 32, h3 <= 16]): layer 2 as above, then layer 3 on
+// the matrix pipe in place of the wm epilogue -- per user and item half g (items c / c + 16) two
+// v_mfma_f32_16x16x32_f16 whose A rows are W3's 16 units with the k-groups of the other item half
+// zeroed (the 16x16x32 B operand mixes items c and c + 16 across k-groups), accumulator seeded
+// with b3 -- relu by the clamp of the f32 -> f16 converts, and the prediction wp3 . relu(h3) as a
+// v_mfma_f32_16x16x16_f16 whose B operand is that accumulator as it lies (rows 4 (lane >> 4) + r =
+// units, columns = items) and whose A row idx = 2 user + g holds wp3: four of them chained on the
+// folded seeds leave the test values where the two-layer epilogue leaves them.  DEBUG uses the
+// same matrix epilogue (seeds = GMF only).  Two waves per SIMD (28 more live registers).
+template <int MODE, bool DEEP = false>
+__global__ __launch_bounds__(256, DEEP ? 2 : HNM_SCAN_OCC) void ncf16_scan_kernel(ScanArgs A) {
   constexpr int RS = 72;   // LDS row stride in halfs (144 B): conflict-free b128 reads
   constexpr int NU = 128;  // users per workgroup
-  constexpr bool FOLD = MODE == SCAN_THRESH || MODE == SCAN_SAMPLE;
+  // the matrix-pipe epilogue and its folded seed table (FOLD: GMF + bound - threshold; the deep
+  // DEBUG pass: GMF alone)
+  constexpr bool FOLD = MODE == SCAN_THRESH || MODE == SCAN_SAMPLE || (DEEP && MODE == SCAN_DEBUG);
   if (MODE == SCAN_SAMPLE && A.gate && *A.gate == 0) return;  // whole grid: gated off
   __shared__ __attribute__((aligned(16))) _Float16 qs[2][TILE * RS];  // double-buffered tiles
   __shared__ __attribute__((aligned(16))) _Float16 gs[2][TILE * RS];
@@ -519,7 +604,25 @@ __global__ __launch_bounds__(256, HNM_SCAN_OCC) void ncf16_scan_kernel(ScanArgs 
   // epilogue A operands (16x16x32: lane holds A[row lane & 15][k = 8 (lane >> 4) + e])
   h8 ewa[2], ewb[2];
   h2 wm2[8];  // DEBUG: wm of this lane's accumulator rows, in pairs
-  {
+  h8 e3[2][2];  // DEEP: layer-3 A operands [item half g][accumulator half f]
+  h4 ep[4];     // DEEP: prediction A operands, wp3 in row idx = 2 user + g
+  f32x4 b3c;    // DEEP: layer-3 accumulator seeds (rows 4 (lane >> 4) + r)
+  if constexpr (DEEP) {
+    const int m = lane & 15, kg = lane >> 4;
+#pragma unroll
+    for (int g = 0; g < 2; ++g)
+#pragma unroll
+      for (int f = 0; f < 2; ++f)
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          e3[g][f][e] = (kg & 1) == g ? A.W3h[m * 32 + mfma32_row(8 * f + e, kg >> 1)] : (_Float16)0.f;
+#pragma unroll
+    for (int idx = 0; idx < 4; ++idx)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) ep[idx][e] = m == idx ? A.wph[4 * kg + e] : (_Float16)0.f;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) b3c[r] = A.b3s[4 * kg + r];
+  } else {
     const int erow = lane & 15, eg = lane >> 4;
 #pragma unroll
     for (int f = 0; f < 2; ++f)
@@ -636,7 +739,7 @@ __global__ __launch_bounds__(256, HNM_SCAN_OCC) void ncf16_scan_kernel(ScanArgs 
         gacc = mfma16(ag[s], *reinterpret_cast<const h8*>(&gs[cur][lrow + 16 * s]), gacc);
       if constexpr (FOLD) {
         // folded test term gmf + sgn * e_i - tau (sgn = +1 for the threshold test, -1 for the
-        // sample's lower bound)
+        // sample's lower bound; the deep DEBUG pass: gmf alone)
         constexpr float sgn = MODE == SCAN_THRESH ? 1.f : -1.f;
         // (measured, round 5: the same stores from one lane base + immediate offsets -- 6 fewer
         // VGPRs -- scheduled the pair loop's LDS reads differently, +1-2 % scan time)
@@ -645,7 +748,7 @@ __global__ __launch_bounds__(256, HNM_SCAN_OCC) void ncf16_scan_kernel(ScanArgs 
           const int row = mfma32_row(r, h);
           const float2 tc = ut[wave][row];
           g7[(((row >> 1) * 16 + (j & 15)) << 2) + ((row & 1) << 1) + (j >> 4)] =
-              (gacc[r] * cg + sgn * fmaf(tc.y, dj, bj)) - tc.x;
+              MODE == SCAN_DEBUG ? gacc[r] * cg : (gacc[r] * cg + sgn * fmaf(tc.y, dj, bj)) - tc.x;
         }
       } else {
 #pragma unroll
@@ -712,12 +815,46 @@ __global__ __launch_bounds__(256, HNM_SCAN_OCC) void ncf16_scan_kernel(ScanArgs 
         }
         // lanes 0-15: (a, c), (a, c + 16), (b, c), (b, c + 16); other lanes' rows are unused
         f32x4 d = *reinterpret_cast<const f32x4*>(&g7[((u >> 1) * 16 + (lane & 15)) << 2]);
-        d = __builtin_amdgcn_mfma_f32_16x16x32_f16(ewa[0], ya[0], d, 0, 0, 0);
-        d = __builtin_amdgcn_mfma_f32_16x16x32_f16(ewa[1], ya[1], d, 0, 0, 0);
-        d = __builtin_amdgcn_mfma_f32_16x16x32_f16(ewb[0], yb[0], d, 0, 0, 0);
-        d = __builtin_amdgcn_mfma_f32_16x16x32_f16(ewb[1], yb[1], d, 0, 0, 0);
+        if constexpr (DEEP) {
+#pragma unroll
+          for (int uu = 0; uu < 2; ++uu)
+#pragma unroll
+            for (int g = 0; g < 2; ++g) {
+              f32x4 t3 = b3c;
+              t3 = __builtin_amdgcn_mfma_f32_16x16x32_f16(e3[g][0], uu ? yb[0] : ya[0], t3, 0, 0, 0);
+              t3 = __builtin_amdgcn_mfma_f32_16x16x32_f16(e3[g][1], uu ? yb[1] : ya[1], t3, 0, 0, 0);
+              h4 z = {(_Float16)t3[0], (_Float16)t3[1], (_Float16)t3[2], (_Float16)t3[3]};
+              z = __builtin_elementwise_min(__builtin_elementwise_max(z, (h4){}), (h4)(_Float16)1.f);
+              d = __builtin_amdgcn_mfma_f32_16x16x16f16(ep[2 * uu + g], z, d, 0, 0, 0);
+            }
+        } else {
+          d = __builtin_amdgcn_mfma_f32_16x16x32_f16(ewa[0], ya[0], d, 0, 0, 0);
+          d = __builtin_amdgcn_mfma_f32_16x16x32_f16(ewa[1], ya[1], d, 0, 0, 0);
+          d = __builtin_amdgcn_mfma_f32_16x16x32_f16(ewb[0], yb[0], d, 0, 0, 0);
+          d = __builtin_amdgcn_mfma_f32_16x16x32_f16(ewb[1], yb[1], d, 0, 0, 0);
+        }
         const uint64_t vmask = vm32 | (hasb ? vm32 << 32 : 0ull);
-        if (MODE == SCAN_SAMPLE) {
+        if (MODE == SCAN_DEBUG) {  // DEEP: approx and the whole bound, per pair, scaled units
+          float bjr[2], djr[2];  // the bound terms of items c and c + 16 (lanes c, c + 16)
+#pragma unroll
+          for (int q2 = 0; q2 < 2; ++q2) {
+            bjr[q2] = __shfl(bj, (lane & 15) + 16 * q2);
+            djr[q2] = __shfl(dj, (lane & 15) + 16 * q2);
+          }
+          const float cua = hnm_readlane_f(cu, ua), cub = hnm_readlane_f(cu, ub);
+          const float eua = hnm_readlane_f(eu, ua), eub = hnm_readlane_f(eu, ub);
+          if (lane < 16) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int it = lane + 16 * (r & 1);
+              if ((vmask >> (32 * (r >> 1) + it)) & 1) {
+                const int64_t o = (u0 + ua + (r >> 1)) * A.ldo + base + it;
+                A.dense[o] = d[r];
+                A.dense2[o] = (r >> 1 ? eub : eua) + fmaf(r >> 1 ? cub : cua, djr[r & 1], bjr[r & 1]);
+              }
+            }
+          }
+        } else if (MODE == SCAN_SAMPLE) {
           if (lane < 16) {
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
@@ -823,7 +960,7 @@ __global__ __launch_bounds__(256) void cert_bound_kernel(const float* __restrict
   const int64_t b = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (b >= B) return;
   const float unit = prm->unit;
-  const float e = unit * (CERT_RHO * (prm->c0 + Au[b]) + prm->absb);
+  const float e = unit * (prm->rho * (prm->c0 + Au[b]) + prm->absb);
   if (Eu) Eu[b] = e;
   if (!kth) return;
   float l = (kth_pick(kth, kth2, gate, b * K + (K - 1)) - e) / unit + bp[0];
@@ -1067,7 +1204,7 @@ __global__ __launch_bounds__(1024) void cert_gate_kernel(
     if (lane == 0) kvs[w] = kv;
   }
   __syncthreads();
-  const float eu2 = 2.f * prm->unit * (CERT_RHO * (prm->c0 + Au[r]) + prm->absb);
+  const float eu2 = 2.f * prm->unit * (prm->rho * (prm->c0 + Au[r]) + prm->absb);
   const float tc = kvs[0] - eu2, ts = fmaxf(kvs[0], kvs[1]) - eu2, cr = Cs[r];
   int nc = 0, nsv = 0;
 #pragma unroll
@@ -1128,9 +1265,16 @@ __global__ __launch_bounds__(1024) void cert_gate_kernel(
 // -> 2.147 ms, W = 8 (32,768 rows of ~1/8 the candidates) 2.381 -> 2.284 ms at 3 per CU, 6 per
 // CU 2.151 / 2.315, against one workgroup per 4 rows): the W2 fragments are staged into LDS once
 // per workgroup instead of once per 4 rows.
+// DEEP (round 6): the candidates' exact scores by the deep tower's chain in ncf_deep_kernel's
+// order (bitwise the exact deep kernels): layer 2 as an f32-MFMA chain FROM ZERO over k = 0..63
+// (the staged A rows permuted so that accumulator register r of lane half h holds unit 2r + h),
+// relu(acc + b2); layer 3 the same way over l = 2s + h with W3 row m on A row mfma32_row(m, 0)
+// (so lane half 0 holds every unit of a candidate), relu(acc + b3); then in lane half 0 ONE fmaf
+// chain over the GMF terms wp_j (g_u,j g_i,j) and the units' wp3_m z_m, + bp.
 #define RESCORE_PERSIST 3
 constexpr int RESCORE_BEST_FIRST = 96;  // rows with more candidates score the best 64 first
-__global__ __launch_bounds__(256, 3) void ncf_rescore_kernel(
+template <bool DEEP>
+__global__ __launch_bounds__(256, DEEP ? 2 : 3) void ncf_rescore_kernel(
     NcfTabs t, int mf, const float* __restrict__ W2, int h1, int h2, const float* __restrict__ b2,
     const float* __restrict__ wm, const float* __restrict__ bp, int64_t B,
     const int* __restrict__ flag, const int* __restrict__ cnt, const int32_t* __restrict__ buf,
@@ -1138,9 +1282,13 @@ __global__ __launch_bounds__(256, 3) void ncf_rescore_kernel(
     const float* __restrict__ Au, const float* __restrict__ Cu, const CertParams* __restrict__ prm,
     int NP, int capp, int K, int short_ok, float* __restrict__ ov, int64_t* __restrict__ oi,
     int32_t* __restrict__ ovf_rows, int32_t* __restrict__ ovf_cnt,
-    unsigned long long* __restrict__ stats) {
+    unsigned long long* __restrict__ stats, CertDeep dp, int64_t num_users) {
   constexpr int KS = 32;
   __shared__ int stg[4][96];  // best-first: staged candidate ordinals
+  // DEEP: layer-3 A fragments (16 k steps), b3, the prediction weights, each wave's user GMF row
+  __shared__ float w3l[DEEP ? 16 * 64 : 1];
+  __shared__ float b3l[16], wpl[DEEP ? 128 + 16 : 1];
+  __shared__ float g0l[DEEP ? 4 : 1][64];
   __shared__ __attribute__((aligned(16))) float wgs[4][64];
   __shared__ __attribute__((aligned(16))) float b2l[32], wml[32];  // 0 beyond h2
   __shared__ int pref[4][CERT_MAX_NP + 1];
@@ -1152,11 +1300,22 @@ __global__ __launch_bounds__(256, 3) void ncf_rescore_kernel(
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5, j = lane & 31;
   if (tid < 32) {
     b2l[tid] = tid < h2 ? b2[tid] : 0.f;
-    wml[tid] = tid < h2 ? wm[tid] : 0.f;
+    wml[tid] = !DEEP && tid < h2 ? wm[tid] : 0.f;  // (deep towers: wp holds mf + h3 only)
   }
   for (int e = tid; e < KS * 64; e += 256) {
     const int s = e >> 6, jj = e & 31, k = 2 * s + ((e >> 5) & 1);
-    w2l[e] = (jj < h2 && k < h1) ? W2[jj * h1 + k] : 0.f;
+    // DEEP: A row jj = mfma32_row(r, h) carries unit 2r + h
+    const int row = DEEP ? 2 * ((jj & 3) + 4 * (jj >> 3)) + ((jj >> 2) & 1) : jj;
+    w2l[e] = (row < h2 && k < h1) ? W2[row * h1 + k] : 0.f;
+  }
+  if constexpr (DEEP) {
+    for (int e = tid; e < 16 * 64; e += 256) {
+      const int s = e >> 6, jj = e & 31, k = 2 * s + ((e >> 5) & 1);
+      const int m = (jj & 3) + 4 * (jj >> 3);  // rows mfma32_row(m, 0): lane half 0
+      w3l[e] = (((jj >> 2) & 1) == 0 && m < dp.h3 && k < h2) ? dp.W3[m * h2 + k] : 0.f;
+    }
+    if (tid < 16) b3l[tid] = tid < dp.h3 ? dp.b3[tid] : 0.f;
+    for (int e = tid; e < mf + dp.h3; e += 256) wpl[e] = dp.wp[e];
   }
   // persistent: the workgroup's shared operands loaded once, then each wave takes rows
   // b, b + 4 * gridDim.x, ... (its per-row LDS arrays are its own: no workgroup barrier inside)
@@ -1168,6 +1327,10 @@ __global__ __launch_bounds__(256, 3) void ncf_rescore_kernel(
     wgs[wave][lane] = t.WGu[b * 64 + lane];  // pair-permuted wp*g_u
     pl[wave][lane] = t.Pu[b * 64 + lane];
     c = lane < NP ? cnt[b * NP + lane] : 0;
+    if constexpr (DEEP) {
+      const int64_t uid = dp.ids[b];  // out of range: flagged by the tables' gather
+      g0l[wave][lane] = (lane < mf && uid >= 0 && uid < num_users) ? dp.gmf_user[uid * mf + lane] : 0.f;
+    }
   }
   // inclusive scan of the segment counts over the lanes
   int incl = c;
@@ -1214,7 +1377,61 @@ __global__ __launch_bounds__(256, 3) void ncf_rescore_kernel(
   };
   auto cand = [&](int g) { return g < n ? rowbuf[slot(g)] : 0; };
   // exact fp32 score of lane j's candidate (both halves of the wave), offered to the top-K
+  auto score_deep = [&](int item, bool ok) {
+    float q[KS];
+    const float* qrow = t.Qi + (int64_t)item * 64 + h * KS;
+#pragma unroll
+    for (int s4 = 0; s4 < KS / 4; ++s4) {
+      const float4 v = *reinterpret_cast<const float4*>(qrow + 4 * s4);
+      q[4 * s4] = v.x; q[4 * s4 + 1] = v.y; q[4 * s4 + 2] = v.z; q[4 * s4 + 3] = v.w;
+    }
+    f32x16 acc = {};
+    typedef __attribute__((address_space(3))) const float* lds_ptr;
+#pragma unroll
+    for (int s = 0; s < KS; s += 4) {
+      float w[4], pv[4];
+      asm volatile("ds_read_b32 %0, %8\n\tds_read_b32 %1, %9\n\tds_read_b32 %2, %10\n\t"
+                   "ds_read_b32 %3, %11\n\tds_read_b32 %4, %12\n\tds_read_b32 %5, %13\n\t"
+                   "ds_read_b32 %6, %14\n\tds_read_b32 %7, %15\n\ts_waitcnt lgkmcnt(0)"
+                   : "=&v"(w[0]), "=&v"(w[1]), "=&v"(w[2]), "=&v"(w[3]),
+                     "=&v"(pv[0]), "=&v"(pv[1]), "=&v"(pv[2]), "=&v"(pv[3])
+                   : "v"((unsigned)(uintptr_t)(lds_ptr)&w2l[s * 64 + lane]),
+                     "v"((unsigned)(uintptr_t)(lds_ptr)&w2l[(s + 1) * 64 + lane]),
+                     "v"((unsigned)(uintptr_t)(lds_ptr)&w2l[(s + 2) * 64 + lane]),
+                     "v"((unsigned)(uintptr_t)(lds_ptr)&w2l[(s + 3) * 64 + lane]),
+                     "v"((unsigned)(uintptr_t)(lds_ptr)&pl[wave][h * KS + s]),
+                     "v"((unsigned)(uintptr_t)(lds_ptr)&pl[wave][h * KS + s + 1]),
+                     "v"((unsigned)(uintptr_t)(lds_ptr)&pl[wave][h * KS + s + 2]),
+                     "v"((unsigned)(uintptr_t)(lds_ptr)&pl[wave][h * KS + s + 3]));
+#pragma unroll
+      for (int e = 0; e < 4; ++e) acc = mfma32x32x2(w[e], fmaxf(pv[e] + q[s + e], 0.f), acc);
+    }
+    // layer 3: register s of half h is unit 2s + h, its relu(acc + b2) the k = 2s + h operand
+    f32x16 a3 = {};
+#pragma unroll
+    for (int s = 0; s < 16; ++s)
+      a3 = mfma32x32x2(w3l[s * 64 + lane], fmaxf(acc[s] + b2l[2 * s + h], 0.f), a3);
+    float sc = 0.f;
+    if (h == 0 && ok) {
+      const float* grow = dp.gmf_item + (int64_t)item * mf;
+      for (int j4 = 0; j4 < mf; j4 += 4) {
+        const float4 gv = *reinterpret_cast<const float4*>(grow + j4);
+        sc = fmaf(wpl[j4], g0l[wave][j4] * gv.x, sc);
+        sc = fmaf(wpl[j4 + 1], g0l[wave][j4 + 1] * gv.y, sc);
+        sc = fmaf(wpl[j4 + 2], g0l[wave][j4 + 2] * gv.z, sc);
+        sc = fmaf(wpl[j4 + 3], g0l[wave][j4 + 3] * gv.w, sc);
+      }
+#pragma unroll
+      for (int m = 0; m < 16; ++m)
+        if (m < dp.h3) sc = fmaf(wpl[mf + m], fmaxf(a3[m] + b3l[m], 0.f), sc);
+    }
+    L.offer(sc + bp[0], item, ok && h == 0, K);
+  };
   auto score_item = [&](int item, bool ok) {
+    if constexpr (DEEP) {
+      score_deep(item, ok);
+      return;
+    }
     // GMF: fma chain in the f32 MFMA's order (k = 2s, then 2s + 1) over all 64 k (zero
     // beyond mf, as the fp32 kernel's padded operands); loads in two batches of 8 float4
     // issued together (a runtime-bounded loop would wait on each load)
@@ -1367,6 +1584,30 @@ __global__ __launch_bounds__(256, 3) void ncf_rescore_kernel(
   }
 }
 
+// Deep towers: the candidates the main scan would append for the proxy rows (whose every item the
+// proxy pass scored: pd = approx - e_i), approx + e_i >= tau with tau ~ kv - 2 Eu (cert_tau_kernel)
+// -- where the worst-case bound through two absolute-value layers is wider than the rows' score
+// spread (init-like weights) the certified scan cannot prune and the call takes the exact kernels
+// instead.  An unusable bound counts every item.
+__global__ __launch_bounds__(256) void cert_predict_kernel(const float* __restrict__ pd, int64_t I,
+                                                           int K, const float* __restrict__ kthv,
+                                                           const float* __restrict__ Eu,
+                                                           const float* __restrict__ Bs,
+                                                           const float* __restrict__ Cs,
+                                                           const float* __restrict__ Di,
+                                                           const CertParams* __restrict__ prm,
+                                                           unsigned long long* __restrict__ cnt) {
+  const int r = blockIdx.y;
+  const float thr = kthv[(int64_t)r * K + K - 1] - 2.f * Eu[r], cs = Cs[r];
+  const bool bad = prm->bad || !__builtin_isfinite(thr);
+  unsigned n = 0;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < I; i += (int64_t)gridDim.x * 256)
+    n += bad || !(pd[(int64_t)r * I + i] + 2.f * fmaf(cs, Di[i], Bs[i]) < thr);
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) n += __shfl_xor(n, o);
+  if ((threadIdx.x & 63) == 0 && n) atomicAdd(cnt, (unsigned long long)n);
+}
+
 // scaled -> real units, for the diagnostics entry point
 __global__ void cert_unscale_kernel(float* __restrict__ a, float* __restrict__ e, int64_t lda,
                                     int64_t B, int64_t I, const CertParams* __restrict__ prm) {
@@ -1393,6 +1634,8 @@ struct CertWs {
   int32_t *buf, *ovf_cnt, *ovf_rows;
   float* bufd;  // the appended candidates' test values
   _Float16 *P16, *WG16, *Q16, *G16, *W2h, *wmh;
+  _Float16 *W3h, *wph;  // deep towers: layer 3 and the prediction weights (f16, scaled)
+  float *b3s, *u;       // deep towers: layer-3 bias (scaled); |wp3|^T |W3| (bound statistics)
   float* cv;
   int32_t* ci;
 };
@@ -1482,6 +1725,10 @@ size_t cert_carve(char* base, int64_t B, int64_t I, int K, int num_cus, int wg, 
   x.G16 = (_Float16*)take((size_t)I * 64 * 2);
   x.W2h = (_Float16*)take(32 * 64 * 2);
   x.wmh = (_Float16*)take(32 * 2);
+  x.W3h = (_Float16*)take(16 * 32 * 2);
+  x.wph = (_Float16*)take(16 * 2);
+  x.b3s = (float*)take(16 * 4);
+  x.u = (float*)take(32 * 4);
   const size_t lb = ncf_list_bytes(B, I, K, num_cus);
   x.cv = (float*)take(lb);
   x.ci = (int32_t*)take(lb);
@@ -1490,32 +1737,45 @@ size_t cert_carve(char* base, int64_t B, int64_t I, int K, int num_cus, int wg, 
 }
 
 hnm_status cert_prepare(hnm_ctx* ctx, const hnm_ncf_weights* w, const NcfTabs& t, int64_t B,
-                        const CertWs& x) {
+                        const CertWs& x, const CertDeep* dp) {
   const int64_t I = w->num_items;
   const int ib = (int)std::min<int64_t>(1024, hnm_cdiv(I, 4));
   const int ub = (int)std::min<int64_t>(256, hnm_cdiv(B, 4));
+  // the weights behind layer 2's outputs: wm (two-layer tower) or u = |wp3|^T |W3| (deep)
+  const float* wm = w->wp + w->mf;
+  const CertDeep dv = dp ? *dp : CertDeep{};
+  if (dp) {
+    hipLaunchKernelGGL(cert_deep_u_kernel, dim3(1), dim3(64), 0, ctx->stream, dv, w->h2, x.u);
+    HNM_LAUNCH_CHECK();
+    wm = x.u;
+  }
   hipLaunchKernelGGL(cert_stats_kernel, dim3(ib + ub), dim3(256), 0, ctx->stream, t, B, I, w->mf,
-                     w->w2, w->h1, w->h2, w->wp + w->mf, x.prm, x.Au, x.Cu, x.Bi, x.Di, x.part,
-                     ib, ub);
+                     w->w2, w->h1, w->h2, wm, x.prm, x.Au, x.Cu, x.Bi, x.Di, x.part, ib, ub);
   HNM_LAUNCH_CHECK();
   hipLaunchKernelGGL(cert_scales_kernel, dim3(1), dim3(256), 0, ctx->stream, w->w2, w->h1, w->h2,
-                     w->b2, w->wp + w->mf, w->bp, x.prm, x.part, ib, ub, x.ovf_cnt);
+                     w->b2, wm, w->bp, x.prm, x.part, ib, ub, x.ovf_cnt, dv);
   HNM_LAUNCH_CHECK();
   const int cb = (int)std::min<int64_t>(2048, std::max<int64_t>(1, hnm_cdiv(I * 16, 256)));
   hipLaunchKernelGGL(cert_convert_kernel, dim3(cb), dim3(256), 0, ctx->stream, t, B, I, w->mf,
-                     x.prm, x.P16, x.WG16, x.Q16, x.G16, w->w2, w->h1, w->h2, w->b2,
-                     w->wp + w->mf, x.W2h, x.wmh, x.b2s, x.Bi, x.Cu, x.Bs, x.Cs);
+                     x.prm, x.P16, x.WG16, x.Q16, x.G16, w->w2, w->h1, w->h2, w->b2, wm, x.W2h,
+                     x.wmh, x.b2s, x.Bi, x.Cu, x.Bs, x.Cs, dv, x.W3h, x.wph, x.b3s);
   HNM_LAUNCH_CHECK();
   return HNM_OK;
 }
 
 template <int MODE>
 void launch_scan(hnm_ctx* ctx, dim3 grid, const ScanArgs& a) {
-  hipLaunchKernelGGL((ncf16_scan_kernel<MODE>), grid, dim3(256), 0, ctx->stream, a);
+  if (a.W3h)
+    hipLaunchKernelGGL((ncf16_scan_kernel<MODE, true>), grid, dim3(256), 0, ctx->stream, a);
+  else
+    hipLaunchKernelGGL((ncf16_scan_kernel<MODE, false>), grid, dim3(256), 0, ctx->stream, a);
 }
 
-ScanArgs scan_args(const CertWs& x, int64_t B) {
+ScanArgs scan_args(const CertWs& x, int64_t B, bool deep) {
   ScanArgs a{};
+  a.W3h = deep ? x.W3h : nullptr;  // selects the deep scan (launch_scan)
+  a.wph = x.wph;
+  a.b3s = x.b3s;
   a.P16 = x.P16;
   a.WG16 = x.WG16;
   a.Q16 = x.Q16;
@@ -1556,20 +1816,21 @@ size_t ncf_cert_bytes(int64_t B, int64_t I, int K, int num_cus, int wg, bool str
 // certified lower bound of the exact K-th best score (real units) into lb[B].
 hnm_status ncf_cert_begin(hnm_ctx* ctx, const hnm_ncf_weights* w, const NcfTabs& t, int64_t B,
                           const int64_t* mptr, const int32_t* midx, int K, void* scratch,
-                          bool strided, float* lb, float* lists) {
+                          bool strided, float* lb, float* lists, const CertDeep* dp) {
   const int64_t I = w->num_items;
   const int wg = ncf_cert_wg(ctx);
   const CertShape sh = cert_shape(B, I, K, ctx->num_cus, wg);
   CertWs x;
   cert_carve((char*)scratch, B, I, K, ctx->num_cus, wg, strided, &x);
-  hnm_status st = cert_prepare(ctx, w, t, B, x);
+  hnm_status st = cert_prepare(ctx, w, t, B, x, dp);
   if (st) return st;
   const int64_t ublocks = hnm_cdiv(B, 128);
+  const bool deep = dp != nullptr;
   // champion sample: the first rows' approx - e over all items -> the best item of each of
   // nch groups -> every row's K-th best approx - e over those items -> L (a lower bound of
   // the exact K-th for any item subset; this one tends to hold the rows' best items)
   const int64_t bp = std::min<int64_t>(CERT_PROXY_USERS, B);
-  ScanArgs a = scan_args(x, bp);
+  ScanArgs a = scan_args(x, bp, deep);
   a.I = I;
   a.dense = x.pdense;
   a.ldo = I;
@@ -1599,7 +1860,7 @@ hnm_status ncf_cert_begin(hnm_ctx* ctx, const hnm_ncf_weights* w, const NcfTabs&
   } else if (strided) {
     HNM_HIP_CHECK(hipMemsetAsync(x.gate, 0, 4, ctx->stream));
   }
-  ScanArgs c = scan_args(x, B);
+  ScanArgs c = scan_args(x, B, deep);
   c.I = sh.nch;
   c.sidx = x.sidx;
   c.dense = x.cdense;
@@ -1615,7 +1876,7 @@ hnm_status ncf_cert_begin(hnm_ctx* ctx, const hnm_ncf_weights* w, const NcfTabs&
   st = hnm_sample_kth(ctx, x.cdense, sh.nch, B, sh.nch, mptr, midx, K, 1, 1, x.sidx, x.kthv);
   if (st) return st;
   // gated strided sample: every row against one tile in CERT_STRIDE (exits when gated off)
-  ScanArgs g2 = scan_args(x, B);
+  ScanArgs g2 = scan_args(x, B, deep);
   g2.I = sh.ns;
   g2.sidx = x.sidx2;
   g2.dense = x.sdense;
@@ -1648,7 +1909,8 @@ hnm_status ncf_cert_begin(hnm_ctx* ctx, const hnm_ncf_weights* w, const NcfTabs&
 // short_ok: a row may keep fewer than K candidates (its bound came from another shard).
 hnm_status ncf_cert_finish(hnm_ctx* ctx, const hnm_ncf_weights* w, const NcfTabs& t, int64_t B,
                            const int64_t* mptr, const int32_t* midx, int K, void* scratch,
-                           bool strided, const float* lb, int short_ok, float* ov, int64_t* oi) {
+                           bool strided, const float* lb, int short_ok, float* ov, int64_t* oi,
+                           const CertDeep* dp, int32_t** ovf_rows, int32_t** ovf_cnt) {
   const int64_t I = w->num_items;
   const int wg = ncf_cert_wg(ctx);
   const CertShape sh = cert_shape(B, I, K, ctx->num_cus, wg);
@@ -1659,7 +1921,7 @@ hnm_status ncf_cert_finish(hnm_ctx* ctx, const hnm_ncf_weights* w, const NcfTabs
                      ctx->stream, lb ? lb : x.lb, x.Au, x.Cu, x.Eu, x.prm, w->bp, B, x.tau, x.flag);
   HNM_LAUNCH_CHECK();
   // main f16 scan: append items with approx + e >= tau_u to per-partition segments
-  ScanArgs a = scan_args(x, B);
+  ScanArgs a = scan_args(x, B, dp != nullptr);
   a.I = I;
   a.mptr = mptr;
   a.midx = midx;
@@ -1676,12 +1938,25 @@ hnm_status ncf_cert_finish(hnm_ctx* ctx, const hnm_ncf_weights* w, const NcfTabs
   HNM_LAUNCH_CHECK();
   // exact fp32 re-scoring + top-K of the candidates; unusable rows -> queue
   const int64_t rgrid = std::min<int64_t>(hnm_cdiv(B, 4), (int64_t)RESCORE_PERSIST * ctx->num_cus);
-  hipLaunchKernelGGL(ncf_rescore_kernel, dim3((unsigned)rgrid), dim3(256), 0, ctx->stream,
-                     t, w->mf, w->w2, w->h1, w->h2, w->b2, w->wp + w->mf, w->bp, B, x.flag, x.cnt,
-                     x.buf, x.bufd, x.tau, x.Eu, x.Au, x.Cu, x.prm, sh.part.np, sh.capp, K,
-                     short_ok, ov, oi, x.ovf_rows, x.ovf_cnt,
-                     ctx->stats_on ? ctx->stats_dev : nullptr);
+  const CertDeep dv = dp ? *dp : CertDeep{};
+#define HNM_RESCORE(DEEPV)                                                                       \
+  hipLaunchKernelGGL(ncf_rescore_kernel<DEEPV>, dim3((unsigned)rgrid), dim3(256), 0, ctx->stream, \
+                     t, w->mf, w->w2, w->h1, w->h2, w->b2, w->wp + w->mf, w->bp, B, x.flag,       \
+                     x.cnt, x.buf, x.bufd, x.tau, x.Eu, x.Au, x.Cu, x.prm, sh.part.np, sh.capp,  \
+                     K, short_ok, ov, oi, x.ovf_rows, x.ovf_cnt,                                 \
+                     ctx->stats_on ? ctx->stats_dev : nullptr, dv, w->num_users);
+  if (dp) {
+    HNM_RESCORE(true)
+  } else {
+    HNM_RESCORE(false)
+  }
+#undef HNM_RESCORE
   HNM_LAUNCH_CHECK();
+  if (dp) {  // the deep tower's exact scan of the queued rows is the caller's (ncf_deep.hip)
+    *ovf_rows = x.ovf_rows;
+    *ovf_cnt = x.ovf_cnt;
+    return HNM_OK;
+  }
   // exact fp32 scan over all items for the queued rows (device-side row list)
   return ncf_list_rows(ctx, w, t, B, mptr, midx, K, x.ovf_rows, x.ovf_cnt, x.cv, x.ci, ov, oi);
 }
@@ -1694,17 +1969,48 @@ hnm_status ncf_cert_topk(hnm_ctx* ctx, const hnm_ncf_weights* w, const NcfTabs& 
   return ncf_cert_finish(ctx, w, t, B, mptr, midx, K, scratch, strided, nullptr, 0, ov, oi);
 }
 
+hnm_status ncf_deep_cert_topk(hnm_ctx* ctx, const hnm_ncf_weights* w, const CertDeep& dp,
+                              const NcfTabs& t, int64_t B, const int64_t* mptr,
+                              const int32_t* midx, int K, void* scratch, float* ov, int64_t* oi,
+                              int32_t** ovf_rows, int32_t** ovf_cnt, bool* pruned) {
+  hnm_status st = ncf_cert_begin(ctx, w, t, B, mptr, midx, K, scratch, false, nullptr, nullptr, &dp);
+  if (st) return st;
+  // can the bound prune?  the proxy rows' predicted candidates (one read-back)
+  const int64_t I = w->num_items;
+  const CertShape sh = cert_shape(B, I, K, ctx->num_cus, ncf_cert_wg(ctx));
+  CertWs x;
+  cert_carve((char*)scratch, B, I, K, ctx->num_cus, ncf_cert_wg(ctx), false, &x);
+  const int np_rows = (int)std::min<int64_t>(CERT_PROXY_USERS, B);
+  HNM_HIP_CHECK(hipMemsetAsync(x.gcnt, 0, 8, ctx->stream));
+  hipLaunchKernelGGL(cert_predict_kernel,
+                     dim3((unsigned)std::min<int64_t>(64, hnm_cdiv(I, 256)), (unsigned)np_rows),
+                     dim3(256), 0, ctx->stream, x.pdense, I, K, x.kthv, x.Eu, x.Bs, x.Cs, x.Di,
+                     x.prm, x.gcnt);
+  HNM_LAUNCH_CHECK();
+  unsigned long long pc = 0;
+  HNM_HIP_CHECK(hipMemcpyAsync(&pc, x.gcnt, 8, hipMemcpyDeviceToHost, ctx->stream));
+  HNM_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+  // prune when a row would re-score at most 1/16 of the catalogue (re-scoring a candidate costs
+  // several pairs of the exact tiled scan) and half its segments' capacity
+  const int64_t limit = std::min<int64_t>(I / 16, (int64_t)sh.part.np * sh.capp / 2);
+  *pruned = (int64_t)(pc / (unsigned long long)np_rows) <= limit;
+  if (!*pruned) return HNM_OK;
+  return ncf_cert_finish(ctx, w, t, B, mptr, midx, K, scratch, false, nullptr, 0, ov, oi, &dp,
+                         ovf_rows, ovf_cnt);
+}
+
 hnm_status ncf_cert_debug(hnm_ctx* ctx, const hnm_ncf_weights* w, const NcfTabs& t, int64_t B,
-                          void* scratch, float* approx, int64_t lda, float* bound) {
+                          void* scratch, float* approx, int64_t lda, float* bound,
+                          const CertDeep* dp) {
   const int64_t I = w->num_items;
   CertWs x;
   cert_carve((char*)scratch, B, I, 1, ctx->num_cus, ncf_cert_wg(ctx), false, &x);
-  hnm_status st = cert_prepare(ctx, w, t, B, x);
+  hnm_status st = cert_prepare(ctx, w, t, B, x, dp);
   if (st) return st;
   hipLaunchKernelGGL(cert_bound_kernel, dim3((unsigned)hnm_cdiv(B, 256)), dim3(256), 0, ctx->stream,
                      nullptr, nullptr, nullptr, 1, x.Au, x.prm, w->bp, B, nullptr, x.Eu);
   HNM_LAUNCH_CHECK();
-  ScanArgs a = scan_args(x, B);
+  ScanArgs a = scan_args(x, B, dp != nullptr);
   a.I = I;
   a.dense = approx;
   a.dense2 = bound;

@@ -15,8 +15,11 @@
 //     words) and 256 / TP lane groups share each layer's output units (the weights are
 //     wave-uniform loads).  DENSE: pairs (b, i) for every item; else pairs (user_ids[n],
 //     item_ids[n]) (forward).
+#include <vector>
+
 #include "hnm_device.h"
 #include "hnm_internal.h"
+#include "ncf_internal.h"
 
 hnm_status hnm_topk_merge_i32(hnm_ctx* ctx, const float* cv, const int32_t* ci, int64_t B,
                               int64_t G, int64_t gstride, int64_t bstride, int kc, int k,
@@ -840,7 +843,7 @@ extern "C" hnm_status hnm_ncf_deep_scores_f32(hnm_ctx* ctx, const hnm_ncf_deep_w
   return HNM_OK;
 }
 
-static hnm_status deep_topk_chunk(hnm_ctx* ctx, const hnm_ncf_deep_weights* w,
+static hnm_status deep_topk_exact(hnm_ctx* ctx, const hnm_ncf_deep_weights* w,
                                   const int64_t* ids, int64_t B, const int64_t* mptr,
                                   const int32_t* midx, int K, float* ov, int64_t* oi) {
   const int64_t I = w->num_items;
@@ -881,6 +884,104 @@ static hnm_status deep_topk_chunk(hnm_ctx* ctx, const hnm_ncf_deep_weights* w,
     if (st) return st;
   }
   return HNM_OK;
+}
+
+__global__ void deep_stats_kernel(unsigned long long* stats, int64_t B) {
+  atomicAdd(&stats[0], (unsigned long long)B);
+  atomicAdd(&stats[2], (unsigned long long)B);
+}
+
+__global__ void deep_scatter_rows_kernel(const int32_t* __restrict__ rows, int n, int K,
+                                        const float* __restrict__ tv, const int64_t* __restrict__ ti,
+                                        float* __restrict__ ov, int64_t* __restrict__ oi) {
+  const int64_t x = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (x >= (int64_t)n * K) return;
+  const int64_t o = (int64_t)rows[x / K] * K + x % K;
+  if (ov) ov[o] = tv[o];
+  oi[o] = ti[o];
+}
+
+// Round 6: towers [2 h0, h1 <= 64, h2 <= 32, h3 <= 16] (the bench's [128, 64, 32, 16]) take the
+// certified f16 pre-filter (ncf_cert.hip: the two-layer scan with a layer-3 matrix epilogue, exact
+// deep re-scoring -- results bitwise the exact path's); the rows it queues (unusable bound,
+// overflowing segments) take the exact deep scan: one B = 1 call each for a few rows, else the
+// whole chunk exactly with those rows' lists copied over (the count is read back: one sync).
+// When the proxy rows predict that the bound cannot prune (a worst-case bound through two
+// absolute-value layers wider than the score spread: init-like weights, tests/test_gpu_ncf_deep.py
+// prints the ratio) the whole call takes the exact kernels after the begin phase.
+static hnm_status deep_topk_chunk(hnm_ctx* ctx, const hnm_ncf_deep_weights* w,
+                                  const int64_t* ids, int64_t B, const int64_t* mptr,
+                                  const int32_t* midx, int K, float* ov, int64_t* oi) {
+  if (!(ctx->prefilter && B >= 16 && ncf_deep_cert_eligible(w, K)))
+    return deep_topk_exact(ctx, w, ids, B, mptr, midx, K, ov, oi);
+  int32_t *orows = nullptr, *ocnt = nullptr;
+  bool pruned = false;
+  hnm_status st = ncf_deep_cert(ctx, w, ids, B, mptr, midx, K, ov, oi, &orows, &ocnt, &pruned);
+  if (st) return st;
+  if (!pruned) {  // the bound is wider than the rows' spread: the exact kernels for every row
+    if (ctx->stats_on) {  // counted as B rows scored, all B on the exact fallback
+      hipLaunchKernelGGL(deep_stats_kernel, dim3(1), dim3(1), 0, ctx->stream, ctx->stats_dev, B);
+      HNM_LAUNCH_CHECK();
+    }
+    return deep_topk_exact(ctx, w, ids, B, mptr, midx, K, ov, oi);
+  }
+  int32_t n = 0;
+  HNM_HIP_CHECK(hipMemcpyAsync(&n, ocnt, 4, hipMemcpyDeviceToHost, ctx->stream));
+  HNM_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+  if (n <= 0) return HNM_OK;
+  if (n <= 16) {  // the rows' list is read before the exact calls reuse the workspace
+    std::vector<int32_t> rows((size_t)n);
+    HNM_HIP_CHECK(hipMemcpy(rows.data(), orows, (size_t)n * 4, hipMemcpyDeviceToHost));
+    for (int32_t r : rows) {
+      st = deep_topk_exact(ctx, w, ids + r, 1, mptr ? mptr + r : nullptr, midx, K,
+                           ov ? ov + (int64_t)r * K : nullptr, oi + (int64_t)r * K);
+      if (st) return st;
+    }
+    return HNM_OK;
+  }
+  int32_t* drows = nullptr;
+  float* tv = nullptr;
+  int64_t* ti = nullptr;
+  if (hipMallocAsync((void**)&drows, (size_t)n * 4, ctx->stream) != hipSuccess ||
+      hipMallocAsync((void**)&tv, (size_t)B * K * 4, ctx->stream) != hipSuccess ||
+      hipMallocAsync((void**)&ti, (size_t)B * K * 8, ctx->stream) != hipSuccess) {
+    if (drows) (void)hipFreeAsync(drows, ctx->stream);
+    if (tv) (void)hipFreeAsync(tv, ctx->stream);
+    hnm_set_error("ncf_deep_topk: fallback buffers: hipMallocAsync failed");
+    return HNM_ENOMEM;
+  }
+  HNM_HIP_CHECK(hipMemcpyAsync(drows, orows, (size_t)n * 4, hipMemcpyDeviceToDevice, ctx->stream));
+  st = deep_topk_exact(ctx, w, ids, B, mptr, midx, K, tv, ti);
+  if (!st) {
+    hipLaunchKernelGGL(deep_scatter_rows_kernel, dim3((unsigned)hnm_cdiv((int64_t)n * K, 256)),
+                       dim3(256), 0, ctx->stream, drows, n, K, tv, ti, ov, oi);
+    if (hipGetLastError() != hipSuccess) st = HNM_EHIP;
+  }
+  (void)hipFreeAsync(drows, ctx->stream);
+  (void)hipFreeAsync(tv, ctx->stream);
+  (void)hipFreeAsync(ti, ctx->stream);
+  if (st == HNM_EHIP) hnm_set_error("ncf_deep_topk: fallback scatter launch failed");
+  return st;
+}
+
+// Diagnostics of the deep certified pre-filter (no reference counterpart): approx[b, i] = the f16
+// scan's score without bp, bound[b, i] its certified bound (real units): |approx + bp - exact| <=
+// bound for every pair (tests check it on the full catalogue).
+extern "C" hnm_status hnm_ncf_deep_prefilter_debug_f32(hnm_ctx* ctx, const hnm_ncf_deep_weights* w,
+                                                       const int64_t* user_ids, int64_t B,
+                                                       float* approx, int64_t lda, float* bound) {
+  HNM_CTX_DEVICE(ctx);
+  hnm_status st = deep_check(w);
+  if (st) return st;
+  HNM_REQUIRE(ctx && user_ids && approx && bound && lda >= w->num_items, HNM_EINVAL,
+              "ncf_deep_prefilter_debug: bad argument");
+  HNM_REQUIRE(w->nl == 3 && w->dims[1] <= 64 && w->dims[2] <= 32 && w->dims[3] <= 16 &&
+                  w->mf <= 64 && w->mf % 4 == 0 && w->num_items * 64 < ((int64_t)1 << 31),
+              HNM_EUNSUPPORTED,
+              "ncf_deep_prefilter_debug: the deep pre-filter covers towers [2 h0, <= 64, <= 32, "
+              "<= 16], mf <= 64 (a multiple of 4), < 2^25 items");
+  if (B <= 0) return HNM_OK;
+  return ncf_deep_cert_debug(ctx, w, user_ids, B, approx, lda, bound);
 }
 
 extern "C" hnm_status hnm_ncf_deep_topk_f32(hnm_ctx* ctx, const hnm_ncf_deep_weights* w,

@@ -298,14 +298,26 @@ hnm_status hnm_ncf_deep_scores_f32(hnm_ctx* ctx, const hnm_ncf_deep_weights* w,
                                    float* out, int64_t ldo);
 /* Fused top-k of a deep tower (NeuralCF.recommend, neural_cf.py:300-326, with the -inf filter
  * and torch.topk of neural_cf.py:316-324): (score desc, item asc), scores bitwise those of
- * hnm_ncf_deep_scores_f32, 1 <= k <= 64, mask as hnm_ncf_topk_f32.  Towers with every width
- * dims[1..nl] <= 64 and mf <= 128 take the fp32-MFMA scan that keeps per-partition top-k
+ * hnm_ncf_deep_scores_f32, 1 <= k <= 64, mask as hnm_ncf_topk_f32.  Three-layer towers
+ * [2 h0, h1 <= 64, h2 <= 32, h3 <= 16] with mf <= 64 (a multiple of 4) take the certified f16
+ * pre-filter when HNM_OPT_PREFILTER is on and the call is in its range (B >= 16, >= 8,192 items,
+ * >= 64 k): the two-layer tower's f16 scan with a third layer on the matrix pipe, its worst-case
+ * bound carried through |wp3|^T |W3| |W2|, exact fp32 re-scoring of the survivors by the deep
+ * chain (outputs bitwise the exact path's); rows the bound cannot serve take the exact scan
+ * (their count is read back: the call synchronizes its stream).  Otherwise towers with every
+ * width dims[1..nl] <= 64 and mf <= 128 take the fp32-MFMA scan that keeps per-partition top-k
  * lists (no [B, I] score matrix); wider towers score dense rows per user chunk in the
  * workspace and take the row top-k kernel. */
 hnm_status hnm_ncf_deep_topk_f32(hnm_ctx* ctx, const hnm_ncf_deep_weights* w,
                                  const int64_t* user_ids, int64_t B, const int64_t* mask_ptr,
                                  const int32_t* mask_idx, int k, float* out_val,
                                  int64_t* out_idx);
+/* Diagnostics of that pre-filter (no reference counterpart): approx[b, i] = the f16 scan's score
+ * of item i without bp, bound[b, i] its certified bound ([B, lda], real units); |approx + bp -
+ * exact| <= bound for every pair (tests check it on the full catalogue). */
+hnm_status hnm_ncf_deep_prefilter_debug_f32(hnm_ctx* ctx, const hnm_ncf_deep_weights* w,
+                                            const int64_t* user_ids, int64_t B, float* approx,
+                                            int64_t lda, float* bound);
 
 /* ---- a9 + a10: Wide&Deep ------------------------------------------------------------
  * Reference layout (wide_deep.py:92-134): deep tower Linear -> ReLU -> BatchNorm1d (eval:

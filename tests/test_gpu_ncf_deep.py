@@ -100,16 +100,28 @@ def test_deep_mfma_bitwise_and_fused_topk(mf, dims, B):
     np.testing.assert_array_equal(m.recommend_with_scores(users, k=64)[1].cpu().numpy(), ref_i)
 
 
+def exact(fn):
+    """Run fn with the certified pre-filter off (the exact deep kernels everywhere)."""
+    _lib.set_prefilter(DEV, False)
+    try:
+        return fn()
+    finally:
+        _lib.set_prefilter(DEV, True)
+
+
 def test_deep_mfma_full_catalogue_topk():
     """[128,64,32,16] over the full H&M catalogue (105,542 items, many partitions) at B = 512:
-    fused top-12 equals the per-pair route's lists bitwise; oracle rows agree."""
+    the fused exact top-12 (pre-filter off) equals the per-pair route's lists bitwise, and so does
+    the default (certified, round 6) call; oracle rows agree."""
     U, I = 3000, syn.HM_ITEMS
     m, sd = model(U, I, 64, (128, 64, 32, 16), seed=21)
     users_np = syn.user_batch(U, 512, seed=4)
     users = torch.from_numpy(users_np).to(DEV)
-    v, i = m.recommend_with_scores(users)
-    v2, i2 = per_pair(lambda: m.recommend_with_scores(users))
+    v, i = exact(lambda: m.recommend_with_scores(users))
+    v2, i2 = exact(lambda: per_pair(lambda: m.recommend_with_scores(users)))
     assert torch.equal(i, i2) and torch.equal(v.view(torch.int32), v2.view(torch.int32))
+    v3, i3 = m.recommend_with_scores(users)
+    assert torch.equal(i, i3) and torch.equal(v.view(torch.int32), v3.view(torch.int32))
     rows = [0, 255, 511]
     ref = O.ncf_predict_all_items(sd, users_np[rows])
     got = m.predict_all_items(users[rows]).cpu().numpy()
@@ -143,3 +155,104 @@ def test_deep_item_shards_merge_to_the_unsharded_topk():
         assert torch.equal(mi, full_i)
         assert torch.equal(mv.view(torch.int32), full_v.view(torch.int32))
 
+
+
+# ------------------------------------------------------------------ certified deep pre-filter
+# Round 6: three-layer towers take the two-layer tower's certified f16 scan with a
+# third layer on the matrix pipe and a worst-case bound carried through |wp3|^T |W3| |W2|
+# (ncf_cert.hip); survivors are re-scored by the exact deep chain.  The bound must hold pair by
+# pair over the full catalogue, and the top-k must be bitwise the exact path's, for weights unlike
+# the init too (synthetic.stress_state_dict) -- and rows the bound cannot serve must come back
+# exact through both fallback routes.
+DEEP_DIMS = (128, 64, 32, 16)
+DEEP_WEIGHTS = ["init", "personal", "norms", "student_t"]
+
+
+def deep_weights_model(U, I, kind, seed=3):
+    kw = ({} if kind == "init" else dict(bias_scale=0.05, emb_scale=20.0) if kind == "personal"
+          else dict(bias_scale=0.05))
+    sd = syn.ncf_state_dict(U, I, 64, DEEP_DIMS, seed=seed, **kw)
+    if kind not in ("init", "personal"):
+        sd = syn.stress_state_dict(sd, kind, syn.NCF_EMB_KEYS, "mlp_item_embedding.weight")
+    m = NeuralCF(U, I, mf_dim=64, mlp_dims=list(DEEP_DIMS))
+    m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in sd.items()})
+    return m.to(DEV).eval()
+
+
+def deep_debug(m, users):
+    import ctypes as C
+    w, keep = m._deep_weights()
+    I = m.num_items
+    approx = torch.empty(users.numel(), I, device=DEV)
+    bound = torch.empty_like(approx)
+    _lib.check(_lib.fn("hnm_ncf_deep_prefilter_debug_f32")(
+        _lib.ctx(users.device), C.byref(w), _lib.ptr(users), users.numel(), _lib.ptr(approx), I,
+        _lib.ptr(bound)), "hnm_ncf_deep_prefilter_debug_f32")
+    return approx, bound
+
+
+@pytest.mark.parametrize("kind", DEEP_WEIGHTS)
+def test_deep_bound_holds_full_catalogue(kind):
+    U, I = 4000, syn.HM_ITEMS
+    m = deep_weights_model(U, I, kind)
+    users = torch.from_numpy(syn.user_batch(U, 16, seed=9)).to(DEV)
+    approx, bound = deep_debug(m, users)
+    ex = m.predict_all_items(users)
+    bp = float(m.prediction_layer.bias.detach())
+    err = (approx + bp - ex).abs()
+    ratio = (err / bound).max().item()
+    spread = ex.std(1, keepdim=True)
+    print(f"deep bound [{kind}]: max |approx - exact| / bound {ratio:.4f}, "
+          f"mean bound / score std {(bound / spread).mean().item():.4f}")
+    assert torch.isfinite(bound).all()
+    assert (err <= bound).all(), ratio
+
+
+@pytest.mark.parametrize("kind", DEEP_WEIGHTS)
+def test_deep_certified_topk_bitwise(kind):
+    U, I, B = 6000, syn.HM_ITEMS, 700
+    m = deep_weights_model(U, I, kind, seed=5)
+    users_np = syn.user_batch(U, B, seed=11)
+    users = torch.from_numpy(users_np).to(DEV)
+    ks = (12, 64) if kind == "init" else (12,)
+    for k in ks:
+        _lib.prefilter_stats(DEV, reset=True)
+        _lib.set_option(DEV, _lib.HNM_OPT_STATS, 1)
+        v, i = m.recommend_with_scores(users, k=k)
+        _lib.set_option(DEV, _lib.HNM_OPT_STATS, 0)
+        rows, cands, fb = _lib.prefilter_stats(DEV, reset=True)
+        ev, ei = exact(lambda: m.recommend_with_scores(users, k=k))
+        print(f"deep certified [{kind}, k={k}]: {cands / max(rows - fb, 1):.1f} candidates a row, "
+              f"{fb} fallback rows of {rows}")
+        assert rows == B
+        assert torch.equal(i, ei), kind
+        assert torch.equal(v.view(torch.int32), ev.view(torch.int32)), kind
+    if kind == "init":  # the history filter (every 3rd row: its top-3 and 40 random items)
+        rng = np.random.default_rng(1)
+        filt = {}
+        top = ei.cpu().numpy()
+        for b in range(0, B, 3):
+            u = int(users_np[b])
+            filt.setdefault(u, set()).update(int(x) for x in top[b, :3])
+            filt[u].update(int(x) for x in rng.integers(0, I, 40))
+        v, i = m.recommend_with_scores(users, filter_items=filt, k=12)
+        ev, ei = exact(lambda: m.recommend_with_scores(users, filter_items=filt, k=12))
+        assert torch.equal(i, ei) and torch.equal(v.view(torch.int32), ev.view(torch.int32))
+
+
+@pytest.mark.parametrize("B", [16, 40])
+def test_deep_certified_fallback_rows(B):
+    """One item row at 1e13 makes the bound unusable (maxima above the 2^40 guard): every row is
+    queued for the exact scan -- B = 16 through one exact call per row, B = 40 through the whole
+    batch exactly with the queued rows' lists copied over -- and the lists equal the exact path's."""
+    U, I = 3000, syn.HM_ITEMS
+    m = deep_weights_model(U, I, "huge", seed=7)
+    users = torch.from_numpy(syn.user_batch(U, B, seed=B)).to(DEV)
+    _lib.prefilter_stats(DEV, reset=True)
+    _lib.set_option(DEV, _lib.HNM_OPT_STATS, 1)
+    v, i = m.recommend_with_scores(users)
+    _lib.set_option(DEV, _lib.HNM_OPT_STATS, 0)
+    rows, cands, fb = _lib.prefilter_stats(DEV, reset=True)
+    assert fb == B, (rows, fb)
+    ev, ei = exact(lambda: m.recommend_with_scores(users))
+    assert torch.equal(i, ei) and torch.equal(v.view(torch.int32), ev.view(torch.int32))
