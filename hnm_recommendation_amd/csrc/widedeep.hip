@@ -1522,6 +1522,8 @@ struct WdRescoreArgs {
   const float* v2p;  // [RB2*32] plain v2
   const float* b2s;  // [RB2*32] b2' s2
   int64_t rstride;   // row stride of segi / segu / segl (NP * cap)
+  float* segs;       // [B, NP * cap] the survivors' SCAN upper bounds, compacted by wdc_collect
+  const int* rstart; // refining stage: row b's tiles start at position rstart[b] (nullptr: 0)
   float* dbg_a;      // hnm_widedeep_refine_debug_f32: refined score / bound per item, [B, lda]
   float* dbg_e;
   int64_t lda;
@@ -1711,10 +1713,16 @@ __device__ __forceinline__ void wd_tile_f16x3(const float* __restrict__ psr,
 // fp32 tile: 15.7 ms a batch):
 //   wdc_collect_kernel  one wave per row: fallback rows queued; the row's scan survivors
 //                       (ub >= L_u) compacted to the front of its segment area, their count;
+//   wdc_best_kernel     (round 6) one wave per row: the refining list's first phase -- the
+//                       WDC_BF survivors of best scan upper bound (rows of <= WDC_BF_MIN: all);
 //   wdc_tiles_kernel    exclusive prefix of the rows' 32-item refining tiles (one block);
 //   wdc_refine_kernel   a fixed grid, each wave a contiguous run of tiles (balanced whatever
 //                       the rows' survivor counts): wd_tile_f16x3 -> refined bounds
-//                       lb2 <= exact <= ub2 per survivor;
+//                       lb2 <= exact <= ub2 per listed survivor;
+//   wdc_filter_kernel   (round 6) one wave per row: the remaining survivors whose scan upper
+//                       bound reaches the first phase's K-th refined lower bound appended to
+//                       the list, then tiles + refine again over them (~1,145 -> ~570 refined
+//                       a row at configs[3]: profiles/r10c_wd_best_first_probe.txt);
 //   wdc_rescore_kernel  one wave per row: L2 = the K-th best lb2 (a lower bound of the row's
 //                       exact K-th best), then the survivors with ub2 >= max(L2, L_u) -- every
 //                       item that can be in the top-K -- through wd_tile_fp32, the exact
@@ -1748,16 +1756,22 @@ __global__ __launch_bounds__(256) void wdc_collect_kernel(WdRescoreArgs R) {
       const int e = c0 + lane;
       const bool in = e < n;
       const int32_t it = in ? R.segi[base + e] : 0;
-      const bool ok = in && R.segu[base + e] >= Lu;
+      const float u = in ? R.segu[base + e] : 0.f;
+      const bool ok = in && u >= Lu;
       const uint64_t m = __ballot(ok);
-      if (ok) R.segi[rowbase + no + __popcll(m & ((1ull << lane) - 1))] = it;
+      if (ok) {
+        const int64_t o = rowbase + no + __popcll(m & ((1ull << lane) - 1));
+        R.segi[o] = it;
+        R.segs[o] = u;  // a separate array: the scan's upper bounds are read in place above
+      }
       no += __popcll(m);
     }
   }
   if (lane == 0) R.ns[b] = no;
 }
 
-__global__ __launch_bounds__(1024) void wdc_tiles_kernel(const int* __restrict__ ns, int64_t B,
+__global__ __launch_bounds__(1024) void wdc_tiles_kernel(const int* __restrict__ ns,
+                                                         const int* __restrict__ start, int64_t B,
                                                          int* __restrict__ toff) {
   __shared__ int wsum[16];
   __shared__ int carry;
@@ -1766,7 +1780,7 @@ __global__ __launch_bounds__(1024) void wdc_tiles_kernel(const int* __restrict__
   __syncthreads();
   for (int64_t b0 = 0; b0 < B; b0 += 1024) {
     const int64_t b = b0 + tid;
-    const int t = b < B ? (int)hnm_cdiv(std::max(ns[b], 0), WD_TILE) : 0;
+    const int t = b < B ? (int)hnm_cdiv(std::max(ns[b] - (start ? start[b] : 0), 0), WD_TILE) : 0;
     int incl = t;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
@@ -1839,8 +1853,9 @@ __global__ __launch_bounds__(256, 1) void wdc_refine_kernel(WdRescoreArgs R) {
       cb = b;
     }
     const int k = (int)(t - R.toff[b]);
-    const int nv = std::min(WD_TILE, R.ns[b] - WD_TILE * k);
-    const int64_t at = b * R.rstride + (int64_t)WD_TILE * k;
+    const int st = R.rstart ? R.rstart[b] : 0;
+    const int nv = std::min(WD_TILE, R.ns[b] - st - WD_TILE * k);
+    const int64_t at = b * R.rstride + st + (int64_t)WD_TILE * k;
     const bool ivalid = lane < 32 && j < nv;
     const int it = R.segi[at + (j < nv ? j : 0)];
     float fv, b1, b2, b3;
@@ -1860,6 +1875,84 @@ __global__ __launch_bounds__(256, 1) void wdc_refine_kernel(WdRescoreArgs R) {
       }
     }
   }
+}
+
+// Best-first refining (round 6).  A row of more than WDC_BF_MIN survivors
+// refines its WDC_BF survivors of best scan upper bound first (wdc_best_kernel); their K-th best
+// refined lower bound L2' is a certified lower bound of the row's exact K-th, so a remaining
+// survivor is refined only if its scan upper bound reaches max(L2', L_u) (wdc_filter_kernel):
+// otherwise exact <= scan ub < L2' <= the exact K-th, and it cannot be in the top-K.  The rows'
+// refining lists (cli: the first phase, then the filtered rest) replace the survivor lists in
+// the refining stage and in wdc_rescore_kernel, whose output is unchanged (bitwise the exact
+// path).  Rows of at most WDC_BF_MIN survivors refine them all in the first phase.
+constexpr int WDC_BF = 64;
+constexpr int WDC_BF_MIN = 96;
+
+// one wave per row: cli[0, nA) = the first phase's items (the WDC_BF best by (scan ub desc,
+// survivor position asc), or every survivor), tv / tg = the WDC_BF-th (ub, position)
+__global__ __launch_bounds__(256) void wdc_best_kernel(WdRescoreArgs R, int32_t* __restrict__ cli,
+                                                       int* __restrict__ nA,
+                                                       float* __restrict__ tv,
+                                                       int* __restrict__ tg) {
+  const int lane = threadIdx.x & 63;
+  const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (b >= R.B) return;
+  const int ns = R.ns[b];
+  const int64_t rowbase = b * R.rstride;
+  if (ns <= WDC_BF_MIN) {  // incl. the exact kernel's rows (-1)
+    for (int e = lane; e < ns; e += 64) cli[rowbase + e] = R.segi[rowbase + e];
+    if (lane == 0) nA[b] = ns;
+    return;
+  }
+  float v0 = -__builtin_inff();
+  int i0 = HNM_SENTINEL_IDX;
+  for (int c0 = 0; c0 < ns; c0 += 64) {  // running WDC_BF best; survivors' ubs are finite
+    const int g = c0 + lane;
+    float v1 = g < ns ? R.segs[rowbase + g] : -__builtin_inff();
+    int i1 = g < ns ? g : HNM_SENTINEL_IDX;
+    const float c63 = hnm_readlane_f(v0, 63);
+    const int c63i = hnm_readlane_i(i0, 63);
+    if (__ballot(hnm_better(v1, i1, c63, c63i))) hnm_sort128(v0, i0, v1, i1);
+  }
+  cli[rowbase + lane] = R.segi[rowbase + i0];
+  if (lane == 63) {
+    tv[b] = v0;
+    tg[b] = i0;
+  }
+  if (lane == 0) nA[b] = WDC_BF;
+}
+
+// one wave per row (after the first phase's refining): L2' from the first phase's refined lower
+// bounds; the remaining survivors with scan ub >= max(L2', L_u) appended to cli; ns = the list's
+// final length
+__global__ __launch_bounds__(256) void wdc_filter_kernel(WdRescoreArgs R, int32_t* __restrict__ cli,
+                                                         const float* __restrict__ tv,
+                                                         const int* __restrict__ tg) {
+  const int lane = threadIdx.x & 63;
+  const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (b >= R.B) return;
+  const int ns = R.ns[b];
+  if (ns <= WDC_BF_MIN) return;  // single phase (or the exact kernel's row): the list is complete
+  const int K = R.K;
+  const int64_t rowbase = b * R.rstride;
+  WaveTopK<1> T2;  // K <= 64 = WDC_BF distinct items
+  T2.init();
+  T2.offer(R.segl[rowbase + lane], cli[rowbase + lane], true, K);
+  const float thr = fmaxf(T2.thr_v, R.Lk[b * K + K - 1]);
+  const float v64 = tv[b];
+  const int g64 = tg[b];
+  int no = WDC_BF;
+  for (int c0 = 0; c0 < ns; c0 += 64) {
+    const int g = c0 + lane;
+    const bool in = g < ns;
+    const float u = in ? R.segs[rowbase + g] : -__builtin_inff();
+    const bool first = u > v64 || (u == v64 && g <= g64);  // refined in the first phase
+    const bool keep = in && !first && u >= thr;
+    const uint64_t m = __ballot(keep);
+    if (keep) cli[rowbase + no + __popcll(m & ((1ull << lane) - 1))] = R.segi[rowbase + g];
+    no += __popcll(m);
+  }
+  if (lane == 0) R.ns[b] = no;
 }
 
 template <int RB2, int OB>
@@ -2187,6 +2280,11 @@ struct WdcWs {
   float* segu;
   int* cnt;
   float* segl;
+  float* segs;
+  int32_t* cli;
+  int* nA;
+  float* tv;
+  int* tg;
   int* ns;
   int* toff;
   int32_t* fbrows;
@@ -2235,6 +2333,11 @@ static size_t wdc_carve(const hnm_ctx* ctx, const WdPrep& pr, int64_t B, int64_t
   t.segu = (float*)take((size_t)B * np * cap * 4);
   t.cnt = (int*)take((size_t)B * np * 4);
   t.segl = (float*)take((size_t)B * np * cap * 4);
+  t.segs = (float*)take((size_t)B * np * cap * 4);
+  t.cli = (int32_t*)take((size_t)B * np * cap * 4);
+  t.nA = (int*)take((size_t)B * 4);
+  t.tv = (float*)take((size_t)B * 4);
+  t.tg = (int*)take((size_t)B * 4);
   t.ns = (int*)take((size_t)B * 4);
   t.toff = (int*)take((size_t)(B + 1) * 4);
   t.fbrows = (int32_t*)take((size_t)B * 4);
@@ -2278,18 +2381,38 @@ static void wdc_launch_scan(hnm_ctx* ctx, dim3 grid, size_t lds, const WdScanArg
 template <int RB2, int OB>
 static void wdc_launch_refine(hnm_ctx* ctx, const WdRescoreArgs& r) {
   constexpr int NOB = OB > 0 ? OB : 1, NL = OB > 0 ? OB : RB2;
-  hipLaunchKernelGGL(wdc_tiles_kernel, dim3(1), dim3(1024), 0, ctx->stream, r.ns, r.B, r.toff);
+  hipLaunchKernelGGL(wdc_tiles_kernel, dim3(1), dim3(1024), 0, ctx->stream, r.ns, r.rstart, r.B,
+                     r.toff);
   const size_t lds = (size_t)(5 * r.K1P + 2 * RB2 * 32 + NOB * 32 + NL * 32) * 4;
   auto kern = wdc_refine_kernel<RB2, OB>;
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   hipLaunchKernelGGL(kern, dim3(ctx->num_cus), dim3(256), lds, ctx->stream, r);
 }
 
+struct WdcBestFirst {
+  int32_t* cli;  // [B, rstride] the rows' refining lists
+  int* nA;       // [B] first-phase length
+  float* tv;     // [B] the first phase's last (scan ub, position)
+  int* tg;
+};
+
 template <int RB2, int OB>
-static void wdc_launch_rescore(hnm_ctx* ctx, dim3 grid, const WdRescoreArgs& r) {
-  hipLaunchKernelGGL(wdc_collect_kernel, grid, dim3(256), 0, ctx->stream, r);
-  wdc_launch_refine<RB2, OB>(ctx, r);
-  hipLaunchKernelGGL((wdc_rescore_kernel<RB2, OB>), grid, dim3(256), 0, ctx->stream, r);
+static void wdc_launch_rescore(hnm_ctx* ctx, dim3 grid, const WdRescoreArgs& r,
+                               const WdcBestFirst& bf) {
+  hipStream_t s = ctx->stream;
+  hipLaunchKernelGGL(wdc_collect_kernel, grid, dim3(256), 0, s, r);
+  hipLaunchKernelGGL(wdc_best_kernel, grid, dim3(256), 0, s, r, bf.cli, bf.nA, bf.tv, bf.tg);
+  WdRescoreArgs q = r;  // the refining lists replace the survivor lists from here on
+  q.segi = bf.cli;
+  WdRescoreArgs qa = q;  // first phase: cli[0, nA)
+  qa.ns = bf.nA;
+  qa.rstart = nullptr;
+  wdc_launch_refine<RB2, OB>(ctx, qa);
+  hipLaunchKernelGGL(wdc_filter_kernel, grid, dim3(256), 0, s, r, bf.cli, bf.tv, bf.tg);
+  WdRescoreArgs qb = q;  // second phase: cli[nA, ns)
+  qb.rstart = bf.nA;
+  wdc_launch_refine<RB2, OB>(ctx, qb);
+  hipLaunchKernelGGL((wdc_rescore_kernel<RB2, OB>), grid, dim3(256), 0, s, q);
 }
 
 static hnm_status wdc_scan(hnm_ctx* ctx, const hnm_widedeep_weights* w, const WdSetup& S,
@@ -2399,9 +2522,12 @@ static hnm_status wdc_topk(hnm_ctx* ctx, const hnm_widedeep_weights* w, const Wd
   r.v1p = c.v1o;
   r.v2p = c.v2o;
   r.b2s = c.b2s;
+  r.segs = c.segs;
+  r.rstart = nullptr;
+  const WdcBestFirst bf = {c.cli, c.nA, c.tv, c.tg};
   dim3 grid((unsigned)hnm_cdiv(B, 4));
 #define WDC_CASE(R, O) \
-  if (pr.RB2 == R && pr.OB == O) wdc_launch_rescore<R, O>(ctx, grid, r);
+  if (pr.RB2 == R && pr.OB == O) wdc_launch_rescore<R, O>(ctx, grid, r, bf);
   WDC_CASE(8, 4)
   WDC_CASE(4, 2)
   WDC_CASE(2, 1)
