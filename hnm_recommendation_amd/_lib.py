@@ -312,6 +312,7 @@ HNM_OPT_PREFILTER = 1
 HNM_OPT_STATS = 3
 HNM_OPT_STRIDED = 4
 HNM_OPT_DEEP_MFMA = 5
+HNM_OPT_LINEAR_MFMA = 6
 
 
 def set_option(device, option, value):

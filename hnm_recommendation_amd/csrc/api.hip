@@ -35,6 +35,10 @@ extern "C" hnm_status hnm_ctx_create(int device, hnm_ctx** out) {
   c->prefilter = 1;
   c->strided = 0;
   c->deep_mfma = 1;
+#ifndef HNM_LINEAR_MFMA_DEFAULT  // A/B builds only (tools/build_variant.sh)
+#define HNM_LINEAR_MFMA_DEFAULT 1
+#endif
+  c->linear_mfma = HNM_LINEAR_MFMA_DEFAULT;
   if (hipMalloc((void**)&c->err_dev, 64) != hipSuccess) {
     free(c);
     hnm_set_error("hnm_ctx_create: hipMalloc of the error word failed");
@@ -107,6 +111,9 @@ extern "C" hnm_status hnm_ctx_set_option(hnm_ctx* ctx, int option, int64_t value
       return HNM_OK;
     case HNM_OPT_DEEP_MFMA:
       ctx->deep_mfma = value != 0;
+      return HNM_OK;
+    case HNM_OPT_LINEAR_MFMA:
+      ctx->linear_mfma = value != 0;
       return HNM_OK;
     default:
       hnm_set_error("hnm_ctx_set_option: unknown option %d", option);
@@ -421,6 +428,74 @@ __global__ __launch_bounds__(256) void linear_rows_kernel(
   }
 }
 
+// Round 6: the same projection on the fp32 matrix pipe when K is a multiple of 32 (the NCF
+// and W&D layer-1 halves: K = h0 / d = 64).  v_mfma_f32_32x32x2_f32 is an exact fp32 fma chain
+// in k order (tools/mfma_semantics_probe.hip (a)), so a chain of them from C = 0 over k = 0, 1,
+// .., K-1 and the bias added after is bitwise linear_rows_kernel's per-output fmaf chain
+// (tests/test_gpu_abi_rows.py checks both kernels on the same inputs).  64 rows x 64 outputs a
+// block, one 32 x 32 output tile a wave (waves 2 r + c: rows 32 r, outputs 32 c), K in chunks
+// of 32 staged through LDS as in linear_rows_kernel (16-B global loads).  rocprofv3 minima
+// (profiles/r10g_linear_rows_ab.txt): NCF's item half (105,542 x 64 x 64) 21.0 -> 18.1 us,
+// W&D's (105,542 x 512 x 64) 115.2 -> 100.5 us -- the staging, not the FMAs, bounds both.
+__global__ __launch_bounds__(256) void linear_rows_mfma_kernel(
+    const float* __restrict__ X, int64_t ldx, const int64_t* __restrict__ ids, int64_t x_rows,
+    int64_t M, int K, const float* __restrict__ W, int64_t ldw, const float* __restrict__ bias,
+    int N, float* __restrict__ Y, int64_t ldy, int pair_permute, unsigned* err) {
+  constexpr int RS = LIN_TK + 1;  // LDS row stride (floats): rows spread over the banks
+  __shared__ float xs[64 * RS];   // [row][k] of the chunk
+  __shared__ float ws[64 * RS];   // [output][k]
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int i = lane & 31, h = lane >> 5;
+  const int64_t m0 = (int64_t)blockIdx.x * 64;
+  const int n0 = blockIdx.y * LIN_TN;
+  const int wr = 32 * (wave >> 1), wc = 32 * (wave & 1);
+  f32x16 acc = {};
+  for (int k0 = 0; k0 < K; k0 += LIN_TK) {
+    for (int e = t; e < 64 * LIN_TK / 4; e += 256) {
+      const int rr = e / (LIN_TK / 4), kq = 4 * (e % (LIN_TK / 4));
+      const int64_t m = m0 + rr;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (m < M) {
+        const int64_t src = ids ? ids[m] : m;
+        if (src < 0 || src >= x_rows) {
+          if (kq == 0) hnm_flag(err, HNM_ERR_OOB);
+          v = make_float4(__builtin_nanf(""), __builtin_nanf(""), __builtin_nanf(""),
+                          __builtin_nanf(""));
+        } else {
+          v = *reinterpret_cast<const float4*>(X + src * ldx + k0 + kq);
+        }
+      }
+      float* xr = xs + rr * RS + kq;
+      xr[0] = v.x; xr[1] = v.y; xr[2] = v.z; xr[3] = v.w;
+    }
+    for (int e = t; e < LIN_TN * LIN_TK / 4; e += 256) {
+      const int nn = e / (LIN_TK / 4), kq = 4 * (e % (LIN_TK / 4));
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (n0 + nn < N) v = *reinterpret_cast<const float4*>(W + (int64_t)(n0 + nn) * ldw + k0 + kq);
+      float* wr4 = ws + nn * RS + kq;
+      wr4[0] = v.x; wr4[1] = v.y; wr4[2] = v.z; wr4[3] = v.w;
+    }
+    __syncthreads();
+    const float* xa = xs + (wr + i) * RS + h;  // A[i][h] of step s: row wr + i, k = 2 s + h
+    const float* wb = ws + (wc + i) * RS + h;  // B[h][j = i]: output wc + i, k = 2 s + h
+#pragma unroll
+    for (int st = 0; st < LIN_TK / 2; ++st) acc = mfma32x32x2(xa[2 * st], wb[2 * st], acc);
+    __syncthreads();
+  }
+  const int n = n0 + wc + i;
+  if (n >= N) return;
+  const float bn = bias ? bias[n] : 0.f;
+  const int64_t c = pair_permute ? (int64_t)(n & 1) * (ldy / 2) + (n >> 1) : n;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int64_t m = m0 + wr + mfma32_row(r, h);
+    if (m >= M) continue;
+    float v = acc[r];
+    if (bias) v += bn;
+    Y[m * ldy + c] = v;
+  }
+}
+
 extern "C" hnm_status hnm_linear_rows_f32(hnm_ctx* ctx, const float* X, int64_t ldx,
                                           const int64_t* ids, int64_t x_rows, int64_t M, int K,
                                           const float* W, int64_t ldw, const float* bias, int N,
@@ -436,6 +511,13 @@ extern "C" hnm_status hnm_linear_rows_f32(hnm_ctx* ctx, const float* X, int64_t 
   const int tm = short_in ? 16 : 64;
   const bool vec = K % 4 == 0 && ldx % 4 == 0 && ldw % 4 == 0 && ((uintptr_t)X & 15) == 0 &&
                    ((uintptr_t)W & 15) == 0;
+  if (vec && K % LIN_TK == 0 && !short_in && ctx->linear_mfma) {
+    hipLaunchKernelGGL(linear_rows_mfma_kernel, dim3((unsigned)hnm_cdiv(M, 64), (unsigned)hnm_cdiv(N, LIN_TN)),
+                       dim3(256), 0, ctx->stream, X, ldx, ids, ids ? x_rows : M, M, K, W, ldw, bias,
+                       N, Y, ldy, pair_permute, ctx->err_dev);
+    HNM_LAUNCH_CHECK();
+    return HNM_OK;
+  }
   dim3 grid((unsigned)hnm_cdiv(M, tm), (unsigned)hnm_cdiv(N, LIN_TN));
   auto launch = [&](auto kern) {
     hipLaunchKernelGGL(kern, grid, dim3(256), 0, ctx->stream, X, ldx, ids, ids ? x_rows : M, M,

@@ -30,6 +30,7 @@ struct hnm_ctx {
   int prefilter;                   // HNM_OPT_PREFILTER (default 1)
   int strided;                     // HNM_OPT_STRIDED (default 0)
   int deep_mfma;                   // HNM_OPT_DEEP_MFMA (default 1)
+  int linear_mfma;                 // HNM_OPT_LINEAR_MFMA (default 1)
   void* comm;                      // RCCL communicator (ncclComm_t) of the C-side exchange
   int comm_owned;                  // 1: created by hnm_ctx_rccl_init, destroyed with the ctx
   unsigned long long* stats_dev;   // pre-filter counters: rows, candidates, fallback rows,

@@ -53,7 +53,10 @@ constexpr float CERT_RHO = 0.0029296875f; // 6 u16 = 3 * 2^-10
 constexpr float CERT_RHO_DEEP = 0.00390625f;
 constexpr int CERT_MAX_NP = 64;           // item partitions (candidate segments per row)
 constexpr int CERT_PROXY_USERS = 8;       // batch rows that pick the champion sample
-constexpr int64_t CERT_CHAMPIONS = 2048;  // champion sample size (item groups), at most
+#ifndef CERT_CHAMPIONS_AB  // A/B builds only (tools/build_variant.sh)
+#define CERT_CHAMPIONS_AB 2048
+#endif
+constexpr int64_t CERT_CHAMPIONS = CERT_CHAMPIONS_AB;  // champion sample size (item groups), at most
 constexpr int64_t CERT_GROUP_MIN = 48;    // items per champion group, at least
 // Gated per-user strided sample (round 5).  The champion sample is tight when the rows' best
 // items are shared (init weights at the H&M shape: ~70 candidates a row) and degrades to a

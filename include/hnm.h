@@ -91,7 +91,11 @@ enum { HNM_OPT_PREFILTER = 1,
        HNM_OPT_DEEP_MFMA = 5   /* deep NeuralCF towers (hnm_ncf_deep_*): 1 (default) = the
                                   fp32-MFMA tile kernel where the tower fits it (widths <= 64,
                                   mf <= 128); 0 = the per-pair LDS kernel everywhere (same
-                                  scores bitwise: the A/B and parity switch) */ };
+                                  scores bitwise: the A/B and parity switch) */,
+       HNM_OPT_LINEAR_MFMA = 6 /* hnm_linear_rows_f32 (every per-call layer-1 projection): 1
+                                  (default) = the fp32-MFMA kernel where K % 32 == 0 (exact fp32
+                                  fma chain in k order: bitwise the VALU kernel); 0 = the VALU
+                                  kernel everywhere (the A/B and parity switch) */ };
 hnm_status hnm_ctx_set_option(hnm_ctx* ctx, int option, int64_t value);
 /* Pre-filter counters since the last reset (counted only while HNM_OPT_STATS is 1): out[0]
  * rows scored, out[1] candidates re-scored in fp32, out[2] rows that took the exact fallback

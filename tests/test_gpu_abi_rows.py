@@ -86,6 +86,53 @@ def test_linear_rows(K, N, permute, with_ids, M):
     assert (got[:, untouched] == -3.0).all()
 
 
+@pytest.mark.parametrize("K,N,permute,with_ids,M", [(64, 64, 1, True, 40000), (64, 512, 0, False, 33000),
+                                                    (32, 96, 1, True, 35001), (128, 64, 0, True, 40000)])
+def test_linear_rows_mfma_bitwise_valu(K, N, permute, with_ids, M):
+    """The fp32-MFMA projection (linear_rows_mfma_kernel, HNM_OPT_LINEAR_MFMA, taken for
+    K % 32 == 0 at >= 2 row blocks a CU) is bitwise the VALU kernel's k-ordered fmaf chain --
+    incl. rows of zeros, -0, fp32 denormals and an out-of-range id (NaN row)."""
+    rng = np.random.default_rng(K * N + M)
+    R = 50000
+    X = rng.standard_normal((R, K)).astype(np.float32)
+    X[7] = 0.0
+    X[8] = -0.0
+    X[9] = np.float32(1e-40) * rng.standard_normal(K).astype(np.float32)  # denormals
+    X[10, ::3] = 0.0
+    W = rng.standard_normal((N, 2 * K)).astype(np.float32) * 0.1
+    W[3] = -0.0
+    W[4, :] = np.float32(3e-39)
+    b = rng.standard_normal(N).astype(np.float32)
+    ids = rng.integers(0, R, M).astype(np.int64) if with_ids else None
+    if with_ids:
+        ids[:6] = [7, 8, 9, 10, 7, 8]
+        ids[100] = R  # out of range: NaN row, IndexError at the check
+    ldy = N + (4 if permute else 2)
+    Xt, Wt, bt = (torch.from_numpy(a).to(DEV) for a in (X, W, b))
+    It = torch.from_numpy(ids).to(DEV) if with_ids else None
+    rows = M if with_ids else min(M, R)
+    outs = []
+    try:
+        for opt in (0, 1):
+            _lib.set_option(Xt.device, _lib.HNM_OPT_LINEAR_MFMA, opt)
+            Y = torch.full((rows, ldy), -3.0, device=DEV)
+            _lib.check(_lib.fn("hnm_linear_rows_f32")(_c(Xt), _lib.ptr(Xt), K, _lib.ptr(It), R, rows,
+                                                      K, _lib._p(Wt.data_ptr() + 4 * K), 2 * K,
+                                                      _lib.ptr(bt), N, _lib.ptr(Y), ldy, permute),
+                       "linear_rows")
+            if with_ids:
+                with pytest.raises(IndexError):
+                    _lib.sync_check(Xt.device)
+            else:
+                _lib.sync_check(Xt.device)
+            outs.append(Y.cpu().numpy())
+    finally:
+        _lib.set_option(Xt.device, _lib.HNM_OPT_LINEAR_MFMA, 1)
+    assert np.array_equal(outs[0].view(np.uint32), outs[1].view(np.uint32))
+    if with_ids:
+        assert np.isnan(outs[1][100, :N if not permute else N // 2]).all()
+
+
 def test_linear_rows_oob():
     X = torch.randn(100, 16, device=DEV)
     W = torch.randn(8, 16, device=DEV)
