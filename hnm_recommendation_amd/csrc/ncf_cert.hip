@@ -1274,8 +1274,13 @@ __global__ __launch_bounds__(1024) void cert_gate_kernel(
 // relu(acc + b2); layer 3 the same way over l = 2s + h with W3 row m on A row mfma32_row(m, 0)
 // (so lane half 0 holds every unit of a candidate), relu(acc + b3); then in lane half 0 ONE fmaf
 // chain over the GMF terms wp_j (g_u,j g_i,j) and the units' wp3_m z_m, + bp.
+#ifndef RESCORE_PERSIST  // A/B builds only (tools/build_variant.sh)
 #define RESCORE_PERSIST 3
-constexpr int RESCORE_BEST_FIRST = 96;  // rows with more candidates score the best 64 first
+#endif
+#ifndef RESCORE_BEST_FIRST_AB
+#define RESCORE_BEST_FIRST_AB 96
+#endif
+constexpr int RESCORE_BEST_FIRST = RESCORE_BEST_FIRST_AB;  // rows with more candidates score the best 64 first
 template <bool DEEP>
 __global__ __launch_bounds__(256, DEEP ? 2 : 3) void ncf_rescore_kernel(
     NcfTabs t, int mf, const float* __restrict__ W2, int h1, int h2, const float* __restrict__ b2,
