@@ -43,20 +43,22 @@ constexpr float DCERT_RHO = 0.00146484375f;  // 3 u16 = 3 * 2^-11
 constexpr int DCERT_MAX_NP = 64;
 constexpr int DCERT_USER_BLOCKS = 2048;  // dcert_stats_kernel user blocks (4 waves x 4 rows), at most
 
-// user blocks of 32 per scan wave (each item fragment feeds NB MFMAs), per DP.  Round 4 A/B
-// (MF d=64 step / THRESH scan, one box): NB = 1 0.1827 / 0.0835 ms, NB = 2 at 2 workgroups per
-// CU 0.1845 / 0.0866 (half the LDS fragment reads did not pay for the lost occupancy), the
-// sample pass at NB = 2 0.2011 (its running max then costs 3 instructions a value); round 3's
-// 64-bit tile addressing 0.1872 / 0.0886
+// user blocks of 32 per scan wave (each item fragment feeds NB MFMAs).  Round 4 A/B (MF d=64
+// step / THRESH scan, one box): NB = 1 0.1827 / 0.0835 ms, NB = 2 at 2 workgroups per CU
+// 0.1845 / 0.0866, the sample pass at NB = 2 0.2011 (its running max then costs 3 instructions
+// a value); round 3's 64-bit tile addressing 0.1872 / 0.0886.  Round 6: the THRESH scan at
+// NB = 2 now fits three workgroups per CU in 168 VGPRs without spills where DP = 64 and no
+// filter is applied: half the LDS fragment reads and half the L2 tile traffic per MFMA, MF scan
+// 0.0853-0.0877 -> 0.0773-0.0805 ms, step 0.181-0.186 -> 0.172-0.178 ms
+// (profiles/r10k_dot_nb2_ab.txt); the masked and DP = 128 variants spill at NB = 2 (filtered
+// LightGCN -3 %) and the sample pass at NB = 2 is slower (44 vs 39.5 us): both stay at NB = 1.
 enum { DSCAN_DENSE = 0, DSCAN_THRESH = 1, DSCAN_SAMPLE = 2 };  // scan modes (below)
-// (the kernel keeps its NB template parameter; every product launch uses NB = 1)
-__host__ __device__ constexpr int dscan_nb(int DP, int MODE) { return 1; }
-__host__ __device__ constexpr int dscan_users(int DP, int MODE) { return 128 * dscan_nb(DP, MODE); }
-// scan occupancy (workgroups per CU): NB = 1, two sub-tiles in flight, fits 3 in 168 VGPRs;
-// NB = 2 (two user blocks' A operands and thresholds) needs ~230: 2
-// Round 4 A/B (MF step / THRESH scan): 3 workgroups per CU 0.1805 / 0.0832 ms, 2 per CU
-// 0.1911 / 0.0953; 64-item tiles 0.1804 / 0.0859; 256-item tiles at 2 per CU 0.1899 / 0.0923
-__host__ __device__ constexpr int dcert_wg_per_cu(int NB) { return NB == 2 ? 2 : 3; }
+// scan occupancy (workgroups per CU): three at NB = 1 and NB = 2 (168 VGPRs).  Round 4 A/B (MF
+// step / THRESH scan): 3 workgroups per CU 0.1805 / 0.0832 ms, 2 per CU 0.1911 / 0.0953; 64-item
+// tiles 0.1804 / 0.0859; 256-item tiles at 2 per CU 0.1899 / 0.0923
+__host__ __device__ constexpr int dcert_wg_per_cu(int NB) { return 3; }
+// the main scan's NB for a call (host): unfiltered calls at DP = 64
+static inline int dscan_thresh_nb(int d, bool masked) { return d <= 64 && !masked ? 2 : 1; }
 
 enum { DM_U, DM_I, DM_NI, DM_IB, DM_N };
 
@@ -98,9 +100,10 @@ struct DotCertWs {
 struct DotCertShape {
   int DP;
   int64_t stride, Ns;
-  Partition spart;  // of the sample pass
-  Partition part;   // of the main scan
+  Partition spart;  // of the sample pass (NB = 1)
+  Partition part;   // of the main scan (NB = nb)
   int capp;
+  int nb;
 };
 
 Partition xcd_partition(int64_t I, int64_t ublocks, int num_cus, int NB) {
@@ -114,22 +117,24 @@ Partition xcd_partition(int64_t I, int64_t ublocks, int num_cus, int NB) {
   return {(int)hnm_cdiv(I, ipp), ipp};
 }
 
-DotCertShape dcert_shape(int64_t B, int64_t I, int d, int K, int num_cus) {
+DotCertShape dcert_shape(int64_t B, int64_t I, int d, int K, int num_cus, int nb = 1) {
   DotCertShape sh;
   sh.DP = d <= 64 ? 64 : 128;
+  sh.nb = nb;
   sh.stride = std::max<int64_t>(DCERT_MIN_STRIDE, I / DCERT_SAMPLE);  // sample <= 1/stride of the items
   sh.Ns = hnm_cdiv(I, sh.stride);
-  sh.part = xcd_partition(I, hnm_cdiv(B, dscan_users(sh.DP, DSCAN_THRESH)), num_cus,
-                          dscan_nb(sh.DP, DSCAN_THRESH));
-  sh.spart = xcd_partition(sh.Ns, hnm_cdiv(B, dscan_users(sh.DP, DSCAN_SAMPLE)), num_cus,
-                           dscan_nb(sh.DP, DSCAN_SAMPLE));
+  sh.part = xcd_partition(I, hnm_cdiv(B, 128 * nb), num_cus, nb);
+  sh.spart = xcd_partition(sh.Ns, hnm_cdiv(B, 128), num_cus, 1);
   const int64_t total = std::min<int64_t>(8192, std::max<int64_t>(256, 8 * (int64_t)K * sh.stride));
   sh.capp = (int)std::max<int64_t>(32, std::min<int64_t>(total, hnm_cdiv(4 * total, sh.part.np)));
   return sh;
 }
 
-size_t dcert_carve(char* base, int64_t B, int64_t I, int d, int K, int num_cus, DotCertWs* w) {
-  const DotCertShape sh = dcert_shape(B, I, d, K, num_cus);
+// the main scan's segments (cnt, buf: sized by its NB) come last, so the begin phase's tables
+// sit at the same offsets whichever NB the finish phase takes (its own filter decides)
+size_t dcert_carve(char* base, int64_t B, int64_t I, int d, int K, int num_cus, DotCertWs* w,
+                   int nb = 1) {
+  const DotCertShape sh = dcert_shape(B, I, d, K, num_cus, nb);
   size_t off = 0;
   auto take = [&](size_t bytes) {
     char* p = base ? base + off : nullptr;
@@ -148,17 +153,17 @@ size_t dcert_carve(char* base, int64_t B, int64_t I, int d, int K, int num_cus, 
   x.kthv = (float*)take((size_t)B * K * 4);
   x.lb = (float*)take((size_t)B * 4);
   x.kthi = (int64_t*)take((size_t)B * K * 8);
-  x.cnt = (int*)take((size_t)B * sh.part.np * 4);
   x.flag = (int*)take(B * 4);
   x.ovf_cnt = (int32_t*)take(256);
   x.ovf_rows = (int32_t*)take(B * 4);
-  x.buf = (int32_t*)take((size_t)B * sh.part.np * sh.capp * 4);
   x.sdense = (float*)take((size_t)B * sh.spart.np * 32 * 4);
   x.U16 = (_Float16*)take((size_t)B * sh.DP * 2);
   x.I16 = (_Float16*)take((size_t)I * sh.DP * 2);
   const size_t lb = list_cand_bytes(B, I, K, num_cus);
   x.cv = (float*)take(lb);
   x.ci = (int32_t*)take(lb);
+  x.cnt = (int*)take((size_t)B * sh.part.np * 4);
+  x.buf = (int32_t*)take((size_t)B * sh.part.np * sh.capp * 4);
   if (w) *w = x;
   return off;
 }
@@ -894,14 +899,18 @@ hnm_status dcert_prepare(hnm_ctx* ctx, const DotArgs& a, const DotCertShape& sh,
 }
 
 template <int MODE>
-void launch_dscan(hnm_ctx* ctx, dim3 grid, const DScanArgs& s, int DP, bool bias) {
+void launch_dscan(hnm_ctx* ctx, dim3 grid, const DScanArgs& s, int DP, bool bias, int nb = 1) {
+  // NB = 2: the unfiltered DP = 64 main scan only (dscan_thresh_nb)
 #define HNM_DS2(DPV, BV)                                                                      \
   if (s.mptr && MODE != DSCAN_DENSE)                                                          \
-    hipLaunchKernelGGL((dot16_scan_kernel<DPV, MODE, BV, MODE != DSCAN_DENSE, dscan_nb(DPV, MODE)>), \
+    hipLaunchKernelGGL((dot16_scan_kernel<DPV, MODE, BV, MODE != DSCAN_DENSE, 1>), grid,       \
+                       dim3(256), 0, ctx->stream, s);                                         \
+  else if (MODE == DSCAN_THRESH && DPV == 64 && nb == 2)                                      \
+    hipLaunchKernelGGL((dot16_scan_kernel<DPV, MODE, BV, false, (MODE == DSCAN_THRESH && DPV == 64) ? 2 : 1>), \
                        grid, dim3(256), 0, ctx->stream, s);                                   \
   else                                                                                        \
-    hipLaunchKernelGGL((dot16_scan_kernel<DPV, MODE, BV, false, dscan_nb(DPV, MODE)>), grid,        \
-                       dim3(256), 0, ctx->stream, s);
+    hipLaunchKernelGGL((dot16_scan_kernel<DPV, MODE, BV, false, 1>), grid, dim3(256), 0,       \
+                       ctx->stream, s);
 #define HNM_DS(DPV)    \
   if (bias) {          \
     HNM_DS2(DPV, true) \
@@ -937,7 +946,8 @@ bool dot_cert_eligible(int d, int64_t I, int K) {
 }
 
 size_t dot_cert_bytes(int64_t B, int64_t I, int d, int K, int num_cus) {
-  return dcert_carve(nullptr, B, I, d, K, num_cus, nullptr);
+  return std::max(dcert_carve(nullptr, B, I, d, K, num_cus, nullptr, 1),
+                  dcert_carve(nullptr, B, I, d, K, num_cus, nullptr, 2));
 }
 
 // Phase 1: bound statistics, f16 copies, the sample pass and every row's certified lower
@@ -949,7 +959,7 @@ static hnm_status dot_cert_begin_impl(hnm_ctx* ctx, const DotArgs& a, bool bias,
   dcert_carve((char*)scratch, a.B, a.I, a.d, a.K, ctx->num_cus, &x);
   hnm_status st = dcert_prepare(ctx, a, sh, x);
   if (st) return st;
-  const int64_t ublocks = hnm_cdiv(a.B, dscan_users(sh.DP, DSCAN_SAMPLE));
+  const int64_t ublocks = hnm_cdiv(a.B, (int64_t)128);  // the sample pass: NB = 1
   DScanArgs s = dscan_args(x, a);
   s.I = sh.Ns;
   s.istride = sh.stride;
@@ -988,10 +998,11 @@ hnm_status dot_cert_begin(hnm_ctx* ctx, const DotArgs& a, bool bias, void* scrat
 static hnm_status dot_cert_finish_impl(hnm_ctx* ctx, const DotArgs& a, bool bias, void* scratch,
                                        const float* lb, int short_ok, float* ov, int64_t* oi,
                                        bool fused) {
-  const DotCertShape sh = dcert_shape(a.B, a.I, a.d, a.K, ctx->num_cus);
+  const int nb = dscan_thresh_nb(a.d, a.mptr != nullptr);
+  const DotCertShape sh = dcert_shape(a.B, a.I, a.d, a.K, ctx->num_cus, nb);
   DotCertWs x;
-  dcert_carve((char*)scratch, a.B, a.I, a.d, a.K, ctx->num_cus, &x);
-  const int64_t ublocks = hnm_cdiv(a.B, dscan_users(sh.DP, DSCAN_THRESH));
+  dcert_carve((char*)scratch, a.B, a.I, a.d, a.K, ctx->num_cus, &x, nb);
+  const int64_t ublocks = hnm_cdiv(a.B, (int64_t)128 * nb);
   if (fused)
     hipLaunchKernelGGL(dcert_bound_tau_kernel, dim3((unsigned)hnm_cdiv(a.B, 256)), dim3(256), 0,
                        ctx->stream, x.kthv, a.K, x.Nu, x.ubr, x.prm, a.B, x.tau, x.flag);
@@ -1011,7 +1022,8 @@ static hnm_status dot_cert_finish_impl(hnm_ctx* ctx, const DotArgs& a, bool bias
     s.ipp = sh.part.ipp;
     s.NP = sh.part.np;
     hnm_timer_begin(ctx, HNM_TIME_SCORE);
-    launch_dscan<DSCAN_THRESH>(ctx, dim3((unsigned)sh.part.np, (unsigned)ublocks), s, sh.DP, bias);
+    launch_dscan<DSCAN_THRESH>(ctx, dim3((unsigned)sh.part.np, (unsigned)ublocks), s, sh.DP, bias,
+                               nb);
     hnm_timer_end(ctx, HNM_TIME_SCORE);
     HNM_LAUNCH_CHECK();
   }
@@ -1058,8 +1070,8 @@ hnm_status dot_cert_debug(hnm_ctx* ctx, const DotArgs& a, bool bias, void* scrat
   s.I = a.I;
   s.dense = approx;
   s.ldo = lda;
-  const int64_t ublocks = hnm_cdiv(a.B, dscan_users(sh.DP, DSCAN_DENSE));
-  const Partition ps = xcd_partition(a.I, ublocks, ctx->num_cus, dscan_nb(sh.DP, DSCAN_DENSE));
+  const int64_t ublocks = hnm_cdiv(a.B, (int64_t)128);
+  const Partition ps = xcd_partition(a.I, ublocks, ctx->num_cus, 1);
   s.ipp = ps.ipp;
   s.NP = ps.np;
   launch_dscan<DSCAN_DENSE>(ctx, dim3((unsigned)ps.np, (unsigned)ublocks), s, sh.DP,
