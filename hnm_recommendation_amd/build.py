@@ -17,7 +17,7 @@ BUILD = os.path.join(REPO, "build", "obj")
 LIB = os.path.join(PKG, "libhnm_mi355x.so")
 SOURCES = ["api.hip", "score.hip", "dot_cert.hip", "ncf.hip", "ncf_cert.hip", "ncf_deep.hip", "graph.hip",
            "widedeep.hip", "eval.hip", "topk_sort.hip", "collective.hip"]
-HEADERS = ["hnm_device.h", "hnm_internal.h", "dot_internal.h", "ncf_internal.h"]
+HEADERS = ["hnm_device.h", "hnm_internal.h", "dot_internal.h", "ncf_internal.h", "sample_kth.h"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-Wall",
          "-Wno-unused-function", "-Wno-unused-variable", "-Wno-unused-but-set-variable"]

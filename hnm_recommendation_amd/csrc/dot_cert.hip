@@ -27,6 +27,7 @@
 
 #include "dot_internal.h"
 #include "hnm_device.h"
+#include "sample_kth.h"
 
 typedef _Float16 h8 __attribute__((ext_vector_type(8)));
 
@@ -714,30 +715,30 @@ __global__ __launch_bounds__(256) void dcert_tau_kernel(const float* __restrict_
 }
 
 // One-shot calls (dot_cert_topk): dcert_bound_kernel's lower bound and dcert_tau_kernel's
-// threshold in one pass per row -- the same arithmetic, L kept in a register (one launch and one
-// kernel boundary less on the per-call latency chain).
-__global__ __launch_bounds__(256) void dcert_bound_tau_kernel(const float* __restrict__ kth,
-                                                              int K,
-                                                              const float* __restrict__ Nu,
-                                                              const float* __restrict__ ubr,
-                                                              const DParams* __restrict__ prm,
-                                                              int64_t B, float* __restrict__ tau,
-                                                              int* __restrict__ flag) {
-  const int64_t b = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (b >= B) return;
-  const float s = prm->s;
-  const float nimax = __uint_as_float(prm->mx[DM_NI]), ibmax = __uint_as_float(prm->mx[DM_IB]);
-  const float E = s * (DCERT_RHO * Nu[b] * nimax + 2.4e-7f * (fabsf(ubr[b]) + ibmax)) + prm->absb;
-  float l = (kth[b * K + (K - 1)] - E) / s + ubr[b];
-  l -= fabsf(l) * 4.76837158203125e-07f;  // 2^-21
-  if (!(!prm->bad && __builtin_isfinite(l) && __builtin_isfinite(E))) l = -__builtin_inff();
-  const float scale = s * (Nu[b] * nimax + fabsf(ubr[b]) + ibmax);
-  float tv = (l - ubr[b]) * s - E - 3.814697265625e-06f * scale;  // 2^-18
-  tv -= fabsf(tv) * 9.5367431640625e-07f;                          // 2^-20
-  const bool ok = !prm->bad && __builtin_isfinite(tv) && __builtin_isfinite(scale);
-  tau[b] = ok ? tv : __builtin_inff();
-  flag[b] = ok ? 0 : 1;
-}
+// threshold per row in the epilogue of the sample K-th launch -- the same arithmetic, L kept in
+// a register (round 5 fused the two into one kernel after the K-th; round 6 folds that kernel
+// into the K-th launch: one launch and one kernel boundary less on the per-call latency chain).
+struct DotTauEpi {
+  const DParams* prm;
+  const float* Nu;
+  const float* ubr;
+  float* tau;
+  int* flag;
+  __device__ void operator()(int64_t b, float kv) const {
+    const float s = prm->s;
+    const float nimax = __uint_as_float(prm->mx[DM_NI]), ibmax = __uint_as_float(prm->mx[DM_IB]);
+    const float E = s * (DCERT_RHO * Nu[b] * nimax + 2.4e-7f * (fabsf(ubr[b]) + ibmax)) + prm->absb;
+    float l = (kv - E) / s + ubr[b];
+    l -= fabsf(l) * 4.76837158203125e-07f;  // 2^-21
+    if (!(!prm->bad && __builtin_isfinite(l) && __builtin_isfinite(E))) l = -__builtin_inff();
+    const float scale = s * (Nu[b] * nimax + fabsf(ubr[b]) + ibmax);
+    float tv = (l - ubr[b]) * s - E - 3.814697265625e-06f * scale;  // 2^-18
+    tv -= fabsf(tv) * 9.5367431640625e-07f;                          // 2^-20
+    const bool ok = !prm->bad && __builtin_isfinite(tv) && __builtin_isfinite(scale);
+    tau[b] = ok ? tv : __builtin_inff();
+    flag[b] = ok ? 0 : 1;
+  }
+};
 
 // ------------------------------------------------------------------ exact re-scoring
 // One wave per user; each lane re-scores one candidate with the sequential fp32 fma chain
@@ -972,10 +973,12 @@ static hnm_status dot_cert_begin_impl(hnm_ctx* ctx, const DotArgs& a, bool bias,
   launch_dscan<DSCAN_SAMPLE>(ctx, dim3((unsigned)sh.spart.np, (unsigned)ublocks), s, sh.DP, bias);
   HNM_LAUNCH_CHECK();
   const int64_t nmax_cols = (int64_t)sh.spart.np * 32;
+  if (fused)  // the one-shot call: bound + threshold in the K-th launch's epilogue
+    return sample_kth_launch(ctx, x.sdense, nmax_cols, a.B, nmax_cols, nullptr, nullptr, a.K, 1, 1,
+                             nullptr, x.kthv, nullptr, DotTauEpi{x.prm, x.Nu, x.ubr, x.tau, x.flag});
   st = hnm_sample_kth(ctx, x.sdense, nmax_cols, a.B, nmax_cols, nullptr, nullptr, a.K, 1, 1,
                       nullptr, x.kthv);
   if (st) return st;
-  if (fused) return HNM_OK;  // bound + threshold in dot_cert_finish_impl's first kernel
   hipLaunchKernelGGL(dcert_bound_kernel, dim3((unsigned)hnm_cdiv(a.B, 256)), dim3(256), 0,
                      ctx->stream, x.kthv, a.K, x.Nu, x.ubr, x.prm, a.B, lb ? lb : x.lb, x.E);
   HNM_LAUNCH_CHECK();
@@ -994,7 +997,7 @@ hnm_status dot_cert_begin(hnm_ctx* ctx, const DotArgs& a, bool bias, void* scrat
 
 // Phase 2: thresholds from lower bounds lb (this call's, or the max over item shards), the
 // main f16 scan, exact re-scoring + top-K, the exact LIST scan for unusable rows.  fused: the
-// one-shot call, thresholds straight from the sample K-th (dcert_bound_tau_kernel).
+// one-shot call, thresholds already written by the sample K-th launch (DotTauEpi).
 static hnm_status dot_cert_finish_impl(hnm_ctx* ctx, const DotArgs& a, bool bias, void* scratch,
                                        const float* lb, int short_ok, float* ov, int64_t* oi,
                                        bool fused) {
@@ -1003,13 +1006,11 @@ static hnm_status dot_cert_finish_impl(hnm_ctx* ctx, const DotArgs& a, bool bias
   DotCertWs x;
   dcert_carve((char*)scratch, a.B, a.I, a.d, a.K, ctx->num_cus, &x, nb);
   const int64_t ublocks = hnm_cdiv(a.B, (int64_t)128 * nb);
-  if (fused)
-    hipLaunchKernelGGL(dcert_bound_tau_kernel, dim3((unsigned)hnm_cdiv(a.B, 256)), dim3(256), 0,
-                       ctx->stream, x.kthv, a.K, x.Nu, x.ubr, x.prm, a.B, x.tau, x.flag);
-  else
+  if (!fused) {  // fused: tau / flag came with the sample K-th (DotTauEpi)
     hipLaunchKernelGGL(dcert_tau_kernel, dim3((unsigned)hnm_cdiv(a.B, 256)), dim3(256), 0,
                        ctx->stream, lb ? lb : x.lb, x.Nu, x.ubr, x.prm, a.B, x.tau, x.flag);
-  HNM_LAUNCH_CHECK();
+    HNM_LAUNCH_CHECK();
+  }
   {  // main f16 scan: append approx >= tau_u
     DScanArgs s = dscan_args(x, a);
     s.I = a.I;

@@ -37,6 +37,7 @@
 
 #include "hnm_device.h"
 #include "ncf_internal.h"
+#include "sample_kth.h"
 
 typedef _Float16 h8 __attribute__((ext_vector_type(8)));
 typedef _Float16 h4 __attribute__((ext_vector_type(4)));
@@ -1016,6 +1017,37 @@ __global__ __launch_bounds__(256) void cert_tau_kernel(const float* __restrict__
   flag[b] = ok ? 0 : 1;
 }
 
+// One-shot calls (ncf_cert_topk, the deep towers' certified call): cert_bound_kernel's lower
+// bound and cert_tau_kernel's threshold per row in the epilogue of the champion sample's K-th
+// launch (round 6) -- the same arithmetic (L stored and reused as a register: bit for bit),
+// two launches and kernel boundaries less on the per-call latency chain.  Not with the gated
+// strided sample (its K-th comes from a second launch).
+struct NcfBoundTauEpi {
+  const CertParams* prm;
+  const float* Au;
+  const float* Cu;
+  const float* bp;
+  float* Eu;
+  float* lb;
+  float* tau;
+  int* flag;
+  __device__ void operator()(int64_t b, float kv) const {
+    const float unit = prm->unit;
+    const float e = unit * (prm->rho * (prm->c0 + Au[b]) + prm->absb);
+    Eu[b] = e;
+    float l = (kv - e) / unit + bp[0];
+    l -= fabsf(l) * 4.76837158203125e-07f;  // 2^-21
+    l = (!prm->bad && __builtin_isfinite(l) && __builtin_isfinite(e)) ? l : -__builtin_inff();
+    lb[b] = l;
+    const float scale = unit * (prm->c0 + Au[b] + prm->Bmax + Cu[b] * prm->Dmax);
+    float tv = (l - bp[0]) * unit - e - 3.814697265625e-06f * scale;  // 2^-18
+    tv -= fabsf(tv) * 9.5367431640625e-07f;                           // 2^-20
+    const bool ok = !prm->bad && __builtin_isfinite(tv) && __builtin_isfinite(scale);
+    tau[b] = ok ? tv : __builtin_inff();
+    flag[b] = ok ? 0 : 1;
+  }
+};
+
 // Champion sample: items split into nch contiguous groups of gsz; each group's item with the
 // best mean (approx - e_i) over the proxy rows (the first users of the batch) -- a
 // popularity-like sample in increasing item order.  Any item subset gives a valid lower
@@ -1881,6 +1913,13 @@ hnm_status ncf_cert_begin(hnm_ctx* ctx, const hnm_ncf_weights* w, const NcfTabs&
   launch_scan<SCAN_SAMPLE>(ctx, dim3((unsigned)c.NP, (unsigned)ublocks), c);
   if (gated) HNM_HIP_CHECK(hipStreamWaitEvent(ctx->stream, ctx->side_out, 0));  // join
   HNM_LAUNCH_CHECK();
+  // one-shot call (no bound out, no lists, no strided sample): bound + threshold fused into the
+  // K-th launch; ncf_cert_finish then skips cert_tau_kernel (same condition there)
+  const bool fuse = lb == nullptr && lists == nullptr && !strided;
+  if (fuse)
+    return sample_kth_launch(ctx, x.cdense, sh.nch, B, sh.nch, mptr, midx, K, 1, 1, x.sidx, x.kthv,
+                             nullptr, NcfBoundTauEpi{x.prm, x.Au, x.Cu, w->bp, x.Eu, x.lb, x.tau,
+                                                     x.flag});
   st = hnm_sample_kth(ctx, x.cdense, sh.nch, B, sh.nch, mptr, midx, K, 1, 1, x.sidx, x.kthv);
   if (st) return st;
   // gated strided sample: every row against one tile in CERT_STRIDE (exits when gated off)
@@ -1925,9 +1964,12 @@ hnm_status ncf_cert_finish(hnm_ctx* ctx, const hnm_ncf_weights* w, const NcfTabs
   CertWs x;
   cert_carve((char*)scratch, B, I, K, ctx->num_cus, wg, strided, &x);
   const int64_t ublocks = hnm_cdiv(B, 128);
-  hipLaunchKernelGGL(cert_tau_kernel, dim3((unsigned)hnm_cdiv(B, 256)), dim3(256), 0,
-                     ctx->stream, lb ? lb : x.lb, x.Au, x.Cu, x.Eu, x.prm, w->bp, B, x.tau, x.flag);
-  HNM_LAUNCH_CHECK();
+  if (lb != nullptr || strided) {  // else tau / flag came with the begin phase's K-th
+    hipLaunchKernelGGL(cert_tau_kernel, dim3((unsigned)hnm_cdiv(B, 256)), dim3(256), 0,
+                       ctx->stream, lb ? lb : x.lb, x.Au, x.Cu, x.Eu, x.prm, w->bp, B, x.tau,
+                       x.flag);
+    HNM_LAUNCH_CHECK();
+  }
   // main f16 scan: append items with approx + e >= tau_u to per-partition segments
   ScanArgs a = scan_args(x, B, dp != nullptr);
   a.I = I;
