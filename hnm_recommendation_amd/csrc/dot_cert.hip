@@ -39,7 +39,10 @@ constexpr int64_t DCERT_MIN_ITEMS = 8192;
 // step is the same for 4 and 2 (the sample pass grows by what the scan saves), 10 % shorter
 // than stride 8 once the sample pass's max runs as one v_max3 per row and sub-tile pair.
 constexpr int64_t DCERT_SAMPLE = 52771;  // sampled items: stride max(DCERT_MIN_STRIDE, I / this)
-constexpr int64_t DCERT_MIN_STRIDE = 2;
+#ifndef DCERT_MIN_STRIDE_AB  // A/B builds only (tools/build_variant.sh)
+#define DCERT_MIN_STRIDE_AB 2
+#endif
+constexpr int64_t DCERT_MIN_STRIDE = DCERT_MIN_STRIDE_AB;
 constexpr float DCERT_RHO = 0.00146484375f;  // 3 u16 = 3 * 2^-11
 constexpr int DCERT_MAX_NP = 64;
 constexpr int DCERT_USER_BLOCKS = 2048;  // dcert_stats_kernel user blocks (4 waves x 4 rows), at most
