@@ -38,9 +38,12 @@ constexpr int64_t DCERT_MIN_ITEMS = 8192;
 // candidates a row, scan 0.105 ms; stride 4 -> 55, 0.096 ms; stride 2 -> 28, 0.087 ms -- the
 // step is the same for 4 and 2 (the sample pass grows by what the scan saves), 10 % shorter
 // than stride 8 once the sample pass's max runs as one v_max3 per row and sub-tile pair.
-constexpr int64_t DCERT_SAMPLE = 52771;  // sampled items: stride max(DCERT_MIN_STRIDE, I / this)
+// Round 6, with the two-block main scan (profiles/r10p_dot_sample_stride_ab.txt, MF step, three
+// interleaved rounds): stride 2 0.1767-0.1825 ms (27.6 candidates a row), 3 0.1755-0.1780 (40.7),
+// 4 0.1776-0.1801 (55.3): stride 3.
+constexpr int64_t DCERT_SAMPLE = 35181;  // sampled items: stride max(DCERT_MIN_STRIDE, I / this)
 #ifndef DCERT_MIN_STRIDE_AB  // A/B builds only (tools/build_variant.sh)
-#define DCERT_MIN_STRIDE_AB 2
+#define DCERT_MIN_STRIDE_AB 3
 #endif
 constexpr int64_t DCERT_MIN_STRIDE = DCERT_MIN_STRIDE_AB;
 constexpr float DCERT_RHO = 0.00146484375f;  // 3 u16 = 3 * 2^-11
