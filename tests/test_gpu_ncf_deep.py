@@ -10,7 +10,7 @@ scored as neural_cf.py:131-141 and ranked as neural_cf.py:300-326).
   inside the library) gives the same lists; item shards (sharding.ncf_deep_shard_topk) merge to
   the unsharded lists.
 * Rows against the CPU oracle (oracle/hnm_oracle.py ncf_predict_all_items) within the fp32
-  tolerance of tests/parity.py.
+  tolerance of tests/parity.py: every row at B = 37, every 4th at B = 300, 17 full-catalogue rows.
 """
 import numpy as np
 import pytest
@@ -70,7 +70,8 @@ def test_deep_mfma_bitwise_and_fused_topk(mf, dims, B):
     slow = per_pair(lambda: m.predict_all_items(users))
     assert torch.equal(fast.view(torch.int32), slow.view(torch.int32)), "MFMA vs per-pair"
     dense = fast.cpu().numpy()
-    rows = [0, B // 2, B - 1]
+    # every row (B = 37) / every 4th row and the last (B = 300) against the oracle
+    rows = list(range(B)) if B <= 64 else list(range(0, B, 4)) + [B - 1]
     assert_scores_close(dense[rows], O.ncf_predict_all_items(sd, users_np[rows]), "deep oracle")
 
     ref_i, ref_v = topk_order(dense, K)
@@ -122,7 +123,7 @@ def test_deep_mfma_full_catalogue_topk():
     assert torch.equal(i, i2) and torch.equal(v.view(torch.int32), v2.view(torch.int32))
     v3, i3 = m.recommend_with_scores(users)
     assert torch.equal(i, i3) and torch.equal(v.view(torch.int32), v3.view(torch.int32))
-    rows = [0, 255, 511]
+    rows = list(range(0, 512, 32)) + [511]  # 17 rows x 105,542 items
     ref = O.ncf_predict_all_items(sd, users_np[rows])
     got = m.predict_all_items(users[rows]).cpu().numpy()
     assert_scores_close(got, ref, "deep full-catalogue rows")
