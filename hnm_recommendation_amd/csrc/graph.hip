@@ -49,6 +49,11 @@
 // step ahead 1.415 / 2.920, 8 entries 1.435 / 3.017), pieces cut for ~WALK_GROUPS_TARGET groups
 #define WALK_THREADS 1024
 #define WALK_WIN 16
+// d >= 128 (512-B rows): more, narrower windows (round 6, A/B on one box, configs[4] d = 128
+// step: 16 windows 7.09 ms, 24: 7.01, 32: 7.02, 64: 7.29; the d = 64 step: 8: 3.47, 16: 3.49,
+// 32: 3.58 -- profiles/r11d_spmm_windows_ab.txt)
+#define WALK_WIN_WIDE 24
+static inline int walk_windows(int d) { return d >= 128 ? WALK_WIN_WIDE : WALK_WIN; }
 #define WALK_STEP 4
 #define WALK_LDS_F4 9216
 #define WALK_GROUPS_TARGET 16384
@@ -545,7 +550,7 @@ template <int LPR>
 __global__ __launch_bounds__(WALK_THREADS) void spmm_walk_kernel(
     const int64_t* __restrict__ gptr, const uint32_t* __restrict__ ent,
     const float* __restrict__ wt, const int32_t* __restrict__ slot_out,
-    const int32_t* __restrict__ nslot, int maxloc, const float* __restrict__ X, int d,
+    const int32_t* __restrict__ nslot, int maxloc, int nwin, const float* __restrict__ X, int d,
     float* __restrict__ partial, SpmmEpi ep, int64_t r0, int64_t r1) {
   constexpr int NG = WALK_THREADS / LPR;
   __shared__ float4 acc[WALK_LDS_F4];
@@ -554,7 +559,7 @@ __global__ __launch_bounds__(WALK_THREADS) void spmm_walk_kernel(
   for (int i = tid; i < ns * LPR; i += WALK_THREADS) acc[i] = make_float4(0.f, 0.f, 0.f, 0.f);
   __syncthreads();
   // WALK_STEP entries per step (round 3: 2: 1.741 ms per d=64 layer, 4: 1.694, 8: 1.848)
-  constexpr int K = WALK_WIN;
+  const int K = nwin;  // column windows (walk_windows)
   constexpr int ST = WALK_STEP;
   auto consume = [&](const uint32_t* c, const float* w) {
     float4 x[ST];
@@ -951,8 +956,8 @@ __global__ __launch_bounds__(256) void spmm_rows_combine_kernel(
 
 // ---------------------------------------------------------------- walk schedules (host)
 struct WalkSched {
-  int lpr, ng, nwg, maxloc;
-  int64_t* gptr;       // [nwg * ng * K + 1] (K column windows per group list, WALK_WIN)
+  int lpr, ng, nwg, maxloc, nwin;
+  int64_t* gptr;       // [nwg * ng * nwin + 1] (nwin column windows per group list)
   uint32_t* ent;       // [walk_nnz] col << 10 | slot
   float* wt;
   int32_t* slot_out;   // [nwg * maxloc]: row (unsplit piece) or -(partial index) - 1
@@ -1142,9 +1147,8 @@ static hnm_status plan_bind(hnm_ctx* ctx, hnm_spmm_plan* pl, const int32_t* col,
 // order inside each piece (and so every result) is fixed by the pieces themselves.
 static hnm_status walk_build(hnm_spmm_plan* pl, int d, WalkSched** out) {
   const int lpr = d / 4, ng = WALK_THREADS / lpr;
-  // WALK_WIN > 1: slot maxloc absorbs the windows' padding entries (never stored)
-  const int maxloc = WALK_WIN > 1 ? std::min(1022, WALK_LDS_F4 / lpr - 1)
-                                  : std::min(1023, WALK_LDS_F4 / lpr);
+  // slot maxloc absorbs the windows' padding entries (never stored)
+  const int maxloc = std::min(1022, WALK_LDS_F4 / lpr - 1);
   const std::vector<int64_t>& rp = *pl->h_rowptr;
   const std::vector<int32_t>& wr = *pl->h_walk_rows;
   const int64_t cap = pl->walk_cap, T = pl->walk_nnz;
@@ -1209,9 +1213,9 @@ static hnm_status walk_build(hnm_spmm_plan* pl, int d, WalkSched** out) {
       slot_out[w * maxloc + sl] = pc.n == 1 ? wr[pc.k] : (int32_t)(-(kpart[pc.k] + pc.j) - 1);
     }
   }
-  // WALK_WIN > 1: each group's list is cut at K column bounds (k + 1) * cdiv(N, K), each window
-  // padded to a multiple of 4 entries; the kernel syncs its groups after every window
-  constexpr int K = WALK_WIN > 1 ? WALK_WIN : 1;
+  // each group's list is cut at K column bounds (k + 1) * cdiv(N, K), each window padded to a
+  // multiple of 4 entries; the kernel syncs its groups after every window
+  const int K = walk_windows(d);
   const int64_t wlen = hnm_cdiv(pl->N, K);
   const std::vector<int32_t>& hc = *pl->h_scol;
   const std::vector<float>& hv = *pl->h_sval;
@@ -1258,6 +1262,7 @@ static hnm_status walk_build(hnm_spmm_plan* pl, int d, WalkSched** out) {
   ws->ng = ng;
   ws->nwg = (int)nwg;
   ws->maxloc = maxloc;
+  ws->nwin = K;
   ws->n_split = (int64_t)srows.size();
   ws->n_part = sptr.back();
   hnm_status st;
@@ -1723,7 +1728,7 @@ static hnm_status spmm_launch(hnm_ctx* ctx, const hnm_spmm_plan* pl, int64_t N,
     if (any) {
       hipLaunchKernelGGL(spmm_walk_kernel<LPR>, dim3((unsigned)ws->nwg), dim3(WALK_THREADS), 0,
                          ctx->stream, ws->gptr, ws->ent, ws->wt, ws->slot_out, ws->nslot, ws->maxloc,
-                         X, d, partial, ep, r0, r1);
+                         ws->nwin, X, d, partial, ep, r0, r1);
       HNM_LAUNCH_CHECK();
       if (ws->n_split > 0) {
         hipLaunchKernelGGL(spmm_walk_finish_kernel, dim3((unsigned)ws->n_split), dim3(256), 0,
