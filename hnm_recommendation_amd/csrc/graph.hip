@@ -67,6 +67,12 @@ static inline int walk_windows(int d) { return d >= 128 ? WALK_WIN_WIDE : WALK_W
 #define SWALK_THREADS 512
 #define SWALK_LDS_F4 4608
 #define SWALK_STEP 8
+// d >= 128 (LPR >= 32): 4 entries a step (round 6, A/B on one box: configs[4] d = 128 step
+// 7.02 -> 6.94 ms; 2 entries 7.33-7.37, 16 entries 8.21; d = 64 the same at 4 and 8; the long
+// walk's WALK_STEP at d = 128: 2 entries 8.42, 8 entries 7.79 vs 6.94 ms at 4 --
+// profiles/r11f_swalk_step_ab.txt)
+#define SWALK_STEP_WIDE 4
+__host__ __device__ constexpr int swalk_step(int lpr) { return lpr >= 32 ? SWALK_STEP_WIDE : SWALK_STEP; }
 // Round 4, measured and dropped: aligning the workgroups of an XCD -- a bounded wait (per-XCD
 // progress counters, atomics at agent scope) before each short-walk round until all but 1/8 of
 // the XCD's workgroups finished the previous one, and the same before each of the long-row
@@ -633,7 +639,7 @@ __global__ __launch_bounds__(SWALK_THREADS) void spmm_swalk_kernel(
     const int32_t* __restrict__ nslot, int S, const float* __restrict__ X, int d, SpmmEpi ep,
     int64_t r0, int64_t r1, int64_t b0, int64_t b1) {
   constexpr int NG = SWALK_THREADS / LPR;
-  constexpr int ST = SWALK_STEP;
+  constexpr int ST = swalk_step(LPR);
   __shared__ float4 acc[SWALK_LDS_F4];
   const int tid = threadIdx.x, g = tid / LPR, sub = tid % LPR;
   for (int i = tid; i < SWALK_LDS_F4; i += SWALK_THREADS) acc[i] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -1282,9 +1288,9 @@ static hnm_status walk_build(hnm_spmm_plan* pl, int d, WalkSched** out) {
 // Short-walk schedule for d: the short rows cut into nb blocks of consecutive rows at equal
 // shares of their entries (at most S rows a block; nb a multiple of the persistent grid once the
 // graph fills it), each block's rows dealt to its ng lane groups (longest first, least-loaded
-// group), each group's rows' entries merged by column and padded to multiples of SWALK_STEP with
-// weight-0 entries into the spare slot S.  The placement only moves rows between lanes; each row's chain order is its
-// sorted entries' order.
+// group), each group's rows' entries merged by column and padded to multiples of swalk_step with
+// weight-0 entries into the spare slot S.  The placement only moves rows between lanes; each
+// row's chain order is its sorted entries' order.
 static hnm_status swalk_build(hnm_spmm_plan* pl, int d, ShortSched** out) {
   const int lpr = d / 4, ng = SWALK_THREADS / lpr;
   const int S = std::min(1022, SWALK_LDS_F4 / lpr - 1);
@@ -1339,7 +1345,7 @@ static hnm_status swalk_build(hnm_spmm_plan* pl, int d, ShortSched** out) {
   });
   std::vector<int64_t> gptr((size_t)(nb * ng + 1), 0);
   for (int64_t i = 0; i < nb * ng; ++i)
-    gptr[i + 1] = gptr[i] + hnm_cdiv(wcnt[i], SWALK_STEP) * SWALK_STEP;
+    gptr[i + 1] = gptr[i] + hnm_cdiv(wcnt[i], swalk_step(lpr)) * swalk_step(lpr);
   const int64_t Tp = gptr.back();
   std::vector<uint32_t> ent((size_t)Tp, (uint32_t)S);
   std::vector<float> wt((size_t)Tp, 0.f);
