@@ -48,10 +48,10 @@
 // (round 4, whole-graph layer d=64 / d=128: 4 entries 1.308 / 2.676 ms, 4 + records prefetched a
 // step ahead 1.415 / 2.920, 8 entries 1.435 / 3.017), pieces cut for ~WALK_GROUPS_TARGET groups
 #define WALK_THREADS 1024
-#define WALK_WIN 16
+#define WALK_WIN 12
 // d >= 128 (512-B rows): more, narrower windows (round 6, A/B on one box, configs[4] d = 128
-// step: 16 windows 7.09 ms, 24: 7.01, 32: 7.02, 64: 7.29; the d = 64 step: 8: 3.47, 16: 3.49,
-// 32: 3.58 -- profiles/r11d_spmm_windows_ab.txt)
+// step: 16 windows 7.09 ms, 24: 7.01, 32: 7.02, 64: 7.29; the d = 64 step: 8: 3.464, 12: 3.462,
+// 16: 3.474, 32: 3.58 -- profiles/r11d_spmm_windows_ab.txt)
 #define WALK_WIN_WIDE 24
 static inline int walk_windows(int d) { return d >= 128 ? WALK_WIN_WIDE : WALK_WIN; }
 #define WALK_STEP 4
