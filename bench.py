@@ -538,6 +538,12 @@ def compact_line(line):
     return out
 
 
+# workloads whose step is a fraction of a millisecond (MF: ~0.18 ms): 20 steps time ~4 ms,
+# where one host hiccup moved a whole line by 60 % (gpurun_out/r11x); their extra lines time
+# at least 200 steps
+SHORT_STEP_WORKLOADS = ("mf",)
+
+
 def run_extras(args):
     """Every other workload's bench line and the B = 1 serve latencies, measured by child
     processes after the headline line's timed region (one process per workload: each
@@ -547,6 +553,8 @@ def run_extras(args):
     out, lat, full = {}, {}, {}
     for w, what in EXTRA_WORKLOADS:
         steps, warmup = (5, 1) if w == "widedeep" else (args.steps, args.warmup)
+        if w in SHORT_STEP_WORKLOADS:  # sub-ms steps: a longer timed region (host jitter)
+            steps, warmup = max(steps, 200), max(warmup, 20)
         argv = ["--workload", w, "--steps", str(steps), "--warmup", str(warmup), "--no-extras"]
         if args.no_cpu_baseline:
             argv.append("--no-cpu-baseline")
@@ -565,8 +573,11 @@ def run_extras(args):
                   ("mf", ("norms", "student_t")), ("ncf_deep", ("norms",))):
         for wt in ws:
             wname, _, opt = wt.partition("+")
-            line = run_child(["--workload", w, "--weights", wname, "--steps", str(args.steps),
-                              "--warmup", str(args.warmup), "--profile-only"]
+            st, wu = args.steps, args.warmup
+            if w in SHORT_STEP_WORKLOADS:
+                st, wu = max(st, 200), max(wu, 20)
+            line = run_child(["--workload", w, "--weights", wname, "--steps", str(st),
+                              "--warmup", str(wu), "--profile-only"]
                              + (["--" + opt] if opt else []), 600)
             log(f"robustness {w} {wt} done")
             if line is not None:
@@ -592,8 +603,8 @@ def run_extras(args):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--batch", type=int, default=4096)
     ap.add_argument("--workload", default="ncf")
     ap.add_argument("--no-cpu-baseline", action="store_true")

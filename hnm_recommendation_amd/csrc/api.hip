@@ -196,20 +196,26 @@ extern "C" hnm_status hnm_ctx_reserve(hnm_ctx* ctx, size_t bytes) {
 }
 
 // ------------------------------------------------------------------ kernel timer
+#define HNM_TIMER_PREALLOC 1024
+static bool timer_grow(hnm_ctx* ctx, int ncap) {
+  hipEvent_t* a = (hipEvent_t*)realloc(ctx->ev0, ncap * sizeof(hipEvent_t));
+  if (a) ctx->ev0 = a;
+  hipEvent_t* b = (hipEvent_t*)realloc(ctx->ev1, ncap * sizeof(hipEvent_t));
+  if (b) ctx->ev1 = b;
+  if (!a || !b) return false;
+  for (int i = ctx->cap; i < ncap; ++i) {
+    (void)hipEventCreate(&ctx->ev0[i]);
+    (void)hipEventCreate(&ctx->ev1[i]);
+  }
+  ctx->cap = ncap;
+  return true;
+}
+
 void hnm_timer_begin(hnm_ctx* ctx, int cls) {
   if (!(ctx->timing & cls)) return;
-  if (ctx->nev == ctx->cap) {
-    const int ncap = ctx->cap ? 2 * ctx->cap : 256;
-    hipEvent_t* a = (hipEvent_t*)realloc(ctx->ev0, ncap * sizeof(hipEvent_t));
-    hipEvent_t* b = (hipEvent_t*)realloc(ctx->ev1, ncap * sizeof(hipEvent_t));
-    if (!a || !b) { ctx->timing = 0; return; }
-    ctx->ev0 = a;
-    ctx->ev1 = b;
-    for (int i = ctx->cap; i < ncap; ++i) {
-      (void)hipEventCreate(&ctx->ev0[i]);
-      (void)hipEventCreate(&ctx->ev1[i]);
-    }
-    ctx->cap = ncap;
+  if (ctx->nev == ctx->cap && !timer_grow(ctx, ctx->cap ? 2 * ctx->cap : 256)) {
+    ctx->timing = 0;
+    return;
   }
   (void)hipEventRecord(ctx->ev0[ctx->nev], ctx->stream);
 }
@@ -223,6 +229,9 @@ void hnm_timer_end(hnm_ctx* ctx, int cls) {
 extern "C" hnm_status hnm_ctx_enable_timing(hnm_ctx* ctx, int on) {
   HNM_CTX_DEVICE(ctx);
   HNM_REQUIRE(ctx, HNM_EINVAL, "ctx is NULL");
+  // the events are created here, outside the caller's timed region (a bench loop of a few
+  // hundred launches records into them without creating any)
+  if (on && ctx->cap < HNM_TIMER_PREALLOC && !timer_grow(ctx, HNM_TIMER_PREALLOC)) on = 0;
   ctx->timing = on;
   ctx->nev = 0;
   return HNM_OK;
