@@ -112,7 +112,9 @@ hnm_status hnm_ctx_prefilter_stats_ex(hnm_ctx* ctx, int64_t* out, int n, int res
  * main kernel; `mask` selects the class: 1 = the scoring / scan kernel of every top-K or
  * dense call, 2 = each LightGCN propagation layer (SpMM), 3 = both.  hnm_ctx_timing()
  * syncs, returns the summed kernel time and the number of timed launches, and resets.
- * (bench.py's live roofline figures.) */
+ * Enabling creates 1,024 event pairs up front (more are created only past that many timed
+ * launches), so a timed loop records without creating events.  (bench.py's live roofline
+ * figures.) */
 hnm_status hnm_ctx_enable_timing(hnm_ctx* ctx, int mask);
 hnm_status hnm_ctx_timing(hnm_ctx* ctx, double* total_ms, int64_t* launches);
 
